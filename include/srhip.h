@@ -1,0 +1,238 @@
+/*
+ * srhip.h — C ABI of libsrhip.so, the MI355X-native batched expression
+ * evaluation engine behind SymbolicRegression.jl's scoring hot path.
+ *
+ * Every entry point below replaces (a batched form of) one reference
+ * interface; the reference file:line is cited on each declaration
+ * (paths relative to the SymbolicRegression.jl v0.15.0 repository).
+ *
+ * Conventions
+ *  - Plain C: pointers + sizes, no C++ exceptions cross this boundary.
+ *  - Status codes: SRHIP_OK (0) on success, < 0 on error; the message of the
+ *    last error on the calling thread is returned by srhip_last_error().
+ *  - SRHIP_ERR_UNSUPPORTED means "this call is outside the engine's
+ *    coverage" (unknown operator, unsupported loss / dtype, non-finite X):
+ *    the caller is expected to fall back to the reference CPU path.
+ *  - All host buffers are owned by the caller. Calls are synchronous: the
+ *    results are in the caller's buffers when the call returns.
+ *  - A context serialises the calls made through it (one mutex, one stream).
+ *    Use one context per host thread for concurrency; datasets and
+ *    programs belong to the context that created them.
+ *  - Trees cross the boundary as post-order (postfix) node streams: for a
+ *    node, its left subtree, then its right subtree, then the node itself.
+ *    Constants are listed separately, in the order of the constant leaves in
+ *    that stream, which is DynamicExpressions' get_constants order (leaf
+ *    order, left to right; test/test_derivatives.jl:126-150).
+ */
+#ifndef SRHIP_H
+#define SRHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRHIP_ABI_VERSION 1
+
+/* ---- status codes ------------------------------------------------------ */
+#define SRHIP_OK 0
+#define SRHIP_ERR_INVALID (-1)     /* malformed arguments / trees           */
+#define SRHIP_ERR_UNSUPPORTED (-2) /* fall back to the reference CPU path  */
+#define SRHIP_ERR_DEVICE (-3)      /* HIP runtime failure                  */
+#define SRHIP_ERR_NOMEM (-4)       /* host or device allocation failed     */
+
+/* ---- element types (Dataset{T}: src/Dataset.jl:24-34) ------------------ */
+#define SRHIP_F32 0
+#define SRHIP_F64 1
+
+/* ---- X layouts ---------------------------------------------------------- */
+/* Julia's Dataset.X is (nfeatures, n) column-major (src/ProgramConstants.jl:3-5):
+ * element (f, i) at X[i*nfeat + f]. FEATURE_MAJOR is element (f, i) at X[f*n + i]. */
+#define SRHIP_X_JULIA 0
+#define SRHIP_X_FEATURE_MAJOR 1
+
+/* ---- node kinds of the postfix stream ----------------------------------- */
+#define SRHIP_NODE_CONST 0   /* Node(; val=c)                               */
+#define SRHIP_NODE_FEATURE 1 /* Node(; feature=f); arg = f-1 (0-based)      */
+#define SRHIP_NODE_UNARY 2   /* degree-1 node; arg = SRHIP_UOP_*            */
+#define SRHIP_NODE_BINARY 3  /* degree-2 node; arg = SRHIP_BOP_*            */
+
+/* ---- operator ids --------------------------------------------------------
+ * Semantics follow src/Operators.jl:8-111 after the user-op → safe-op mapping
+ * of src/Options.jl:86-120 (binopmap / unaopmap). The Julia shim maps
+ * options.operators.binops[i] / unaops[i] to these ids once per Options
+ * (srhip_op_lookup gives the id for a Julia function name).            */
+#define SRHIP_BOP_ADD 0          /* +, plus            Operators.jl:23-25 */
+#define SRHIP_BOP_SUB 1          /* -, sub             :26-28             */
+#define SRHIP_BOP_MUL 2          /* *, mult            :29-31             */
+#define SRHIP_BOP_DIV 3          /* /, div             :47-49             */
+#define SRHIP_BOP_POW 4          /* ^, safe_pow        :38-46             */
+#define SRHIP_BOP_GREATER 5      /* greater            :94-99             */
+#define SRHIP_BOP_LOGICAL_OR 6   /* logical_or         :104-106           */
+#define SRHIP_BOP_LOGICAL_AND 7  /* logical_and        :109-111           */
+#define SRHIP_BOP_MOD 8          /* Base.mod (float)   :17                */
+#define SRHIP_BOP_MAX 9          /* Base.max (float)                      */
+#define SRHIP_BOP_MIN 10         /* Base.min (float)                      */
+#define SRHIP_NUM_BOPS 11
+
+#define SRHIP_UOP_NEG 0          /* neg                :90-92             */
+#define SRHIP_UOP_SQUARE 1       /* square = x*x       :32-34             */
+#define SRHIP_UOP_CUBE 2         /* cube = x*x*x       :35-37             */
+#define SRHIP_UOP_EXP 3
+#define SRHIP_UOP_ABS 4
+#define SRHIP_UOP_LOG 5          /* safe_log           :50-53             */
+#define SRHIP_UOP_LOG2 6         /* safe_log2          :54-57             */
+#define SRHIP_UOP_LOG10 7        /* safe_log10         :58-61             */
+#define SRHIP_UOP_LOG1P 8        /* safe_log1p         :62-65             */
+#define SRHIP_UOP_SQRT 9         /* safe_sqrt          :70-73             */
+#define SRHIP_UOP_SIN 10
+#define SRHIP_UOP_COS 11
+#define SRHIP_UOP_TAN 12
+#define SRHIP_UOP_SINH 13
+#define SRHIP_UOP_COSH 14
+#define SRHIP_UOP_TANH 15
+#define SRHIP_UOP_ATAN 16
+#define SRHIP_UOP_ASINH 17
+#define SRHIP_UOP_ACOSH 18       /* safe_acosh         :66-69             */
+#define SRHIP_UOP_ATANH_CLIP 19  /* atanh_clip         :14                */
+#define SRHIP_UOP_ERF 20
+#define SRHIP_UOP_ERFC 21
+#define SRHIP_UOP_GAMMA 22       /* gamma (Inf → NaN)  :8-12              */
+#define SRHIP_UOP_RELU 23        /* (x+abs(x))/2       :100-102           */
+#define SRHIP_UOP_ROUND 24       /* round, ties to even                   */
+#define SRHIP_UOP_FLOOR 25
+#define SRHIP_UOP_CEIL 26
+#define SRHIP_UOP_SIGN 27
+#define SRHIP_UOP_INV 28         /* inv(x) = 1/x                          */
+#define SRHIP_NUM_UOPS 29
+
+/* ---- elementwise losses (LossFunctions.jl distance losses; r = ŷ - y,
+ * docs/src/losses.md:16-80; default L2DistLoss, src/Options.jl:429-431) -- */
+#define SRHIP_LOSS_L2 0        /* r^2                                       */
+#define SRHIP_LOSS_L1 1        /* |r|                                       */
+#define SRHIP_LOSS_LP 2        /* |r|^p,        params[0] = p               */
+#define SRHIP_LOSS_HUBER 3     /* |r|<=d ? r^2/2 : d(|r|-d/2), params[0]=d  */
+#define SRHIP_LOSS_LOGCOSH 4   /* log(cosh(r))                              */
+#define SRHIP_LOSS_L1EPSINS 5  /* max(0, |r|-eps),  params[0] = eps         */
+#define SRHIP_LOSS_L2EPSINS 6  /* max(0, |r|-eps)^2, params[0] = eps        */
+#define SRHIP_LOSS_QUANTILE 7  /* r>=0 ? tau*r : (tau-1)*r,  params[0] = tau */
+#define SRHIP_LOSS_PERIODIC 8  /* 1 - cos(2πr/c), params[0] = c             */
+#define SRHIP_LOSS_LOGITDIST 9 /* -log(4 e^r / (1+e^r)^2)                   */
+#define SRHIP_NUM_LOSSES 10
+
+typedef struct srhip_ctx srhip_ctx;
+typedef struct srhip_dataset srhip_dataset;
+typedef struct srhip_program srhip_program;
+
+/* A batch of trees as postfix node streams (see header comment). */
+typedef struct srhip_trees {
+  int32_t ntrees;
+  const int32_t* node_off;  /* [ntrees+1]: nodes of tree t are node_off[t] .. node_off[t+1]-1 */
+  const uint8_t* kind;      /* [node_off[ntrees]] SRHIP_NODE_*                                  */
+  const uint16_t* arg;      /* [node_off[ntrees]] feature (0-based) or operator id              */
+  const int32_t* const_off; /* [ntrees+1]: constants of tree t                                   */
+  const void* consts;       /* [const_off[ntrees]] of the program dtype                          */
+} srhip_trees;
+
+/* ---- library / context ------------------------------------------------- */
+int32_t srhip_version(void);
+const char* srhip_last_error(void);
+int32_t srhip_device_count(int32_t* out_count);
+int32_t srhip_open(int32_t device, srhip_ctx** out_ctx);
+int32_t srhip_close(srhip_ctx* ctx);
+
+/* Operator table: id and arity (1 or 2) for a Julia operator name
+ * ("+", "*", "safe_log", "log", "cos", "^", ...), applying binopmap/unaopmap
+ * (src/Options.jl:86-120). Unknown → SRHIP_ERR_UNSUPPORTED. */
+int32_t srhip_op_lookup(const char* name, int32_t* out_arity, int32_t* out_id);
+
+/* ---- dataset: Dataset(X, y; weights) src/Dataset.jl:43-64 ----------------
+ * Uploads rows [row_begin, row_end) of X / y / w once (the row shard of this
+ * device); X is transposed to feature-major on the device. w may be NULL
+ * (unweighted). The dataset is immutable after creation. */
+int32_t srhip_dataset_create(srhip_ctx* ctx, int32_t dtype, int32_t x_layout,
+                             const void* X, const void* y, const void* w,
+                             int64_t n, int32_t nfeat, int64_t row_begin,
+                             int64_t row_end, srhip_dataset** out_ds);
+int32_t srhip_dataset_destroy(srhip_dataset* ds);
+/* rows of this shard, Σw (or the row count), Σ y·w (or Σ y) over the shard —
+ * the pieces of avg_y (src/Dataset.jl:56-60) — and whether X is all-finite. */
+int32_t srhip_dataset_info(const srhip_dataset* ds, int64_t* out_rows,
+                           int32_t* out_nfeat, double* out_sum_w,
+                           double* out_sum_yw, int32_t* out_x_finite);
+
+/* ---- programs: a compiled, device-resident batch of trees ---------------
+ * Flattens/compiles the postfix streams (register allocation, leaf fusion,
+ * static constant checks) and uploads them once; evaluate any number of
+ * times afterwards. */
+int32_t srhip_program_create(srhip_ctx* ctx, int32_t dtype,
+                             const srhip_trees* trees, srhip_program** out_prog);
+int32_t srhip_program_destroy(srhip_program* prog);
+/* per-tree node counts (count_nodes, = compute_complexity without a custom
+ * complexity mapping, src/Complexity.jl:13-19) */
+int32_t srhip_program_info(const srhip_program* prog, int32_t* out_ntrees,
+                           int64_t* out_total_nodes, int32_t* out_nodes /*[ntrees] or NULL*/);
+/* Replace the constants of every tree (set_constants, in get_constants
+ * order) without recompiling; used by batched constant optimisation
+ * (src/ConstantOptimization.jl:12-19). consts has const_off[ntrees] entries. */
+int32_t srhip_program_set_constants(srhip_program* prog, const void* consts);
+
+/* ---- batched loss: eval_loss / _eval_loss src/LossFunctions.jl:34-67 ----
+ * For every tree t:
+ *   out_loss_sum[t] = Σ_i w_i · ℓ(ŷ_t,i, y_i) over the shard (fp64)
+ *   out_ok[t]       = did_succeed of eval_tree_array (1/0)
+ *   *out_weight_sum = Σ_i w_i (or the row count when unweighted)
+ * The reference loss is out_loss_sum[t] / *out_weight_sum computed in T, and
+ * T(Inf) when !out_ok[t] (src/LossFunctions.jl:36-38). row_idx (NULL = all
+ * rows) selects rows with repetition, as score_func_batch does
+ * (src/LossFunctions.jl:95-115); indices are 0-based within the shard.
+ * Trees whose evaluation fails get out_loss_sum = NaN. */
+int32_t srhip_eval_loss(srhip_dataset* ds, const srhip_program* prog,
+                        int32_t loss_kind, const double* loss_params,
+                        const int64_t* row_idx, int64_t nidx,
+                        double* out_loss_sum, double* out_weight_sum,
+                        uint8_t* out_ok);
+/* Convenience: srhip_program_create + srhip_eval_loss + destroy. */
+int32_t srhip_eval_loss_batch(srhip_dataset* ds, const srhip_trees* trees,
+                              int32_t loss_kind, const double* loss_params,
+                              const int64_t* row_idx, int64_t nidx,
+                              double* out_loss_sum, double* out_weight_sum,
+                              uint8_t* out_ok);
+
+/* ---- per-row outputs: eval_tree_array src/InterfaceDynamicExpressions.jl:50-52
+ * out is [ntrees][rows] of the dataset dtype (row-major per tree); rows of a
+ * failed tree are unspecified (the reference returns an undef array). */
+int32_t srhip_eval_tree_array(srhip_dataset* ds, const srhip_program* prog,
+                              void* out, uint8_t* out_ok);
+
+/* ---- constant gradients: eval_grad_tree_array(tree, X, options;
+ * variable=false) src/InterfaceDynamicExpressions.jl:105-107, fused with the
+ * loss: out_dloss[c] = Σ_i w_i ∂ℓ(ŷ_i, y_i)/∂c for every constant c of every
+ * tree (laid out like consts, const_off order). Also returns the loss sums
+ * and did_succeed like srhip_eval_loss. */
+int32_t srhip_eval_loss_grad(srhip_dataset* ds, const srhip_program* prog,
+                             int32_t loss_kind, const double* loss_params,
+                             double* out_loss_sum, double* out_dloss,
+                             double* out_weight_sum, uint8_t* out_ok);
+
+/* Per-row constant gradients for few trees: out_grad is
+ * [total consts][rows] (∂ŷ_i/∂c), out_value [ntrees][rows]. */
+int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog,
+                                   void* out_value, void* out_grad,
+                                   uint8_t* out_ok);
+
+/* ---- instrumentation ----------------------------------------------------
+ * Device time (ms, HIP events on the context's stream) of the evaluation
+ * kernel(s) of the last eval call on this context, and the number of kernel
+ * launches it made. */
+int32_t srhip_last_kernel_time(const srhip_ctx* ctx, double* out_ms,
+                               int32_t* out_launches);
+/* Synchronise the context's stream. */
+int32_t srhip_sync(srhip_ctx* ctx);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* SRHIP_H */

@@ -1,0 +1,112 @@
+/*
+ * sr_oracle.c — CPU restatement of the SymbolicRegression.jl scoring hot
+ * path (TEST INFRASTRUCTURE ONLY; see sr_oracle.h for scope and pinning).
+ *
+ * Built twice by oracle/Makefile from this one source:
+ *   liboracle_scalar.so  -O2 -fno-tree-vectorize   ~ Options(turbo=false)
+ *   liboracle_simd.so    -O3 -march=x86-64-v3      ~ Options(turbo=true)
+ * both with -ffp-contract=off (no fused multiply-add: Julia does not contract
+ * `a*b + c`), no fast-math, and OpenMP over trees for the batched entry.
+ */
+#include "sr_oracle.h"
+
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+#include "../include/srhip.h"
+
+int oracle_max_threads(void) {
+#ifdef _OPENMP
+  return omp_get_max_threads();
+#else
+  return 1;
+#endif
+}
+
+#define CAT_(a, b) a##b
+#define CAT(a, b) CAT_(a, b)
+
+/* ---------------- T = float ---------------- */
+#define T float
+#define SFX _f32
+#define TRUNC truncf
+#define FMOD fmodf
+#define COPYSIGN copysignf
+#define SIGNBIT signbit
+#define FABS fabsf
+#define SQRT sqrtf
+#define RINT rintf
+#define FLOOR floorf
+#define CEIL ceilf
+#define ISINF isinf
+#define ISFINITE isfinite
+#include "sr_oracle_ops.h"
+#include "sr_oracle_eval.h"
+#undef ONODE
+#undef ECTX
+#undef XAT
+#undef BOP_CASE
+#undef FOR_EACH_BOP
+#undef UOP_CASE
+#undef FOR_EACH_UOP
+#undef T
+#undef SFX
+#undef TRUNC
+#undef FMOD
+#undef COPYSIGN
+#undef FABS
+#undef SQRT
+#undef RINT
+#undef FLOOR
+#undef CEIL
+
+/* ---------------- T = double ---------------- */
+#define T double
+#define SFX _f64
+#define TRUNC trunc
+#define FMOD fmod
+#define COPYSIGN copysign
+#define FABS fabs
+#define SQRT sqrt
+#define RINT rint
+#define FLOOR floor
+#define CEIL ceil
+#include "sr_oracle_ops.h"
+#include "sr_oracle_eval.h"
+
+float oracle_binop_f32(int op, float x, float y) { return apply_b_f32(op, x, y); }
+double oracle_binop_f64(int op, double x, double y) { return apply_b_f64(op, x, y); }
+float oracle_unop_f32(int op, float x) { return apply_u_f32(op, x); }
+double oracle_unop_f64(int op, double x) { return apply_u_f64(op, x); }
+
+double oracle_elem_loss_f64(int loss, const double* params, double yhat, double y) {
+  return elem_loss_f64(loss, params, yhat, y);
+}
+float oracle_elem_loss_f32(int loss, const double* params, float yhat, float y) {
+  return elem_loss_f32(loss, params, yhat, y);
+}
+
+int oracle_eval_grad_consts_f64(const uint8_t* kind, const uint16_t* arg,
+                                const double* consts, int32_t nnodes,
+                                const double* X, int64_t n, int32_t nfeat,
+                                double* out, double* grad) {
+  if (nnodes <= 0) return 0;
+  onode_f64* nd = (onode_f64*)malloc(sizeof(onode_f64) * nnodes);
+  int root = parse_f64(kind, arg, consts, nnodes, nd);
+  if (root < 0) { free(nd); return 0; }
+  int nc = 0;
+  for (int i = 0; i < nnodes; ++i) nc += (kind[i] == SRHIP_NODE_CONST);
+  ectx_f64 c = {nd, X, n, nfeat};
+  int cidx = 0;
+  double* val = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
+  double* tan = (double*)malloc(sizeof(double) * (size_t)(nc > 0 ? nc : 1) * (size_t)(n > 0 ? n : 1));
+  int ok = grad_rec_f64(&c, root, nc, &cidx, val, tan);
+  if (out) memcpy(out, val, sizeof(double) * (size_t)n);
+  if (grad) memcpy(grad, tan, sizeof(double) * (size_t)nc * (size_t)n);
+  free(val); free(tan); free(nd);
+  return ok;
+}

@@ -1,0 +1,743 @@
+// api.cpp — the C ABI of libsrhip.so (include/srhip.h).
+//
+// Host runtime: contexts (device + stream + workspace, one mutex), device
+// datasets (uploaded once, feature-major, rows padded), compiled programs
+// (device resident), evaluation planning and launches, results back to the
+// caller's buffers. No C++ exception crosses the boundary.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <mutex>
+#include <numeric>
+#include <string>
+#include <vector>
+
+#include "../../include/srhip.h"
+#include "compile.h"
+#include "kernels.h"
+
+using namespace srhip;
+
+namespace {
+
+thread_local std::string g_last_error;
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_CHECK(expr)                                                              \
+  do {                                                                               \
+    hipError_t _e = (expr);                                                          \
+    if (_e != hipSuccess)                                                            \
+      throw Error(SRHIP_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e)); \
+  } while (0)
+
+template <typename F>
+int guarded(F&& f) {
+  try {
+    return f();
+  } catch (const Error& e) {
+    return set_error(e.code, e.what());
+  } catch (const std::bad_alloc&) {
+    return set_error(SRHIP_ERR_NOMEM, "host allocation failed");
+  } catch (const std::exception& e) {
+    return set_error(SRHIP_ERR_INVALID, e.what());
+  } catch (...) {
+    return set_error(SRHIP_ERR_INVALID, "unknown error");
+  }
+}
+
+// grow-only device buffer
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  void ensure(size_t n) {
+    if (n <= bytes) return;
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+    hipError_t e = hipMalloc(&p, n);
+    if (e != hipSuccess) throw Error(SRHIP_ERR_NOMEM, std::string("hipMalloc: ") + hipGetErrorString(e));
+    bytes = n;
+  }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+};
+
+constexpr int64_t kRowPad = 8192;  // dataset rows are padded to a multiple of this
+
+int64_t pad_rows(int64_t rows) { return ((std::max<int64_t>(rows, 1) + kRowPad - 1) / kRowPad) * kRowPad; }
+
+size_t dtype_size(int dtype) { return dtype == SRHIP_F32 ? 4 : 8; }
+
+}  // namespace
+
+struct srhip_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  std::mutex mu;
+  hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  double last_ms = 0.0;
+  int last_launches = 0;
+  DevBuf partial, sums, oks, scratch_idx, gather;
+  std::vector<double> h_sum;
+  std::vector<uint8_t> h_ok;
+};
+
+struct srhip_dataset {
+  srhip_ctx* ctx = nullptr;
+  int dtype = SRHIP_F32;
+  int64_t rows = 0;
+  int nfeat = 0;
+  int64_t n_pad = 0;
+  void* X = nullptr;
+  void* y = nullptr;
+  void* w = nullptr;
+  double sum_w = 0.0, sum_yw = 0.0;
+  bool x_finite = true;
+  std::vector<double> h_w;  // host copy of the shard weights (Σw of row samples)
+};
+
+struct srhip_program {
+  srhip_ctx* ctx = nullptr;
+  int dtype = SRHIP_F32;
+  int ntrees = 0;
+  // host copy of the postfix streams (for set_constants → recompile)
+  std::vector<int32_t> node_off, const_off;
+  std::vector<uint8_t> kind;
+  std::vector<uint16_t> arg;
+  std::vector<unsigned char> consts;
+  // compiled metadata
+  std::vector<int32_t> nodes;
+  std::vector<uint8_t> static_fail, fail_if_rows;
+  int max_feature = -1;
+  int64_t total_nodes = 0;
+  // device
+  void* d_code = nullptr;
+  int32_t* d_tree_off = nullptr;
+  int32_t* d_list = nullptr;  // [nlist_a + nlist_b]: shallow trees then deep trees
+  int nlist_a = 0, nlist_b = 0;
+};
+
+namespace {
+
+void free_program_device(srhip_program* p) {
+  if (p->d_code) (void)hipFree(p->d_code);
+  if (p->d_tree_off) (void)hipFree(p->d_tree_off);
+  if (p->d_list) (void)hipFree(p->d_list);
+  p->d_code = nullptr;
+  p->d_tree_off = nullptr;
+  p->d_list = nullptr;
+}
+
+template <typename T>
+void build_program(srhip_program* p) {
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->consts.data();
+  CompiledBatch<T> cb = compile_batch<T>(tr);
+  p->nodes = cb.nodes;
+  p->static_fail = cb.static_fail;
+  p->fail_if_rows = cb.fail_if_rows;
+  p->max_feature = cb.max_feature;
+  p->total_nodes = cb.total_nodes;
+  // trees to run, cost-descending; shallow (<= 4 slots) and deep lists
+  std::vector<int32_t> a, b;
+  for (int t = 0; t < p->ntrees; ++t) {
+    if (cb.tree_off[t] < 0) continue;
+    (cb.need[t] <= 4 ? a : b).push_back(t);
+  }
+  auto by_cost = [&](int32_t x, int32_t y) {
+    return cb.cost[x] != cb.cost[y] ? cb.cost[x] > cb.cost[y] : x < y;
+  };
+  std::stable_sort(a.begin(), a.end(), by_cost);
+  std::stable_sort(b.begin(), b.end(), by_cost);
+  p->nlist_a = (int)a.size();
+  p->nlist_b = (int)b.size();
+  std::vector<int32_t> list(a);
+  list.insert(list.end(), b.begin(), b.end());
+  std::vector<int32_t> toff(cb.tree_off);
+  for (auto& v : toff) v = std::max(v, 0);
+
+  free_program_device(p);
+  hipStream_t s = p->ctx->stream;
+  HIP_CHECK(hipMalloc(&p->d_code, std::max<size_t>(cb.code.size(), 1) * sizeof(Ins<T>)));
+  HIP_CHECK(hipMalloc((void**)&p->d_tree_off, std::max<size_t>(toff.size(), 1) * sizeof(int32_t)));
+  HIP_CHECK(hipMalloc((void**)&p->d_list, std::max<size_t>(list.size(), 1) * sizeof(int32_t)));
+  HIP_CHECK(hipMemcpyAsync(p->d_code, cb.code.data(), cb.code.size() * sizeof(Ins<T>), hipMemcpyHostToDevice, s));
+  if (!toff.empty())
+    HIP_CHECK(hipMemcpyAsync(p->d_tree_off, toff.data(), toff.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  if (!list.empty())
+    HIP_CHECK(hipMemcpyAsync(p->d_list, list.data(), list.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+}
+
+void check_program_vs_dataset(const srhip_dataset* ds, const srhip_program* p) {
+  if (!ds || !p) throw Error(SRHIP_ERR_INVALID, "null dataset or program");
+  if (ds->ctx != p->ctx) throw Error(SRHIP_ERR_INVALID, "dataset and program belong to different contexts");
+  if (ds->dtype != p->dtype) throw Error(SRHIP_ERR_INVALID, "dataset and program dtypes differ");
+  if (p->max_feature >= ds->nfeat)
+    throw Error(SRHIP_ERR_INVALID, "tree references feature " + std::to_string(p->max_feature + 1) +
+                                       " but the dataset has " + std::to_string(ds->nfeat));
+  if (!ds->x_finite)
+    throw Error(SRHIP_ERR_UNSUPPORTED,
+                "X contains non-finite values: did_succeed of fused leaves differs from the reference; use the CPU path");
+}
+
+// Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
+// n_pad) may be the dataset itself or a gathered row subset.
+template <typename T>
+void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const T* y,
+              const T* w, int64_t rows, int64_t n_pad, int nfeat, int loss, double lparam,
+              T* out, int64_t out_stride) {
+  hipStream_t s = c->stream;
+  c->last_ms = 0.0;
+  c->last_launches = 0;
+  c->sums.ensure(std::max<size_t>(p->ntrees, 1) * sizeof(double));
+  c->oks.ensure(std::max<size_t>(p->ntrees, 1));
+  for (int pass = 0; pass < 2; ++pass) {
+    const int nlist = pass == 0 ? p->nlist_a : p->nlist_b;
+    if (nlist == 0 || rows == 0) continue;
+    EvalPlan plan;
+    if (!plan_eval(p->dtype, pass == 1, mode, w != nullptr, nfeat, rows, nlist, &plan))
+      throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
+    EvalArgs<T> a;
+    a.prog = static_cast<const Ins<T>*>(p->d_code);
+    a.tree_off = p->d_tree_off;
+    a.list = p->d_list + (pass == 0 ? 0 : p->nlist_a);
+    a.nlist = nlist;
+    a.X = X;
+    a.y = y;
+    a.w = w;
+    a.n = rows;
+    a.n_pad = n_pad;
+    a.nfeat = nfeat;
+    a.ntiles = plan.ntiles;
+    a.ntg = plan.ntg;
+    a.tpb = plan.tpb;
+    a.nrg = plan.nrg;
+    a.loss = loss;
+    a.lparam = (T)lparam;
+    c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
+    a.partial = static_cast<Part<T>*>(c->partial.p);
+    a.out = out;
+    a.out_stride = out_stride;
+    HIP_CHECK(hipEventRecord(c->ev[0], s));
+    HIP_CHECK(launch_eval<T>(plan, a, mode, s));
+    HIP_CHECK(hipEventRecord(c->ev[1], s));
+    HIP_CHECK(launch_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
+    HIP_CHECK(hipEventSynchronize(c->ev[1]));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    c->last_ms += ms;
+    c->last_launches += 1;
+  }
+}
+
+// Copy per-tree results to the caller, applying the static verdicts.
+void collect_results(srhip_ctx* c, const srhip_program* p, int64_t rows, double* out_sum,
+                     uint8_t* out_ok) {
+  const int nt = p->ntrees;
+  c->h_sum.assign(nt, 0.0);
+  c->h_ok.assign(nt, 1);
+  if (rows > 0 && nt > 0 && (p->nlist_a + p->nlist_b) > 0) {
+    HIP_CHECK(hipMemcpyAsync(c->h_sum.data(), c->sums.p, nt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipMemcpyAsync(c->h_ok.data(), c->oks.p, nt, hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  for (int t = 0; t < nt; ++t) {
+    bool ok;
+    double sm;
+    if (p->static_fail[t]) { ok = false; sm = NAN; }
+    else if (p->fail_if_rows[t]) { ok = rows == 0; sm = rows == 0 ? 0.0 : NAN; }
+    else if (rows == 0) { ok = true; sm = 0.0; }
+    else { ok = c->h_ok[t] != 0; sm = c->h_sum[t]; }
+    if (out_sum) out_sum[t] = sm;
+    if (out_ok) out_ok[t] = ok ? 1 : 0;
+  }
+}
+
+template <typename T>
+int eval_loss_impl(srhip_dataset* ds, const srhip_program* p, int loss, const double* params,
+                   const int64_t* row_idx, int64_t nidx, double* out_sum, double* out_wsum,
+                   uint8_t* out_ok) {
+  srhip_ctx* c = ds->ctx;
+  const T* X = static_cast<const T*>(ds->X);
+  const T* y = static_cast<const T*>(ds->y);
+  const T* w = static_cast<const T*>(ds->w);
+  int64_t rows = ds->rows, n_pad = ds->n_pad;
+  double wsum = ds->w ? ds->sum_w : (double)ds->rows;
+  if (row_idx) {
+    if (nidx < 0) throw Error(SRHIP_ERR_INVALID, "negative index count");
+    for (int64_t k = 0; k < nidx; ++k)
+      if (row_idx[k] < 0 || row_idx[k] >= ds->rows) throw Error(SRHIP_ERR_INVALID, "row index out of range");
+    const int64_t gp = pad_rows(nidx);
+    const size_t es = sizeof(T);
+    c->scratch_idx.ensure(std::max<int64_t>(nidx, 1) * sizeof(int64_t));
+    c->gather.ensure((size_t)gp * (ds->nfeat + 2) * es);
+    T* Xg = static_cast<T*>(c->gather.p);
+    T* yg = Xg + (size_t)gp * ds->nfeat;
+    T* wg = yg + gp;
+    if (nidx > 0) {
+      HIP_CHECK(hipMemcpyAsync(c->scratch_idx.p, row_idx, nidx * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+      HIP_CHECK(launch_gather_rows<T>(X, y, w, ds->nfeat, ds->n_pad,
+                                      static_cast<const int64_t*>(c->scratch_idx.p), nidx, gp, Xg,
+                                      yg, w ? wg : nullptr, c->stream));
+    }
+    if (w) {  // Σ w over the (repeated) sample
+      wsum = 0.0;
+      for (int64_t k = 0; k < nidx; ++k) wsum += ds->h_w[row_idx[k]];
+    } else {
+      wsum = (double)nidx;
+    }
+    X = Xg;
+    y = yg;
+    w = w ? wg : nullptr;
+    rows = nidx;
+    n_pad = gp;
+  }
+  run_eval<T>(c, p, MODE_LOSS, X, y, w, rows, n_pad, ds->nfeat, loss, params ? params[0] : 0.0,
+              nullptr, 0);
+  collect_results(c, p, rows, out_sum, out_ok);
+  if (out_wsum) *out_wsum = wsum;
+  return SRHIP_OK;
+}
+
+template <typename T>
+int eval_tree_array_impl(srhip_dataset* ds, const srhip_program* p, void* out, uint8_t* out_ok) {
+  srhip_ctx* c = ds->ctx;
+  const int nt = p->ntrees;
+  const int64_t rows = ds->rows, n_pad = ds->n_pad;
+  const size_t es = sizeof(T);
+  c->gather.ensure(std::max<size_t>((size_t)nt * n_pad * es, es));
+  T* d_out = static_cast<T*>(c->gather.p);
+  run_eval<T>(c, p, MODE_OUT, static_cast<const T*>(ds->X), nullptr, nullptr, rows, n_pad,
+              ds->nfeat, SRHIP_LOSS_L2, 0.0, d_out, n_pad);
+  if (out && rows > 0 && nt > 0)
+    HIP_CHECK(hipMemcpy2DAsync(out, rows * es, d_out, n_pad * es, rows * es, nt, hipMemcpyDeviceToHost, c->stream));
+  collect_results(c, p, rows, nullptr, out_ok);
+  if (out) {  // rows of trees that were never run: NaN (reference: undefined)
+    T* o = static_cast<T*>(out);
+    for (int t = 0; t < nt; ++t)
+      if (p->static_fail[t] || p->fail_if_rows[t])
+        for (int64_t i = 0; i < rows; ++i) o[(size_t)t * rows + i] = (T)NAN;
+  }
+  return SRHIP_OK;
+}
+
+struct OpName {
+  const char* name;
+  int arity;
+  int id;
+};
+// Julia operator names → ids, including binopmap/unaopmap (src/Options.jl:86-120)
+const OpName kOpNames[] = {
+    {"+", 2, SRHIP_BOP_ADD}, {"plus", 2, SRHIP_BOP_ADD},
+    {"-", 2, SRHIP_BOP_SUB}, {"sub", 2, SRHIP_BOP_SUB},
+    {"*", 2, SRHIP_BOP_MUL}, {"mult", 2, SRHIP_BOP_MUL},
+    {"/", 2, SRHIP_BOP_DIV}, {"div", 2, SRHIP_BOP_DIV},
+    {"^", 2, SRHIP_BOP_POW}, {"pow", 2, SRHIP_BOP_POW}, {"safe_pow", 2, SRHIP_BOP_POW},
+    {"greater", 2, SRHIP_BOP_GREATER},
+    {"logical_or", 2, SRHIP_BOP_LOGICAL_OR},
+    {"logical_and", 2, SRHIP_BOP_LOGICAL_AND},
+    {"mod", 2, SRHIP_BOP_MOD},
+    {"max", 2, SRHIP_BOP_MAX},
+    {"min", 2, SRHIP_BOP_MIN},
+    {"neg", 1, SRHIP_UOP_NEG},
+    {"square", 1, SRHIP_UOP_SQUARE},
+    {"cube", 1, SRHIP_UOP_CUBE},
+    {"exp", 1, SRHIP_UOP_EXP},
+    {"abs", 1, SRHIP_UOP_ABS},
+    {"log", 1, SRHIP_UOP_LOG}, {"safe_log", 1, SRHIP_UOP_LOG},
+    {"log2", 1, SRHIP_UOP_LOG2}, {"safe_log2", 1, SRHIP_UOP_LOG2},
+    {"log10", 1, SRHIP_UOP_LOG10}, {"safe_log10", 1, SRHIP_UOP_LOG10},
+    {"log1p", 1, SRHIP_UOP_LOG1P}, {"safe_log1p", 1, SRHIP_UOP_LOG1P},
+    {"sqrt", 1, SRHIP_UOP_SQRT}, {"safe_sqrt", 1, SRHIP_UOP_SQRT},
+    {"sin", 1, SRHIP_UOP_SIN},
+    {"cos", 1, SRHIP_UOP_COS},
+    {"tan", 1, SRHIP_UOP_TAN},
+    {"sinh", 1, SRHIP_UOP_SINH},
+    {"cosh", 1, SRHIP_UOP_COSH},
+    {"tanh", 1, SRHIP_UOP_TANH},
+    {"atan", 1, SRHIP_UOP_ATAN},
+    {"asinh", 1, SRHIP_UOP_ASINH},
+    {"acosh", 1, SRHIP_UOP_ACOSH}, {"safe_acosh", 1, SRHIP_UOP_ACOSH},
+    {"atanh", 1, SRHIP_UOP_ATANH_CLIP}, {"atanh_clip", 1, SRHIP_UOP_ATANH_CLIP},
+    {"erf", 1, SRHIP_UOP_ERF},
+    {"erfc", 1, SRHIP_UOP_ERFC},
+    {"gamma", 1, SRHIP_UOP_GAMMA},
+    {"relu", 1, SRHIP_UOP_RELU},
+    {"round", 1, SRHIP_UOP_ROUND},
+    {"floor", 1, SRHIP_UOP_FLOOR},
+    {"ceil", 1, SRHIP_UOP_CEIL},
+    {"sign", 1, SRHIP_UOP_SIGN},
+    {"inv", 1, SRHIP_UOP_INV},
+};
+
+}  // namespace
+
+extern "C" {
+
+int32_t srhip_version(void) { return SRHIP_ABI_VERSION; }
+
+const char* srhip_last_error(void) { return g_last_error.c_str(); }
+
+int32_t srhip_device_count(int32_t* out_count) {
+  return guarded([&] {
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    if (out_count) *out_count = n;
+    return n > 0 ? SRHIP_OK : set_error(SRHIP_ERR_DEVICE, "no HIP device available");
+  });
+}
+
+int32_t srhip_open(int32_t device, srhip_ctx** out_ctx) {
+  return guarded([&] {
+    if (!out_ctx) throw Error(SRHIP_ERR_INVALID, "out_ctx is null");
+    *out_ctx = nullptr;
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0) throw Error(SRHIP_ERR_DEVICE, "no HIP device available");
+    if (device < 0 || device >= n) throw Error(SRHIP_ERR_INVALID, "device index out of range");
+    HIP_CHECK(hipSetDevice(device));
+    auto* c = new srhip_ctx();
+    c->device = device;
+    hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
+    for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e != hipSuccess) {
+      delete c;
+      throw Error(SRHIP_ERR_DEVICE, std::string("stream/event creation: ") + hipGetErrorString(e));
+    }
+    *out_ctx = c;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_close(srhip_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) return SRHIP_OK;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    ctx->partial.release();
+    ctx->sums.release();
+    ctx->oks.release();
+    ctx->scratch_idx.release();
+    ctx->gather.release();
+    for (auto& e : ctx->ev)
+      if (e) (void)hipEventDestroy(e);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_op_lookup(const char* name, int32_t* out_arity, int32_t* out_id) {
+  return guarded([&] {
+    if (!name) throw Error(SRHIP_ERR_INVALID, "null name");
+    for (const auto& o : kOpNames) {
+      if (std::strcmp(o.name, name) == 0) {
+        if (out_arity) *out_arity = o.arity;
+        if (out_id) *out_id = o.id;
+        return SRHIP_OK;
+      }
+    }
+    throw Error(SRHIP_ERR_UNSUPPORTED, std::string("operator not supported by the engine: ") + name);
+  });
+}
+
+int32_t srhip_dataset_create(srhip_ctx* ctx, int32_t dtype, int32_t x_layout, const void* X,
+                             const void* y, const void* w, int64_t n, int32_t nfeat,
+                             int64_t row_begin, int64_t row_end, srhip_dataset** out_ds) {
+  return guarded([&] {
+    if (!ctx || !out_ds) throw Error(SRHIP_ERR_INVALID, "null ctx or out_ds");
+    *out_ds = nullptr;
+    if (dtype != SRHIP_F32 && dtype != SRHIP_F64) throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
+    if (x_layout != SRHIP_X_JULIA && x_layout != SRHIP_X_FEATURE_MAJOR) throw Error(SRHIP_ERR_INVALID, "bad X layout");
+    if (n < 0 || nfeat <= 0 || nfeat > 65535) throw Error(SRHIP_ERR_INVALID, "bad shape");
+    if (row_begin < 0 || row_end < row_begin || row_end > n) throw Error(SRHIP_ERR_INVALID, "bad row range");
+    if ((row_end > row_begin) && (!X || !y)) throw Error(SRHIP_ERR_INVALID, "null X or y");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    HIP_CHECK(hipSetDevice(ctx->device));
+    const size_t es = dtype_size(dtype);
+    const int64_t rows = row_end - row_begin;
+    const int64_t n_pad = pad_rows(rows);
+    auto* ds = new srhip_dataset();
+    ds->ctx = ctx;
+    ds->dtype = dtype;
+    ds->rows = rows;
+    ds->nfeat = nfeat;
+    ds->n_pad = n_pad;
+    try {
+      HIP_CHECK(hipMalloc(&ds->X, (size_t)n_pad * nfeat * es));
+      HIP_CHECK(hipMalloc(&ds->y, (size_t)n_pad * es));
+      if (w) HIP_CHECK(hipMalloc(&ds->w, (size_t)n_pad * es));
+      HIP_CHECK(hipMemsetAsync(ds->X, 0, (size_t)n_pad * nfeat * es, ctx->stream));
+      HIP_CHECK(hipMemsetAsync(ds->y, 0, (size_t)n_pad * es, ctx->stream));
+      if (w) HIP_CHECK(hipMemsetAsync(ds->w, 0, (size_t)n_pad * es, ctx->stream));
+      if (rows > 0) {
+        // raw shard upload, then pack/transposes on the device
+        void* raw = nullptr;
+        void* rawv = nullptr;
+        int* bad = nullptr;
+        HIP_CHECK(hipMalloc(&raw, (size_t)rows * nfeat * es));
+        HIP_CHECK(hipMalloc(&rawv, (size_t)rows * es));
+        HIP_CHECK(hipMalloc((void**)&bad, sizeof(int)));
+        HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int), ctx->stream));
+        if (x_layout == SRHIP_X_JULIA) {
+          HIP_CHECK(hipMemcpyAsync(raw, static_cast<const char*>(X) + (size_t)row_begin * nfeat * es,
+                                   (size_t)rows * nfeat * es, hipMemcpyHostToDevice, ctx->stream));
+        } else {
+          HIP_CHECK(hipMemcpy2DAsync(raw, rows * es, static_cast<const char*>(X) + row_begin * es, n * es,
+                                     rows * es, nfeat, hipMemcpyHostToDevice, ctx->stream));
+        }
+        const int64_t src_stride = rows;  // packed feature-major shard
+        if (dtype == SRHIP_F32)
+          HIP_CHECK(launch_pack_x<float>((const float*)raw, x_layout, src_stride, rows, nfeat, n_pad, (float*)ds->X, bad, ctx->stream));
+        else
+          HIP_CHECK(launch_pack_x<double>((const double*)raw, x_layout, src_stride, rows, nfeat, n_pad, (double*)ds->X, bad, ctx->stream));
+        const void* vecs[2] = {y, w};
+        void* dsts[2] = {ds->y, ds->w};
+        for (int k = 0; k < 2; ++k) {
+          if (!vecs[k]) continue;
+          HIP_CHECK(hipMemcpyAsync(rawv, static_cast<const char*>(vecs[k]) + (size_t)row_begin * es, (size_t)rows * es,
+                                   hipMemcpyHostToDevice, ctx->stream));
+          if (dtype == SRHIP_F32)
+            HIP_CHECK(launch_pack_vec<float>((const float*)rawv, rows, n_pad, (float*)dsts[k], ctx->stream));
+          else
+            HIP_CHECK(launch_pack_vec<double>((const double*)rawv, rows, n_pad, (double*)dsts[k], ctx->stream));
+        }
+        int hbad = 0;
+        HIP_CHECK(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
+        HIP_CHECK(hipStreamSynchronize(ctx->stream));
+        (void)hipFree(raw);
+        (void)hipFree(rawv);
+        (void)hipFree(bad);
+        ds->x_finite = hbad == 0;
+      }
+      HIP_CHECK(hipStreamSynchronize(ctx->stream));
+      // Σw and Σ y·w over the shard, in double (src/Dataset.jl:56-60)
+      double sw = 0.0, syw = 0.0;
+      for (int64_t i = row_begin; i < row_end; ++i) {
+        const double yi = dtype == SRHIP_F32 ? (double)static_cast<const float*>(y)[i] : static_cast<const double*>(y)[i];
+        double wi = 1.0;
+        if (w) {
+          wi = dtype == SRHIP_F32 ? (double)static_cast<const float*>(w)[i] : static_cast<const double*>(w)[i];
+          ds->h_w.push_back(wi);
+        }
+        sw += wi;
+        syw += yi * wi;
+      }
+      ds->sum_w = sw;
+      ds->sum_yw = syw;
+    } catch (...) {
+      if (ds->X) (void)hipFree(ds->X);
+      if (ds->y) (void)hipFree(ds->y);
+      if (ds->w) (void)hipFree(ds->w);
+      delete ds;
+      throw;
+    }
+    *out_ds = ds;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_dataset_destroy(srhip_dataset* ds) {
+  return guarded([&] {
+    if (!ds) return SRHIP_OK;
+    std::lock_guard<std::mutex> lk(ds->ctx->mu);
+    (void)hipSetDevice(ds->ctx->device);
+    (void)hipStreamSynchronize(ds->ctx->stream);
+    if (ds->X) (void)hipFree(ds->X);
+    if (ds->y) (void)hipFree(ds->y);
+    if (ds->w) (void)hipFree(ds->w);
+    delete ds;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_dataset_info(const srhip_dataset* ds, int64_t* out_rows, int32_t* out_nfeat,
+                           double* out_sum_w, double* out_sum_yw, int32_t* out_x_finite) {
+  return guarded([&] {
+    if (!ds) throw Error(SRHIP_ERR_INVALID, "null dataset");
+    if (out_rows) *out_rows = ds->rows;
+    if (out_nfeat) *out_nfeat = ds->nfeat;
+    if (out_sum_w) *out_sum_w = ds->sum_w;
+    if (out_sum_yw) *out_sum_yw = ds->sum_yw;
+    if (out_x_finite) *out_x_finite = ds->x_finite ? 1 : 0;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_program_create(srhip_ctx* ctx, int32_t dtype, const srhip_trees* trees,
+                             srhip_program** out_prog) {
+  return guarded([&] {
+    if (!ctx || !trees || !out_prog) throw Error(SRHIP_ERR_INVALID, "null argument");
+    *out_prog = nullptr;
+    if (dtype != SRHIP_F32 && dtype != SRHIP_F64) throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
+    if (trees->ntrees < 0) throw Error(SRHIP_ERR_INVALID, "negative tree count");
+    const int nt = trees->ntrees;
+    auto* p = new srhip_program();
+    p->ctx = ctx;
+    p->dtype = dtype;
+    p->ntrees = nt;
+    try {
+      if (nt > 0) {
+        if (!trees->node_off || !trees->const_off) throw Error(SRHIP_ERR_INVALID, "null offsets");
+        const int nn = trees->node_off[nt];
+        const int nc = trees->const_off[nt];
+        if (trees->node_off[0] != 0 || trees->const_off[0] != 0 || nn < 0 || nc < 0)
+          throw Error(SRHIP_ERR_INVALID, "offsets must start at 0");
+        for (int t = 0; t < nt; ++t)
+          if (trees->node_off[t + 1] < trees->node_off[t] || trees->const_off[t + 1] < trees->const_off[t])
+            throw Error(SRHIP_ERR_INVALID, "offsets must be non-decreasing");
+        if (nn > 0 && (!trees->kind || !trees->arg)) throw Error(SRHIP_ERR_INVALID, "null node arrays");
+        if (nc > 0 && !trees->consts) throw Error(SRHIP_ERR_INVALID, "null constants");
+        p->node_off.assign(trees->node_off, trees->node_off + nt + 1);
+        p->const_off.assign(trees->const_off, trees->const_off + nt + 1);
+        p->kind.assign(trees->kind, trees->kind + nn);
+        p->arg.assign(trees->arg, trees->arg + nn);
+        const size_t cb = (size_t)nc * dtype_size(dtype);
+        p->consts.resize(std::max<size_t>(cb, 1));
+        if (cb) std::memcpy(p->consts.data(), trees->consts, cb);
+      } else {
+        p->node_off.assign(1, 0);
+        p->const_off.assign(1, 0);
+        p->consts.resize(1);
+      }
+      std::lock_guard<std::mutex> lk(ctx->mu);
+      HIP_CHECK(hipSetDevice(ctx->device));
+      if (dtype == SRHIP_F32) build_program<float>(p);
+      else build_program<double>(p);
+    } catch (...) {
+      free_program_device(p);
+      delete p;
+      throw;
+    }
+    *out_prog = p;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_program_destroy(srhip_program* prog) {
+  return guarded([&] {
+    if (!prog) return SRHIP_OK;
+    std::lock_guard<std::mutex> lk(prog->ctx->mu);
+    (void)hipSetDevice(prog->ctx->device);
+    (void)hipStreamSynchronize(prog->ctx->stream);
+    free_program_device(prog);
+    delete prog;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_program_info(const srhip_program* prog, int32_t* out_ntrees, int64_t* out_total_nodes,
+                           int32_t* out_nodes) {
+  return guarded([&] {
+    if (!prog) throw Error(SRHIP_ERR_INVALID, "null program");
+    if (out_ntrees) *out_ntrees = prog->ntrees;
+    if (out_total_nodes) *out_total_nodes = prog->total_nodes;
+    if (out_nodes) std::copy(prog->nodes.begin(), prog->nodes.end(), out_nodes);
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_program_set_constants(srhip_program* prog, const void* consts) {
+  return guarded([&] {
+    if (!prog) throw Error(SRHIP_ERR_INVALID, "null program");
+    const size_t cb = (size_t)prog->const_off.back() * dtype_size(prog->dtype);
+    if (cb && !consts) throw Error(SRHIP_ERR_INVALID, "null constants");
+    if (cb) std::memcpy(prog->consts.data(), consts, cb);
+    std::lock_guard<std::mutex> lk(prog->ctx->mu);
+    HIP_CHECK(hipSetDevice(prog->ctx->device));
+    if (prog->dtype == SRHIP_F32) build_program<float>(prog);
+    else build_program<double>(prog);
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_eval_loss(srhip_dataset* ds, const srhip_program* prog, int32_t loss_kind,
+                        const double* loss_params, const int64_t* row_idx, int64_t nidx,
+                        double* out_loss_sum, double* out_weight_sum, uint8_t* out_ok) {
+  return guarded([&] {
+    check_program_vs_dataset(ds, prog);
+    if (loss_kind < 0 || loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
+    const bool needs_param = loss_kind == SRHIP_LOSS_LP || loss_kind == SRHIP_LOSS_HUBER ||
+                             loss_kind == SRHIP_LOSS_L1EPSINS || loss_kind == SRHIP_LOSS_L2EPSINS ||
+                             loss_kind == SRHIP_LOSS_QUANTILE || loss_kind == SRHIP_LOSS_PERIODIC;
+    if (needs_param && !loss_params) throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
+    std::lock_guard<std::mutex> lk(ds->ctx->mu);
+    HIP_CHECK(hipSetDevice(ds->ctx->device));
+    if (ds->dtype == SRHIP_F32)
+      return eval_loss_impl<float>(ds, prog, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
+    return eval_loss_impl<double>(ds, prog, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
+  });
+}
+
+int32_t srhip_eval_loss_batch(srhip_dataset* ds, const srhip_trees* trees, int32_t loss_kind,
+                              const double* loss_params, const int64_t* row_idx, int64_t nidx,
+                              double* out_loss_sum, double* out_weight_sum, uint8_t* out_ok) {
+  if (!ds) return set_error(SRHIP_ERR_INVALID, "null dataset");
+  srhip_program* p = nullptr;
+  int32_t rc = srhip_program_create(ds->ctx, ds->dtype, trees, &p);
+  if (rc != SRHIP_OK) return rc;
+  rc = srhip_eval_loss(ds, p, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
+  std::string err = g_last_error;
+  srhip_program_destroy(p);
+  g_last_error = err;
+  return rc;
+}
+
+int32_t srhip_eval_tree_array(srhip_dataset* ds, const srhip_program* prog, void* out, uint8_t* out_ok) {
+  return guarded([&] {
+    check_program_vs_dataset(ds, prog);
+    std::lock_guard<std::mutex> lk(ds->ctx->mu);
+    HIP_CHECK(hipSetDevice(ds->ctx->device));
+    if (ds->dtype == SRHIP_F32) return eval_tree_array_impl<float>(ds, prog, out, out_ok);
+    return eval_tree_array_impl<double>(ds, prog, out, out_ok);
+  });
+}
+
+int32_t srhip_eval_loss_grad(srhip_dataset* ds, const srhip_program* prog, int32_t loss_kind,
+                             const double* loss_params, double* out_loss_sum, double* out_dloss,
+                             double* out_weight_sum, uint8_t* out_ok) {
+  (void)ds; (void)prog; (void)loss_kind; (void)loss_params; (void)out_loss_sum;
+  (void)out_dloss; (void)out_weight_sum; (void)out_ok;
+  return set_error(SRHIP_ERR_UNSUPPORTED, "constant gradients are not implemented yet");
+}
+
+int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog, void* out_value,
+                                   void* out_grad, uint8_t* out_ok) {
+  (void)ds; (void)prog; (void)out_value; (void)out_grad; (void)out_ok;
+  return set_error(SRHIP_ERR_UNSUPPORTED, "constant gradients are not implemented yet");
+}
+
+int32_t srhip_last_kernel_time(const srhip_ctx* ctx, double* out_ms, int32_t* out_launches) {
+  return guarded([&] {
+    if (!ctx) throw Error(SRHIP_ERR_INVALID, "null ctx");
+    if (out_ms) *out_ms = ctx->last_ms;
+    if (out_launches) *out_launches = ctx->last_launches;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_sync(srhip_ctx* ctx) {
+  return guarded([&] {
+    if (!ctx) throw Error(SRHIP_ERR_INVALID, "null ctx");
+    HIP_CHECK(hipSetDevice(ctx->device));
+    HIP_CHECK(hipStreamSynchronize(ctx->stream));
+    return SRHIP_OK;
+  });
+}
+
+}  // extern "C"

@@ -1,0 +1,274 @@
+// compile.cpp — postfix node streams → device accumulator-machine programs.
+//
+// Per tree:
+//  1. parse the post-order stream into nodes (DAG sharing was already
+//     expanded by the flattener: a shared child appears once per reference,
+//     as DynamicExpressions evaluates it, test_preserve_multiple_parents.jl:9-14);
+//  2. fold every maximal feature-free subtree of degree >= 1 into one
+//     constant with host_ops.h, reproducing `_eval_constant_tree` (a folded
+//     operator output that is non-finite makes the tree fail for every row
+//     count, as the reference does before looking at rows);
+//  3. static checks of the remaining constant leaves: DynamicExpressions
+//     checks every constant leaf that sits next to a feature-bearing subtree
+//     (`@return_on_check` in the fused deg2_l0*/deg1_l2* kernels), so a
+//     non-finite one fails the tree; a non-finite constant ROOT fails only
+//     when there are rows (fill + final array check);
+//  4. emit code in Sethi–Ullman order (the operand needing more stack slots
+//     first), fusing leaf operands into the consuming instruction.
+#include "compile.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+
+#include "host_ops.h"
+
+namespace srhip {
+namespace {
+
+struct HNode {
+  int deg;       // 0, 1, 2
+  int op;        // operator id (deg >= 1)
+  int feat;      // feature index (deg 0, -1 for a constant)
+  int l, r;      // children
+  double val;    // constant value (deg 0 const), held in T precision
+  bool has_feature;
+  int need;      // stack slots needed (Sethi–Ullman number for this machine)
+};
+
+template <typename T>
+struct TreeCompiler {
+  std::vector<HNode> nd;
+  std::vector<Ins<T>>* out;
+  bool fold_fail = false;
+  int max_feat = -1;
+
+  static bool is_leaf(const HNode& x) { return x.deg == 0; }
+
+  // Scalar evaluation of a feature-free subtree (`_eval_constant_tree`).
+  bool eval_const(int i, T* v) {
+    const HNode& x = nd[i];
+    if (x.deg == 0) { *v = (T)x.val; return true; }
+    if (x.deg == 1) {
+      T a;
+      if (!eval_const(x.l, &a)) return false;
+      *v = host::unop<T>(x.op, a);
+      return std::isfinite(*v);
+    }
+    T a, b;
+    if (!eval_const(x.l, &a) || !eval_const(x.r, &b)) return false;
+    *v = host::binop<T>(x.op, a, b);
+    return std::isfinite(*v);
+  }
+
+  void fold(int i) {
+    HNode& x = nd[i];
+    if (x.deg == 0) return;
+    if (!x.has_feature) {
+      T v;
+      if (!eval_const(i, &v)) fold_fail = true;
+      x.deg = 0; x.feat = -1; x.val = (double)v; x.l = x.r = -1;
+      return;
+    }
+    fold(x.l);
+    if (x.deg == 2) fold(x.r);
+  }
+
+  int compute_need(int i) {
+    HNode& x = nd[i];
+    if (x.deg == 0) return x.need = 0;
+    if (x.deg == 1) return x.need = compute_need(x.l);
+    int a = compute_need(x.l), b = compute_need(x.r);
+    const HNode& L = nd[x.l];
+    const HNode& R = nd[x.r];
+    if (is_leaf(L) || is_leaf(R)) return x.need = std::max(a, b);
+    int hi = std::max(a, b), lo = std::min(a, b);
+    return x.need = std::max(hi, lo + 1);
+  }
+
+  bool nonroot_const_nonfinite(int i) {
+    const HNode& x = nd[i];
+    if (x.deg == 0) return x.feat < 0 && !std::isfinite(x.val);
+    if (nonroot_const_nonfinite(x.l)) return true;
+    return x.deg == 2 && nonroot_const_nonfinite(x.r);
+  }
+
+  void put(int opc, int slot, int feat, T imm) {
+    Ins<T> ins;
+    std::memset(&ins, 0, sizeof(ins));
+    ins.code = make_code(opc, slot, feat);
+    ins.imm = imm;
+    out->push_back(ins);
+  }
+  void put_feat2(int opc, int f, int g) {
+    Ins<T> ins;
+    std::memset(&ins, 0, sizeof(ins));
+    ins.code = make_code(opc, 0, f);
+    if constexpr (sizeof(T) == 4) {
+      uint32_t gg = (uint32_t)g;
+      std::memcpy(&ins.imm, &gg, 4);
+    } else {
+      uint64_t gg = (uint64_t)g;
+      std::memcpy(&ins.imm, &gg, 8);
+    }
+    out->push_back(ins);
+  }
+
+  // Emit code leaving node i's value in acc; slots [base, ...) are free.
+  void emit(int i, int base) {
+    const HNode& x = nd[i];
+    if (x.deg == 0) {
+      if (x.feat >= 0) put(OP_LDX, 0, x.feat, T(0));
+      else put(OP_LDC, 0, 0, (T)x.val);
+      return;
+    }
+    if (x.deg == 1) {
+      emit(x.l, base);
+      put(OP_UN0 + x.op, 0, 0, T(0));
+      return;
+    }
+    const HNode& L = nd[x.l];
+    const HNode& R = nd[x.r];
+    const int op = x.op;
+    if (is_leaf(L) && is_leaf(R)) {
+      if (L.feat >= 0 && R.feat >= 0) put_feat2(bin_opcode(V_XX, op), L.feat, R.feat);
+      else if (L.feat >= 0) put(bin_opcode(V_XC, op), 0, L.feat, (T)R.val);
+      else if (R.feat >= 0) put(bin_opcode(V_CX, op), 0, R.feat, (T)L.val);
+      else {  // cannot happen after folding, kept for safety
+        put(OP_LDC, 0, 0, (T)L.val);
+        put(bin_opcode(V_AC, op), 0, 0, (T)R.val);
+      }
+      return;
+    }
+    if (is_leaf(R)) {
+      emit(x.l, base);
+      if (R.feat >= 0) put(bin_opcode(V_AX, op), 0, R.feat, T(0));
+      else put(bin_opcode(V_AC, op), 0, 0, (T)R.val);
+      return;
+    }
+    if (is_leaf(L)) {
+      emit(x.r, base);
+      if (L.feat >= 0) put(bin_opcode(V_XA, op), 0, L.feat, T(0));
+      else put(bin_opcode(V_CA, op), 0, 0, (T)L.val);
+      return;
+    }
+    if (base >= kMaxSlots) throw Error(SRHIP_ERR_UNSUPPORTED, "tree needs more than 16 stack slots");
+    if (L.need >= R.need) {
+      emit(x.l, base);
+      put(OP_PUSH0 + base, base, 0, T(0));
+      emit(x.r, base + 1);
+      put(OP_POP0 + base, base, 0, T(0));
+      put(bin_opcode(V_TA, op), 0, 0, T(0));  // lhs = tmp (left), rhs = acc (right)
+    } else {
+      emit(x.r, base);
+      put(OP_PUSH0 + base, base, 0, T(0));
+      emit(x.l, base + 1);
+      put(OP_POP0 + base, base, 0, T(0));
+      put(bin_opcode(V_AT, op), 0, 0, T(0));  // lhs = acc (left), rhs = tmp (right)
+    }
+  }
+
+  int cost(int i) const {
+    const HNode& x = nd[i];
+    if (x.deg == 0) return 1;
+    if (x.deg == 1) return uop_cost(x.op) + cost(x.l);
+    return bop_cost(x.op) + cost(x.l) + cost(x.r);
+  }
+};
+
+}  // namespace
+
+template <typename T>
+CompiledBatch<T> compile_batch(const srhip_trees& trees) {
+  if (trees.ntrees < 0) throw Error(SRHIP_ERR_INVALID, "negative tree count");
+  if (trees.ntrees > 0 && (!trees.node_off || !trees.kind || !trees.arg || !trees.const_off))
+    throw Error(SRHIP_ERR_INVALID, "null tree arrays");
+  CompiledBatch<T> cb;
+  const int nt = trees.ntrees;
+  cb.ntrees = nt;
+  cb.tree_off.assign(nt, -1);
+  cb.nodes.assign(nt, 0);
+  cb.static_fail.assign(nt, 0);
+  cb.fail_if_rows.assign(nt, 0);
+  cb.need.assign(nt, 0);
+  cb.cost.assign(nt, 0);
+  const T* consts = static_cast<const T*>(trees.consts);
+  TreeCompiler<T> tc;
+  tc.out = &cb.code;
+  std::vector<int> stk;
+  for (int t = 0; t < nt; ++t) {
+    const int b = trees.node_off[t], e = trees.node_off[t + 1];
+    const int cb0 = trees.const_off[t], ce = trees.const_off[t + 1];
+    if (e <= b) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + " is empty");
+    if (ce < cb0) throw Error(SRHIP_ERR_INVALID, "bad const_off");
+    tc.nd.assign(e - b, HNode{});
+    tc.fold_fail = false;
+    stk.clear();
+    int ci = cb0;
+    for (int i = 0; i < e - b; ++i) {
+      HNode& x = tc.nd[i];
+      x.l = x.r = -1; x.op = 0; x.feat = -1; x.val = 0; x.need = 0;
+      const int kind = trees.kind[b + i];
+      const int arg = trees.arg[b + i];
+      switch (kind) {
+        case SRHIP_NODE_CONST:
+          if (ci >= ce) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": more constant leaves than constants");
+          x.deg = 0; x.val = (double)consts[ci++]; x.has_feature = false;
+          break;
+        case SRHIP_NODE_FEATURE:
+          x.deg = 0; x.feat = arg; x.has_feature = true;
+          tc.max_feat = std::max(tc.max_feat, arg);
+          break;
+        case SRHIP_NODE_UNARY:
+          if (arg >= SRHIP_NUM_UOPS) throw Error(SRHIP_ERR_UNSUPPORTED, "unknown unary operator id " + std::to_string(arg));
+          if (stk.empty()) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": stack underflow");
+          x.deg = 1; x.op = arg; x.l = stk.back(); stk.pop_back();
+          x.has_feature = tc.nd[x.l].has_feature;
+          break;
+        case SRHIP_NODE_BINARY:
+          if (arg >= SRHIP_NUM_BOPS) throw Error(SRHIP_ERR_UNSUPPORTED, "unknown binary operator id " + std::to_string(arg));
+          if (stk.size() < 2) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": stack underflow");
+          x.deg = 2; x.op = arg;
+          x.r = stk.back(); stk.pop_back();
+          x.l = stk.back(); stk.pop_back();
+          x.has_feature = tc.nd[x.l].has_feature || tc.nd[x.r].has_feature;
+          break;
+        default:
+          throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": bad node kind " + std::to_string(kind));
+      }
+      stk.push_back(i);
+    }
+    if (stk.size() != 1) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": postfix stream does not reduce to one root");
+    if (ci != ce) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": constant count mismatch");
+    const int root = stk[0];
+    cb.nodes[t] = e - b;
+    cb.total_nodes += e - b;
+    cb.cost[t] = tc.cost(root);
+
+    const bool root_is_leaf = tc.nd[root].deg == 0;
+    tc.fold(root);
+    if (tc.fold_fail) { cb.static_fail[t] = 1; continue; }
+    if (root_is_leaf || tc.nd[root].deg == 0) {
+      // a leaf (or folded) root: `deg0_eval` fill/copy + the final array check
+      const HNode& r = tc.nd[root];
+      if (r.feat < 0 && !std::isfinite(r.val)) { cb.fail_if_rows[t] = 1; continue; }
+    } else if (tc.nonroot_const_nonfinite(root)) {
+      cb.static_fail[t] = 1;
+      continue;
+    }
+    cb.need[t] = tc.compute_need(root);
+    if (cb.need[t] > kMaxSlots) throw Error(SRHIP_ERR_UNSUPPORTED, "tree needs more than 16 stack slots");
+    cb.tree_off[t] = (int32_t)cb.code.size();
+    tc.emit(root, 0);
+    tc.put(OP_END, 0, 0, T(0));
+  }
+  cb.max_feature = tc.max_feat;
+  // trailing OP_END: the kernel prefetches one instruction past each END
+  tc.put(OP_END, 0, 0, T(0));
+  return cb;
+}
+
+template CompiledBatch<float> compile_batch<float>(const srhip_trees&);
+template CompiledBatch<double> compile_batch<double>(const srhip_trees&);
+
+}  // namespace srhip

@@ -1,0 +1,164 @@
+// device_ops.h — operator and loss semantics on the device (gfx950).
+//
+// Semantics: src/Operators.jl:8-111 after the mapping of
+// src/Options.jl:86-120; Base.mod / max / min for floats; LossFunctions.jl
+// distance losses (docs/src/losses.md). `+ - * /` and sqrt are IEEE
+// correctly rounded (built with -ffp-contract=off, no fast-math, f32
+// denormals kept), so they are bit-identical to Julia; transcendentals use
+// OCML's full-precision routines (never the __expf-style intrinsics).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "srhip_internal.h"
+
+namespace srhip {
+namespace dev {
+
+// ---- thin overload set over OCML ----------------------------------------------
+#define SR_M1(name, f32, f64)                                              \
+  __device__ __forceinline__ float name(float x) { return f32(x); }        \
+  __device__ __forceinline__ double name(double x) { return f64(x); }
+SR_M1(m_exp, expf, exp)
+SR_M1(m_log, logf, log)
+SR_M1(m_log2, log2f, log2)
+SR_M1(m_log10, log10f, log10)
+SR_M1(m_log1p, log1pf, log1p)
+SR_M1(m_sqrt, sqrtf, sqrt)
+SR_M1(m_sin, sinf, sin)
+SR_M1(m_cos, cosf, cos)
+SR_M1(m_tan, tanf, tan)
+SR_M1(m_sinh, sinhf, sinh)
+SR_M1(m_cosh, coshf, cosh)
+SR_M1(m_tanh, tanhf, tanh)
+SR_M1(m_atan, atanf, atan)
+SR_M1(m_asinh, asinhf, asinh)
+SR_M1(m_acosh, acoshf, acosh)
+SR_M1(m_atanh, atanhf, atanh)
+SR_M1(m_erf, erff, erf)
+SR_M1(m_erfc, erfcf, erfc)
+SR_M1(m_tgamma, tgammaf, tgamma)
+SR_M1(m_rint, rintf, rint)
+SR_M1(m_floor, floorf, floor)
+SR_M1(m_ceil, ceilf, ceil)
+SR_M1(m_trunc, truncf, trunc)
+SR_M1(m_fabs, fabsf, fabs)
+#undef SR_M1
+__device__ __forceinline__ float m_pow(float x, float y) { return powf(x, y); }
+__device__ __forceinline__ double m_pow(double x, double y) { return pow(x, y); }
+__device__ __forceinline__ float m_fmod(float x, float y) { return fmodf(x, y); }
+__device__ __forceinline__ double m_fmod(double x, double y) { return fmod(x, y); }
+__device__ __forceinline__ float m_copysign(float x, float y) { return copysignf(x, y); }
+__device__ __forceinline__ double m_copysign(double x, double y) { return copysign(x, y); }
+__device__ __forceinline__ bool m_isinf(float x) { return __builtin_isinf(x); }
+__device__ __forceinline__ bool m_isinf(double x) { return __builtin_isinf(x); }
+__device__ __forceinline__ bool m_signbit(float x) { return __builtin_signbit(x); }
+__device__ __forceinline__ bool m_signbit(double x) { return __builtin_signbit(x); }
+template <typename T>
+__device__ __forceinline__ T qnan() { return __builtin_nan(""); }
+template <>
+__device__ __forceinline__ float qnan<float>() { return __builtin_nanf(""); }
+
+// Base.mod for floats: r = rem(x, y) (= fmod, exact); r == 0 → copysign(r, y);
+// sign(r) != sign(y) → r + y; else r.
+template <typename T>
+__device__ __forceinline__ T jl_mod(T x, T y) {
+  T r = m_fmod(x, y);
+  T s = r + y;
+  bool flip = (r > T(0)) != (y > T(0));
+  T v = flip ? s : r;
+  return (r == T(0)) ? m_copysign(r, y) : v;
+}
+
+// ---- binary operators -----------------------------------------------------------
+template <int OP, typename T>
+__device__ __forceinline__ T bop(T x, T y) {
+  if constexpr (OP == SRHIP_BOP_ADD) return x + y;
+  else if constexpr (OP == SRHIP_BOP_SUB) return x - y;
+  else if constexpr (OP == SRHIP_BOP_MUL) return x * y;
+  else if constexpr (OP == SRHIP_BOP_DIV) return x / y;
+  else if constexpr (OP == SRHIP_BOP_POW) {
+    // safe_pow, Operators.jl:38-46
+    const bool isint = (y == m_trunc(y));
+    const bool bad = isint ? (y < T(0) && x == T(0))
+                           : ((y > T(0) && x < T(0)) || (y < T(0) && x <= T(0)));
+    const T p = m_pow(x, y);
+    return bad ? qnan<T>() : p;
+  } else if constexpr (OP == SRHIP_BOP_GREATER) return x > y ? T(1) : T(0);
+  else if constexpr (OP == SRHIP_BOP_LOGICAL_OR) return (x > T(0) || y > T(0)) ? T(1) : T(0);
+  else if constexpr (OP == SRHIP_BOP_LOGICAL_AND) return (x > T(0) && y > T(0)) ? T(1) : T(0);
+  else if constexpr (OP == SRHIP_BOP_MOD) return jl_mod(x, y);
+  else if constexpr (OP == SRHIP_BOP_MAX) {
+    // operands are finite whenever the result matters; keep -0.0 < +0.0
+    T m = (x > y) ? x : y;
+    return (x == y) ? (m_signbit(x) ? y : x) : m;
+  } else if constexpr (OP == SRHIP_BOP_MIN) {
+    T m = (x < y) ? x : y;
+    return (x == y) ? (m_signbit(x) ? x : y) : m;
+  } else {
+    static_assert(OP < SRHIP_NUM_BOPS, "unknown binary op");
+    return x;
+  }
+}
+
+// ---- unary operators --------------------------------------------------------------
+template <int OP, typename T>
+__device__ __forceinline__ T uop(T x) {
+  if constexpr (OP == SRHIP_UOP_NEG) return -x;
+  else if constexpr (OP == SRHIP_UOP_SQUARE) return x * x;
+  else if constexpr (OP == SRHIP_UOP_CUBE) return (x * x) * x;
+  else if constexpr (OP == SRHIP_UOP_EXP) return m_exp(x);
+  else if constexpr (OP == SRHIP_UOP_ABS) return m_fabs(x);
+  else if constexpr (OP == SRHIP_UOP_LOG) { T v = m_log(x); return x <= T(0) ? qnan<T>() : v; }
+  else if constexpr (OP == SRHIP_UOP_LOG2) { T v = m_log2(x); return x <= T(0) ? qnan<T>() : v; }
+  else if constexpr (OP == SRHIP_UOP_LOG10) { T v = m_log10(x); return x <= T(0) ? qnan<T>() : v; }
+  else if constexpr (OP == SRHIP_UOP_LOG1P) { T v = m_log1p(x); return x <= T(-1) ? qnan<T>() : v; }
+  else if constexpr (OP == SRHIP_UOP_SQRT) { T v = m_sqrt(x); return x < T(0) ? qnan<T>() : v; }
+  else if constexpr (OP == SRHIP_UOP_SIN) return m_sin(x);
+  else if constexpr (OP == SRHIP_UOP_COS) return m_cos(x);
+  else if constexpr (OP == SRHIP_UOP_TAN) return m_tan(x);
+  else if constexpr (OP == SRHIP_UOP_SINH) return m_sinh(x);
+  else if constexpr (OP == SRHIP_UOP_COSH) return m_cosh(x);
+  else if constexpr (OP == SRHIP_UOP_TANH) return m_tanh(x);
+  else if constexpr (OP == SRHIP_UOP_ATAN) return m_atan(x);
+  else if constexpr (OP == SRHIP_UOP_ASINH) return m_asinh(x);
+  else if constexpr (OP == SRHIP_UOP_ACOSH) { T v = m_acosh(x); return x < T(1) ? qnan<T>() : v; }
+  else if constexpr (OP == SRHIP_UOP_ATANH_CLIP) return m_atanh(jl_mod(x + T(1), T(2)) - T(1));
+  else if constexpr (OP == SRHIP_UOP_ERF) return m_erf(x);
+  else if constexpr (OP == SRHIP_UOP_ERFC) return m_erfc(x);
+  else if constexpr (OP == SRHIP_UOP_GAMMA) { T g = m_tgamma(x); return m_isinf(g) ? qnan<T>() : g; }
+  else if constexpr (OP == SRHIP_UOP_RELU) return (x + m_fabs(x)) * T(0.5);  // == /2 exactly
+  else if constexpr (OP == SRHIP_UOP_ROUND) return m_rint(x);
+  else if constexpr (OP == SRHIP_UOP_FLOOR) return m_floor(x);
+  else if constexpr (OP == SRHIP_UOP_CEIL) return m_ceil(x);
+  else if constexpr (OP == SRHIP_UOP_SIGN) return x > T(0) ? T(1) : (x < T(0) ? T(-1) : x);
+  else if constexpr (OP == SRHIP_UOP_INV) return T(1) / x;
+  else {
+    static_assert(OP < SRHIP_NUM_UOPS, "unknown unary op");
+    return x;
+  }
+}
+
+// ---- elementwise losses, r = ŷ - y -------------------------------------------------
+// L2 and L1 are formed in T like LossFunctions (abs2 / abs of the T residual);
+// the parametric losses evaluate in T with the parameter rounded to T.
+template <typename T>
+__device__ __forceinline__ T elem_loss(int kind, T p, T yhat, T y) {
+  const T r = yhat - y;
+  const T ar = m_fabs(r);
+  switch (kind) {
+    case SRHIP_LOSS_L2: return r * r;
+    case SRHIP_LOSS_L1: return ar;
+    case SRHIP_LOSS_LP: return m_pow(ar, p);
+    case SRHIP_LOSS_HUBER: return ar <= p ? T(0.5) * r * r : p * (ar - T(0.5) * p);
+    case SRHIP_LOSS_LOGCOSH: return ar + m_log1p(m_exp(T(-2) * ar)) - T(0.69314718055994530942);
+    case SRHIP_LOSS_L1EPSINS: return ar > p ? ar - p : T(0);
+    case SRHIP_LOSS_L2EPSINS: { T e = ar > p ? ar - p : T(0); return e * e; }
+    case SRHIP_LOSS_QUANTILE: return r >= T(0) ? p * r : (p - T(1)) * r;
+    case SRHIP_LOSS_PERIODIC: return T(1) - m_cos(T(6.28318530717958647692) * r / p);
+    case SRHIP_LOSS_LOGITDIST: return ar + T(2) * m_log1p(m_exp(-ar)) - T(1.38629436111989061883);
+  }
+  return qnan<T>();
+}
+
+}  // namespace dev
+}  // namespace srhip

@@ -1,0 +1,88 @@
+// kernels.h — launch interface of the HIP kernels (kernels.hip) for the
+// host runtime (api.cpp). No torch, no HIP types beyond the stream.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "srhip_internal.h"
+
+namespace srhip {
+
+enum EvalMode : int { MODE_LOSS = 0, MODE_OUT = 1 };
+
+// Per-(tree, row-group) partial result: Σ w·ℓ over the group's rows and the
+// non-finite marker (0, or NaN when some checked value was non-finite).
+template <typename T>
+struct alignas(2 * sizeof(T)) Part {
+  T sum;
+  T chk;
+};
+
+template <typename T>
+struct EvalArgs {
+  const Ins<T>* prog;      // all programs
+  const int32_t* tree_off; // [ntrees] program start per tree
+  const int32_t* list;     // tree ids handled by this launch, cost-descending
+  int nlist;
+  const T* X;              // [nfeat][n_pad] feature-major, rows padded
+  const T* y;              // [n_pad]
+  const T* w;              // [n_pad] or nullptr
+  int64_t n;               // valid rows
+  int64_t n_pad;
+  int nfeat;
+  int ntiles;              // row tiles per workgroup
+  int ntg;                 // tree groups
+  int tpb;                 // trees per group
+  int nrg;                 // row groups
+  int loss;
+  T lparam;
+  Part<T>* partial;        // [nrg][ntg*tpb]
+  T* out;                  // MODE_OUT: [ntrees][out_stride]
+  int64_t out_stride;
+};
+
+// Geometry of one evaluation launch, chosen by plan_eval().
+struct EvalPlan {
+  int R;          // rows per lane per instruction
+  int D;          // stack slots of the kernel variant (4 or 16)
+  int tile;       // rows per tile = 64 * R
+  int ntiles;
+  int rows_wg;    // rows per workgroup
+  int nrg, ntg, tpb;
+  size_t lds_bytes;
+  int threads;    // workgroup size
+};
+
+// Choose the geometry for `nlist` trees over `n` rows; returns false when the
+// row tile of this feature count does not fit in LDS.
+bool plan_eval(int dtype, bool deep, int mode, bool weighted, int nfeat,
+               int64_t n, int nlist, EvalPlan* plan);
+
+template <typename T>
+hipError_t launch_eval(const EvalPlan& plan, const EvalArgs<T>& a, int mode,
+                       hipStream_t stream);
+
+// Σ over row groups of the partials → per-tree fp64 sum and ok flag.
+template <typename T>
+hipError_t launch_finalize(const EvalArgs<T>& a, double* out_sum,
+                           uint8_t* out_ok, hipStream_t stream);
+
+// Dataset packing: src rows [0, rows) in Julia (nfeat, n) column-major layout
+// (layout 0) or feature-major with row stride src_stride (layout 1) →
+// dst [nfeat][n_pad], padding rows replicate the last row. Sets *bad if a
+// non-finite value is seen.
+template <typename T>
+hipError_t launch_pack_x(const T* src, int layout, int64_t src_stride,
+                         int64_t rows, int nfeat, int64_t n_pad, T* dst,
+                         int* bad, hipStream_t stream);
+template <typename T>
+hipError_t launch_pack_vec(const T* src, int64_t rows, int64_t n_pad, T* dst,
+                           hipStream_t stream);
+// Row gather for score_func_batch: dst[f][k] = src[f][idx[k]] (+ y, w).
+template <typename T>
+hipError_t launch_gather_rows(const T* X, const T* y, const T* w, int nfeat,
+                              int64_t src_pad, const int64_t* idx, int64_t nidx,
+                              int64_t dst_pad, T* Xd, T* yd, T* wd,
+                              hipStream_t stream);
+
+}  // namespace srhip

@@ -1,0 +1,194 @@
+"""Thin object layer over the C ABI: device contexts, device datasets and
+compiled programs. Everything here calls libsrhip.so; nothing computes on
+the CPU."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import threading
+from typing import Optional
+
+import numpy as np
+
+from . import constants as K
+from ._lib import SrhipError, Trees, check, lib
+from .node import FlatTrees
+
+_ctx_lock = threading.Lock()
+_contexts: dict = {}
+
+
+def _p(a: Optional[np.ndarray]):
+    return None if a is None else a.ctypes.data_as(C.c_void_p)
+
+
+def dtype_code(dtype) -> int:
+    dt = np.dtype(dtype)
+    if dt == np.float32:
+        return K.F32
+    if dt == np.float64:
+        return K.F64
+    from ._lib import Unsupported
+
+    raise Unsupported(-2, f"dtype {dt} is not supported by the engine (Float32/Float64 only)")
+
+
+def device_count() -> int:
+    n = C.c_int32(0)
+    lib().srhip_device_count(C.byref(n))
+    return n.value
+
+
+class Context:
+    """One device + stream (srhip_open). Calls through one context are
+    serialised by the library."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(lib().srhip_open(int(device), C.byref(h)))
+        self.handle = h
+        self.device = int(device)
+
+    def close(self):
+        if self.handle:
+            lib().srhip_close(self.handle)
+            self.handle = None
+
+    def last_kernel_time(self):
+        ms = C.c_double(0)
+        n = C.c_int32(0)
+        check(lib().srhip_last_kernel_time(self.handle, C.byref(ms), C.byref(n)))
+        return ms.value, n.value
+
+    def sync(self):
+        check(lib().srhip_sync(self.handle))
+
+
+def default_device() -> int:
+    return int(os.environ.get("SRHIP_DEVICE", os.environ.get("LOCAL_RANK", "0")))
+
+
+def get_context(device: Optional[int] = None) -> Context:
+    d = default_device() if device is None else int(device)
+    with _ctx_lock:
+        c = _contexts.get(d)
+        if c is None:
+            c = Context(d)
+            _contexts[d] = c
+        return c
+
+
+class DeviceDataset:
+    """srhip_dataset: rows [row_begin, row_end) of X (nfeatures, n), y, w
+    resident on one device."""
+
+    def __init__(self, ctx: Context, X: np.ndarray, y: np.ndarray, w: Optional[np.ndarray] = None,
+                 row_begin: int = 0, row_end: Optional[int] = None):
+        if X.ndim != 2:
+            raise ValueError("X must be (nfeatures, n)")
+        dt = np.result_type(X.dtype, y.dtype)
+        code = dtype_code(dt)
+        nfeat, n = X.shape
+        if X.flags.c_contiguous:
+            layout, Xa = K.X_FEATURE_MAJOR, np.ascontiguousarray(X, dtype=dt)
+        else:  # Fortran order = Julia's column-major (nfeatures, n)
+            layout, Xa = K.X_JULIA, np.asfortranarray(X, dtype=dt)
+        ya = np.ascontiguousarray(y, dtype=dt)
+        wa = None if w is None else np.ascontiguousarray(w, dtype=dt)
+        if ya.shape != (n,) or (wa is not None and wa.shape != (n,)):
+            raise AssertionError("Dataset dimensions are invalid")  # Configure.jl:53-60
+        rb = int(row_begin)
+        re = n if row_end is None else int(row_end)
+        h = C.c_void_p()
+        check(lib().srhip_dataset_create(ctx.handle, code, layout, _p(Xa), _p(ya), _p(wa), n, nfeat, rb,
+                                         re, C.byref(h)))
+        self.handle = h
+        self.ctx = ctx
+        self.dtype = dt
+        self.nfeat = nfeat
+        self.rows = re - rb
+        self.weighted = w is not None
+
+    def info(self):
+        rows = C.c_int64()
+        nf = C.c_int32()
+        sw = C.c_double()
+        syw = C.c_double()
+        fin = C.c_int32()
+        check(lib().srhip_dataset_info(self.handle, C.byref(rows), C.byref(nf), C.byref(sw), C.byref(syw),
+                                       C.byref(fin)))
+        return dict(rows=rows.value, nfeat=nf.value, sum_w=sw.value, sum_yw=syw.value, x_finite=bool(fin.value))
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().srhip_dataset_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+class Program:
+    """srhip_program: a compiled, device-resident batch of trees."""
+
+    def __init__(self, ctx: Context, flat: FlatTrees, dtype):
+        self.ctx = ctx
+        self.dtype = np.dtype(dtype)
+        self.flat = flat
+        consts = np.ascontiguousarray(flat.consts, dtype=self.dtype)
+        self._keep = (flat.node_off, flat.kind, flat.arg, flat.const_off, consts)
+        tr = Trees(
+            flat.ntrees,
+            flat.node_off.ctypes.data_as(C.POINTER(C.c_int32)),
+            flat.kind.ctypes.data_as(C.POINTER(C.c_uint8)),
+            flat.arg.ctypes.data_as(C.POINTER(C.c_uint16)),
+            flat.const_off.ctypes.data_as(C.POINTER(C.c_int32)),
+            consts.ctypes.data_as(C.c_void_p),
+        )
+        h = C.c_void_p()
+        check(lib().srhip_program_create(ctx.handle, dtype_code(self.dtype), C.byref(tr), C.byref(h)))
+        self.handle = h
+        self.ntrees = flat.ntrees
+
+    def info(self):
+        nt = C.c_int32()
+        tot = C.c_int64()
+        nodes = np.zeros(max(self.ntrees, 1), dtype=np.int32)
+        check(lib().srhip_program_info(self.handle, C.byref(nt), C.byref(tot), _p(nodes)))
+        return nt.value, tot.value, nodes[: nt.value]
+
+    def set_constants(self, consts: np.ndarray):
+        c = np.ascontiguousarray(consts, dtype=self.dtype)
+        if c.shape != (int(self.flat.const_off[-1]),):
+            raise ValueError("constant vector has the wrong length")
+        check(lib().srhip_program_set_constants(self.handle, _p(c)))
+
+    def eval_loss(self, ds: DeviceDataset, loss_kind: int, params=None, row_idx=None):
+        nt = self.ntrees
+        sums = np.zeros(max(nt, 1), dtype=np.float64)
+        ok = np.zeros(max(nt, 1), dtype=np.uint8)
+        wsum = C.c_double(0)
+        par = None if params is None else np.asarray(params, dtype=np.float64)
+        idx = None if row_idx is None else np.ascontiguousarray(row_idx, dtype=np.int64)
+        nidx = 0 if idx is None else len(idx)
+        check(lib().srhip_eval_loss(ds.handle, self.handle, int(loss_kind), _p(par), _p(idx), nidx, _p(sums),
+                                    C.byref(wsum), _p(ok)))
+        return sums[:nt], wsum.value, ok[:nt].astype(bool)
+
+    def eval_tree_array(self, ds: DeviceDataset):
+        nt = self.ntrees
+        out = np.empty((nt, ds.rows), dtype=self.dtype)
+        ok = np.zeros(max(nt, 1), dtype=np.uint8)
+        check(lib().srhip_eval_tree_array(ds.handle, self.handle, _p(out), _p(ok)))
+        return out, ok[:nt].astype(bool)
+
+    def __del__(self):
+        try:
+            if getattr(self, "handle", None):
+                lib().srhip_program_destroy(self.handle)
+                self.handle = None
+        except Exception:
+            pass
+
+
+__all__ = ["Context", "DeviceDataset", "Program", "get_context", "device_count", "SrhipError"]

@@ -1,0 +1,145 @@
+"""The reference's scoring surface, evaluated on the MI355X engine.
+
+Single-tree functions keep the reference signatures
+  eval_tree_array(tree, X, options)        src/InterfaceDynamicExpressions.jl:50-52
+  eval_loss(tree, dataset, options)        src/LossFunctions.jl:60-67
+  score_func(dataset, tree, options)       src/LossFunctions.jl:86-92
+  score_func_batch(dataset, tree, options) src/LossFunctions.jl:95-115
+  update_baseline_loss_(dataset, options)  src/LossFunctions.jl:122-126
+  loss_to_score(loss, baseline, tree, options)  src/LossFunctions.jl:70-83
+  compute_complexity(tree, options)        src/Complexity.jl:13-40
+and each has a batched form over a list of trees (one device launch), which
+is what the search's callers are meant to use.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple, Union
+
+import numpy as np
+
+from .dataset import Dataset
+from .engine import DeviceDataset, Program, get_context
+from .node import Node, count_nodes, flatten
+from .options import Options
+
+TreeOrTrees = Union[Node, Sequence[Node]]
+
+
+def _as_list(trees: TreeOrTrees) -> Tuple[List[Node], bool]:
+    if isinstance(trees, Node):
+        return [trees], True
+    return list(trees), False
+
+
+def compile_trees(trees: Sequence[Node], options: Options, dtype, device: Optional[int] = None) -> Program:
+    """Flatten + compile + upload a batch of trees (srhip_program_create)."""
+    ctx = get_context(device)
+    return Program(ctx, flatten(trees, options, dtype=dtype), dtype)
+
+
+# ---- eval_tree_array ----------------------------------------------------------------
+def eval_tree_array(tree: TreeOrTrees, X: np.ndarray, options: Options, device: Optional[int] = None):
+    """(output, did_succeed). X is (nfeatures, n). For a list of trees the
+    outputs are (ntrees, n) and did_succeed is a bool array. On failure the
+    output rows are unspecified (the reference returns an undef array)."""
+    trees, single = _as_list(tree)
+    X = np.asarray(X)
+    T = X.dtype if X.dtype in (np.float32, np.float64) else np.dtype(np.float64)
+    ctx = get_context(device)
+    ds = DeviceDataset(ctx, X.astype(T, copy=False), np.zeros(X.shape[1], dtype=T))
+    prog = Program(ctx, flatten(trees, options, dtype=T), T)
+    out, ok = prog.eval_tree_array(ds)
+    if single:
+        return out[0], bool(ok[0])
+    return out, ok
+
+
+# ---- losses -------------------------------------------------------------------------
+def eval_loss_batch(trees: Sequence[Node], dataset: Dataset, options: Options,
+                    row_idx: Optional[np.ndarray] = None, device: Optional[int] = None,
+                    program: Optional[Program] = None) -> np.ndarray:
+    """eval_loss for many trees in one launch: the reference's `_eval_loss`
+    value in T per tree (T(Inf) where the evaluation fails)."""
+    return eval_loss_batch_ok(trees, dataset, options, row_idx, device, program)[0]
+
+
+def eval_loss_batch_ok(trees: Sequence[Node], dataset: Dataset, options: Options,
+                       row_idx: Optional[np.ndarray] = None, device: Optional[int] = None,
+                       program: Optional[Program] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """(losses in T, did_succeed per tree)."""
+    if options.loss_function is not None:
+        f = options.loss_function
+        vals = np.asarray([f(t, dataset, options) for t in trees], dtype=dataset.T)
+        return vals, np.isfinite(vals)
+    dev = dataset.device(device)
+    prog = program if program is not None else compile_trees(trees, options, dataset.T, dev.ctx.device)
+    loss = options.elementwise_loss
+    sums, wsum, ok = prog.eval_loss(dev, loss.kind, loss.params, row_idx)
+    T = dataset.T
+    with np.errstate(invalid="ignore", divide="ignore"):
+        out = (sums / wsum).astype(T)
+    out[~ok] = T(np.inf)
+    return out, ok
+
+
+def eval_loss(tree: Node, dataset: Dataset, options: Options) -> float:
+    return eval_loss_batch([tree], dataset, options)[0]
+
+
+def compute_complexity(tree: Node, options: Options) -> int:
+    if not options.complexity_use:
+        return count_nodes(tree)
+
+    def rec(t: Node) -> float:
+        if t.degree == 0:
+            return options.constant_complexity if t.constant else options.variable_complexity
+        if t.degree == 1:
+            return options.unaop_complexities[t.op - 1] + rec(t.l)
+        return options.binop_complexities[t.op - 1] + rec(t.l) + rec(t.r)
+
+    return int(round(rec(tree)))
+
+
+def loss_to_score(loss, baseline, tree: Node, options: Options):
+    T = type(loss) if isinstance(loss, np.floating) else np.float64
+    normalization = T(0.01) if baseline < T(0.01) else T(baseline)
+    return T(loss / normalization + T(compute_complexity(tree, options) * options.parsimony))
+
+
+def score_func_batched(dataset: Dataset, trees: Sequence[Node], options: Options,
+                       device: Optional[int] = None) -> Tuple[np.ndarray, np.ndarray]:
+    """score_func over many trees: (scores, losses)."""
+    losses = eval_loss_batch(trees, dataset, options, device=device)
+    scores = np.asarray([loss_to_score(l, dataset.baseline_loss, t, options) for l, t in zip(losses, trees)],
+                        dtype=dataset.T)
+    return scores, losses
+
+
+def score_func(dataset: Dataset, tree: Node, options: Options):
+    s, l = score_func_batched(dataset, [tree], options)
+    return s[0], l[0]
+
+
+def score_func_batch(dataset: Dataset, tree: TreeOrTrees, options: Options,
+                     rng: Optional[np.random.Generator] = None, row_idx: Optional[np.ndarray] = None):
+    """Minibatch score (src/LossFunctions.jl:95-115): batch_size rows sampled
+    with replacement; a failed evaluation scores (0, Inf) as in the reference."""
+    trees, single = _as_list(tree)
+    if row_idx is None:
+        rng = rng or np.random.default_rng()
+        row_idx = rng.integers(0, dataset.n, size=options.batch_size)
+    losses, ok = eval_loss_batch_ok(trees, dataset, options, row_idx=row_idx)
+    T = dataset.T
+    scores = np.asarray(
+        [loss_to_score(l, dataset.baseline_loss, t, options) if k else T(0)
+         for l, t, k in zip(losses, trees, ok)],
+        dtype=T,
+    )
+    if single:
+        return scores[0], losses[0]
+    return scores, losses
+
+
+def update_baseline_loss_(dataset: Dataset, options: Options) -> None:
+    """update_baseline_loss!: loss of the constant tree avg_y."""
+    dataset.baseline_loss = eval_loss(Node(val=dataset.avg_y), dataset, options)

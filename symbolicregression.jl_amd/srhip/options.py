@@ -1,0 +1,177 @@
+"""Options and losses: the subset of SymbolicRegression.jl's `Options`
+(src/Options.jl:315-686, src/OptionsStruct.jl:106-164) that the scoring path
+reads — operators, elementwise_loss, loss_function, parsimony, batching,
+batch_size, turbo — with the reference's defaults and operator mapping.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, Optional, Sequence, Tuple
+
+from . import constants as K
+from ._lib import Unsupported
+
+
+# ---- LossFunctions.jl distance losses (docs/src/losses.md) -------------------
+@dataclass(frozen=True)
+class SupervisedLoss:
+    kind: int
+    param: float = 0.0
+
+    @property
+    def params(self):
+        return [float(self.param)]
+
+
+def L2DistLoss():
+    return SupervisedLoss(K.LOSS["L2"])
+
+
+def L1DistLoss():
+    return SupervisedLoss(K.LOSS["L1"])
+
+
+def LPDistLoss(p: float):
+    return SupervisedLoss(K.LOSS["LP"], p)
+
+
+def HuberLoss(d: float = 1.0):
+    return SupervisedLoss(K.LOSS["HUBER"], d)
+
+
+def LogCoshLoss():
+    return SupervisedLoss(K.LOSS["LOGCOSH"])
+
+
+def L1EpsilonInsLoss(eps: float):
+    return SupervisedLoss(K.LOSS["L1EPSINS"], eps)
+
+
+def L2EpsilonInsLoss(eps: float):
+    return SupervisedLoss(K.LOSS["L2EPSINS"], eps)
+
+
+def QuantileLoss(tau: float):
+    return SupervisedLoss(K.LOSS["QUANTILE"], tau)
+
+
+def PeriodicLoss(c: float):
+    return SupervisedLoss(K.LOSS["PERIODIC"], c)
+
+
+def LogitDistLoss():
+    return SupervisedLoss(K.LOSS["LOGITDIST"])
+
+
+def _opname(op) -> str:
+    if isinstance(op, str):
+        return op
+    name = getattr(op, "__name__", None)
+    if name is None:
+        raise TypeError(f"operator {op!r} has no name")
+    return name
+
+
+class Options:
+    """`Options(; binary_operators=[+, -, /, *], unary_operators=[], ...)`.
+    Operators are given by their Julia names ("+", "cos", "safe_log", "^", ...)
+    or by Python callables with such a __name__. The user → safe operator
+    mapping of src/Options.jl:86-120 is applied (log → safe_log, ^ → safe_pow,
+    atanh → atanh_clip, ...)."""
+
+    def __init__(
+        self,
+        binary_operators: Sequence = ("+", "-", "/", "*"),
+        unary_operators: Sequence = (),
+        elementwise_loss=None,
+        loss_function: Optional[Callable] = None,
+        parsimony: float = 0.0032,
+        batching: bool = False,
+        batch_size: int = 50,
+        turbo: bool = False,
+        complexity_of_operators: Optional[dict] = None,
+        complexity_of_constants: Optional[float] = None,
+        complexity_of_variables: Optional[float] = None,
+        maxsize: int = 20,
+        npopulations: int = 15,
+        **_ignored,
+    ):
+        self.binary_operators: Tuple[str, ...] = tuple(_opname(o) for o in binary_operators)
+        self.unary_operators: Tuple[str, ...] = tuple(_opname(o) for o in unary_operators)
+        if set(self.binary_operators) & set(self.unary_operators):
+            raise AssertionError("operators appear in both the binary and unary lists")  # Configure.jl:43-50
+        self.elementwise_loss = elementwise_loss if elementwise_loss is not None else L2DistLoss()
+        self.loss_function = loss_function
+        self.parsimony = float(parsimony)
+        self.batching = bool(batching)
+        self.batch_size = int(batch_size)
+        self.turbo = bool(turbo)
+        self.maxsize = maxsize
+        self.npopulations = npopulations
+        self.nbin = len(self.binary_operators)
+        self.nuna = len(self.unary_operators)
+        # ComplexityMapping (src/OptionsStruct.jl:55-104): use when any is given
+        self.complexity_use = any(
+            v is not None for v in (complexity_of_operators, complexity_of_constants, complexity_of_variables)
+        )
+        cop = complexity_of_operators or {}
+        self.binop_complexities = [float(cop.get(o, 1)) for o in self.binary_operators]
+        self.unaop_complexities = [float(cop.get(o, 1)) for o in self.unary_operators]
+        self.constant_complexity = float(1 if complexity_of_constants is None else complexity_of_constants)
+        self.variable_complexity = float(1 if complexity_of_variables is None else complexity_of_variables)
+        self._ids = None
+
+    def engine_operator_ids(self):
+        """Engine ids of binary_operators / unary_operators (raises Unsupported
+        for operators outside the engine's table)."""
+        if self._ids is None:
+            b, u = [], []
+            for name in self.binary_operators:
+                ar, i = K.OP_NAMES.get(name, (0, -1))
+                if ar != 2:
+                    raise Unsupported(-2, f"binary operator {name!r} is not supported by the engine")
+                b.append(i)
+            for name in self.unary_operators:
+                ar, i = K.OP_NAMES.get(name, (0, -1))
+                if ar != 1:
+                    raise Unsupported(-2, f"unary operator {name!r} is not supported by the engine")
+                u.append(i)
+            self._ids = (b, u)
+        return self._ids
+
+    # tree building helpers
+    def make_binary(self, name: str, a, b):
+        from .node import Node
+
+        return Node(self.binary_operators.index(name) + 1, a, b)
+
+    def make_unary(self, name: str, a):
+        from .node import Node
+
+        return Node(self.unary_operators.index(name) + 1, a)
+
+    def __getattr__(self, name):
+        # options.cos(node) etc. for the configured unary operators
+        if name.startswith("_"):
+            raise AttributeError(name)
+        una = self.__dict__.get("unary_operators", ())
+        bina = self.__dict__.get("binary_operators", ())
+        if name in una:
+            return lambda a: self.make_unary(name, a)
+        if name in bina:
+            return lambda a, b: self.make_binary(name, a, b)
+        raise AttributeError(name)
+
+
+_DEFAULT: Optional[Options] = None
+
+
+def extend_operators(options: Options) -> None:
+    """Mirror of `@extend_operators options`: Python operators on Node build
+    trees with this options' operator indices."""
+    global _DEFAULT
+    _DEFAULT = options
+
+
+def _default_options() -> Optional[Options]:
+    return _DEFAULT
