@@ -416,7 +416,10 @@ void CAT(oracle_eval_loss_batch, SFX)(int32_t ntrees, const int32_t* node_off,
   free(Xg); free(yg); free(wg);
 }
 
-/* forward-mode constant gradients (one tangent per constant) */
+/* forward-mode constant gradients (one tangent per constant).
+ * did_succeed here: every node value (constant leaves included) finite at
+ * every row — the eval_tree_array rule without constant folding; identical
+ * to it whenever all constants are finite. */
 static int CAT(grad_rec, SFX)(const ECTX* c, int i, int nc, int* cidx,
                               T* val, T* tan /*[nc][n]*/) {
   const ONODE* nd = c->nd;
@@ -426,6 +429,7 @@ static int CAT(grad_rec, SFX)(const ECTX* c, int i, int nc, int* cidx,
     for (int k = 0; k < nc; ++k) memset(tan + (size_t)k * n, 0, sizeof(T) * (size_t)n);
     if (x->feat < 0) {
       int k = (*cidx)++;
+      if (!CAT(isfin, SFX)(x->val)) return 0; /* every node finite, constants included */
       for (int64_t j = 0; j < n; ++j) { val[j] = x->val; tan[(size_t)k * n + j] = 1; }
     } else {
       for (int64_t j = 0; j < n; ++j) val[j] = XAT(c, x->feat, j);

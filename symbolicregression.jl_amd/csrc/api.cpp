@@ -86,7 +86,7 @@ struct srhip_ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   double last_ms = 0.0;
   int last_launches = 0;
-  DevBuf partial, sums, oks, scratch_idx, gather;
+  DevBuf partial, sums, oks, dloss, scratch_idx, gather;
   std::vector<double> h_sum;
   std::vector<uint8_t> h_ok;
 };
@@ -124,9 +124,25 @@ struct srhip_program {
   int32_t* d_tree_off = nullptr;
   int32_t* d_list = nullptr;  // [nlist_a + nlist_b]: shallow trees then deep trees
   int nlist_a = 0, nlist_b = 0;
+  // gradient programs (compiled on first use)
+  bool grad_built = false;
+  std::vector<uint8_t> g_static_fail;
+  void* d_gcode = nullptr;
+  int32_t* d_gtree_off = nullptr;
+  int32_t* d_gitems = nullptr;  // work items (tree | group << 24): shallow then deep
+  int32_t* d_const_off = nullptr;
+  int ngitems_a = 0, ngitems_b = 0;
 };
 
 namespace {
+
+void free_grad_device(srhip_program* p) {
+  for (void* q : {p->d_gcode, (void*)p->d_gtree_off, (void*)p->d_gitems, (void*)p->d_const_off})
+    if (q) (void)hipFree(q);
+  p->d_gcode = nullptr;
+  p->d_gtree_off = p->d_gitems = p->d_const_off = nullptr;
+  p->grad_built = false;
+}
 
 void free_program_device(srhip_program* p) {
   if (p->d_code) (void)hipFree(p->d_code);
@@ -135,6 +151,58 @@ void free_program_device(srhip_program* p) {
   p->d_code = nullptr;
   p->d_tree_off = nullptr;
   p->d_list = nullptr;
+  free_grad_device(p);
+}
+
+// Gradient programs: compiled without folding, one work item per (tree,
+// tangent group of kGradG constants), cost-sorted.
+template <typename T>
+void build_grad_program(srhip_program* p) {
+  if (p->grad_built) return;
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->consts.data();
+  CompiledBatch<T> cb = compile_batch<T>(tr, /*grad=*/true);
+  if (p->ntrees >= (1 << 24)) throw Error(SRHIP_ERR_UNSUPPORTED, "too many trees for gradient work items");
+  p->g_static_fail = cb.static_fail;
+  std::vector<std::pair<int, int32_t>> a, b;  // (cost, item)
+  for (int t = 0; t < p->ntrees; ++t) {
+    if (cb.tree_off[t] < 0) continue;
+    const int nc = p->const_off[t + 1] - p->const_off[t];
+    const int ngroups = std::max(1, (nc + kGradG - 1) / kGradG);
+    for (int gi = 0; gi < ngroups; ++gi)
+      (cb.need[t] <= 4 ? a : b).push_back({cb.cost[t], (int32_t)(t | (gi << 24))});
+  }
+  auto by_cost = [](const std::pair<int, int32_t>& x, const std::pair<int, int32_t>& y) {
+    return x.first != y.first ? x.first > y.first : x.second < y.second;
+  };
+  std::stable_sort(a.begin(), a.end(), by_cost);
+  std::stable_sort(b.begin(), b.end(), by_cost);
+  std::vector<int32_t> items;
+  for (auto& q : a) items.push_back(q.second);
+  for (auto& q : b) items.push_back(q.second);
+  p->ngitems_a = (int)a.size();
+  p->ngitems_b = (int)b.size();
+  std::vector<int32_t> toff(cb.tree_off);
+  for (auto& v : toff) v = std::max(v, 0);
+  hipStream_t s = p->ctx->stream;
+  HIP_CHECK(hipMalloc(&p->d_gcode, std::max<size_t>(cb.code.size(), 1) * sizeof(Ins<T>)));
+  HIP_CHECK(hipMalloc((void**)&p->d_gtree_off, std::max<size_t>(toff.size(), 1) * sizeof(int32_t)));
+  HIP_CHECK(hipMalloc((void**)&p->d_gitems, std::max<size_t>(items.size(), 1) * sizeof(int32_t)));
+  HIP_CHECK(hipMalloc((void**)&p->d_const_off, p->const_off.size() * sizeof(int32_t)));
+  HIP_CHECK(hipMemcpyAsync(p->d_gcode, cb.code.data(), cb.code.size() * sizeof(Ins<T>), hipMemcpyHostToDevice, s));
+  if (!toff.empty())
+    HIP_CHECK(hipMemcpyAsync(p->d_gtree_off, toff.data(), toff.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  if (!items.empty())
+    HIP_CHECK(hipMemcpyAsync(p->d_gitems, items.data(), items.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipMemcpyAsync(p->d_const_off, p->const_off.data(), p->const_off.size() * sizeof(int32_t),
+                           hipMemcpyHostToDevice, s));
+  HIP_CHECK(hipStreamSynchronize(s));
+  p->grad_built = true;
 }
 
 template <typename T>
@@ -336,6 +404,115 @@ int eval_tree_array_impl(srhip_dataset* ds, const srhip_program* p, void* out, u
   return SRHIP_OK;
 }
 
+template <typename T>
+void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds, int loss, double lparam,
+              T* out_value, T* out_grad, int64_t out_stride) {
+  build_grad_program<T>(p);
+  hipStream_t s = c->stream;
+  c->last_ms = 0.0;
+  c->last_launches = 0;
+  const int nt = p->ntrees;
+  const int nconst = p->const_off.back();
+  c->sums.ensure(std::max<size_t>(nt, 1) * sizeof(double));
+  c->oks.ensure(std::max<size_t>(nt, 1));
+  c->dloss.ensure(std::max<size_t>(nconst, 1) * sizeof(double));
+  for (int pass = 0; pass < 2; ++pass) {
+    const int nitems = pass == 0 ? p->ngitems_a : p->ngitems_b;
+    if (nitems == 0 || ds->rows == 0) continue;
+    EvalPlan plan;
+    if (!plan_grad(p->dtype, pass == 1, mode, ds->w != nullptr, ds->nfeat, ds->rows, nitems, &plan))
+      throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(ds->nfeat) + " features does not fit in LDS");
+    GradArgs<T> a;
+    a.prog = static_cast<const Ins<T>*>(p->d_gcode);
+    a.tree_off = p->d_gtree_off;
+    a.items = p->d_gitems + (pass == 0 ? 0 : p->ngitems_a);
+    a.nitems = nitems;
+    a.const_off = p->d_const_off;
+    a.X = static_cast<const T*>(ds->X);
+    a.y = static_cast<const T*>(ds->y);
+    a.w = static_cast<const T*>(ds->w);
+    a.n = ds->rows;
+    a.n_pad = ds->n_pad;
+    a.nfeat = ds->nfeat;
+    a.ntiles = plan.ntiles;
+    a.ntg = plan.ntg;
+    a.tpb = plan.tpb;
+    a.nrg = plan.nrg;
+    a.loss = loss;
+    a.lparam = (T)lparam;
+    c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * (2 + kGradG) * sizeof(T));
+    a.partial = static_cast<T*>(c->partial.p);
+    a.out_value = out_value;
+    a.out_grad = out_grad;
+    a.out_stride = out_stride;
+    HIP_CHECK(hipEventRecord(c->ev[0], s));
+    HIP_CHECK(launch_grad<T>(plan, a, mode, s));
+    HIP_CHECK(hipEventRecord(c->ev[1], s));
+    HIP_CHECK(launch_grad_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p),
+                                      static_cast<double*>(c->dloss.p), s));
+    HIP_CHECK(hipEventSynchronize(c->ev[1]));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+    c->last_ms += ms;
+    c->last_launches += 1;
+  }
+}
+
+// per-tree results of a gradient pass: static verdicts applied
+void collect_grad_results(srhip_ctx* c, const srhip_program* p, int64_t rows, double* out_sum,
+                          double* out_dloss, uint8_t* out_ok) {
+  const int nt = p->ntrees;
+  const int nconst = p->const_off.back();
+  c->h_sum.assign(nt, 0.0);
+  c->h_ok.assign(nt, 1);
+  std::vector<double> hd(nconst, 0.0);
+  if (rows > 0 && nt > 0 && (p->ngitems_a + p->ngitems_b) > 0) {
+    HIP_CHECK(hipMemcpyAsync(c->h_sum.data(), c->sums.p, nt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+    HIP_CHECK(hipMemcpyAsync(c->h_ok.data(), c->oks.p, nt, hipMemcpyDeviceToHost, c->stream));
+    if (nconst > 0)
+      HIP_CHECK(hipMemcpyAsync(hd.data(), c->dloss.p, nconst * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  }
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  for (int t = 0; t < nt; ++t) {
+    const bool fail = p->g_static_fail[t] || (rows > 0 && !c->h_ok[t]);
+    if (out_ok) out_ok[t] = fail ? 0 : 1;
+    if (out_sum) out_sum[t] = fail ? NAN : (rows > 0 ? c->h_sum[t] : 0.0);
+    for (int k = p->const_off[t]; k < p->const_off[t + 1]; ++k)
+      if (out_dloss) out_dloss[k] = fail ? NAN : (rows > 0 ? hd[k] : 0.0);
+  }
+}
+
+template <typename T>
+int eval_loss_grad_impl(srhip_dataset* ds, srhip_program* p, int loss, const double* params,
+                        double* out_sum, double* out_dloss, double* out_wsum, uint8_t* out_ok) {
+  run_grad<T>(ds->ctx, p, GRAD_LOSS, ds, loss, params ? params[0] : 0.0, nullptr, nullptr, 0);
+  collect_grad_results(ds->ctx, p, ds->rows, out_sum, out_dloss, out_ok);
+  if (out_wsum) *out_wsum = ds->w ? ds->sum_w : (double)ds->rows;
+  return SRHIP_OK;
+}
+
+template <typename T>
+int eval_grad_tree_array_impl(srhip_dataset* ds, srhip_program* p, void* out_value, void* out_grad,
+                              uint8_t* out_ok) {
+  srhip_ctx* c = ds->ctx;
+  const int nt = p->ntrees;
+  const int nconst = p->const_off.back();
+  const int64_t rows = ds->rows, n_pad = ds->n_pad;
+  const size_t es = sizeof(T);
+  c->gather.ensure(std::max<size_t>((size_t)(nt + nconst) * n_pad * es, es));
+  T* d_val = static_cast<T*>(c->gather.p);
+  T* d_grad = d_val + (size_t)nt * n_pad;
+  run_grad<T>(c, p, GRAD_OUT, ds, SRHIP_LOSS_L2, 0.0, d_val, d_grad, n_pad);
+  if (rows > 0) {
+    if (out_value && nt > 0)
+      HIP_CHECK(hipMemcpy2DAsync(out_value, rows * es, d_val, n_pad * es, rows * es, nt, hipMemcpyDeviceToHost, c->stream));
+    if (out_grad && nconst > 0)
+      HIP_CHECK(hipMemcpy2DAsync(out_grad, rows * es, d_grad, n_pad * es, rows * es, nconst, hipMemcpyDeviceToHost, c->stream));
+  }
+  collect_grad_results(c, p, rows, nullptr, nullptr, out_ok);
+  return SRHIP_OK;
+}
+
 struct OpName {
   const char* name;
   int arity;
@@ -432,6 +609,7 @@ int32_t srhip_close(srhip_ctx* ctx) {
     ctx->partial.release();
     ctx->sums.release();
     ctx->oks.release();
+    ctx->dloss.release();
     ctx->scratch_idx.release();
     ctx->gather.release();
     for (auto& e : ctx->ev)
@@ -711,15 +889,31 @@ int32_t srhip_eval_tree_array(srhip_dataset* ds, const srhip_program* prog, void
 int32_t srhip_eval_loss_grad(srhip_dataset* ds, const srhip_program* prog, int32_t loss_kind,
                              const double* loss_params, double* out_loss_sum, double* out_dloss,
                              double* out_weight_sum, uint8_t* out_ok) {
-  (void)ds; (void)prog; (void)loss_kind; (void)loss_params; (void)out_loss_sum;
-  (void)out_dloss; (void)out_weight_sum; (void)out_ok;
-  return set_error(SRHIP_ERR_UNSUPPORTED, "constant gradients are not implemented yet");
+  return guarded([&] {
+    check_program_vs_dataset(ds, prog);
+    if (loss_kind < 0 || loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
+    if (loss_kind != SRHIP_LOSS_L2 && loss_kind != SRHIP_LOSS_L1 && loss_kind != SRHIP_LOSS_LOGCOSH &&
+        loss_kind != SRHIP_LOSS_LOGITDIST && !loss_params)
+      throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
+    std::lock_guard<std::mutex> lk(ds->ctx->mu);
+    HIP_CHECK(hipSetDevice(ds->ctx->device));
+    auto* p = const_cast<srhip_program*>(prog);  // gradient programs are built lazily
+    if (ds->dtype == SRHIP_F32)
+      return eval_loss_grad_impl<float>(ds, p, loss_kind, loss_params, out_loss_sum, out_dloss, out_weight_sum, out_ok);
+    return eval_loss_grad_impl<double>(ds, p, loss_kind, loss_params, out_loss_sum, out_dloss, out_weight_sum, out_ok);
+  });
 }
 
 int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog, void* out_value,
                                    void* out_grad, uint8_t* out_ok) {
-  (void)ds; (void)prog; (void)out_value; (void)out_grad; (void)out_ok;
-  return set_error(SRHIP_ERR_UNSUPPORTED, "constant gradients are not implemented yet");
+  return guarded([&] {
+    check_program_vs_dataset(ds, prog);
+    std::lock_guard<std::mutex> lk(ds->ctx->mu);
+    HIP_CHECK(hipSetDevice(ds->ctx->device));
+    auto* p = const_cast<srhip_program*>(prog);
+    if (ds->dtype == SRHIP_F32) return eval_grad_tree_array_impl<float>(ds, p, out_value, out_grad, out_ok);
+    return eval_grad_tree_array_impl<double>(ds, p, out_value, out_grad, out_ok);
+  });
 }
 
 int32_t srhip_last_kernel_time(const srhip_ctx* ctx, double* out_ms, int32_t* out_launches) {

@@ -32,6 +32,7 @@ struct HNode {
   int feat;      // feature index (deg 0, -1 for a constant)
   int l, r;      // children
   double val;    // constant value (deg 0 const), held in T precision
+  int cidx;      // constant index in get_constants order (deg 0 const)
   bool has_feature;
   int need;      // stack slots needed (Sethi–Ullman number for this machine)
 };
@@ -40,6 +41,7 @@ template <typename T>
 struct TreeCompiler {
   std::vector<HNode> nd;
   std::vector<Ins<T>>* out;
+  bool grad = false;  // slot field carries constant indices
   bool fold_fail = false;
   int max_feat = -1;
 
@@ -119,7 +121,7 @@ struct TreeCompiler {
     const HNode& x = nd[i];
     if (x.deg == 0) {
       if (x.feat >= 0) put(OP_LDX, 0, x.feat, T(0));
-      else put(OP_LDC, 0, 0, (T)x.val);
+      else put(OP_LDC, ci(x), 0, (T)x.val);
       return;
     }
     if (x.deg == 1) {
@@ -132,24 +134,24 @@ struct TreeCompiler {
     const int op = x.op;
     if (is_leaf(L) && is_leaf(R)) {
       if (L.feat >= 0 && R.feat >= 0) put_feat2(bin_opcode(V_XX, op), L.feat, R.feat);
-      else if (L.feat >= 0) put(bin_opcode(V_XC, op), 0, L.feat, (T)R.val);
-      else if (R.feat >= 0) put(bin_opcode(V_CX, op), 0, R.feat, (T)L.val);
-      else {  // cannot happen after folding, kept for safety
-        put(OP_LDC, 0, 0, (T)L.val);
-        put(bin_opcode(V_AC, op), 0, 0, (T)R.val);
+      else if (L.feat >= 0) put(bin_opcode(V_XC, op), ci(R), L.feat, (T)R.val);
+      else if (R.feat >= 0) put(bin_opcode(V_CX, op), ci(L), R.feat, (T)L.val);
+      else {  // two constants: only without folding (gradient programs)
+        put(OP_LDC, ci(L), 0, (T)L.val);
+        put(bin_opcode(V_AC, op), ci(R), 0, (T)R.val);
       }
       return;
     }
     if (is_leaf(R)) {
       emit(x.l, base);
       if (R.feat >= 0) put(bin_opcode(V_AX, op), 0, R.feat, T(0));
-      else put(bin_opcode(V_AC, op), 0, 0, (T)R.val);
+      else put(bin_opcode(V_AC, op), ci(R), 0, (T)R.val);
       return;
     }
     if (is_leaf(L)) {
       emit(x.r, base);
       if (L.feat >= 0) put(bin_opcode(V_XA, op), 0, L.feat, T(0));
-      else put(bin_opcode(V_CA, op), 0, 0, (T)L.val);
+      else put(bin_opcode(V_CA, op), ci(L), 0, (T)L.val);
       return;
     }
     if (base >= kMaxSlots) throw Error(SRHIP_ERR_UNSUPPORTED, "tree needs more than 16 stack slots");
@@ -168,6 +170,16 @@ struct TreeCompiler {
     }
   }
 
+  // slot-field value of a constant operand: its index (gradient programs)
+  int ci(const HNode& x) const { return grad ? x.cidx : 0; }
+
+  bool any_const_nonfinite(int i) const {
+    const HNode& x = nd[i];
+    if (x.deg == 0) return x.feat < 0 && !std::isfinite(x.val);
+    if (any_const_nonfinite(x.l)) return true;
+    return x.deg == 2 && any_const_nonfinite(x.r);
+  }
+
   int cost(int i) const {
     const HNode& x = nd[i];
     if (x.deg == 0) return 1;
@@ -179,7 +191,7 @@ struct TreeCompiler {
 }  // namespace
 
 template <typename T>
-CompiledBatch<T> compile_batch(const srhip_trees& trees) {
+CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
   if (trees.ntrees < 0) throw Error(SRHIP_ERR_INVALID, "negative tree count");
   if (trees.ntrees > 0 && (!trees.node_off || !trees.kind || !trees.arg || !trees.const_off))
     throw Error(SRHIP_ERR_INVALID, "null tree arrays");
@@ -195,6 +207,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees) {
   const T* consts = static_cast<const T*>(trees.consts);
   TreeCompiler<T> tc;
   tc.out = &cb.code;
+  tc.grad = grad;
   std::vector<int> stk;
   for (int t = 0; t < nt; ++t) {
     const int b = trees.node_off[t], e = trees.node_off[t + 1];
@@ -213,6 +226,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees) {
       switch (kind) {
         case SRHIP_NODE_CONST:
           if (ci >= ce) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": more constant leaves than constants");
+          x.cidx = ci - cb0;
           x.deg = 0; x.val = (double)consts[ci++]; x.has_feature = false;
           break;
         case SRHIP_NODE_FEATURE:
@@ -245,6 +259,17 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees) {
     cb.total_nodes += e - b;
     cb.cost[t] = tc.cost(root);
 
+    if (grad) {
+      // gradient programs: no folding; a non-finite constant fails statically
+      if (ce - cb0 > 255) throw Error(SRHIP_ERR_UNSUPPORTED, "gradients support at most 255 constants per tree");
+      if (tc.any_const_nonfinite(root)) { cb.static_fail[t] = 1; continue; }
+      cb.need[t] = tc.compute_need(root);
+      if (cb.need[t] > kMaxSlots) throw Error(SRHIP_ERR_UNSUPPORTED, "tree needs more than 16 stack slots");
+      cb.tree_off[t] = (int32_t)cb.code.size();
+      tc.emit(root, 0);
+      tc.put(OP_END, 0, 0, T(0));
+      continue;
+    }
     const bool root_is_leaf = tc.nd[root].deg == 0;
     tc.fold(root);
     if (tc.fold_fail) { cb.static_fail[t] = 1; continue; }
@@ -268,7 +293,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees) {
   return cb;
 }
 
-template CompiledBatch<float> compile_batch<float>(const srhip_trees&);
-template CompiledBatch<double> compile_batch<double>(const srhip_trees&);
+template CompiledBatch<float> compile_batch<float>(const srhip_trees&, bool);
+template CompiledBatch<double> compile_batch<double>(const srhip_trees&, bool);
 
 }  // namespace srhip

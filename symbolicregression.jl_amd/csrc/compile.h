@@ -30,7 +30,10 @@ struct CompiledBatch {
 
 // Compile every tree of the batch. Throws srhip::Error on malformed input
 // (SRHIP_ERR_INVALID) or on operators outside the table (SRHIP_ERR_UNSUPPORTED).
+// grad = true compiles for the constant-gradient kernels: no constant folding,
+// every constant operand carries its get_constants index in the slot field,
+// and a non-finite constant anywhere fails the tree statically.
 template <typename T>
-CompiledBatch<T> compile_batch(const srhip_trees& trees);
+CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad = false);
 
 }  // namespace srhip

@@ -160,5 +160,77 @@ __device__ __forceinline__ T elem_loss(int kind, T p, T yhat, T y) {
   return qnan<T>();
 }
 
+
+// ---- forward-mode partial derivatives (constant gradients) -----------------------
+// f = op(x, y) exactly as bop/uop compute it, plus ∂f/∂x, ∂f/∂y. The rules are
+// the textbook ones that Zygote/ForwardDiff derive for these functions;
+// piecewise-constant operators (greater, logical_*, round, floor, ceil, sign)
+// have zero derivative, gamma's (digamma) is not provided (0).
+template <int OP, typename T>
+__device__ __forceinline__ void bop_d(T x, T y, T& f, T& fx, T& fy) {
+  f = bop<OP>(x, y);
+  if constexpr (OP == SRHIP_BOP_ADD) { fx = T(1); fy = T(1); }
+  else if constexpr (OP == SRHIP_BOP_SUB) { fx = T(1); fy = T(-1); }
+  else if constexpr (OP == SRHIP_BOP_MUL) { fx = y; fy = x; }
+  else if constexpr (OP == SRHIP_BOP_DIV) { fx = T(1) / y; fy = -x / (y * y); }
+  else if constexpr (OP == SRHIP_BOP_POW) {
+    fx = y * bop<SRHIP_BOP_POW>(x, y - T(1));
+    fy = x > T(0) ? f * m_log(x) : T(0);
+  } else if constexpr (OP == SRHIP_BOP_MOD) { fx = T(1); fy = -m_floor(x / y); }
+  else if constexpr (OP == SRHIP_BOP_MAX) { fx = x >= y ? T(1) : T(0); fy = x >= y ? T(0) : T(1); }
+  else if constexpr (OP == SRHIP_BOP_MIN) { fx = x <= y ? T(1) : T(0); fy = x <= y ? T(0) : T(1); }
+  else { fx = T(0); fy = T(0); }
+}
+
+template <int OP, typename T>
+__device__ __forceinline__ void uop_d(T x, T& f, T& fx) {
+  f = uop<OP>(x);
+  if constexpr (OP == SRHIP_UOP_NEG) fx = T(-1);
+  else if constexpr (OP == SRHIP_UOP_SQUARE) fx = T(2) * x;
+  else if constexpr (OP == SRHIP_UOP_CUBE) fx = T(3) * x * x;
+  else if constexpr (OP == SRHIP_UOP_EXP) fx = f;
+  else if constexpr (OP == SRHIP_UOP_ABS) fx = x > T(0) ? T(1) : (x < T(0) ? T(-1) : T(0));
+  else if constexpr (OP == SRHIP_UOP_LOG) fx = T(1) / x;
+  else if constexpr (OP == SRHIP_UOP_LOG2) fx = T(1) / (x * T(0.69314718055994530942));
+  else if constexpr (OP == SRHIP_UOP_LOG10) fx = T(1) / (x * T(2.30258509299404568402));
+  else if constexpr (OP == SRHIP_UOP_LOG1P) fx = T(1) / (T(1) + x);
+  else if constexpr (OP == SRHIP_UOP_SQRT) fx = T(0.5) / f;
+  else if constexpr (OP == SRHIP_UOP_SIN) fx = m_cos(x);
+  else if constexpr (OP == SRHIP_UOP_COS) fx = -m_sin(x);
+  else if constexpr (OP == SRHIP_UOP_TAN) { T c = m_cos(x); fx = T(1) / (c * c); }
+  else if constexpr (OP == SRHIP_UOP_SINH) fx = m_cosh(x);
+  else if constexpr (OP == SRHIP_UOP_COSH) fx = m_sinh(x);
+  else if constexpr (OP == SRHIP_UOP_TANH) fx = T(1) - f * f;
+  else if constexpr (OP == SRHIP_UOP_ATAN) fx = T(1) / (T(1) + x * x);
+  else if constexpr (OP == SRHIP_UOP_ASINH) fx = T(1) / m_sqrt(x * x + T(1));
+  else if constexpr (OP == SRHIP_UOP_ACOSH) fx = T(1) / m_sqrt(x * x - T(1));
+  else if constexpr (OP == SRHIP_UOP_ERF) fx = T(1.1283791670955126) * m_exp(-x * x);
+  else if constexpr (OP == SRHIP_UOP_ERFC) fx = T(-1.1283791670955126) * m_exp(-x * x);
+  else if constexpr (OP == SRHIP_UOP_RELU) fx = x > T(0) ? T(1) : T(0);
+  else if constexpr (OP == SRHIP_UOP_INV) fx = T(-1) / (x * x);
+  else fx = T(0);
+}
+
+// dℓ/dŷ of the elementwise losses (r = ŷ - y)
+template <typename T>
+__device__ __forceinline__ T elem_dloss(int kind, T p, T yhat, T y) {
+  const T r = yhat - y;
+  const T ar = m_fabs(r);
+  const T sg = r > T(0) ? T(1) : (r < T(0) ? T(-1) : T(0));
+  switch (kind) {
+    case SRHIP_LOSS_L2: return T(2) * r;
+    case SRHIP_LOSS_L1: return sg;
+    case SRHIP_LOSS_LP: return p * m_pow(ar, p - T(1)) * sg;
+    case SRHIP_LOSS_HUBER: return ar <= p ? r : p * sg;
+    case SRHIP_LOSS_LOGCOSH: return m_tanh(r);
+    case SRHIP_LOSS_L1EPSINS: return ar > p ? sg : T(0);
+    case SRHIP_LOSS_L2EPSINS: return ar > p ? T(2) * (ar - p) * sg : T(0);
+    case SRHIP_LOSS_QUANTILE: return r >= T(0) ? p : p - T(1);
+    case SRHIP_LOSS_PERIODIC: { T k = T(6.28318530717958647692) / p; return k * m_sin(k * r); }
+    case SRHIP_LOSS_LOGITDIST: return m_tanh(T(0.5) * r);
+  }
+  return qnan<T>();
+}
+
 }  // namespace dev
 }  // namespace srhip

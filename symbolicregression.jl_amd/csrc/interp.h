@@ -1,0 +1,229 @@
+// interp.h — the wave-uniform tree interpreter (device side), shared by the
+// evaluation kernels (kernels.hip) and the constant-gradient kernels
+// (grad_kernels.hip).
+//
+// A program is fetched with scalar loads and dispatched with a uniform
+// branch tree; each instruction processes R rows per lane held in VGPRs.
+// Leaf features are read from the LDS row tile, constants are immediates.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "device_ops.h"
+#include "srhip_internal.h"
+
+namespace srhip {
+namespace interp {
+
+using dev::bop;
+using dev::uop;
+
+template <typename T>
+struct V16;
+template <>
+struct V16<float> {
+  using type = float4;
+  static constexpr int N = 4;
+};
+template <>
+struct V16<double> {
+  using type = double2;
+  static constexpr int N = 2;
+};
+
+__device__ __forceinline__ float uni(float v) {
+  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
+}
+__device__ __forceinline__ double uni(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
+  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ int imm_int(float v) { return __float_as_int(v); }
+__device__ __forceinline__ int imm_int(double v) { return (int)(__double_as_longlong(v) & 0xffffffffll); }
+
+// Non-finite marker: fma(v, 0, chk) is NaN iff v is ±Inf or NaN.
+__device__ __forceinline__ float mark(float v, float chk) { return __builtin_fmaf(v, 0.0f, chk); }
+__device__ __forceinline__ double mark(double v, double chk) { return __builtin_fma(v, 0.0, chk); }
+
+// The R rows of this lane inside one LDS tile row: element e = c*N + i is
+// tile row (c*64 + lane)*N + i, so every ds_read_b128 of a wave reads one
+// contiguous 1 KiB (conflict-free).
+// Vector width used for a lane's R rows: 16 bytes, or R elements if fewer.
+template <typename T, int R>
+struct RowVec {
+  static constexpr int W = (R < V16<T>::N) ? R : V16<T>::N;
+};
+
+template <typename T, int R>
+__device__ __forceinline__ int row_of(int e, int lane) {
+  constexpr int W = RowVec<T, R>::W;
+  return ((e / W) * 64 + lane) * W + (e % W);
+}
+
+template <typename T, int R>
+__device__ __forceinline__ void lds_rows(const T* __restrict__ p, int lane, T (&v)[R]) {
+  constexpr int W = RowVec<T, R>::W;
+  static_assert(R % W == 0, "R must be a multiple of the row vector width");
+#pragma unroll
+  for (int c = 0; c < R / W; ++c) {
+    const T* q = p + (c * 64 + lane) * W;
+    if constexpr (W * sizeof(T) == 16) {
+      using V = typename V16<T>::type;
+      const V a = *reinterpret_cast<const V*>(q);
+      if constexpr (W == 4) {
+        v[c * 4 + 0] = a.x; v[c * 4 + 1] = a.y; v[c * 4 + 2] = a.z; v[c * 4 + 3] = a.w;
+      } else {
+        v[c * 2 + 0] = a.x; v[c * 2 + 1] = a.y;
+      }
+    } else if constexpr (W == 2) {
+      const float2 a = *reinterpret_cast<const float2*>(q);
+      v[c * 2 + 0] = a.x; v[c * 2 + 1] = a.y;
+    } else {
+      v[c] = q[0];
+    }
+  }
+}
+
+template <typename T, int R>
+__device__ __forceinline__ void store_rows(T* __restrict__ p, int lane, const T (&v)[R]) {
+  constexpr int W = RowVec<T, R>::W;
+#pragma unroll
+  for (int c = 0; c < R / W; ++c) {
+    T* q = p + (c * 64 + lane) * W;
+    if constexpr (W * sizeof(T) == 16) {
+      using V = typename V16<T>::type;
+      V a;
+      if constexpr (W == 4) {
+        a.x = v[c * 4 + 0]; a.y = v[c * 4 + 1]; a.z = v[c * 4 + 2]; a.w = v[c * 4 + 3];
+      } else {
+        a.x = v[c * 2 + 0]; a.y = v[c * 2 + 1];
+      }
+      *reinterpret_cast<V*>(q) = a;
+    } else if constexpr (W == 2) {
+      *reinterpret_cast<float2*>(q) = make_float2(v[c * 2 + 0], v[c * 2 + 1]);
+    } else {
+      q[0] = v[c];
+    }
+  }
+}
+
+template <int U, typename T, int R>
+__device__ __forceinline__ void un_apply(T (&acc)[R], T& chk) {
+#pragma unroll
+  for (int r = 0; r < R; ++r) {
+    if constexpr (uop_lossy(U)) chk = mark(acc[r], chk);
+    acc[r] = uop<U>(acc[r]);
+  }
+}
+
+template <int V, int B, typename T, int R>
+__device__ __forceinline__ void bin_apply(T (&acc)[R], const T (&tmp)[R],
+                                          const T* __restrict__ sXt, int rs,
+                                          int lane, int f, T imm, T& chk) {
+  constexpr bool LL = bop_lossy_lhs(B);
+  constexpr bool LR = bop_lossy_rhs(B);
+  if constexpr (V == V_AX || V == V_XA || V == V_XX || V == V_XC || V == V_CX) {
+    T x[R];
+    lds_rows<T, R>(sXt + f * rs, lane, x);
+    if constexpr (V == V_XX) {
+      T x2[R];
+      lds_rows<T, R>(sXt + imm_int(imm) * rs, lane, x2);
+#pragma unroll
+      for (int r = 0; r < R; ++r) acc[r] = bop<B>(x[r], x2[r]);
+    } else {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        if constexpr (V == V_AX) {
+          if constexpr (LL) chk = mark(acc[r], chk);
+          acc[r] = bop<B>(acc[r], x[r]);
+        } else if constexpr (V == V_XA) {
+          if constexpr (LR) chk = mark(acc[r], chk);
+          acc[r] = bop<B>(x[r], acc[r]);
+        } else if constexpr (V == V_XC) {
+          acc[r] = bop<B>(x[r], imm);
+        } else {
+          acc[r] = bop<B>(imm, x[r]);
+        }
+      }
+    }
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (V == V_AC) {
+        if constexpr (LL) chk = mark(acc[r], chk);
+        acc[r] = bop<B>(acc[r], imm);
+      } else if constexpr (V == V_CA) {
+        if constexpr (LR) chk = mark(acc[r], chk);
+        acc[r] = bop<B>(imm, acc[r]);
+      } else if constexpr (V == V_AT) {
+        if constexpr (LL) chk = mark(acc[r], chk);
+        if constexpr (LR) chk = mark(tmp[r], chk);
+        acc[r] = bop<B>(acc[r], tmp[r]);
+      } else {  // V_TA
+        if constexpr (LL) chk = mark(tmp[r], chk);
+        if constexpr (LR) chk = mark(acc[r], chk);
+        acc[r] = bop<B>(tmp[r], acc[r]);
+      }
+    }
+  }
+}
+
+#define SR_UNROLL _Pragma("unroll")
+#define SR_PUSH(K)                                                   \
+  case OP_PUSH0 + K:                                                 \
+    if constexpr (K < D) { SR_UNROLL for (int r = 0; r < R; ++r) slot[K][r] = acc[r]; } \
+    break;
+#define SR_POP(K)                                                    \
+  case OP_POP0 + K:                                                  \
+    if constexpr (K < D) { SR_UNROLL for (int r = 0; r < R; ++r) tmp[r] = slot[K][r]; } \
+    break;
+#define SR_UN(U) \
+  case OP_UN0 + U: un_apply<U, T, R>(acc, chk); break;
+#define SR_BV(V, B) \
+  case bin_opcode(V, B): bin_apply<V, B, T, R>(acc, tmp, sXt, rs, lane, f, imm, chk); break;
+#define SR_BIN(B) SR_BV(V_AX, B) SR_BV(V_XA, B) SR_BV(V_AC, B) SR_BV(V_CA, B) \
+  SR_BV(V_AT, B) SR_BV(V_TA, B) SR_BV(V_XX, B) SR_BV(V_XC, B) SR_BV(V_CX, B)
+
+// Run one tree's program over one row tile; the result is left in acc.
+template <typename T, int R, int D>
+__device__ __forceinline__ void run_program(const Ins<T>* __restrict__ p,
+                                            const T* __restrict__ sXt, int rs,
+                                            int lane, T (&acc)[R], T& chk) {
+  T tmp[R];
+  T slot[D][R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) { acc[r] = T(0); tmp[r] = T(0); }
+  int pc = 0;
+  Ins<T> cur = p[0];
+  for (;;) {
+    const Ins<T> nxt = p[pc + 1];  // prefetch; every program ends with OP_END + slack
+    const uint32_t code = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.code);
+    const T imm = uni(cur.imm);
+    const int f = (int)(code >> 16);
+    switch (code & 0xffu) {
+      case OP_END: return;
+      case OP_LDX: lds_rows<T, R>(sXt + f * rs, lane, acc); break;
+      case OP_LDC:
+        SR_UNROLL for (int r = 0; r < R; ++r) acc[r] = imm;
+        break;
+      SR_PUSH(0) SR_PUSH(1) SR_PUSH(2) SR_PUSH(3) SR_PUSH(4) SR_PUSH(5) SR_PUSH(6) SR_PUSH(7)
+      SR_PUSH(8) SR_PUSH(9) SR_PUSH(10) SR_PUSH(11) SR_PUSH(12) SR_PUSH(13) SR_PUSH(14) SR_PUSH(15)
+      SR_POP(0) SR_POP(1) SR_POP(2) SR_POP(3) SR_POP(4) SR_POP(5) SR_POP(6) SR_POP(7)
+      SR_POP(8) SR_POP(9) SR_POP(10) SR_POP(11) SR_POP(12) SR_POP(13) SR_POP(14) SR_POP(15)
+      SR_UN(0) SR_UN(1) SR_UN(2) SR_UN(3) SR_UN(4) SR_UN(5) SR_UN(6) SR_UN(7) SR_UN(8) SR_UN(9)
+      SR_UN(10) SR_UN(11) SR_UN(12) SR_UN(13) SR_UN(14) SR_UN(15) SR_UN(16) SR_UN(17) SR_UN(18)
+      SR_UN(19) SR_UN(20) SR_UN(21) SR_UN(22) SR_UN(23) SR_UN(24) SR_UN(25) SR_UN(26) SR_UN(27)
+      SR_UN(28)
+      SR_BIN(0) SR_BIN(1) SR_BIN(2) SR_BIN(3) SR_BIN(4) SR_BIN(5) SR_BIN(6) SR_BIN(7) SR_BIN(8)
+      SR_BIN(9) SR_BIN(10)
+      default: break;
+    }
+    cur = nxt;
+    ++pc;
+  }
+}
+static_assert(SRHIP_NUM_UOPS == 29 && SRHIP_NUM_BOPS == 11, "update the case lists");
+
+}  // namespace interp
+}  // namespace srhip

@@ -57,6 +57,42 @@ struct EvalPlan {
 // row tile of this feature count does not fit in LDS.
 bool plan_eval(int dtype, bool deep, int mode, bool weighted, int nfeat,
                int64_t n, int nlist, EvalPlan* plan);
+// Same, for explicit R / D / LDS arrays / partial bytes per tree slot.
+bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n,
+                   int nlist, EvalPlan* plan);
+
+// ---- constant gradients (grad_kernels.hip) -----------------------------------
+constexpr int kGradG = 4;  // tangents per pass (constants per "tangent group")
+enum GradMode : int { GRAD_LOSS = 0, GRAD_OUT = 1 };
+
+template <typename T>
+struct GradArgs {
+  const Ins<T>* prog;       // programs compiled for gradients (no folding)
+  const int32_t* tree_off;
+  const int32_t* items;     // work items: tree | (tangent group << 24)
+  int nitems;
+  const int32_t* const_off; // [ntrees+1]
+  const T* X;
+  const T* y;
+  const T* w;
+  int64_t n, n_pad;
+  int nfeat;
+  int ntiles, ntg, tpb, nrg;
+  int loss;
+  T lparam;
+  T* partial;               // [nrg][ntg*tpb][2 + kGradG]
+  T* out_value;             // GRAD_OUT: [ntrees][out_stride]
+  T* out_grad;              // GRAD_OUT: [total consts][out_stride]
+  int64_t out_stride;
+};
+
+bool plan_grad(int dtype, bool deep, int mode, bool weighted, int nfeat, int64_t n,
+               int nitems, EvalPlan* plan);
+template <typename T>
+hipError_t launch_grad(const EvalPlan& plan, const GradArgs<T>& a, int mode, hipStream_t stream);
+template <typename T>
+hipError_t launch_grad_finalize(const GradArgs<T>& a, double* out_sum, uint8_t* out_ok,
+                                double* out_dloss, hipStream_t stream);
 
 template <typename T>
 hipError_t launch_eval(const EvalPlan& plan, const EvalArgs<T>& a, int mode,

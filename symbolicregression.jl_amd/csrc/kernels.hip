@@ -3,9 +3,8 @@
 // eval_kernel: one workgroup = (row group, tree group).
 //   1. The workgroup stages its row group (ntiles × 64·R rows) of every
 //      feature, y and w into LDS once (16-byte vector loads, coalesced).
-//   2. Each wave repeatedly takes the next tree of the group from an LDS
-//      counter (trees are cost-sorted, so this is LPT scheduling) and runs
-//      its program over every tile: the program is wave-uniform (scalar
+//   2. The waves take the group's trees round-robin (trees are sorted by
+//      cost, longest first) and run each program over every tile: the program is wave-uniform (scalar
 //      loads, uniform branches), each instruction processes R rows per lane
 //      held in VGPRs; leaf features come straight from LDS with ds_read_b128.
 //   3. Per tree the wave reduces Σ w·ℓ and the non-finite marker over its
@@ -14,208 +13,25 @@
 // There is no MFMA: this is a VALU-bound interpreter, not a contraction.
 #include <hip/hip_runtime.h>
 
-#include "device_ops.h"
+#include "interp.h"
 #include "kernels.h"
 
 namespace srhip {
 namespace {
 
-using dev::bop;
-using dev::uop;
-
-template <typename T>
-struct V16;
-template <>
-struct V16<float> {
-  using type = float4;
-  static constexpr int N = 4;
-};
-template <>
-struct V16<double> {
-  using type = double2;
-  static constexpr int N = 2;
-};
-
-__device__ __forceinline__ float uni(float v) {
-  return __int_as_float(__builtin_amdgcn_readfirstlane(__float_as_int(v)));
-}
-__device__ __forceinline__ double uni(double v) {
-  const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_readfirstlane((int)(b & 0xffffffffll));
-  const int hi = __builtin_amdgcn_readfirstlane((int)(b >> 32));
-  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
-}
-__device__ __forceinline__ int imm_int(float v) { return __float_as_int(v); }
-__device__ __forceinline__ int imm_int(double v) { return (int)(__double_as_longlong(v) & 0xffffffffll); }
-
-// Non-finite marker: fma(v, 0, chk) is NaN iff v is ±Inf or NaN.
-__device__ __forceinline__ float mark(float v, float chk) { return __builtin_fmaf(v, 0.0f, chk); }
-__device__ __forceinline__ double mark(double v, double chk) { return __builtin_fma(v, 0.0, chk); }
-
-// The R rows of this lane inside one LDS tile row: element e = c*N + i is
-// tile row (c*64 + lane)*N + i, so every ds_read_b128 of a wave reads one
-// contiguous 1 KiB (conflict-free).
-template <typename T, int R>
-__device__ __forceinline__ void lds_rows(const T* __restrict__ p, int lane, T (&v)[R]) {
-  using V = typename V16<T>::type;
-  constexpr int N = V16<T>::N;
-  static_assert(R % N == 0, "R must be a multiple of the 16-byte vector width");
-#pragma unroll
-  for (int c = 0; c < R / N; ++c) {
-    const V q = *reinterpret_cast<const V*>(p + (c * 64 + lane) * N);
-    if constexpr (N == 4) {
-      v[c * 4 + 0] = q.x; v[c * 4 + 1] = q.y; v[c * 4 + 2] = q.z; v[c * 4 + 3] = q.w;
-    } else {
-      v[c * 2 + 0] = q.x; v[c * 2 + 1] = q.y;
-    }
-  }
-}
-
-template <typename T, int R>
-__device__ __forceinline__ void store_rows(T* __restrict__ p, int lane, const T (&v)[R]) {
-  using V = typename V16<T>::type;
-  constexpr int N = V16<T>::N;
-#pragma unroll
-  for (int c = 0; c < R / N; ++c) {
-    V q;
-    if constexpr (N == 4) {
-      q.x = v[c * 4 + 0]; q.y = v[c * 4 + 1]; q.z = v[c * 4 + 2]; q.w = v[c * 4 + 3];
-    } else {
-      q.x = v[c * 2 + 0]; q.y = v[c * 2 + 1];
-    }
-    *reinterpret_cast<V*>(p + (c * 64 + lane) * N) = q;
-  }
-}
-
-template <int U, typename T, int R>
-__device__ __forceinline__ void un_apply(T (&acc)[R], T& chk) {
-#pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if constexpr (uop_lossy(U)) chk = mark(acc[r], chk);
-    acc[r] = uop<U>(acc[r]);
-  }
-}
-
-template <int V, int B, typename T, int R>
-__device__ __forceinline__ void bin_apply(T (&acc)[R], const T (&tmp)[R],
-                                          const T* __restrict__ sXt, int rs,
-                                          int lane, int f, T imm, T& chk) {
-  constexpr bool LL = bop_lossy_lhs(B);
-  constexpr bool LR = bop_lossy_rhs(B);
-  if constexpr (V == V_AX || V == V_XA || V == V_XX || V == V_XC || V == V_CX) {
-    T x[R];
-    lds_rows<T, R>(sXt + f * rs, lane, x);
-    if constexpr (V == V_XX) {
-      T x2[R];
-      lds_rows<T, R>(sXt + imm_int(imm) * rs, lane, x2);
-#pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = bop<B>(x[r], x2[r]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if constexpr (V == V_AX) {
-          if constexpr (LL) chk = mark(acc[r], chk);
-          acc[r] = bop<B>(acc[r], x[r]);
-        } else if constexpr (V == V_XA) {
-          if constexpr (LR) chk = mark(acc[r], chk);
-          acc[r] = bop<B>(x[r], acc[r]);
-        } else if constexpr (V == V_XC) {
-          acc[r] = bop<B>(x[r], imm);
-        } else {
-          acc[r] = bop<B>(imm, x[r]);
-        }
-      }
-    }
-  } else {
-#pragma unroll
-    for (int r = 0; r < R; ++r) {
-      if constexpr (V == V_AC) {
-        if constexpr (LL) chk = mark(acc[r], chk);
-        acc[r] = bop<B>(acc[r], imm);
-      } else if constexpr (V == V_CA) {
-        if constexpr (LR) chk = mark(acc[r], chk);
-        acc[r] = bop<B>(imm, acc[r]);
-      } else if constexpr (V == V_AT) {
-        if constexpr (LL) chk = mark(acc[r], chk);
-        if constexpr (LR) chk = mark(tmp[r], chk);
-        acc[r] = bop<B>(acc[r], tmp[r]);
-      } else {  // V_TA
-        if constexpr (LL) chk = mark(tmp[r], chk);
-        if constexpr (LR) chk = mark(acc[r], chk);
-        acc[r] = bop<B>(tmp[r], acc[r]);
-      }
-    }
-  }
-}
-
-#define SR_UNROLL _Pragma("unroll")
-#define SR_PUSH(K)                                                   \
-  case OP_PUSH0 + K:                                                 \
-    if constexpr (K < D) { SR_UNROLL for (int r = 0; r < R; ++r) slot[K][r] = acc[r]; } \
-    break;
-#define SR_POP(K)                                                    \
-  case OP_POP0 + K:                                                  \
-    if constexpr (K < D) { SR_UNROLL for (int r = 0; r < R; ++r) tmp[r] = slot[K][r]; } \
-    break;
-#define SR_UN(U) \
-  case OP_UN0 + U: un_apply<U, T, R>(acc, chk); break;
-#define SR_BV(V, B) \
-  case bin_opcode(V, B): bin_apply<V, B, T, R>(acc, tmp, sXt, rs, lane, f, imm, chk); break;
-#define SR_BIN(B) SR_BV(V_AX, B) SR_BV(V_XA, B) SR_BV(V_AC, B) SR_BV(V_CA, B) \
-  SR_BV(V_AT, B) SR_BV(V_TA, B) SR_BV(V_XX, B) SR_BV(V_XC, B) SR_BV(V_CX, B)
-
-// Run one tree's program over one row tile; the result is left in acc.
-template <typename T, int R, int D>
-__device__ __forceinline__ void run_program(const Ins<T>* __restrict__ p,
-                                            const T* __restrict__ sXt, int rs,
-                                            int lane, T (&acc)[R], T& chk) {
-  T tmp[R];
-  T slot[D][R];
-#pragma unroll
-  for (int r = 0; r < R; ++r) { acc[r] = T(0); tmp[r] = T(0); }
-  int pc = 0;
-  Ins<T> cur = p[0];
-  for (;;) {
-    const Ins<T> nxt = p[pc + 1];  // prefetch; every program ends with OP_END + slack
-    const uint32_t code = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.code);
-    const T imm = uni(cur.imm);
-    const int f = (int)(code >> 16);
-    switch (code & 0xffu) {
-      case OP_END: return;
-      case OP_LDX: lds_rows<T, R>(sXt + f * rs, lane, acc); break;
-      case OP_LDC:
-        SR_UNROLL for (int r = 0; r < R; ++r) acc[r] = imm;
-        break;
-      SR_PUSH(0) SR_PUSH(1) SR_PUSH(2) SR_PUSH(3) SR_PUSH(4) SR_PUSH(5) SR_PUSH(6) SR_PUSH(7)
-      SR_PUSH(8) SR_PUSH(9) SR_PUSH(10) SR_PUSH(11) SR_PUSH(12) SR_PUSH(13) SR_PUSH(14) SR_PUSH(15)
-      SR_POP(0) SR_POP(1) SR_POP(2) SR_POP(3) SR_POP(4) SR_POP(5) SR_POP(6) SR_POP(7)
-      SR_POP(8) SR_POP(9) SR_POP(10) SR_POP(11) SR_POP(12) SR_POP(13) SR_POP(14) SR_POP(15)
-      SR_UN(0) SR_UN(1) SR_UN(2) SR_UN(3) SR_UN(4) SR_UN(5) SR_UN(6) SR_UN(7) SR_UN(8) SR_UN(9)
-      SR_UN(10) SR_UN(11) SR_UN(12) SR_UN(13) SR_UN(14) SR_UN(15) SR_UN(16) SR_UN(17) SR_UN(18)
-      SR_UN(19) SR_UN(20) SR_UN(21) SR_UN(22) SR_UN(23) SR_UN(24) SR_UN(25) SR_UN(26) SR_UN(27)
-      SR_UN(28)
-      SR_BIN(0) SR_BIN(1) SR_BIN(2) SR_BIN(3) SR_BIN(4) SR_BIN(5) SR_BIN(6) SR_BIN(7) SR_BIN(8)
-      SR_BIN(9) SR_BIN(10)
-      default: break;
-    }
-    cur = nxt;
-    ++pc;
-  }
-}
-static_assert(SRHIP_NUM_UOPS == 29 && SRHIP_NUM_BOPS == 11, "update the case lists");
+using namespace interp;
 
 // Σ over this lane's rows of the tile of w·ℓ(ŷ, y); masked rows (past n) add 0.
 template <int LK, bool W, bool MASK, typename T, int R>
 __device__ __forceinline__ T tile_loss(const T (&acc)[R], const T (&yv)[R], const T (&wv)[R],
                                        T lp, int lane, int valid) {
-  constexpr int N = V16<T>::N;
   T s0 = T(0), s1 = T(0);
 #pragma unroll
   for (int e = 0; e < R; ++e) {
     T l = dev::elem_loss<T>(LK, lp, acc[e], yv[e]);
     if constexpr (W) l = wv[e] * l;
     if constexpr (MASK) {
-      const int row = ((e / N) * 64 + lane) * N + (e % N);
+      const int row = row_of<T, R>(e, lane);
       l = row < valid ? l : T(0);
     }
     if (e & 1) s1 += l; else s0 += l;
@@ -252,7 +68,6 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
   T* sY = sX + (size_t)a.nfeat * rows;
   T* sW = sY + rows;
   Part<T>* sPart = reinterpret_cast<Part<T>*>(sX + (size_t)narr * rows);
-  int* sCounter = reinterpret_cast<int*>(sPart + a.tpb);
 
   const int rg = blockIdx.x / a.ntg;
   const int g = blockIdx.x - rg * a.ntg;
@@ -269,7 +84,6 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
       reinterpret_cast<V*>(sX + (size_t)arr * rows)[v] = reinterpret_cast<const V*>(src + row0)[v];
     }
     for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) sPart[i] = Part<T>{T(0), T(0)};
-    if (threadIdx.x == 0) *sCounter = 0;
   }
   __syncthreads();
 
@@ -280,11 +94,11 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
   const T lp = a.lparam;
 
   // 2. trees of this group, taken dynamically by the waves
-  for (;;) {
-    int i = 0;
-    if (lane == 0) i = atomicAdd(sCounter, 1);
-    i = __builtin_amdgcn_readfirstlane(i);
-    if (i >= a.tpb) break;
+  // Waves take the group's (cost-sorted) trees round-robin: a static,
+  // wave-uniform schedule (no atomics, no divergent loop exit).
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nwaves = (int)(blockDim.x >> 6);
+  for (int i = wave; i < a.tpb; i += nwaves) {
     const int s = i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
     if (s >= a.nlist) continue;
     const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
@@ -431,14 +245,12 @@ static inline int variant_R(int dtype, bool deep) {
   return dtype == SRHIP_F32 ? (deep ? 4 : 8) : (deep ? 2 : 4);
 }
 
-bool plan_eval(int dtype, bool deep, int mode, bool weighted, int nfeat, int64_t n,
-               int nlist, EvalPlan* p) {
-  const size_t esz = dtype == SRHIP_F32 ? 4 : 8;
-  p->R = variant_R(dtype, deep);
-  p->D = deep ? kMaxSlots : 4;
-  p->tile = 64 * p->R;
+bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n, int nlist,
+                   EvalPlan* p) {
+  p->R = R;
+  p->D = D;
+  p->tile = 64 * R;
   p->threads = 256;
-  const int narr = nfeat + (mode == MODE_LOSS ? (weighted ? 2 : 1) : 0);
   const size_t per_tile = (size_t)narr * p->tile * esz;
   const size_t budget = 40 * 1024;
   int nt = 1;
@@ -456,9 +268,15 @@ bool plan_eval(int dtype, bool deep, int mode, bool weighted, int nfeat, int64_t
   if (ntg < 1) ntg = 1;
   p->tpb = (nlist + ntg - 1) / ntg;
   p->ntg = (nlist + p->tpb - 1) / p->tpb;
-  const size_t part = (size_t)p->tpb * 2 * esz;
-  p->lds_bytes = per_tile * nt + part + 16;
+  p->lds_bytes = per_tile * nt + (size_t)p->tpb * part_bytes + 16;
   return p->lds_bytes <= 160 * 1024;
+}
+
+bool plan_eval(int dtype, bool deep, int mode, bool weighted, int nfeat, int64_t n,
+               int nlist, EvalPlan* p) {
+  const size_t esz = dtype == SRHIP_F32 ? 4 : 8;
+  const int narr = nfeat + (mode == MODE_LOSS ? (weighted ? 2 : 1) : 0);
+  return plan_geometry(esz, variant_R(dtype, deep), deep ? kMaxSlots : 4, narr, 2 * esz, n, nlist, p);
 }
 
 template <typename T>

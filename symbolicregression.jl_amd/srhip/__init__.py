@@ -9,7 +9,8 @@ from . import constants
 from ._lib import SrhipError, Unsupported, lib
 from .dataset import Dataset
 from .engine import Context, DeviceDataset, Program, device_count, get_context
-from .interface import (compile_trees, compute_complexity, eval_loss, eval_loss_batch, eval_loss_batch_ok,
+from .interface import (compile_trees, compute_complexity, eval_grad_tree_array, eval_loss, eval_loss_batch,
+                        eval_loss_batch_ok, eval_loss_grad_batch,
                         eval_tree_array, loss_to_score, score_func, score_func_batch, score_func_batched,
                         update_baseline_loss_)
 from .node import (FlatTrees, Node, count_nodes, flatten, get_constants, has_constants, set_constants,

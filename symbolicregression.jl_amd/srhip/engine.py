@@ -175,6 +175,29 @@ class Program:
                                     C.byref(wsum), _p(ok)))
         return sums[:nt], wsum.value, ok[:nt].astype(bool)
 
+    def eval_loss_grad(self, ds: DeviceDataset, loss_kind: int, params=None):
+        """(Σ w·ℓ per tree, Σ w·∂ℓ/∂c per constant [const_off order], Σw, ok)."""
+        nt = self.ntrees
+        nc = int(self.flat.const_off[-1])
+        sums = np.zeros(max(nt, 1), dtype=np.float64)
+        grads = np.zeros(max(nc, 1), dtype=np.float64)
+        ok = np.zeros(max(nt, 1), dtype=np.uint8)
+        wsum = C.c_double(0)
+        par = None if params is None else np.asarray(params, dtype=np.float64)
+        check(lib().srhip_eval_loss_grad(ds.handle, self.handle, int(loss_kind), _p(par), _p(sums), _p(grads),
+                                         C.byref(wsum), _p(ok)))
+        return sums[:nt], grads[:nc], wsum.value, ok[:nt].astype(bool)
+
+    def eval_grad_tree_array(self, ds: DeviceDataset):
+        """(ŷ [ntrees][rows], ∂ŷ/∂c [total consts][rows], ok)."""
+        nt = self.ntrees
+        nc = int(self.flat.const_off[-1])
+        val = np.empty((nt, ds.rows), dtype=self.dtype)
+        grad = np.empty((nc, ds.rows), dtype=self.dtype)
+        ok = np.zeros(max(nt, 1), dtype=np.uint8)
+        check(lib().srhip_eval_grad_tree_array(ds.handle, self.handle, _p(val), _p(grad), _p(ok)))
+        return val, grad, ok[:nt].astype(bool)
+
     def eval_tree_array(self, ds: DeviceDataset):
         nt = self.ntrees
         out = np.empty((nt, ds.rows), dtype=self.dtype)

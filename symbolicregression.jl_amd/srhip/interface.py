@@ -54,6 +54,49 @@ def eval_tree_array(tree: TreeOrTrees, X: np.ndarray, options: Options, device: 
     return out, ok
 
 
+def eval_grad_tree_array(tree: TreeOrTrees, X: np.ndarray, options: Options, variable: bool = False,
+                         device: Optional[int] = None):
+    """eval_grad_tree_array(tree, X, options; variable=false)
+    (src/InterfaceDynamicExpressions.jl:105-107): (output, gradient, complete)
+    with gradient[k, i] = ∂ŷ_i/∂c_k for the tree's constants in get_constants
+    order. For a list of trees: outputs (ntrees, n), a list of per-tree
+    gradient matrices, and a bool array."""
+    if variable:
+        from ._lib import Unsupported
+
+        raise Unsupported(-2, "derivatives with respect to X (variable=true) are not implemented by the engine")
+    trees, single = _as_list(tree)
+    X = np.asarray(X)
+    T = X.dtype if X.dtype in (np.float32, np.float64) else np.dtype(np.float64)
+    ctx = get_context(device)
+    ds = DeviceDataset(ctx, X.astype(T, copy=False), np.zeros(X.shape[1], dtype=T))
+    prog = Program(ctx, flatten(trees, options, dtype=T), T)
+    val, grad, ok = prog.eval_grad_tree_array(ds)
+    co = prog.flat.const_off
+    grads = [grad[co[t]:co[t + 1]] for t in range(len(trees))]
+    if single:
+        return val[0], grads[0], bool(ok[0])
+    return val, grads, ok
+
+
+def eval_loss_grad_batch(trees: Sequence[Node], dataset: Dataset, options: Options,
+                         device: Optional[int] = None):
+    """Batched loss + constant gradients for ConstantOptimization
+    (src/ConstantOptimization.jl:12-65): per tree (loss in T, ∂loss/∂c as a
+    float64 vector in get_constants order, did_succeed)."""
+    dev = dataset.device(device)
+    prog = compile_trees(trees, options, dataset.T, dev.ctx.device)
+    loss = options.elementwise_loss
+    sums, grads, wsum, ok = prog.eval_loss_grad(dev, loss.kind, loss.params)
+    T = dataset.T
+    with np.errstate(invalid="ignore", divide="ignore"):
+        losses = (sums / wsum).astype(T)
+    losses[~ok] = T(np.inf)
+    co = prog.flat.const_off
+    g = [grads[co[t]:co[t + 1]] / wsum for t in range(len(trees))]
+    return losses, g, ok
+
+
 # ---- losses -------------------------------------------------------------------------
 def eval_loss_batch(trees: Sequence[Node], dataset: Dataset, options: Options,
                     row_idx: Optional[np.ndarray] = None, device: Optional[int] = None,
