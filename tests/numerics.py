@@ -1,0 +1,82 @@
+"""Condition-aware comparison helpers for the parity tests.
+
+Two correct evaluations of the same tree can differ by far more than a few
+ulp when the tree amplifies rounding differences (cos of a huge argument,
+x/(c - x) near a pole, exp of a large value...). The bar the engine must meet
+is per operator (bit-exact + - * /, ≤ 4 ulp transcendentals — checked
+directly by test_each_unary_operator / test_each_binary_operator); for whole
+trees the tests allow, per row, the spread the oracle itself shows when X and
+the constants are perturbed at the ulp scale of T.
+"""
+import numpy as np
+
+import oracle
+import srhip
+
+# perturbation size: 4 ulp of T (a perturbation below 1 ulp of float64 would
+# round away when applied in float64)
+EPS = {np.dtype(np.float32): 4 * 2.0 ** -23, np.dtype(np.float64): 4 * 2.0 ** -52}
+
+
+def _perturbed(flat, X, T, k, rng):
+    eps = EPS[np.dtype(T)]
+    Xp = X.astype(np.float64) * (1 + eps * rng.uniform(-1, 1, X.shape))
+    fp = srhip.node.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off,
+                              flat.consts.astype(np.float64) * (1 + eps * rng.uniform(-1, 1, flat.consts.shape)),
+                              flat.nodes)
+    return fp, Xp
+
+
+def output_spread(trees, options, X, T, nperturb=3, seed=0):
+    """Per (tree, row): max |f(X', c') - f(X, c)| over ulp-scale perturbations,
+    evaluated in float64 by the oracle."""
+    rng = np.random.default_rng(seed)
+    flat = srhip.flatten(trees, options, dtype=np.float64)
+    flat.consts = srhip.flatten(trees, options, dtype=T).consts.astype(np.float64)
+    base, _ = oracle.eval_trees(flat, X.astype(np.float64), dtype=np.float64)
+    spread = np.zeros_like(base)
+    with np.errstate(invalid="ignore", over="ignore"):
+        for _ in range(nperturb):
+            fp, Xp = _perturbed(flat, X, T, 1, rng)
+            pert, _ = oracle.eval_trees(fp, Xp, dtype=np.float64)
+            d = np.abs(pert - base)
+            spread = np.where(np.isfinite(d), np.maximum(spread, d), np.inf)
+    return spread
+
+
+def loss_spread(trees, options, X, y, w, T, nperturb=3, seed=0, loss=None):
+    """Per tree: max |Σ w ℓ (perturbed) - Σ w ℓ| (float64 oracle)."""
+    rng = np.random.default_rng(seed)
+    loss = loss or options.elementwise_loss
+    flat = srhip.flatten(trees, options, dtype=np.float64)
+    flat.consts = srhip.flatten(trees, options, dtype=T).consts.astype(np.float64)
+    y64 = y.astype(np.float64)
+    w64 = None if w is None else w.astype(np.float64)
+    base, _, _ = oracle.eval_loss_batch(flat, X.astype(np.float64), y64, w64, loss.kind, loss.params,
+                                        dtype=np.float64)
+    spread = np.zeros_like(base)
+    with np.errstate(invalid="ignore", over="ignore"):
+        for _ in range(nperturb):
+            fp, Xp = _perturbed(flat, X, T, 1, rng)
+            pert, _, _ = oracle.eval_loss_batch(fp, Xp, y64, w64, loss.kind, loss.params, dtype=np.float64)
+            d = np.abs(pert - base)
+            spread = np.where(np.isfinite(d), np.maximum(spread, d), np.inf)
+    return spread
+
+
+def assert_close_conditioned(actual, desired, spread, rtol, atol=0.0, factor=64.0, msg="", max_bad_frac=0.0):
+    """|actual - desired| <= atol + rtol |desired| + factor * spread, elementwise
+    (a fraction max_bad_frac of the elements may exceed it: the input
+    perturbation does not model rounding inside the tree, which matters for
+    f32 derivatives near cancellations)."""
+    actual = np.asarray(actual, dtype=np.float64)
+    desired = np.asarray(desired, dtype=np.float64)
+    tol = atol + rtol * np.abs(desired) + factor * spread
+    with np.errstate(invalid="ignore"):
+        bad = ~(np.abs(actual - desired) <= tol)
+    bad &= ~(np.isnan(actual) & np.isnan(desired))
+    if bad.sum() > max_bad_frac * bad.size:
+        i = np.flatnonzero(bad.ravel())[:5]
+        raise AssertionError(f"{msg}: {bad.sum()} of {bad.size} beyond the conditioned bound; "
+                             f"actual={actual.ravel()[i]} desired={desired.ravel()[i]} "
+                             f"spread={np.asarray(spread).ravel()[i]}")

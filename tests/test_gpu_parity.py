@@ -9,6 +9,7 @@ import pytest
 
 import oracle
 import srhip
+from numerics import assert_close_conditioned, loss_spread, output_spread
 from srhip import Node
 from srhip import constants as K
 
@@ -61,6 +62,8 @@ def oracle_outputs(trees, options, X, T):
     return oracle.eval_trees(flat, X, dtype=T)
 
 
+
+
 @pytest.mark.parametrize("n", [1, 100, 513, 3000])
 def test_random_trees_f32_outputs(gpu_ctx, n):
     o = srhip.Options(binary_operators=F32_OPS[0], unary_operators=F32_OPS[1])
@@ -69,6 +72,7 @@ def test_random_trees_f32_outputs(gpu_ctx, n):
     out, ok = srhip.eval_tree_array(trees, X, o)
     ref, ref_ok = oracle_outputs(trees, o, X, np.float32)
     assert np.array_equal(ok, ref_ok), f"did_succeed differs on {np.flatnonzero(ok != ref_ok)}"
+    spread = output_spread(trees, o, X, np.float32)
     exact = 0
     for t, tree in enumerate(trees):
         if not ok[t]:
@@ -77,8 +81,8 @@ def test_random_trees_f32_outputs(gpu_ctx, n):
             assert np.array_equal(out[t], ref[t]), f"tree {t} not bit-exact: {srhip.string_tree(tree, o)}"
             exact += 1
         else:
-            np.testing.assert_allclose(out[t], ref[t], rtol=2e-4, atol=1e-5,
-                                       err_msg=srhip.string_tree(tree, o))
+            assert_close_conditioned(out[t], ref[t], spread[t], rtol=1e-5, atol=1e-6,
+                                     msg=srhip.string_tree(tree, o))
     assert exact > 0
 
 
@@ -91,8 +95,9 @@ def test_random_trees_f32_losses(gpu_ctx):
     flat = srhip.flatten(trees, o, dtype=np.float32)
     _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, dtype=np.float32)
     assert np.array_equal(ok, ref_ok)
-    fin = ok & np.isfinite(ref_l)
-    np.testing.assert_allclose(losses[fin], ref_l[fin], rtol=1e-5)
+    spread = loss_spread(trees, o, X, y, None, np.float32) / len(y)
+    m = ok & np.isfinite(ref_l)
+    assert_close_conditioned(losses[m], ref_l[m], spread[m], rtol=1e-5, msg="f32 losses")
     assert np.all(np.isinf(losses[~ok]))
 
 
@@ -105,15 +110,17 @@ def test_nan_heavy_f64(gpu_ctx):
     ref, ref_ok = oracle_outputs(trees, o, X, np.float64)
     assert np.array_equal(ok, ref_ok), f"did_succeed differs on {np.flatnonzero(ok != ref_ok)}"
     assert 0.05 < ok.mean() < 0.95  # the workload really is NaN-heavy
+    spread = output_spread(trees, o, X, np.float64)
     for t in np.flatnonzero(ok):
-        np.testing.assert_allclose(out[t], ref[t], rtol=1e-9, atol=1e-12)
+        assert_close_conditioned(out[t], ref[t], spread[t], rtol=1e-12, atol=1e-14, msg=srhip.string_tree(trees[t], o))
     y = np.random.default_rng(5).standard_normal(2500)
     ds = srhip.Dataset(X, y)
     losses, lok = srhip.eval_loss_batch_ok(trees, ds, o)
     flat = srhip.flatten(trees, o, dtype=np.float64)
     _, ref_l, ref_lok = oracle.eval_loss_batch(flat, X, y, dtype=np.float64)
     assert np.array_equal(lok, ref_lok)
-    np.testing.assert_allclose(losses[lok], ref_l[lok], rtol=1e-10)
+    lsp = loss_spread(trees, o, X, y, None, np.float64) / len(y)
+    assert_close_conditioned(losses[lok], ref_l[lok], lsp[lok], rtol=1e-10, msg="f64 losses")
 
 
 UNARY_EXACT = {"NEG", "SQUARE", "CUBE", "ABS", "SQRT", "RELU", "ROUND", "FLOOR", "CEIL", "SIGN", "INV"}
@@ -183,7 +190,9 @@ def test_weighted_and_all_losses(gpu_ctx):
             _, rl, rok = oracle.eval_loss_batch(flat, X, y, weights, loss.kind, loss.params, dtype=np.float64)
             assert np.array_equal(ok, rok)
             m = ok & np.isfinite(rl)
-            np.testing.assert_allclose(l[m], rl[m], rtol=1e-9, err_msg=str(loss))
+            wsum = len(y) if weights is None else weights.sum()
+            sp = loss_spread(trees, o, X, y, weights, np.float64) / wsum
+            assert_close_conditioned(l[m], rl[m], sp[m], rtol=1e-9, msg=str(loss))
 
 
 def test_score_func_batch_row_subset(gpu_ctx):
@@ -199,7 +208,9 @@ def test_score_func_batch_row_subset(gpu_ctx):
         _, rl, rok = oracle.eval_loss_batch(flat, X, y, weights, row_idx=idx, dtype=np.float32)
         assert np.array_equal(ok, rok)
         m = ok & np.isfinite(rl)
-        np.testing.assert_allclose(l[m], rl[m], rtol=1e-5)
+        wv = None if weights is None else weights[idx]
+        sp = loss_spread(trees, o, X[:, idx], y[idx], wv, np.float32) / (50 if wv is None else wv.sum())
+        assert_close_conditioned(l[m], rl[m], sp[m], rtol=1e-5, msg="minibatch losses")
         s, ls = srhip.score_func_batch(ds, trees, o, row_idx=idx)
         assert np.all(s[~ok] == 0) and np.all(np.isinf(ls[~ok]))  # (0, Inf) on failure
 
@@ -277,7 +288,8 @@ def test_million_rows_properties(gpu_ctx):
     rs, _, rok = oracle.eval_loss_batch(flat, X, y, dtype=np.float32)
     assert np.array_equal(ok, rok) and wsum == 1_000_000
     m = ok & np.isfinite(rs)
-    np.testing.assert_allclose(sums[m], rs[m], rtol=1e-5)
+    sp = loss_spread(trees, o, X, y, None, np.float32, nperturb=2)
+    assert_close_conditioned(sums[m], rs[m], sp[m], rtol=1e-5, msg="1M-row loss sums")
     # row shards through the ABI's row range: Σ shards == whole
     ctx = srhip.get_context(0)
     parts = []
@@ -289,4 +301,4 @@ def test_million_rows_properties(gpu_ctx):
     assert sum(p[1] for p in parts) == 1_000_000
     kk = np.logical_and.reduce([p[2] for p in parts])
     assert np.array_equal(kk, ok)
-    np.testing.assert_allclose(tot[m], sums[m], rtol=1e-5)
+    assert_close_conditioned(tot[m], sums[m], sp[m], rtol=1e-5, msg="sharded sums")

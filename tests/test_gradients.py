@@ -8,6 +8,7 @@ import pytest
 
 import oracle
 import srhip
+from numerics import EPS, assert_close_conditioned
 from srhip import Node
 
 
@@ -61,6 +62,26 @@ def test_engine_derivatives_kat(gpu_ctx):
         assert ok and np.allclose(g, analytic_eq5(X), rtol=1e-3, atol=1e-4)
 
 
+def grad_spread(tree, o, X, T, nperturb=3, seed=0):
+    """Spread of the oracle's (value, gradient) under ulp-scale perturbations
+    of X and the constants (float64 evaluation)."""
+    rng = np.random.default_rng(seed)
+    flat = srhip.flatten([tree], o, dtype=np.float64)
+    k, a, c = flat.tree(0)
+    c = srhip.flatten([tree], o, dtype=T).consts.astype(np.float64)
+    X64 = X.astype(np.float64)
+    v0, g0, ok0 = oracle.eval_grad_consts(k, a, c, X64, len(c))
+    sv, sg = np.zeros_like(v0), np.zeros_like(g0)
+    eps = EPS[np.dtype(T)]
+    with np.errstate(invalid="ignore", over="ignore"):
+        for _ in range(nperturb):
+            v, g, _ = oracle.eval_grad_consts(k, a, c * (1 + eps * rng.uniform(-1, 1, c.shape)),
+                                              X64 * (1 + eps * rng.uniform(-1, 1, X.shape)), len(c))
+            sv = np.where(np.isfinite(v - v0), np.maximum(sv, np.abs(v - v0)), np.inf)
+            sg = np.where(np.isfinite(g - g0), np.maximum(sg, np.abs(g - g0)), np.inf)
+    return v0, g0, ok0, sv, sg
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("T", [np.float64, np.float32])
 def test_engine_gradients_vs_oracle_random(gpu_ctx, T):
@@ -69,25 +90,29 @@ def test_engine_gradients_vs_oracle_random(gpu_ctx, T):
     X = np.random.default_rng(62).standard_normal((4, 777)).astype(T)
     val, grads, ok = srhip.eval_grad_tree_array(trees, X, o)
     ncheck = 0
+    # did_succeed in T (f32 overflows where f64 does not): from the T oracle
+    _, ok_T = oracle.eval_trees(srhip.flatten(trees, o, dtype=T), X, dtype=T)
+    assert np.array_equal(ok, ok_T)
     for t, tree in enumerate(trees):
-        rv, rg, rok = oracle_grad(tree, o, X.astype(np.float64))
-        assert ok[t] == rok, srhip.string_tree(tree, o)
-        if not ok[t]:
+        rv, rg, rok, sv, sg = grad_spread(tree, o, X, T)
+        if not (ok[t] and rok):
             continue
-        rtol = 1e-8 if T == np.float64 else 2e-3
-        np.testing.assert_allclose(val[t], rv, rtol=rtol, atol=rtol)
-        scale = np.maximum(np.abs(rg), 1.0)
-        if T == np.float32:  # f32 rounding amplified by cancellation: compare well-conditioned entries
-            good = np.abs(rg) < 1e4
-            assert np.mean(np.abs(grads[t] - rg)[good] / scale[good] < 1e-2) > 0.99
-        else:
-            np.testing.assert_allclose(grads[t] / scale, rg / scale, rtol=0, atol=1e-7)
-        ncheck += len(rg)
+        vals.append(val[t]); refs.append(rv); svs.append(sv)
+        grs.append(grads[t].ravel()); rgs.append(rg.ravel()); sgs.append(sg.ravel())
+        ncheck += rg.size
+    rtol = 1e-11 if T == np.float64 else 1e-5
+    bad = 0.0 if T == np.float64 else 2e-3
+    cat = np.concatenate
+    assert_close_conditioned(cat(vals), cat(refs), cat(svs), rtol=rtol, atol=rtol, msg="values", max_bad_frac=bad)
+    assert_close_conditioned(cat(grs), cat(rgs), cat(sgs), rtol=rtol, atol=rtol, msg="gradients", max_bad_frac=bad)
     assert ncheck > 100
 
 
 @pytest.mark.gpu
 def test_loss_gradient_matches_finite_differences(gpu_ctx):
+    """∂loss/∂c (fused kernel) against central differences of the oracle's
+    loss, on trees where the difference quotient is stable (two step sizes
+    agree)."""
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     trees = srhip.random_population(120, o, 3, np.float64, seed=71)
     trees = [t for t in trees if srhip.has_constants(t)]
@@ -95,6 +120,7 @@ def test_loss_gradient_matches_finite_differences(gpu_ctx):
     X = rng.standard_normal((3, 3000))
     y = 2 * np.cos(X[2]) + X[0] ** 2 - 2
     w = np.abs(rng.standard_normal(3000))
+    nchecked = 0
     for weights in (None, w):
         ds = srhip.Dataset(X, y, weights=weights)
         losses, grads, ok = srhip.eval_loss_grad_batch(trees, ds, o)
@@ -106,16 +132,17 @@ def test_loss_gradient_matches_finite_differences(gpu_ctx):
             k, a, c = flat.tree(t)
             c = c.astype(np.float64)
             for j in range(len(c)):
-                h = 1e-6 * max(1.0, abs(c[j]))
-                cp, cm = c.copy(), c.copy()
-                cp[j] += h
-                cm[j] -= h
-                lp = loss_of(k, a, cp, X, y, weights)
-                lm = loss_of(k, a, cm, X, y, weights)
-                if not (np.isfinite(lp) and np.isfinite(lm)):
-                    continue
-                fd = (lp - lm) / (2 * h)
-                assert abs(grads[t][j] - fd) <= 1e-4 * max(1.0, abs(fd)), (t, j, grads[t][j], fd)
+                fds = []
+                for h in (1e-5 * max(1.0, abs(c[j])), 1e-6 * max(1.0, abs(c[j]))):
+                    cp, cm = c.copy(), c.copy()
+                    cp[j] += h
+                    cm[j] -= h
+                    fds.append((loss_of(k, a, cp, X, y, weights) - loss_of(k, a, cm, X, y, weights)) / (2 * h))
+                if not np.all(np.isfinite(fds)) or abs(fds[0] - fds[1]) > 1e-5 * max(1.0, abs(fds[1])):
+                    continue  # difference quotient not converged (pole / cancellation nearby)
+                assert abs(grads[t][j] - fds[1]) <= 1e-4 * max(1.0, abs(fds[1])), (t, j, grads[t][j], fds)
+                nchecked += 1
+    assert nchecked > 50
 
 
 def loss_of(kind, arg, consts, X, y, w):
