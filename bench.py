@@ -146,7 +146,7 @@ def main():
     esz = np.dtype(T).itemsize
     alg_bytes = args.rows * (args.nfeat + 1) * esz + prog.ntrees * 17
     roof["hbm_algorithmic_GBs"] = alg_bytes / (k_ms * 1e-3) / 1e9
-    prof = ROOT / "profiles" / "r01_pmc_summary.json"
+    prof = ROOT / "profiles" / "current_pmc_summary.json"
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())

@@ -15,38 +15,50 @@ namespace srhip {
 namespace dev {
 
 // ---- thin overload set over OCML ----------------------------------------------
+// Heavy or branchy routines (trig range reduction, tgamma, pow, fmod, ...)
+// are called out of line: inlined into the interpreter's dispatch switch,
+// their divergent internal branches make the register allocator split the
+// accumulator's live ranges and insert a copy of every accumulator register
+// into EVERY dispatch. A call costs two v_mov and an s_swappc per value.
+// exp, log and sqrt are short and branch-free and stay inline.
 #define SR_M1(name, f32, f64)                                              \
   __device__ __forceinline__ float name(float x) { return f32(x); }        \
   __device__ __forceinline__ double name(double x) { return f64(x); }
+#define SR_M1_OOL(name, f32, f64)                                                       \
+  __device__ __attribute__((noinline)) float name##_ool(float x) { return f32(x); }      \
+  __device__ __attribute__((noinline)) double name##_ool(double x) { return f64(x); }    \
+  __device__ __forceinline__ float name(float x) { return name##_ool(x); }              \
+  __device__ __forceinline__ double name(double x) { return name##_ool(x); }
 SR_M1(m_exp, expf, exp)
 SR_M1(m_log, logf, log)
-SR_M1(m_log2, log2f, log2)
-SR_M1(m_log10, log10f, log10)
-SR_M1(m_log1p, log1pf, log1p)
+SR_M1_OOL(m_log2, log2f, log2)
+SR_M1_OOL(m_log10, log10f, log10)
+SR_M1_OOL(m_log1p, log1pf, log1p)
 SR_M1(m_sqrt, sqrtf, sqrt)
-SR_M1(m_sin, sinf, sin)
-SR_M1(m_cos, cosf, cos)
-SR_M1(m_tan, tanf, tan)
-SR_M1(m_sinh, sinhf, sinh)
-SR_M1(m_cosh, coshf, cosh)
-SR_M1(m_tanh, tanhf, tanh)
-SR_M1(m_atan, atanf, atan)
-SR_M1(m_asinh, asinhf, asinh)
-SR_M1(m_acosh, acoshf, acosh)
-SR_M1(m_atanh, atanhf, atanh)
-SR_M1(m_erf, erff, erf)
-SR_M1(m_erfc, erfcf, erfc)
-SR_M1(m_tgamma, tgammaf, tgamma)
+SR_M1_OOL(m_sin, sinf, sin)
+SR_M1_OOL(m_cos, cosf, cos)
+SR_M1_OOL(m_tan, tanf, tan)
+SR_M1_OOL(m_sinh, sinhf, sinh)
+SR_M1_OOL(m_cosh, coshf, cosh)
+SR_M1_OOL(m_tanh, tanhf, tanh)
+SR_M1_OOL(m_atan, atanf, atan)
+SR_M1_OOL(m_asinh, asinhf, asinh)
+SR_M1_OOL(m_acosh, acoshf, acosh)
+SR_M1_OOL(m_atanh, atanhf, atanh)
+SR_M1_OOL(m_erf, erff, erf)
+SR_M1_OOL(m_erfc, erfcf, erfc)
+SR_M1_OOL(m_tgamma, tgammaf, tgamma)
 SR_M1(m_rint, rintf, rint)
 SR_M1(m_floor, floorf, floor)
 SR_M1(m_ceil, ceilf, ceil)
 SR_M1(m_trunc, truncf, trunc)
 SR_M1(m_fabs, fabsf, fabs)
 #undef SR_M1
-__device__ __forceinline__ float m_pow(float x, float y) { return powf(x, y); }
-__device__ __forceinline__ double m_pow(double x, double y) { return pow(x, y); }
-__device__ __forceinline__ float m_fmod(float x, float y) { return fmodf(x, y); }
-__device__ __forceinline__ double m_fmod(double x, double y) { return fmod(x, y); }
+#undef SR_M1_OOL
+__device__ __attribute__((noinline)) float m_pow(float x, float y) { return powf(x, y); }
+__device__ __attribute__((noinline)) double m_pow(double x, double y) { return pow(x, y); }
+__device__ __attribute__((noinline)) float m_fmod(float x, float y) { return fmodf(x, y); }
+__device__ __attribute__((noinline)) double m_fmod(double x, double y) { return fmod(x, y); }
 __device__ __forceinline__ float m_copysign(float x, float y) { return copysignf(x, y); }
 __device__ __forceinline__ double m_copysign(double x, double y) { return copysign(x, y); }
 __device__ __forceinline__ bool m_isinf(float x) { return __builtin_isinf(x); }
@@ -59,14 +71,35 @@ template <>
 __device__ __forceinline__ float qnan<float>() { return __builtin_nanf(""); }
 
 // Base.mod for floats: r = rem(x, y) (= fmod, exact); r == 0 → copysign(r, y);
-// sign(r) != sign(y) → r + y; else r.
+// sign(r) != sign(y) → r + y; else r. Out of line (fmod loops).
 template <typename T>
-__device__ __forceinline__ T jl_mod(T x, T y) {
+__device__ __attribute__((noinline)) T jl_mod(T x, T y) {
   T r = m_fmod(x, y);
   T s = r + y;
   bool flip = (r > T(0)) != (y > T(0));
   T v = flip ? s : r;
   return (r == T(0)) ? m_copysign(r, y) : v;
+}
+
+// safe_pow, Operators.jl:38-46. Out of line (pow's special-case branches).
+template <typename T>
+__device__ __attribute__((noinline)) T safe_pow(T x, T y) {
+  const bool isint = (y == m_trunc(y));
+  const bool bad = isint ? (y < T(0) && x == T(0))
+                         : ((y > T(0) && x < T(0)) || (y < T(0) && x <= T(0)));
+  return bad ? qnan<T>() : m_pow(x, y);
+}
+
+// Base.max / min on finite operands, -0.0 < +0.0, branch-free: for equal
+// values the bit patterns are equal except for ±0, where AND (max) clears and
+// OR (min) keeps the sign bit.
+__device__ __forceinline__ float bits_and(float a, float b) { return __int_as_float(__float_as_int(a) & __float_as_int(b)); }
+__device__ __forceinline__ float bits_or(float a, float b) { return __int_as_float(__float_as_int(a) | __float_as_int(b)); }
+__device__ __forceinline__ double bits_and(double a, double b) {
+  return __longlong_as_double(__double_as_longlong(a) & __double_as_longlong(b));
+}
+__device__ __forceinline__ double bits_or(double a, double b) {
+  return __longlong_as_double(__double_as_longlong(a) | __double_as_longlong(b));
 }
 
 // ---- binary operators -----------------------------------------------------------
@@ -76,24 +109,19 @@ __device__ __forceinline__ T bop(T x, T y) {
   else if constexpr (OP == SRHIP_BOP_SUB) return x - y;
   else if constexpr (OP == SRHIP_BOP_MUL) return x * y;
   else if constexpr (OP == SRHIP_BOP_DIV) return x / y;
-  else if constexpr (OP == SRHIP_BOP_POW) {
-    // safe_pow, Operators.jl:38-46
-    const bool isint = (y == m_trunc(y));
-    const bool bad = isint ? (y < T(0) && x == T(0))
-                           : ((y > T(0) && x < T(0)) || (y < T(0) && x <= T(0)));
-    const T p = m_pow(x, y);
-    return bad ? qnan<T>() : p;
-  } else if constexpr (OP == SRHIP_BOP_GREATER) return x > y ? T(1) : T(0);
+  else if constexpr (OP == SRHIP_BOP_POW) return safe_pow(x, y);
+  else if constexpr (OP == SRHIP_BOP_GREATER) return x > y ? T(1) : T(0);
   else if constexpr (OP == SRHIP_BOP_LOGICAL_OR) return (x > T(0) || y > T(0)) ? T(1) : T(0);
   else if constexpr (OP == SRHIP_BOP_LOGICAL_AND) return (x > T(0) && y > T(0)) ? T(1) : T(0);
   else if constexpr (OP == SRHIP_BOP_MOD) return jl_mod(x, y);
   else if constexpr (OP == SRHIP_BOP_MAX) {
-    // operands are finite whenever the result matters; keep -0.0 < +0.0
-    T m = (x > y) ? x : y;
-    return (x == y) ? (m_signbit(x) ? y : x) : m;
+    const T e = bits_and(x, y);
+    const T m = (x > y) ? x : y;
+    return (x == y) ? e : m;
   } else if constexpr (OP == SRHIP_BOP_MIN) {
-    T m = (x < y) ? x : y;
-    return (x == y) ? (m_signbit(x) ? x : y) : m;
+    const T e = bits_or(x, y);
+    const T m = (x < y) ? x : y;
+    return (x == y) ? e : m;
   } else {
     static_assert(OP < SRHIP_NUM_BOPS, "unknown binary op");
     return x;
@@ -174,7 +202,7 @@ __device__ __forceinline__ void bop_d(T x, T y, T& f, T& fx, T& fy) {
   else if constexpr (OP == SRHIP_BOP_MUL) { fx = y; fy = x; }
   else if constexpr (OP == SRHIP_BOP_DIV) { fx = T(1) / y; fy = -x / (y * y); }
   else if constexpr (OP == SRHIP_BOP_POW) {
-    fx = y * bop<SRHIP_BOP_POW>(x, y - T(1));
+    fx = y * safe_pow(x, y - T(1));
     fy = x > T(0) ? f * m_log(x) : T(0);
   } else if constexpr (OP == SRHIP_BOP_MOD) { fx = T(1); fy = -m_floor(x / y); }
   else if constexpr (OP == SRHIP_BOP_MAX) { fx = x >= y ? T(1) : T(0); fy = x >= y ? T(0) : T(1); }

@@ -114,10 +114,9 @@ __device__ __forceinline__ void run_program_grad(const Ins<T>* __restrict__ p,
 #pragma unroll
     for (int j = 0; j < G; ++j) { a.d[j][r] = T(0); t.d[j][r] = T(0); }
   }
-  int pc = 0;
   Ins<T> cur = p[0];
   for (;;) {
-    const Ins<T> nxt = p[pc + 1];
+    const Ins<T> nxt = p[1];
     const uint32_t code = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.code);
     const T imm = uni(cur.imm);
     const int f = (int)(code >> 16);
@@ -152,7 +151,7 @@ __device__ __forceinline__ void run_program_grad(const Ins<T>* __restrict__ p,
       default: break;
     }
     cur = nxt;
-    ++pc;
+    ++p;
   }
 }
 

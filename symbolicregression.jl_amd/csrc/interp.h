@@ -194,10 +194,9 @@ __device__ __forceinline__ void run_program(const Ins<T>* __restrict__ p,
   T slot[D][R];
 #pragma unroll
   for (int r = 0; r < R; ++r) { acc[r] = T(0); tmp[r] = T(0); }
-  int pc = 0;
   Ins<T> cur = p[0];
   for (;;) {
-    const Ins<T> nxt = p[pc + 1];  // prefetch; every program ends with OP_END + slack
+    const Ins<T> nxt = p[1];  // prefetch; every program ends with OP_END + slack
     const uint32_t code = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.code);
     const T imm = uni(cur.imm);
     const int f = (int)(code >> 16);
@@ -220,7 +219,7 @@ __device__ __forceinline__ void run_program(const Ins<T>* __restrict__ p,
       default: break;
     }
     cur = nxt;
-    ++pc;
+    ++p;
   }
 }
 static_assert(SRHIP_NUM_UOPS == 29 && SRHIP_NUM_BOPS == 11, "update the case lists");

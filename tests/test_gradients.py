@@ -90,6 +90,7 @@ def test_engine_gradients_vs_oracle_random(gpu_ctx, T):
     X = np.random.default_rng(62).standard_normal((4, 777)).astype(T)
     val, grads, ok = srhip.eval_grad_tree_array(trees, X, o)
     ncheck = 0
+    vals, refs, svs, grs, rgs, sgs = [], [], [], [], [], []
     # did_succeed in T (f32 overflows where f64 does not): from the T oracle
     _, ok_T = oracle.eval_trees(srhip.flatten(trees, o, dtype=T), X, dtype=T)
     assert np.array_equal(ok, ok_T)
@@ -97,8 +98,12 @@ def test_engine_gradients_vs_oracle_random(gpu_ctx, T):
         rv, rg, rok, sv, sg = grad_spread(tree, o, X, T)
         if not (ok[t] and rok):
             continue
-        vals.append(val[t]); refs.append(rv); svs.append(sv)
-        grs.append(grads[t].ravel()); rgs.append(rg.ravel()); sgs.append(sg.ravel())
+        vals.append(val[t])
+        refs.append(rv)
+        svs.append(sv)
+        grs.append(grads[t].ravel())
+        rgs.append(rg.ravel())
+        sgs.append(sg.ravel())
         ncheck += rg.size
     rtol = 1e-11 if T == np.float64 else 1e-5
     bad = 0.0 if T == np.float64 else 2e-3
