@@ -124,6 +124,7 @@ struct srhip_program {
   int32_t* d_tree_off = nullptr;
   int32_t* d_list = nullptr;  // [nlist_a + nlist_b]: shallow trees then deep trees
   int nlist_a = 0, nlist_b = 0;
+  int opset = OPSET_FULL;      // smallest operator set covering the compiled programs
   // gradient programs (compiled on first use)
   bool grad_built = false;
   std::vector<uint8_t> g_static_fail;
@@ -220,11 +221,19 @@ void build_program(srhip_program* p) {
   p->fail_if_rows = cb.fail_if_rows;
   p->max_feature = cb.max_feature;
   p->total_nodes = cb.total_nodes;
-  // trees to run, cost-descending; shallow (<= 4 slots) and deep lists
+  // operator set: every opcode left after folding must be in it
+  p->opset = OPSET_BASIC;
+  for (const Ins<T>& ins : cb.code) {
+    const int opc = (int)(ins.code & 0xffu);
+    if (opc >= OP_BIN0 ? !opset_has_bop(OPSET_BASIC, (opc - OP_BIN0) % SRHIP_NUM_BOPS)
+                       : opc >= OP_UN0 && !opset_has_uop(OPSET_BASIC, opc - OP_UN0))
+      p->opset = OPSET_FULL;
+  }
+  // trees to run, cost-descending; shallow (<= kShallowSlots) and deep lists
   std::vector<int32_t> a, b;
   for (int t = 0; t < p->ntrees; ++t) {
     if (cb.tree_off[t] < 0) continue;
-    (cb.need[t] <= 4 ? a : b).push_back(t);
+    (cb.need[t] <= kShallowSlots ? a : b).push_back(t);
   }
   auto by_cost = [&](int32_t x, int32_t y) {
     return cb.cost[x] != cb.cost[y] ? cb.cost[x] > cb.cost[y] : x < y;
@@ -278,7 +287,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     const int nlist = pass == 0 ? p->nlist_a : p->nlist_b;
     if (nlist == 0 || rows == 0) continue;
     EvalPlan plan;
-    if (!plan_eval(p->dtype, pass == 1, mode, w != nullptr, nfeat, rows, nlist, &plan))
+    if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan))
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
     EvalArgs<T> a;
     a.prog = static_cast<const Ins<T>*>(p->d_code);

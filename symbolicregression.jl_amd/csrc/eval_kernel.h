@@ -1,0 +1,165 @@
+// eval_kernel.h — CDNA4 (gfx950) kernels of the batched tree evaluator.
+//
+// eval_kernel: one workgroup = (row group, tree group).
+//   1. The workgroup stages its row group (ntiles × 64·R rows) of every
+//      feature, y and w into LDS once (16-byte vector loads, coalesced).
+//   2. The waves take the group's trees round-robin (trees are sorted by
+//      cost, longest first) and run each program over every tile: the program is wave-uniform (scalar
+//      loads, uniform branches), each instruction processes R rows per lane
+//      held in VGPRs; leaf features come straight from LDS with ds_read_b128.
+//   3. Per tree the wave reduces Σ w·ℓ and the non-finite marker over its
+//      lanes into an LDS slot; the workgroup writes all its slots with one
+//      coalesced store. finalize_kernel sums the row groups in fp64.
+// There is no MFMA: this is a VALU-bound interpreter, not a contraction.
+//
+// This header holds the kernel templates; eval_f32.hip / eval_f64.hip
+// instantiate the variants of one element type each (parallel compiles).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include "interp.h"
+#include "kernels.h"
+
+namespace srhip {
+namespace {
+
+using namespace interp;
+
+// Σ over this lane's rows of the tile of w·ℓ(ŷ, y); masked rows (past n) add 0.
+template <int LK, bool W, bool MASK, typename T, int R>
+__device__ __forceinline__ T tile_loss(const T (&acc)[R], const T (&yv)[R], const T (&wv)[R],
+                                       T lp, int lane, int valid) {
+  T s0 = T(0), s1 = T(0);
+#pragma unroll
+  for (int e = 0; e < R; ++e) {
+    T l = dev::elem_loss<T>(LK, lp, acc[e], yv[e]);
+    if constexpr (W) l = wv[e] * l;
+    if constexpr (MASK) {
+      const int row = row_of<T, R>(e, lane);
+      l = row < valid ? l : T(0);
+    }
+    if (e & 1) s1 += l; else s0 += l;
+  }
+  return s0 + s1;
+}
+
+template <bool W, bool MASK, typename T, int R>
+__device__ __forceinline__ T tile_loss_any(int lk, const T (&acc)[R], const T (&yv)[R],
+                                           const T (&wv)[R], T lp, int lane, int valid) {
+  switch (lk) {
+    case SRHIP_LOSS_L2: return tile_loss<SRHIP_LOSS_L2, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_L1: return tile_loss<SRHIP_LOSS_L1, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_LP: return tile_loss<SRHIP_LOSS_LP, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_HUBER: return tile_loss<SRHIP_LOSS_HUBER, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_LOGCOSH: return tile_loss<SRHIP_LOSS_LOGCOSH, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_L1EPSINS: return tile_loss<SRHIP_LOSS_L1EPSINS, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_L2EPSINS: return tile_loss<SRHIP_LOSS_L2EPSINS, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_QUANTILE: return tile_loss<SRHIP_LOSS_QUANTILE, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_PERIODIC: return tile_loss<SRHIP_LOSS_PERIODIC, W, MASK>(acc, yv, wv, lp, lane, valid);
+    default: return tile_loss<SRHIP_LOSS_LOGITDIST, W, MASK>(acc, yv, wv, lp, lane, valid);
+  }
+}
+
+template <typename T, int R, int D, int SET, int MODE, bool W>
+__global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int TILE = 64 * R;
+  using V = typename V16<T>::type;
+  constexpr int N = V16<T>::N;
+  const int rows = a.ntiles * TILE;
+  const int narr = a.nfeat + (MODE == MODE_LOSS ? (W ? 2 : 1) : 0);
+  T* sX = reinterpret_cast<T*>(smem);
+  T* sY = sX + (size_t)a.nfeat * rows;
+  T* sW = sY + rows;
+  Part<T>* sPart = reinterpret_cast<Part<T>*>(sX + (size_t)narr * rows);
+
+  const int rg = blockIdx.x / a.ntg;
+  const int g = blockIdx.x - rg * a.ntg;
+  const int64_t row0 = (int64_t)rg * rows;
+
+  // 1. stage the row group in LDS
+  {
+    const int vper = rows / N;
+    const int total = narr * vper;
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int arr = idx / vper;
+      const int v = idx - arr * vper;
+      const T* src = arr < a.nfeat ? a.X + (size_t)arr * a.n_pad : (arr == a.nfeat ? a.y : a.w);
+      reinterpret_cast<V*>(sX + (size_t)arr * rows)[v] = reinterpret_cast<const V*>(src + row0)[v];
+    }
+    for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) sPart[i] = Part<T>{T(0), T(0)};
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int64_t rem = a.n - row0;
+  const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE - 1) / TILE);
+  const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
+  const T lp = a.lparam;
+
+  // 2. trees of this group, taken dynamically by the waves
+  // Waves take the group's (cost-sorted) trees round-robin: a static,
+  // wave-uniform schedule (no atomics, no divergent loop exit).
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nwaves = (int)(blockDim.x >> 6);
+  for (int i = wave; i < a.tpb; i += nwaves) {
+    const int s = i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
+    if (s >= a.nlist) continue;
+    const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
+    const Ins<T>* p = a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[t]);
+    T lsum = T(0), chk = T(0);
+    for (int tl = 0; tl < nt_valid; ++tl) {
+      const T* sXt = sX + tl * TILE;
+      T acc[R];
+      run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
+#pragma unroll
+      for (int r = 0; r < R; ++r) chk = mark(acc[r], chk);  // root value
+      if constexpr (MODE == MODE_OUT) {
+        store_rows<T, R>(a.out + (size_t)t * a.out_stride + row0 + tl * TILE, lane, acc);
+      } else {
+        T yv[R], wv[R];
+        lds_rows<T, R>(sY + tl * TILE, lane, yv);
+        if constexpr (W) lds_rows<T, R>(sW + tl * TILE, lane, wv);
+        if (tl < nt_valid - 1 || last_valid == TILE)
+          lsum += tile_loss_any<W, false, T, R>(a.loss, acc, yv, wv, lp, lane, TILE);
+        else
+          lsum += tile_loss_any<W, true, T, R>(a.loss, acc, yv, wv, lp, lane, last_valid);
+      }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) {
+      lsum += __shfl_xor(lsum, off);
+      chk += __shfl_xor(chk, off);
+    }
+    if (lane == 0) sPart[i] = Part<T>{lsum, chk};
+  }
+  __syncthreads();
+  // 3. one coalesced store of the group's partials
+  Part<T>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
+  for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) dst[i] = sPart[i];
+}
+
+template <typename T, int R, int D, int SET, int MODE, bool W>
+hipError_t launch_one(const EvalPlan& plan, const EvalArgs<T>& a, hipStream_t stream) {
+  static bool attr_set = false;  // raise the dynamic-LDS ceiling once per kernel
+  if (!attr_set) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eval_kernel<T, R, D, SET, MODE, W>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e != hipSuccess) return e;
+    attr_set = true;
+  }
+  const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
+  hipLaunchKernelGGL((eval_kernel<T, R, D, SET, MODE, W>), dim3(grid), dim3(plan.threads),
+                     plan.lds_bytes, stream, a);
+  return hipGetLastError();
+}
+
+template <typename T, int R, int D, int SET>
+hipError_t launch_rd(const EvalPlan& plan, const EvalArgs<T>& a, int mode, hipStream_t stream) {
+  if (mode == MODE_OUT) return launch_one<T, R, D, SET, MODE_OUT, false>(plan, a, stream);
+  if (a.w) return launch_one<T, R, D, SET, MODE_LOSS, true>(plan, a, stream);
+  return launch_one<T, R, D, SET, MODE_LOSS, false>(plan, a, stream);
+}
+
+}  // namespace
+}  // namespace srhip

@@ -110,10 +110,31 @@ __device__ __forceinline__ void store_rows(T* __restrict__ p, int lane, const T 
 
 template <int U, typename T, int R>
 __device__ __forceinline__ void un_apply(T (&acc)[R], T& chk) {
+  if constexpr ((U == SRHIP_UOP_COS || U == SRHIP_UOP_SIN) && sizeof(T) == 4) {
+    // fast f32 sin/cos for all R values, one wave-uniform check for the
+    // rare |x| > 105615 that needs OCML's full reduction
+    T v[R];
+    bool big = false;
 #pragma unroll
-  for (int r = 0; r < R; ++r) {
-    if constexpr (uop_lossy(U)) chk = mark(acc[r], chk);
-    acc[r] = uop<U>(acc[r]);
+    for (int r = 0; r < R; ++r) {
+      v[r] = dev::fast_sincos_f32(acc[r], U == SRHIP_UOP_COS ? 1 : 0);
+      big |= dev::trig_big(acc[r]);
+    }
+    if (__builtin_amdgcn_ballot_w64(big) != 0) {
+#pragma unroll
+      for (int r = 0; r < R; ++r) {
+        const T o = U == SRHIP_UOP_COS ? dev::m_cos_ocml(acc[r]) : dev::m_sin_ocml(acc[r]);
+        v[r] = dev::trig_big(acc[r]) ? o : v[r];
+      }
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = v[r];
+  } else {
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      if constexpr (uop_lossy(U)) chk = mark(acc[r], chk);
+      acc[r] = uop<U>(acc[r]);
+    }
   }
 }
 
@@ -179,14 +200,14 @@ __device__ __forceinline__ void bin_apply(T (&acc)[R], const T (&tmp)[R],
     if constexpr (K < D) { SR_UNROLL for (int r = 0; r < R; ++r) tmp[r] = slot[K][r]; } \
     break;
 #define SR_UN(U) \
-  case OP_UN0 + U: un_apply<U, T, R>(acc, chk); break;
+  case OP_UN0 + U: if constexpr (opset_has_uop(SET, U)) un_apply<U, T, R>(acc, chk); break;
 #define SR_BV(V, B) \
-  case bin_opcode(V, B): bin_apply<V, B, T, R>(acc, tmp, sXt, rs, lane, f, imm, chk); break;
+  case bin_opcode(V, B): if constexpr (opset_has_bop(SET, B)) bin_apply<V, B, T, R>(acc, tmp, sXt, rs, lane, f, imm, chk); break;
 #define SR_BIN(B) SR_BV(V_AX, B) SR_BV(V_XA, B) SR_BV(V_AC, B) SR_BV(V_CA, B) \
   SR_BV(V_AT, B) SR_BV(V_TA, B) SR_BV(V_XX, B) SR_BV(V_XC, B) SR_BV(V_CX, B)
 
 // Run one tree's program over one row tile; the result is left in acc.
-template <typename T, int R, int D>
+template <typename T, int R, int D, int SET>
 __device__ __forceinline__ void run_program(const Ins<T>* __restrict__ p,
                                             const T* __restrict__ sXt, int rs,
                                             int lane, T (&acc)[R], T& chk) {

@@ -44,7 +44,8 @@ struct EvalArgs {
 // Geometry of one evaluation launch, chosen by plan_eval().
 struct EvalPlan {
   int R;          // rows per lane per instruction
-  int D;          // stack slots of the kernel variant (4 or 16)
+  int D;          // stack slots of the kernel variant (kShallowSlots or kMaxSlots)
+  int opset;      // OpSet the kernel variant is compiled for
   int tile;       // rows per tile = 64 * R
   int ntiles;
   int rows_wg;    // rows per workgroup
@@ -55,7 +56,7 @@ struct EvalPlan {
 
 // Choose the geometry for `nlist` trees over `n` rows; returns false when the
 // row tile of this feature count does not fit in LDS.
-bool plan_eval(int dtype, bool deep, int mode, bool weighted, int nfeat,
+bool plan_eval(int dtype, bool deep, int opset, int mode, bool weighted, int nfeat,
                int64_t n, int nlist, EvalPlan* plan);
 // Same, for explicit R / D / LDS arrays / partial bytes per tree slot.
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n,

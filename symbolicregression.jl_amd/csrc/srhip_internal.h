@@ -93,6 +93,23 @@ constexpr bool uop_lossy(int op) {
          op == SRHIP_UOP_INV;
 }
 
+// ---- operator sets -------------------------------------------------------------
+// A kernel variant compiled only with the dispatch cases of a small operator
+// set has a shallower dispatch branch tree. The host picks the smallest set
+// that contains every operator of the batch.
+enum OpSet : int { OPSET_BASIC = 0, OPSET_FULL = 1 };
+constexpr uint32_t kBasicBops = (1u << SRHIP_BOP_ADD) | (1u << SRHIP_BOP_SUB) | (1u << SRHIP_BOP_MUL) |
+                                (1u << SRHIP_BOP_DIV);
+constexpr uint32_t kBasicUops = (1u << SRHIP_UOP_NEG) | (1u << SRHIP_UOP_SQUARE) | (1u << SRHIP_UOP_CUBE) |
+                                (1u << SRHIP_UOP_EXP) | (1u << SRHIP_UOP_ABS) | (1u << SRHIP_UOP_LOG) |
+                                (1u << SRHIP_UOP_SQRT) | (1u << SRHIP_UOP_SIN) | (1u << SRHIP_UOP_COS);
+constexpr bool opset_has_bop(int set, int op) { return set == OPSET_FULL || ((kBasicBops >> op) & 1u); }
+constexpr bool opset_has_uop(int set, int op) { return set == OPSET_FULL || ((kBasicUops >> op) & 1u); }
+
+// Stack slots of the ordinary kernel variant; trees needing more (rare:
+// < 0.01 % of random trees at maxsize 30) run in the 16-slot variant.
+constexpr int kShallowSlots = 2;
+
 // Rough VALU cost per row of each operator (f32), used to balance trees over
 // workgroups. Not a correctness input.
 constexpr int bop_cost(int op) {

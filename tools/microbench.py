@@ -20,6 +20,7 @@ configs = {
     "+-*|cos": (["+", "-", "*"], ["cos"]),
     "+-*|exp": (["+", "-", "*"], ["exp"]),
     "cfg2 +-*/|cos,exp": (["+", "-", "*", "/"], ["cos", "exp"]),
+    "full +-*/|cos,exp,tanh": (["+", "-", "*", "/"], ["cos", "exp", "tanh"]),
 }
 res = {}
 for name, (b, u) in configs.items():
