@@ -34,7 +34,12 @@ import numpy as np
 ROOT = Path(__file__).resolve().parent
 sys.path.insert(0, str(ROOT / "symbolicregression.jl_amd"))
 
-PEAK_VALU_LANE_OPS = 256 * 64 * 2.4e9  # 39.3e12 non-packed FP32 lane-ops/s
+# FP32 VALU peak in lane-ops/s: 256 CUs x 4 SIMD-32 x 32 lanes/clk x 2.4 GHz = 78.6e12
+# (a wave64 v_fma_f32 issues in 2 cycles on a SIMD-32, MI355X_MICROARCH.md; x2 for
+# FMA = the 157.3 TFLOPS spec). SURVEY.md §8d's 39.3e12 assumed SIMD-16; the
+# microarchitecture guide's measured figure is used here.
+PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
+METRIC = "node\u00b7row evals/sec (Float32, 4096 trees\u00d71M rows) at 1/2/4/8 GPUs; % VALU peak"
 HBM_PEAK_GBS = 8000.0
 
 
@@ -150,8 +155,10 @@ def main():
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())
-            roof["traffic"] = pm.get("hbm_bytes_per_launch")
-            roof["valu_busy"] = pm.get("valu_busy")
+            if pm.get("kernel") and pm.get("workload") == "config#2":
+                roof["traffic"] = pm.get("hbm_bytes_per_launch")
+                roof["valu_busy"] = pm.get("valu_busy")
+                roof["pmc_source"] = "profiles/current_pmc_summary.json (rocprofv3 --pmc passes of this bench)"
         except Exception:
             pass
 
@@ -183,8 +190,7 @@ def main():
         }
 
     out = {
-        "metric": "node·row evals/sec (Float32, 4096 trees×1M rows)" if T == np.float32
-        else "node·row evals/sec (Float64)",
+        "metric": METRIC if T == np.float32 else "node·row evals/sec (Float64)",
         "value": value,
         "unit": "node·row/s",
         "n_gpus": world,

@@ -106,7 +106,7 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
     const int s = i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
     if (s >= a.nlist) continue;
     const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
-    const Ins<T>* p = a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[t]);
+    CIns<T>* p = const_prog(a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[t]));
     T lsum = T(0), chk = T(0);
     for (int tl = 0; tl < nt_valid; ++tl) {
       const T* sXt = sX + tl * TILE;

@@ -102,7 +102,7 @@ __device__ __forceinline__ void bin_grad(Dual<T, R, G>& a, const Dual<T, R, G>& 
 // Run one tree's program over one row tile with tangents for constants
 // g0 .. g0+G-1; the result is left in a.
 template <typename T, int R, int D, int G>
-__device__ __forceinline__ void run_program_grad(const Ins<T>* __restrict__ p,
+__device__ __forceinline__ void run_program_grad(CIns<T>* __restrict__ p,
                                                  const T* __restrict__ sXt, int rs, int lane,
                                                  int g0, Dual<T, R, G>& a, T& chk) {
   Dual<T, R, G> t;
@@ -114,9 +114,9 @@ __device__ __forceinline__ void run_program_grad(const Ins<T>* __restrict__ p,
 #pragma unroll
     for (int j = 0; j < G; ++j) { a.d[j][r] = T(0); t.d[j][r] = T(0); }
   }
-  Ins<T> cur = p[0];
+  Ins<T> cur = fetch<T>(p);
   for (;;) {
-    const Ins<T> nxt = p[1];
+    const Ins<T> nxt = fetch<T>(p + 1);
     const uint32_t code = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.code);
     const T imm = uni(cur.imm);
     const int f = (int)(code >> 16);

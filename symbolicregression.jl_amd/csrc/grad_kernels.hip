@@ -65,7 +65,7 @@ __global__ void __launch_bounds__(256) grad_kernel(GradArgs<T> a) {
     const int item = __builtin_amdgcn_readfirstlane(a.items[s]);
     const int t = item & 0xffffff;
     const int g0 = (item >> 24) * G;
-    const Ins<T>* p = a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[t]);
+    CIns<T>* p = const_prog(a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[t]));
     const int cbase = __builtin_amdgcn_readfirstlane(a.const_off[t]);
     const int nc = __builtin_amdgcn_readfirstlane(a.const_off[t + 1]) - cbase;
     T acc[S];

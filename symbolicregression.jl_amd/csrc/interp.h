@@ -17,6 +17,23 @@ namespace interp {
 using dev::bop;
 using dev::uop;
 
+// Programs are read through the constant address space so that the uniform
+// instruction fetch is a scalar load (s_load) into SGPRs: no vector-memory
+// round trip and no readfirstlane on the dispatch path.
+template <typename T>
+using CIns = const __attribute__((address_space(4))) Ins<T>;
+template <typename T>
+__device__ __forceinline__ CIns<T>* const_prog(const Ins<T>* p) {
+  return (CIns<T>*)(p);
+}
+template <typename T>
+__device__ __forceinline__ Ins<T> fetch(CIns<T>* p) {
+  Ins<T> i;
+  i.code = p->code;
+  i.imm = p->imm;
+  return i;
+}
+
 template <typename T>
 struct V16;
 template <>
@@ -208,16 +225,16 @@ __device__ __forceinline__ void bin_apply(T (&acc)[R], const T (&tmp)[R],
 
 // Run one tree's program over one row tile; the result is left in acc.
 template <typename T, int R, int D, int SET>
-__device__ __forceinline__ void run_program(const Ins<T>* __restrict__ p,
+__device__ __forceinline__ void run_program(CIns<T>* __restrict__ p,
                                             const T* __restrict__ sXt, int rs,
                                             int lane, T (&acc)[R], T& chk) {
   T tmp[R];
   T slot[D][R];
 #pragma unroll
   for (int r = 0; r < R; ++r) { acc[r] = T(0); tmp[r] = T(0); }
-  Ins<T> cur = p[0];
+  Ins<T> cur = fetch<T>(p);
   for (;;) {
-    const Ins<T> nxt = p[1];  // prefetch; every program ends with OP_END + slack
+    const Ins<T> nxt = fetch<T>(p + 1);  // prefetch; every program ends with OP_END + slack
     const uint32_t code = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.code);
     const T imm = uni(cur.imm);
     const int f = (int)(code >> 16);

@@ -129,7 +129,8 @@ bool plan_eval(int dtype, bool deep, int opset, int mode, bool weighted, int nfe
                int nlist, EvalPlan* p) {
   const size_t esz = dtype == SRHIP_F32 ? 4 : 8;
   const int narr = nfeat + (mode == MODE_LOSS ? (weighted ? 2 : 1) : 0);
-  const bool ok = plan_geometry(esz, variant_R(dtype, deep), deep ? kMaxSlots : kShallowSlots, narr,
+  const int R = variant_R(dtype, deep);
+  const bool ok = plan_geometry(esz, R, deep ? kMaxSlots : kShallowSlots, narr,
                                 2 * esz, n, nlist, p);
   p->opset = deep ? OPSET_FULL : opset;  // the deep variant is built for the full set only
   return ok;

@@ -30,9 +30,16 @@ def _perturbed(flat, X, T, k, rng):
 def output_spread(trees, options, X, T, nperturb=3, seed=0):
     """Per (tree, row): max |f(X', c') - f(X, c)| over ulp-scale perturbations,
     evaluated in float64 by the oracle."""
-    rng = np.random.default_rng(seed)
     flat = srhip.flatten(trees, options, dtype=np.float64)
     flat.consts = srhip.flatten(trees, options, dtype=T).consts.astype(np.float64)
+    return output_spread_flat(flat, X, T, nperturb, seed)
+
+
+def output_spread_flat(flat, X, T, nperturb=3, seed=0):
+    """output_spread for an already flattened batch (constants rounded to T)."""
+    rng = np.random.default_rng(seed)
+    flat = srhip.node.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off,
+                                np.asarray(flat.consts, dtype=np.float64), flat.nodes)
     base, _ = oracle.eval_trees(flat, X.astype(np.float64), dtype=np.float64)
     spread = np.zeros_like(base)
     with np.errstate(invalid="ignore", over="ignore"):
@@ -46,10 +53,17 @@ def output_spread(trees, options, X, T, nperturb=3, seed=0):
 
 def loss_spread(trees, options, X, y, w, T, nperturb=3, seed=0, loss=None):
     """Per tree: max |Σ w ℓ (perturbed) - Σ w ℓ| (float64 oracle)."""
-    rng = np.random.default_rng(seed)
     loss = loss or options.elementwise_loss
     flat = srhip.flatten(trees, options, dtype=np.float64)
     flat.consts = srhip.flatten(trees, options, dtype=T).consts.astype(np.float64)
+    return loss_spread_flat(flat, X, y, w, T, loss, nperturb, seed)
+
+
+def loss_spread_flat(flat, X, y, w, T, loss, nperturb=3, seed=0):
+    """loss_spread for an already flattened batch (constants rounded to T)."""
+    rng = np.random.default_rng(seed)
+    flat = srhip.node.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off,
+                                np.asarray(flat.consts, dtype=np.float64), flat.nodes)
     y64 = y.astype(np.float64)
     w64 = None if w is None else w.astype(np.float64)
     base, _, _ = oracle.eval_loss_batch(flat, X.astype(np.float64), y64, w64, loss.kind, loss.params,

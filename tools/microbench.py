@@ -9,6 +9,7 @@ import srhip
 from srhip import constants as K
 
 rows = int(sys.argv[1]) if len(sys.argv) > 1 else 1_000_000
+only = sys.argv[2] if len(sys.argv) > 2 else None  # run one config (for PMC passes)
 ctx = srhip.get_context(0)
 X = np.random.default_rng(1).standard_normal((5, rows)).astype(np.float32)
 y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(np.float32)
@@ -24,6 +25,8 @@ configs = {
 }
 res = {}
 for name, (b, u) in configs.items():
+    if only and name != only:
+        continue
     o = srhip.Options(binary_operators=b, unary_operators=u)
     trees = srhip.random_population(4096, o, 5, np.float32, seed=1000)
     prog = srhip.Program(ctx, srhip.flatten(trees, o, np.float32), np.float32)
