@@ -233,7 +233,7 @@ void build_program(srhip_program* p) {
   std::vector<int32_t> a, b;
   for (int t = 0; t < p->ntrees; ++t) {
     if (cb.tree_off[t] < 0) continue;
-    (cb.need[t] <= kShallowSlots ? a : b).push_back(t);
+    (cb.need[t] <= kShallowSlots && cb.len[t] <= kVProgMax ? a : b).push_back(t);
   }
   auto by_cost = [&](int32_t x, int32_t y) {
     return cb.cost[x] != cb.cost[y] ? cb.cost[x] > cb.cost[y] : x < y;

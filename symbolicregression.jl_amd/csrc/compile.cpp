@@ -95,17 +95,22 @@ struct TreeCompiler {
     return x.deg == 2 && nonroot_const_nonfinite(x.r);
   }
 
+  uint32_t need_x(int opc) const {
+    if (grad) return 0;
+    const bool nx = opc == OP_LDX || (opc >= OP_BIN0 && variant_needs_x((opc - OP_BIN0) / SRHIP_NUM_BOPS));
+    return nx ? kNeedX : 0;
+  }
   void put(int opc, int slot, int feat, T imm) {
     Ins<T> ins;
     std::memset(&ins, 0, sizeof(ins));
-    ins.code = make_code(opc, slot, feat);
+    ins.code = make_code(opc, slot, feat) | need_x(opc);
     ins.imm = imm;
     out->push_back(ins);
   }
   void put_feat2(int opc, int f, int g) {
     Ins<T> ins;
     std::memset(&ins, 0, sizeof(ins));
-    ins.code = make_code(opc, 0, f);
+    ins.code = make_code(opc, 0, f) | need_x(opc);
     if constexpr (sizeof(T) == 4) {
       uint32_t gg = (uint32_t)g;
       std::memcpy(&ins.imm, &gg, 4);
@@ -203,6 +208,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
   cb.static_fail.assign(nt, 0);
   cb.fail_if_rows.assign(nt, 0);
   cb.need.assign(nt, 0);
+  cb.len.assign(nt, 0);
   cb.cost.assign(nt, 0);
   const T* consts = static_cast<const T*>(trees.consts);
   TreeCompiler<T> tc;
@@ -268,6 +274,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
       cb.tree_off[t] = (int32_t)cb.code.size();
       tc.emit(root, 0);
       tc.put(OP_END, 0, 0, T(0));
+      cb.len[t] = (int32_t)cb.code.size() - cb.tree_off[t];
       continue;
     }
     const bool root_is_leaf = tc.nd[root].deg == 0;
@@ -286,10 +293,12 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
     cb.tree_off[t] = (int32_t)cb.code.size();
     tc.emit(root, 0);
     tc.put(OP_END, 0, 0, T(0));
+    cb.len[t] = (int32_t)cb.code.size() - cb.tree_off[t];
   }
   cb.max_feature = tc.max_feat;
-  // trailing OP_END: the kernel prefetches one instruction past each END
-  tc.put(OP_END, 0, 0, T(0));
+  // trailing OP_ENDs: the kernels prefetch one instruction past each END and
+  // the VGPR-resident-program variant loads kVProgMax + 1 instructions per tree
+  for (int i = 0; i <= kVProgMax; ++i) tc.put(OP_END, 0, 0, T(0));
   return cb;
 }
 

@@ -23,6 +23,7 @@ struct CompiledBatch {
   std::vector<uint8_t> static_fail;  // fails for every row count (constant checks)
   std::vector<uint8_t> fail_if_rows; // root is a non-finite constant: fails iff n > 0
   std::vector<int32_t> need;         // stack slots used
+  std::vector<int32_t> len;          // program length in instructions (END included)
   std::vector<int32_t> cost;         // VALU cost estimate per row
   int max_feature = -1;              // largest feature index referenced
   int64_t total_nodes = 0;

@@ -102,16 +102,34 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
   // wave-uniform schedule (no atomics, no divergent loop exit).
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nwaves = (int)(blockDim.x >> 6);
+  // The shallow variant keeps each tree's program in VGPRs (run_program_v);
+  // the next tree's program is loaded while the current one runs.
+  constexpr bool VP = false;  // (D == kShallowSlots);
+  auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
+  auto prog_of = [&](int s) {
+    return a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[__builtin_amdgcn_readfirstlane(a.list[s])]);
+  };
+  VProg<T> vnext;
+  if constexpr (VP) {
+    if (wave < a.tpb && slot_of(wave) < a.nlist) vnext.load(prog_of(slot_of(wave)), lane);
+  }
   for (int i = wave; i < a.tpb; i += nwaves) {
-    const int s = i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
-    if (s >= a.nlist) continue;
+    const int s = slot_of(i);
+    if (s >= a.nlist) break;  // slot_of is increasing in i
     const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
+    VProg<T> vp;
+    if constexpr (VP) {
+      vp = vnext;
+      const int s2 = slot_of(i + nwaves);
+      if (i + nwaves < a.tpb && s2 < a.nlist) vnext.load(prog_of(s2), lane);
+    }
     CIns<T>* p = const_prog(a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[t]));
     T lsum = T(0), chk = T(0);
     for (int tl = 0; tl < nt_valid; ++tl) {
       const T* sXt = sX + tl * TILE;
       T acc[R];
-      run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
+      if constexpr (VP) run_program_v<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
+      else run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
 #pragma unroll
       for (int r = 0; r < R; ++r) chk = mark(acc[r], chk);  // root value
       if constexpr (MODE == MODE_OUT) {

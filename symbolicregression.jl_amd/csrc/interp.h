@@ -155,40 +155,33 @@ __device__ __forceinline__ void un_apply(T (&acc)[R], T& chk) {
   }
 }
 
+// x: the instruction's X operand (feature f), already in registers — loaded
+// by the driver (prefetched one instruction ahead by run_program_v).
 template <int V, int B, typename T, int R>
-__device__ __forceinline__ void bin_apply(T (&acc)[R], const T (&tmp)[R],
+__device__ __forceinline__ void bin_apply(T (&acc)[R], const T (&tmp)[R], const T (&x)[R],
                                           const T* __restrict__ sXt, int rs,
-                                          int lane, int f, T imm, T& chk) {
+                                          int lane, T imm, T& chk) {
   constexpr bool LL = bop_lossy_lhs(B);
   constexpr bool LR = bop_lossy_rhs(B);
-  if constexpr (V == V_AX || V == V_XA || V == V_XX || V == V_XC || V == V_CX) {
-    T x[R];
-    lds_rows<T, R>(sXt + f * rs, lane, x);
-    if constexpr (V == V_XX) {
-      T x2[R];
-      lds_rows<T, R>(sXt + imm_int(imm) * rs, lane, x2);
+  if constexpr (V == V_XX) {
+    T x2[R];
+    lds_rows<T, R>(sXt + imm_int(imm) * rs, lane, x2);
 #pragma unroll
-      for (int r = 0; r < R; ++r) acc[r] = bop<B>(x[r], x2[r]);
-    } else {
-#pragma unroll
-      for (int r = 0; r < R; ++r) {
-        if constexpr (V == V_AX) {
-          if constexpr (LL) chk = mark(acc[r], chk);
-          acc[r] = bop<B>(acc[r], x[r]);
-        } else if constexpr (V == V_XA) {
-          if constexpr (LR) chk = mark(acc[r], chk);
-          acc[r] = bop<B>(x[r], acc[r]);
-        } else if constexpr (V == V_XC) {
-          acc[r] = bop<B>(x[r], imm);
-        } else {
-          acc[r] = bop<B>(imm, x[r]);
-        }
-      }
-    }
+    for (int r = 0; r < R; ++r) acc[r] = bop<B>(x[r], x2[r]);
   } else {
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      if constexpr (V == V_AC) {
+      if constexpr (V == V_AX) {
+        if constexpr (LL) chk = mark(acc[r], chk);
+        acc[r] = bop<B>(acc[r], x[r]);
+      } else if constexpr (V == V_XA) {
+        if constexpr (LR) chk = mark(acc[r], chk);
+        acc[r] = bop<B>(x[r], acc[r]);
+      } else if constexpr (V == V_XC) {
+        acc[r] = bop<B>(x[r], imm);
+      } else if constexpr (V == V_CX) {
+        acc[r] = bop<B>(imm, x[r]);
+      } else if constexpr (V == V_AC) {
         if constexpr (LL) chk = mark(acc[r], chk);
         acc[r] = bop<B>(acc[r], imm);
       } else if constexpr (V == V_CA) {
@@ -219,45 +212,111 @@ __device__ __forceinline__ void bin_apply(T (&acc)[R], const T (&tmp)[R],
 #define SR_UN(U) \
   case OP_UN0 + U: if constexpr (opset_has_uop(SET, U)) un_apply<U, T, R>(acc, chk); break;
 #define SR_BV(V, B) \
-  case bin_opcode(V, B): if constexpr (opset_has_bop(SET, B)) bin_apply<V, B, T, R>(acc, tmp, sXt, rs, lane, f, imm, chk); break;
+  case bin_opcode(V, B): if constexpr (opset_has_bop(SET, B)) bin_apply<V, B, T, R>(acc, tmp, x, sXt, rs, lane, imm, chk); break;
 #define SR_BIN(B) SR_BV(V_AX, B) SR_BV(V_XA, B) SR_BV(V_AC, B) SR_BV(V_CA, B) \
   SR_BV(V_AT, B) SR_BV(V_TA, B) SR_BV(V_XX, B) SR_BV(V_XC, B) SR_BV(V_CX, B)
 
-// Run one tree's program over one row tile; the result is left in acc.
+// Execute one instruction (wave-uniform `code`, `imm`); returns false at END.
+template <typename T, int R, int D, int SET>
+__device__ __forceinline__ bool exec_ins(uint32_t code, T imm, T (&acc)[R], T (&tmp)[R],
+                                         T (&slot)[D][R], const T (&x)[R],
+                                         const T* __restrict__ sXt, int rs, int lane, T& chk) {
+  switch (code & 0xffu) {
+    case OP_END: return false;
+    case OP_LDX: SR_UNROLL for (int r = 0; r < R; ++r) acc[r] = x[r]; break;
+    case OP_LDC: SR_UNROLL for (int r = 0; r < R; ++r) acc[r] = imm; break;
+    SR_PUSH(0) SR_PUSH(1) SR_PUSH(2) SR_PUSH(3) SR_PUSH(4) SR_PUSH(5) SR_PUSH(6) SR_PUSH(7)
+    SR_PUSH(8) SR_PUSH(9) SR_PUSH(10) SR_PUSH(11) SR_PUSH(12) SR_PUSH(13) SR_PUSH(14) SR_PUSH(15)
+    SR_POP(0) SR_POP(1) SR_POP(2) SR_POP(3) SR_POP(4) SR_POP(5) SR_POP(6) SR_POP(7)
+    SR_POP(8) SR_POP(9) SR_POP(10) SR_POP(11) SR_POP(12) SR_POP(13) SR_POP(14) SR_POP(15)
+    SR_UN(0) SR_UN(1) SR_UN(2) SR_UN(3) SR_UN(4) SR_UN(5) SR_UN(6) SR_UN(7) SR_UN(8) SR_UN(9)
+    SR_UN(10) SR_UN(11) SR_UN(12) SR_UN(13) SR_UN(14) SR_UN(15) SR_UN(16) SR_UN(17) SR_UN(18)
+    SR_UN(19) SR_UN(20) SR_UN(21) SR_UN(22) SR_UN(23) SR_UN(24) SR_UN(25) SR_UN(26) SR_UN(27)
+    SR_UN(28)
+    SR_BIN(0) SR_BIN(1) SR_BIN(2) SR_BIN(3) SR_BIN(4) SR_BIN(5) SR_BIN(6) SR_BIN(7) SR_BIN(8)
+    SR_BIN(9) SR_BIN(10)
+    default: break;
+  }
+  return true;
+}
+
+// Driver 1 (any program length): instructions fetched with scalar loads, one
+// ahead; the X operand is read from LDS right before the instruction.
 template <typename T, int R, int D, int SET>
 __device__ __forceinline__ void run_program(CIns<T>* __restrict__ p,
                                             const T* __restrict__ sXt, int rs,
                                             int lane, T (&acc)[R], T& chk) {
-  T tmp[R];
+  T tmp[R], x[R];
   T slot[D][R];
 #pragma unroll
-  for (int r = 0; r < R; ++r) { acc[r] = T(0); tmp[r] = T(0); }
+  for (int r = 0; r < R; ++r) { acc[r] = T(0); tmp[r] = T(0); x[r] = T(0); }
   Ins<T> cur = fetch<T>(p);
   for (;;) {
     const Ins<T> nxt = fetch<T>(p + 1);  // prefetch; every program ends with OP_END + slack
     const uint32_t code = (uint32_t)__builtin_amdgcn_readfirstlane((int)cur.code);
     const T imm = uni(cur.imm);
-    const int f = (int)(code >> 16);
-    switch (code & 0xffu) {
-      case OP_END: return;
-      case OP_LDX: lds_rows<T, R>(sXt + f * rs, lane, acc); break;
-      case OP_LDC:
-        SR_UNROLL for (int r = 0; r < R; ++r) acc[r] = imm;
-        break;
-      SR_PUSH(0) SR_PUSH(1) SR_PUSH(2) SR_PUSH(3) SR_PUSH(4) SR_PUSH(5) SR_PUSH(6) SR_PUSH(7)
-      SR_PUSH(8) SR_PUSH(9) SR_PUSH(10) SR_PUSH(11) SR_PUSH(12) SR_PUSH(13) SR_PUSH(14) SR_PUSH(15)
-      SR_POP(0) SR_POP(1) SR_POP(2) SR_POP(3) SR_POP(4) SR_POP(5) SR_POP(6) SR_POP(7)
-      SR_POP(8) SR_POP(9) SR_POP(10) SR_POP(11) SR_POP(12) SR_POP(13) SR_POP(14) SR_POP(15)
-      SR_UN(0) SR_UN(1) SR_UN(2) SR_UN(3) SR_UN(4) SR_UN(5) SR_UN(6) SR_UN(7) SR_UN(8) SR_UN(9)
-      SR_UN(10) SR_UN(11) SR_UN(12) SR_UN(13) SR_UN(14) SR_UN(15) SR_UN(16) SR_UN(17) SR_UN(18)
-      SR_UN(19) SR_UN(20) SR_UN(21) SR_UN(22) SR_UN(23) SR_UN(24) SR_UN(25) SR_UN(26) SR_UN(27)
-      SR_UN(28)
-      SR_BIN(0) SR_BIN(1) SR_BIN(2) SR_BIN(3) SR_BIN(4) SR_BIN(5) SR_BIN(6) SR_BIN(7) SR_BIN(8)
-      SR_BIN(9) SR_BIN(10)
-      default: break;
-    }
+    if (code & kNeedX) lds_rows<T, R>(sXt + (int)(code >> 16) * rs, lane, x);
+    if (!exec_ins<T, R, D, SET>(code, imm, acc, tmp, slot, x, sXt, rs, lane, chk)) return;
     cur = nxt;
     ++p;
+  }
+}
+
+// A program of at most kVProgMax instructions held in VGPRs: lane j holds
+// instruction j (code word and immediate). Loaded once per tree, reused for
+// every row tile, read with v_readlane (no memory round trip per dispatch).
+template <typename T>
+struct VProg;
+template <>
+struct VProg<float> {
+  uint32_t code, imm;
+  __device__ __forceinline__ void load(const Ins<float>* p, int lane) {
+    const uint2 v = *reinterpret_cast<const uint2*>(p + lane);
+    code = v.x; imm = v.y;
+  }
+  __device__ __forceinline__ uint32_t code_at(int pc) const {
+    return (uint32_t)__builtin_amdgcn_readlane((int)code, pc);
+  }
+  __device__ __forceinline__ float imm_at(int pc) const {
+    return __int_as_float(__builtin_amdgcn_readlane((int)imm, pc));
+  }
+};
+template <>
+struct VProg<double> {
+  uint32_t code, lo, hi;
+  __device__ __forceinline__ void load(const Ins<double>* p, int lane) {
+    const uint4 v = *reinterpret_cast<const uint4*>(p + lane);
+    code = v.x; lo = v.z; hi = v.w;
+  }
+  __device__ __forceinline__ uint32_t code_at(int pc) const {
+    return (uint32_t)__builtin_amdgcn_readlane((int)code, pc);
+  }
+  __device__ __forceinline__ double imm_at(int pc) const {
+    const uint32_t l = (uint32_t)__builtin_amdgcn_readlane((int)lo, pc);
+    const uint32_t h = (uint32_t)__builtin_amdgcn_readlane((int)hi, pc);
+    return __longlong_as_double((long long)(((uint64_t)h << 32) | l));
+  }
+};
+
+// Driver 2 (programs of at most kVProgMax instructions): the program is in
+// VGPRs and the X operand of the NEXT instruction is read from LDS while the
+// dispatch of the current one finishes, so neither the fetch nor the LDS read
+// sits on the dispatch path.
+template <typename T, int R, int D, int SET>
+__device__ __forceinline__ void run_program_v(const VProg<T>& vp, const T* __restrict__ sXt, int rs,
+                                              int lane, T (&acc)[R], T& chk) {
+  T tmp[R], x[R];
+  T slot[D][R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) { acc[r] = T(0); tmp[r] = T(0); }
+  uint32_t code = vp.code_at(0);
+  lds_rows<T, R>(sXt + (int)(code >> 16) * rs, lane, x);
+  for (int pc = 0;; ++pc) {
+    const uint32_t ncode = vp.code_at(pc + 1);
+    const T imm = vp.imm_at(pc);
+    if (!exec_ins<T, R, D, SET>(code, imm, acc, tmp, slot, x, sXt, rs, lane, chk)) return;
+    if (ncode & kNeedX) lds_rows<T, R>(sXt + (int)(ncode >> 16) * rs, lane, x);
+    code = ncode;
   }
 }
 static_assert(SRHIP_NUM_UOPS == 29 && SRHIP_NUM_BOPS == 11, "update the case lists");

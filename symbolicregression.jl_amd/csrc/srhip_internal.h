@@ -51,10 +51,21 @@ constexpr int bin_opcode(int variant, int bop) {
   return OP_BIN0 + variant * SRHIP_NUM_BOPS + bop;
 }
 
-// code word: [7:0] opcode, [15:8] slot index, [31:16] feature index
+// code word: [7:0] opcode, [15:8] slot index, [31:16] feature index.
+// Evaluation programs set bit 15 (kNeedX) on instructions with an X[f]
+// operand (LDX and the AX/XA/XX/XC/CX variants): the kernel reads X[f] from
+// LDS ahead of the dispatch. Gradient programs use all 8 slot bits for
+// constant indices and never set it.
+constexpr uint32_t kNeedX = 1u << 15;
 constexpr uint32_t make_code(int opc, int slot, int feat) {
   return (uint32_t)opc | ((uint32_t)slot << 8) | ((uint32_t)feat << 16);
 }
+constexpr bool variant_needs_x(int v) {
+  return v == V_AX || v == V_XA || v == V_XX || v == V_XC || v == V_CX;
+}
+// Longest program (END included) of the VGPR-resident-program kernel
+// variant: one instruction per lane, and the dispatch reads one ahead.
+constexpr int kVProgMax = 63;
 
 template <typename T>
 struct Ins;
