@@ -3,13 +3,17 @@
 //   R = 4 rows per lane, kMaxSlots stack slots (deep trees), full operator set
 #include "eval_kernel.h"
 
+#ifndef SR_R32
+#define SR_R32 8
+#endif
+
 namespace srhip {
 
 template <>
 hipError_t launch_eval<float>(const EvalPlan& plan, const EvalArgs<float>& a, int mode, hipStream_t stream) {
   if (plan.D == kMaxSlots) return launch_rd<float, 4, kMaxSlots, OPSET_FULL>(plan, a, mode, stream);
-  if (plan.opset == OPSET_BASIC) return launch_rd<float, 8, kShallowSlots, OPSET_BASIC>(plan, a, mode, stream);
-  return launch_rd<float, 8, kShallowSlots, OPSET_FULL>(plan, a, mode, stream);
+  if (plan.opset == OPSET_BASIC) return launch_rd<float, SR_R32, kShallowSlots, OPSET_BASIC>(plan, a, mode, stream);
+  return launch_rd<float, SR_R32, kShallowSlots, OPSET_FULL>(plan, a, mode, stream);
 }
 
 }  // namespace srhip

@@ -20,6 +20,12 @@
 #include "interp.h"
 #include "kernels.h"
 
+// Experimental switches (make EXTRA=-D...): SR_VP selects the driver of the
+// shallow variant (0: scalar-load fetch, 1/2: VGPR-resident program).
+#ifndef SR_VP
+#define SR_VP 0
+#endif
+
 namespace srhip {
 namespace {
 
@@ -60,8 +66,13 @@ __device__ __forceinline__ T tile_loss_any(int lk, const T (&acc)[R], const T (&
   }
 }
 
+#ifdef SR_WPE
+#define SR_WPE_ATTR __attribute__((amdgpu_waves_per_eu(SR_WPE)))
+#else
+#define SR_WPE_ATTR
+#endif
 template <typename T, int R, int D, int SET, int MODE, bool W>
-__global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
+__global__ void __launch_bounds__(256) SR_WPE_ATTR eval_kernel(EvalArgs<T> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int TILE = 64 * R;
   using V = typename V16<T>::type;
@@ -104,7 +115,7 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
   const int nwaves = (int)(blockDim.x >> 6);
   // The shallow variant keeps each tree's program in VGPRs (run_program_v);
   // the next tree's program is loaded while the current one runs.
-  constexpr bool VP = false;  // (D == kShallowSlots);
+  constexpr bool VP = SR_VP != 0 && D == kShallowSlots;
   auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
   auto prog_of = [&](int s) {
     return a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[__builtin_amdgcn_readfirstlane(a.list[s])]);
@@ -128,7 +139,8 @@ __global__ void __launch_bounds__(256) eval_kernel(EvalArgs<T> a) {
     for (int tl = 0; tl < nt_valid; ++tl) {
       const T* sXt = sX + tl * TILE;
       T acc[R];
-      if constexpr (VP) run_program_v<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
+      if constexpr (VP && SR_VP == 2) run_program_v2<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
+      else if constexpr (VP) run_program_v<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
       else run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
 #pragma unroll
       for (int r = 0; r < R; ++r) chk = mark(acc[r], chk);  // root value

@@ -319,6 +319,27 @@ __device__ __forceinline__ void run_program_v(const VProg<T>& vp, const T* __res
     code = ncode;
   }
 }
+// Driver 3: as driver 2, unrolled by two with ping-pong X buffers so the X
+// operand of instruction i+1 is read from LDS before instruction i executes
+// (the LDS latency overlaps a whole instruction, not only the dispatch).
+template <typename T, int R, int D, int SET>
+__device__ __forceinline__ void run_program_v2(const VProg<T>& vp, const T* __restrict__ sXt, int rs,
+                                               int lane, T (&acc)[R], T& chk) {
+  T tmp[R], xa[R], xb[R];
+  T slot[D][R];
+#pragma unroll
+  for (int r = 0; r < R; ++r) { acc[r] = T(0); tmp[r] = T(0); }
+  uint32_t c0 = vp.code_at(0);
+  if (c0 & kNeedX) lds_rows<T, R>(sXt + (int)(c0 >> 16) * rs, lane, xa);
+  for (int pc = 0;; pc += 2) {
+    const uint32_t c1 = vp.code_at(pc + 1);
+    if (c1 & kNeedX) lds_rows<T, R>(sXt + (int)(c1 >> 16) * rs, lane, xb);
+    if (!exec_ins<T, R, D, SET>(c0, vp.imm_at(pc), acc, tmp, slot, xa, sXt, rs, lane, chk)) return;
+    c0 = vp.code_at(pc + 2);
+    if (c0 & kNeedX) lds_rows<T, R>(sXt + (int)(c0 >> 16) * rs, lane, xa);
+    if (!exec_ins<T, R, D, SET>(c1, vp.imm_at(pc + 1), acc, tmp, slot, xb, sXt, rs, lane, chk)) return;
+  }
+}
 static_assert(SRHIP_NUM_UOPS == 29 && SRHIP_NUM_BOPS == 11, "update the case lists");
 
 }  // namespace interp

@@ -93,8 +93,11 @@ __global__ void gather_rows_kernel(const T* __restrict__ X, const T* __restrict_
 // Kernel variants: (rows per lane R, stack slots D).
 //   f32: (8, kShallowSlots) for ordinary trees, (4, kMaxSlots) for deep ones
 //   f64: (4, kShallowSlots) and (2, kMaxSlots)
+#ifndef SR_R32
+#define SR_R32 8
+#endif
 static inline int variant_R(int dtype, bool deep) {
-  return dtype == SRHIP_F32 ? (deep ? 4 : 8) : (deep ? 2 : 4);
+  return dtype == SRHIP_F32 ? (deep ? 4 : SR_R32) : (deep ? 2 : 4);
 }
 
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n, int nlist,
@@ -106,8 +109,11 @@ bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_
   p->threads = 256;
   const size_t per_tile = (size_t)narr * p->tile * esz;
   const size_t budget = 40 * 1024;
+#ifndef SR_NTMAX
+#define SR_NTMAX 16
+#endif
   int nt = 1;
-  while ((int64_t)nt * 2 * p->tile <= 8192 && per_tile * nt * 2 <= budget &&
+  while (nt * 2 <= SR_NTMAX && (int64_t)nt * 2 * p->tile <= 8192 && per_tile * nt * 2 <= budget &&
          (int64_t)nt * p->tile < n)
     nt *= 2;
   p->ntiles = nt;
