@@ -246,10 +246,19 @@ void build_program(srhip_program* p) {
   list.insert(list.end(), b.begin(), b.end());
   std::vector<int32_t> toff(cb.tree_off);
   for (auto& v : toff) v = std::max(v, 0);
+  // second half of d_list: program offset of every list slot (one load
+  // instead of list -> tree_off when the kernel prefetches the next program)
+  const size_t nl = list.size();
+  list.resize(2 * nl);
+  for (size_t k = 0; k < nl; ++k) list[nl + k] = toff[list[k]];
 
   free_program_device(p);
   hipStream_t s = p->ctx->stream;
-  HIP_CHECK(hipMalloc(&p->d_code, std::max<size_t>(cb.code.size(), 1) * sizeof(Ins<T>)));
+  // +64 instructions of OP_END padding: the VGPR-resident program load reads
+  // 64 instructions from the start of every program
+  const size_t ncode_alloc = cb.code.size() + 64;
+  HIP_CHECK(hipMalloc(&p->d_code, ncode_alloc * sizeof(Ins<T>)));
+  HIP_CHECK(hipMemsetAsync(p->d_code, 0, ncode_alloc * sizeof(Ins<T>), p->ctx->stream));
   HIP_CHECK(hipMalloc((void**)&p->d_tree_off, std::max<size_t>(toff.size(), 1) * sizeof(int32_t)));
   HIP_CHECK(hipMalloc((void**)&p->d_list, std::max<size_t>(list.size(), 1) * sizeof(int32_t)));
   HIP_CHECK(hipMemcpyAsync(p->d_code, cb.code.data(), cb.code.size() * sizeof(Ins<T>), hipMemcpyHostToDevice, s));
@@ -293,6 +302,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.prog = static_cast<const Ins<T>*>(p->d_code);
     a.tree_off = p->d_tree_off;
     a.list = p->d_list + (pass == 0 ? 0 : p->nlist_a);
+    a.list_off = a.list + (p->nlist_a + p->nlist_b);
     a.nlist = nlist;
     a.X = X;
     a.y = y;

@@ -3,9 +3,6 @@
 //   R = 4 rows per lane, kMaxSlots stack slots (deep trees), full operator set
 #include "eval_kernel.h"
 
-#ifndef SR_R32
-#define SR_R32 8
-#endif
 
 namespace srhip {
 

@@ -17,6 +17,8 @@
 #pragma once
 #include <hip/hip_runtime.h>
 
+#include <type_traits>
+
 #include "interp.h"
 #include "kernels.h"
 
@@ -24,6 +26,21 @@
 // shallow variant (0: scalar-load fetch, 1/2: VGPR-resident program).
 #ifndef SR_VP
 #define SR_VP 0
+#endif
+// SR_TI: the threaded interpreter (gen_asm_interp.py) for f32 trees of the
+// BASIC operator set in the shallow kernel; 0 keeps the C++ dispatch only.
+#ifndef SR_TI
+#define SR_TI 0
+#endif
+#ifndef SR_R32
+#define SR_R32 8  // rows per lane of the shallow f32 kernel
+#endif
+#if SR_TI && defined(__HIP_DEVICE_COMPILE__)
+#if SR_R32 == 16
+#include "gen/asm_interp_f32_r16.inc"
+#else
+#include "gen/asm_interp_f32_r8.inc"
+#endif
 #endif
 
 namespace srhip {
@@ -47,6 +64,55 @@ __device__ __forceinline__ T tile_loss(const T (&acc)[R], const T (&yv)[R], cons
     if (e & 1) s1 += l; else s0 += l;
   }
   return s0 + s1;
+}
+
+// One tile of one program through the threaded interpreter block
+// (gen_asm_interp.py). The program is in VGPRs, one instruction per lane, in
+// the form ti_lanes() prepares; `lane_addr` is the LDS byte address of this
+// lane's rows of feature 0 in the tile. Returns false if the block bailed out
+// (an opcode or argument it does not handle); acc/chk are then garbage and
+// the caller re-runs the tile with the C++ interpreter.
+struct TiLanes {
+  uint32_t pt, xo, im, pn;
+};
+template <int R>
+__device__ __forceinline__ bool run_program_ti(const TiLanes& L, uint32_t lane_addr, float (&acc)[R],
+                                               float& chk) {
+#if SR_TI && defined(__HIP_DEVICE_COMPILE__)
+  static_assert(R == SR_TI_R, "threaded block generated for another R");
+  uint32_t bail;
+  const uint32_t pt = L.pt, xo = L.xo, im = L.im, pn = L.pn, lane = lane_addr;
+  asm volatile(SR_TI_TEXT : SR_TI_OUTPUTS(acc, chk, bail) : SR_TI_INPUTS(pt, xo, im, pn, lane)
+               : SR_TI_CLOBBERS);
+  return bail == 0;
+#else
+  (void)L; (void)lane_addr; (void)acc; (void)chk;
+  return false;
+#endif
+}
+
+// Lane j of the threaded block's program registers (c0 = instruction j,
+// c1 = instruction j+1 of the program, as (code, imm) pairs):
+//   pt = table slot of instruction j+1: 4*opcode + 1024*parity, parity = (j+1)&1
+//        (instruction i runs in table i&1: its X operand is in xa for even i);
+//        lane 63 holds instruction 0's slot (table A)
+//   xo = LDS byte offset of instruction j+1's X operand (lane 63: instruction 0's)
+//   im = immediate of instruction j; for (X[f], X[g]) the byte offset of g
+//   pn = j + 1
+// Programs have at most kVProgMax = 63 instructions, so lane 63 is free.
+__device__ __forceinline__ TiLanes ti_lanes(uint2 c0, uint2 c1, int lane, uint32_t rs_bytes) {
+  const uint32_t code0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)c0.x);
+  const bool l63 = lane == 63;
+  const uint32_t cn = l63 ? code0 : c1.x;
+  const uint32_t par = l63 ? 0u : (uint32_t)((lane + 1) & 1);
+  TiLanes L;
+  L.pt = 4u * (cn & 0xffu) + 1024u * par;
+  L.xo = (cn >> 16) * rs_bytes;
+  const uint32_t op = c0.x & 0xffu;
+  const bool xx = op >= (uint32_t)bin_opcode(V_XX, 0) && op < (uint32_t)bin_opcode(V_XX + 1, 0);
+  L.im = xx ? c0.y * rs_bytes : c0.y;
+  L.pn = (uint32_t)lane + 1u;
+  return L;
 }
 
 template <bool W, bool MASK, typename T, int R>
@@ -116,35 +182,61 @@ __global__ void __launch_bounds__(256) SR_WPE_ATTR eval_kernel(EvalArgs<T> a) {
   // The shallow variant keeps each tree's program in VGPRs (run_program_v);
   // the next tree's program is loaded while the current one runs.
   constexpr bool VP = SR_VP != 0 && D == kShallowSlots;
+  constexpr bool TI = SR_TI != 0 && std::is_same<T, float>::value && R == SR_R32 && D == kShallowSlots &&
+                      SET == OPSET_BASIC;
   auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
-  auto prog_of = [&](int s) {
-    return a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[__builtin_amdgcn_readfirstlane(a.list[s])]);
-  };
+  auto prog_of = [&](int s) { return a.prog + __builtin_amdgcn_readfirstlane(a.list_off[s]); };
   VProg<T> vnext;
-  if constexpr (VP) {
-    if (wave < a.tpb && slot_of(wave) < a.nlist) vnext.load(prog_of(slot_of(wave)), lane);
+  // TI: the program in VGPRs (lane j = instruction j; shallow programs have at
+  // most kVProgMax instructions and the code buffer is padded by 64), loaded
+  // one tree ahead so its memory latency overlaps the current tree
+  uint2 tnext0 = make_uint2(0u, 0u), tnext1 = make_uint2(0u, 0u);
+  const uint32_t rs_bytes = (uint32_t)(rows * sizeof(T));
+  if (wave < a.tpb && slot_of(wave) < a.nlist) {
+    if constexpr (VP) vnext.load(prog_of(slot_of(wave)), lane);
+    if constexpr (TI) {
+      tnext0 = reinterpret_cast<const uint2*>(prog_of(slot_of(wave)))[lane];
+      tnext1 = reinterpret_cast<const uint2*>(prog_of(slot_of(wave)))[lane + 1];
+    }
   }
   for (int i = wave; i < a.tpb; i += nwaves) {
     const int s = slot_of(i);
     if (s >= a.nlist) break;  // slot_of is increasing in i
-    const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
+    const int s2 = slot_of(i + nwaves);
+    const bool more = i + nwaves < a.tpb && s2 < a.nlist;
     VProg<T> vp;
     if constexpr (VP) {
       vp = vnext;
-      const int s2 = slot_of(i + nwaves);
-      if (i + nwaves < a.tpb && s2 < a.nlist) vnext.load(prog_of(s2), lane);
+      if (more) vnext.load(prog_of(s2), lane);
     }
-    CIns<T>* p = const_prog(a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[t]));
+    TiLanes tl_prog{};
+    if constexpr (TI) {
+      tl_prog = ti_lanes(tnext0, tnext1, lane, rs_bytes);
+      if (more) {
+        tnext0 = reinterpret_cast<const uint2*>(prog_of(s2))[lane];
+        tnext1 = reinterpret_cast<const uint2*>(prog_of(s2))[lane + 1];
+      }
+    }
+    CIns<T>* p = const_prog(prog_of(s));
     T lsum = T(0), chk = T(0);
     for (int tl = 0; tl < nt_valid; ++tl) {
       const T* sXt = sX + tl * TILE;
       T acc[R];
-      if constexpr (VP && SR_VP == 2) run_program_v2<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
+      if constexpr (TI) {
+        const T chk0 = chk;
+        const uint32_t lds = (uint32_t)reinterpret_cast<uintptr_t>(
+            (const __attribute__((address_space(3))) T*)(sXt)) + (uint32_t)lane * 16u;
+        if (!run_program_ti<R>(tl_prog, lds, acc, chk)) {
+          chk = chk0;
+          run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
+        }
+      } else if constexpr (VP && SR_VP == 2) run_program_v2<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
       else if constexpr (VP) run_program_v<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
       else run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
 #pragma unroll
       for (int r = 0; r < R; ++r) chk = mark(acc[r], chk);  // root value
       if constexpr (MODE == MODE_OUT) {
+        const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
         store_rows<T, R>(a.out + (size_t)t * a.out_stride + row0 + tl * TILE, lane, acc);
       } else {
         T yv[R], wv[R];
@@ -156,11 +248,8 @@ __global__ void __launch_bounds__(256) SR_WPE_ATTR eval_kernel(EvalArgs<T> a) {
           lsum += tile_loss_any<W, true, T, R>(a.loss, acc, yv, wv, lp, lane, last_valid);
       }
     }
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) {
-      lsum += __shfl_xor(lsum, off);
-      chk += __shfl_xor(chk, off);
-    }
+    lsum = wave_sum(lsum);
+    chk = wave_sum(chk);
     if (lane == 0) sPart[i] = Part<T>{lsum, chk};
   }
   __syncthreads();

@@ -1,0 +1,413 @@
+#!/usr/bin/env python3
+"""Generate the direct-threaded interpreter block of the f32 eval kernel.
+
+The C++ interpreter (interp.h) dispatches each program instruction with a
+uniform binary-search branch tree: ~7 compares + 7 branches + ~14 SALU per
+instruction, on a CU whose single scalar unit is shared by its 4 SIMDs. For
+the +,-,*,/ mix that costs more than the VALU work of the instruction (8 rows
+per lane). This script builds a *threaded* interpreter instead:
+
+  * every opcode has a handler; the dispatch is
+        s_lshl/s_and (opcode) -> s_add/s_addc (table slot) -> s_setpc_b64
+    into a table of `s_branch handler` entries: 2 jumps and 5 SALU;
+  * the program lives in two VGPRs (lane j = instruction j, as in
+    run_program_v), read with v_readlane one instruction ahead;
+  * handler BODIES are not hand-written: each one is compiled by hipcc from the
+    same C++ operator code as the C++ interpreter (device_ops.h: bop/uop/mark,
+    fast_sincos_f32) inside a tiny kernel whose interpreter state is pinned to
+    fixed registers with inline-asm constraints; the body is cut out of the
+    compiler's assembly. Arithmetic, instruction order within a row and hazard
+    nops are therefore the compiler's own: results are bit-identical to the
+    C++ interpreter.
+  * anything the threaded block does not handle (operators outside the
+    handled set, |x| > 105615 for sin/cos) "bails": the block returns a flag
+    and the C++ kernel re-runs that (tree, tile) with run_program.
+
+Output: a header defining SR_TI_TEXT (the asm string), SR_TI_CLOBBERS and
+the register map used by eval_kernel.h. Usage:
+    gen_asm_interp.py <hipcc> <out.inc> [R] [extra hipcc flags...]
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+INCLUDE = os.path.join(HERE, "..", "..", "include", "srhip.h")
+
+
+def enums():
+    txt = open(INCLUDE).read()
+    uops = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define SRHIP_UOP_(\w+)\s+(\d+)", txt)}
+    bops = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define SRHIP_BOP_(\w+)\s+(\d+)", txt)}
+    return uops, bops
+
+
+UOPS, BOPS = enums()
+NUM_UOPS, NUM_BOPS = len(UOPS), len(BOPS)
+MAX_SLOTS = 16
+OP_END, OP_LDX, OP_LDC, OP_PUSH0 = 0, 1, 2, 3
+OP_POP0 = OP_PUSH0 + MAX_SLOTS
+OP_UN0 = OP_POP0 + MAX_SLOTS
+OP_BIN0 = OP_UN0 + NUM_UOPS
+VARIANTS = ["AX", "XA", "AC", "CA", "AT", "TA", "XX", "XC", "CX"]
+NUM_OPCODES = OP_BIN0 + len(VARIANTS) * NUM_BOPS
+D = 2  # stack slots of the shallow kernel (kShallowSlots)
+
+# Operators with handlers (the BASIC set of srhip_internal.h).
+H_BOPS = ["ADD", "SUB", "MUL", "DIV"]
+H_UOPS = ["NEG", "SQUARE", "CUBE", "EXP", "ABS", "LOG", "SQRT", "SIN", "COS"]
+LOSSY_UOPS = {"EXP", "TANH", "ATAN", "ERF", "ERFC", "SIGN", "INV"}
+LOSSY_LHS = {"POW", "GREATER", "LOGICAL_OR", "LOGICAL_AND", "MAX", "MIN"}
+LOSSY_RHS = {"DIV", "POW", "GREATER", "LOGICAL_OR", "LOGICAL_AND", "MOD", "MAX", "MIN"}
+
+
+class RegMap:
+    """Fixed registers of the threaded block for R rows per lane."""
+
+    def __init__(self, R):
+        self.R = R
+        b = 32
+        # acc, tmp, the two X buffers (ping-pong: the X operand of the next
+        # instruction is read while this one runs), the XX second operand, slots
+        self.acc, self.tmp, self.xa, self.xb, self.x2 = b, b + R, b + 2 * R, b + 3 * R, b + 4 * R
+        self.slot = [b + (5 + k) * R for k in range(D)]
+        top = b + (5 + D) * R
+        # per-lane program data (lane j, see eval_kernel.h ti_load):
+        #   pt: table slot of instruction j+1 (4*op + 1024*parity), lane 63: of instruction 0
+        #   xo: LDS byte offset of the X operand of instruction j+1 (lane 63: of instruction 0)
+        #   im: immediate of instruction j (XX: byte offset of the second feature)
+        #   pn: j + 1
+        #   pta: pt + table address (set at block entry)
+        self.chk, self.pt, self.xo, self.im, self.pn, self.lane, self.pta = range(top, top + 7)
+        self.vstate_end = top + 7
+        # SGPRs: imm, pc, scratch, table, target, next X offset, trig flag, bail
+        self.s_imm, self.s_pc, self.s_t, self.s_tbl, self.s_tgt = 65, 66, 67, 68, 70
+        self.s_xo, self.s_flag, self.s_bail = 73, 74, 76
+
+    def vstate(self):
+        """(name, first reg, count) of every VGPR state register group."""
+        R = self.R
+        g = [("acc", self.acc, R), ("tmp", self.tmp, R), ("xa", self.xa, R), ("xb", self.xb, R),
+             ("x2", self.x2, R)]
+        g += [(f"slot{k}", self.slot[k], R) for k in range(D)]
+        g += [("chk", self.chk, 1), ("pt", self.pt, 1), ("xo", self.xo, 1), ("im", self.im, 1),
+              ("pn", self.pn, 1), ("lane", self.lane, 1), ("pta", self.pta, 1)]
+        return g
+
+    def sstate(self):
+        return [("imm", self.s_imm), ("pc", self.s_pc), ("st", self.s_t), ("tbl0", self.s_tbl),
+                ("tbl1", self.s_tbl + 1), ("tgt0", self.s_tgt), ("tgt1", self.s_tgt + 1), ("xo", self.s_xo),
+                ("flag0", self.s_flag), ("flag1", self.s_flag + 1), ("bail", self.s_bail)]
+
+
+# ---------------------------------------------------------------------------
+# 1. handler snippets (C++), compiled by hipcc
+
+def snippet_source(rm, handlers):
+    R = rm.R
+    out = ['#include "interp.h"', "using namespace srhip; using namespace srhip::interp;",
+           "namespace {", "struct St {"]
+    for name, base, cnt in rm.vstate():
+        out.append(f"  float {name}[{cnt}];" if cnt > 1 else
+                   f"  {'float' if name == 'chk' else 'unsigned'} {name};")
+    for name, _ in rm.sstate():
+        out.append(f"  unsigned s_{name};")
+    out.append("};")
+    # IN: define every state register (pinned); OUT: use every one of them.
+    def pin_lines(kind):
+        lines = []
+        for name, base, cnt in rm.vstate():
+            regs = [(f"{name}[{i}]" if cnt > 1 else name, base + i) for i in range(cnt)]
+            for i in range(0, len(regs), 8):
+                chunk = regs[i:i + 8]
+                if kind == "in":
+                    ops = ", ".join(f'"={{v{r}}}"(s.{e})' for e, r in chunk)
+                    lines.append(f'  asm volatile("; IN" : {ops});')
+                else:
+                    ops = ", ".join(f'"{{v{r}}}"(s.{e})' for e, r in chunk)
+                    lines.append(f'  asm volatile("; OUT" :: {ops});')
+        ss = rm.sstate()
+        for i in range(0, len(ss), 8):
+            chunk = ss[i:i + 8]
+            if kind == "in":
+                ops = ", ".join(f'"={{s{r}}}"(s.s_{n})' for n, r in chunk)
+                lines.append(f'  asm volatile("; IN" : {ops});')
+            else:
+                ops = ", ".join(f'"{{s{r}}}"(s.s_{n})' for n, r in chunk)
+                lines.append(f'  asm volatile("; OUT" :: {ops});')
+        return lines
+    for hname, body in handlers:
+        out.append(f'extern "C" __global__ void __launch_bounds__(64) sr_h_{hname}() {{')
+        out.append("  St s;")
+        out += pin_lines("in")
+        out.append("  const float imm = __int_as_float((int)s.s_imm); (void)imm;")
+        out.append("  float& chk = s.chk; (void)chk;")
+        out.append(f"  constexpr int R = {R}; (void)R;")
+        out.append("  " + body)
+        out += pin_lines("out")
+        out.append("}")
+    out.append("}  // namespace")
+    return "\n".join(out) + "\n"
+
+
+def rows(expr):
+    return f"_Pragma(\"unroll\") for (int r = 0; r < R; ++r) {{ {expr} }}"
+
+
+def handler_bodies():
+    """(opcode, name, body C++, needs_x, needs_x2, trig) for every handled opcode."""
+    hs = []
+    hs.append((OP_LDX, "ldx", rows("s.acc[r] = s.{X}[r];"), True, False, False))
+    hs.append((OP_LDC, "ldc", rows("s.acc[r] = imm;"), False, False, False))
+    for k in range(D):
+        hs.append((OP_PUSH0 + k, f"push{k}", rows(f"s.slot{k}[r] = s.acc[r];"), False, False, False))
+        hs.append((OP_POP0 + k, f"pop{k}", rows(f"s.tmp[r] = s.slot{k}[r];"), False, False, False))
+    for u in H_UOPS:
+        code = OP_UN0 + UOPS[u]
+        if u in ("SIN", "COS"):
+            # dev::trig_big over the rows without a mask per row: |x| bits +
+            # 2^23 is negative (as int) exactly for Inf/NaN, so the max is
+            # above 105615.0f's bits + 2^23 iff some row is finite and big
+            body = ("int m = 0; " +
+                    rows(f"m = max(m, (int)(((unsigned)__float_as_int(s.acc[r]) & 0x7fffffffu) + 0x00800000u)); "
+                         f"s.acc[r] = dev::fast_sincos_f32(s.acc[r], {1 if u == 'COS' else 0});") +
+                    " const unsigned long long fl = __builtin_amdgcn_ballot_w64(m > 0x47ce4780 + 0x00800000);"
+                    " s.s_flag0 = (unsigned)fl; s.s_flag1 = (unsigned)(fl >> 32);")
+            hs.append((code, f"un_{u.lower()}", body, False, False, True))
+        else:
+            mk = "chk = mark(s.acc[r], chk); " if u in LOSSY_UOPS else ""
+            hs.append((code, f"un_{u.lower()}",
+                       rows(f"{mk}s.acc[r] = dev::uop<SRHIP_UOP_{u}>(s.acc[r]);"), False, False, False))
+    for b in H_BOPS:
+        LL, LR = b in LOSSY_LHS, b in LOSSY_RHS
+        f = f"dev::bop<SRHIP_BOP_{b}>"
+        for vi, v in enumerate(VARIANTS):
+            code = OP_BIN0 + vi * NUM_BOPS + BOPS[b]
+            mk = ""
+            if v == "AX":
+                mk, e = ("chk = mark(s.acc[r], chk); " if LL else ""), f"{f}(s.acc[r], s.{{X}}[r])"
+            elif v == "XA":
+                mk, e = ("chk = mark(s.acc[r], chk); " if LR else ""), f"{f}(s.{{X}}[r], s.acc[r])"
+            elif v == "AC":
+                mk, e = ("chk = mark(s.acc[r], chk); " if LL else ""), f"{f}(s.acc[r], imm)"
+            elif v == "CA":
+                mk, e = ("chk = mark(s.acc[r], chk); " if LR else ""), f"{f}(imm, s.acc[r])"
+            elif v == "AT":
+                mk = ("chk = mark(s.acc[r], chk); " if LL else "") + ("chk = mark(s.tmp[r], chk); " if LR else "")
+                e = f"{f}(s.acc[r], s.tmp[r])"
+            elif v == "TA":
+                mk = ("chk = mark(s.tmp[r], chk); " if LL else "") + ("chk = mark(s.acc[r], chk); " if LR else "")
+                e = f"{f}(s.tmp[r], s.acc[r])"
+            elif v == "XX":
+                e = f"{f}(s.{{X}}[r], s.x2[r])"
+            elif v == "XC":
+                e = f"{f}(s.{{X}}[r], imm)"
+            else:  # CX
+                e = f"{f}(imm, s.{{X}}[r])"
+            nx = v in ("AX", "XA", "XX", "XC", "CX")
+            hs.append((code, f"b{b.lower()}_{v.lower()}", rows(f"{mk}s.acc[r] = {e};"), nx, v == "XX", False))
+    return hs
+
+
+# ---------------------------------------------------------------------------
+# 2. extraction
+
+REG_V = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
+REG_S = re.compile(r"\bs(\d+)\b|\bs\[(\d+):(\d+)\]")
+BAD = ("s_swappc", "s_setpc", "s_getpc", "scratch_", "buffer_", "global_", "flat_", "s_load", "s_store",
+       "s_buffer", "s_dcache", "s_endpgm", "s_sendmsg", "exec")
+
+
+def extract(asm_text, name):
+    m = re.search(rf"^sr_h_{name}:.*?$(.*?)^\s*s_endpgm", asm_text, re.S | re.M)
+    if not m:
+        raise SystemExit(f"gen_asm_interp: handler {name} not found in compiler output")
+    lines, in_marker = [], False
+    for ln in m.group(1).splitlines():
+        s = ln.strip()
+        if s.startswith(";;#ASMSTART"):
+            in_marker = True
+            continue
+        if s.startswith(";;#ASMEND"):
+            in_marker = False
+            continue
+        if in_marker or not s or s.startswith(";") or s.startswith(".") and not s.endswith(":"):
+            continue
+        s = s.split(";")[0].rstrip()
+        if not s:
+            continue
+        if re.match(r"^\.LBB\w+:$", s):
+            lines.append(s)
+            continue
+        for bad in BAD:
+            if bad in s:
+                raise SystemExit(f"gen_asm_interp: handler {name} contains '{bad}': {s}")
+        lines.append(s)
+    # handler-local labels -> unique per handler (and per asm instance via %=)
+    lbl = {}
+    for s in lines:
+        if s.endswith(":"):
+            lbl[s[:-1]] = f".Lsr{name}_{len(lbl)}_%="
+    out = []
+    for s in lines:
+        for k, v in lbl.items():
+            s = re.sub(re.escape(k) + r"\b", v, s)
+        out.append(s)
+    return out
+
+
+def regs_used(lines, pat):
+    used = set()
+    for s in lines:
+        if s.endswith(":"):
+            continue
+        for m in pat.finditer(s):
+            if m.group(1) is not None:
+                used.add(int(m.group(1)))
+            else:
+                used.update(range(int(m.group(2)), int(m.group(3)) + 1))
+    return used
+
+
+# ---------------------------------------------------------------------------
+# 3. the threaded block
+
+def build(hipcc, out_path, R, extra):
+    rm = RegMap(R)
+    hs = handler_bodies()
+    variants = []  # (opcode, parity, name, body, needs_x, needs_x2, trig)
+    for code, n, body, nx, nx2, trig in hs:
+        for par, xname in (("a", "xa"), ("b", "xb")):
+            variants.append((code, par, f"{n}_{par}", body.replace("{X}", xname), nx, nx2, trig))
+    src = snippet_source(rm, [(n, b) for _, _, n, b, *_ in variants])
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "handlers.hip")
+        open(sp, "w").write(src)
+        ap = os.path.join(td, "handlers.s")
+        cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only",
+               "-S", "-I", HERE, sp, "-o", ap] + extra
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stderr)
+            raise SystemExit("gen_asm_interp: handler compile failed")
+        asm = open(ap).read()
+    bodies = {n: extract(asm, n) for _, _, n, *_ in variants}
+
+    vstate = set(range(rm.acc, rm.vstate_end))
+    sstate = {r for _, r in rm.sstate()}
+    vtemp, stemp = set(), set()
+    for n, lines in bodies.items():
+        vtemp |= regs_used(lines, REG_V) - vstate
+        stemp |= regs_used(lines, REG_S) - sstate
+    vtemp |= {0, 1}  # glue: LDS addresses
+    if vtemp & vstate:
+        raise SystemExit("gen_asm_interp: temp/state VGPR overlap")
+
+    s = rm
+    nrd = R // 4  # ds_read_b128 per R-row operand
+    T = []
+    a = T.append
+
+    def lds_read(dst, addr_v):
+        # R rows per lane: chunk c of 4 rows at +1024*c bytes (interp.h lds_rows)
+        for c in range(nrd):
+            off = f" offset:{1024 * c}" if c else ""
+            a(f"ds_read_b128 v[{dst + 4 * c}:{dst + 4 * c + 3}], v{addr_v}{off}")
+
+    # Hazards (gfx950, as the compiler places them): an SGPR written by
+    # v_readlane needs 2 wait states before a VALU reads it and 4 before a
+    # v_readlane uses it as lane select; SALU readers need none.
+    # entry: table address, pt -> absolute, first instruction's X into xa
+    a(f"s_getpc_b64 s[{s.s_tbl}:{s.s_tbl + 1}]")
+    a(".Lsr_pc_%=:")
+    a(f"s_add_u32 s{s.s_tbl}, s{s.s_tbl}, .Lsr_tbla_%=-.Lsr_pc_%=")
+    a(f"s_addc_u32 s{s.s_tbl + 1}, s{s.s_tbl + 1}, 0")
+    a(f"s_mov_b32 s{s.s_bail}, 0")
+    a(f"s_add_u32 s{s.s_t}, s{s.s_tbl}, 2048")  # both tables in one 4 GiB page:
+    a("s_cbranch_scc1 .Lsr_bail_%=")           # the target's high word is constant
+    a(f"s_mov_b32 s{s.s_tgt + 1}, s{s.s_tbl + 1}")
+    a(f"v_add_u32_e32 v{s.pta}, s{s.s_tbl}, v{s.pt}")
+    a(f"v_readlane_b32 s{s.s_xo}, v{s.xo}, 63")
+    a(f"v_readlane_b32 s{s.s_tgt}, v{s.pta}, 63")
+    a(f"s_mov_b32 s{s.s_pc}, 0")
+    a("s_nop 1")
+    a(f"v_add_u32_e32 v0, s{s.s_xo}, v{s.lane}")
+    lds_read(s.xa, 0)
+    a(f"s_setpc_b64 s[{s.s_tgt}:{s.s_tgt + 1}]")
+    # tables: A = handlers reading xa (prefetching into xb), B = the reverse;
+    # entry k of table P at +4k (+1024 for B) is `s_branch handler(k, P)`
+    for par in ("a", "b"):
+        a(f".Lsr_tbl{par}_%=:")
+        handled = {code: n for code, p_, n, *_ in variants if p_ == par}
+        handled[OP_END] = "end"
+        for code in range(256):
+            a(f"s_branch .Lsr_h_{handled[code]}_%=" if code in handled else "s_branch .Lsr_bail_%=")
+    a(".Lsr_h_end_%=:")
+    a("s_branch .Lsr_done_%=")
+    a(".Lsr_bail_%=:")
+    a(f"s_mov_b32 s{s.s_bail}, 1")
+    a("s_branch .Lsr_done_%=")
+    for code, par, n, body, nx, nx2, trig in variants:
+        xother = s.xb if par == "a" else s.xa
+        a(f".Lsr_h_{n}_%=:")
+        uses_imm = nx2 or re.search(r"\bs%d\b" % s.s_imm, "\n".join(bodies[n])) is not None
+        a(f"v_readlane_b32 s{s.s_xo}, v{s.xo}, s{s.s_pc}")       # next X offset
+        a(f"v_readlane_b32 s{s.s_tgt}, v{s.pta}, s{s.s_pc}")     # next table slot
+        if uses_imm:
+            a(f"v_readlane_b32 s{s.s_imm}, v{s.im}, s{s.s_pc}")  # this immediate
+        a(f"v_readlane_b32 s{s.s_pc}, v{s.pn}, s{s.s_pc}")       # pc + 1
+        if nx2:  # second X operand (its byte offset is the immediate), read now
+            a("s_nop 0")
+            a(f"v_add_u32_e32 v1, s{s.s_imm}, v{s.lane}")
+            lds_read(s.x2, 1)
+        a(f"v_add_u32_e32 v0, s{s.s_xo}, v{s.lane}")
+        lds_read(xother, 0)  # X operand of the NEXT instruction (offset 0 if none)
+        a(f"s_waitcnt lgkmcnt({nrd})")  # all but the prefetch just issued
+        # the body's leading s_nop (placed by the compiler after the pinning
+        # asm) is not needed: >= 4 instructions separate it from the readlanes
+        body_lines = list(bodies[n])
+        while body_lines and body_lines[0].startswith("s_nop"):
+            body_lines.pop(0)
+        for ln in body_lines:
+            a(ln)
+        if trig:
+            a(f"s_cmp_lg_u64 s[{s.s_flag}:{s.s_flag + 1}], 0")
+            a("s_cbranch_scc1 .Lsr_bail_%=")
+        a(f"s_setpc_b64 s[{s.s_tgt}:{s.s_tgt + 1}]")
+    a(".Lsr_done_%=:")
+    a("s_waitcnt lgkmcnt(0)")  # the last prefetch may still be in flight
+
+    # clobbers: every register the block writes besides its outputs
+    outs_v = set(range(s.acc, s.acc + R)) | {s.chk}
+    ins_v = {s.pt, s.xo, s.im, s.pn, s.lane}
+    clob_v = sorted((vtemp | vstate) - outs_v - ins_v)
+    clob_s = sorted((stemp | sstate) - {s.s_bail})
+    clob = [f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s] + ['"vcc"', '"scc"']
+    hdr = [f"// Generated by gen_asm_interp.py (R={R}); do not edit.",
+           "#pragma once",
+           f"#define SR_TI_R {R}",
+           f"#define SR_TI_NUM_OPCODES {NUM_OPCODES}",
+           f"#define SR_TI_OP_BIN0 {OP_BIN0}",
+           "#define SR_TI_TEXT \\"]
+    for ln in T:
+        for l2 in ln.split("\n"):
+            hdr.append('  "' + l2.replace("\\", "\\\\").replace('"', '\\"') + '\\n" \\')
+    hdr.append("  \"\"")
+    hdr.append("#define SR_TI_CLOBBERS " + ", ".join(clob))
+    outs = [f'"={{v{s.acc + i}}}"(acc[{i}])' for i in range(R)]
+    outs += [f'"+{{v{s.chk}}}"(chk)', f'"={{s{s.s_bail}}}"(bail)']
+    hdr.append("#define SR_TI_OUTPUTS(acc, chk, bail) " + ", ".join(outs))
+    ins = [f'"{{v{s.pt}}}"(pt)', f'"{{v{s.xo}}}"(xo)', f'"{{v{s.im}}}"(im)', f'"{{v{s.pn}}}"(pn)',
+           f'"{{v{s.lane}}}"(lane)']
+    hdr.append("#define SR_TI_INPUTS(pt, xo, im, pn, lane) " + ", ".join(ins))
+    hdr.append(f"// handlers: {len(variants)} (+end, bail), VGPR temps {min(vtemp)}..{max(vtemp)}, "
+               f"SGPR temps {sorted(stemp)}")
+    open(out_path, "w").write("\n".join(hdr) + "\n")
+
+
+if __name__ == "__main__":
+    hipcc, out = sys.argv[1], sys.argv[2]
+    R = int(sys.argv[3]) if len(sys.argv) > 3 else 8
+    build(hipcc, out, R, sys.argv[4:])

@@ -59,6 +59,38 @@ __device__ __forceinline__ double uni(double v) {
 __device__ __forceinline__ int imm_int(float v) { return __float_as_int(v); }
 __device__ __forceinline__ int imm_int(double v) { return (int)(__double_as_longlong(v) & 0xffffffffll); }
 
+// Wave sum without LDS round trips (ds_bpermute): DPP butterflies inside each
+// 16-lane row (xor 1, xor 2, half-mirror, mirror), then the four row sums
+// read with v_readlane. The result is wave-uniform.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+template <int CTRL>
+__device__ __forceinline__ double dpp_f(double v) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+__device__ __forceinline__ float lane_val(float v, int l) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), l));
+}
+__device__ __forceinline__ double lane_val(double v, int l) {
+  const long long b = __double_as_longlong(v);
+  const int lo = __builtin_amdgcn_readlane((int)(b & 0xffffffffll), l);
+  const int hi = __builtin_amdgcn_readlane((int)(b >> 32), l);
+  return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <typename T>
+__device__ __forceinline__ T wave_sum(T v) {
+  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);  // row_half_mirror
+  v += dpp_f<0x140>(v);  // row_mirror: every lane holds its row's sum
+  return (lane_val(v, 0) + lane_val(v, 16)) + (lane_val(v, 32) + lane_val(v, 48));
+}
+
 // Non-finite marker: fma(v, 0, chk) is NaN iff v is ±Inf or NaN.
 __device__ __forceinline__ float mark(float v, float chk) { return __builtin_fmaf(v, 0.0f, chk); }
 __device__ __forceinline__ double mark(double v, double chk) { return __builtin_fma(v, 0.0, chk); }
