@@ -29,7 +29,24 @@ namespace dev {
   __device__ __attribute__((noinline)) double name##_ool(double x) { return f64(x); }    \
   __device__ __forceinline__ float name(float x) { return name##_ool(x); }              \
   __device__ __forceinline__ double name(double x) { return name##_ool(x); }
-SR_M1(m_exp, expf, exp)
+// f32 exp: OCML's expf is a 2^x kernel plus over/underflow selects; here the
+// argument is clamped first (exp(89) = Inf and exp(-104) rounds to 0 like the
+// unclamped value; NaN/Inf operands fail the tree before the value is used,
+// exp being checked as lossy) and the selects go. x*log2(e) is carried as
+// hi + lo so that the reduced argument is accurate to ~2^-35; v_exp_f32 then
+// v_ldexp. Validated exhaustively against the correctly rounded value on
+// MI355X (tools/check_fast_exp.hip): see DESIGN.md §4.
+__device__ __forceinline__ float fast_exp_f32(float x) {
+  x = __builtin_amdgcn_fmed3f(x, -104.0f, 89.0f);
+  const float ph = x * 1.44269502e+00f;
+  float pl = __builtin_fmaf(x, 1.44269502e+00f, -ph);
+  pl = __builtin_fmaf(x, 1.92596299e-08f, pl);
+  const float e = __builtin_rintf(ph);
+  const float a = (ph - e) + pl;
+  return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(a), (int)e);
+}
+__device__ __forceinline__ float m_exp(float x) { return fast_exp_f32(x); }
+__device__ __forceinline__ double m_exp(double x) { return exp(x); }
 SR_M1(m_log, logf, log)
 SR_M1_OOL(m_log2, log2f, log2)
 SR_M1_OOL(m_log10, log10f, log10)
@@ -72,8 +89,9 @@ __device__ __forceinline__ bool m_signbit(double x) { return __builtin_signbit(x
 // correctly rounded values: ≤ 2 ulp over all floats with |x| ≤ 105615
 // (tools/check_fast_trig.c). Larger finite arguments are recomputed with OCML
 // behind a wave-uniform branch (taken only if some lane needs it).
-__device__ __forceinline__ float fast_sincos_f32(float x, int want_cos) {
+__device__ __forceinline__ float fast_sincos_f32(float x, int want_cos, float& qabs) {
   const float q = __builtin_rintf(x * 0.636619772f);
+  qabs = __builtin_fabsf(q);
   float r = __builtin_fmaf(q, -1.57079601e+00f, x);
   r = __builtin_fmaf(q, -3.13916473e-07f, r);
   r = __builtin_fmaf(q, -5.39030253e-15f, r);
@@ -87,6 +105,15 @@ __device__ __forceinline__ float fast_sincos_f32(float x, int want_cos) {
   const float t = (i & 1) ? pc : ps;
   return (i & 2) ? -t : t;
 }
+
+__device__ __forceinline__ float fast_sincos_f32(float x, int want_cos) {
+  float qa;
+  return fast_sincos_f32(x, want_cos, qa);
+}
+// Fast-path domain test from the quadrant index: |q| <= kTrigQMax implies
+// |x| < 105300 (inside the validated range). max() ignores NaN rows (their
+// result is NaN either way); an Inf argument gives q = Inf and takes OCML.
+constexpr float kTrigQMax = 67000.0f;
 
 // The fallback is taken with a wave-uniform branch (ballot) and a select, so
 // no divergent region enters the interpreter's dispatch switch.

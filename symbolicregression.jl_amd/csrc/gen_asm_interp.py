@@ -167,13 +167,11 @@ def handler_bodies():
     for u in H_UOPS:
         code = OP_UN0 + UOPS[u]
         if u in ("SIN", "COS"):
-            # dev::trig_big over the rows without a mask per row: |x| bits +
-            # 2^23 is negative (as int) exactly for Inf/NaN, so the max is
-            # above 105615.0f's bits + 2^23 iff some row is finite and big
-            body = ("int m = 0; " +
-                    rows(f"m = max(m, (int)(((unsigned)__float_as_int(s.acc[r]) & 0x7fffffffu) + 0x00800000u)); "
-                         f"s.acc[r] = dev::fast_sincos_f32(s.acc[r], {1 if u == 'COS' else 0});") +
-                    " const unsigned long long fl = __builtin_amdgcn_ballot_w64(m > 0x47ce4780 + 0x00800000);"
+            # fast path only while every row's |quadrant| <= kTrigQMax (device_ops.h)
+            body = ("float qm = 0.0f; " +
+                    rows(f"float qa; s.acc[r] = dev::fast_sincos_f32(s.acc[r], {1 if u == 'COS' else 0}, qa); "
+                         "qm = __builtin_fmaxf(qm, qa);") +
+                    " const unsigned long long fl = __builtin_amdgcn_ballot_w64(!(qm <= dev::kTrigQMax));"
                     " s.s_flag0 = (unsigned)fl; s.s_flag1 = (unsigned)(fl >> 32);")
             hs.append((code, f"un_{u.lower()}", body, False, False, True))
         else:

@@ -163,13 +163,14 @@ __device__ __forceinline__ void un_apply(T (&acc)[R], T& chk) {
     // fast f32 sin/cos for all R values, one wave-uniform check for the
     // rare |x| > 105615 that needs OCML's full reduction
     T v[R];
-    bool big = false;
+    float qmax = 0.0f;
 #pragma unroll
     for (int r = 0; r < R; ++r) {
-      v[r] = dev::fast_sincos_f32(acc[r], U == SRHIP_UOP_COS ? 1 : 0);
-      big |= dev::trig_big(acc[r]);
+      float qa;
+      v[r] = dev::fast_sincos_f32(acc[r], U == SRHIP_UOP_COS ? 1 : 0, qa);
+      qmax = __builtin_fmaxf(qmax, qa);
     }
-    if (__builtin_amdgcn_ballot_w64(big) != 0) {
+    if (__builtin_amdgcn_ballot_w64(!(qmax <= dev::kTrigQMax)) != 0) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
         const T o = U == SRHIP_UOP_COS ? dev::m_cos_ocml(acc[r]) : dev::m_sin_ocml(acc[r]);
