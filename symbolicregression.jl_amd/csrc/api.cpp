@@ -87,6 +87,7 @@ struct srhip_ctx {
   double last_ms = 0.0;
   int last_launches = 0;
   DevBuf partial, sums, oks, dloss, scratch_idx, gather;
+  DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
   std::vector<double> h_sum;
   std::vector<uint8_t> h_ok;
 };
@@ -292,6 +293,11 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   c->last_launches = 0;
   c->sums.ensure(std::max<size_t>(p->ntrees, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(p->ntrees, 1));
+  const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
+  if (mode == MODE_LOSS) {
+    c->fail.ensure(std::max<size_t>(nslots, 1) * sizeof(uint32_t));
+    HIP_CHECK(hipMemsetAsync(c->fail.p, 0, std::max<size_t>(nslots, 1) * sizeof(uint32_t), s));
+  }
   for (int pass = 0; pass < 2; ++pass) {
     const int nlist = pass == 0 ? p->nlist_a : p->nlist_b;
     if (nlist == 0 || rows == 0) continue;
@@ -303,6 +309,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.tree_off = p->d_tree_off;
     a.list = p->d_list + (pass == 0 ? 0 : p->nlist_a);
     a.list_off = a.list + (p->nlist_a + p->nlist_b);
+    a.fail = mode == MODE_LOSS ? static_cast<uint32_t*>(c->fail.p) + (pass == 0 ? 0 : p->nlist_a) : nullptr;
     a.nlist = nlist;
     a.X = X;
     a.y = y;

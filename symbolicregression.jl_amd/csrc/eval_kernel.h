@@ -66,6 +66,11 @@ __device__ __forceinline__ T tile_loss(const T (&acc)[R], const T (&yv)[R], cons
   return s0 + s1;
 }
 
+template <typename T>
+__device__ __forceinline__ T qnan_v() { return __builtin_nan(""); }
+template <>
+__device__ __forceinline__ float qnan_v<float>() { return __builtin_nanf(""); }
+
 // One tile of one program through the threaded interpreter block
 // (gen_asm_interp.py). The program is in VGPRs, one instruction per lane, in
 // the form ti_lanes() prepares; `lane_addr` is the LDS byte address of this
@@ -132,13 +137,14 @@ __device__ __forceinline__ T tile_loss_any(int lk, const T (&acc)[R], const T (&
   }
 }
 
-#ifdef SR_WPE
-#define SR_WPE_ATTR __attribute__((amdgpu_waves_per_eu(SR_WPE)))
-#else
-#define SR_WPE_ATTR
-#endif
+// Occupancy floor of the shallow f32 variant: 5 waves per SIMD (<= 96 VGPRs;
+// the LDS row tile allows 6 workgroups per CU). Without it the compiler
+// settles at 97-104 VGPRs and 4 waves.
+template <typename T, int D>
+constexpr int kWavesPerEU = (sizeof(T) == 4 && D == kShallowSlots) ? 5 : 1;
 template <typename T, int R, int D, int SET, int MODE, bool W>
-__global__ void __launch_bounds__(256) SR_WPE_ATTR eval_kernel(EvalArgs<T> a) {
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<T, D>)))
+eval_kernel(EvalArgs<T> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int TILE = 64 * R;
   using V = typename V16<T>::type;
@@ -185,29 +191,50 @@ __global__ void __launch_bounds__(256) SR_WPE_ATTR eval_kernel(EvalArgs<T> a) {
   constexpr bool TI = SR_TI != 0 && std::is_same<T, float>::value && R == SR_R32 && D == kShallowSlots &&
                       SET == OPSET_BASIC;
   auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
-  auto prog_of = [&](int s) { return a.prog + __builtin_amdgcn_readfirstlane(a.list_off[s]); };
+  // list_off is read through the constant address space: scalar loads (the
+  // early-exit flag stores would otherwise make the compiler use vector loads)
+  auto prog_of = [&](int s) {
+    return a.prog + __builtin_amdgcn_readfirstlane(
+                        ((const __attribute__((address_space(4))) int32_t*)(a.list_off))[s]);
+  };
   VProg<T> vnext;
   // TI: the program in VGPRs (lane j = instruction j; shallow programs have at
   // most kVProgMax instructions and the code buffer is padded by 64), loaded
   // one tree ahead so its memory latency overlaps the current tree
+  // Early exit (MODE_LOSS): DynamicExpressions stops a tree at its first
+  // non-finite value. A wave that sees one marks the list slot in a.fail; the
+  // row groups that reach the slot later skip it (their partial is the failure
+  // marker). Flags are read one tree ahead; a stale 0 only costs the work.
+  constexpr bool EE = MODE == MODE_LOSS;
+  auto ld_flag = [&](int slot) {
+    return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  uint32_t fnext = 0;
   uint2 tnext0 = make_uint2(0u, 0u), tnext1 = make_uint2(0u, 0u);
   const uint32_t rs_bytes = (uint32_t)(rows * sizeof(T));
   if (wave < a.tpb && slot_of(wave) < a.nlist) {
+    if constexpr (EE) fnext = ld_flag(slot_of(wave));
     if constexpr (VP) vnext.load(prog_of(slot_of(wave)), lane);
     if constexpr (TI) {
       tnext0 = reinterpret_cast<const uint2*>(prog_of(slot_of(wave)))[lane];
       tnext1 = reinterpret_cast<const uint2*>(prog_of(slot_of(wave)))[lane + 1];
     }
   }
-  for (int i = wave; i < a.tpb; i += nwaves) {
-    const int s = slot_of(i);
+  for (int i0 = wave; i0 < a.tpb; i0 += nwaves) {
+    // all wave-uniform: keep the schedule in SGPRs
+    const int i = __builtin_amdgcn_readfirstlane(i0);
+    const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
     if (s >= a.nlist) break;  // slot_of is increasing in i
-    const int s2 = slot_of(i + nwaves);
+    const int s2 = __builtin_amdgcn_readfirstlane(slot_of(i + nwaves));
     const bool more = i + nwaves < a.tpb && s2 < a.nlist;
     VProg<T> vp;
     if constexpr (VP) {
       vp = vnext;
       if (more) vnext.load(prog_of(s2), lane);
+    }
+    const bool skip = EE && __builtin_amdgcn_readfirstlane((int)fnext) != 0;
+    if constexpr (EE) {
+      if (more) fnext = ld_flag(s2);
     }
     TiLanes tl_prog{};
     if constexpr (TI) {
@@ -218,8 +245,8 @@ __global__ void __launch_bounds__(256) SR_WPE_ATTR eval_kernel(EvalArgs<T> a) {
       }
     }
     CIns<T>* p = const_prog(prog_of(s));
-    T lsum = T(0), chk = T(0);
-    for (int tl = 0; tl < nt_valid; ++tl) {
+    T lsum = T(0), chk = skip ? qnan_v<T>() : T(0);
+    for (int tl = 0; tl < (skip ? 0 : nt_valid); ++tl) {
       const T* sXt = sX + tl * TILE;
       T acc[R];
       if constexpr (TI) {
@@ -246,11 +273,16 @@ __global__ void __launch_bounds__(256) SR_WPE_ATTR eval_kernel(EvalArgs<T> a) {
           lsum += tile_loss_any<W, false, T, R>(a.loss, acc, yv, wv, lp, lane, TILE);
         else
           lsum += tile_loss_any<W, true, T, R>(a.loss, acc, yv, wv, lp, lane, last_valid);
+        if (__builtin_amdgcn_ballot_w64(chk != chk) != 0) break;  // failed: the rest is moot
       }
     }
     lsum = wave_sum(lsum);
     chk = wave_sum(chk);
     if (lane == 0) sPart[i] = Part<T>{lsum, chk};
+    if constexpr (EE) {
+      if (!skip && chk != chk && lane == 0)
+        __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
   __syncthreads();
   // 3. one coalesced store of the group's partials

@@ -24,6 +24,7 @@ struct EvalArgs {
   const int32_t* tree_off; // [ntrees] program start per tree
   const int32_t* list;     // tree ids handled by this launch, cost-descending
   const int32_t* list_off; // [nlist] program start of list[s] (= tree_off[list[s]])
+  uint32_t* fail;          // [nlist] MODE_LOSS: set once slot s is known to fail (early exit)
   int nlist;
   const T* X;              // [nfeat][n_pad] feature-major, rows padded
   const T* y;              // [n_pad]
