@@ -62,15 +62,16 @@ __device__ __forceinline__ int imm_int(double v) { return (int)(__double_as_long
 // Wave sum without LDS round trips (ds_bpermute): DPP butterflies inside each
 // 16-lane row (xor 1, xor 2, half-mirror, mirror), then the four row sums
 // read with v_readlane. The result is wave-uniform.
-template <int CTRL>
+// DPP move of v (lanes of rows outside ROWS get 0, the `old` operand).
+template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ float dpp_f(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, ROWS, 0xf, false));
 }
-template <int CTRL>
+template <int CTRL, int ROWS = 0xf>
 __device__ __forceinline__ double dpp_f(double v) {
   const long long b = __double_as_longlong(v);
-  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, 0xf, 0xf, false);
-  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+  const int lo = __builtin_amdgcn_update_dpp(0, (int)(b & 0xffffffffll), CTRL, ROWS, 0xf, false);
+  const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, ROWS, 0xf, false);
   return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 __device__ __forceinline__ float lane_val(float v, int l) {
@@ -84,11 +85,13 @@ __device__ __forceinline__ double lane_val(double v, int l) {
 }
 template <typename T>
 __device__ __forceinline__ T wave_sum(T v) {
-  v += dpp_f<0xB1>(v);   // quad_perm [1,0,3,2]
-  v += dpp_f<0x4E>(v);   // quad_perm [2,3,0,1]
-  v += dpp_f<0x141>(v);  // row_half_mirror
-  v += dpp_f<0x140>(v);  // row_mirror: every lane holds its row's sum
-  return (lane_val(v, 0) + lane_val(v, 16)) + (lane_val(v, 32) + lane_val(v, 48));
+  v += dpp_f<0xB1>(v);         // quad_perm [1,0,3,2]
+  v += dpp_f<0x4E>(v);         // quad_perm [2,3,0,1]
+  v += dpp_f<0x141>(v);        // row_half_mirror
+  v += dpp_f<0x140>(v);        // row_mirror: every lane holds its row's sum
+  v += dpp_f<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3: r0+r1, r2+r3
+  v += dpp_f<0x143, 0xc>(v);   // row_bcast:31 -> rows 2, 3: lane 63 = r0+r1+r2+r3
+  return lane_val(v, 63);
 }
 
 // Non-finite marker: fma(v, 0, chk) is NaN iff v is ±Inf or NaN.
