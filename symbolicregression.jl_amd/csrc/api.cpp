@@ -9,7 +9,9 @@
 #include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <cstdlib>
 #include <mutex>
+#include <type_traits>
 #include <numeric>
 #include <string>
 #include <vector>
@@ -88,6 +90,7 @@ struct srhip_ctx {
   int last_launches = 0;
   DevBuf partial, sums, oks, dloss, scratch_idx, gather;
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
+  DevBuf ti_rec;  // threaded-interpreter records of the shallow f32 list
   std::vector<double> h_sum;
   std::vector<uint8_t> h_ok;
 };
@@ -282,6 +285,16 @@ void check_program_vs_dataset(const srhip_dataset* ds, const srhip_program* p) {
                 "X contains non-finite values: did_succeed of fused leaves differs from the reference; use the CPU path");
 }
 
+// Threaded interpreter on/off (SRHIP_TI=0 disables it; built only when the
+// kernels were compiled with SR_TI).
+static bool ti_enabled() {
+  static const bool on = [] {
+    const char* e = std::getenv("SRHIP_TI");
+    return ti_compiled() && !(e && e[0] == '0');
+  }();
+  return on;
+}
+
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
 // n_pad) may be the dataset itself or a gathered row subset.
 template <typename T>
@@ -310,6 +323,14 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.list = p->d_list + (pass == 0 ? 0 : p->nlist_a);
     a.list_off = a.list + (p->nlist_a + p->nlist_b);
     a.fail = mode == MODE_LOSS ? static_cast<uint32_t*>(c->fail.p) + (pass == 0 ? 0 : p->nlist_a) : nullptr;
+    a.ti_rec = nullptr;
+    if (ti_enabled() && std::is_same<T, float>::value && pass == 0 && plan.opset == OPSET_BASIC) {
+      c->ti_rec.ensure((size_t)nlist * 64 * sizeof(uint4));
+      HIP_CHECK(launch_ti_records(reinterpret_cast<const Ins<float>*>(a.prog), a.list_off, nlist,
+                                  (uint32_t)(plan.ntiles * plan.tile * sizeof(T)),
+                                  static_cast<uint4*>(c->ti_rec.p), s));
+      a.ti_rec = static_cast<const uint4*>(c->ti_rec.p);
+    }
     a.nlist = nlist;
     a.X = X;
     a.y = y;

@@ -6,6 +6,8 @@
 
 namespace srhip {
 
+bool ti_compiled() { return SR_TI != 0; }
+
 template <>
 hipError_t launch_eval<float>(const EvalPlan& plan, const EvalArgs<float>& a, int mode, hipStream_t stream) {
   if (plan.D == kMaxSlots) return launch_rd<float, 4, kMaxSlots, OPSET_FULL>(plan, a, mode, stream);

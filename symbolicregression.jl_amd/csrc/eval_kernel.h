@@ -30,7 +30,7 @@
 // SR_TI: the threaded interpreter (gen_asm_interp.py) for f32 trees of the
 // BASIC operator set in the shallow kernel; 0 keeps the C++ dispatch only.
 #ifndef SR_TI
-#define SR_TI 0
+#define SR_TI 1
 #endif
 #ifndef SR_R32
 #define SR_R32 8  // rows per lane of the shallow f32 kernel
@@ -72,52 +72,26 @@ template <>
 __device__ __forceinline__ float qnan_v<float>() { return __builtin_nanf(""); }
 
 // One tile of one program through the threaded interpreter block
-// (gen_asm_interp.py). The program is in VGPRs, one instruction per lane, in
-// the form ti_lanes() prepares; `lane_addr` is the LDS byte address of this
-// lane's rows of feature 0 in the tile. Returns false if the block bailed out
-// (an opcode or argument it does not handle); acc/chk are then garbage and
-// the caller re-runs the tile with the C++ interpreter.
-struct TiLanes {
-  uint32_t pt, xo, im, pn;
-};
+// (gen_asm_interp.py): `recs` = the program's instruction records
+// (ti_records_kernel), `lane_addr` = LDS byte address of this lane's rows of
+// feature 0 in the tile. Returns false if the block bailed out (an opcode or
+// argument it does not handle); acc/chk are then garbage and the caller
+// re-runs the tile with the C++ interpreter.
 template <int R>
-__device__ __forceinline__ bool run_program_ti(const TiLanes& L, uint32_t lane_addr, float (&acc)[R],
+__device__ __forceinline__ bool run_program_ti(const uint4* recs, uint32_t lane_addr, float (&acc)[R],
                                                float& chk) {
 #if SR_TI && defined(__HIP_DEVICE_COMPILE__)
   static_assert(R == SR_TI_R, "threaded block generated for another R");
   uint32_t bail;
-  const uint32_t pt = L.pt, xo = L.xo, im = L.im, pn = L.pn, lane = lane_addr;
-  asm volatile(SR_TI_TEXT : SR_TI_OUTPUTS(acc, chk, bail) : SR_TI_INPUTS(pt, xo, im, pn, lane)
-               : SR_TI_CLOBBERS);
+  const uint64_t rp = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)recs) |
+                      ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)((uintptr_t)recs >> 32)) << 32);
+  const uint32_t lane = lane_addr;
+  asm volatile(SR_TI_TEXT : SR_TI_OUTPUTS(acc, chk, bail) : SR_TI_INPUTS(rp, lane) : SR_TI_CLOBBERS);
   return bail == 0;
 #else
-  (void)L; (void)lane_addr; (void)acc; (void)chk;
+  (void)recs; (void)lane_addr; (void)acc; (void)chk;
   return false;
 #endif
-}
-
-// Lane j of the threaded block's program registers (c0 = instruction j,
-// c1 = instruction j+1 of the program, as (code, imm) pairs):
-//   pt = table slot of instruction j+1: 4*opcode + 1024*parity, parity = (j+1)&1
-//        (instruction i runs in table i&1: its X operand is in xa for even i);
-//        lane 63 holds instruction 0's slot (table A)
-//   xo = LDS byte offset of instruction j+1's X operand (lane 63: instruction 0's)
-//   im = immediate of instruction j; for (X[f], X[g]) the byte offset of g
-//   pn = j + 1
-// Programs have at most kVProgMax = 63 instructions, so lane 63 is free.
-__device__ __forceinline__ TiLanes ti_lanes(uint2 c0, uint2 c1, int lane, uint32_t rs_bytes) {
-  const uint32_t code0 = (uint32_t)__builtin_amdgcn_readfirstlane((int)c0.x);
-  const bool l63 = lane == 63;
-  const uint32_t cn = l63 ? code0 : c1.x;
-  const uint32_t par = l63 ? 0u : (uint32_t)((lane + 1) & 1);
-  TiLanes L;
-  L.pt = 4u * (cn & 0xffu) + 1024u * par;
-  L.xo = (cn >> 16) * rs_bytes;
-  const uint32_t op = c0.x & 0xffu;
-  const bool xx = op >= (uint32_t)bin_opcode(V_XX, 0) && op < (uint32_t)bin_opcode(V_XX + 1, 0);
-  L.im = xx ? c0.y * rs_bytes : c0.y;
-  L.pn = (uint32_t)lane + 1u;
-  return L;
 }
 
 template <bool W, bool MASK, typename T, int R>
@@ -210,15 +184,10 @@ eval_kernel(EvalArgs<T> a) {
     return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
   uint32_t fnext = 0;
-  uint2 tnext0 = make_uint2(0u, 0u), tnext1 = make_uint2(0u, 0u);
-  const uint32_t rs_bytes = (uint32_t)(rows * sizeof(T));
+
   if (wave < a.tpb && slot_of(wave) < a.nlist) {
     if constexpr (EE) fnext = ld_flag(slot_of(wave));
     if constexpr (VP) vnext.load(prog_of(slot_of(wave)), lane);
-    if constexpr (TI) {
-      tnext0 = reinterpret_cast<const uint2*>(prog_of(slot_of(wave)))[lane];
-      tnext1 = reinterpret_cast<const uint2*>(prog_of(slot_of(wave)))[lane + 1];
-    }
   }
   for (int i0 = wave; i0 < a.tpb; i0 += nwaves) {
     // all wave-uniform: keep the schedule in SGPRs
@@ -236,27 +205,22 @@ eval_kernel(EvalArgs<T> a) {
     if constexpr (EE) {
       if (more) fnext = ld_flag(s2);
     }
-    TiLanes tl_prog{};
-    if constexpr (TI) {
-      tl_prog = ti_lanes(tnext0, tnext1, lane, rs_bytes);
-      if (more) {
-        tnext0 = reinterpret_cast<const uint2*>(prog_of(s2))[lane];
-        tnext1 = reinterpret_cast<const uint2*>(prog_of(s2))[lane + 1];
-      }
-    }
     CIns<T>* p = const_prog(prog_of(s));
     T lsum = T(0), chk = skip ? qnan_v<T>() : T(0);
     for (int tl = 0; tl < (skip ? 0 : nt_valid); ++tl) {
       const T* sXt = sX + tl * TILE;
       T acc[R];
+      bool done = false;
       if constexpr (TI) {
-        const T chk0 = chk;
-        const uint32_t lds = (uint32_t)reinterpret_cast<uintptr_t>(
-            (const __attribute__((address_space(3))) T*)(sXt)) + (uint32_t)lane * 16u;
-        if (!run_program_ti<R>(tl_prog, lds, acc, chk)) {
-          chk = chk0;
-          run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
+        if (a.ti_rec) {
+          const T chk0 = chk;
+          const uint32_t lds = (uint32_t)reinterpret_cast<uintptr_t>(
+              (const __attribute__((address_space(3))) T*)(sXt)) + (uint32_t)lane * 16u;
+          done = run_program_ti<R>(a.ti_rec + (size_t)s * 64, lds, acc, chk);
+          if (!done) chk = chk0;
         }
+      }
+      if (done) {
       } else if constexpr (VP && SR_VP == 2) run_program_v2<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
       else if constexpr (VP) run_program_v<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
       else run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);

@@ -74,17 +74,17 @@ class RegMap:
         self.acc, self.tmp, self.xa, self.xb, self.x2 = b, b + R, b + 2 * R, b + 3 * R, b + 4 * R
         self.slot = [b + (5 + k) * R for k in range(D)]
         top = b + (5 + D) * R
-        # per-lane program data (lane j, see eval_kernel.h ti_load):
-        #   pt: table slot of instruction j+1 (4*op + 1024*parity), lane 63: of instruction 0
-        #   xo: LDS byte offset of the X operand of instruction j+1 (lane 63: of instruction 0)
-        #   im: immediate of instruction j (XX: byte offset of the second feature)
-        #   pn: j + 1
-        #   pta: pt + table address (set at block entry)
-        self.chk, self.pt, self.xo, self.im, self.pn, self.lane, self.pta = range(top, top + 7)
-        self.vstate_end = top + 7
-        # SGPRs: imm, pc, scratch, table, target, next X offset, trig flag, bail
-        self.s_imm, self.s_pc, self.s_t, self.s_tbl, self.s_tgt = 65, 66, 67, 68, 70
-        self.s_xo, self.s_flag, self.s_bail = 73, 74, 76
+        self.chk, self.lane = top, top + 1
+        self.vstate_end = top + 2
+        # SGPRs: scratch, table (2), target (2), trig flag (2), instruction
+        # records of parity A and B (4 + 4: next table slot, next X offset,
+        # immediate, pad), record base (2), record offset, bail
+        self.s_t, self.s_tbl, self.s_tgt, self.s_flag = 67, 68, 70, 74
+        self.s_rec = {"a": 76, "b": 80}
+        self.s_rbase, self.s_roff, self.s_bail = 84, 86, 87
+
+    def imm_sgpr(self, par):
+        return self.s_rec[par] + 2
 
     def vstate(self):
         """(name, first reg, count) of every VGPR state register group."""
@@ -92,14 +92,17 @@ class RegMap:
         g = [("acc", self.acc, R), ("tmp", self.tmp, R), ("xa", self.xa, R), ("xb", self.xb, R),
              ("x2", self.x2, R)]
         g += [(f"slot{k}", self.slot[k], R) for k in range(D)]
-        g += [("chk", self.chk, 1), ("pt", self.pt, 1), ("xo", self.xo, 1), ("im", self.im, 1),
-              ("pn", self.pn, 1), ("lane", self.lane, 1), ("pta", self.pta, 1)]
+        g += [("chk", self.chk, 1), ("lane", self.lane, 1)]
         return g
 
     def sstate(self):
-        return [("imm", self.s_imm), ("pc", self.s_pc), ("st", self.s_t), ("tbl0", self.s_tbl),
-                ("tbl1", self.s_tbl + 1), ("tgt0", self.s_tgt), ("tgt1", self.s_tgt + 1), ("xo", self.s_xo),
-                ("flag0", self.s_flag), ("flag1", self.s_flag + 1), ("bail", self.s_bail)]
+        out = [("st", self.s_t), ("tbl0", self.s_tbl), ("tbl1", self.s_tbl + 1), ("tgt0", self.s_tgt),
+               ("tgt1", self.s_tgt + 1), ("flag0", self.s_flag), ("flag1", self.s_flag + 1)]
+        for par in ("a", "b"):
+            out += [(f"r{par}{k}", self.s_rec[par] + k) for k in range(4)]
+        out += [("rbase0", self.s_rbase), ("rbase1", self.s_rbase + 1), ("roff", self.s_roff),
+                ("bail", self.s_bail)]
+        return out
 
 
 # ---------------------------------------------------------------------------
@@ -138,11 +141,11 @@ def snippet_source(rm, handlers):
                 ops = ", ".join(f'"{{s{r}}}"(s.s_{n})' for n, r in chunk)
                 lines.append(f'  asm volatile("; OUT" :: {ops});')
         return lines
-    for hname, body in handlers:
+    for hname, body, par in handlers:
         out.append(f'extern "C" __global__ void __launch_bounds__(64) sr_h_{hname}() {{')
         out.append("  St s;")
         out += pin_lines("in")
-        out.append("  const float imm = __int_as_float((int)s.s_imm); (void)imm;")
+        out.append(f"  const float imm = __int_as_float((int)s.s_r{par}2); (void)imm;")
         out.append("  float& chk = s.chk; (void)chk;")
         out.append(f"  constexpr int R = {R}; (void)R;")
         out.append("  " + body)
@@ -279,7 +282,7 @@ def build(hipcc, out_path, R, extra):
     for code, n, body, nx, nx2, trig in hs:
         for par, xname in (("a", "xa"), ("b", "xb")):
             variants.append((code, par, f"{n}_{par}", body.replace("{X}", xname), nx, nx2, trig))
-    src = snippet_source(rm, [(n, b) for _, _, n, b, *_ in variants])
+    src = snippet_source(rm, [(n, b, par) for _, par, n, b, *_ in variants])
     with tempfile.TemporaryDirectory() as td:
         sp = os.path.join(td, "handlers.hip")
         open(sp, "w").write(src)
@@ -314,10 +317,15 @@ def build(hipcc, out_path, R, extra):
             off = f" offset:{1024 * c}" if c else ""
             a(f"ds_read_b128 v[{dst + 4 * c}:{dst + 4 * c + 3}], v{addr_v}{off}")
 
-    # Hazards (gfx950, as the compiler places them): an SGPR written by
-    # v_readlane needs 2 wait states before a VALU reads it and 4 before a
-    # v_readlane uses it as lane select; SALU readers need none.
-    # entry: table address, pt -> absolute, first instruction's X into xa
+    def rec(par, k):
+        return s.s_rec[par] + k
+
+    # Records (ti_records_kernel): record 0 of a tree = {slot(0), xo(0)}, record
+    # i+1 = {slot(i+1), xo(i+1), imm(i)} with slot(j) = 4*opcode(j) + 1024*(j&1)
+    # (table of instruction j's parity) and xo(j) the LDS byte offset of its X.
+    # Instruction i runs in parity (i&1) with record i+1 in that parity's SGPRs;
+    # it loads record i+2 into the other parity's SGPRs and X(i+1) into the
+    # other X buffer; everything it waits for was issued one instruction ago.
     a(f"s_getpc_b64 s[{s.s_tbl}:{s.s_tbl + 1}]")
     a(".Lsr_pc_%=:")
     a(f"s_add_u32 s{s.s_tbl}, s{s.s_tbl}, .Lsr_tbla_%=-.Lsr_pc_%=")
@@ -326,15 +334,16 @@ def build(hipcc, out_path, R, extra):
     a(f"s_add_u32 s{s.s_t}, s{s.s_tbl}, 2048")  # both tables in one 4 GiB page:
     a("s_cbranch_scc1 .Lsr_bail_%=")           # the target's high word is constant
     a(f"s_mov_b32 s{s.s_tgt + 1}, s{s.s_tbl + 1}")
-    a(f"v_add_u32_e32 v{s.pta}, s{s.s_tbl}, v{s.pt}")
-    a(f"v_readlane_b32 s{s.s_xo}, v{s.xo}, 63")
-    a(f"v_readlane_b32 s{s.s_tgt}, v{s.pta}, 63")
-    a(f"s_mov_b32 s{s.s_pc}, 0")
-    a("s_nop 1")
-    a(f"v_add_u32_e32 v0, s{s.s_xo}, v{s.lane}")
+    a(f"s_load_dwordx4 s[{rec('b', 0)}:{rec('b', 3)}], s[{s.s_rbase}:{s.s_rbase + 1}], 0x0")
+    a(f"s_load_dwordx4 s[{rec('a', 0)}:{rec('a', 3)}], s[{s.s_rbase}:{s.s_rbase + 1}], 0x10")
+    a(f"s_mov_b32 s{s.s_roff}, 32")
+    a("s_waitcnt lgkmcnt(0)")
+    a(f"v_add_u32_e32 v0, s{rec('b', 1)}, v{s.lane}")
     lds_read(s.xa, 0)
+    a(f"s_and_b32 s{s.s_t}, s{rec('b', 0)}, 0x7fc")
+    a(f"s_add_u32 s{s.s_tgt}, s{s.s_tbl}, s{s.s_t}")
     a(f"s_setpc_b64 s[{s.s_tgt}:{s.s_tgt + 1}]")
-    # tables: A = handlers reading xa (prefetching into xb), B = the reverse;
+    # tables: A = handlers of even instructions (X in xa), B = odd (X in xb);
     # entry k of table P at +4k (+1024 for B) is `s_branch handler(k, P)`
     for par in ("a", "b"):
         a(f".Lsr_tbl{par}_%=:")
@@ -348,23 +357,20 @@ def build(hipcc, out_path, R, extra):
     a(f"s_mov_b32 s{s.s_bail}, 1")
     a("s_branch .Lsr_done_%=")
     for code, par, n, body, nx, nx2, trig in variants:
+        other = "b" if par == "a" else "a"
         xother = s.xb if par == "a" else s.xa
         a(f".Lsr_h_{n}_%=:")
-        uses_imm = nx2 or re.search(r"\bs%d\b" % s.s_imm, "\n".join(bodies[n])) is not None
-        a(f"v_readlane_b32 s{s.s_xo}, v{s.xo}, s{s.s_pc}")       # next X offset
-        a(f"v_readlane_b32 s{s.s_tgt}, v{s.pta}, s{s.s_pc}")     # next table slot
-        if uses_imm:
-            a(f"v_readlane_b32 s{s.s_imm}, v{s.im}, s{s.s_pc}")  # this immediate
-        a(f"v_readlane_b32 s{s.s_pc}, v{s.pn}, s{s.s_pc}")       # pc + 1
+        a("s_waitcnt lgkmcnt(0)")  # this record + this X (issued one instruction ago)
         if nx2:  # second X operand (its byte offset is the immediate), read now
-            a("s_nop 0")
-            a(f"v_add_u32_e32 v1, s{s.s_imm}, v{s.lane}")
+            a(f"v_add_u32_e32 v1, s{rec(par, 2)}, v{s.lane}")
             lds_read(s.x2, 1)
-        a(f"v_add_u32_e32 v0, s{s.s_xo}, v{s.lane}")
+            a("s_waitcnt lgkmcnt(0)")
+        a(f"s_load_dwordx4 s[{rec(other, 0)}:{rec(other, 3)}], s[{s.s_rbase}:{s.s_rbase + 1}], s{s.s_roff}")
+        a(f"s_add_u32 s{s.s_roff}, s{s.s_roff}, 16")
+        a(f"v_add_u32_e32 v0, s{rec(par, 1)}, v{s.lane}")
         lds_read(xother, 0)  # X operand of the NEXT instruction (offset 0 if none)
-        a(f"s_waitcnt lgkmcnt({nrd})")  # all but the prefetch just issued
-        # the body's leading s_nop (placed by the compiler after the pinning
-        # asm) is not needed: >= 4 instructions separate it from the readlanes
+        a(f"s_and_b32 s{s.s_t}, s{rec(par, 0)}, 0x7fc")  # next table slot (masked: never
+        a(f"s_add_u32 s{s.s_tgt}, s{s.s_tbl}, s{s.s_t}")   # a jump outside the tables)
         body_lines = list(bodies[n])
         while body_lines and body_lines[0].startswith("s_nop"):
             body_lines.pop(0)
@@ -375,13 +381,13 @@ def build(hipcc, out_path, R, extra):
             a("s_cbranch_scc1 .Lsr_bail_%=")
         a(f"s_setpc_b64 s[{s.s_tgt}:{s.s_tgt + 1}]")
     a(".Lsr_done_%=:")
-    a("s_waitcnt lgkmcnt(0)")  # the last prefetch may still be in flight
+    a("s_waitcnt lgkmcnt(0)")  # the last record load and X prefetch may be in flight
 
     # clobbers: every register the block writes besides its outputs
     outs_v = set(range(s.acc, s.acc + R)) | {s.chk}
-    ins_v = {s.pt, s.xo, s.im, s.pn, s.lane}
+    ins_v = {s.lane}
     clob_v = sorted((vtemp | vstate) - outs_v - ins_v)
-    clob_s = sorted((stemp | sstate) - {s.s_bail})
+    clob_s = sorted((stemp | sstate) - {s.s_bail, s.s_rbase, s.s_rbase + 1})
     clob = [f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s] + ['"vcc"', '"scc"']
     hdr = [f"// Generated by gen_asm_interp.py (R={R}); do not edit.",
            "#pragma once",
@@ -397,9 +403,8 @@ def build(hipcc, out_path, R, extra):
     outs = [f'"={{v{s.acc + i}}}"(acc[{i}])' for i in range(R)]
     outs += [f'"+{{v{s.chk}}}"(chk)', f'"={{s{s.s_bail}}}"(bail)']
     hdr.append("#define SR_TI_OUTPUTS(acc, chk, bail) " + ", ".join(outs))
-    ins = [f'"{{v{s.pt}}}"(pt)', f'"{{v{s.xo}}}"(xo)', f'"{{v{s.im}}}"(im)', f'"{{v{s.pn}}}"(pn)',
-           f'"{{v{s.lane}}}"(lane)']
-    hdr.append("#define SR_TI_INPUTS(pt, xo, im, pn, lane) " + ", ".join(ins))
+    ins = [f'"{{s[{s.s_rbase}:{s.s_rbase + 1}]}}"(recs)', f'"{{v{s.lane}}}"(lane)']
+    hdr.append("#define SR_TI_INPUTS(recs, lane) " + ", ".join(ins))
     hdr.append(f"// handlers: {len(variants)} (+end, bail), VGPR temps {min(vtemp)}..{max(vtemp)}, "
                f"SGPR temps {sorted(stemp)}")
     open(out_path, "w").write("\n".join(hdr) + "\n")

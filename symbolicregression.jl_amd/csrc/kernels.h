@@ -25,6 +25,7 @@ struct EvalArgs {
   const int32_t* list;     // tree ids handled by this launch, cost-descending
   const int32_t* list_off; // [nlist] program start of list[s] (= tree_off[list[s]])
   uint32_t* fail;          // [nlist] MODE_LOSS: set once slot s is known to fail (early exit)
+  const uint4* ti_rec;     // [nlist][64] threaded-interpreter records (nullptr: C++ dispatch)
   int nlist;
   const T* X;              // [nfeat][n_pad] feature-major, rows padded
   const T* y;              // [n_pad]
@@ -58,6 +59,12 @@ struct EvalPlan {
 
 // Choose the geometry for `nlist` trees over `n` rows; returns false when the
 // row tile of this feature count does not fit in LDS.
+// Threaded-interpreter instruction records of every list slot (f32 shallow
+// programs; eval_kernel.h / gen_asm_interp.py): [nlist][64] uint4.
+bool ti_compiled();  // eval kernels built with the threaded interpreter (SR_TI)
+hipError_t launch_ti_records(const Ins<float>* prog, const int32_t* list_off, int nlist,
+                             uint32_t rs_bytes, uint4* rec, hipStream_t stream);
+
 bool plan_eval(int dtype, bool deep, int opset, int mode, bool weighted, int nfeat,
                int64_t n, int nlist, EvalPlan* plan);
 // Same, for explicit R / D / LDS arrays / partial bytes per tree slot.

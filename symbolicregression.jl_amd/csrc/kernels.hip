@@ -100,6 +100,33 @@ static inline int variant_R(int dtype, bool deep) {
   return dtype == SRHIP_F32 ? (deep ? 4 : SR_R32) : (deep ? 2 : 4);
 }
 
+// Records of the threaded interpreter (gen_asm_interp.py): record 0 of a slot
+// = {slot(0), xo(0)}, record i+1 = {slot(i+1), xo(i+1), imm(i), 0} where
+// slot(j) = 4*opcode(j) + 1024*(j&1) is instruction j's entry in the handler
+// table of its parity and xo(j) = feature(j) * rs_bytes the LDS byte offset of
+// its X operand; an (X[f], X[g]) immediate becomes g's byte offset.
+__global__ void __launch_bounds__(64) ti_records_kernel(const Ins<float>* __restrict__ prog,
+                                                        const int32_t* __restrict__ list_off, int nlist,
+                                                        uint32_t rs_bytes, uint4* __restrict__ rec) {
+  const int s = blockIdx.x, j = threadIdx.x;
+  if (s >= nlist || j >= kVProgMax) return;
+  const Ins<float>* p = prog + list_off[s];  // programs are followed by 64 OP_END of padding
+  const uint32_t c0 = p[j].code, c1 = p[j + 1].code;
+  const uint32_t op0 = c0 & 0xffu, op1 = c1 & 0xffu;
+  uint32_t imm = __float_as_uint(p[j].imm);
+  if (op0 >= (uint32_t)bin_opcode(V_XX, 0) && op0 < (uint32_t)bin_opcode(V_XX + 1, 0)) imm *= rs_bytes;
+  rec[(size_t)s * 64 + j + 1] = make_uint4(4u * op1 + 1024u * (uint32_t)((j + 1) & 1), (c1 >> 16) * rs_bytes, imm, 0u);
+  if (j == 0) rec[(size_t)s * 64] = make_uint4(4u * op0, (c0 >> 16) * rs_bytes, 0u, 0u);
+}
+
+hipError_t launch_ti_records(const Ins<float>* prog, const int32_t* list_off, int nlist,
+                             uint32_t rs_bytes, uint4* rec, hipStream_t stream) {
+  if (nlist <= 0) return hipSuccess;
+  hipLaunchKernelGGL(ti_records_kernel, dim3((unsigned)nlist), dim3(64), 0, stream, prog, list_off, nlist,
+                     rs_bytes, rec);
+  return hipGetLastError();
+}
+
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n, int nlist,
                    EvalPlan* p) {
   p->R = R;
