@@ -70,10 +70,13 @@ class RegMap:
         self.R = R
         b = 32
         # acc, tmp, the two X buffers (ping-pong: the X operand of the next
-        # instruction is read while this one runs), the XX second operand, slots
-        self.acc, self.tmp, self.xa, self.xb, self.x2 = b, b + R, b + 2 * R, b + 3 * R, b + 4 * R
-        self.slot = [b + (5 + k) * R for k in range(D)]
-        top = b + (5 + D) * R
+        # instruction is read while this one runs), slots. The XX second
+        # operand goes to tmp: the compiler emits every POP right before the
+        # AT/TA instruction that consumes tmp, so tmp is dead at an XX.
+        self.acc, self.tmp, self.xa, self.xb = b, b + R, b + 2 * R, b + 3 * R
+        self.x2 = self.tmp
+        self.slot = [b + (4 + k) * R for k in range(D)]
+        top = b + (4 + D) * R
         self.chk, self.lane = top, top + 1
         self.vstate_end = top + 2
         # SGPRs: scratch, table (2), target (2), trig flag (2), instruction
@@ -89,8 +92,7 @@ class RegMap:
     def vstate(self):
         """(name, first reg, count) of every VGPR state register group."""
         R = self.R
-        g = [("acc", self.acc, R), ("tmp", self.tmp, R), ("xa", self.xa, R), ("xb", self.xb, R),
-             ("x2", self.x2, R)]
+        g = [("acc", self.acc, R), ("tmp", self.tmp, R), ("xa", self.xa, R), ("xb", self.xb, R)]
         g += [(f"slot{k}", self.slot[k], R) for k in range(D)]
         g += [("chk", self.chk, 1), ("lane", self.lane, 1)]
         return g
@@ -202,7 +204,7 @@ def handler_bodies():
                 mk = ("chk = mark(s.tmp[r], chk); " if LL else "") + ("chk = mark(s.acc[r], chk); " if LR else "")
                 e = f"{f}(s.tmp[r], s.acc[r])"
             elif v == "XX":
-                e = f"{f}(s.{{X}}[r], s.x2[r])"
+                e = f"{f}(s.{{X}}[r], s.tmp[r])"  # second X operand read into tmp
             elif v == "XC":
                 e = f"{f}(s.{{X}}[r], imm)"
             else:  # CX
@@ -320,19 +322,29 @@ def build(hipcc, out_path, R, extra):
     def rec(par, k):
         return s.s_rec[par] + k
 
-    # Records (ti_records_kernel): record 0 of a tree = {slot(0), xo(0)}, record
-    # i+1 = {slot(i+1), xo(i+1), imm(i)} with slot(j) = 4*opcode(j) + 1024*(j&1)
-    # (table of instruction j's parity) and xo(j) the LDS byte offset of its X.
-    # Instruction i runs in parity (i&1) with record i+1 in that parity's SGPRs;
-    # it loads record i+2 into the other parity's SGPRs and X(i+1) into the
-    # other X buffer; everything it waits for was issued one instruction ago.
+    # Records (ti_records_kernel): record 0 of a tree = {h(0), xo(0)}, record
+    # i+1 = {h(i+1), xo(i+1), imm(i)} with h(j) the byte offset (from
+    # .Lsr_base) of instruction j's handler in the parity j&1 and xo(j) the LDS
+    # byte offset of its X operand. Instruction i runs in parity (i&1) with
+    # record i+1 in that parity's SGPRs; it loads record i+2 into the other
+    # parity's SGPRs and X(i+1) into the other X buffer, and jumps straight to
+    # the next handler: everything it waits for was issued one instruction ago.
     a(f"s_getpc_b64 s[{s.s_tbl}:{s.s_tbl + 1}]")
     a(".Lsr_pc_%=:")
-    a(f"s_add_u32 s{s.s_tbl}, s{s.s_tbl}, .Lsr_tbla_%=-.Lsr_pc_%=")
+    a(f"s_add_u32 s{s.s_tbl}, s{s.s_tbl}, .Lsr_base_%=-.Lsr_pc_%=")
     a(f"s_addc_u32 s{s.s_tbl + 1}, s{s.s_tbl + 1}, 0")
     a(f"s_mov_b32 s{s.s_bail}, 0")
-    a(f"s_add_u32 s{s.s_t}, s{s.s_tbl}, 2048")  # both tables in one 4 GiB page:
-    a("s_cbranch_scc1 .Lsr_bail_%=")           # the target's high word is constant
+    # the handler offsets were measured on a standalone assembly of this text:
+    # check two of them against the assembled layout, else run the C++ path
+    # (biased by 2^20 so that no value is an inline constant: sizes are fixed)
+    a(f"s_mov_b32 s{s.s_t}, .Lsr_h_end_%=-.Lsr_base_%=+0x100000")
+    a(f"s_cmp_lg_u32 s{s.s_t}, @HOFF_END@")
+    a("s_cbranch_scc1 .Lsr_bail_%=")
+    a(f"s_mov_b32 s{s.s_t}, .Lsr_done_%=-.Lsr_base_%=+0x100000")
+    a(f"s_cmp_lg_u32 s{s.s_t}, @HOFF_DONE@")
+    a("s_cbranch_scc1 .Lsr_bail_%=")
+    a(f"s_add_u32 s{s.s_t}, s{s.s_tbl}, @SPAN@")  # the block in one 4 GiB page:
+    a("s_cbranch_scc1 .Lsr_bail_%=")             # the target's high word is constant
     a(f"s_mov_b32 s{s.s_tgt + 1}, s{s.s_tbl + 1}")
     a(f"s_load_dwordx4 s[{rec('b', 0)}:{rec('b', 3)}], s[{s.s_rbase}:{s.s_rbase + 1}], 0x0")
     a(f"s_load_dwordx4 s[{rec('a', 0)}:{rec('a', 3)}], s[{s.s_rbase}:{s.s_rbase + 1}], 0x10")
@@ -340,17 +352,10 @@ def build(hipcc, out_path, R, extra):
     a("s_waitcnt lgkmcnt(0)")
     a(f"v_add_u32_e32 v0, s{rec('b', 1)}, v{s.lane}")
     lds_read(s.xa, 0)
-    a(f"s_and_b32 s{s.s_t}, s{rec('b', 0)}, 0x7fc")
+    a(f"s_and_b32 s{s.s_t}, s{rec('b', 0)}, @MASK@")
     a(f"s_add_u32 s{s.s_tgt}, s{s.s_tbl}, s{s.s_t}")
     a(f"s_setpc_b64 s[{s.s_tgt}:{s.s_tgt + 1}]")
-    # tables: A = handlers of even instructions (X in xa), B = odd (X in xb);
-    # entry k of table P at +4k (+1024 for B) is `s_branch handler(k, P)`
-    for par in ("a", "b"):
-        a(f".Lsr_tbl{par}_%=:")
-        handled = {code: n for code, p_, n, *_ in variants if p_ == par}
-        handled[OP_END] = "end"
-        for code in range(256):
-            a(f"s_branch .Lsr_h_{handled[code]}_%=" if code in handled else "s_branch .Lsr_bail_%=")
+    a(".Lsr_base_%=:")
     a(".Lsr_h_end_%=:")
     a("s_branch .Lsr_done_%=")
     a(".Lsr_bail_%=:")
@@ -369,8 +374,8 @@ def build(hipcc, out_path, R, extra):
         a(f"s_add_u32 s{s.s_roff}, s{s.s_roff}, 16")
         a(f"v_add_u32_e32 v0, s{rec(par, 1)}, v{s.lane}")
         lds_read(xother, 0)  # X operand of the NEXT instruction (offset 0 if none)
-        a(f"s_and_b32 s{s.s_t}, s{rec(par, 0)}, 0x7fc")  # next table slot (masked: never
-        a(f"s_add_u32 s{s.s_tgt}, s{s.s_tbl}, s{s.s_t}")   # a jump outside the tables)
+        a(f"s_and_b32 s{s.s_t}, s{rec(par, 0)}, @MASK@")  # next handler (masked: never
+        a(f"s_add_u32 s{s.s_tgt}, s{s.s_tbl}, s{s.s_t}")   # a jump outside the block)
         body_lines = list(bodies[n])
         while body_lines and body_lines[0].startswith("s_nop"):
             body_lines.pop(0)
@@ -382,6 +387,36 @@ def build(hipcc, out_path, R, extra):
         a(f"s_setpc_b64 s[{s.s_tgt}:{s.s_tgt + 1}]")
     a(".Lsr_done_%=:")
     a("s_waitcnt lgkmcnt(0)")  # the last record load and X prefetch may be in flight
+
+    # handler offsets from a standalone assembly of the block (same encoding)
+    handled = {(p_, code): n for code, p_, n, *_ in variants}
+    # placeholders large enough to be literals, then iterate to a fixed point
+    subst = {"@HOFF_END@": "0x1ffff0", "@HOFF_DONE@": "0x1ffff0", "@SPAN@": "0x1ffff0", "@MASK@": "0x1ffff0"}
+    for _ in range(4):
+        offs = label_offsets([_subst(ln, subst) for ln in T])
+        span = 1
+        while span < offs["done"] + 64:
+            span *= 2
+        new = {"@HOFF_END@": hex(offs["h_end"] + 0x100000), "@HOFF_DONE@": hex(offs["done"] + 0x100000),
+               "@SPAN@": hex(span), "@MASK@": hex(span - 4)}
+        if new == subst:
+            break
+        subst = new
+    else:
+        raise SystemExit("gen_asm_interp: handler layout did not converge")
+    T = [_subst(ln, subst) for ln in T]
+    if label_offsets(T) != offs:
+        raise SystemExit("gen_asm_interp: handler offsets changed after substitution")
+    hoff = []
+    for par in ("a", "b"):
+        for code in range(256):
+            n = "end" if code == OP_END else handled.get((par, code))
+            hoff.append(offs[f"h_{n}"] if n else offs["bail"])
+    hp = out_path.replace(".inc", "_hoff.h")
+    with open(hp, "w") as f:
+        f.write(f"// Generated by gen_asm_interp.py (R={R}): byte offset from the block's base of the\n"
+                "// handler of (parity, opcode), index parity*256 + opcode; unhandled = bail.\n#pragma once\n")
+        f.write(f"#define SR_TI_HOFF_INIT {{{', '.join(str(v) for v in hoff)}}}\n")
 
     # clobbers: every register the block writes besides its outputs
     outs_v = set(range(s.acc, s.acc + R)) | {s.chk}
@@ -408,6 +443,37 @@ def build(hipcc, out_path, R, extra):
     hdr.append(f"// handlers: {len(variants)} (+end, bail), VGPR temps {min(vtemp)}..{max(vtemp)}, "
                f"SGPR temps {sorted(stemp)}")
     open(out_path, "w").write("\n".join(hdr) + "\n")
+
+
+def _subst(ln, subst):
+    for k, v in subst.items():
+        ln = ln.replace(k, v)
+    return ln
+
+
+def label_offsets(T):
+    """Assemble the block standalone (labels made symbols) and return the offset
+    of every .Lsr_<name>_%= label from .Lsr_base_%=."""
+    txt = "\n".join(T).replace("%=", "0")
+    txt = re.sub(r"\.Lsr_", "srlab_", txt)
+    llvm = "/opt/rocm/lib/llvm/bin"
+    with tempfile.TemporaryDirectory() as td:
+        sp, op = os.path.join(td, "blk.s"), os.path.join(td, "blk.o")
+        open(sp, "w").write("\t.text\n" + txt + "\n")
+        r = subprocess.run([os.path.join(llvm, "clang"), "-x", "assembler", "-target", "amdgcn-amd-amdhsa",
+                            "-mcpu=gfx950", "-c", sp, "-o", op], capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stderr)
+            raise SystemExit("gen_asm_interp: standalone assembly failed")
+        r = subprocess.run([os.path.join(llvm, "llvm-objdump"), "-t", op], capture_output=True, text=True,
+                           check=True)
+    sym = {}
+    for ln in r.stdout.splitlines():
+        parts = ln.split()
+        if parts and parts[-1].startswith("srlab_"):
+            sym[parts[-1][len("srlab_"):-1]] = int(parts[0], 16)  # strip the trailing %= ("0")
+    base = sym["base_"]
+    return {k.rstrip("_"): v - base for k, v in sym.items()}
 
 
 if __name__ == "__main__":

@@ -101,10 +101,19 @@ static inline int variant_R(int dtype, bool deep) {
 }
 
 // Records of the threaded interpreter (gen_asm_interp.py): record 0 of a slot
-// = {slot(0), xo(0)}, record i+1 = {slot(i+1), xo(i+1), imm(i), 0} where
-// slot(j) = 4*opcode(j) + 1024*(j&1) is instruction j's entry in the handler
-// table of its parity and xo(j) = feature(j) * rs_bytes the LDS byte offset of
-// its X operand; an (X[f], X[g]) immediate becomes g's byte offset.
+// = {h(0), xo(0)}, record i+1 = {h(i+1), xo(i+1), imm(i), 0} where h(j) is the
+// byte offset (from the block's base) of instruction j's handler in the parity
+// j&1 and xo(j) = feature(j) * rs_bytes the LDS byte offset of its X operand;
+// an (X[f], X[g]) immediate becomes g's byte offset.
+#ifndef SR_R32
+#define SR_R32 8
+#endif
+#if SR_R32 == 16
+#include "gen/asm_interp_f32_r16_hoff.h"
+#else
+#include "gen/asm_interp_f32_r8_hoff.h"
+#endif
+__constant__ uint32_t c_ti_hoff[512] = SR_TI_HOFF_INIT;
 __global__ void __launch_bounds__(64) ti_records_kernel(const Ins<float>* __restrict__ prog,
                                                         const int32_t* __restrict__ list_off, int nlist,
                                                         uint32_t rs_bytes, uint4* __restrict__ rec) {
@@ -115,8 +124,8 @@ __global__ void __launch_bounds__(64) ti_records_kernel(const Ins<float>* __rest
   const uint32_t op0 = c0 & 0xffu, op1 = c1 & 0xffu;
   uint32_t imm = __float_as_uint(p[j].imm);
   if (op0 >= (uint32_t)bin_opcode(V_XX, 0) && op0 < (uint32_t)bin_opcode(V_XX + 1, 0)) imm *= rs_bytes;
-  rec[(size_t)s * 64 + j + 1] = make_uint4(4u * op1 + 1024u * (uint32_t)((j + 1) & 1), (c1 >> 16) * rs_bytes, imm, 0u);
-  if (j == 0) rec[(size_t)s * 64] = make_uint4(4u * op0, (c0 >> 16) * rs_bytes, 0u, 0u);
+  rec[(size_t)s * 64 + j + 1] = make_uint4(c_ti_hoff[256u * (uint32_t)((j + 1) & 1) + op1], (c1 >> 16) * rs_bytes, imm, 0u);
+  if (j == 0) rec[(size_t)s * 64] = make_uint4(c_ti_hoff[op0], (c0 >> 16) * rs_bytes, 0u, 0u);
 }
 
 hipError_t launch_ti_records(const Ins<float>* prog, const int32_t* list_off, int nlist,
