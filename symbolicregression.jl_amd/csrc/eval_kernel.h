@@ -66,6 +66,10 @@ __device__ __forceinline__ T tile_loss(const T (&acc)[R], const T (&yv)[R], cons
   return s0 + s1;
 }
 
+// Kernel mode of a MODE_LOSS launch whose loss is L2 (the default loss):
+// the tile epilogue is compiled for it instead of switching on a.loss.
+constexpr int kModeLossL2 = 2;
+
 template <typename T>
 __device__ __forceinline__ T qnan_v() { return __builtin_nan(""); }
 template <>
@@ -124,7 +128,7 @@ eval_kernel(EvalArgs<T> a) {
   using V = typename V16<T>::type;
   constexpr int N = V16<T>::N;
   const int rows = a.ntiles * TILE;
-  const int narr = a.nfeat + (MODE == MODE_LOSS ? (W ? 2 : 1) : 0);
+  const int narr = a.nfeat + (MODE != MODE_OUT ? (W ? 2 : 1) : 0);
   T* sX = reinterpret_cast<T*>(smem);
   T* sY = sX + (size_t)a.nfeat * rows;
   T* sW = sY + rows;
@@ -179,7 +183,7 @@ eval_kernel(EvalArgs<T> a) {
   // non-finite value. A wave that sees one marks the list slot in a.fail; the
   // row groups that reach the slot later skip it (their partial is the failure
   // marker). Flags are read one tree ahead; a stale 0 only costs the work.
-  constexpr bool EE = MODE == MODE_LOSS;
+  constexpr bool EE = MODE != MODE_OUT;
   auto ld_flag = [&](int slot) {
     return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   };
@@ -233,10 +237,16 @@ eval_kernel(EvalArgs<T> a) {
         T yv[R], wv[R];
         lds_rows<T, R>(sY + tl * TILE, lane, yv);
         if constexpr (W) lds_rows<T, R>(sW + tl * TILE, lane, wv);
-        if (tl < nt_valid - 1 || last_valid == TILE)
+        if constexpr (MODE == kModeLossL2) {  // L2 known at compile time: no loss switch
+          if (tl < nt_valid - 1 || last_valid == TILE)
+            lsum += tile_loss<SRHIP_LOSS_L2, W, false>(acc, yv, wv, lp, lane, TILE);
+          else
+            lsum += tile_loss<SRHIP_LOSS_L2, W, true>(acc, yv, wv, lp, lane, last_valid);
+        } else if (tl < nt_valid - 1 || last_valid == TILE) {
           lsum += tile_loss_any<W, false, T, R>(a.loss, acc, yv, wv, lp, lane, TILE);
-        else
+        } else {
           lsum += tile_loss_any<W, true, T, R>(a.loss, acc, yv, wv, lp, lane, last_valid);
+        }
         if (__builtin_amdgcn_ballot_w64(chk != chk) != 0) break;  // failed: the rest is moot
       }
     }
@@ -272,6 +282,10 @@ hipError_t launch_one(const EvalPlan& plan, const EvalArgs<T>& a, hipStream_t st
 template <typename T, int R, int D, int SET>
 hipError_t launch_rd(const EvalPlan& plan, const EvalArgs<T>& a, int mode, hipStream_t stream) {
   if (mode == MODE_OUT) return launch_one<T, R, D, SET, MODE_OUT, false>(plan, a, stream);
+  if (a.loss == SRHIP_LOSS_L2) {
+    if (a.w) return launch_one<T, R, D, SET, kModeLossL2, true>(plan, a, stream);
+    return launch_one<T, R, D, SET, kModeLossL2, false>(plan, a, stream);
+  }
   if (a.w) return launch_one<T, R, D, SET, MODE_LOSS, true>(plan, a, stream);
   return launch_one<T, R, D, SET, MODE_LOSS, false>(plan, a, stream);
 }
