@@ -288,11 +288,8 @@ void check_program_vs_dataset(const srhip_dataset* ds, const srhip_program* p) {
 // Threaded interpreter on/off (SRHIP_TI=0 disables it; built only when the
 // kernels were compiled with SR_TI).
 static bool ti_enabled() {
-  static const bool on = [] {
-    const char* e = std::getenv("SRHIP_TI");
-    return ti_compiled() && !(e && e[0] == '0');
-  }();
-  return on;
+  const char* e = std::getenv("SRHIP_TI");  // read per launch: tests compare both paths
+  return ti_compiled() && !(e && e[0] == '0');
 }
 
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
@@ -324,7 +321,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.list_off = a.list + (p->nlist_a + p->nlist_b);
     a.fail = mode == MODE_LOSS ? static_cast<uint32_t*>(c->fail.p) + (pass == 0 ? 0 : p->nlist_a) : nullptr;
     a.ti_rec = nullptr;
-    if (ti_enabled() && std::is_same<T, float>::value && pass == 0 && plan.opset == OPSET_BASIC) {
+    if (ti_enabled() && std::is_same<T, float>::value && pass == 0) {
       c->ti_rec.ensure((size_t)nlist * 64 * sizeof(uint4));
       HIP_CHECK(launch_ti_records(reinterpret_cast<const Ins<float>*>(a.prog), a.list_off, nlist,
                                   (uint32_t)(plan.ntiles * plan.tile * sizeof(T)),

@@ -24,9 +24,16 @@ namespace dev {
 #define SR_M1(name, f32, f64)                                              \
   __device__ __forceinline__ float name(float x) { return f32(x); }        \
   __device__ __forceinline__ double name(double x) { return f64(x); }
+// SRHIP_INLINE_ALL (the threaded interpreter's handler snippets,
+// gen_asm_interp.py): everything inline, a handler body cannot call.
+#ifdef SRHIP_INLINE_ALL
+#define SR_NOINLINE __attribute__((always_inline))
+#else
+#define SR_NOINLINE __attribute__((noinline))
+#endif
 #define SR_M1_OOL(name, f32, f64)                                                       \
-  __device__ __attribute__((noinline)) float name##_ool(float x) { return f32(x); }      \
-  __device__ __attribute__((noinline)) double name##_ool(double x) { return f64(x); }    \
+  __device__ SR_NOINLINE float name##_ool(float x) { return f32(x); }      \
+  __device__ SR_NOINLINE double name##_ool(double x) { return f64(x); }    \
   __device__ __forceinline__ float name(float x) { return name##_ool(x); }              \
   __device__ __forceinline__ double name(double x) { return name##_ool(x); }
 // f32 exp: OCML's expf is a 2^x kernel plus over/underflow selects; here the
@@ -72,10 +79,10 @@ SR_M1(m_trunc, truncf, trunc)
 SR_M1(m_fabs, fabsf, fabs)
 #undef SR_M1
 #undef SR_M1_OOL
-__device__ __attribute__((noinline)) float m_pow(float x, float y) { return powf(x, y); }
-__device__ __attribute__((noinline)) double m_pow(double x, double y) { return pow(x, y); }
-__device__ __attribute__((noinline)) float m_fmod(float x, float y) { return fmodf(x, y); }
-__device__ __attribute__((noinline)) double m_fmod(double x, double y) { return fmod(x, y); }
+__device__ SR_NOINLINE float m_pow(float x, float y) { return powf(x, y); }
+__device__ SR_NOINLINE double m_pow(double x, double y) { return pow(x, y); }
+__device__ SR_NOINLINE float m_fmod(float x, float y) { return fmodf(x, y); }
+__device__ SR_NOINLINE double m_fmod(double x, double y) { return fmod(x, y); }
 __device__ __forceinline__ float m_copysign(float x, float y) { return copysignf(x, y); }
 __device__ __forceinline__ double m_copysign(double x, double y) { return copysign(x, y); }
 __device__ __forceinline__ bool m_isinf(float x) { return __builtin_isinf(x); }
@@ -149,7 +156,7 @@ __device__ __forceinline__ float qnan<float>() { return __builtin_nanf(""); }
 // Base.mod for floats: r = rem(x, y) (= fmod, exact); r == 0 → copysign(r, y);
 // sign(r) != sign(y) → r + y; else r. Out of line (fmod loops).
 template <typename T>
-__device__ __attribute__((noinline)) T jl_mod(T x, T y) {
+__device__ SR_NOINLINE T jl_mod(T x, T y) {
   T r = m_fmod(x, y);
   T s = r + y;
   bool flip = (r > T(0)) != (y > T(0));
@@ -159,7 +166,7 @@ __device__ __attribute__((noinline)) T jl_mod(T x, T y) {
 
 // safe_pow, Operators.jl:38-46. Out of line (pow's special-case branches).
 template <typename T>
-__device__ __attribute__((noinline)) T safe_pow(T x, T y) {
+__device__ SR_NOINLINE T safe_pow(T x, T y) {
   const bool isint = (y == m_trunc(y));
   const bool bad = isint ? (y < T(0) && x == T(0))
                          : ((y > T(0) && x < T(0)) || (y < T(0) && x <= T(0)));

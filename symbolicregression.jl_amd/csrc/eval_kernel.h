@@ -166,8 +166,7 @@ eval_kernel(EvalArgs<T> a) {
   // The shallow variant keeps each tree's program in VGPRs (run_program_v);
   // the next tree's program is loaded while the current one runs.
   constexpr bool VP = SR_VP != 0 && D == kShallowSlots;
-  constexpr bool TI = SR_TI != 0 && std::is_same<T, float>::value && R == SR_R32 && D == kShallowSlots &&
-                      SET == OPSET_BASIC;
+  constexpr bool TI = SR_TI != 0 && std::is_same<T, float>::value && R == SR_R32 && D == kShallowSlots;
   auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
   // list_off is read through the constant address space: scalar loads (the
   // early-exit flag stores would otherwise make the compiler use vector loads)

@@ -55,9 +55,10 @@ VARIANTS = ["AX", "XA", "AC", "CA", "AT", "TA", "XX", "XC", "CX"]
 NUM_OPCODES = OP_BIN0 + len(VARIANTS) * NUM_BOPS
 D = 2  # stack slots of the shallow kernel (kShallowSlots)
 
-# Operators with handlers (the BASIC set of srhip_internal.h).
-H_BOPS = ["ADD", "SUB", "MUL", "DIV"]
-H_UOPS = ["NEG", "SQUARE", "CUBE", "EXP", "ABS", "LOG", "SQRT", "SIN", "COS"]
+# Operators with handlers: all but the five whose inline code is large
+# (pow, mod, atanh_clip's mod, gamma, tan): those bail to the C++ interpreter.
+H_BOPS = [b for b in BOPS if b not in ("POW", "MOD")]
+H_UOPS = [u for u in UOPS if u not in ("ATANH_CLIP", "GAMMA", "TAN")]
 LOSSY_UOPS = {"EXP", "TANH", "ATAN", "ERF", "ERFC", "SIGN", "INV"}
 LOSSY_LHS = {"POW", "GREATER", "LOGICAL_OR", "LOGICAL_AND", "MAX", "MIN"}
 LOSSY_RHS = {"DIV", "POW", "GREATER", "LOGICAL_OR", "LOGICAL_AND", "MOD", "MAX", "MIN"}
@@ -85,6 +86,7 @@ class RegMap:
         self.s_t, self.s_tbl, self.s_tgt, self.s_flag = 67, 68, 70, 74
         self.s_rec = {"a": 76, "b": 80}
         self.s_rbase, self.s_roff, self.s_bail = 84, 86, 87
+        self.s_exit = 72  # address of the block's exit (handlers are > 128 KiB apart)
 
     def imm_sgpr(self, par):
         return self.s_rec[par] + 2
@@ -103,7 +105,7 @@ class RegMap:
         for par in ("a", "b"):
             out += [(f"r{par}{k}", self.s_rec[par] + k) for k in range(4)]
         out += [("rbase0", self.s_rbase), ("rbase1", self.s_rbase + 1), ("roff", self.s_roff),
-                ("bail", self.s_bail)]
+                ("bail", self.s_bail), ("exit0", self.s_exit), ("exit1", self.s_exit + 1)]
         return out
 
 
@@ -112,7 +114,7 @@ class RegMap:
 
 def snippet_source(rm, handlers):
     R = rm.R
-    out = ['#include "interp.h"', "using namespace srhip; using namespace srhip::interp;",
+    out = ["#define SRHIP_INLINE_ALL 1", '#include "interp.h"', "using namespace srhip; using namespace srhip::interp;",
            "namespace {", "struct St {"]
     for name, base, cnt in rm.vstate():
         out.append(f"  float {name}[{cnt}];" if cnt > 1 else
@@ -211,7 +213,19 @@ def handler_bodies():
                 e = f"{f}(imm, s.{{X}}[r])"
             nx = v in ("AX", "XA", "XX", "XC", "CX")
             hs.append((code, f"b{b.lower()}_{v.lower()}", rows(f"{mk}s.acc[r] = {e};"), nx, v == "XX", False))
-    return hs
+    # code layout: the BASIC operator set (srhip_internal.h) first, so that the
+    # common handlers share instruction-cache lines; the rest after it
+    basic_u = {"NEG", "SQUARE", "CUBE", "EXP", "ABS", "LOG", "SQRT", "SIN", "COS"}
+    basic_b = {"ADD", "SUB", "MUL", "DIV"}
+
+    def is_basic(h):
+        u = h[1].upper()
+        if u in ("LDX", "LDC") or u.startswith(("PUSH", "POP")):
+            return True
+        if u.startswith("UN_"):
+            return u[3:] in basic_u
+        return u[1:].split("_")[0] in basic_b
+    return [h for h in hs if is_basic(h)] + [h for h in hs if not is_basic(h)]
 
 
 # ---------------------------------------------------------------------------
@@ -220,7 +234,7 @@ def handler_bodies():
 REG_V = re.compile(r"\bv(\d+)\b|\bv\[(\d+):(\d+)\]")
 REG_S = re.compile(r"\bs(\d+)\b|\bs\[(\d+):(\d+)\]")
 BAD = ("s_swappc", "s_setpc", "s_getpc", "scratch_", "buffer_", "global_", "flat_", "s_load", "s_store",
-       "s_buffer", "s_dcache", "s_endpgm", "s_sendmsg", "exec")
+       "s_buffer", "s_dcache", "s_endpgm", "s_sendmsg", "ds_", "s_waitcnt")
 
 
 def extract(asm_text, name):
@@ -334,6 +348,8 @@ def build(hipcc, out_path, R, extra):
     a(f"s_add_u32 s{s.s_tbl}, s{s.s_tbl}, .Lsr_base_%=-.Lsr_pc_%=")
     a(f"s_addc_u32 s{s.s_tbl + 1}, s{s.s_tbl + 1}, 0")
     a(f"s_mov_b32 s{s.s_bail}, 0")
+    a(f"s_add_u32 s{s.s_exit}, s{s.s_tbl}, .Lsr_done_%=-.Lsr_base_%=")
+    a(f"s_mov_b32 s{s.s_exit + 1}, s{s.s_tbl + 1}")
     # the handler offsets were measured on a standalone assembly of this text:
     # check two of them against the assembled layout, else run the C++ path
     # (biased by 2^20 so that no value is an inline constant: sizes are fixed)
@@ -357,10 +373,10 @@ def build(hipcc, out_path, R, extra):
     a(f"s_setpc_b64 s[{s.s_tgt}:{s.s_tgt + 1}]")
     a(".Lsr_base_%=:")
     a(".Lsr_h_end_%=:")
-    a("s_branch .Lsr_done_%=")
+    a(f"s_setpc_b64 s[{s.s_exit}:{s.s_exit + 1}]")
     a(".Lsr_bail_%=:")
     a(f"s_mov_b32 s{s.s_bail}, 1")
-    a("s_branch .Lsr_done_%=")
+    a(f"s_setpc_b64 s[{s.s_exit}:{s.s_exit + 1}]")
     for code, par, n, body, nx, nx2, trig in variants:
         other = "b" if par == "a" else "a"
         xother = s.xb if par == "a" else s.xa
@@ -383,8 +399,12 @@ def build(hipcc, out_path, R, extra):
             a(ln)
         if trig:
             a(f"s_cmp_lg_u64 s[{s.s_flag}:{s.s_flag + 1}], 0")
-            a("s_cbranch_scc1 .Lsr_bail_%=")
+            a(f"s_cbranch_scc1 .Lsr_tb_{n}_%=")
         a(f"s_setpc_b64 s[{s.s_tgt}:{s.s_tgt + 1}]")
+        if trig:  # bail stub within branch range
+            a(f".Lsr_tb_{n}_%=:")
+            a(f"s_mov_b32 s{s.s_bail}, 1")
+            a(f"s_setpc_b64 s[{s.s_exit}:{s.s_exit + 1}]")
     a(".Lsr_done_%=:")
     a("s_waitcnt lgkmcnt(0)")  # the last record load and X prefetch may be in flight
 
