@@ -6,6 +6,8 @@
 
 #include "kernels.h"
 
+#include <algorithm>
+
 namespace srhip {
 namespace {
 
@@ -160,6 +162,13 @@ bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_
   int ntg = (target_wg + p->nrg - 1) / p->nrg;
   const int max_groups = (nlist + 3) / 4;  // at least ~4 trees (one per wave) per group
   if (ntg > max_groups) ntg = max_groups;
+  // the group's partial slots live in LDS next to the row tile: with many
+  // trees and few tree groups (huge row counts) they bound the group size
+  const size_t lds_cap = 160 * 1024 - 16;
+  if (per_tile * nt + part_bytes > lds_cap) return false;
+  const int max_tpb = (int)std::min<size_t>((lds_cap - per_tile * nt) / part_bytes, 1 << 20);
+  const int min_groups = (nlist + max_tpb - 1) / max_tpb;
+  if (ntg < min_groups) ntg = min_groups;
   if (ntg < 1) ntg = 1;
   p->tpb = (nlist + ntg - 1) / ntg;
   p->ntg = (nlist + p->tpb - 1) / p->tpb;
