@@ -302,3 +302,25 @@ def test_million_rows_properties(gpu_ctx):
     kk = np.logical_and.reduce([p[2] for p in parts])
     assert np.array_equal(kk, ok)
     assert_close_conditioned(tot[m], sums[m], sp[m], rtol=1e-5, msg="sharded sums")
+
+
+@pytest.mark.gpu
+def test_wide_dataset_many_trees(gpu_ctx):
+    """Config #5 shape, reduced: 20 features make the row tile 43 KB of LDS and
+    15k trees in one tree group would overflow LDS with their partial slots —
+    the planner splits the group (regression: this raised UNSUPPORTED)."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    n, nf = 4_300_000, 20
+    rng = np.random.default_rng(5)
+    X = rng.standard_normal((nf, n), dtype=np.float32)
+    y = (2 * np.cos(X[3]) + X[0] * X[0] - 2).astype(np.float32)
+    trees = srhip.random_population(15000, o, nf, np.float32, seed=5, maxsize=5)
+    ds = srhip.Dataset(X, y)
+    losses, ok = srhip.eval_loss_batch_ok(trees, ds, o)
+    pick = np.linspace(0, len(trees) - 1, 40).astype(int)
+    sub = [trees[i] for i in pick]
+    flat = srhip.flatten(sub, o, dtype=np.float32)
+    _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, dtype=np.float32)
+    assert np.array_equal(ok[pick], ref_ok)
+    m = ref_ok & np.isfinite(ref_l)
+    assert np.allclose(losses[pick][m], ref_l[m], rtol=1e-5), (losses[pick][m], ref_l[m])
