@@ -49,6 +49,8 @@ def load(variant: str = "simd"):
     L.oracle_eval_grad_consts_f64.argtypes = [vp, vp, vp, i32, vp, i64, i32, vp, vp]
     L.oracle_eval_grad_consts_f64.restype = C.c_int
     L.oracle_max_threads.restype = C.c_int
+    L.oracle_set_noise.argtypes = [C.c_double, C.c_uint64]
+    L.oracle_set_noise.restype = None
     _libs[variant] = L
     return L
 
@@ -133,6 +135,12 @@ def eval_grad_consts(kind, arg, consts, X, nconst):
     grad = np.empty((max(nconst, 1), n))
     ok = L.oracle_eval_grad_consts_f64(_p(kind), _p(arg), _p(c), len(kind), _p(Xj), n, nfeat, _p(out), _p(grad))
     return out, grad[:nconst], bool(ok)
+
+
+def set_noise(eps: float, seed: int = 0, variant: str = "simd"):
+    """Test-only: multiply every float64 transcendental value by (1 + eps u),
+    u in [-1, 1) hashed from the operand and seed (0 = off); see sr_oracle.c."""
+    load(variant).oracle_set_noise(float(eps), int(seed) & (2**64 - 1))
 
 
 def max_threads() -> int:

@@ -30,8 +30,33 @@ int oracle_max_threads(void) {
 #define CAT_(a, b) a##b
 #define CAT(a, b) CAT_(a, b)
 
+/* Rounding-noise model for the parity tests' condition estimates (TEST
+ * INFRASTRUCTURE, default off): with eps > 0 every transcendental value of
+ * the float64 evaluator is multiplied by (1 + eps u), u in [-1, 1) a hash of
+ * the operand bits and the seed. Two correct evaluations of one tree may
+ * differ by each operator's error bound (<= 4 ulp for transcendentals), and
+ * a tree can amplify that far beyond what input perturbations show (cos of a
+ * cancellation); the tests take the spread of such noisy evaluations as the
+ * tolerance of a whole-tree comparison. */
+static double g_noise_eps = 0.0;
+static uint64_t g_noise_seed = 0;
+void oracle_set_noise(double eps, uint64_t seed) {
+  g_noise_eps = eps;
+  g_noise_seed = seed;
+}
+static inline double oracle_noise_f64(double v) {
+  if (g_noise_eps == 0.0) return v;
+  uint64_t h;
+  memcpy(&h, &v, 8);
+  h ^= g_noise_seed;
+  h ^= h >> 33; h *= 0xff51afd7ed558ccdull; h ^= h >> 33; h *= 0xc4ceb9fe1a85ec53ull; h ^= h >> 33;
+  const double u = (double)(h >> 11) * (1.0 / 4503599627370496.0) - 1.0; /* [-1, 1) */
+  return v * (1.0 + g_noise_eps * u);
+}
+
 /* ---------------- T = float ---------------- */
 #define T float
+#define TNOISE(v) (v)
 #define SFX _f32
 #define TRUNC truncf
 #define FMOD fmodf
@@ -54,6 +79,7 @@ int oracle_max_threads(void) {
 #undef UOP_CASE
 #undef FOR_EACH_UOP
 #undef T
+#undef TNOISE
 #undef SFX
 #undef TRUNC
 #undef FMOD
@@ -66,6 +92,7 @@ int oracle_max_threads(void) {
 
 /* ---------------- T = double ---------------- */
 #define T double
+#define TNOISE(v) oracle_noise_f64(v)
 #define SFX _f64
 #define TRUNC trunc
 #define FMOD fmod

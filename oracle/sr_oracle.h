@@ -77,6 +77,8 @@ int oracle_eval_grad_consts_f64(const uint8_t* kind, const uint16_t* arg,
                                 double* out, double* grad);
 
 int oracle_max_threads(void);
+/* test-only rounding-noise model of the float64 evaluator (sr_oracle.c) */
+void oracle_set_noise(double eps, uint64_t seed);
 
 #ifdef __cplusplus
 }

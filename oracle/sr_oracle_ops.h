@@ -7,8 +7,9 @@
  * what Julia's Base does for Float32 trig/exp/log (Float64 kernels) and what
  * SpecialFunctions does for Float32 gamma/erf (promote, evaluate, convert).
  *
- * Expected macros: T, SFX (suffix token), and the libm function mapping
- * MF(name) that evaluates name in double and rounds to T.
+ * Expected macros: T, SFX (suffix token), and TNOISE(v): the identity, except
+ * in the float64 build while a test has set a rounding-noise amplitude
+ * (oracle_set_noise, sr_oracle.c) to estimate a tree's condition.
  */
 
 static inline T CAT(b_add, SFX)(T x, T y) { return x + y; }
@@ -24,7 +25,7 @@ static inline T CAT(b_pow, SFX)(T x, T y) {
     if (y > (T)0 && x < (T)0) return (T)NAN;
     if (y < (T)0 && x <= (T)0) return (T)NAN;
   }
-  return (T)pow((double)x, (double)y);
+  return TNOISE((T)pow((double)x, (double)y));
 }
 /* greater / logical_or / logical_and, Operators.jl:94-111 */
 static inline T CAT(b_greater, SFX)(T x, T y) { return x > y ? (T)1 : (T)0; }
@@ -55,33 +56,33 @@ static inline T CAT(b_min, SFX)(T x, T y) {
 static inline T CAT(u_neg, SFX)(T x) { return -x; }
 static inline T CAT(u_square, SFX)(T x) { return x * x; }
 static inline T CAT(u_cube, SFX)(T x) { return (x * x) * x; } /* literal_pow x^3 = x*x*x */
-static inline T CAT(u_exp, SFX)(T x) { return (T)exp((double)x); }
+static inline T CAT(u_exp, SFX)(T x) { return TNOISE((T)exp((double)x)); }
 static inline T CAT(u_abs, SFX)(T x) { return FABS(x); }
-static inline T CAT(u_log, SFX)(T x) { return x <= (T)0 ? (T)NAN : (T)log((double)x); }
-static inline T CAT(u_log2, SFX)(T x) { return x <= (T)0 ? (T)NAN : (T)log2((double)x); }
-static inline T CAT(u_log10, SFX)(T x) { return x <= (T)0 ? (T)NAN : (T)log10((double)x); }
-static inline T CAT(u_log1p, SFX)(T x) { return x <= (T)-1 ? (T)NAN : (T)log1p((double)x); }
+static inline T CAT(u_log, SFX)(T x) { return x <= (T)0 ? (T)NAN : TNOISE((T)log((double)x)); }
+static inline T CAT(u_log2, SFX)(T x) { return x <= (T)0 ? (T)NAN : TNOISE((T)log2((double)x)); }
+static inline T CAT(u_log10, SFX)(T x) { return x <= (T)0 ? (T)NAN : TNOISE((T)log10((double)x)); }
+static inline T CAT(u_log1p, SFX)(T x) { return x <= (T)-1 ? (T)NAN : TNOISE((T)log1p((double)x)); }
 static inline T CAT(u_sqrt, SFX)(T x) { return x < (T)0 ? (T)NAN : SQRT(x); }
-static inline T CAT(u_sin, SFX)(T x) { return (T)sin((double)x); }
-static inline T CAT(u_cos, SFX)(T x) { return (T)cos((double)x); }
-static inline T CAT(u_tan, SFX)(T x) { return (T)tan((double)x); }
-static inline T CAT(u_sinh, SFX)(T x) { return (T)sinh((double)x); }
-static inline T CAT(u_cosh, SFX)(T x) { return (T)cosh((double)x); }
-static inline T CAT(u_tanh, SFX)(T x) { return (T)tanh((double)x); }
-static inline T CAT(u_atan, SFX)(T x) { return (T)atan((double)x); }
-static inline T CAT(u_asinh, SFX)(T x) { return (T)asinh((double)x); }
-static inline T CAT(u_acosh, SFX)(T x) { return x < (T)1 ? (T)NAN : (T)acosh((double)x); }
+static inline T CAT(u_sin, SFX)(T x) { return TNOISE((T)sin((double)x)); }
+static inline T CAT(u_cos, SFX)(T x) { return TNOISE((T)cos((double)x)); }
+static inline T CAT(u_tan, SFX)(T x) { return TNOISE((T)tan((double)x)); }
+static inline T CAT(u_sinh, SFX)(T x) { return TNOISE((T)sinh((double)x)); }
+static inline T CAT(u_cosh, SFX)(T x) { return TNOISE((T)cosh((double)x)); }
+static inline T CAT(u_tanh, SFX)(T x) { return TNOISE((T)tanh((double)x)); }
+static inline T CAT(u_atan, SFX)(T x) { return TNOISE((T)atan((double)x)); }
+static inline T CAT(u_asinh, SFX)(T x) { return TNOISE((T)asinh((double)x)); }
+static inline T CAT(u_acosh, SFX)(T x) { return x < (T)1 ? (T)NAN : TNOISE((T)acosh((double)x)); }
 /* atanh_clip(x) = atanh(mod(x + 1, 2) - 1), Operators.jl:14 */
 static inline T CAT(u_atanh_clip, SFX)(T x) {
   T m = CAT(b_mod, SFX)(x + (T)1, (T)2) - (T)1;
-  return (T)atanh((double)m);
+  return TNOISE((T)atanh((double)m));
 }
-static inline T CAT(u_erf, SFX)(T x) { return (T)erf((double)x); }
-static inline T CAT(u_erfc, SFX)(T x) { return (T)erfc((double)x); }
+static inline T CAT(u_erf, SFX)(T x) { return TNOISE((T)erf((double)x)); }
+static inline T CAT(u_erfc, SFX)(T x) { return TNOISE((T)erfc((double)x)); }
 /* gamma: Inf → NaN, Operators.jl:8-11 (check made on the T result) */
 static inline T CAT(u_gamma, SFX)(T x) {
   T g = (T)tgamma((double)x);
-  return ISINF(g) ? (T)NAN : g;
+  return ISINF(g) ? (T)NAN : TNOISE(g);
 }
 static inline T CAT(u_relu, SFX)(T x) { return (x + FABS(x)) / (T)2; } /* :100-102 */
 static inline T CAT(u_round, SFX)(T x) { return RINT(x); }             /* RoundNearest */

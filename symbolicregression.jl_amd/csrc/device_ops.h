@@ -39,17 +39,16 @@ namespace dev {
 // f32 exp: OCML's expf is a 2^x kernel plus over/underflow selects; here the
 // argument is clamped first (exp(89) = Inf and exp(-104) rounds to 0 like the
 // unclamped value; NaN/Inf operands fail the tree before the value is used,
-// exp being checked as lossy) and the selects go. x*log2(e) is carried as
-// hi + lo so that the reduced argument is accurate to ~2^-35; v_exp_f32 then
-// v_ldexp. Validated exhaustively against the correctly rounded value on
-// MI355X (tools/check_fast_exp.hip): see DESIGN.md §4.
+// exp being checked as lossy) and the selects go. e = rint(x log2 e); the
+// reduced argument a = x log2(e) - e comes from two FMAs (log2 e as hi + lo,
+// |error| <= 2^-25), then v_exp_f32(a) and v_ldexp by e: 8 VALU. Validated
+// exhaustively against the correctly rounded value on MI355X: <= 1 ulp over
+// every float (tools/check_fast_exp.hip), as OCML's expf.
 __device__ __forceinline__ float fast_exp_f32(float x) {
   x = __builtin_amdgcn_fmed3f(x, -104.0f, 89.0f);
-  const float ph = x * 1.44269502e+00f;
-  float pl = __builtin_fmaf(x, 1.44269502e+00f, -ph);
-  pl = __builtin_fmaf(x, 1.92596299e-08f, pl);
-  const float e = __builtin_rintf(ph);
-  const float a = (ph - e) + pl;
+  const float e = __builtin_rintf(x * 1.44269502e+00f);
+  float a = __builtin_fmaf(x, 1.44269502e+00f, -e);
+  a = __builtin_fmaf(x, 1.92596299e-08f, a);
   return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(a), (int)e);
 }
 __device__ __forceinline__ float m_exp(float x) { return fast_exp_f32(x); }
@@ -90,37 +89,43 @@ __device__ __forceinline__ bool m_isinf(double x) { return __builtin_isinf(x); }
 __device__ __forceinline__ bool m_signbit(float x) { return __builtin_signbit(x); }
 __device__ __forceinline__ bool m_signbit(double x) { return __builtin_signbit(x); }
 // ---- fast single-precision sin / cos ------------------------------------------
-// Branch-free: 3-part Cody–Waite reduction by π/2 with FMA (exact enough for
-// |x| ≤ 105615) and minimax polynomials on [-π/4, π/4]; both polynomials are
-// evaluated and the quadrant selects. Validated exhaustively on the CPU against
-// correctly rounded values: ≤ 2 ulp over all floats with |x| ≤ 105615
-// (tools/check_fast_trig.c). Larger finite arguments are recomputed with OCML
-// behind a wave-uniform branch (taken only if some lane needs it).
-__device__ __forceinline__ float fast_sincos_f32(float x, int want_cos, float& qabs) {
-  const float q = __builtin_rintf(x * 0.636619772f);
-  qabs = __builtin_fabsf(q);
-  float r = __builtin_fmaf(q, -1.57079601e+00f, x);
-  r = __builtin_fmaf(q, -3.13916473e-07f, r);
-  r = __builtin_fmaf(q, -5.39030253e-15f, r);
-  const int i = (int)q + want_cos;
+// Branch-free, one polynomial: reduction by pi to r in [-pi/2, pi/2],
+//   sin x = (-1)^n sin(x - n pi),             n = rint(x / pi),
+//   cos x = (-1)^(n+1) sin(x - (n + 1/2) pi),  n = rint(x / pi - 1/2),
+// r = x - m pi/2 with m = 2n (sin) or 2n + 1 (cos) by a 3-part Cody–Waite
+// split of pi/2 with FMA (exact enough for |x| <= 105615), then
+// sin r = r + r^3 P(r^2), P a degree-3 minimax fit (tools/fit_sin.py, 6e-9
+// relative), and the sign from n's parity as one XOR (cos folds its extra
+// minus into the last FMA). 16 VALU per value for cos, where evaluating both
+// quadrant polynomials and selecting took 22. Validated exhaustively on the
+// CPU against correctly rounded values: <= 2 ulp over all floats with
+// |x| <= 105615 (tools/check_fast_trig.c). Larger finite arguments are
+// recomputed with OCML behind a wave-uniform branch (taken only if some lane
+// needs it); `nabs` = |n| feeds that test.
+__device__ __forceinline__ float fast_sincos_f32(float x, int want_cos, float& nabs) {
+  const float n = want_cos ? __builtin_rintf(__builtin_fmaf(x, 0.318309873f, -0.5f))
+                           : __builtin_rintf(x * 0.318309873f);
+  nabs = __builtin_fabsf(n);
+  const float m = want_cos ? __builtin_fmaf(n, 2.0f, 1.0f) : n + n;
+  float r = __builtin_fmaf(m, -1.57079601e+00f, x);
+  r = __builtin_fmaf(m, -3.13916473e-07f, r);
+  r = __builtin_fmaf(m, -5.39030253e-15f, r);
   const float s = r * r;
-  float pc = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.44331571e-5f, s, -1.38873163e-3f), s,
-                                           4.16666457e-2f), s, -5.00000000e-1f);
-  pc = __builtin_fmaf(pc, s, 1.0f);
-  float ps = __builtin_fmaf(__builtin_fmaf(-1.95152959e-4f, s, 8.33216087e-3f), s, -1.66666546e-1f);
-  ps = __builtin_fmaf(ps * s, r, r);
-  const float t = (i & 1) ? pc : ps;
-  return (i & 2) ? -t : t;
+  float p = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.606342605e-06f, s, -1.980987436e-04f), s,
+                                          8.333070204e-03f), s, -1.666665971e-01f);
+  p = p * s;
+  const float v = want_cos ? __builtin_fmaf(p, -r, -r) : __builtin_fmaf(p, r, r);
+  return __int_as_float(__float_as_int(v) ^ ((int)n << 31));
 }
 
 __device__ __forceinline__ float fast_sincos_f32(float x, int want_cos) {
-  float qa;
-  return fast_sincos_f32(x, want_cos, qa);
+  float na;
+  return fast_sincos_f32(x, want_cos, na);
 }
-// Fast-path domain test from the quadrant index: |q| <= kTrigQMax implies
-// |x| < 105300 (inside the validated range). max() ignores NaN rows (their
-// result is NaN either way); an Inf argument gives q = Inf and takes OCML.
-constexpr float kTrigQMax = 67000.0f;
+// Fast-path domain test from n: |n| <= kTrigQMax implies |x| < 105250 (inside
+// the validated range). max() ignores NaN rows (their result is NaN either
+// way); an Inf argument gives n = Inf and takes OCML.
+constexpr float kTrigQMax = 33500.0f;
 
 // The fallback is taken with a wave-uniform branch (ballot) and a select, so
 // no divergent region enters the interpreter's dispatch switch.

@@ -118,10 +118,11 @@ __device__ __forceinline__ T tile_loss_any(int lk, const T (&acc)[R], const T (&
 // Occupancy floor of the shallow f32 variant: 5 waves per SIMD (<= 96 VGPRs;
 // the LDS row tile allows 6 workgroups per CU). Without it the compiler
 // settles at 97-104 VGPRs and 4 waves.
-template <typename T, int D>
-constexpr int kWavesPerEU = (sizeof(T) == 4 && D == kShallowSlots) ? 5 : 1;
+// (R = 16 pins 130 VGPRs of threaded-interpreter state: 3 waves.)
+template <typename T, int R, int D>
+constexpr int kWavesPerEU = (sizeof(T) == 4 && D == kShallowSlots) ? (R > 8 ? 3 : 5) : 1;
 template <typename T, int R, int D, int SET, int MODE, bool W>
-__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<T, D>)))
+__global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<T, R, D>)))
 eval_kernel(EvalArgs<T> a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int TILE = 64 * R;

@@ -6,7 +6,8 @@ x/(c - x) near a pole, exp of a large value...). The bar the engine must meet
 is per operator (bit-exact + - * /, ≤ 4 ulp transcendentals — checked
 directly by test_each_unary_operator / test_each_binary_operator); for whole
 trees the tests allow, per row, the spread the oracle itself shows when X and
-the constants are perturbed at the ulp scale of T.
+the constants are perturbed at the ulp scale of T and every transcendental
+value carries rounding noise of the per-operator bar (oracle.set_noise).
 """
 import numpy as np
 
@@ -16,6 +17,11 @@ import srhip
 # perturbation size: 4 ulp of T (a perturbation below 1 ulp of float64 would
 # round away when applied in float64)
 EPS = {np.dtype(np.float32): 4 * 2.0 ** -23, np.dtype(np.float64): 4 * 2.0 ** -52}
+# rounding noise on every transcendental value (oracle.set_noise): the engine's
+# per-operator bar is <= 4 ulp, so two correct evaluations of one tree may
+# differ by what noise of that size does to it (rounding INSIDE the tree,
+# which input perturbations do not model: cos of a cancellation, exp chains)
+OP_EPS = {np.dtype(np.float32): 4 * 2.0 ** -24, np.dtype(np.float64): 4 * 2.0 ** -53}
 
 
 def _perturbed(flat, X, T, k, rng):
@@ -43,9 +49,13 @@ def output_spread_flat(flat, X, T, nperturb=3, seed=0):
     base, _ = oracle.eval_trees(flat, X.astype(np.float64), dtype=np.float64)
     spread = np.zeros_like(base)
     with np.errstate(invalid="ignore", over="ignore"):
-        for _ in range(nperturb):
+        for k in range(nperturb):
             fp, Xp = _perturbed(flat, X, T, 1, rng)
-            pert, _ = oracle.eval_trees(fp, Xp, dtype=np.float64)
+            oracle.set_noise(OP_EPS[np.dtype(T)], seed * 1000 + k + 1)
+            try:
+                pert, _ = oracle.eval_trees(fp, Xp, dtype=np.float64)
+            finally:
+                oracle.set_noise(0.0)
             d = np.abs(pert - base)
             spread = np.where(np.isfinite(d), np.maximum(spread, d), np.inf)
     return spread
@@ -70,9 +80,13 @@ def loss_spread_flat(flat, X, y, w, T, loss, nperturb=3, seed=0):
                                         dtype=np.float64)
     spread = np.zeros_like(base)
     with np.errstate(invalid="ignore", over="ignore"):
-        for _ in range(nperturb):
+        for k in range(nperturb):
             fp, Xp = _perturbed(flat, X, T, 1, rng)
-            pert, _, _ = oracle.eval_loss_batch(fp, Xp, y64, w64, loss.kind, loss.params, dtype=np.float64)
+            oracle.set_noise(OP_EPS[np.dtype(T)], seed * 1000 + k + 1)
+            try:
+                pert, _, _ = oracle.eval_loss_batch(fp, Xp, y64, w64, loss.kind, loss.params, dtype=np.float64)
+            finally:
+                oracle.set_noise(0.0)
             d = np.abs(pert - base)
             spread = np.where(np.isfinite(d), np.maximum(spread, d), np.inf)
     return spread

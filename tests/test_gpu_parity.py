@@ -81,6 +81,10 @@ def test_random_trees_f32_outputs(gpu_ctx, n):
             assert np.array_equal(out[t], ref[t]), f"tree {t} not bit-exact: {srhip.string_tree(tree, o)}"
             exact += 1
         else:
+            # the spread includes per-operator rounding noise: e.g. seed 3000's
+            # cos(cos(a / (cos(x5 / x4) - exp(x5)))) cancels to ~1e-4 in the
+            # denominator, so a 1-ulp cos difference (within the <= 4 ulp bar,
+            # test_each_unary_operator) moves cos(z) by O(1) on 3 of 3000 rows
             assert_close_conditioned(out[t], ref[t], spread[t], rtol=1e-5, atol=1e-6,
                                      msg=srhip.string_tree(tree, o))
     assert exact > 0

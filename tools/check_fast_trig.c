@@ -8,19 +8,27 @@
 #include <string.h>
 #include <stdlib.h>
 
+/* Reduction by pi to r in [-pi/2, pi/2] and one odd polynomial:
+ *   sin x = (-1)^n sin(x - n pi),            n = rint(x / pi)
+ *   cos x = (-1)^(n+1) sin(x - (n + 1/2) pi), n = rint(x / pi - 1/2)
+ * r = x - m pi/2 (m = 2n or 2n+1) by the 3-part Cody-Waite split of pi/2;
+ * sin r = r + r^3 P(r^2), P minimax of degree 3 (tools/fit_sin.py). */
 static float fast_sincos(float x, int want_cos) {
-  float q = rintf(x * 0.636619772f);
-  float r = fmaf(q, -1.57079601e+00f, x);
-  r = fmaf(q, -3.13916473e-07f, r);
-  r = fmaf(q, -5.39030253e-15f, r);
-  int i = (int)q + (want_cos ? 1 : 0);
-  float s = r * r;
-  float pc = fmaf(fmaf(fmaf(2.44331571e-5f, s, -1.38873163e-3f), s, 4.16666457e-2f), s, -5.00000000e-1f);
-  pc = fmaf(pc, s, 1.0f);
-  float ps = fmaf(fmaf(-1.95152959e-4f, s, 8.33216087e-3f), s, -1.66666546e-1f);
-  ps = fmaf(ps * s, r, r);
-  float t = (i & 1) ? pc : ps;
-  return (i & 2) ? -t : t;
+  const float n = want_cos ? rintf(fmaf(x, 0.318309873f, -0.5f)) : rintf(x * 0.318309873f);
+  const float m = want_cos ? fmaf(n, 2.0f, 1.0f) : n + n;
+  float r = fmaf(m, -1.57079601e+00f, x);
+  r = fmaf(m, -3.13916473e-07f, r);
+  r = fmaf(m, -5.39030253e-15f, r);
+  const float s = r * r;
+  float p = fmaf(fmaf(fmaf(2.606342605e-06f, s, -1.980987436e-04f), s, 8.333070204e-03f), s,
+                 -1.666665971e-01f);
+  p = p * s;
+  float v = want_cos ? fmaf(p, -r, -r) : fmaf(p, r, r);
+  uint32_t vb, sg = ((uint32_t)(int32_t)n) << 31;
+  memcpy(&vb, &v, 4);
+  vb ^= sg;
+  memcpy(&v, &vb, 4);
+  return v;
 }
 
 static int64_t ulp_dist(float a, float b) {
