@@ -7,6 +7,7 @@ so that parity tests read like the reference's own tests.
 """
 from . import constants
 from ._lib import SrhipError, Unsupported, lib
+from .constant_optimization import ConstOptResult, optimize_constants_batch
 from .dataset import Dataset
 from .engine import Context, DeviceDataset, Program, device_count, get_context
 from .interface import (compile_trees, compute_complexity, eval_grad_tree_array, eval_loss, eval_loss_batch,

@@ -1,0 +1,319 @@
+"""Batched constant optimisation on the device.
+
+The reference optimises one PopMember at a time
+(`optimize_constants`, src/ConstantOptimization.jl:22-65): Optim.Newton
+(one constant) or Optim.BFGS, both with LineSearches.BackTracking,
+`optimizer_iterations` = 8 (src/Options.jl:607-621), from x0 and from
+`optimizer_nrestarts` = 2 perturbed starts x0 .* (1 + randn/2) (:46-54); the
+best run is kept if Optim reports convergence, else the constants go back to
+x0 (:56-63). Every loss value is a full `eval_loss` (:12-19) and the
+gradient comes from finite differences of it.
+
+Here every start of every tree is one *candidate*, all candidates advance in
+lockstep, and each phase of the iteration is ONE engine launch over all of
+them: the constant vector of the compiled program is replaced
+(`srhip_program_set_constants`) and `srhip_eval_loss_grad` returns loss and
+the analytic forward-mode ∂L/∂c (or `srhip_eval_loss` for line-search trials).
+The per-candidate algebra (BFGS inverse-Hessian update, backtracking
+interpolation) is a few flops per constant and stays on the host.
+
+Deviations from Optim, all deliberate:
+* gradients are analytic (the engine's tangents), not finite differences;
+* Newton's Hessian (one constant) is the central difference of the analytic
+  gradient, made positive as PositiveFactorizations does for a 1×1 matrix;
+* `f_calls` counts loss evaluations (a loss+gradient launch counts once).
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Callable, List, Optional, Sequence, Tuple
+
+import numpy as np
+
+from .dataset import Dataset
+from .interface import eval_loss_batch
+from .node import Node, get_constants, set_constants
+from .options import Options
+
+# Optim.Options defaults the reference inherits (g_abstol = 1e-8; x/f tolerances 0).
+G_TOL = 1e-8
+# LineSearches.BackTracking defaults (c_1, ρ_hi, ρ_lo, order = 3, iterations = 1000).
+# Its iterations = 1000 is replaced by 60 shrinks: each shrink multiplies α by at
+# most ρ_hi, so after 60 the step is below 2⁻⁶⁰ of the search direction and no
+# longer changes x in Float64; a candidate still failing Armijo then is a failed
+# line search (LineSearchException → Optim stops, not converged).
+C1, RHO_HI, RHO_LO, LS_ITERATIONS = 1e-4, 0.5, 0.1, 60
+
+
+@dataclass
+class ConstOptResult:
+    """Per input tree: the loss after optimisation (the reference re-scores a
+    converged member, :56-60; else the loss at x0), Optim's convergence flag of
+    the best start, and the number of loss evaluations (num_evals)."""
+
+    losses: np.ndarray
+    converged: np.ndarray
+    num_evals: np.ndarray
+
+
+class EngineEvaluator:
+    """Loss / loss+gradient of all candidates in one launch each, through the
+    C ABI (srhip_program_set_constants + srhip_eval_loss[_grad])."""
+
+    def __init__(self, candidates: Sequence[Node], dataset: Dataset, options: Options,
+                 device: Optional[int] = None):
+        from .interface import compile_trees
+
+        self.dev = dataset.device(device)
+        self.prog = compile_trees(candidates, options, dataset.T, self.dev.ctx.device)
+        self.loss = options.elementwise_loss
+        self.T = dataset.T
+
+    def _set(self, consts: np.ndarray) -> None:
+        self.prog.set_constants(consts.astype(self.T, copy=False))
+
+    def loss_grad(self, consts: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
+        self._set(consts)
+        sums, grads, wsum, ok = self.prog.eval_loss_grad(self.dev, self.loss.kind, self.loss.params)
+        return _finish(sums, wsum, ok), _grad_finish(grads, wsum, ok, self.prog.flat.const_off)
+
+    def loss_only(self, consts: np.ndarray) -> np.ndarray:
+        self._set(consts)
+        sums, wsum, ok = self.prog.eval_loss(self.dev, self.loss.kind, self.loss.params)
+        return _finish(sums, wsum, ok)
+
+
+def _finish(sums, wsum, ok) -> np.ndarray:
+    with np.errstate(invalid="ignore", divide="ignore"):
+        f = sums / wsum
+    f = np.where(ok & np.isfinite(f), f, np.inf)
+    return f
+
+
+def _grad_finish(grads, wsum, ok, const_off) -> np.ndarray:
+    g = grads / wsum
+    bad = np.repeat(~ok, np.diff(const_off))
+    g[bad] = np.nan
+    return g
+
+
+def _backtrack_step(a1, a2, phi0, dphi0, phix0, phix1, first: bool) -> float:
+    """One BackTracking shrink (LineSearches.jl, order 3): quadratic
+    interpolation on the first shrink, cubic after, safeguarded to
+    [ρ_lo·α, ρ_hi·α]. Published algorithm: Nocedal & Wright §3.5."""
+    if first:
+        den = 2.0 * (phix1 - phi0 - dphi0 * a2)
+        at = -(dphi0 * a2 * a2) / den if den != 0 else np.nan
+    else:
+        div = 1.0 / (a1 * a1 * a2 * a2 * (a2 - a1))
+        r1 = phix1 - phi0 - dphi0 * a2
+        r0 = phix0 - phi0 - dphi0 * a1
+        a = (a1 * a1 * r1 - a2 * a2 * r0) * div
+        b = (-a1 ** 3 * r1 + a2 ** 3 * r0) * div
+        if abs(a) <= 1e-12 * max(1.0, abs(b)):
+            at = dphi0 / (2.0 * b) if b != 0 else np.nan
+        else:
+            d = max(b * b - 3.0 * a * dphi0, 0.0)
+            at = (-b + np.sqrt(d)) / (3.0 * a)
+    hi, lo = a2 * RHO_HI, a2 * RHO_LO
+    at = hi if not np.isfinite(at) else min(at, hi)  # NaNMath.min
+    return max(at, lo)
+
+
+def optimize_constants_batch(dataset: Dataset, trees: Sequence[Node], options: Options,
+                             rng: Optional[np.random.Generator] = None, device: Optional[int] = None,
+                             evaluator_factory: Optional[Callable] = None) -> ConstOptResult:
+    """`optimize_constants` for many trees at once. Trees are updated in place
+    (constants of the best start when it converged, else left at x0).
+    `evaluator_factory(candidates)` replaces the engine evaluator (tests use
+    it to run the same driver over the CPU oracle)."""
+    with np.errstate(all="ignore"):  # NaN/Inf losses and gradients are data here
+        return _optimize(dataset, trees, options, rng or np.random.default_rng(), device, evaluator_factory)
+
+
+def _optimize(dataset, trees, options, rng, device, evaluator_factory) -> ConstOptResult:
+    T = np.dtype(dataset.T).type
+    iterations = int(getattr(options, "optimizer_iterations", 8))
+    nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
+    algorithm = getattr(options, "optimizer_algorithm", "BFGS")
+    if algorithm == "NelderMead":
+        from ._lib import Unsupported
+
+        raise Unsupported(-2, "NelderMead is derivative-free; the engine batches BFGS/Newton only")
+    if algorithm != "BFGS":
+        raise ValueError("Optimization function not implemented.")  # :39-41
+
+    ntrees = len(trees)
+    x0s = [np.asarray(get_constants(t), dtype=T) for t in trees]
+    cand_tree: List[int] = []
+    cand_x: List[np.ndarray] = []
+    for i, x0 in enumerate(x0s):
+        if x0.size == 0:
+            continue
+        cand_tree.append(i)
+        cand_x.append(x0.copy())
+        for _ in range(nrestarts):  # :47
+            cand_tree.append(i)
+            cand_x.append((x0 * (T(1) + T(0.5) * rng.standard_normal(x0.size).astype(T))).astype(T))
+    losses = np.full(ntrees, np.inf)
+    converged_out = np.zeros(ntrees, dtype=bool)
+    num_evals = np.zeros(ntrees)
+    if not cand_tree:
+        return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory)
+                              if ntrees else losses, converged_out, num_evals)
+
+    cands = []
+    for i, x in zip(cand_tree, cand_x):
+        c = trees[i].copy()
+        set_constants(c, list(x))
+        cands.append(c)
+    ev = (evaluator_factory(cands) if evaluator_factory is not None
+          else EngineEvaluator(cands, dataset, options, device))
+
+    nc = len(cands)
+    sizes = np.array([x.size for x in cand_x])
+    off = np.concatenate([[0], np.cumsum(sizes)])
+    X = np.concatenate(cand_x).astype(T)
+    newton = sizes == 1
+    f_calls = np.zeros(nc)
+
+    def seg(v, k):
+        return v[off[k]:off[k + 1]]
+
+    f, G = ev.loss_grad(X)
+    f_calls += 1
+    invH = [np.eye(s) for s in sizes]
+    active = np.isfinite(f)
+    conv = np.zeros(nc, dtype=bool)
+    for k in range(nc):
+        if active[k] and np.max(np.abs(seg(G, k))) <= G_TOL:  # converged at x0
+            conv[k], active[k] = True, False
+
+    for _ in range(iterations):
+        if not active.any():
+            break
+        # search directions
+        S = np.zeros_like(X, dtype=np.float64)
+        if (newton & active).any():
+            h = np.zeros(nc)
+            step = np.where(newton & active, np.cbrt(np.finfo(T).eps) * np.maximum(1.0, np.abs(X[off[:-1]])), 0)
+            Xp, Xm = X.astype(np.float64).copy(), X.astype(np.float64).copy()
+            for k in np.nonzero(newton & active)[0]:
+                Xp[off[k]] += step[k]
+                Xm[off[k]] -= step[k]
+            _, Gp = ev.loss_grad(Xp.astype(T))
+            _, Gm = ev.loss_grad(Xm.astype(T))
+            for k in np.nonzero(newton & active)[0]:
+                h[k] = (Gp[off[k]] - Gm[off[k]]) / (2 * step[k])
+        for k in np.nonzero(active)[0]:
+            g = seg(G, k)
+            if newton[k]:
+                hk = abs(h[k]) if np.isfinite(h[k]) and abs(h[k]) > np.finfo(T).eps else 1.0
+                s = -g / hk
+            else:
+                s = -invH[k] @ g
+                if not np.dot(g, s) < 0:  # not a descent direction: restart from I
+                    invH[k] = np.eye(sizes[k])
+                    s = -g
+            S[off[k]:off[k + 1]] = s
+        dphi0 = np.array([np.dot(seg(G, k), seg(S, k)) if active[k] else 0.0 for k in range(nc)])
+        # a NaN gradient (or no descent at all) ends the run: Optim's x would turn NaN
+        active &= np.isfinite(dphi0) & (dphi0 < 0)
+
+        # BackTracking line search, all candidates in lockstep
+        a1 = np.ones(nc)
+        a2 = np.ones(nc)
+        phix0 = f.copy()
+        searching = active.copy()
+        Xbase = X.astype(np.float64)
+        alpha_full = np.repeat(a2, sizes)
+        trial = ev.loss_only((Xbase + alpha_full * S).astype(T))
+        f_calls += searching
+        phix1 = np.where(searching, trial, f)
+        finite_left = np.where(searching, int(-np.log2(np.finfo(T).eps)), 0)
+        first = np.ones(nc, dtype=bool)
+        ls_iter = np.zeros(nc, dtype=int)
+        while True:
+            shrink = np.zeros(nc, dtype=bool)
+            for k in np.nonzero(searching)[0]:
+                if not np.isfinite(phix1[k]):
+                    if finite_left[k] > 0:  # halve until the loss is finite
+                        finite_left[k] -= 1
+                        a1[k] = a2[k]
+                        a2[k] *= 0.5
+                        shrink[k] = True
+                    else:
+                        searching[k] = False
+                    continue
+                if phix1[k] <= f[k] + C1 * a2[k] * dphi0[k]:
+                    searching[k] = False
+                    continue
+                if ls_iter[k] >= LS_ITERATIONS:  # failed line search: stays at x
+                    searching[k] = False
+                    phix1[k] = np.inf
+                    continue
+                ls_iter[k] += 1
+                at = _backtrack_step(a1[k], a2[k], f[k], dphi0[k], phix0[k], phix1[k], first[k])
+                first[k] = False
+                a1[k] = a2[k]
+                a2[k] = at
+                shrink[k] = True
+            if not shrink.any():
+                break
+            alpha_full = np.repeat(a2, sizes)
+            trial = ev.loss_only(np.where(np.repeat(shrink, sizes), Xbase + alpha_full * S, Xbase).astype(T))
+            f_calls += shrink
+            phix0 = np.where(shrink, phix1, phix0)
+            phix1 = np.where(shrink, trial, phix1)
+
+        # accept, new gradient (one launch), BFGS update, convergence (Optim.converged)
+        moved = active & np.isfinite(phix1)
+        Xn = np.where(np.repeat(moved, sizes), Xbase + np.repeat(a2, sizes) * S, Xbase).astype(T)
+        fn, Gn = ev.loss_grad(Xn)
+        f_calls += moved
+        for k in np.nonzero(active)[0]:
+            if not moved[k] or not np.isfinite(fn[k]):
+                active[k] = False
+                continue
+            dx = seg(Xn, k).astype(np.float64) - seg(X, k).astype(np.float64)
+            dg = seg(Gn, k) - seg(G, k)
+            x_conv = np.max(np.abs(dx)) <= 0.0
+            f_conv = abs(fn[k] - f[k]) <= 0.0
+            g_conv = np.max(np.abs(seg(Gn, k))) <= G_TOL
+            if not newton[k]:
+                dxdg = float(np.dot(dx, dg))
+                if dxdg > 0:
+                    Hdg = invH[k] @ dg
+                    invH[k] = (invH[k] + (dxdg + dg @ Hdg) * np.outer(dx, dx) / dxdg ** 2
+                               - (np.outer(Hdg, dx) + np.outer(dx, Hdg)) / dxdg)
+            if x_conv or f_conv or g_conv:
+                conv[k], active[k] = True, False
+        keep = np.repeat(moved, sizes)
+        X = np.where(keep, Xn, X).astype(T)
+        G = np.where(keep, Gn, G)
+        f = np.where(moved & np.isfinite(fn), fn, f)
+
+    # best start per tree (:51-53), then the converged check (:56-63)
+    best = {}
+    for k, i in enumerate(cand_tree):
+        num_evals[i] += f_calls[k]
+        if i not in best or f[k] < f[best[i]]:
+            best[i] = k
+    for i, k in best.items():
+        if conv[k]:
+            set_constants(trees[i], [T(v) for v in seg(X, k)])
+            converged_out[i] = True
+            num_evals[i] += 1
+    return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory), converged_out,
+                          num_evals)
+
+
+def _final_losses(trees, dataset, options, device, factory) -> np.ndarray:
+    """Losses of the trees as they stand (one launch; the reference's
+    score_func re-score of a converged member, :58)."""
+    if factory is None:
+        return np.asarray(eval_loss_batch(trees, dataset, options, device=device), dtype=np.float64)
+    ev = factory(list(trees))
+    consts = [np.asarray(get_constants(t), dtype=np.float64) for t in trees]
+    X = np.concatenate(consts) if consts else np.zeros(0)
+    return ev.loss_only(X)

@@ -94,6 +94,11 @@ class Options:
         complexity_of_variables: Optional[float] = None,
         maxsize: int = 20,
         npopulations: int = 15,
+        optimizer_algorithm: str = "BFGS",
+        optimizer_nrestarts: int = 2,
+        optimizer_probability: float = 0.14,
+        optimizer_iterations: Optional[int] = None,
+        should_optimize_constants: bool = True,
         **_ignored,
     ):
         self.binary_operators: Tuple[str, ...] = tuple(_opname(o) for o in binary_operators)
@@ -108,6 +113,12 @@ class Options:
         self.turbo = bool(turbo)
         self.maxsize = maxsize
         self.npopulations = npopulations
+        # constant optimisation (src/Options.jl:360-364, 607-621: iterations default 8)
+        self.optimizer_algorithm = optimizer_algorithm
+        self.optimizer_nrestarts = int(optimizer_nrestarts)
+        self.optimizer_probability = float(optimizer_probability)
+        self.optimizer_iterations = 8 if optimizer_iterations is None else int(optimizer_iterations)
+        self.should_optimize_constants = bool(should_optimize_constants)
         self.nbin = len(self.binary_operators)
         self.nuna = len(self.unary_operators)
         # ComplexityMapping (src/OptionsStruct.jl:55-104): use when any is given

@@ -1,0 +1,139 @@
+"""Batched constant optimisation (srhip.optimize_constants_batch), the
+batched form of optimize_constants (src/ConstantOptimization.jl:22-65).
+
+CPU tests drive the same optimiser over the oracle (forward-mode gradients of
+the C restatement, L2 loss in fp64): known-answer recoveries in the spirit of
+test/test_optimizer_mutation.jl / test_derivatives.jl. GPU tests run it on the
+engine and compare with the oracle-driven run."""
+import numpy as np
+import pytest
+
+import oracle
+import srhip
+from srhip import Node
+
+
+class OracleEvaluator:
+    """Test-only evaluator: loss and ∂L/∂c of every candidate on the CPU oracle."""
+
+    def __init__(self, cands, options, X, y):
+        self.flat = srhip.flatten(cands, options, dtype=np.float64)
+        self.X, self.y = X.astype(np.float64), y.astype(np.float64)
+
+    def _one(self, t, c):
+        k, a, _ = self.flat.tree(t)
+        out, g, ok = oracle.eval_grad_consts(k, a, c, self.X, len(c))
+        if not ok:
+            return np.inf, np.full(len(c), np.nan)
+        r = out - self.y
+        return float(np.mean(r * r)), 2.0 * (g @ r) / len(r)
+
+    def loss_grad(self, consts):
+        co = self.flat.const_off
+        fs, gs = [], []
+        for t in range(self.flat.ntrees):
+            f, g = self._one(t, np.asarray(consts[co[t]:co[t + 1]], dtype=np.float64))
+            fs.append(f)
+            gs.append(g)
+        return np.asarray(fs), (np.concatenate(gs) if gs else np.zeros(0))
+
+    def loss_only(self, consts):
+        return self.loss_grad(consts)[0]
+
+
+def problem(T=np.float64, n=200, seed=1):
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((5, n)).astype(T)
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(T)
+    B, U = o.make_binary, o.make_unary
+    x1, x4 = Node("x1"), Node("x4")
+    three = B("+", B("+", B("*", Node(val=1.0), U("cos", x4)), B("*", Node(val=0.5), B("*", x1, x1))),
+              Node(val=0.0))
+    one = B("+", B("*", Node(val=0.7), U("cos", Node("x4"))), B("-", B("*", Node("x1"), Node("x1")),
+                                                                  Node(val=2.0)))
+    none = B("*", Node("x1"), Node("x1"))
+    return o, X, y, [three, one, none]
+
+
+def oracle_factory(o, X, y):
+    return lambda cands: OracleEvaluator(cands, o, X, y)
+
+
+def test_recovers_constants_on_oracle():
+    o, X, y, trees = problem()
+    ds = srhip.Dataset(X, y)
+    res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(0),
+                                         evaluator_factory=oracle_factory(o, X, y))
+    assert res.converged[0] and res.converged[1]
+    assert np.allclose(srhip.get_constants(trees[0]), [2.0, 1.0, -2.0], atol=1e-6)
+    assert np.allclose(srhip.get_constants(trees[1]), [2.0, 2.0], atol=1e-6)  # Newton path (1 constant)
+    assert res.losses[0] < 1e-10 and res.losses[1] < 1e-10
+    assert not res.converged[2] and res.num_evals[2] == 0  # no constants: untouched (:27-29)
+    assert res.num_evals[0] > 3 and res.num_evals[1] > 3
+
+
+def test_not_converged_keeps_x0():
+    """With one iteration nothing converges: constants go back to x0 (:61-63)."""
+    o, X, y, trees = problem()
+    o.optimizer_iterations = 1
+    x0 = [srhip.get_constants(t) for t in trees]
+    ds = srhip.Dataset(X, y)
+    res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(0),
+                                         evaluator_factory=oracle_factory(o, X, y))
+    assert not res.converged[0]
+    assert srhip.get_constants(trees[0]) == x0[0]
+
+
+def test_failing_tree_stays_failed():
+    o, X, y, _ = problem()
+    # exp(exp(c * x1)) overflows on every start → loss Inf, never converges
+    t = o.make_unary("exp", o.make_unary("exp", o.make_binary("*", Node(val=40.0), Node("x1"))))
+    ds = srhip.Dataset(X, y)
+    res = srhip.optimize_constants_batch(ds, [t], o, rng=np.random.default_rng(0),
+                                         evaluator_factory=oracle_factory(o, X, y))
+    assert not res.converged[0] and np.isinf(res.losses[0])
+    assert srhip.get_constants(t) == [40.0]
+
+
+def test_nelder_mead_is_unsupported():
+    o, X, y, trees = problem()
+    o.optimizer_algorithm = "NelderMead"
+    with pytest.raises(srhip.Unsupported):
+        srhip.optimize_constants_batch(srhip.Dataset(X, y), trees, o)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [np.float64, np.float32])
+def test_engine_optimizer_matches_oracle_driver(gpu_ctx, T):
+    o, X, y, trees = problem(T)
+    _, _, _, trees_ref = problem(T)
+    ds = srhip.Dataset(X, y)
+    res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(0))
+    ref = srhip.optimize_constants_batch(ds, trees_ref, o, rng=np.random.default_rng(0),
+                                         evaluator_factory=oracle_factory(o, X, y))
+    atol = 1e-6 if T == np.float64 else 2e-3
+    assert res.converged[1] and ref.converged[1]
+    for t, r in zip(trees, trees_ref):
+        assert np.allclose(srhip.get_constants(t), srhip.get_constants(r), atol=atol)
+    assert np.allclose(srhip.get_constants(trees[0]), [2.0, 1.0, -2.0], atol=atol)
+    assert res.losses[0] < (1e-10 if T == np.float64 else 1e-5)
+
+
+@pytest.mark.gpu
+def test_engine_optimizer_random_population(gpu_ctx):
+    """Random config-#2-style population: the optimiser never makes a loss
+    worse, and converged trees' losses are the engine's own eval_loss."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(256, o, 5, np.float32, seed=3)
+    rng = np.random.default_rng(2)
+    X = rng.standard_normal((5, 4000)).astype(np.float32)
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(np.float32)
+    ds = srhip.Dataset(X, y)
+    before = srhip.eval_loss_batch(trees, ds, o)
+    res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(0))
+    after = srhip.eval_loss_batch(trees, ds, o)
+    assert np.array_equal(np.isfinite(after), np.isfinite(res.losses))
+    m = np.isfinite(before)
+    assert np.all(after[m] <= before[m] * (1 + 1e-4) + 1e-9)
+    assert res.converged.any()
