@@ -54,19 +54,104 @@ def eval_tree_array(tree: TreeOrTrees, X: np.ndarray, options: Options, device: 
     return out, ok
 
 
+def _seed_features(tree: Node, plus: int, direction: Optional[int]):
+    """Copy of `tree` where every feature leaf x_f (only f == direction, when
+    given) becomes (x_f + c) with a new constant c = -0.0. x + (-0.0) == x for
+    every x (including ±0, ±Inf, NaN), so values and did_succeed are those of
+    the original tree, and ∂ŷ/∂x_f = Σ over the seeds of x_f of ∂ŷ/∂c.
+    Returns the copy and, per constant in get_constants order, the feature it
+    seeds (0 for the tree's own constants)."""
+    def rec(t: Node) -> Node:
+        if t.degree == 0:
+            if t.constant or (direction is not None and t.feature != direction):
+                return t.copy()
+            return Node(plus, Node(feature=t.feature), Node(val=-0.0))
+        if t.degree == 1:
+            return Node(t.op, rec(t.l))
+        return Node(t.op, rec(t.l), rec(t.r))
+
+    aug = rec(tree)
+    seeds: List[int] = []
+    _mark(aug, tree, seeds)
+    return aug, seeds
+
+
+def _mark(aug: Node, orig: Node, seeds: List[int]) -> None:
+    """Walk `aug` and the original tree together in post-order and list, per
+    constant of `aug`, the feature it seeds (0 = an original constant)."""
+    if orig.degree == 0:
+        if orig.constant:
+            seeds.append(0)
+        elif aug.degree == 2:  # seeded feature leaf: (x_f + c)
+            seeds.append(orig.feature)
+        return
+    _mark(aug.l, orig.l, seeds)
+    if orig.degree == 2:
+        _mark(aug.r, orig.r, seeds)
+
+
+def _feature_grads(trees: List[Node], X: np.ndarray, options: Options, direction: Optional[int],
+                   device: Optional[int]):
+    """(ŷ (ntrees, n), per tree ∂ŷ/∂x (nfeat, n) or, with direction, (n,), ok)."""
+    T = X.dtype if X.dtype in (np.float32, np.float64) else np.dtype(np.float64)
+    X = X.astype(T, copy=False)
+    nfeat, n = X.shape
+    if direction is not None and not 1 <= direction <= nfeat:
+        raise ValueError("direction must be a 1-based feature index")
+    binops = tuple(options.binary_operators)
+    if "+" in binops:
+        o, plus = options, binops.index("+") + 1
+    else:  # same operator indices, "+" appended for the seeds
+        o = Options(binary_operators=binops + ("+",), unary_operators=options.unary_operators)
+        plus = len(binops) + 1
+    augs, seeds = zip(*[_seed_features(t, plus, direction) for t in trees]) if trees else ((), ())
+    ctx = get_context(device)
+    ds = DeviceDataset(ctx, X, np.zeros(n, dtype=T))
+    prog = Program(ctx, flatten(list(augs), o, dtype=T), T)
+    val, grad, ok = prog.eval_grad_tree_array(ds)
+    co = prog.flat.const_off
+    out = []
+    for t, sd in enumerate(seeds):
+        g = grad[co[t]:co[t + 1]]
+        sd = np.asarray(sd, dtype=np.int64)
+        if direction is not None:
+            d = g[sd == direction].sum(axis=0, dtype=T) if (sd == direction).any() else np.zeros(n, dtype=T)
+            out.append(d.astype(T))
+        else:
+            G = np.zeros((nfeat, n), dtype=T)
+            for f in np.unique(sd[sd > 0]):
+                G[f - 1] = g[sd == f].sum(axis=0, dtype=T)
+            out.append(G)
+    return val, out, ok
+
+
+def eval_diff_tree_array(tree: TreeOrTrees, X: np.ndarray, options: Options, direction: int,
+                         device: Optional[int] = None):
+    """eval_diff_tree_array(tree, X, options, direction)
+    (src/InterfaceDynamicExpressions.jl:55-80): (output, ∂output/∂x_direction,
+    complete), forward mode on the engine (seeded-feature tangents)."""
+    trees, single = _as_list(tree)
+    val, d, ok = _feature_grads(trees, np.asarray(X), options, int(direction), device)
+    if single:
+        return val[0], d[0], bool(ok[0])
+    return val, d, ok
+
+
 def eval_grad_tree_array(tree: TreeOrTrees, X: np.ndarray, options: Options, variable: bool = False,
                          device: Optional[int] = None):
     """eval_grad_tree_array(tree, X, options; variable=false)
-    (src/InterfaceDynamicExpressions.jl:105-107): (output, gradient, complete)
+    (src/InterfaceDynamicExpressions.jl:83-107): (output, gradient, complete)
     with gradient[k, i] = ∂ŷ_i/∂c_k for the tree's constants in get_constants
-    order. For a list of trees: outputs (ntrees, n), a list of per-tree
-    gradient matrices, and a bool array."""
-    if variable:
-        from ._lib import Unsupported
-
-        raise Unsupported(-2, "derivatives with respect to X (variable=true) are not implemented by the engine")
+    order, or with variable=true gradient[f, i] = ∂ŷ_i/∂x_f (nfeatures × n).
+    For a list of trees: outputs (ntrees, n), a list of per-tree gradient
+    matrices, and a bool array."""
     trees, single = _as_list(tree)
     X = np.asarray(X)
+    if variable:
+        val, grads, ok = _feature_grads(trees, X, options, None, device)
+        if single:
+            return val[0], grads[0], bool(ok[0])
+        return val, grads, ok
     T = X.dtype if X.dtype in (np.float32, np.float64) else np.dtype(np.float64)
     ctx = get_context(device)
     ds = DeviceDataset(ctx, X.astype(T, copy=False), np.zeros(X.shape[1], dtype=T))
