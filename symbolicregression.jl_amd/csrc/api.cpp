@@ -292,6 +292,13 @@ static bool ti_enabled() {
   return ti_compiled() && !(e && e[0] == '0');
 }
 
+// Row-group rotation of the tree order, off by default (SRHIP_ROT=1 enables
+// it): measured 4.09 -> 4.15 ms on config #2.
+static bool rotate_enabled() {
+  const char* e = std::getenv("SRHIP_ROT");  // read per launch: A/B measurements
+  return e && e[0] == '1';
+}
+
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
 // n_pad) may be the dataset itself or a gathered row subset.
 template <typename T>
@@ -340,6 +347,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.tpb = plan.tpb;
     a.nrg = plan.nrg;
     a.loss = loss;
+    a.rotate = rotate_enabled() ? 1 : 0;
     a.lparam = (T)lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);

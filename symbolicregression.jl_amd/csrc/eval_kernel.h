@@ -189,17 +189,32 @@ eval_kernel(EvalArgs<T> a) {
   };
   uint32_t fnext = 0;
 
-  if (wave < a.tpb && slot_of(wave) < a.nlist) {
-    if constexpr (EE) fnext = ld_flag(slot_of(wave));
-    if constexpr (VP) vnext.load(prog_of(slot_of(wave)), lane);
+  // Each wave runs the trees i = wave + k·nwaves, k < m. With a.rotate the
+  // sequence starts at k = rot (row group rg at fraction rg/nrg of it): row
+  // groups then reach a tree at different times, so a failure found by one
+  // row group is skipped by the others that get there later (a tree that
+  // overflows on a few rows is otherwise evaluated by every row group at
+  // once). Each wave keeps its own set of trees: load balance is unchanged.
+  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
+  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
+  m = __builtin_amdgcn_readfirstlane(m);
+  const int rot = (EE && a.rotate && m > 1)
+                      ? __builtin_amdgcn_readfirstlane((int)(((int64_t)rg * m) / a.nrg))
+                      : 0;
+  auto idx_of = [&](int k) {
+    const int kk = k + rot < m ? k + rot : k + rot - m;
+    return wave + kk * nwaves;
+  };
+  if (m > 0) {
+    if constexpr (EE) fnext = ld_flag(slot_of(idx_of(0)));
+    if constexpr (VP) vnext.load(prog_of(slot_of(idx_of(0))), lane);
   }
-  for (int i0 = wave; i0 < a.tpb; i0 += nwaves) {
+  for (int k = 0; k < m; ++k) {
     // all wave-uniform: keep the schedule in SGPRs
-    const int i = __builtin_amdgcn_readfirstlane(i0);
+    const int i = __builtin_amdgcn_readfirstlane(idx_of(k));
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
-    if (s >= a.nlist) break;  // slot_of is increasing in i
-    const int s2 = __builtin_amdgcn_readfirstlane(slot_of(i + nwaves));
-    const bool more = i + nwaves < a.tpb && s2 < a.nlist;
+    const bool more = k + 1 < m;
+    const int s2 = __builtin_amdgcn_readfirstlane(more ? slot_of(idx_of(k + 1)) : s);
     VProg<T> vp;
     if constexpr (VP) {
       vp = vnext;

@@ -38,6 +38,7 @@ struct EvalArgs {
   int tpb;                 // trees per group
   int nrg;                 // row groups
   int loss;
+  int rotate;              // MODE_LOSS: start each wave's tree sequence at row-group-dependent offsets
   T lparam;
   Part<T>* partial;        // [nrg][ntg*tpb]
   T* out;                  // MODE_OUT: [ntrees][out_stride]
