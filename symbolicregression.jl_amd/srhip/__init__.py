@@ -19,6 +19,7 @@ from .node import (FlatTrees, Node, count_nodes, flatten, get_constants, has_con
 from .options import (HuberLoss, L1DistLoss, L1EpsilonInsLoss, L2DistLoss, L2EpsilonInsLoss, LogCoshLoss,
                       LogitDistLoss, LPDistLoss, Options, PeriodicLoss, QuantileLoss, SupervisedLoss,
                       extend_operators)
+from .search import HallOfFame, PopMember, equation_search, print_hall_of_fame
 from .trees import gen_random_tree, gen_random_tree_fixed_size, random_population
 
 __all__ = [n for n in dir() if not n.startswith("_")]
