@@ -171,9 +171,9 @@ def main():
         threads = args.cpu_threads or min(os.cpu_count() or 1, 16)
         fl = srhip.flatten(trees, options, dtype=T)
 
-        def run_cpu(nrows):
+        def run_cpu(nrows, variant="simd"):
             t_ = time.perf_counter()
-            oracle.eval_loss_batch(fl, X[:, :nrows], y[:nrows], dtype=T, nthreads=threads, variant="simd")
+            oracle.eval_loss_batch(fl, X[:, :nrows], y[:nrows], dtype=T, nthreads=threads, variant=variant)
             return time.perf_counter() - t_, float(fl.nodes.sum()) * nrows
 
         probe = min(args.rows, 10_000)
@@ -188,6 +188,10 @@ def main():
             "sample": f"all {len(trees)} trees x first {nrows} rows; oracle simd build (turbo=true analogue), "
                       f"OpenMP over trees; {dt:.1f} s",
         }
+        # turbo=false analogue (scalar build), a smaller sample
+        ns = max(probe, nrows // 3)
+        dts, nrs = run_cpu(ns, "scalar")
+        cpu["turbo_false"] = {"value": nrs / dts, "sample": f"first {ns} rows; oracle scalar build; {dts:.1f} s"}
 
     out = {
         "metric": METRIC if T == np.float32 else "node·row evals/sec (Float64)",
