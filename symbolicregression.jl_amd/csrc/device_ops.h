@@ -51,7 +51,45 @@ __device__ __forceinline__ float fast_exp_f32(float x) {
   a = __builtin_fmaf(x, 1.92596299e-08f, a);
   return __builtin_amdgcn_ldexpf(__builtin_amdgcn_exp2f(a), (int)e);
 }
+// SR_PRECISE_TRANSC (default 1): Float32 exp / sin / cos are evaluated in
+// Float64 and rounded once, as Julia does for Float32 arguments and as the
+// oracle does. A 1-ulp difference in one of them decides did_succeed when a
+// divisor cancels to exactly 0 on some row (4 of 4096 config #2
+// trees with the f32 routines); with one rounding of a ~2^-52-accurate value
+// the engine returns the correctly rounded Float32 except within ~2^-28 of a
+// rounding boundary. SR_PRECISE_TRANSC=0 builds the all-f32 routines.
+#ifndef SR_PRECISE_TRANSC
+#define SR_PRECISE_TRANSC 1
+#endif
+// e^x = 2^n e^r, n = rint(x log2 e), r = x - n ln2 (two-part ln2, exact
+// products for |n| <= 151), e^r by its Taylor series to r^12 (|r| <= 0.347:
+// truncation < 2^-47 relative), one v_ldexp_f64, one rounding to Float32.
+__device__ __forceinline__ float precise_exp_f32(float x) {
+  x = __builtin_amdgcn_fmed3f(x, -104.0f, 89.0f);
+  const double xd = (double)x;
+  const double n = __builtin_rint(xd * 1.4426950408889634);
+  double r = __builtin_fma(n, -6.93147180369123816490e-01, xd);
+  r = __builtin_fma(n, -1.90821492927058770002e-10, r);
+  double p = 2.08767569878680989792e-09;        // 1/12!
+  p = __builtin_fma(p, r, 2.50521083854417187751e-08);  // 1/11!
+  p = __builtin_fma(p, r, 2.75573192239858906526e-07);  // 1/10!
+  p = __builtin_fma(p, r, 2.75573192239858906526e-06);  // 1/9!
+  p = __builtin_fma(p, r, 2.48015873015873015873e-05);  // 1/8!
+  p = __builtin_fma(p, r, 1.98412698412698412698e-04);  // 1/7!
+  p = __builtin_fma(p, r, 1.38888888888888888889e-03);  // 1/6!
+  p = __builtin_fma(p, r, 8.33333333333333333333e-03);  // 1/5!
+  p = __builtin_fma(p, r, 4.16666666666666666667e-02);  // 1/4!
+  p = __builtin_fma(p, r, 1.66666666666666666667e-01);  // 1/3!
+  p = __builtin_fma(p, r, 0.5);
+  p = __builtin_fma(p, r, 1.0);
+  p = __builtin_fma(p, r, 1.0);
+  return (float)__builtin_amdgcn_ldexp(p, (int)n);
+}
+#if SR_PRECISE_TRANSC
+__device__ __forceinline__ float m_exp(float x) { return precise_exp_f32(x); }
+#else
 __device__ __forceinline__ float m_exp(float x) { return fast_exp_f32(x); }
+#endif
 __device__ __forceinline__ double m_exp(double x) { return exp(x); }
 SR_M1(m_log, logf, log)
 SR_M1_OOL(m_log2, log2f, log2)
@@ -107,6 +145,30 @@ __device__ __forceinline__ float fast_sincos_f32(float x, int want_cos, float& n
                            : __builtin_rintf(x * 0.318309873f);
   nabs = __builtin_fabsf(n);
   const float m = want_cos ? __builtin_fmaf(n, 2.0f, 1.0f) : n + n;
+#if SR_PRECISE_TRANSC
+  // Same reduction in Float64: r = x - m pi/2 (pi/2 = HI + LO, HI with 33
+  // significant bits so m*HI is exact for |m| < 2^20; |r| <= pi/2 + tiny),
+  // sin r by its Taylor series to r^19 (truncation < 2^-51 at pi/2), one
+  // rounding to Float32, then the sign of n's parity.
+  {
+    const double md = (double)m;
+    double r = __builtin_fma(md, -1.57079632673412561417e+00, (double)x);
+    r = __builtin_fma(md, -6.07710050650619224932e-11, r);
+    const double s2 = r * r;
+    double p = 8.22063524662432971696e-18;           // 1/19!
+    p = __builtin_fma(p, s2, -2.81145725434552076320e-15);  // -1/17!
+    p = __builtin_fma(p, s2, 7.64716373181981647590e-13);   // 1/15!
+    p = __builtin_fma(p, s2, -1.60590438368216145994e-10);  // -1/13!
+    p = __builtin_fma(p, s2, 2.50521083854417187751e-08);   // 1/11!
+    p = __builtin_fma(p, s2, -2.75573192239858906526e-06);  // -1/9!
+    p = __builtin_fma(p, s2, 1.98412698412698412698e-04);   // 1/7!
+    p = __builtin_fma(p, s2, -8.33333333333333333333e-03);  // -1/5!
+    p = __builtin_fma(p, s2, 1.66666666666666666667e-01);   // 1/3!: sin r = r - r^3 p
+    const double v = __builtin_fma(-p * s2, r, r);
+    const float f = (float)(want_cos ? -v : v);
+    return __int_as_float(__float_as_int(f) ^ ((int)n << 31));
+  }
+#endif
   float r = __builtin_fmaf(m, -1.57079601e+00f, x);
   r = __builtin_fmaf(m, -3.13916473e-07f, r);
   r = __builtin_fmaf(m, -5.39030253e-15f, r);
