@@ -62,7 +62,7 @@ __device__ __forceinline__ float fast_exp_f32(float x) {
 #define SR_PRECISE_TRANSC 1
 #endif
 // e^x = 2^n e^r, n = rint(x log2 e), r = x - n ln2 (two-part ln2, exact
-// products for |n| <= 151), e^r by its Taylor series to r^12 (|r| <= 0.347:
+// products for |n| <= 151), e^r by its Taylor series to r^11 (|r| <= 0.347:
 // truncation < 2^-47 relative), one v_ldexp_f64, one rounding to Float32.
 __device__ __forceinline__ float precise_exp_f32(float x) {
   x = __builtin_amdgcn_fmed3f(x, -104.0f, 89.0f);
@@ -70,8 +70,7 @@ __device__ __forceinline__ float precise_exp_f32(float x) {
   const double n = __builtin_rint(xd * 1.4426950408889634);
   double r = __builtin_fma(n, -6.93147180369123816490e-01, xd);
   r = __builtin_fma(n, -1.90821492927058770002e-10, r);
-  double p = 2.08767569878680989792e-09;        // 1/12!
-  p = __builtin_fma(p, r, 2.50521083854417187751e-08);  // 1/11!
+  double p = 2.50521083854417187751e-08;        // 1/11!
   p = __builtin_fma(p, r, 2.75573192239858906526e-07);  // 1/10!
   p = __builtin_fma(p, r, 2.75573192239858906526e-06);  // 1/9!
   p = __builtin_fma(p, r, 2.48015873015873015873e-05);  // 1/8!
@@ -148,15 +147,14 @@ __device__ __forceinline__ float fast_sincos_f32(float x, int want_cos, float& n
 #if SR_PRECISE_TRANSC
   // Same reduction in Float64: r = x - m pi/2 (pi/2 = HI + LO, HI with 33
   // significant bits so m*HI is exact for |m| < 2^20; |r| <= pi/2 + tiny),
-  // sin r by its Taylor series to r^19 (truncation < 2^-51 at pi/2), one
+  // sin r by its Taylor series to r^17 (truncation < 2^-44 at pi/2), one
   // rounding to Float32, then the sign of n's parity.
   {
     const double md = (double)m;
     double r = __builtin_fma(md, -1.57079632673412561417e+00, (double)x);
     r = __builtin_fma(md, -6.07710050650619224932e-11, r);
     const double s2 = r * r;
-    double p = 8.22063524662432971696e-18;           // 1/19!
-    p = __builtin_fma(p, s2, -2.81145725434552076320e-15);  // -1/17!
+    double p = -2.81145725434552076320e-15;          // -1/17!
     p = __builtin_fma(p, s2, 7.64716373181981647590e-13);   // 1/15!
     p = __builtin_fma(p, s2, -1.60590438368216145994e-10);  // -1/13!
     p = __builtin_fma(p, s2, 2.50521083854417187751e-08);   // 1/11!
