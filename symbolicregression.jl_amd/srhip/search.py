@@ -36,7 +36,7 @@ import numpy as np
 from .constant_optimization import optimize_constants_batch
 from .dataset import Dataset
 from .interface import compute_complexity, eval_loss_batch, loss_to_score, update_baseline_loss_
-from .node import Node, count_nodes, set_constants, string_tree, _postorder
+from .node import Node, _postorder, string_tree
 from .options import Options
 from .trees import _set_node, append_random_op, gen_random_tree, gen_random_tree_fixed_size, make_random_leaf
 
