@@ -137,15 +137,31 @@ struct srhip_program {
   int32_t* d_gitems = nullptr;  // work items (tree | group << 24): shallow then deep
   int32_t* d_const_off = nullptr;
   int ngitems_a = 0, ngitems_b = 0;
+  // byte capacities of the device buffers above (kept across rebuilds)
+  size_t code_cap = 0, toff_cap = 0, list_cap = 0;
+  size_t gcode_cap = 0, gtoff_cap = 0, gitems_cap = 0, gconst_cap = 0;
 };
 
 namespace {
+
+// Programs are rebuilt by every srhip_program_set_constants (the batched
+// constant optimiser does so once per line-search round) and hipFree
+// synchronises the device, so rebuilds reuse buffers that are large enough.
+void ensure_dev(void** ptr, size_t* cap, size_t bytes) {
+  if (*ptr && *cap >= bytes) return;
+  if (*ptr) (void)hipFree(*ptr);
+  *ptr = nullptr;
+  *cap = 0;
+  HIP_CHECK(hipMalloc(ptr, bytes));
+  *cap = bytes;
+}
 
 void free_grad_device(srhip_program* p) {
   for (void* q : {p->d_gcode, (void*)p->d_gtree_off, (void*)p->d_gitems, (void*)p->d_const_off})
     if (q) (void)hipFree(q);
   p->d_gcode = nullptr;
   p->d_gtree_off = p->d_gitems = p->d_const_off = nullptr;
+  p->gcode_cap = p->gtoff_cap = p->gitems_cap = p->gconst_cap = 0;
   p->grad_built = false;
 }
 
@@ -156,6 +172,7 @@ void free_program_device(srhip_program* p) {
   p->d_code = nullptr;
   p->d_tree_off = nullptr;
   p->d_list = nullptr;
+  p->code_cap = p->toff_cap = p->list_cap = 0;
   free_grad_device(p);
 }
 
@@ -195,10 +212,10 @@ void build_grad_program(srhip_program* p) {
   std::vector<int32_t> toff(cb.tree_off);
   for (auto& v : toff) v = std::max(v, 0);
   hipStream_t s = p->ctx->stream;
-  HIP_CHECK(hipMalloc(&p->d_gcode, std::max<size_t>(cb.code.size(), 1) * sizeof(Ins<T>)));
-  HIP_CHECK(hipMalloc((void**)&p->d_gtree_off, std::max<size_t>(toff.size(), 1) * sizeof(int32_t)));
-  HIP_CHECK(hipMalloc((void**)&p->d_gitems, std::max<size_t>(items.size(), 1) * sizeof(int32_t)));
-  HIP_CHECK(hipMalloc((void**)&p->d_const_off, p->const_off.size() * sizeof(int32_t)));
+  ensure_dev(&p->d_gcode, &p->gcode_cap, std::max<size_t>(cb.code.size(), 1) * sizeof(Ins<T>));
+  ensure_dev((void**)&p->d_gtree_off, &p->gtoff_cap, std::max<size_t>(toff.size(), 1) * sizeof(int32_t));
+  ensure_dev((void**)&p->d_gitems, &p->gitems_cap, std::max<size_t>(items.size(), 1) * sizeof(int32_t));
+  ensure_dev((void**)&p->d_const_off, &p->gconst_cap, p->const_off.size() * sizeof(int32_t));
   HIP_CHECK(hipMemcpyAsync(p->d_gcode, cb.code.data(), cb.code.size() * sizeof(Ins<T>), hipMemcpyHostToDevice, s));
   if (!toff.empty())
     HIP_CHECK(hipMemcpyAsync(p->d_gtree_off, toff.data(), toff.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
@@ -256,15 +273,16 @@ void build_program(srhip_program* p) {
   list.resize(2 * nl);
   for (size_t k = 0; k < nl; ++k) list[nl + k] = toff[list[k]];
 
-  free_program_device(p);
+  p->grad_built = false;  // the gradient programs embed the constants too
   hipStream_t s = p->ctx->stream;
+  HIP_CHECK(hipStreamSynchronize(s));  // no launch may still read the old buffers
   // +64 instructions of OP_END padding: the VGPR-resident program load reads
   // 64 instructions from the start of every program
   const size_t ncode_alloc = cb.code.size() + 64;
-  HIP_CHECK(hipMalloc(&p->d_code, ncode_alloc * sizeof(Ins<T>)));
+  ensure_dev(&p->d_code, &p->code_cap, ncode_alloc * sizeof(Ins<T>));
   HIP_CHECK(hipMemsetAsync(p->d_code, 0, ncode_alloc * sizeof(Ins<T>), p->ctx->stream));
-  HIP_CHECK(hipMalloc((void**)&p->d_tree_off, std::max<size_t>(toff.size(), 1) * sizeof(int32_t)));
-  HIP_CHECK(hipMalloc((void**)&p->d_list, std::max<size_t>(list.size(), 1) * sizeof(int32_t)));
+  ensure_dev((void**)&p->d_tree_off, &p->toff_cap, std::max<size_t>(toff.size(), 1) * sizeof(int32_t));
+  ensure_dev((void**)&p->d_list, &p->list_cap, std::max<size_t>(list.size(), 1) * sizeof(int32_t));
   HIP_CHECK(hipMemcpyAsync(p->d_code, cb.code.data(), cb.code.size() * sizeof(Ins<T>), hipMemcpyHostToDevice, s));
   if (!toff.empty())
     HIP_CHECK(hipMemcpyAsync(p->d_tree_off, toff.data(), toff.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
