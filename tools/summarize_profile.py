@@ -28,6 +28,7 @@ avg_ns = float(ev["AverageNs"])
 cycles = mean.get("GRBM_GUI_ACTIVE", 0) / 8
 out = {
     "kernel": meta.get("Kernel_Name"),
+    "workload": "config#2",  # tools/gpu_profile.sh profiles bench.py's default workload
     "avg_duration_ms": avg_ns / 1e6,
     "calls": int(ev["Calls"]),
     "grid_threads": int(meta.get("Grid_Size", 0)),
