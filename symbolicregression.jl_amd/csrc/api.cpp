@@ -73,6 +73,15 @@ struct DevBuf {
   }
 };
 
+// scoped device buffer: freed when it goes out of scope (hipFree waits for
+// the device, so an in-flight copy never reads freed memory)
+struct ScopedBuf : DevBuf {
+  ScopedBuf() = default;
+  ScopedBuf(const ScopedBuf&) = delete;
+  ScopedBuf& operator=(const ScopedBuf&) = delete;
+  ~ScopedBuf() { release(); }
+};
+
 constexpr int64_t kRowPad = 8192;  // dataset rows are padded to a multiple of this
 
 int64_t pad_rows(int64_t rows) { return ((std::max<int64_t>(rows, 1) + kRowPad - 1) / kRowPad) * kRowPad; }
@@ -682,6 +691,8 @@ int32_t srhip_close(srhip_ctx* ctx) {
     ctx->dloss.release();
     ctx->scratch_idx.release();
     ctx->gather.release();
+    ctx->fail.release();
+    ctx->ti_rec.release();
     for (auto& e : ctx->ev)
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
@@ -734,13 +745,15 @@ int32_t srhip_dataset_create(srhip_ctx* ctx, int32_t dtype, int32_t x_layout, co
       HIP_CHECK(hipMemsetAsync(ds->y, 0, (size_t)n_pad * es, ctx->stream));
       if (w) HIP_CHECK(hipMemsetAsync(ds->w, 0, (size_t)n_pad * es, ctx->stream));
       if (rows > 0) {
-        // raw shard upload, then pack/transposes on the device
-        void* raw = nullptr;
-        void* rawv = nullptr;
-        int* bad = nullptr;
-        HIP_CHECK(hipMalloc(&raw, (size_t)rows * nfeat * es));
-        HIP_CHECK(hipMalloc(&rawv, (size_t)rows * es));
-        HIP_CHECK(hipMalloc((void**)&bad, sizeof(int)));
+        // raw shard upload, then pack/transposes on the device; the staging
+        // buffers are freed on every path (ScopedBuf), the error path included
+        ScopedBuf raw_b, rawv_b, bad_b;
+        raw_b.ensure((size_t)rows * nfeat * es);
+        rawv_b.ensure((size_t)rows * es);
+        bad_b.ensure(sizeof(int));
+        void* raw = raw_b.p;
+        void* rawv = rawv_b.p;
+        int* bad = static_cast<int*>(bad_b.p);
         HIP_CHECK(hipMemsetAsync(bad, 0, sizeof(int), ctx->stream));
         if (x_layout == SRHIP_X_JULIA) {
           HIP_CHECK(hipMemcpyAsync(raw, static_cast<const char*>(X) + (size_t)row_begin * nfeat * es,
@@ -768,9 +781,6 @@ int32_t srhip_dataset_create(srhip_ctx* ctx, int32_t dtype, int32_t x_layout, co
         int hbad = 0;
         HIP_CHECK(hipMemcpyAsync(&hbad, bad, sizeof(int), hipMemcpyDeviceToHost, ctx->stream));
         HIP_CHECK(hipStreamSynchronize(ctx->stream));
-        (void)hipFree(raw);
-        (void)hipFree(rawv);
-        (void)hipFree(bad);
         ds->x_finite = hbad == 0;
       }
       HIP_CHECK(hipStreamSynchronize(ctx->stream));

@@ -281,13 +281,11 @@ eval_kernel(EvalArgs<T> a) {
 
 template <typename T, int R, int D, int SET, int MODE, bool W>
 hipError_t launch_one(const EvalPlan& plan, const EvalArgs<T>& a, hipStream_t stream) {
-  static bool attr_set = false;  // raise the dynamic-LDS ceiling once per kernel
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&eval_kernel<T, R, D, SET, MODE, W>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  // raise the dynamic-LDS ceiling once per kernel instantiation: a function-
+  // local static is initialised exactly once even with concurrent callers
+  static const hipError_t attr_err = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&eval_kernel<T, R, D, SET, MODE, W>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr_err != hipSuccess) return attr_err;
   const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
   hipLaunchKernelGGL((eval_kernel<T, R, D, SET, MODE, W>), dim3(grid), dim3(plan.threads),
                      plan.lds_bytes, stream, a);

@@ -158,13 +158,11 @@ __global__ void __launch_bounds__(256) grad_finalize_kernel(GradArgs<T> a, doubl
 
 template <typename T, int R, int D, int MODE, bool W>
 hipError_t launch_grad_one(const EvalPlan& plan, const GradArgs<T>& a, hipStream_t stream) {
-  static bool attr_set = false;
-  if (!attr_set) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&grad_kernel<T, R, D, MODE, W>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-    if (e != hipSuccess) return e;
-    attr_set = true;
-  }
+  // raise the dynamic-LDS ceiling once per kernel instantiation: a function-
+  // local static is initialised exactly once even with concurrent callers
+  static const hipError_t attr_err = hipFuncSetAttribute(
+      reinterpret_cast<const void*>(&grad_kernel<T, R, D, MODE, W>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  if (attr_err != hipSuccess) return attr_err;
   const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
   hipLaunchKernelGGL((grad_kernel<T, R, D, MODE, W>), dim3(grid), dim3(plan.threads), plan.lds_bytes,
                      stream, a);

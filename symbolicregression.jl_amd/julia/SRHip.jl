@@ -1,20 +1,30 @@
 # SRHip.jl — the Julia side of the drop-in boundary (ccall into libsrhip.so).
 #
-# This is the binding a SymbolicRegression.jl maintainer would add; Julia is
-# not available in this build image, so it is not executed here (the C ABI it
-# calls is tested from Python, tests/test_abi.py and tests/test_gpu_parity.py).
-# See INTEGRATION.md for where it plugs into the reference.
+# This is the binding a SymbolicRegression.jl maintainer would add (INTEGRATION.md
+# shows where it plugs in). UNTESTED AS JULIA: the build image has no Julia, so
+# this file has never been executed. What is tested (tests/test_julia_binding.py,
+# CPU): every `ccall((:srhip_*, libsrhip), R, (A...), ...)` below names a symbol
+# that include/srhip.h declares and libsrhip.so exports, with the declared number
+# of arguments and compatible argument / return types; and every loss type maps
+# to a SRHIP_LOSS_* code. The C ABI itself is exercised from Python through the
+# same entry points (tests/test_abi.py, tests/test_gpu_parity.py, ...).
 module SRHip
 
-using DynamicExpressions: Node
+using DynamicExpressions: Node, count_nodes
+using LossFunctions: L2DistLoss, L1DistLoss, LPDistLoss, HuberLoss, LogCoshLoss, L1EpsilonInsLoss,
+    L2EpsilonInsLoss, QuantileLoss, PeriodicLoss, LogitDistLoss
 import ..CoreModule: Options, Dataset
 
 const libsrhip = get(ENV, "SRHIP_LIB", joinpath(@__DIR__, "..", "lib", "libsrhip.so"))
 
+# include/srhip.h
 const SRHIP_OK = Int32(0)
 const SRHIP_ERR_UNSUPPORTED = Int32(-2)
 const NODE_CONST, NODE_FEATURE, NODE_UNARY, NODE_BINARY = UInt8(0), UInt8(1), UInt8(2), UInt8(3)
-const LOSS_L2, LOSS_L1, LOSS_LP, LOSS_HUBER = Int32(0), Int32(1), Int32(2), Int32(3)
+const X_JULIA = Int32(0)
+const LOSS_L2, LOSS_L1, LOSS_LP, LOSS_HUBER, LOSS_LOGCOSH = Int32(0), Int32(1), Int32(2), Int32(3), Int32(4)
+const LOSS_L1EPSINS, LOSS_L2EPSINS, LOSS_QUANTILE, LOSS_PERIODIC, LOSS_LOGITDIST =
+    Int32(5), Int32(6), Int32(7), Int32(8), Int32(9)
 
 struct SrhipTrees              # include/srhip.h: srhip_trees
     ntrees::Int32
@@ -25,6 +35,8 @@ struct SrhipTrees              # include/srhip.h: srhip_trees
     consts::Ptr{Cvoid}
 end
 
+"""Raised for anything outside the engine's coverage: the caller falls back to
+the reference CPU path (srhip.h: SRHIP_ERR_UNSUPPORTED)."""
 struct Unsupported <: Exception
     msg::String
 end
@@ -40,7 +52,22 @@ dtype_code(::Type{Float32}) = Int32(0)
 dtype_code(::Type{Float64}) = Int32(1)
 dtype_code(::Type) = throw(Unsupported("only Float32/Float64 run on the GPU"))
 
-# one context per (thread, device): calls through a context are serialised
+# ---- elementwise losses -> SRHIP_LOSS_* (LossFunctions.jl distance losses,
+# src/Options.jl:429-431 default L2DistLoss; docs/src/losses.md) ----------------
+loss_code(::L2DistLoss) = (LOSS_L2, 0.0)
+loss_code(::L1DistLoss) = (LOSS_L1, 0.0)
+loss_code(::LPDistLoss{P}) where {P} = (LOSS_LP, Float64(P))
+loss_code(l::HuberLoss) = (LOSS_HUBER, Float64(l.d))
+loss_code(::LogCoshLoss) = (LOSS_LOGCOSH, 0.0)
+loss_code(l::L1EpsilonInsLoss) = (LOSS_L1EPSINS, Float64(l.ε))
+loss_code(l::L2EpsilonInsLoss) = (LOSS_L2EPSINS, Float64(l.ε))
+loss_code(l::QuantileLoss) = (LOSS_QUANTILE, Float64(l.τ))
+# PeriodicLoss stores k = 2π/circumference; the engine takes the circumference
+loss_code(l::PeriodicLoss) = (LOSS_PERIODIC, 2π / Float64(l.k))
+loss_code(::LogitDistLoss) = (LOSS_LOGITDIST, 0.0)
+loss_code(l) = throw(Unsupported("elementwise loss $(typeof(l)) is not in the engine's table"))
+
+# ---- contexts: one per (thread, device); calls through a context are serialised
 const CTX = Dict{Tuple{Int,Int},Ptr{Cvoid}}()
 const CTX_LOCK = ReentrantLock()
 function context(device::Int=0)
@@ -54,7 +81,16 @@ function context(device::Int=0)
     end
 end
 
-# operator ids, once per Options (srhip_op_lookup applies binopmap/unaopmap names)
+function device_available()
+    n = Ref{Int32}(0)
+    try
+        ccall((:srhip_device_count, libsrhip), Int32, (Ptr{Int32},), n) == SRHIP_OK && n[] > 0
+    catch
+        false  # library missing or not loadable
+    end
+end
+
+# ---- operator ids (srhip_op_lookup applies binopmap/unaopmap names) ------------
 function op_id(op, arity)
     a = Ref{Int32}(0); i = Ref{Int32}(0)
     check(ccall((:srhip_op_lookup, libsrhip), Int32, (Cstring, Ptr{Int32}, Ptr{Int32}),
@@ -62,12 +98,36 @@ function op_id(op, arity)
     a[] == arity || throw(Unsupported("operator $(op) has arity $(a[])"))
     return UInt16(i[])
 end
-operator_ids(options::Options) = (
-    [op_id(op, 2) for op in options.operators.binops],
-    [op_id(op, 1) for op in options.operators.unaops],
-)
+const OPS_CACHE = IdDict{Any,Any}()
+operator_ids(options::Options) = lock(CTX_LOCK) do
+    get!(OPS_CACHE, options) do
+        ([op_id(op, 2) for op in options.operators.binops], [op_id(op, 1) for op in options.operators.unaops])
+    end
+end
 
-# post-order flattening; constants in get_constants order
+"""
+    enabled(options) -> Bool
+
+Whether `options` can run on the engine: a device is visible, `loss_function`
+is not set (arbitrary Julia stays on the CPU, src/LossFunctions.jl:60-67), the
+elementwise loss and every operator are in the engine's table. Set
+ENV["SRHIP_DISABLE"] = "1" to force the reference path.
+"""
+function enabled(options::Options)
+    get(ENV, "SRHIP_DISABLE", "0") == "1" && return false
+    options.loss_function === nothing || return false
+    device_available() || return false
+    try
+        loss_code(options.elementwise_loss)
+        operator_ids(options)
+        return true
+    catch e
+        e isa Unsupported || rethrow()
+        return false
+    end
+end
+
+# ---- flattening: post-order node streams, constants in get_constants order ----
 function flatten(trees::AbstractVector{Node{T}}, options::Options) where {T}
     bin, una = operator_ids(options)
     kind = UInt8[]; arg = UInt16[]; consts = T[]
@@ -92,32 +152,76 @@ function flatten(trees::AbstractVector{Node{T}}, options::Options) where {T}
     return node_off, kind, arg, const_off, consts
 end
 
-# device copy of a Dataset, uploaded once (src/Dataset.jl:24-64)
+# A compiled, device-resident batch of trees (srhip_program_create); destroyed
+# by the caller (`destroy`) or by the finaliser.
+mutable struct Program
+    h::Ptr{Cvoid}
+    ntrees::Int
+    const_off::Vector{Int32}
+end
+function destroy(p::Program)
+    p.h == C_NULL && return nothing
+    ccall((:srhip_program_destroy, libsrhip), Int32, (Ptr{Cvoid},), p.h)
+    p.h = C_NULL
+    return nothing
+end
+function Program(trees::AbstractVector{Node{T}}, options::Options, device::Int=0) where {T}
+    node_off, kind, arg, const_off, consts = flatten(trees, options)
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    GC.@preserve node_off kind arg const_off consts begin
+        tr = Ref(SrhipTrees(Int32(length(trees)), pointer(node_off), pointer(kind), pointer(arg),
+                            pointer(const_off), Ptr{Cvoid}(pointer(consts))))
+        check(ccall((:srhip_program_create, libsrhip), Int32,
+                    (Ptr{Cvoid}, Int32, Ref{SrhipTrees}, Ptr{Ptr{Cvoid}}),
+                    context(device), dtype_code(T), tr, h))
+    end
+    p = Program(h[], length(trees), const_off)
+    finalizer(destroy, p)
+    return p
+end
+
+function set_constants!(p::Program, consts::Vector{T}) where {T}
+    length(consts) == p.const_off[end] || throw(ArgumentError("expected $(p.const_off[end]) constants"))
+    GC.@preserve consts check(ccall((:srhip_program_set_constants, libsrhip), Int32,
+                                    (Ptr{Cvoid}, Ptr{Cvoid}), p.h, consts))
+    return p
+end
+
+# ---- device datasets ----------------------------------------------------------
+function upload(X::AbstractMatrix{T}, y::AbstractVector{T}, w, device::Int) where {T}
+    h = Ref{Ptr{Cvoid}}(C_NULL)
+    Xc = Matrix{T}(X); yc = Vector{T}(y)
+    wc = w === nothing ? nothing : Vector{T}(w)
+    nfeat, n = size(Xc)
+    GC.@preserve Xc yc wc begin
+        check(ccall((:srhip_dataset_create, libsrhip), Int32,
+                    (Ptr{Cvoid}, Int32, Int32, Ptr{T}, Ptr{T}, Ptr{T}, Int64, Int32, Int64, Int64,
+                     Ptr{Ptr{Cvoid}}),
+                    context(device), dtype_code(T), X_JULIA, Xc, yc,
+                    wc === nothing ? Ptr{T}(C_NULL) : wc, n, nfeat, 0, n, h))
+    end
+    return h[]
+end
+destroy_dataset(h::Ptr{Cvoid}) = ccall((:srhip_dataset_destroy, libsrhip), Int32, (Ptr{Cvoid},), h)
+
+# one device copy per Dataset (src/Dataset.jl:24-64), uploaded once; the table
+# is shared by all threads, so it is guarded by CTX_LOCK
 const DEVICE_DATASETS = IdDict{Any,Ptr{Cvoid}}()
 function device_dataset(dataset::Dataset{T}, device::Int=0) where {T}
-    get!(DEVICE_DATASETS, dataset) do
-        h = Ref{Ptr{Cvoid}}(C_NULL)
-        X = Matrix{T}(dataset.X); y = Vector{T}(dataset.y)
-        w = dataset.weighted ? Vector{T}(dataset.weights) : nothing
-        GC.@preserve X y w begin
-            check(ccall((:srhip_dataset_create, libsrhip), Int32,
-                        (Ptr{Cvoid}, Int32, Int32, Ptr{T}, Ptr{T}, Ptr{T}, Int64, Int32, Int64, Int64,
-                         Ptr{Ptr{Cvoid}}),
-                        context(device), dtype_code(T), Int32(0), X, y,
-                        w === nothing ? Ptr{T}(C_NULL) : w, dataset.n, dataset.nfeatures, 0, dataset.n, h))
+    lock(CTX_LOCK) do
+        get!(DEVICE_DATASETS, dataset) do
+            upload(dataset.X, dataset.y, dataset.weighted ? dataset.weights : nothing, device)
         end
-        h[]
     end
 end
 
-loss_code(::Any) = throw(Unsupported("elementwise loss not in the engine's table"))
-# (the shim maps L2DistLoss/L1DistLoss/LPDistLoss/HuberLoss/... to SRHIP_LOSS_*)
-
+# ---- eval_loss (src/LossFunctions.jl:34-67), batched ------------------------------
 """
-    eval_loss_batch(trees, dataset, options) -> Vector{T}
+    eval_loss_batch(trees, dataset, options; idx=nothing) -> Vector{T}
 
 Batched `eval_loss` (src/LossFunctions.jl:60-67): one device launch for all
-trees; T(Inf) where evaluation fails.
+trees; T(Inf) where evaluation fails. `idx` (1-based, with repetition) is
+score_func_batch's row sample (src/LossFunctions.jl:95-115).
 """
 function eval_loss_batch(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, options::Options;
                          idx=nothing) where {T}
@@ -128,7 +232,7 @@ function eval_loss_batch(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, op
     params = Float64[param]
     rows = idx === nothing ? Int64[] : Int64.(idx .- 1)
     GC.@preserve node_off kind arg const_off consts sums ok params rows begin
-        tr = Ref(SrhipTrees(nt, pointer(node_off), pointer(kind), pointer(arg), pointer(const_off),
+        tr = Ref(SrhipTrees(Int32(nt), pointer(node_off), pointer(kind), pointer(arg), pointer(const_off),
                             Ptr{Cvoid}(pointer(consts))))
         check(ccall((:srhip_eval_loss_batch, libsrhip), Int32,
                     (Ptr{Cvoid}, Ref{SrhipTrees}, Int32, Ptr{Float64}, Ptr{Int64}, Int64, Ptr{Float64},
@@ -137,6 +241,113 @@ function eval_loss_batch(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, op
                     idx === nothing ? Ptr{Int64}(C_NULL) : pointer(rows), length(rows), sums, wsum, ok))
     end
     return [ok[i] == 1 ? T(sums[i] / wsum[]) : T(Inf) for i in 1:nt]
+end
+
+"""
+    eval_loss_grad_batch(p::Program, dataset, options) -> (losses, grads, ok)
+
+Loss and ∂loss/∂c of every constant of every tree of `p` in one launch
+(`srhip_eval_loss_grad`), for batched constant optimisation
+(src/ConstantOptimization.jl:12-65). grads[t] is in get_constants order.
+"""
+function eval_loss_grad_batch(p::Program, dataset::Dataset{T}, options::Options) where {T}
+    nt = p.ntrees
+    ncon = Int(p.const_off[end])
+    sums = Vector{Float64}(undef, nt); ok = Vector{UInt8}(undef, nt); wsum = Ref{Float64}(0)
+    dloss = Vector{Float64}(undef, ncon)
+    kindcode, param = loss_code(options.elementwise_loss)
+    params = Float64[param]
+    GC.@preserve sums ok dloss params begin
+        check(ccall((:srhip_eval_loss_grad, libsrhip), Int32,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{Float64},
+                     Ptr{UInt8}),
+                    device_dataset(dataset), p.h, kindcode, params, sums, dloss, wsum, ok))
+    end
+    losses = [ok[i] == 1 ? T(sums[i] / wsum[]) : T(Inf) for i in 1:nt]
+    grads = [dloss[(p.const_off[i] + 1):p.const_off[i + 1]] ./ wsum[] for i in 1:nt]
+    return losses, grads, ok .== 1
+end
+
+# ---- eval_tree_array (src/InterfaceDynamicExpressions.jl:50-52) -------------------
+"""
+    eval_tree_array(tree, X, options) -> (output, did_succeed)
+
+Per-row outputs of one tree on the engine. X is (nfeatures, n); it is uploaded
+for this call. On failure the output contents are unspecified, as in the
+reference (an undef array).
+"""
+function eval_tree_array(tree::Node{T}, X::AbstractMatrix{T}, options::Options; device::Int=0) where {T}
+    n = size(X, 2)
+    ds = upload(X, zeros(T, n), nothing, device)
+    p = Program([tree], options, device)
+    out = Vector{T}(undef, n); ok = Ref{UInt8}(0)
+    try
+        GC.@preserve out check(ccall((:srhip_eval_tree_array, libsrhip), Int32,
+                                     (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ref{UInt8}), ds, p.h, out, ok))
+    finally
+        destroy(p)
+        destroy_dataset(ds)
+    end
+    return out, ok[] == 1
+end
+
+# ---- eval_grad_tree_array (src/InterfaceDynamicExpressions.jl:83-107) -------------
+"""
+    eval_grad_tree_array(tree, X, options; variable=false) -> (output, gradient, did_succeed)
+
+variable=false: gradient[k, i] = ∂ŷ_i/∂c_k for the constants in get_constants
+order (srhip_eval_grad_tree_array). variable=true: gradient[f, i] = ∂ŷ_i/∂x_f,
+computed by seeding each feature leaf x_f as (x_f + c) with c = -0.0 (x + -0.0
+== x bit for bit, so values and did_succeed are unchanged) and summing the
+seeds' tangents per feature; needs `+` among the binary operators, else
+Unsupported.
+"""
+function eval_grad_tree_array(tree::Node{T}, X::AbstractMatrix{T}, options::Options;
+                              variable::Bool=false, device::Int=0) where {T}
+    nfeat, n = size(X)
+    if !variable
+        value, G, ok = _const_grads(tree, X, options, device)
+        return value, permutedims(G), ok
+    end
+    plus = findfirst(op -> op === (+), options.operators.binops)
+    plus === nothing && throw(Unsupported("variable=true needs + among the binary operators"))
+    seeds = Int[]
+    function seed(t::Node{T})
+        if t.degree == 0
+            t.constant && (push!(seeds, 0); return Node(T; val=t.val))
+            push!(seeds, t.feature)
+            return Node(plus, Node(T; feature=t.feature), Node(T; val=T(-0.0)))
+        elseif t.degree == 1
+            return Node(t.op, seed(t.l))
+        else
+            l = seed(t.l)
+            return Node(t.op, l, seed(t.r))
+        end
+    end
+    aug = seed(tree)
+    value, G, ok = _const_grads(aug, X, options, device)
+    grad = zeros(T, nfeat, n)
+    for (k, f) in enumerate(seeds)
+        f > 0 && (grad[f, :] .+= view(G, :, k))
+    end
+    return value, grad, ok
+end
+
+function _const_grads(tree::Node{T}, X::AbstractMatrix{T}, options::Options, device::Int) where {T}
+    n = size(X, 2)
+    ds = upload(X, zeros(T, n), nothing, device)
+    p = Program([tree], options, device)
+    ncon = Int(p.const_off[end])
+    value = Vector{T}(undef, n); G = Matrix{T}(undef, n, ncon); ok = Ref{UInt8}(0)
+    try
+        GC.@preserve value G check(ccall((:srhip_eval_grad_tree_array, libsrhip), Int32,
+                                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ref{UInt8}),
+                                         ds, p.h, value, G, ok))
+    finally
+        destroy(p)
+        destroy_dataset(ds)
+    end
+    return value, G, ok[] == 1
 end
 
 end # module

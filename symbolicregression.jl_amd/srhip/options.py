@@ -5,6 +5,7 @@ batch_size, turbo — with the reference's defaults and operator mapping.
 """
 from __future__ import annotations
 
+import warnings
 from dataclasses import dataclass
 from typing import Callable, Optional, Sequence, Tuple
 
@@ -63,6 +64,18 @@ def LogitDistLoss():
     return SupervisedLoss(K.LOSS["LOGITDIST"])
 
 
+# Keywords of the reference's Options (src/Options.jl:315-379) that steer only
+# its search control plane (mutation/crossover schedule, constraints, output,
+# recorder, stopping rules): accepted, stored, not used by this engine.
+REFERENCE_ONLY_KWARGS = frozenset("""
+constraints tournament_selection_p fast_cycle migration hof_migration output_file mutation_weights
+crossover_probability warmup_maxsize_by use_frequency use_frequency_in_tournament adaptive_parsimony_scaling
+verbosity save_to_file seed bin_constraints una_constraints progress terminal_width optimizer_options
+recorder recorder_file early_stop_condition return_state timeout_in_seconds max_evals skip_mutation_failures
+enable_autodiff nested_constraints deterministic define_helper_functions
+""".split())
+
+
 def _opname(op) -> str:
     if isinstance(op, str):
         return op
@@ -99,8 +112,31 @@ class Options:
         optimizer_probability: float = 0.14,
         optimizer_iterations: Optional[int] = None,
         should_optimize_constants: bool = True,
-        **_ignored,
+        # search (src/Options.jl:315-370 defaults), read by srhip.equation_search
+        npop: int = 33,
+        ncycles_per_iteration: int = 550,
+        tournament_selection_n: int = 12,
+        topn: int = 12,
+        alpha: float = 0.1,
+        perturbation_factor: float = 0.076,
+        annealing: bool = False,
+        probability_negate_constant: float = 0.01,
+        fraction_replaced: float = 0.00036,
+        fraction_replaced_hof: float = 0.035,
+        maxdepth: Optional[int] = None,
+        **kws,
     ):
+        # Options(; kws...) raises on unknown keywords (src/Options.jl:388-390);
+        # keywords of the reference that only steer its control plane (which
+        # this engine does not rebuild) are accepted and kept in
+        # `self.ignored`, with one warning.
+        unknown = sorted(k for k in kws if k not in REFERENCE_ONLY_KWARGS)
+        if unknown:
+            raise TypeError(f"Unknown keyword argument(s): {', '.join(unknown)}")
+        self.ignored = dict(kws)
+        if kws:
+            warnings.warn("Options: keyword(s) " + ", ".join(sorted(kws)) + " only affect the reference's "
+                          "search control plane and are ignored here", stacklevel=2)
         self.binary_operators: Tuple[str, ...] = tuple(_opname(o) for o in binary_operators)
         self.unary_operators: Tuple[str, ...] = tuple(_opname(o) for o in unary_operators)
         if set(self.binary_operators) & set(self.unary_operators):
@@ -119,6 +155,17 @@ class Options:
         self.optimizer_probability = float(optimizer_probability)
         self.optimizer_iterations = 8 if optimizer_iterations is None else int(optimizer_iterations)
         self.should_optimize_constants = bool(should_optimize_constants)
+        self.npop = int(npop)
+        self.ncycles_per_iteration = int(ncycles_per_iteration)
+        self.tournament_selection_n = int(tournament_selection_n)
+        self.topn = int(topn)
+        self.alpha = float(alpha)
+        self.perturbation_factor = float(perturbation_factor)
+        self.annealing = bool(annealing)
+        self.probability_negate_constant = float(probability_negate_constant)
+        self.fraction_replaced = float(fraction_replaced)
+        self.fraction_replaced_hof = float(fraction_replaced_hof)
+        self.maxdepth = maxdepth
         self.nbin = len(self.binary_operators)
         self.nuna = len(self.unary_operators)
         # ComplexityMapping (src/OptionsStruct.jl:55-104): use when any is given

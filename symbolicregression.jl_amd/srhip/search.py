@@ -18,7 +18,9 @@ fame per complexity, migration from the other islands' best and from the hall
 of fame (SymbolicRegression.jl:717-778). Left out (host bookkeeping that does
 not change what the engine evaluates): simplify/combine_operators (treated as
 do_nothing), crossover (fast_cycle forbids it, :41), `use_frequency`
-adaptive parsimony, the recorder, progress output, early stopping.
+adaptive parsimony, the recorder, progress output, early stopping. One
+deviation: with `batching=true` the babies of one launch share one minibatch
+row sample (the reference draws one per `score_func_batch` call).
 
 Islands are independent between migrations, so with `world > 1` each rank
 runs its own islands (no data-path collective) and the best members are
@@ -80,6 +82,18 @@ class HallOfFame:
 
 def _opt(options: Options, name: str):
     return getattr(options, name, SEARCH_DEFAULTS[name])
+
+
+def _acceptance(after: float, before: float, temperature: float, options: Options) -> float:
+    """probChange of next_generation (src/Mutate.jl:229-233) with Julia's IEEE
+    semantics: exp(-delta / (T * alpha)) where T = 0 on the last annealing cycle
+    gives exp(±Inf) (0 or Inf) and an overflowing exponent gives Inf, not an
+    exception; NaN (e.g. Inf - Inf) never passes `probChange < rand()` as false."""
+    if not _opt(options, "annealing"):
+        return 1.0
+    with np.errstate(all="ignore"):
+        delta = np.float64(after) - np.float64(before)
+        return float(np.exp(-delta / (np.float64(temperature) * np.float64(_opt(options, "alpha")))))
 
 
 def _depth(t: Node) -> int:
@@ -154,10 +168,12 @@ def _new_op(left: Node, options: Options, nfeat: int, T, rng) -> Node:
 def equation_search(X: np.ndarray, y: np.ndarray, options: Options, niterations: int = 10,
                     weights: Optional[np.ndarray] = None, seed: int = 0, rank: int = 0, world: int = 1,
                     group=None, scorer: Optional[Callable[[Sequence[Node]], np.ndarray]] = None,
-                    evaluator_factory: Optional[Callable] = None, verbose: bool = False):
+                    evaluator_factory: Optional[Callable] = None, verbose: bool = False,
+                    batch_scorer: Optional[Callable[[Sequence[Node], np.ndarray], np.ndarray]] = None):
     """EquationSearch(X, y; niterations, options) with all islands in lockstep.
-    Returns (hall_of_fame, stats). `scorer(trees) -> losses` replaces the
-    engine (tests run the same driver over the CPU oracle)."""
+    Returns (hall_of_fame, stats). `scorer(trees) -> losses` and
+    `batch_scorer(trees, row_idx) -> losses` replace the engine (tests run the
+    same driver over the CPU oracle)."""
     rng = np.random.default_rng(seed + 1000 * rank)
     dataset = Dataset(np.asarray(X), np.asarray(y), weights)
     T = np.dtype(dataset.T).type
@@ -184,6 +200,24 @@ def equation_search(X: np.ndarray, y: np.ndarray, options: Options, niterations:
         stats["evals"] += len(trees)
         losses = np.asarray(score_losses(trees), dtype=np.float64) if trees else np.zeros(0)
         scores = [float(loss_to_score(T(l), dataset.baseline_loss, t, options)) if np.isfinite(l) else math.inf
+                  for l, t in zip(losses, trees)]
+        return scores, losses
+
+    def score_babies(trees: List[Node]):
+        """next_generation's scoring (Mutate.jl:199-205): score_func, or with
+        options.batching score_func_batch on batch_size rows sampled with
+        replacement (one sample per launch, shared by the launch's babies)."""
+        if not options.batching or not trees:
+            return score(trees)
+        stats["launches"] += 1
+        stats["evals"] += len(trees) * options.batch_size / dataset.n
+        idx = rng.integers(0, dataset.n, size=options.batch_size)
+        if batch_scorer is not None:
+            losses = np.asarray(batch_scorer(trees, idx), dtype=np.float64)
+        else:
+            losses = np.asarray(eval_loss_batch(trees, dataset, options, row_idx=idx), dtype=np.float64)
+        # a failed minibatch evaluation scores (0, Inf) (LossFunctions.jl:102-104)
+        scores = [float(loss_to_score(T(l), dataset.baseline_loss, t, options)) if np.isfinite(l) else 0.0
                   for l, t in zip(losses, trees)]
         return scores, losses
 
@@ -224,7 +258,7 @@ def equation_search(X: np.ndarray, y: np.ndarray, options: Options, niterations:
                     parents.append((k, allstar, choice, baby))
                     if baby is not None and choice not in ("do_nothing", "simplify", "optimize"):
                         babies.append(baby)
-            sc, lo = score(babies)  # ONE launch for every island's babies
+            sc, lo = score_babies(babies)  # ONE launch for every island's babies
             b = 0
             for k, allstar, choice, baby in parents:
                 if baby is None:
@@ -234,11 +268,10 @@ def equation_search(X: np.ndarray, y: np.ndarray, options: Options, niterations:
                 else:
                     s, l = sc[b], lo[b]
                     b += 1
-                    if not np.isfinite(s):
+                    if np.isnan(s):  # Mutate.jl:207: only a NaN score is rejected outright
                         continue
-                    prob = math.exp(-(s - allstar.score) / (temperature * _opt(options, "alpha"))) \
-                        if _opt(options, "annealing") else 1.0
-                    if prob < rng.random():
+                    prob = _acceptance(s, allstar.score, temperature, options)
+                    if not (prob >= rng.random()):  # `probChange < rand()` rejects; NaN never accepts
                         continue
                     new = PopMember(baby, s, l, born())
                 pop = pops[k]

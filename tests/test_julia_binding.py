@@ -1,0 +1,159 @@
+"""The Julia binding (symbolicregression.jl_amd/julia/SRHip.jl) against the C ABI.
+
+Julia is not installed in this image, so SRHip.jl cannot run here. This CPU
+test checks what can be checked statically: every `ccall((:srhip_*, libsrhip),
+R, (A...), args...)` names a function that include/srhip.h declares and
+libsrhip.so exports, passes as many arguments as the prototype has, and uses
+Julia types that match the C parameter types (Int32 <-> int32_t, Int64 <->
+int64_t, Ptr/Ref/Cstring <-> pointers); the constants it defines equal the
+header's; every SRHIP_LOSS_* code is reachable from a loss type
+(LossFunctions.jl's distance losses, src/Options.jl:429-431)."""
+import ctypes
+import re
+from pathlib import Path
+
+import pytest
+
+ROOT = Path(__file__).resolve().parent.parent
+JL = ROOT / "symbolicregression.jl_amd" / "julia" / "SRHip.jl"
+HDR = ROOT / "include" / "srhip.h"
+LIB = ROOT / "symbolicregression.jl_amd" / "lib" / "libsrhip.so"
+
+
+def _split_top(s):
+    """Split on commas at nesting depth 0 (braces, parentheses, brackets)."""
+    out, depth, cur = [], 0, ""
+    for ch in s:
+        if ch in "({[":
+            depth += 1
+        elif ch in ")}]":
+            depth -= 1
+        if ch == "," and depth == 0:
+            out.append(cur.strip())
+            cur = ""
+        else:
+            cur += ch
+    if cur.strip():
+        out.append(cur.strip())
+    return out
+
+
+def _matching(s, i):
+    """Index of the parenthesis closing the one at s[i]."""
+    depth = 0
+    for j in range(i, len(s)):
+        if s[j] == "(":
+            depth += 1
+        elif s[j] == ")":
+            depth -= 1
+            if depth == 0:
+                return j
+    raise ValueError("unbalanced")
+
+
+def julia_ccalls():
+    src = "\n".join(ln.split("#")[0] for ln in JL.read_text().splitlines())  # drop comments
+    calls = []
+    for m in re.finditer(r"ccall\(", src):
+        start = m.end() - 1
+        body = src[start + 1:_matching(src, start)]
+        parts = _split_top(body)
+        sym = re.match(r"\(:(\w+),\s*libsrhip\)", parts[0])
+        assert sym, f"ccall without (:symbol, libsrhip): {parts[0]}"
+        ret = parts[1]
+        tup = parts[2]
+        assert tup.startswith("(") and tup.endswith(")"), tup
+        argtypes = _split_top(tup[1:-1])
+        calls.append((sym.group(1), ret, argtypes, parts[3:]))
+    return calls
+
+
+def header_prototypes():
+    txt = re.sub(r"/\*.*?\*/", "", HDR.read_text(), flags=re.S)
+    protos = {}
+    for m in re.finditer(r"^([\w\s\*]+?)\s*\b(srhip_\w+)\s*\(([^)]*)\)\s*;", txt, re.M):
+        ret, name, params = m.group(1).strip(), m.group(2), m.group(3).strip()
+        plist = [] if params in ("", "void") else [p.strip() for p in params.split(",")]
+        protos[name] = (ret, plist)
+    return protos
+
+
+def _c_kind(param):
+    p = re.sub(r"\b(const|struct)\b", "", param).strip()
+    if "*" in p:
+        return "ptr"
+    ty = p.split()[0]
+    return {"int32_t": "i32", "int64_t": "i64", "double": "f64", "uint8_t": "u8"}[ty]
+
+
+def _jl_kind(t):
+    t = t.strip()
+    if t.startswith(("Ptr{", "Ref{")) or t == "Cstring":
+        return "ptr"
+    return {"Int32": "i32", "Int64": "i64", "Float64": "f64", "UInt8": "u8", "Cint": "i32"}[t]
+
+
+def test_every_ccall_matches_the_header():
+    protos = header_prototypes()
+    calls = julia_ccalls()
+    assert len(calls) >= 12
+    seen = set()
+    for name, ret, argtypes, args in calls:
+        assert name in protos, f"{name} is not declared in include/srhip.h"
+        cret, cparams = protos[name]
+        seen.add(name)
+        assert len(argtypes) == len(cparams), f"{name}: {len(argtypes)} Julia argument types, {len(cparams)} in C"
+        assert len(args) == len(argtypes), f"{name}: {len(args)} arguments for {len(argtypes)} types"
+        for jt, cp in zip(argtypes, cparams):
+            assert _jl_kind(jt) == _c_kind(cp), f"{name}: Julia {jt} vs C {cp}"
+        if "char" in cret:
+            assert ret == "Cstring", name
+        else:
+            assert ret == "Int32" and cret == "int32_t", f"{name}: returns {ret} / {cret}"
+    # the entry points the shim of INTEGRATION.md §3 needs are all bound
+    for need in ("srhip_eval_loss_batch", "srhip_eval_tree_array", "srhip_eval_grad_tree_array",
+                 "srhip_eval_loss_grad", "srhip_program_create", "srhip_program_set_constants",
+                 "srhip_dataset_create", "srhip_op_lookup", "srhip_open", "srhip_device_count"):
+        assert need in seen, need
+
+
+def test_ccall_symbols_are_exported():
+    if not LIB.exists():
+        pytest.skip("libsrhip.so not built")
+    lib = ctypes.CDLL(str(LIB))
+    for name, *_ in julia_ccalls():
+        assert hasattr(lib, name), f"libsrhip.so does not export {name}"
+
+
+def test_constants_and_loss_table_match_the_header():
+    hdr = HDR.read_text()
+    src = JL.read_text()
+    defs = {m.group(1): int(m.group(2)) for m in re.finditer(r"#define SRHIP_(\w+)\s+\(?(-?\d+)\)?", hdr)}
+    # scalar constants: const NAME = Int32(v)
+    for name, val in re.findall(r"const (SRHIP_\w+) = Int32\((-?\d+)\)", src):
+        assert defs[name[len("SRHIP_"):]] == int(val), name
+    # tuple-assigned LOSS_* constants
+    losses = {}
+    for lhs, rhs in re.findall(r"const ((?:LOSS_\w+,?\s*)+)=\s*((?:Int32\(\d+\),?\s*)+)", src):
+        names = [x.strip() for x in lhs.split(",") if x.strip()]
+        vals = [int(v) for v in re.findall(r"Int32\((\d+)\)", rhs)]
+        losses.update(zip(names, vals))
+    hdr_losses = {k: v for k, v in defs.items() if k.startswith("LOSS_")}
+    assert losses == hdr_losses
+    # every loss code has a loss_code method
+    mapped = set(re.findall(r"loss_code\([^)]*\)(?: where \{P\})? = \((LOSS_\w+),", src))
+    assert mapped == set(hdr_losses), set(hdr_losses) ^ mapped
+    # node kinds and the X layout
+    kinds = re.search(r"const NODE_CONST, NODE_FEATURE, NODE_UNARY, NODE_BINARY = (.*)", src).group(1)
+    assert [int(v) for v in re.findall(r"UInt8\((\d)\)", kinds)] == [
+        defs["NODE_CONST"], defs["NODE_FEATURE"], defs["NODE_UNARY"], defs["NODE_BINARY"]]
+    assert int(re.search(r"const X_JULIA = Int32\((\d)\)", src).group(1)) == defs["X_JULIA"]
+
+
+def test_binding_exposes_the_shim_api():
+    src = JL.read_text()
+    for fn in ("enabled", "eval_loss_batch", "eval_tree_array", "eval_grad_tree_array", "eval_loss_grad_batch",
+               "set_constants!", "flatten"):
+        assert re.search(rf"^function {re.escape(fn)}\(|^{re.escape(fn)}\(.*\) =", src, re.M), fn
+    # the shared device-dataset table is only touched under the lock
+    assert re.search(r"lock\(CTX_LOCK\) do\s+get!\(DEVICE_DATASETS", src)

