@@ -222,6 +222,27 @@ int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog,
                                    void* out_value, void* out_grad,
                                    uint8_t* out_ok);
 
+/* ---- tree compiler ---------------------------------------------------------
+ * Large Float32 programs are compiled to machine code, one block per tree
+ * (symbolicregression.jl_amd/csrc/jit.cpp; SRHIP_JIT=0 turns it off, =1 on
+ * for every size). Tree code computes exactly what the interpreter computes
+ * (eval_loss with the L2 loss; other losses and per-row outputs run
+ * interpreted). This reports: trees compiled, of which with a guarded
+ * Float32-transcendental path, code bytes, host code generation and
+ * code-object load times (ms). All zero for an interpreted program. */
+int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nfast,
+                               int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load);
+/* Trees of the last eval on this context whose tree code handed a tile back
+ * (a sin/cos argument beyond the fast reduction) and were re-evaluated. */
+int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees);
+/* Testing hook (no device needed): compile Float32 trees with the tree
+ * compiler. Returns the code bytes, their assembly text ('\n'-separated lines)
+ * and, per compiled tree, (tree id, byte offset). Each inout_n* holds the
+ * capacity on entry and the size on return; SRHIP_ERR_INVALID if too small. */
+int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_bytes, int64_t* inout_nbytes,
+                          char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
+                          int64_t* inout_noffsets);
+
 /* ---- instrumentation ----------------------------------------------------
  * Device time (ms, HIP events on the context's stream) of the evaluation
  * kernel(s) of the last eval call on this context, and the number of kernel

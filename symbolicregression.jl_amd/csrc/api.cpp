@@ -18,6 +18,7 @@
 
 #include "../../include/srhip.h"
 #include "compile.h"
+#include "jit.h"
 #include "kernels.h"
 
 using namespace srhip;
@@ -97,9 +98,11 @@ struct srhip_ctx {
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
   double last_ms = 0.0;
   int last_launches = 0;
+  int last_bailed = 0;  // trees re-evaluated after their tree code handed a tile back
   DevBuf partial, sums, oks, dloss, scratch_idx, gather;
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
   DevBuf ti_rec;  // threaded-interpreter records of the shallow f32 list
+  DevBuf bail_list, bail_fail;  // trees whose tree code handed a tile back, and their flags
   std::vector<double> h_sum;
   std::vector<uint8_t> h_ok;
 };
@@ -137,6 +140,10 @@ struct srhip_program {
   int32_t* d_tree_off = nullptr;
   int32_t* d_list = nullptr;  // [nlist_a + nlist_b]: shallow trees then deep trees
   int nlist_a = 0, nlist_b = 0;
+  // tree code (jit.cpp) of the first nlist_j shallow slots, Float32 programs
+  jit::Module* jit = nullptr;
+  int nlist_j = 0;
+  jit::Stats jit_stats;
   int opset = OPSET_FULL;      // smallest operator set covering the compiled programs
   // gradient programs (compiled on first use)
   bool grad_built = false;
@@ -175,6 +182,9 @@ void free_grad_device(srhip_program* p) {
 }
 
 void free_program_device(srhip_program* p) {
+  jit::destroy(p->jit);
+  p->jit = nullptr;
+  p->nlist_j = 0;
   if (p->d_code) (void)hipFree(p->d_code);
   if (p->d_tree_off) (void)hipFree(p->d_tree_off);
   if (p->d_list) (void)hipFree(p->d_list);
@@ -236,6 +246,21 @@ void build_grad_program(srhip_program* p) {
   p->grad_built = true;
 }
 
+// Tree code (jit.cpp) on/off: SRHIP_JIT=0 never, =1 for every Float32
+// program, default for programs of at least 512 shallow trees (loading a code
+// object costs about a millisecond). SRHIP_JIT_FAST=0 keeps the FAST path out.
+bool jit_wanted(int nshallow) {
+  if (!jit::available() || nshallow == 0) return false;
+  const char* e = std::getenv("SRHIP_JIT");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return nshallow >= 512;
+}
+bool jit_fast_enabled() {
+  const char* e = std::getenv("SRHIP_JIT_FAST");
+  return !(e && e[0] == '0');
+}
+
 template <typename T>
 void build_program(srhip_program* p) {
   srhip_trees tr;
@@ -270,6 +295,25 @@ void build_program(srhip_program* p) {
   };
   std::stable_sort(a.begin(), a.end(), by_cost);
   std::stable_sort(b.begin(), b.end(), by_cost);
+  // tree code for the shallow Float32 trees of large batches: the compiled
+  // trees lead the shallow list, the others follow (interpreter)
+  jit::destroy(p->jit);
+  p->jit = nullptr;
+  p->nlist_j = 0;
+  p->jit_stats = jit::Stats();
+  if constexpr (std::is_same<T, float>::value) {
+    if (jit_wanted((int)a.size())) {
+      std::vector<int32_t> jl, rest;
+      jit::Options jo;
+      jo.fast = jit_fast_enabled();
+      p->jit = jit::build(cb, a, jl, rest, jo, &p->jit_stats);
+      if (p->jit) {
+        p->nlist_j = (int)jl.size();
+        a = jl;
+        a.insert(a.end(), rest.begin(), rest.end());
+      }
+    }
+  }
   p->nlist_a = (int)a.size();
   p->nlist_b = (int)b.size();
   std::vector<int32_t> list(a);
@@ -326,6 +370,76 @@ static bool rotate_enabled() {
   return e && e[0] == '1';
 }
 
+// Trees whose tree code handed a tile back (a sin/cos argument beyond the
+// fast reduction, jit_template.hip) are evaluated again, whole, by the
+// shallow interpreter kernel; finalize overwrites their results.
+template <typename T>
+void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, const EvalPlan& jplan, int nfeat,
+                  int64_t rows, int loss, double lparam) {
+  (void)jplan;
+  if constexpr (std::is_same<T, float>::value) {
+    hipStream_t s = c->stream;
+    const int nj = p->nlist_j;
+    std::vector<uint32_t> flags((size_t)nj + 1);
+    HIP_CHECK(hipMemcpyAsync(flags.data(), jit::bail_flags(p->jit), flags.size() * sizeof(uint32_t),
+                             hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (flags[nj] == 0) return;
+    std::vector<int32_t> slots;
+    for (int k = 0; k < nj; ++k)
+      if (flags[k]) slots.push_back(k);
+    if (slots.empty()) return;
+    // list = tree ids, list_off = program offsets (copied from the program's list)
+    std::vector<int32_t> all((size_t)2 * (p->nlist_a + p->nlist_b));
+    HIP_CHECK(hipMemcpyAsync(all.data(), p->d_list, all.size() * sizeof(int32_t), hipMemcpyDeviceToHost, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    const size_t nl = (size_t)p->nlist_a + p->nlist_b;
+    const int nb = (int)slots.size();
+    std::vector<int32_t> bl(2 * (size_t)nb);
+    for (int k = 0; k < nb; ++k) {
+      bl[k] = all[slots[k]];
+      bl[nb + k] = all[nl + slots[k]];
+    }
+    c->bail_list.ensure(bl.size() * sizeof(int32_t));
+    c->bail_fail.ensure((size_t)nb * sizeof(uint32_t));
+    HIP_CHECK(hipMemcpyAsync(c->bail_list.p, bl.data(), bl.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipMemsetAsync(c->bail_fail.p, 0, (size_t)nb * sizeof(uint32_t), s));
+    EvalPlan plan;
+    if (!plan_eval(p->dtype, false, OPSET_FULL, MODE_LOSS, ja.w != nullptr, nfeat, rows, nb, &plan))
+      throw Error(SRHIP_ERR_UNSUPPORTED, "row tile does not fit in LDS");
+    EvalArgs<T> a = ja;
+    a.list = static_cast<const int32_t*>(c->bail_list.p);
+    a.list_off = a.list + nb;
+    a.fail = static_cast<uint32_t*>(c->bail_fail.p);
+    a.nlist = nb;
+    a.ti_rec = nullptr;
+    if (ti_enabled()) {
+      c->ti_rec.ensure((size_t)nb * 64 * sizeof(uint4));
+      HIP_CHECK(launch_ti_records(reinterpret_cast<const Ins<float>*>(a.prog), a.list_off, nb,
+                                  (uint32_t)(plan.ntiles * plan.tile * sizeof(T)), static_cast<uint4*>(c->ti_rec.p), s));
+      a.ti_rec = static_cast<const uint4*>(c->ti_rec.p);
+    }
+    a.ntiles = plan.ntiles;
+    a.ntg = plan.ntg;
+    a.tpb = plan.tpb;
+    a.nrg = plan.nrg;
+    a.loss = loss;
+    a.lparam = (T)lparam;
+    c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
+    a.partial = static_cast<Part<T>*>(c->partial.p);
+    HIP_CHECK(hipEventRecord(c->ev[2], s));
+    HIP_CHECK(launch_eval<T>(plan, a, MODE_LOSS, s));
+    HIP_CHECK(hipEventRecord(c->ev[3], s));
+    HIP_CHECK(launch_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
+    HIP_CHECK(hipEventSynchronize(c->ev[3]));
+    float ms = 0.f;
+    HIP_CHECK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
+    c->last_ms += ms;
+    c->last_launches += 1;
+    c->last_bailed = nb;
+  }
+}
+
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
 // n_pad) may be the dataset itself or a gathered row subset.
 template <typename T>
@@ -335,6 +449,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   hipStream_t s = c->stream;
   c->last_ms = 0.0;
   c->last_launches = 0;
+  c->last_bailed = 0;
   c->sums.ensure(std::max<size_t>(p->ntrees, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(p->ntrees, 1));
   const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
@@ -342,18 +457,29 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     c->fail.ensure(std::max<size_t>(nslots, 1) * sizeof(uint32_t));
     HIP_CHECK(hipMemsetAsync(c->fail.p, 0, std::max<size_t>(nslots, 1) * sizeof(uint32_t), s));
   }
-  for (int pass = 0; pass < 2; ++pass) {
-    const int nlist = pass == 0 ? p->nlist_a : p->nlist_b;
+  // slot ranges: [0, nj) tree code, [nj, nlist_a) shallow interpreter, then deep
+  const bool use_jit = std::is_same<T, float>::value && p->jit && p->nlist_j > 0 && mode == MODE_LOSS &&
+                       loss == SRHIP_LOSS_L2;
+  const int nj = use_jit ? p->nlist_j : 0;
+  for (int pass = -1; pass < 2; ++pass) {
+    if (pass == -1 && nj == 0) continue;
+    const int s0 = pass == -1 ? 0 : pass == 0 ? nj : p->nlist_a;
+    const int nlist = pass == -1 ? nj : pass == 0 ? p->nlist_a - nj : p->nlist_b;
     if (nlist == 0 || rows == 0) continue;
     EvalPlan plan;
-    if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan))
+    if (pass == -1) {
+      const int narr = 1 + nfeat + (w ? 1 : 0);
+      if (!plan_geometry(4, 4, kShallowSlots, narr, 2 * 4, rows, nlist, &plan))
+        throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
+    } else if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan)) {
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
+    }
     EvalArgs<T> a;
     a.prog = static_cast<const Ins<T>*>(p->d_code);
     a.tree_off = p->d_tree_off;
-    a.list = p->d_list + (pass == 0 ? 0 : p->nlist_a);
-    a.list_off = a.list + (p->nlist_a + p->nlist_b);
-    a.fail = mode == MODE_LOSS ? static_cast<uint32_t*>(c->fail.p) + (pass == 0 ? 0 : p->nlist_a) : nullptr;
+    a.list = p->d_list + s0;
+    a.list_off = p->d_list + (p->nlist_a + p->nlist_b) + s0;
+    a.fail = mode == MODE_LOSS ? static_cast<uint32_t*>(c->fail.p) + s0 : nullptr;
     a.ti_rec = nullptr;
     if (ti_enabled() && std::is_same<T, float>::value && pass == 0) {
       c->ti_rec.ensure((size_t)nlist * 64 * sizeof(uint4));
@@ -381,7 +507,11 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.out = out;
     a.out_stride = out_stride;
     HIP_CHECK(hipEventRecord(c->ev[0], s));
-    HIP_CHECK(launch_eval<T>(plan, a, mode, s));
+    if (pass == -1) {
+      if constexpr (std::is_same<T, float>::value) HIP_CHECK(jit::launch(p->jit, plan, a, jit_fast_enabled(), s));
+    } else {
+      HIP_CHECK(launch_eval<T>(plan, a, mode, s));
+    }
     HIP_CHECK(hipEventRecord(c->ev[1], s));
     HIP_CHECK(launch_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
     HIP_CHECK(hipEventSynchronize(c->ev[1]));
@@ -389,6 +519,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     c->last_ms += ms;
     c->last_launches += 1;
+    if (pass == -1) rerun_bailed<T>(c, p, a, plan, nfeat, rows, loss, lparam);
   }
 }
 
@@ -490,6 +621,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
   hipStream_t s = c->stream;
   c->last_ms = 0.0;
   c->last_launches = 0;
+  c->last_bailed = 0;
   const int nt = p->ntrees;
   const int nconst = p->const_off.back();
   c->sums.ensure(std::max<size_t>(nt, 1) * sizeof(double));
@@ -693,6 +825,8 @@ int32_t srhip_close(srhip_ctx* ctx) {
     ctx->gather.release();
     ctx->fail.release();
     ctx->ti_rec.release();
+    ctx->bail_list.release();
+    ctx->bail_fail.release();
     for (auto& e : ctx->ev)
       if (e) (void)hipEventDestroy(e);
     (void)hipStreamDestroy(ctx->stream);
@@ -1015,3 +1149,59 @@ int32_t srhip_sync(srhip_ctx* ctx) {
 }
 
 }  // extern "C"
+
+int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nfast,
+                               int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load) {
+  return guarded([&] {
+    if (!prog) throw Error(SRHIP_ERR_INVALID, "null program");
+    const bool on = prog->jit != nullptr;
+    if (out_ntrees) *out_ntrees = on ? prog->nlist_j : 0;
+    if (out_nfast) *out_nfast = on ? prog->jit_stats.nfast : 0;
+    if (out_code_bytes) *out_code_bytes = on ? (int64_t)prog->jit_stats.code_bytes : 0;
+    if (out_ms_codegen) *out_ms_codegen = on ? prog->jit_stats.ms_codegen : 0.0;
+    if (out_ms_load) *out_ms_load = on ? prog->jit_stats.ms_load : 0.0;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees) {
+  return guarded([&] {
+    if (!ctx || !out_ntrees) throw Error(SRHIP_ERR_INVALID, "null argument");
+    *out_ntrees = ctx->last_bailed;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_bytes, int64_t* inout_nbytes,
+                          char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
+                          int64_t* inout_noffsets) {
+  return guarded([&] {
+    if (!trees || !inout_nbytes || !inout_ntext || !inout_noffsets) throw Error(SRHIP_ERR_INVALID, "null argument");
+    if (!jit::available()) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("tree compiler: ") + jit::unavailable_reason());
+    CompiledBatch<float> cb = compile_batch<float>(*trees);
+    std::vector<int32_t> cand;
+    for (int t = 0; t < cb.ntrees; ++t)
+      if (cb.tree_off[t] >= 0 && cb.need[t] <= kShallowSlots) cand.push_back(t);
+    jit::Options jo;
+    jo.fast = fast != 0;
+    jo.text = true;
+    std::vector<uint8_t> bytes;
+    std::string text;
+    std::vector<int32_t> offs;
+    jit::compile_only(cb, cand, jo, &bytes, &text, &offs, nullptr);
+    if ((int64_t)bytes.size() > *inout_nbytes || (int64_t)text.size() + 1 > *inout_ntext ||
+        (int64_t)offs.size() > *inout_noffsets) {
+      *inout_nbytes = (int64_t)bytes.size();
+      *inout_ntext = (int64_t)text.size() + 1;
+      *inout_noffsets = (int64_t)offs.size();
+      throw Error(SRHIP_ERR_INVALID, "output buffers too small");
+    }
+    if (out_bytes && !bytes.empty()) std::memcpy(out_bytes, bytes.data(), bytes.size());
+    if (out_text) std::memcpy(out_text, text.c_str(), text.size() + 1);
+    if (out_offsets && !offs.empty()) std::memcpy(out_offsets, offs.data(), offs.size() * sizeof(int32_t));
+    *inout_nbytes = (int64_t)bytes.size();
+    *inout_ntext = (int64_t)text.size() + 1;
+    *inout_noffsets = (int64_t)offs.size();
+    return SRHIP_OK;
+  });
+}

@@ -253,10 +253,8 @@ def extract(asm_text, name):
         if s.startswith(";;#ASMEND"):
             in_marker = False
             continue
-        if in_marker or not s or s.startswith(";") or s.startswith(".") and not s.endswith(":"):
-            continue
-        s = s.split(";")[0].rstrip()
-        if not s:
+        s = s.split(";")[0].rstrip()  # (a loop header label carries a trailing comment)
+        if in_marker or not s or s.startswith(".") and not s.endswith(":"):
             continue
         if re.match(r"^\.LBB\w+:$", s):
             lines.append(s)

@@ -1,0 +1,278 @@
+#!/usr/bin/env python3
+"""Generate the operator routines of the tree compiler (jit.cpp) for gfx950.
+
+The tree compiler turns every tree of a large batch into straight-line CDNA4
+machine code (one code block per tree, values in VGPRs, no dispatch). Cheap
+operators (+ - * neg abs square cube) are emitted inline by jit.cpp; every
+other operator is a *routine* called with s_swappc_b64: operands in the fixed
+VGPR blocks A and B (R rows each), result in A, non-finite marker in CHK.
+
+Routine bodies are not hand-written: each is compiled by hipcc from the same
+C++ operator code as the interpreters (device_ops.h: bop / uop / mark /
+fast_sincos_f32) inside a tiny kernel whose state is pinned to fixed registers
+with inline-asm constraints, and cut out of the compiler's assembly (the
+machinery of gen_asm_interp.py). Results are therefore bit-identical to the
+interpreters' for the same transcendental build.
+
+Two regions are emitted with the same layout, routine k at the same offset in
+both: FAST (exp / sin / cos in Float32, SR_PRECISE_TRANSC=0) and PRECISE
+(Float64-evaluated, the default build). A tree switches region by adding a
+constant to the call target (s_mdelta), which is how a tile is redone
+precisely when a fast-mode guard fires (jit.cpp).
+
+Outputs (argv[2] = output directory):
+  jit_routines_r<R>.inc  SR_JIT_ROUTINES_TEXT: asm of the routines kernel
+  jit_layout_r<R>.h      register map, routine table, call clobbers
+Usage: gen_jit.py <hipcc> <outdir> [R]
+"""
+import os
+import re
+import subprocess
+import sys
+import tempfile
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, HERE)
+import gen_asm_interp as G  # noqa: E402
+
+UOPS, BOPS = G.UOPS, G.BOPS
+LOSSY_UOPS, LOSSY_LHS, LOSSY_RHS = G.LOSSY_UOPS, G.LOSSY_LHS, G.LOSSY_RHS
+
+
+class JitRegs:
+    """Fixed registers of tree code (jit.cpp mirrors these through jit_layout.h)."""
+
+    def __init__(self, R):
+        self.R = R
+        assert R == 4, "the tree compiler is laid out for 4 rows per lane"
+        self.A, self.B, self.CHK = 32, 36, 40
+        self.LANE, self.LSUM, self.LANE4, self.CHKSAVE = 41, 42, 43, 44
+        self.GCAN, self.GMIN, self.GEXP = 45, 46, 47
+        self.GT, self.Y = 48, 52  # guard temp block, y / loss block
+        self.POOL0, self.NPOOL = 56, 8  # value blocks v56..v87
+        self.VEND = self.POOL0 + self.NPOOL * R  # first register above tree-code state
+        # SGPR state of tree code (pinned in the routine snippets so that no
+        # routine uses them as temporaries)
+        self.S = dict(tile=64, nt=65, partial=66, tilebytes=67, woff=68, status=69, flag=70, rr=72, tgt=74,
+                      rt=76, mdelta=78, fastok=79, eps=80, k=81, pe=82, mode=83, x0=84, x1=85, x2=86, x3=87)
+        self.SPAIRS = {"flag", "rr", "tgt", "rt"}
+
+    def vstate(self):
+        g = [("a", self.A, self.R), ("b", self.B, self.R), ("chk", self.CHK, 1)]
+        # everything else of tree-code state, pinned as one list
+        rest = list(range(self.CHK + 1, self.VEND))
+        return g, rest
+
+    def sregs(self):
+        out = []
+        for n, r in self.S.items():
+            out.append((n, r))
+            if n in self.SPAIRS:
+                out.append((n + "_hi", r + 1))
+        return out
+
+
+def snippet_source(rg, routines):
+    R = rg.R
+    _, rest = rg.vstate()
+    out = ["#define SRHIP_INLINE_ALL 1", '#include "interp.h"', "using namespace srhip; using namespace srhip::interp;",
+           "namespace {", "struct St {", f"  float a[{R}]; float b[{R}]; float chk;", f"  unsigned v[{len(rest)}];"]
+    for n, _ in rg.sregs():
+        out.append(f"  unsigned s_{n};")
+    out.append("};")
+
+    def pins(kind):
+        lines = []
+        regs = [(f"a[{i}]", rg.A + i) for i in range(R)] + [(f"b[{i}]", rg.B + i) for i in range(R)]
+        regs += [("chk", rg.CHK)] + [(f"v[{i}]", r) for i, r in enumerate(rest)]
+        for i in range(0, len(regs), 8):
+            ch = regs[i:i + 8]
+            if kind == "in":
+                lines.append('  asm volatile("; IN" : ' + ", ".join(f'"={{v{r}}}"(s.{e})' for e, r in ch) + ");")
+            else:
+                lines.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{v{r}}}"(s.{e})' for e, r in ch) + ");")
+        ss = rg.sregs()
+        for i in range(0, len(ss), 8):
+            ch = ss[i:i + 8]
+            if kind == "in":
+                lines.append('  asm volatile("; IN" : ' + ", ".join(f'"={{s{r}}}"(s.s_{n})' for n, r in ch) + ");")
+            else:
+                lines.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{s{r}}}"(s.s_{n})' for n, r in ch) + ");")
+        return lines
+
+    for name, body in routines:
+        out.append(f'extern "C" __global__ void __launch_bounds__(64) sr_h_{name}() {{')
+        out.append("  St s;")
+        out += pins("in")
+        out.append("  float& chk = s.chk; (void)chk;")
+        out.append(f"  constexpr int R = {R}; (void)R;")
+        out.append("  " + body)
+        out += pins("out")
+        out.append("}")
+    out.append("}  // namespace")
+    return "\n".join(out) + "\n"
+
+
+def rows(expr):
+    return f"_Pragma(\"unroll\") for (int r = 0; r < R; ++r) {{ {expr} }}"
+
+
+# Operators emitted inline by jit.cpp (no routine).
+INLINE_BOPS = {"ADD", "SUB", "MUL"}
+INLINE_UOPS = {"NEG", "ABS", "SQUARE", "CUBE"}
+
+
+def routine_list():
+    """(name, body, trig) of every routine: one per operator not emitted inline."""
+    rs = []
+    for u in sorted(UOPS, key=lambda k: UOPS[k]):
+        if u in INLINE_UOPS:
+            continue
+        if u in ("SIN", "COS"):
+            body = ("float qm = 0.0f; " +
+                    rows(f"float qa; s.a[r] = dev::fast_sincos_f32(s.a[r], {1 if u == 'COS' else 0}, qa); "
+                         "qm = __builtin_fmaxf(qm, qa);") +
+                    " const unsigned long long fl = __builtin_amdgcn_ballot_w64(!(qm <= dev::kTrigQMax));"
+                    " s.s_flag = (unsigned)fl; s.s_flag_hi = (unsigned)(fl >> 32);")
+            rs.append((f"u_{u.lower()}", body, True))
+        else:
+            mk = "chk = mark(s.a[r], chk); " if u in LOSSY_UOPS else ""
+            rs.append((f"u_{u.lower()}", rows(f"{mk}s.a[r] = dev::uop<SRHIP_UOP_{u}>(s.a[r]);"), False))
+    for b in sorted(BOPS, key=lambda k: BOPS[k]):
+        if b in INLINE_BOPS:
+            continue
+        mk = ("chk = mark(s.a[r], chk); " if b in LOSSY_LHS else "") + \
+             ("chk = mark(s.b[r], chk); " if b in LOSSY_RHS else "")
+        rs.append((f"b_{b.lower()}", rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], s.b[r]);"), False))
+    return rs
+
+
+def compile_bodies(hipcc, rg, routines, extra):
+    src = snippet_source(rg, [(n, b) for n, b, _ in routines])
+    with tempfile.TemporaryDirectory() as td:
+        sp = os.path.join(td, "routines.hip")
+        open(sp, "w").write(src)
+        ap = os.path.join(td, "routines.s")
+        cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-ffp-contract=off", "--cuda-device-only",
+               "-S", "-I", HERE, sp, "-o", ap] + extra
+        r = subprocess.run(cmd, capture_output=True, text=True)
+        if r.returncode != 0:
+            sys.stderr.write(r.stderr)
+            raise SystemExit("gen_jit: routine compile failed")
+        asm = open(ap).read()
+    bodies = {}
+    for n, _, _ in routines:
+        try:
+            bodies[n] = G.extract(asm, n)
+        except SystemExit as e:  # a body the block cannot hold (memory operands, calls): no routine
+            sys.stderr.write(f"gen_jit: routine {n} skipped ({e})\n")
+    return bodies
+
+
+def label_sizes(lines_by_name, order):
+    """Assemble every body standalone; return its byte size."""
+    T = []
+    for n in order:
+        T.append(f".Lsr_start_{n}_%=:")
+        T += lines_by_name[n]
+        T.append(f".Lsr_end_{n}_%=:")
+    T.insert(0, ".Lsr_base_%=:")
+    offs = G.label_offsets(T)
+    return {n: offs[f"end_{n}"] - offs[f"start_{n}"] for n in order}
+
+
+def build(hipcc, outdir, R):
+    rg = JitRegs(R)
+    routines = routine_list()
+    fast = compile_bodies(hipcc, rg, routines, ["-DSR_PRECISE_TRANSC=0"])
+    prec = compile_bodies(hipcc, rg, routines, [])
+    names = [n for n, _, _ in routines if n in fast and n in prec]
+    trig = {n for n, _, t in routines if t}
+    vstate = set(range(rg.A, rg.VEND))
+    sstate = {r for _, r in rg.sregs()}
+    vtemp, stemp = set(), set()
+    for d in (fast, prec):
+        for n in names:
+            vtemp |= G.regs_used(d[n], G.REG_V) - vstate
+            stemp |= G.regs_used(d[n], G.REG_S) - sstate
+    if vtemp & vstate or stemp & sstate:
+        raise SystemExit("gen_jit: temp/state overlap")
+    if max(vtemp, default=0) >= rg.A:
+        raise SystemExit(f"gen_jit: routine VGPR temps reach v{max(vtemp)} (state starts at v{rg.A})")
+    if max(stemp, default=0) >= 64:
+        raise SystemExit(f"gen_jit: routine SGPR temps reach s{max(stemp)}")
+
+    def with_ret(lines, n, t):
+        body = list(lines)
+        while body and body[0].startswith("s_nop"):
+            body.pop(0)
+        out = [l.replace("%=", f"{t}") for l in body]
+        # a trig routine's bail flag is tested by the caller (tree code)
+        out.append(f"s_setpc_b64 s[{rg.S['rr']}:{rg.S['rr'] + 1}]")
+        return out
+
+    fb = {n: with_ret(fast[n], n, "f") for n in names}
+    pb = {n: with_ret(prec[n], n, "p") for n in names}
+    fs = label_sizes(fb, names)
+    ps = label_sizes(pb, names)
+    slot = {n: (max(fs[n], ps[n]) + 63) // 64 * 64 for n in names}
+    text = ["s_endpgm"]
+    for region, bodies, sizes in (("fast", fb, fs), ("prec", pb, ps)):
+        text.append(".p2align 8")
+        text.append(f".globl sr_rt_{region}")
+        text.append(f"sr_rt_{region}:")
+        for n in names:
+            text.append(f".globl sr_rt_{region}_{n}")
+            text.append(f"sr_rt_{region}_{n}:")
+            text += bodies[n]
+            pad = slot[n] - sizes[n]
+            assert pad % 4 == 0
+            if pad:
+                text.append(f".fill {pad // 4}, 4, 0xbf800000")  # s_nop 0
+    os.makedirs(outdir, exist_ok=True)
+    inc = os.path.join(outdir, f"jit_routines_r{R}.inc")
+    with open(inc, "w") as f:
+        f.write(f"// Generated by gen_jit.py (R={R}); do not edit.\n#pragma once\n#define SR_JIT_ROUTINES_TEXT \\\n")
+        for ln in text:
+            f.write('  "' + ln.replace("\\", "\\\\").replace('"', '\\"') + '\\n" \\\n')
+        f.write('  ""\n')
+    # layout header
+    uop_rt = {UOPS[u]: f"u_{u.lower()}" for u in UOPS}
+    bop_rt = {BOPS[b]: f"b_{b.lower()}" for b in BOPS}
+    hp = os.path.join(outdir, f"jit_layout_r{R}.h")
+    clob_v = sorted(vtemp | (vstate - {rg.CHK, rg.LANE, rg.LSUM, rg.LANE4}))
+    clob_s = sorted(stemp | (sstate - {rg.S[k] for k in ("tile", "nt", "partial", "tilebytes", "woff", "fastok",
+                                                          "status")}))
+    with open(hp, "w") as f:
+        f.write(f"// Generated by gen_jit.py (R={R}); do not edit.\n#pragma once\n")
+        f.write(f"#define SR_JIT_R {R}\n")
+        for k, v in (("A", rg.A), ("B", rg.B), ("CHK", rg.CHK), ("LANE", rg.LANE), ("LSUM", rg.LSUM),
+                     ("LANE4", rg.LANE4), ("CHKSAVE", rg.CHKSAVE), ("GCAN", rg.GCAN), ("GMIN", rg.GMIN),
+                     ("GEXP", rg.GEXP), ("GT", rg.GT), ("Y", rg.Y), ("POOL0", rg.POOL0), ("NPOOL", rg.NPOOL),
+                     ("VEND", rg.VEND)):
+            f.write(f"#define SR_JIT_V_{k} {v}\n")
+        for k, v in rg.S.items():
+            f.write(f"#define SR_JIT_S_{k.upper()} {v}\n")
+        f.write("// routine of each unary / binary operator (-1: inline or not available)\n")
+        def rid(n):
+            return names.index(n) if n in names else -1
+        f.write("#define SR_JIT_UOP_ROUTINE {" + ", ".join(
+            str(-1 if u_name.upper()[2:] in INLINE_UOPS else rid(u_name))
+            for _, u_name in sorted(uop_rt.items())) + "}\n")
+        f.write("#define SR_JIT_BOP_ROUTINE {" + ", ".join(
+            str(-1 if b_name.upper()[2:] in INLINE_BOPS else rid(b_name))
+            for _, b_name in sorted(bop_rt.items())) + "}\n")
+        f.write(f"#define SR_JIT_NUM_ROUTINES {len(names)}\n")
+        f.write("#define SR_JIT_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
+        f.write("#define SR_JIT_ROUTINE_TRIG {" + ", ".join("1" if n in trig else "0" for n in names) + "}\n")
+        f.write("#define SR_JIT_CLOBBERS " + ", ".join([f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s]
+                                                          + ['"vcc"', '"scc"', '"m0"']) + "\n")
+        f.write(f"// routine VGPR temps v{min(vtemp)}..v{max(vtemp)}, SGPR temps {sorted(stemp)}\n")
+        f.write("// routine sizes (fast / precise bytes): " +
+                ", ".join(f"{n} {fs[n]}/{ps[n]}" for n in names) + "\n")
+
+
+if __name__ == "__main__":
+    hipcc, outdir = sys.argv[1], sys.argv[2]
+    R = int(sys.argv[3]) if len(sys.argv) > 3 else 4
+    build(hipcc, outdir, R)

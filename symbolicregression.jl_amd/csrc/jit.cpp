@@ -1,0 +1,1077 @@
+// jit.cpp — the tree compiler: accumulator-machine programs (compile.cpp) →
+// straight-line gfx950 machine code, one block per tree, loaded per program.
+//
+// Why: the threaded interpreter pays, per node, a scalar record load, an
+// s_setpc dispatch and an LDS read of the next X operand whether or not it is
+// needed (2 KiB of LDS per wave-instruction, the LDS array's 256 B/clk is the
+// bound for + - * trees: DESIGN.md §3). Tree code has none of that: values
+// live in VGPR blocks chosen by a register allocator, the features a tree
+// uses are read from LDS once per tile, constants are instruction literals,
+// + - * neg abs square cube are single VALU instructions, every other
+// operator is a routine (gen_jit.py: hipcc-compiled device_ops.h code with
+// pinned registers) entered with s_swappc_b64.
+//
+// Tree code (R = 4 rows per lane, tiles of 256 rows, LDS layout of the driver
+// in jit_template.hip): for each tile from s_tile to s_nt: read y and the
+// used features, run the operators, mark the root, add the tile's L2 sum in
+// the order of eval_kernel.h's tile_loss, stop at the first non-finite tile.
+//
+// FAST path (trees whose operators are + - * / neg abs square cube exp sin
+// cos): exp / sin / cos run their Float32 routines (<= 1-2 ulp), and guards
+// catch every row where that could change did_succeed against the Float64-
+// evaluated routines: a cancellation |a ± b| <= 2^-14 (|a|+|b|)
+// or a magnitude below 2^-120 on a transcendental-derived value that can
+// make a divisor exactly 0, and |x| > 87 at exp (overflow / underflow
+// thresholds). A tile whose guards fire, or that fails, is redone at once
+// with the PRECISE routines (same code, call targets shifted to the PRECISE
+// region); only what the PRECISE pass says is kept.
+#include "jit.h"
+
+#include <elf.h>
+
+#include <algorithm>
+#include <chrono>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+
+#include "gen/jit_layout_r4.h"
+
+// code-object templates (jit_blob.S): 1 MiB and 4 MiB code areas
+extern "C" const unsigned char srhip_jit_tmpl_s[];
+extern "C" const unsigned char srhip_jit_tmpl_s_end[];
+extern "C" const unsigned char srhip_jit_tmpl_l[];
+extern "C" const unsigned char srhip_jit_tmpl_l_end[];
+
+#define HIP_CHECK(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw Error(SRHIP_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));  \
+  } while (0)
+
+namespace srhip {
+namespace jit {
+namespace {
+
+constexpr int R = SR_JIT_R;
+static_assert(R == 4, "tree code is laid out for 4 rows per lane");
+constexpr int VA = SR_JIT_V_A, VB = SR_JIT_V_B, VCHK = SR_JIT_V_CHK, VLANE = SR_JIT_V_LANE;
+constexpr int VLSUM = SR_JIT_V_LSUM, VLANE4 = SR_JIT_V_LANE4, VCHKSAVE = SR_JIT_V_CHKSAVE;
+constexpr int VGCAN = SR_JIT_V_GCAN, VGMIN = SR_JIT_V_GMIN, VGEXP = SR_JIT_V_GEXP;
+constexpr int VGT = SR_JIT_V_GT, VY = SR_JIT_V_Y, VPOOL0 = SR_JIT_V_POOL0, NPOOL = SR_JIT_V_NPOOL;
+constexpr int S_TILE = SR_JIT_S_TILE, S_NT = SR_JIT_S_NT, S_PARTIAL = SR_JIT_S_PARTIAL;
+constexpr int S_TILEBYTES = SR_JIT_S_TILEBYTES, S_WOFF = SR_JIT_S_WOFF, S_STATUS = SR_JIT_S_STATUS;
+constexpr int S_FLAG = SR_JIT_S_FLAG, S_RR = SR_JIT_S_RR, S_TGT = SR_JIT_S_TGT, S_RT = SR_JIT_S_RT;
+constexpr int S_MDELTA = SR_JIT_S_MDELTA, S_FASTOK = SR_JIT_S_FASTOK, S_EPS = SR_JIT_S_EPS;
+constexpr int S_K = SR_JIT_S_K, S_PE = SR_JIT_S_PE, S_MODE = SR_JIT_S_MODE;
+constexpr int TILE = 64 * R;
+constexpr int kNumRoutines = SR_JIT_NUM_ROUTINES;
+const int kUopRoutine[SRHIP_NUM_UOPS] = SR_JIT_UOP_ROUTINE;
+const int kBopRoutine[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE;
+const char* const kRoutineName[kNumRoutines] = SR_JIT_ROUTINE_NAMES;
+const int kRoutineTrig[kNumRoutines] = SR_JIT_ROUTINE_TRIG;
+
+// ---- the code-object template ---------------------------------------------------
+struct Tmpl {
+  const uint8_t* img = nullptr;
+  size_t size = 0;
+  size_t area_off = 0;     // file offset of sr_jit_code
+  size_t area_bytes = 0;   // usable bytes of the area
+  uint64_t area_va = 0;    // its address in the image
+  uint64_t rt_va[kNumRoutines] = {};  // FAST routine addresses
+  uint64_t delta = 0;      // PRECISE - FAST region offset
+  bool ok = false;
+  std::string why;
+};
+
+bool parse_tmpl(const uint8_t* img, size_t size, Tmpl* t) {
+  t->img = img;
+  t->size = size;
+  if (size < sizeof(Elf64_Ehdr)) { t->why = "template too small"; return false; }
+  Elf64_Ehdr eh;
+  std::memcpy(&eh, img, sizeof(eh));
+  if (std::memcmp(eh.e_ident, ELFMAG, SELFMAG) != 0 || eh.e_ident[EI_CLASS] != ELFCLASS64 ||
+      eh.e_shoff + (size_t)eh.e_shnum * sizeof(Elf64_Shdr) > size) {
+    t->why = "template is not an ELF64 image";
+    return false;
+  }
+  std::vector<Elf64_Shdr> sh(eh.e_shnum);
+  std::memcpy(sh.data(), img + eh.e_shoff, sh.size() * sizeof(Elf64_Shdr));
+  const Elf64_Shdr* symtab = nullptr;
+  for (auto& s : sh)
+    if (s.sh_type == SHT_SYMTAB) symtab = &s;
+  if (!symtab || symtab->sh_link >= sh.size()) { t->why = "template has no symbol table"; return false; }
+  const Elf64_Shdr& strtab = sh[symtab->sh_link];
+  const size_t nsym = symtab->sh_size / sizeof(Elf64_Sym);
+  uint64_t code_va = 0, area_fn_va = 0, area_fn_size = 0, fast0 = 0, prec0 = 0;
+  uint64_t prec_va[kNumRoutines] = {};
+  int found = 0;
+  for (size_t i = 0; i < nsym; ++i) {
+    Elf64_Sym sym;
+    std::memcpy(&sym, img + symtab->sh_offset + i * sizeof(Elf64_Sym), sizeof(sym));
+    if (sym.st_name >= strtab.sh_size) continue;
+    const char* nm = reinterpret_cast<const char*>(img + strtab.sh_offset + sym.st_name);
+    const std::string n(nm);
+    if (n == "sr_jit_code") { code_va = sym.st_value; found |= 1; }
+    else if (n == "sr_jit_area") { area_fn_va = sym.st_value; area_fn_size = sym.st_size; found |= 2; }
+    else if (n == "sr_rt_fast") { fast0 = sym.st_value; found |= 4; }
+    else if (n == "sr_rt_prec") { prec0 = sym.st_value; found |= 8; }
+    else if (n.rfind("sr_rt_fast_", 0) == 0 || n.rfind("sr_rt_prec_", 0) == 0) {
+      const std::string rn = n.substr(11);
+      for (int k = 0; k < kNumRoutines; ++k)
+        if (rn == kRoutineName[k]) (n[6] == 'f' ? t->rt_va : prec_va)[k] = sym.st_value;
+    }
+  }
+  if (found != 15) { t->why = "template symbols missing"; return false; }
+  for (int k = 0; k < kNumRoutines; ++k) {
+    if (!t->rt_va[k] || !prec_va[k]) { t->why = std::string("routine missing: ") + kRoutineName[k]; return false; }
+    if (prec_va[k] - t->rt_va[k] != prec0 - fast0) { t->why = "FAST / PRECISE routine layouts differ"; return false; }
+  }
+  t->delta = prec0 - fast0;
+  const Elf64_Shdr* text = nullptr;
+  for (auto& s : sh)
+    if (s.sh_type == SHT_PROGBITS && (s.sh_flags & SHF_EXECINSTR) && code_va >= s.sh_addr &&
+        code_va < s.sh_addr + s.sh_size)
+      text = &s;
+  if (!text) { t->why = "code area outside .text"; return false; }
+  t->area_va = code_va;
+  t->area_off = (size_t)(code_va - text->sh_addr + text->sh_offset);
+  // the area function: s_endpgm, the area, the compiler's closing s_endpgm
+  const uint64_t end = area_fn_va + area_fn_size;
+  if (end <= code_va + 64 || end > text->sh_addr + text->sh_size) { t->why = "bad area size"; return false; }
+  t->area_bytes = (size_t)(end - code_va) - 64;
+  if (t->area_off + t->area_bytes > size) { t->why = "area beyond the image"; return false; }
+  t->ok = true;
+  return true;
+}
+
+struct Templates {
+  Tmpl small, large;
+  bool ok = false;
+  std::string why;
+};
+
+const Templates& templates() {
+  static Templates T;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    const bool a = parse_tmpl(srhip_jit_tmpl_s, (size_t)(srhip_jit_tmpl_s_end - srhip_jit_tmpl_s), &T.small);
+    const bool b = parse_tmpl(srhip_jit_tmpl_l, (size_t)(srhip_jit_tmpl_l_end - srhip_jit_tmpl_l), &T.large);
+    T.ok = a && b && T.small.delta == T.large.delta;
+    T.why = !a ? T.small.why : !b ? T.large.why : (T.ok ? "" : "templates disagree");
+  });
+  return T;
+}
+
+// ---- instruction encoder (gfx950 formats), with an assembly-text mirror ---------
+struct Src {
+  int enc = 0;        // 9-bit operand field
+  bool lit = false;   // a 32-bit literal follows
+  uint32_t val = 0;
+  std::string name;
+};
+
+bool inline_const(uint32_t b, int* enc) {
+  const int32_t i = (int32_t)b;
+  if (i >= 0 && i <= 64) { *enc = 128 + i; return true; }
+  if (i >= -16 && i <= -1) { *enc = 192 - i; return true; }
+  switch (b) {
+    case 0x3f000000u: *enc = 240; return true;  // 0.5
+    case 0xbf000000u: *enc = 241; return true;
+    case 0x3f800000u: *enc = 242; return true;  // 1.0
+    case 0xbf800000u: *enc = 243; return true;
+    case 0x40000000u: *enc = 244; return true;  // 2.0
+    case 0xc0000000u: *enc = 245; return true;
+    case 0x40800000u: *enc = 246; return true;  // 4.0
+    case 0xc0800000u: *enc = 247; return true;
+    case 0x3e22f983u: *enc = 248; return true;  // 1/(2 pi)
+    default: return false;
+  }
+}
+
+std::string hex32(uint32_t v) {
+  char b[16];
+  std::snprintf(b, sizeof b, "0x%x", v);
+  return b;
+}
+
+Src V(int r) { return Src{256 + r, false, 0, "v" + std::to_string(r)}; }
+Src S(int r) { return Src{r, false, 0, "s" + std::to_string(r)}; }
+Src K(uint32_t bits) {
+  Src s;
+  int e;
+  if (inline_const(bits, &e)) {
+    s.enc = e;
+  } else {
+    s.enc = 255;
+    s.lit = true;
+    s.val = bits;
+  }
+  s.name = hex32(bits);
+  return s;
+}
+
+struct Asm {
+  std::vector<uint32_t> w;
+  bool want_text = false;
+  std::vector<std::string> lines;
+  std::vector<int> lab;  // word index of each label (-1: unbound)
+  struct Fix { size_t word; int label; size_t line; };
+  std::vector<Fix> fix;
+
+  size_t bytes() const { return w.size() * 4; }
+  void put(uint32_t x) { w.push_back(x); }
+  void t(const std::string& s) {
+    if (want_text) lines.push_back(s);
+  }
+  int label() { lab.push_back(-1); return (int)lab.size() - 1; }
+  void bind(int l) { lab[l] = (int)w.size(); }
+
+  // SOP1/SOP2/SOPC/VOP1/VOP2/VOPC with an optional literal
+  void lit(const Src& a) {
+    if (a.lit) put(a.val);
+  }
+  void sop1(int op, const char* nm, int sdst, const Src& s0, const std::string& dname) {
+    put(0xbe800000u | ((uint32_t)sdst << 16) | ((uint32_t)op << 8) | (uint32_t)s0.enc);
+    lit(s0);
+    t(std::string(nm) + " " + dname + ", " + s0.name);
+  }
+  void sop2(int op, const char* nm, int sdst, const Src& s0, const Src& s1) {
+    put(0x80000000u | ((uint32_t)op << 23) | ((uint32_t)sdst << 16) | ((uint32_t)s1.enc << 8) | (uint32_t)s0.enc);
+    lit(s0.lit ? s0 : s1);
+    t(std::string(nm) + " s" + std::to_string(sdst) + ", " + s0.name + ", " + s1.name);
+  }
+  void sopc(int op, const char* nm, const Src& s0, const Src& s1, const std::string& n0 = "") {
+    put(0xbf000000u | ((uint32_t)op << 16) | ((uint32_t)s1.enc << 8) | (uint32_t)s0.enc);
+    lit(s0.lit ? s0 : s1);
+    t(std::string(nm) + " " + (n0.empty() ? s0.name : n0) + ", " + s1.name);
+  }
+  void sopp(int op, const char* nm, int imm, bool show = true) {
+    put(0xbf800000u | ((uint32_t)op << 16) | ((uint32_t)imm & 0xffffu));
+    t(show ? std::string(nm) + " " + std::to_string(imm) : std::string(nm));
+  }
+  void branch(int op, const char* nm, int l) {
+    fix.push_back({w.size(), l, want_text ? lines.size() : 0});
+    put(0xbf800000u | ((uint32_t)op << 16));
+    t(std::string(nm) + " @");
+  }
+  void vop1(int op, const char* nm, int vdst, const Src& s0) {
+    put(0x7e000000u | ((uint32_t)vdst << 17) | ((uint32_t)op << 9) | (uint32_t)s0.enc);
+    lit(s0);
+    t(std::string(nm) + " v" + std::to_string(vdst) + ", " + s0.name);
+  }
+  void vop2(int op, const char* nm, int vdst, const Src& s0, int vsrc1, const char* tail = "") {
+    put(((uint32_t)op << 25) | ((uint32_t)vdst << 17) | ((uint32_t)vsrc1 << 9) | (uint32_t)s0.enc);
+    lit(s0);
+    t(std::string(nm) + " v" + std::to_string(vdst) + ", " + s0.name + ", v" + std::to_string(vsrc1) + tail);
+  }
+  void vopc(int op, const char* nm, const Src& s0, int vsrc1) {
+    put(0x7c000000u | ((uint32_t)op << 17) | ((uint32_t)vsrc1 << 9) | (uint32_t)s0.enc);
+    lit(s0);
+    t(std::string(nm) + " vcc, " + s0.name + ", v" + std::to_string(vsrc1));
+  }
+  // VOP3 (no literals on gfx9): abs / neg bit i applies to source i
+  void vop3(int op, const char* nm, int vdst, const Src& s0, const Src& s1, const Src* s2, int abs, int neg) {
+    if (s0.lit || s1.lit || (s2 && s2->lit)) throw Error(SRHIP_ERR_INVALID, "jit: literal in a VOP3 operand");
+    put(0xd0000000u | ((uint32_t)op << 16) | ((uint32_t)(abs & 7) << 8) | (uint32_t)vdst);
+    put(((uint32_t)(neg & 7) << 29) | ((uint32_t)(s2 ? s2->enc : 0) << 18) | ((uint32_t)s1.enc << 9) |
+        (uint32_t)s0.enc);
+    auto f = [&](const Src& s, int i) {
+      std::string n = s.name;
+      if (abs & (1 << i)) n = "|" + n + "|";
+      if (neg & (1 << i)) n = "-" + n;
+      return n;
+    };
+    t(std::string(nm) + " v" + std::to_string(vdst) + ", " + f(s0, 0) + ", " + f(s1, 1) + (s2 ? ", " + f(*s2, 2) : ""));
+  }
+  void ds_read_b128(int vdst, int vaddr, int offset) {
+    put(0xd8000000u | (0xffu << 17) | (uint32_t)(offset & 0xffff));
+    put(((uint32_t)vdst << 24) | (uint32_t)vaddr);
+    t("ds_read_b128 v[" + std::to_string(vdst) + ":" + std::to_string(vdst + 3) + "], v" + std::to_string(vaddr) +
+      (offset ? " offset:" + std::to_string(offset) : ""));
+  }
+  void waitcnt_lgkm(int n) { sopp(0x0c, "s_waitcnt", 0xc07f | (n << 8), false); if (want_text) lines.back() = "s_waitcnt lgkmcnt(" + std::to_string(n) + ")"; }
+
+  void finish() {
+    for (const Fix& f : fix) {
+      if (lab[f.label] < 0) throw Error(SRHIP_ERR_INVALID, "jit: unbound label");
+      const int d = lab[f.label] - (int)(f.word + 1);
+      if (d < -32768 || d > 32767) throw Error(SRHIP_ERR_INVALID, "jit: branch out of range");
+      w[f.word] = (w[f.word] & 0xffff0000u) | ((uint32_t)d & 0xffffu);
+      if (want_text) {
+        std::string& s = lines[f.line];
+        s = s.substr(0, s.size() - 1) + std::to_string(d);
+      }
+    }
+    fix.clear();
+  }
+};
+
+// VALU / SALU opcodes (gfx9 encodings, checked against llvm-mc by tests/test_jit.py)
+enum : int {
+  VOP2_CNDMASK = 0x00, VOP2_ADD_F32 = 0x01, VOP2_SUB_F32 = 0x02, VOP2_SUBREV_F32 = 0x03, VOP2_MUL_F32 = 0x05,
+  VOP2_MIN_F32 = 0x0a, VOP2_MAX_F32 = 0x0b, VOP2_AND_B32 = 0x13, VOP2_XOR_B32 = 0x15, VOP2_ADD_U32 = 0x34,
+  VOP1_MOV = 0x01,
+  VOP3_ADD_F32 = 0x101, VOP3_MIN_F32 = 0x10a, VOP3_MAX_F32 = 0x10b, VOP3_FMA_F32 = 0x1cb,
+  VOPC_LT_F32 = 0x41, VOPC_LE_F32 = 0x43, VOPC_GT_F32 = 0x44, VOPC_U_F32 = 0x48, VOPC_GT_I32 = 0xc4,
+  SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
+  SOP2_ADD_U32 = 0x00, SOP2_SUB_I32 = 0x03, SOP2_ADDC_U32 = 0x04, SOP2_CSELECT = 0x0a,
+  SOPC_EQ_U32 = 0x06, SOPC_LG_U32 = 0x07, SOPC_GE_U32 = 0x09, SOPC_LT_U32 = 0x0a, SOPC_LG_U64 = 0x13,
+  SOPP_BRANCH = 0x02, SOPP_SCC0 = 0x04, SOPP_SCC1 = 0x05, SOPP_VCCNZ = 0x07,
+};
+
+// ---- IR ------------------------------------------------------------------------
+enum { O_VAL = 0, O_X = 1, O_C = 2 };
+struct Opnd {
+  int k = O_VAL;
+  int v = -1;        // value id (O_VAL) or feature (O_X)
+  uint32_t c = 0;    // constant bits (O_C)
+};
+struct IrOp {
+  bool un = false;
+  int op = 0;
+  Opnd a, b;
+  int rid = -1;      // routine, -1: inline
+  bool taint = false, zs = false;
+  int consumer = -1, cpos = 0;
+};
+
+constexpr uint32_t kFastUops = (1u << SRHIP_UOP_NEG) | (1u << SRHIP_UOP_ABS) | (1u << SRHIP_UOP_SQUARE) |
+                               (1u << SRHIP_UOP_CUBE) | (1u << SRHIP_UOP_EXP) | (1u << SRHIP_UOP_SIN) |
+                               (1u << SRHIP_UOP_COS);
+constexpr uint32_t kFastBops = (1u << SRHIP_BOP_ADD) | (1u << SRHIP_BOP_SUB) | (1u << SRHIP_BOP_MUL) |
+                               (1u << SRHIP_BOP_DIV);
+
+bool is_inline(const IrOp& o) {
+  return o.un ? (o.op == SRHIP_UOP_NEG || o.op == SRHIP_UOP_ABS || o.op == SRHIP_UOP_SQUARE || o.op == SRHIP_UOP_CUBE)
+              : (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB || o.op == SRHIP_BOP_MUL);
+}
+
+uint32_t fbits(float f) {
+  uint32_t u;
+  std::memcpy(&u, &f, 4);
+  return u;
+}
+
+// Program (compile.cpp) → IR: the accumulator machine with register renaming.
+bool build_ir(const Ins<float>* p, std::vector<IrOp>& ops, Opnd& root) {
+  ops.clear();
+  Opnd acc, tmp, slot[kMaxSlots];
+  for (int pc = 0;; ++pc) {
+    if (pc > 4096) return false;
+    const uint32_t code = p[pc].code;
+    const int opc = (int)(code & 0xffu);
+    const int f = (int)(code >> 16);
+    const float imm = p[pc].imm;
+    auto X = [&](int ff) { Opnd o; o.k = O_X; o.v = ff; return o; };
+    auto C = [&](float c) { Opnd o; o.k = O_C; o.c = fbits(c); return o; };
+    auto val = [&](IrOp o) {
+      ops.push_back(o);
+      Opnd r; r.k = O_VAL; r.v = (int)ops.size() - 1;
+      return r;
+    };
+    if (opc == OP_END) { root = acc; return true; }
+    if (opc == OP_LDX) { acc = X(f); continue; }
+    if (opc == OP_LDC) { acc = C(imm); continue; }
+    if (opc >= OP_PUSH0 && opc < OP_PUSH0 + kMaxSlots) { slot[opc - OP_PUSH0] = acc; continue; }
+    if (opc >= OP_POP0 && opc < OP_POP0 + kMaxSlots) { tmp = slot[opc - OP_POP0]; continue; }
+    if (opc >= OP_UN0 && opc < OP_BIN0) {
+      IrOp o; o.un = true; o.op = opc - OP_UN0; o.a = acc;
+      if (acc.k != O_VAL && !(o.un && is_inline(o) && acc.k == O_X)) {
+        // a unary operator on a leaf (only with constant folding off): keep it simple
+        if (acc.k == O_C) return false;
+      }
+      acc = val(o);
+      continue;
+    }
+    const int v = (opc - OP_BIN0) / SRHIP_NUM_BOPS;
+    const int b = (opc - OP_BIN0) % SRHIP_NUM_BOPS;
+    IrOp o; o.un = false; o.op = b;
+    uint32_t g;
+    std::memcpy(&g, &imm, 4);
+    switch (v) {
+      case V_AX: o.a = acc; o.b = X(f); break;
+      case V_XA: o.a = X(f); o.b = acc; break;
+      case V_AC: o.a = acc; o.b = C(imm); break;
+      case V_CA: o.a = C(imm); o.b = acc; break;
+      case V_AT: o.a = acc; o.b = tmp; break;
+      case V_TA: o.a = tmp; o.b = acc; break;
+      case V_XX: o.a = X(f); o.b = X((int)g); break;
+      case V_XC: o.a = X(f); o.b = C(imm); break;
+      case V_CX: o.a = C(imm); o.b = X(f); break;
+      default: return false;
+    }
+    if (o.a.k == O_C && o.b.k == O_C) return false;
+    acc = val(o);
+  }
+}
+
+// ---- code generation of one tree --------------------------------------------------
+struct Gen {
+  Asm& as;
+  const Tmpl& T;
+  uint64_t base_va;     // address of this tree's first instruction
+  bool fast_opt;
+  std::vector<IrOp> ops;
+  Opnd root;
+  bool fast = false;    // this tree has a guarded FAST path
+  bool g_can = false, g_min = false, g_exp = false, has_trig = false;
+  // allocation state
+  enum { L_NONE = -1, L_A = 100, L_B = 101 };
+  std::vector<int> loc;          // per value
+  int pool_owner[NPOOL];         // -1 free, value id, or 1000 + feature
+  int a_owner = -1, b_owner = -1;
+  int xblk[256];
+  int xlast[256];
+  std::vector<int> feats;        // features in first-use order
+  int load_idx[256];             // load number (0 = y)
+  int nloads = 0, waited = 0;
+  std::vector<int> next_call;    // first call index > i
+  int L_tile = -1, L_done = -1, L_redo = -1, L_bail = -1;
+  std::string why;
+
+  Gen(Asm& a, const Tmpl& t, uint64_t va, bool f) : as(a), T(t), base_va(va), fast_opt(f) {}
+
+  uint64_t cur_va() const { return base_va + as.bytes(); }
+  int reg_of_loc(int l) const { return l == L_A ? VA : l == L_B ? VB : VPOOL0 + R * l; }
+
+  bool analyze() {
+    const int n = (int)ops.size();
+    // routines, consumers
+    for (int i = 0; i < n; ++i) {
+      IrOp& o = ops[i];
+      if (!is_inline(o)) {
+        o.rid = o.un ? kUopRoutine[o.op] : kBopRoutine[o.op];
+        if (o.rid < 0) { why = "operator without routine"; return false; }
+        if (kRoutineTrig[o.rid]) has_trig = true;
+      }
+      for (int s = 0; s < 2; ++s) {
+        const Opnd& q = s ? o.b : o.a;
+        if (s && o.un) break;
+        if (q.k == O_VAL) { ops[q.v].consumer = i; ops[q.v].cpos = s; }
+      }
+    }
+    // FAST eligibility, taint, zero sensitivity
+    bool elig = fast_opt, trans = false;
+    for (auto& o : ops) {
+      if (o.un ? !((kFastUops >> o.op) & 1u) : !((kFastBops >> o.op) & 1u)) elig = false;
+      if (o.un && (o.op == SRHIP_UOP_EXP || o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS)) trans = true;
+    }
+    fast = elig && trans;
+    for (int i = 0; i < n; ++i) {
+      IrOp& o = ops[i];
+      o.taint = o.un && (o.op == SRHIP_UOP_EXP || o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS);
+      if (o.a.k == O_VAL && ops[o.a.v].taint) o.taint = true;
+      if (!o.un && o.b.k == O_VAL && ops[o.b.v].taint) o.taint = true;
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      IrOp& o = ops[i];
+      auto mark = [&](const Opnd& q) {
+        if (q.k == O_VAL) ops[q.v].zs = true;
+      };
+      if (!o.un) {
+        if (o.op == SRHIP_BOP_DIV) {
+          mark(o.b);
+          if (o.zs) mark(o.a);
+        } else if (o.zs && (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB || o.op == SRHIP_BOP_MUL)) {
+          mark(o.a);
+          mark(o.b);
+        }
+      } else if (o.zs && (o.op == SRHIP_UOP_NEG || o.op == SRHIP_UOP_ABS || o.op == SRHIP_UOP_SQUARE ||
+                          o.op == SRHIP_UOP_CUBE || o.op == SRHIP_UOP_SIN)) {
+        mark(o.a);
+      }
+    }
+    if (fast) {
+      for (auto& o : ops) {
+        if (o.un && o.op == SRHIP_UOP_EXP) g_exp = true;
+        if (o.taint && o.zs) {
+          if (!o.un && (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB)) g_can = true;
+          if ((!o.un && (o.op == SRHIP_BOP_MUL || o.op == SRHIP_BOP_DIV)) ||
+              (o.un && (o.op == SRHIP_UOP_SQUARE || o.op == SRHIP_UOP_CUBE)))
+            g_min = true;
+        }
+      }
+    }
+    // features: first use order, last use
+    for (int f = 0; f < 256; ++f) { xblk[f] = -1; xlast[f] = -1; load_idx[f] = -1; }
+    auto usef = [&](const Opnd& q, int i) {
+      if (q.k != O_X) return true;
+      if (q.v < 0 || q.v > 255) return false;
+      if (xlast[q.v] < 0) feats.push_back(q.v);
+      xlast[q.v] = i;
+      return true;
+    };
+    for (int i = 0; i < n; ++i) {
+      if (!usef(ops[i].a, i)) return false;
+      if (!ops[i].un && !usef(ops[i].b, i)) return false;
+    }
+    if (!usef(root, n)) return false;
+    if ((int)feats.size() > NPOOL) { why = "more features than register blocks"; return false; }
+    for (int f : feats)
+      if ((1 + f) * TILE * 4 + 3 * 4 * 64 > 65535) { why = "feature offset beyond the DS immediate"; return false; }
+    next_call.assign(n + 1, n);
+    for (int i = n - 1; i >= 0; --i) next_call[i] = ops[i].rid >= 0 ? i : next_call[i + 1];
+    loc.assign(n, L_NONE);
+    return true;
+  }
+
+  // ---- emission helpers ----
+  Src opsrc(const Opnd& q, int e) const {
+    if (q.k == O_C) return K(q.c);
+    if (q.k == O_X) return V(VPOOL0 + R * xblk[q.v] + e);
+    return V(reg_of_loc(loc[q.v]) + e);
+  }
+  bool opnd_is_vgpr(const Opnd& q) const { return q.k != O_C; }
+
+  void wait_for(const Opnd& q) {
+    if (q.k != O_X) return;
+    const int li = load_idx[q.v];
+    if (li >= waited) {
+      as.waitcnt_lgkm(nloads - 1 - li);
+      waited = li + 1;
+    }
+  }
+  void wait_all() {
+    if (waited < nloads) {
+      as.waitcnt_lgkm(0);
+      waited = nloads;
+    }
+  }
+  int free_block() const {
+    for (int k = 0; k < NPOOL; ++k)
+      if (pool_owner[k] == -1) return k;
+    return -1;
+  }
+  void mov_block(int dst, const Src (&src)[R]) {
+    for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", dst + e, src[e]);
+  }
+  void mov_block_reg(int dst, int srcreg) {
+    for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", dst + e, V(srcreg + e));
+  }
+  // value v leaves its location (its last use)
+  void release_val(int v) {
+    const int l = loc[v];
+    if (l == L_A) { if (a_owner == v) a_owner = -1; }
+    else if (l == L_B) { if (b_owner == v) b_owner = -1; }
+    else if (l >= 0 && pool_owner[l] == v) pool_owner[l] = -1;
+  }
+  void release_x(int f, int i) {
+    if (xlast[f] == i && xblk[f] >= 0 && pool_owner[xblk[f]] == 1000 + f) pool_owner[xblk[f]] = -1;
+  }
+  bool evict(int owner_slot_loc, int keep_a, int keep_b) {
+    int& own = owner_slot_loc == L_A ? a_owner : b_owner;
+    if (own < 0 || own == keep_a || own == keep_b) return true;
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted (evict)"; return false; }
+    mov_block_reg(VPOOL0 + R * k, owner_slot_loc == L_A ? VA : VB);
+    pool_owner[k] = own;
+    loc[own] = k;
+    own = -1;
+    return true;
+  }
+
+  void call_routine(int rid) {
+    as.sop1(SOP1_GETPC, "s_getpc_b64", S_TGT, Src{0, false, 0, ""}, "s[" + std::to_string(S_TGT) + ":" +
+                                                                          std::to_string(S_TGT + 1) + "]");
+    if (as.want_text) as.lines.back() = "s_getpc_b64 s[" + std::to_string(S_TGT) + ":" + std::to_string(S_TGT + 1) + "]";
+    // patch: s_getpc has no source operand (encoding field 0)
+    const uint64_t pc_next = cur_va();
+    const int64_t rel = (int64_t)(T.rt_va[rid] - pc_next);
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TGT, S(S_TGT), K((uint32_t)(uint64_t)rel));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_TGT + 1, S(S_TGT + 1), K((uint32_t)((uint64_t)rel >> 32)));
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TGT, S(S_TGT), S(S_MDELTA));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_TGT + 1, S(S_TGT + 1), K(0));
+    as.sop1(SOP1_SWAPPC, "s_swappc_b64", S_RR, S(S_TGT), "s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "]");
+    if (as.want_text)
+      as.lines.back() = "s_swappc_b64 s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "], s[" +
+                        std::to_string(S_TGT) + ":" + std::to_string(S_TGT + 1) + "]";
+    if (kRoutineTrig[rid]) {
+      as.sopc(SOPC_LG_U64, "s_cmp_lg_u64", S(S_FLAG), K(0),
+              "s[" + std::to_string(S_FLAG) + ":" + std::to_string(S_FLAG + 1) + "]");
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_bail);
+    }
+  }
+
+  bool emit_call(int i) {
+    IrOp& o = ops[i];
+    const int va_ = o.a.k == O_VAL ? o.a.v : -1;
+    const int vb_ = (!o.un && o.b.k == O_VAL) ? o.b.v : -1;
+    wait_for(o.a);
+    if (!o.un) wait_for(o.b);
+    if (!evict(L_A, va_, vb_) || !evict(L_B, va_, vb_)) return false;
+    // move the operands into A (lhs) and B (rhs)
+    auto srcs = [&](const Opnd& q, Src (&s)[R]) {
+      for (int e = 0; e < R; ++e) s[e] = opsrc(q, e);
+    };
+    const int la = va_ >= 0 ? loc[va_] : L_NONE;
+    const int lb = vb_ >= 0 ? loc[vb_] : L_NONE;
+    Src sa[R], sb[R];
+    if (o.un) {
+      if (la != L_A) { srcs(o.a, sa); mov_block(VA, sa); }
+    } else if (la == L_B && lb == L_A) {
+      mov_block_reg(VGT, VA);
+      mov_block_reg(VA, VB);
+      mov_block_reg(VB, VGT);
+    } else if (la == L_B) {
+      mov_block_reg(VA, VB);
+      srcs(o.b, sb);
+      mov_block(VB, sb);
+    } else if (lb == L_A) {
+      mov_block_reg(VB, VA);
+      srcs(o.a, sa);
+      mov_block(VA, sa);
+    } else {
+      if (la != L_A) { srcs(o.a, sa); mov_block(VA, sa); }
+      if (lb != L_B) { srcs(o.b, sb); mov_block(VB, sb); }
+    }
+    // the operands are consumed
+    if (va_ >= 0) release_val(va_);
+    if (vb_ >= 0) release_val(vb_);
+    if (o.a.k == O_X) release_x(o.a.v, i);
+    if (!o.un && o.b.k == O_X) release_x(o.b.v, i);
+    a_owner = b_owner = -1;
+    if (fast && o.un && o.op == SRHIP_UOP_EXP)
+      for (int e = 0; e < R; ++e) {
+        const Src g = V(VGEXP), x = V(VA + e);
+        as.vop3(VOP3_MAX_F32, "v_max_f32_e64", VGEXP, g, x, nullptr, 2, 0);
+      }
+    call_routine(o.rid);
+    loc[i] = L_A;
+    a_owner = i;
+    if (fast && o.taint && o.zs && !o.un && o.op == SRHIP_BOP_DIV) guard_min(VA);
+    return true;
+  }
+
+  void guard_min(int reg) {
+    for (int e = 0; e < R; ++e) {
+      const Src g = V(VGMIN), x = V(reg + e);
+      as.vop3(VOP3_MIN_F32, "v_min_f32_e64", VGMIN, g, x, nullptr, 2, 0);
+    }
+  }
+
+  bool emit_inline(int i) {
+    IrOp& o = ops[i];
+    wait_for(o.a);
+    if (!o.un) wait_for(o.b);
+    const bool gcan = fast && o.taint && o.zs && !o.un && (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB);
+    const bool gmin = fast && o.taint && o.zs &&
+                      ((!o.un && o.op == SRHIP_BOP_MUL) || (o.un && (o.op == SRHIP_UOP_SQUARE || o.op == SRHIP_UOP_CUBE)));
+    if (gcan) {  // t = |a| + |b| before the operands are overwritten
+      Src ka, kb;
+      if (o.a.k == O_C) { as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(o.a.c & 0x7fffffffu), "s" + std::to_string(S_K)); }
+      if (o.b.k == O_C) { as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(o.b.c & 0x7fffffffu), "s" + std::to_string(S_K)); }
+      for (int e = 0; e < R; ++e) {
+        ka = o.a.k == O_C ? S(S_K) : opsrc(o.a, e);
+        kb = o.b.k == O_C ? S(S_K) : opsrc(o.b, e);
+        as.vop3(VOP3_ADD_F32, "v_add_f32_e64", VGT + e, ka, kb, nullptr, 3, 0);
+      }
+    }
+    // operand registers (read below), then release dying operands
+    Src a[R], b[R];
+    for (int e = 0; e < R; ++e) {
+      a[e] = opsrc(o.a, e);
+      if (!o.un) b[e] = opsrc(o.b, e);
+    }
+    const int va_ = o.a.k == O_VAL ? o.a.v : -1;
+    const int vb_ = (!o.un && o.b.k == O_VAL) ? o.b.v : -1;
+    int freed = -1;
+    auto rel = [&](int v) {
+      if (v < 0) return;
+      const int l = loc[v];
+      release_val(v);
+      if (l >= 0 && freed < 0) freed = l;
+    };
+    rel(va_);
+    rel(vb_);
+    if (o.a.k == O_X) { const int k = xblk[o.a.v]; release_x(o.a.v, i); if (pool_owner[k] == -1 && freed < 0) freed = k; }
+    if (!o.un && o.b.k == O_X) { const int k = xblk[o.b.v]; release_x(o.b.v, i); if (pool_owner[k] == -1 && freed < 0) freed = k; }
+    // destination: the operand block of the consuming routine when no call
+    // comes in between, else a freed or free pool block
+    int dst = L_NONE;
+    if (o.consumer >= 0 && ops[o.consumer].rid >= 0 && next_call[i + 1] == o.consumer) {
+      const bool lhs = o.cpos == 0;
+      if (lhs && a_owner < 0) dst = L_A;
+      if (!lhs && b_owner < 0) dst = L_B;
+    }
+    if (dst == L_NONE) dst = freed >= 0 ? freed : free_block();
+    if (dst == L_NONE) { why = "register pool exhausted"; return false; }
+    const int d = reg_of_loc(dst);
+    for (int e = 0; e < R; ++e) {
+      if (o.un) {
+        switch (o.op) {
+          case SRHIP_UOP_NEG: as.vop2(VOP2_XOR_B32, "v_xor_b32_e32", d + e, K(0x80000000u), a[e].enc - 256); break;
+          case SRHIP_UOP_ABS: as.vop2(VOP2_AND_B32, "v_and_b32_e32", d + e, K(0x7fffffffu), a[e].enc - 256); break;
+          case SRHIP_UOP_SQUARE: as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, a[e], a[e].enc - 256); break;
+          default: {  // CUBE = (x*x)*x
+            const int tt = (d + e == a[e].enc - 256) ? VGT + e : d + e;
+            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", tt, a[e], a[e].enc - 256);
+            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, V(tt), a[e].enc - 256);
+          }
+        }
+      } else {
+        const bool ca = o.a.k == O_C, cb = o.b.k == O_C;
+        switch (o.op) {
+          case SRHIP_BOP_ADD:
+          case SRHIP_BOP_MUL: {
+            const int opc = o.op == SRHIP_BOP_ADD ? VOP2_ADD_F32 : VOP2_MUL_F32;
+            const char* nm = o.op == SRHIP_BOP_ADD ? "v_add_f32_e32" : "v_mul_f32_e32";
+            if (cb) as.vop2(opc, nm, d + e, b[e], a[e].enc - 256);
+            else as.vop2(opc, nm, d + e, a[e], b[e].enc - 256);
+            break;
+          }
+          default:  // SUB
+            if (cb) as.vop2(VOP2_SUBREV_F32, "v_subrev_f32_e32", d + e, b[e], a[e].enc - 256);
+            else if (ca) as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", d + e, a[e], b[e].enc - 256);
+            else as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", d + e, a[e], b[e].enc - 256);
+        }
+      }
+    }
+    if (o.un && (o.a.k == O_C)) { why = "unary operator on a constant"; return false; }
+    loc[i] = dst;
+    if (dst == L_A) a_owner = i;
+    else if (dst == L_B) b_owner = i;
+    else pool_owner[dst] = i;
+    if (gcan)
+      for (int e = 0; e < R; ++e) {
+        const Src t_ = V(VGT + e), eps = S(S_EPS), r = V(d + e);
+        as.vop3(VOP3_FMA_F32, "v_fma_f32", VGT + e, t_, eps, &r, 4, 4);
+        as.vop2(VOP2_MAX_F32, "v_max_f32_e32", VGCAN, V(VGT + e), VGCAN);
+      }
+    if (gmin) guard_min(d);
+    return true;
+  }
+
+  bool emit_tree(const std::vector<IrOp>& ir, const Opnd& rt) {
+    ops = ir;
+    root = rt;
+    if (!analyze()) return false;
+    for (int k = 0; k < NPOOL; ++k) pool_owner[k] = -1;
+    L_tile = as.label();
+    L_done = as.label();
+    L_redo = as.label();
+    L_bail = as.label();
+    const uint32_t D = (uint32_t)T.delta;
+    // ---- prologue
+    as.sop1(SOP1_MOV, "s_mov_b32", S_STATUS, K(0), "s" + std::to_string(S_STATUS));
+    if (g_can) as.sop1(SOP1_MOV, "s_mov_b32", S_EPS, K(0x38800000u), "s" + std::to_string(S_EPS));  // 2^-14
+    if (fast) {
+      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_FASTOK), K(0));
+      as.sop2(SOP2_CSELECT, "s_cselect_b32", S_MODE, K(1), K(0));
+      as.sop2(SOP2_CSELECT, "s_cselect_b32", S_MDELTA, K(D), K(0));
+    } else {
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(1), "s" + std::to_string(S_MODE));
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MDELTA, K(D), "s" + std::to_string(S_MDELTA));
+    }
+    as.sopc(SOPC_GE_U32, "s_cmp_ge_u32", S(S_TILE), S(S_NT));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_done);
+    // ---- tile
+    as.bind(L_tile);
+    as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHKSAVE, V(VCHK));
+    if (g_can) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGCAN, K(0xbf800000u));   // -1
+    if (g_min) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGMIN, K(0x3f800000u));   // 1
+    if (g_exp) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGEXP, K(0));
+    a_owner = b_owner = -1;
+    for (int k = 0; k < NPOOL; ++k) pool_owner[k] = -1;
+    nloads = 0;
+    waited = 0;
+    as.ds_read_b128(VY, VLANE, 0);
+    ++nloads;
+    for (size_t j = 0; j < feats.size(); ++j) {
+      const int f = feats[j];
+      xblk[f] = (int)j;
+      pool_owner[j] = 1000 + f;
+      load_idx[f] = nloads++;
+      as.ds_read_b128(VPOOL0 + R * (int)j, VLANE, (1 + f) * TILE * 4);
+    }
+    std::fill(loc.begin(), loc.end(), (int)L_NONE);
+    for (int i = 0; i < (int)ops.size(); ++i) {
+      if (ops[i].rid >= 0) { if (!emit_call(i)) return false; }
+      else if (!emit_inline(i)) return false;
+    }
+    // root value
+    int rreg;
+    if (root.k == O_VAL) rreg = reg_of_loc(loc[root.v]);
+    else if (root.k == O_X) { wait_for(root); rreg = VPOOL0 + R * xblk[root.v]; }
+    else {
+      for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGT + e, K(root.c));
+      rreg = VGT;
+    }
+    for (int e = 0; e < R; ++e) {
+      const Src r = V(rreg + e), z = K(0), c = V(VCHK);
+      as.vop3(VOP3_FMA_F32, "v_fma_f32", VCHK, r, z, &c, 0, 0);
+    }
+    wait_all();
+    // ---- FAST-mode verdict: a failure or a guard redoes the tile precisely
+    if (fast) {
+      const int L_skip = as.label();
+      as.sopc(SOPC_LG_U32, "s_cmp_lg_u32", S(S_MODE), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_skip);
+      as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
+      as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      if (g_can) {
+        as.vopc(VOPC_LE_F32, "v_cmp_le_f32_e32", K(0), VGCAN);
+        as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      }
+      if (g_min) {
+        as.vopc(VOPC_GT_F32, "v_cmp_gt_f32_e32", K(0x03800000u), VGMIN);  // 2^-120 > min|v|
+        as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      }
+      if (g_exp) {
+        as.vopc(VOPC_LT_F32, "v_cmp_lt_f32_e32", K(0x42ae0000u), VGEXP);  // 87 < max|x|
+        as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      }
+      as.bind(L_skip);
+    }
+    // ---- L2 loss of the tile (eval_kernel.h tile_loss order)
+    for (int e = 0; e < R; ++e) as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", VY + e, V(rreg + e), VY + e);
+    for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VY + e), VY + e);
+    return true;
+  }
+
+  // second half of the tile: weights (s_woff != 0), mask, sums, loop
+  void emit_tail() {
+    {
+      const int L_now = as.label();
+      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_now);
+      as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VGT, S(S_WOFF), VLANE);
+      as.ds_read_b128(VGT, VGT, 0);
+      as.waitcnt_lgkm(0);
+      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VGT + e), VY + e);
+      as.bind(L_now);
+    }
+    // the last, partial tile: rows past `partial` add 0
+    const int L_nomask = as.label();
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_PE, S(S_TILE), K(1));
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_PE), S(S_NT));
+    as.branch(SOPP_SCC0, "s_cbranch_scc0", L_nomask);
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_PARTIAL), K((uint32_t)TILE));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_nomask);
+    for (int e = 0; e < R; ++e) {
+      as.sop2(SOP2_SUB_I32, "s_sub_i32", S_PE, S(S_PARTIAL), K((uint32_t)e));
+      as.vopc(VOPC_GT_I32, "v_cmp_gt_i32_e32", S(S_PE), VLANE4);
+      as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", VY + e, K(0), VY + e, ", vcc");
+    }
+    as.bind(L_nomask);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 2);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY + 1, V(VY + 1), VY + 3);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 1);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VLSUM, V(VLSUM), VY);
+    // a failed tile ends the tree
+    as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
+    as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
+    if (fast) {  // the next tile starts FAST again
+      const int L_keep = as.label();
+      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_FASTOK), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_keep);
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(0), "s" + std::to_string(S_MODE));
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MDELTA, K(0), "s" + std::to_string(S_MDELTA));
+      as.bind(L_keep);
+    }
+    as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VLANE, S(S_TILEBYTES), VLANE);
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TILE, S(S_TILE), K(1));
+    as.sopc(SOPC_LT_U32, "s_cmp_lt_u32", S(S_TILE), S(S_NT));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_tile);
+    as.bind(L_done);
+    as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(S_RT), "");
+    if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(S_RT) + ":" + std::to_string(S_RT + 1) + "]";
+    if (fast) {
+      as.bind(L_redo);
+      as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHK, V(VCHKSAVE));
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(1), "s" + std::to_string(S_MODE));
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MDELTA, K((uint32_t)T.delta), "s" + std::to_string(S_MDELTA));
+      as.branch(SOPP_BRANCH, "s_branch", L_tile);
+    }
+    if (has_trig) {
+      as.bind(L_bail);
+      as.waitcnt_lgkm(0);
+      as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHK, V(VCHKSAVE));
+      as.sop1(SOP1_MOV, "s_mov_b32", S_STATUS, K(1), "s" + std::to_string(S_STATUS));
+      as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(S_RT), "");
+      if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(S_RT) + ":" + std::to_string(S_RT + 1) + "]";
+    }
+  }
+};
+
+}  // namespace
+
+// One tree: returns false (nothing appended) when it cannot be compiled.
+static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool text, std::vector<uint32_t>& out,
+                     std::vector<std::string>* lines, uint64_t area_va, int32_t* off, bool* is_fast,
+                     std::string* why) {
+  std::vector<IrOp> ir;
+  Opnd root;
+  if (!build_ir(prog, ir, root)) { *why = "program not translatable"; return false; }
+  const size_t start = (out.size() + 15) / 16 * 16;  // 64-byte aligned entries
+  Asm as;
+  as.want_text = text;
+  Gen g(as, T, area_va + start * 4, fast_opt);
+  if (!g.emit_tree(ir, root)) { *why = g.why; return false; }
+  g.emit_tail();
+  as.finish();
+  while (out.size() < start) {  // s_nop padding
+    out.push_back(0xbf800000u);
+    if (lines) lines->push_back("s_nop 0");
+  }
+  out.insert(out.end(), as.w.begin(), as.w.end());
+  if (lines) {
+    lines->push_back("; tree code at " + std::to_string(start * 4));
+    lines->insert(lines->end(), as.lines.begin(), as.lines.end());
+  }
+  *off = (int32_t)(start * 4);
+  *is_fast = g.fast;
+  return true;
+}
+
+struct Module {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr, fn_w = nullptr;
+  int32_t* d_off = nullptr;    // [nslots] code offsets
+  uint32_t* d_bail = nullptr;  // [nslots + 1]
+  int nslots = 0;
+};
+
+bool available() { return templates().ok; }
+const char* unavailable_reason() { return templates().why.c_str(); }
+
+static bool codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt,
+                    std::vector<uint32_t>& words, std::vector<std::string>* lines, std::vector<int32_t>& offs,
+                    std::vector<int32_t>& ok_trees, std::vector<int32_t>& rest, Stats* st, const Tmpl& T) {
+  for (int32_t t : cand) {
+    int32_t off = -1;
+    bool f = false;
+    std::string why;
+    const size_t before = words.size();
+    const size_t lbefore = lines ? lines->size() : 0;
+    const bool okc = cb.tree_off[t] >= 0 &&
+                     gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, opt.text, words, lines, T.area_va, &off, &f, &why);
+    if (okc && words.size() * 4 <= T.area_bytes) {
+      ok_trees.push_back(t);
+      offs.push_back(off);
+      if (st) { st->ntrees++; st->nfast += f ? 1 : 0; }
+    } else {
+      if (okc) why = "code area full";
+      words.resize(before);
+      if (lines) lines->resize(lbefore);
+      rest.push_back(t);
+      if (st) st->nrejected++;
+      static const bool dbg = std::getenv("SRHIP_JIT_DEBUG") != nullptr;
+      if (dbg) std::fprintf(stderr, "jit: tree %d not compiled: %s\n", t, why.c_str());
+    }
+  }
+  if (st) st->code_bytes = words.size() * 4;
+  return !ok_trees.empty();
+}
+
+bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt,
+                  std::vector<uint8_t>* bytes, std::string* text, std::vector<int32_t>* offsets, Stats* st) {
+  const Templates& TT = templates();
+  if (!TT.ok) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("jit templates unavailable: ") + TT.why);
+  std::vector<uint32_t> words;
+  std::vector<std::string> lines;
+  std::vector<int32_t> offs, okt, rest;
+  codegen(cb, cand, opt, words, opt.text ? &lines : nullptr, offs, okt, rest, st, TT.large);
+  if (bytes) {
+    bytes->resize(words.size() * 4);
+    std::memcpy(bytes->data(), words.data(), bytes->size());
+  }
+  if (text) {
+    text->clear();
+    for (auto& l : lines) { *text += l; *text += '\n'; }
+  }
+  if (offsets) {
+    offsets->clear();
+    for (size_t k = 0; k < okt.size(); ++k) {
+      offsets->push_back(okt[k]);
+      offsets->push_back(offs[k]);
+    }
+  }
+  return !okt.empty();
+}
+
+Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list,
+              std::vector<int32_t>& rest, const Options& opt, Stats* st) {
+  const Templates& TT = templates();
+  if (!TT.ok) { rest = cand; return nullptr; }
+  auto t0 = std::chrono::steady_clock::now();
+  std::vector<uint32_t> words;
+  std::vector<int32_t> offs;
+  codegen(cb, cand, opt, words, nullptr, offs, jit_list, rest, st, TT.large);
+  if (jit_list.empty()) return nullptr;
+  const Tmpl& T = words.size() * 4 <= TT.small.area_bytes ? TT.small : TT.large;
+  if (&T == &TT.small) {  // the code was laid out for the large template's addresses: redo
+    words.clear();
+    offs.clear();
+    std::vector<int32_t> jl, rs;
+    codegen(cb, jit_list, opt, words, nullptr, offs, jl, rs, nullptr, T);
+    if (jl.size() != jit_list.size()) throw Error(SRHIP_ERR_INVALID, "jit: small-template relayout differs");
+  }
+  std::vector<uint8_t> img(T.img, T.img + T.size);
+  std::memcpy(img.data() + T.area_off, words.data(), words.size() * 4);
+  auto t1 = std::chrono::steady_clock::now();
+  Module* m = new Module();
+  m->nslots = (int)jit_list.size();
+  try {
+    HIP_CHECK(hipModuleLoadData(&m->mod, img.data()));
+    HIP_CHECK(hipModuleGetFunction(&m->fn, m->mod, "sr_jit_eval"));
+    HIP_CHECK(hipModuleGetFunction(&m->fn_w, m->mod, "sr_jit_eval_w"));
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(m->fn), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(m->fn_w),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+    HIP_CHECK(hipMalloc((void**)&m->d_off, offs.size() * sizeof(int32_t)));
+    HIP_CHECK(hipMemcpy(m->d_off, offs.data(), offs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    HIP_CHECK(hipMalloc((void**)&m->d_bail, (size_t)(m->nslots + 1) * sizeof(uint32_t)));
+  } catch (...) {
+    destroy(m);
+    throw;
+  }
+  auto t2 = std::chrono::steady_clock::now();
+  if (st) {
+    st->ms_codegen = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    st->ms_load = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    st->code_bytes = words.size() * 4;
+  }
+  return m;
+}
+
+void destroy(Module* m) {
+  if (!m) return;
+  if (m->d_off) (void)hipFree(m->d_off);
+  if (m->d_bail) (void)hipFree(m->d_bail);
+  if (m->mod) (void)hipModuleUnload(m->mod);
+  delete m;
+}
+
+const int32_t* code_off(const Module* m) { return m->d_off; }
+uint32_t* bail_flags(Module* m) { return m->d_bail; }
+int nslots(const Module* m) { return m->nslots; }
+
+struct JitArgs {
+  EvalArgs<float> e;
+  const int32_t* code_off;
+  uint32_t* bail;
+  int fast;
+};
+
+hipError_t launch(Module* m, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream) {
+  hipError_t err = hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 1) * sizeof(uint32_t), stream);
+  if (err != hipSuccess) return err;
+  JitArgs ja;
+  ja.e = a;
+  ja.code_off = m->d_off;
+  ja.bail = m->d_bail;
+  ja.fast = fast ? 1 : 0;
+  size_t sz = sizeof(ja);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
+  return hipModuleLaunchKernel(a.w ? m->fn_w : m->fn, grid, 1, 1, (unsigned)plan.threads, 1, 1,
+                               (unsigned)plan.lds_bytes, stream, nullptr, cfg);
+}
+
+}  // namespace jit
+}  // namespace srhip

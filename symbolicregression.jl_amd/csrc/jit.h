@@ -1,0 +1,62 @@
+// jit.h — the tree compiler: every tree of a large Float32 batch becomes
+// straight-line gfx950 machine code (jit.cpp), loaded as one code object per
+// program and run by the driver kernel of jit_template.hip.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <string>
+#include <vector>
+
+#include "compile.h"
+#include "kernels.h"
+
+namespace srhip {
+namespace jit {
+
+struct Module;
+
+// Options of one compilation (the defaults are the product path).
+struct Options {
+  bool fast = true;       // emit the FAST-routine path + guards in eligible trees
+  bool text = false;      // also produce the assembly text (tests: checked against llvm-mc)
+};
+
+// Statistics of one build.
+struct Stats {
+  int ntrees = 0;          // trees compiled to code
+  int nfast = 0;           // of which have a guarded FAST path
+  int nrejected = 0;       // trees left to the interpreter (register pool exhausted, ...)
+  size_t code_bytes = 0;
+  double ms_codegen = 0.0, ms_load = 0.0;
+};
+
+// The embedded template could be parsed (false: no tree compiler, the
+// interpreter runs everything).
+bool available();
+const char* unavailable_reason();
+
+// Compile the trees `cand` (tree ids, in list order) of `cb`. Trees that
+// compile are appended to `jit_list` (same order), the others to `rest`.
+// Returns the loaded module, or nullptr when no tree compiled. Throws
+// srhip::Error on HIP failures.
+Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list,
+              std::vector<int32_t>& rest, const Options& opt, Stats* st);
+void destroy(Module* m);
+
+// Per-slot code offsets of the module, in jit_list order (device array).
+const int32_t* code_off(const Module* m);
+// bail flags + counter: [nslots + 1] uint32 (device), cleared by launch
+uint32_t* bail_flags(Module* m);
+int nslots(const Module* m);
+
+// Launch the driver over the module's trees (EvalArgs as for eval_kernel:
+// list / list_off / fail / partial of the module's slots).
+hipError_t launch(Module* m, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream);
+
+// Test hook: compile without loading; returns bytes and (opt.text) the
+// assembly text of the whole area image.
+bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt,
+                  std::vector<uint8_t>* bytes, std::string* text, std::vector<int32_t>* offsets, Stats* st);
+
+}  // namespace jit
+}  // namespace srhip

@@ -1,0 +1,151 @@
+// jit_template.hip — the code object that carries compiled tree code (jit.cpp).
+//
+// Built once (make) into a standalone gfx950 code object, embedded in
+// libsrhip.so, copied and patched per program: jit.cpp writes the machine
+// code of every tree into the `sr_jit_code` area and loads the image with
+// hipModuleLoadData. Three kernels:
+//   sr_jit_routines  never launched: holds the operator routines of
+//                    gen_jit.py (FAST and PRECISE regions, same layout);
+//   sr_jit_area      never launched: s_endpgm, then the code area (filled
+//                    with s_endpgm, so a stray jump ends the wave);
+//   sr_jit_eval      the driver: one workgroup = (row group, tree group) as
+//                    in eval_kernel (eval_kernel.h), but the row group is
+//                    staged tile-major ([tile][y, x_0 .. x_{F-1}, w][256]) so
+//                    that tree code addresses every array of a tile with an
+//                    immediate offset, and each tree is one call of its code.
+// Trees without code run in the interpreter's launch (api.cpp); a tree whose
+// code hands a tile back (a sin/cos argument beyond the fast reduction) is
+// flagged in `bail` and re-evaluated by the interpreter after this launch.
+#include <hip/hip_runtime.h>
+
+#include "interp.h"
+#include "kernels.h"
+#include "gen/jit_layout_r4.h"
+#include "gen/jit_routines_r4.inc"
+
+#ifndef SR_JIT_AREA_WORDS
+#define SR_JIT_AREA_WORDS "65536"
+#endif
+
+using namespace srhip;
+using namespace srhip::interp;
+
+extern "C" __global__ void __launch_bounds__(64) sr_jit_routines() { asm volatile(SR_JIT_ROUTINES_TEXT); }
+
+extern "C" __global__ void __launch_bounds__(64) sr_jit_area() {
+  asm volatile("s_endpgm\n.globl sr_jit_code\n.hidden sr_jit_code\nsr_jit_code:\n.fill " SR_JIT_AREA_WORDS ", 4, 0xbf810000\n");
+}
+
+namespace {
+constexpr int R = SR_JIT_R;
+constexpr int TILE = 64 * R;
+}  // namespace
+
+struct JitArgs {
+  EvalArgs<float> e;
+  const int32_t* code_off;  // [nlist] byte offset of each slot's tree code in the area
+  uint32_t* bail;           // [nlist] set when tree code hands a tile back; bail[nlist] counts them
+  int fast;                 // 1: trees may run their FAST-routine path (guarded)
+};
+
+template <bool W>
+__device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
+  const EvalArgs<float>& a = ja.e;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* sX = reinterpret_cast<float*>(smem);
+  const int narr = 1 + a.nfeat + (W ? 1 : 0);
+  const int rows = a.ntiles * TILE;
+  Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
+  const int rg = blockIdx.x / a.ntg;
+  const int g = blockIdx.x - rg * a.ntg;
+  const int64_t row0 = (int64_t)rg * rows;
+
+  // 1. stage the row group tile-major: tile t, array k (0 = y, 1.. = x_{k-1}, last = w)
+  {
+    constexpr int V = TILE / 4;  // float4 per array per tile
+    const int total = a.ntiles * narr * V;
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int v = idx % V;
+      const int tk = idx / V;
+      const int k = tk % narr;
+      const int t = tk / narr;
+      const float* src = k == 0 ? a.y : (k <= a.nfeat ? a.X + (size_t)(k - 1) * a.n_pad : a.w);
+      reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
+          reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
+    }
+    for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) sPart[i] = Part<float>{0.0f, 0.0f};
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int64_t rem = a.n - row0;
+  const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE - 1) / TILE);
+  const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nwaves = (int)(blockDim.x >> 6);
+  auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
+  auto code_of = [&](int s) {
+    return __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(ja.code_off))[s]);
+  };
+  auto ld_flag = [&](int slot) { return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+
+  // address of the code area (PC-relative, resolved when the image is linked)
+  uint64_t area;
+  asm volatile(
+      "s_getpc_b64 s[88:89]\n"
+      "s_add_u32 s88, s88, sr_jit_code@rel32@lo+4\n"
+      "s_addc_u32 s89, s89, sr_jit_code@rel32@hi+12"
+      : "={s[88:89]}"(area));
+  const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)sX) +
+                            (uint32_t)lane * 16u;
+  const uint32_t tilebytes = (uint32_t)(narr * TILE * 4);
+  const uint32_t woff = W ? (uint32_t)((1 + a.nfeat) * TILE * 4) : 0u;  // 0: unweighted
+  const uint32_t lane4 = (uint32_t)lane * R;
+  const uint32_t partial = (uint32_t)last_valid;
+  const uint32_t nt_u = (uint32_t)nt_valid;
+  const uint32_t fastok = (uint32_t)ja.fast;
+
+  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
+  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
+  m = __builtin_amdgcn_readfirstlane(m);
+  uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
+  for (int k = 0; k < m; ++k) {
+    const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
+    const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
+    const bool more = k + 1 < m;
+    const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
+    if (more) fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
+    float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
+    if (!skip) {
+      const uint64_t target = area + (uint32_t)code_of(s);
+      uint32_t la = lds_lane;
+      uint32_t tile = 0, status;
+      asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                   : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status)
+                   : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+                     "{s68}"(woff), "{s79}"(fastok)
+                   : SR_JIT_CLOBBERS, "memory");
+      if (__builtin_amdgcn_readfirstlane((int)status) != 0) {
+        // a tile the routines cannot do (sin/cos argument beyond the fast
+        // reduction): the host re-evaluates this tree with the interpreter;
+        // the other row groups skip it
+        chk = __builtin_nanf("");
+        if (lane == 0) {
+          __hip_atomic_store(ja.bail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(ja.bail + a.nlist, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+    }
+    lsum = wave_sum(lsum);
+    chk = wave_sum(chk);
+    if (lane == 0) sPart[i] = Part<float>{lsum, chk};
+    if (!skip && chk != chk && lane == 0)
+      __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
+  for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) dst[i] = sPart[i];
+}
+
+extern "C" __global__ void __launch_bounds__(256) sr_jit_eval(JitArgs ja) { jit_eval_body<false>(ja); }
+extern "C" __global__ void __launch_bounds__(256) sr_jit_eval_w(JitArgs ja) { jit_eval_body<true>(ja); }

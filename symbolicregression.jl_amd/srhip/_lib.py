@@ -72,6 +72,11 @@ SIGNATURES = {
     "srhip_eval_grad_tree_array": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
     "srhip_last_kernel_time": [C.c_void_p, C.POINTER(C.c_double), C.POINTER(C.c_int32)],
     "srhip_sync": [C.c_void_p],
+    "srhip_program_jit_info": [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
+                               C.POINTER(C.c_double), C.POINTER(C.c_double)],
+    "srhip_last_bailed": [C.c_void_p, C.POINTER(C.c_int32)],
+    "srhip_jit_compile": [C.POINTER(Trees), C.c_int32, C.c_void_p, C.POINTER(C.c_int64), C.c_char_p,
+                          C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)],
 }
 
 

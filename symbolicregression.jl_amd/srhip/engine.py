@@ -63,6 +63,12 @@ class Context:
     def sync(self):
         check(lib().srhip_sync(self.handle))
 
+    def last_bailed(self) -> int:
+        """Trees of the last eval whose tree code handed a tile back."""
+        n = C.c_int32(0)
+        check(lib().srhip_last_bailed(self.handle, C.byref(n)))
+        return n.value
+
 
 def default_device() -> int:
     return int(os.environ.get("SRHIP_DEVICE", os.environ.get("LOCAL_RANK", "0")))
@@ -157,6 +163,15 @@ class Program:
         check(lib().srhip_program_info(self.handle, C.byref(nt), C.byref(tot), _p(nodes)))
         return nt.value, tot.value, nodes[: nt.value]
 
+    def jit_info(self):
+        """Tree code of this program (srhip_program_jit_info)."""
+        nt, nf = C.c_int32(), C.c_int32()
+        nb = C.c_int64()
+        mc, ml = C.c_double(), C.c_double()
+        check(lib().srhip_program_jit_info(self.handle, C.byref(nt), C.byref(nf), C.byref(nb), C.byref(mc),
+                                           C.byref(ml)))
+        return dict(ntrees=nt.value, nfast=nf.value, code_bytes=nb.value, ms_codegen=mc.value, ms_load=ml.value)
+
     def set_constants(self, consts: np.ndarray):
         c = np.ascontiguousarray(consts, dtype=self.dtype)
         if c.shape != (int(self.flat.const_off[-1]),):
@@ -214,4 +229,33 @@ class Program:
             pass
 
 
-__all__ = ["Context", "DeviceDataset", "Program", "get_context", "device_count", "SrhipError"]
+def _trees_struct(flat: FlatTrees, consts: np.ndarray) -> Trees:
+    return Trees(
+        flat.ntrees,
+        flat.node_off.ctypes.data_as(C.POINTER(C.c_int32)),
+        flat.kind.ctypes.data_as(C.POINTER(C.c_uint8)),
+        flat.arg.ctypes.data_as(C.POINTER(C.c_uint16)),
+        flat.const_off.ctypes.data_as(C.POINTER(C.c_int32)),
+        consts.ctypes.data_as(C.c_void_p),
+    )
+
+
+def jit_compile(flat: FlatTrees, fast: bool = True):
+    """Tree compiler without a device (srhip_jit_compile): (code bytes,
+    assembly text, {tree id: byte offset})."""
+    consts = np.ascontiguousarray(flat.consts, dtype=np.float32)
+    tr = _trees_struct(flat, consts)
+    nb, nt, no = C.c_int64(0), C.c_int64(0), C.c_int64(0)
+    rc = lib().srhip_jit_compile(C.byref(tr), int(fast), None, C.byref(nb), None, C.byref(nt), None, C.byref(no))
+    if rc != -1:
+        check(rc)
+    buf = np.zeros(max(nb.value, 1), dtype=np.uint8)
+    txt = C.create_string_buffer(max(nt.value, 1))
+    offs = np.zeros(max(no.value, 1), dtype=np.int32)
+    check(lib().srhip_jit_compile(C.byref(tr), int(fast), _p(buf), C.byref(nb), txt, C.byref(nt), _p(offs),
+                                  C.byref(no)))
+    pairs = offs[: no.value].reshape(-1, 2)
+    return bytes(buf[: nb.value]), txt.value.decode(), {int(t): int(o) for t, o in pairs}
+
+
+__all__ = ["Context", "DeviceDataset", "Program", "get_context", "device_count", "SrhipError", "jit_compile"]

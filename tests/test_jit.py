@@ -1,0 +1,65 @@
+"""Tree compiler (csrc/jit.cpp) on the CPU: its machine code is what the LLVM
+assembler makes of its own assembly text, instruction for instruction.
+
+The tree compiler writes gfx950 machine code directly (no assembler at run
+time). Every encoding it can emit appears in random programs of several
+operator sets; the test assembles the text mirror with llvm-mc
+(/opt/rocm/lib/llvm/bin) and compares the bytes. The GPU tests
+(tests/test_jit_gpu.py) check what the code computes."""
+import os
+import subprocess
+import tempfile
+from pathlib import Path
+
+import numpy as np
+import pytest
+
+import srhip
+from srhip.engine import jit_compile
+
+LLVM = Path("/opt/rocm/lib/llvm/bin")
+OPSETS = [
+    (["+", "-", "*", "/"], ["cos", "exp"]),  # config #2: FAST path with guards
+    (["+", "-", "*", "/"], ["sin", "cos", "exp", "neg", "square", "cube", "abs"]),
+    (["+", "*", "/", "-", "^", "max", "min", "mod"], ["safe_log", "safe_sqrt", "tanh", "relu", "inv", "sign"]),
+]
+
+
+def assemble(text: str) -> bytes:
+    with tempfile.TemporaryDirectory() as td:
+        s, o, b = (os.path.join(td, n) for n in ("t.s", "t.o", "t.bin"))
+        Path(s).write_text(".text\n" + text)
+        subprocess.run([str(LLVM / "llvm-mc"), "-triple", "amdgcn-amd-amdhsa", "-mcpu=gfx950", "-filetype=obj",
+                        s, "-o", o], check=True, capture_output=True)
+        subprocess.run([str(LLVM / "llvm-objcopy"), "-O", "binary", "--only-section=.text", o, b], check=True)
+        return Path(b).read_bytes()
+
+
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.parametrize("k", range(len(OPSETS)))
+def test_machine_code_equals_llvm_mc(k):
+    b_ops, u_ops = OPSETS[k]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    trees = srhip.random_population(300, o, 7, np.float32, seed=11 + k)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    for fast in (True, False):
+        code, text, offs = jit_compile(flat, fast=fast)
+        assert len(offs) >= 0.7 * len(trees), f"only {len(offs)} of {len(trees)} trees compiled"
+        ref = assemble(text)
+        assert len(ref) == len(code)
+        if ref != code:
+            a = np.frombuffer(code, dtype=np.uint32)
+            r = np.frombuffer(ref, dtype=np.uint32)
+            i = int(np.flatnonzero(a != r)[0])
+            lines = [ln for ln in text.splitlines() if not ln.startswith(";")]
+            raise AssertionError(f"word {i}: jit {a[i]:#010x} vs llvm-mc {r[i]:#010x} near '{lines[:]}'"[:400])
+
+
+def test_every_tree_of_config2_compiles():
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(1000, o, 5, np.float32, seed=0)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    code, _, offs = jit_compile(flat)
+    assert len(offs) >= 990
+    assert all(v % 64 == 0 for v in offs.values())
+    print(f"{len(offs)} trees, {len(code) / len(offs):.0f} bytes per tree")

@@ -1,0 +1,142 @@
+"""Tree code (csrc/jit.cpp) on the MI355X against the interpreter and the oracle.
+
+Programs are compiled to machine code when SRHIP_JIT=1 at program creation
+(the default only for >= 512 shallow trees). Checks:
+  * PRECISE routines only (SRHIP_JIT_FAST=0): did_succeed identical to the
+    interpreter, losses equal up to the summation grouping (4 vs 8 rows per
+    lane: a few ulp of the tree's fp32 partial sums);
+  * with the guarded FAST path (default): did_succeed identical, losses
+    within the oracle's conditioning (tests/numerics.py), on config #2's
+    operator set at full parity with the oracle;
+  * weights, a partial last tile, the full operator table through routines;
+  * sin/cos arguments beyond the fast reduction: the tree is handed back and
+    re-evaluated by the interpreter (srhip_last_bailed > 0), same results.
+"""
+import os
+
+import numpy as np
+import pytest
+
+import oracle
+import srhip
+from srhip import constants as K
+
+pytestmark = pytest.mark.gpu
+
+
+class env:
+    def __init__(self, **kv):
+        self.kv = kv
+
+    def __enter__(self):
+        self.old = {k: os.environ.get(k) for k in self.kv}
+        os.environ.update({k: str(v) for k, v in self.kv.items()})
+
+    def __exit__(self, *a):
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+def run(trees, o, X, y, w=None, jit="1", fast="1"):
+    ctx = srhip.get_context(0)
+    ds = srhip.DeviceDataset(ctx, X, y, w)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    with env(SRHIP_JIT=jit, SRHIP_JIT_FAST=fast):
+        prog = srhip.Program(ctx, flat, np.float32)
+        sums, wsum, ok = prog.eval_loss(ds, K.LOSS["L2"])
+        info = prog.jit_info()
+        bailed = ctx.last_bailed()
+    return sums, wsum, ok, info, bailed
+
+
+def data(nfeat, n, seed, weighted=False):
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((nfeat, n)).astype(np.float32)
+    y = (np.float32(2) * np.cos(X[min(3, nfeat - 1)]) + X[0] * X[0] - np.float32(2)).astype(np.float32)
+    w = rng.uniform(0.5, 2.0, n).astype(np.float32) if weighted else None
+    return X, y, w
+
+
+def check_vs_interp(trees, o, X, y, w=None, fast="0", rtol=2e-6):
+    s_i, w_i, ok_i, info_i, _ = run(trees, o, X, y, w, jit="0")
+    s_j, w_j, ok_j, info_j, bailed = run(trees, o, X, y, w, jit="1", fast=fast)
+    assert info_i["ntrees"] == 0
+    assert info_j["ntrees"] >= 0.7 * len(trees), info_j  # deep and statically failing trees stay interpreted
+    assert w_i == w_j
+    bad = np.flatnonzero(ok_i != ok_j)
+    assert bad.size == 0, f"did_succeed differs on trees {bad[:10]}"
+    m = ok_i
+    np.testing.assert_allclose(s_j[m], s_i[m], rtol=rtol, atol=0)
+    return info_j, bailed
+
+
+CFG2 = dict(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+
+
+def test_precise_tree_code_equals_interpreter(gpu_ctx):
+    o = srhip.Options(**CFG2)
+    trees = srhip.random_population(1024, o, 5, np.float32, seed=0)
+    X, y, _ = data(5, 50_000, 1)
+    info, _ = check_vs_interp(trees, o, X, y, fast="0")
+    assert info["nfast"] == 0 and info["code_bytes"] > 0  # FAST path off
+
+
+def test_weighted_and_partial_tile(gpu_ctx):
+    o = srhip.Options(**CFG2)
+    trees = srhip.random_population(600, o, 5, np.float32, seed=4)
+    X, y, w = data(5, 30_001, 5, weighted=True)  # 30001 = 117 tiles of 256 + 49 rows
+    check_vs_interp(trees, o, X, y, w, fast="0")
+    X, y, _ = data(5, 777, 6)  # one row group, partial tile
+    check_vs_interp(trees, o, X, y, None, fast="0")
+
+
+def test_all_operators_through_routines(gpu_ctx):
+    o = srhip.Options(binary_operators=["+", "-", "*", "/", "^", "max", "min", "mod", "greater", "logical_or",
+                                        "logical_and"],
+                      unary_operators=["neg", "square", "cube", "exp", "abs", "safe_log", "safe_log2",
+                                       "safe_log10", "safe_log1p", "safe_sqrt", "sin", "cos", "tan", "sinh",
+                                       "cosh", "tanh", "atan", "asinh", "safe_acosh", "atanh_clip", "erf",
+                                       "erfc", "gamma", "relu", "round", "floor", "ceil", "sign", "inv"])
+    trees = srhip.random_population(1500, o, 6, np.float32, seed=7)
+    X, y, _ = data(6, 20_000, 8)
+    check_vs_interp(trees, o, X, y, fast="0", rtol=2e-6)
+    check_vs_interp(trees, o, X, y, fast="1", rtol=1e-3)
+
+
+def test_fast_path_did_succeed_matches_oracle(gpu_ctx):
+    o = srhip.Options(**CFG2)
+    trees = srhip.random_population(2048, o, 5, np.float32, seed=0)
+    X, y, _ = data(5, 100_000, 1)
+    s_j, w_j, ok_j, info, _ = run(trees, o, X, y, jit="1", fast="1")
+    assert info["nfast"] > 500
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, dtype=np.float32, nthreads=16)
+    bad = np.flatnonzero(ok_j != ref_ok)
+    assert bad.size == 0, f"did_succeed differs from the oracle on {bad[:10]}"
+    m = ok_j & np.isfinite(ref_l)
+    rel = np.abs(s_j[m] / w_j - ref_l[m]) / np.abs(ref_l[m])
+    assert np.median(rel) < 1e-6
+
+
+def test_big_trig_arguments_bail_to_interpreter(gpu_ctx):
+    o = srhip.Options(**CFG2)
+    c, e = o.make_unary, srhip.Node
+    # cos(exp(30 x1)) reaches arguments far beyond the fast reduction
+    trees = [c("cos", c("exp", o.make_binary("*", e(val=np.float32(30.0)), e(feature=1))))] * 3
+    trees += srhip.random_population(600, o, 5, np.float32, seed=9)
+    X, y, _ = data(5, 20_000, 10)
+    for fast in ("0", "1"):
+        s_i, w_i, ok_i, _, _ = run(trees, o, X, y, jit="0")
+        s_j, w_j, ok_j, info, bailed = run(trees, o, X, y, jit="1", fast=fast)
+        assert bailed >= 1
+        assert np.array_equal(ok_i, ok_j)
+        if fast == "0":
+            np.testing.assert_allclose(s_j[ok_i], s_i[ok_i], rtol=2e-6)
+        else:  # Float32 transcendentals: ill-conditioned trees move more (tests/numerics.py)
+            m = ok_i & np.isfinite(s_i)
+            assert np.array_equal(np.isfinite(s_j[ok_i]), np.isfinite(s_i[ok_i]))
+            rel = np.abs(s_j[m] - s_i[m]) / np.abs(s_i[m])
+            assert np.median(rel) < 1e-6 and np.mean(rel < 1e-4) > 0.98
