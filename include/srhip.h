@@ -233,8 +233,10 @@ int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog,
 int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nfast,
                                int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load);
 /* Trees of the last eval on this context whose tree code handed a tile back
- * (a sin/cos argument beyond the fast reduction) and were re-evaluated. */
-int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees);
+ * (a sin/cos argument beyond the fast reduction) and were re-evaluated, and
+ * tiles that tree code redid with the Float64-evaluated routines (a FAST-path
+ * guard fired or the tile failed; out_redone may be NULL). */
+int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* out_redone);
 /* Testing hook (no device needed): compile Float32 trees with the tree
  * compiler. Returns the code bytes, their assembly text ('\n'-separated lines)
  * and, per compiled tree, (tree id, byte offset). Each inout_n* holds the

@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cstdio>
 #include <cmath>
 #include <cstring>
 #include <cstdlib>
@@ -99,6 +100,7 @@ struct srhip_ctx {
   double last_ms = 0.0;
   int last_launches = 0;
   int last_bailed = 0;  // trees re-evaluated after their tree code handed a tile back
+  int64_t last_redone = 0;  // tiles tree code redid with the PRECISE routines
   DevBuf partial, sums, oks, dloss, scratch_idx, gather;
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
   DevBuf ti_rec;  // threaded-interpreter records of the shallow f32 list
@@ -380,10 +382,11 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
   if constexpr (std::is_same<T, float>::value) {
     hipStream_t s = c->stream;
     const int nj = p->nlist_j;
-    std::vector<uint32_t> flags((size_t)nj + 1);
+    std::vector<uint32_t> flags((size_t)nj + 2);
     HIP_CHECK(hipMemcpyAsync(flags.data(), jit::bail_flags(p->jit), flags.size() * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
+    c->last_redone = flags[nj + 1];
     if (flags[nj] == 0) return;
     std::vector<int32_t> slots;
     for (int k = 0; k < nj; ++k)
@@ -437,6 +440,8 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
     c->last_ms += ms;
     c->last_launches += 1;
     c->last_bailed = nb;
+    if (std::getenv("SRHIP_DEBUG_PASSES"))
+      std::fprintf(stderr, "srhip pass bail-rerun: %d trees, %.3f ms\n", nb, ms);
   }
 }
 
@@ -450,6 +455,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   c->last_ms = 0.0;
   c->last_launches = 0;
   c->last_bailed = 0;
+  c->last_redone = 0;
   c->sums.ensure(std::max<size_t>(p->ntrees, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(p->ntrees, 1));
   const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
@@ -519,6 +525,11 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     c->last_ms += ms;
     c->last_launches += 1;
+    static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
+    if (dbg)
+      std::fprintf(stderr, "srhip pass %s: %d trees, %.3f ms (grid %d x %d, %d tiles/wg)\n",
+                   pass == -1 ? "tree-code" : pass == 0 ? "shallow" : "deep", nlist, ms, plan.nrg, plan.ntg,
+                   plan.ntiles);
     if (pass == -1) rerun_bailed<T>(c, p, a, plan, nfeat, rows, loss, lparam);
   }
 }
@@ -622,6 +633,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
   c->last_ms = 0.0;
   c->last_launches = 0;
   c->last_bailed = 0;
+  c->last_redone = 0;
   const int nt = p->ntrees;
   const int nconst = p->const_off.back();
   c->sums.ensure(std::max<size_t>(nt, 1) * sizeof(double));
@@ -1164,10 +1176,11 @@ int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, i
   });
 }
 
-int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees) {
+int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* out_redone) {
   return guarded([&] {
     if (!ctx || !out_ntrees) throw Error(SRHIP_ERR_INVALID, "null argument");
     *out_ntrees = ctx->last_bailed;
+    if (out_redone) *out_redone = ctx->last_redone;
     return SRHIP_OK;
   });
 }

@@ -187,8 +187,75 @@ __device__ __forceinline__ float fast_sincos_f32(float x, int want_cos) {
 // way); an Inf argument gives n = Inf and takes OCML.
 constexpr float kTrigQMax = 33500.0f;
 
-// The fallback is taken with a wave-uniform branch (ballot) and a select, so
-// no divergent region enters the interpreter's dispatch switch.
+// ---- sin / cos beyond the fast reduction (|x| > 105615) ------------------------
+// Payne–Hanek reduction with the bits of 2/pi as instruction literals (no
+// table in memory, so the tree compiler's routines can hold it, gen_jit.py):
+// |x| = M 2^(e-23) with a 24-bit M; the 96 bits of 2/pi from bit e-24 on
+// (one leading zero word covers small e) times M give |x| 2/pi mod 4 with 64
+// fraction bits (truncation < 2^-70, far below the closest approach of a
+// float to a multiple of pi/2); rounding to the nearest quadrant leaves
+// r = f pi/2, |r| <= pi/4, in Float64; the Float64 Taylor polynomials of sin
+// and cos (to r^17 / r^16) and one rounding to Float32 give the value the
+// oracle's Float64 sin/cos rounds to (except within ~2^-45 of a rounding
+// boundary).
+__device__ __forceinline__ float big_sincos_f32(float x, int want_cos) {
+  const uint32_t ax = __float_as_uint(x) & 0x7fffffffu;
+  const int e = (int)(ax >> 23) - 127;  // >= 16 on this path
+  const uint64_t M = (ax & 0x7fffffu) | 0x800000u;
+  const int p0 = e + 7;                  // first window bit in the table below
+  const int k = p0 >> 5, sh = p0 & 31;
+  // scalars made opaque: a select chain, never an array in memory or LDS
+  uint32_t t1 = 0xA2F9836Eu, t2 = 0x4E441529u, t3 = 0xFC2757D1u, t4 = 0xF534DDC0u, t5 = 0xDB629599u,
+           t6 = 0x3C439041u, t7 = 0xFE5163ABu;
+  asm volatile("" : "+s"(t1), "+s"(t2), "+s"(t3), "+s"(t4), "+s"(t5), "+s"(t6), "+s"(t7));
+  auto word = [&](int j) {
+    uint32_t r = j == 1 ? t1 : 0u;
+    r = j == 2 ? t2 : r;
+    r = j == 3 ? t3 : r;
+    r = j == 4 ? t4 : r;
+    r = j == 5 ? t5 : r;
+    r = j == 6 ? t6 : r;
+    return j == 7 ? t7 : r;
+  };
+  const uint32_t a0 = word(k), a1 = word(k + 1), a2 = word(k + 2), a3 = word(k + 3);
+  auto funnel = [&](uint32_t hi, uint32_t lo) { return sh ? (hi << sh) | (lo >> (32 - sh)) : hi; };
+  const uint64_t q2 = M * funnel(a2, a3), q1 = M * funnel(a1, a2), q0 = M * funnel(a0, a1);
+  // P = q0 2^64 + q1 2^32 + q2 has 94 fraction bits: quadrant = P[95:94], fraction = P[93:30]
+  const uint64_t t = q1 + (q2 >> 32);
+  const uint64_t u = q0 + (t >> 32);
+  uint32_t q = (uint32_t)(u >> 30) & 3u;
+  const uint64_t frac = ((u & 0x3fffffffull) << 34) | ((t & 0xffffffffull) << 2) | ((q2 & 0xffffffffull) >> 30);
+  const int64_t f = (int64_t)frac;  // >= 1/2 reads negative: the next quadrant, r < 0
+  if (f < 0) q = (q + 1u) & 3u;
+  const double r = (double)f * (1.5707963267948966 * 0x1p-64);  // f * pi/2 * 2^-64
+  const double s2 = r * r;
+  double ps = -2.81145725434552076320e-15;
+  ps = __builtin_fma(ps, s2, 7.64716373181981647590e-13);
+  ps = __builtin_fma(ps, s2, -1.60590438368216145994e-10);
+  ps = __builtin_fma(ps, s2, 2.50521083854417187751e-08);
+  ps = __builtin_fma(ps, s2, -2.75573192239858906526e-06);
+  ps = __builtin_fma(ps, s2, 1.98412698412698412698e-04);
+  ps = __builtin_fma(ps, s2, -8.33333333333333333333e-03);
+  ps = __builtin_fma(ps, s2, 1.66666666666666666667e-01);
+  const double sn = __builtin_fma(-ps * s2, r, r);
+  double pc = 4.77947733238738529744e-14;           // 1/16!
+  pc = __builtin_fma(pc, s2, -1.14707455977297247139e-11);  // -1/14!
+  pc = __builtin_fma(pc, s2, 2.08767569878680989792e-09);   // 1/12!
+  pc = __builtin_fma(pc, s2, -2.75573192239858906526e-07);  // -1/10!
+  pc = __builtin_fma(pc, s2, 2.48015873015873015873e-05);   // 1/8!
+  pc = __builtin_fma(pc, s2, -1.38888888888888888889e-03);  // -1/6!
+  pc = __builtin_fma(pc, s2, 4.16666666666666666667e-02);   // 1/4!
+  pc = __builtin_fma(pc, s2, -0.5);
+  const double cs = __builtin_fma(pc, s2, 1.0);
+  const uint32_t idx = (q + (want_cos ? 1u : 0u)) & 3u;  // sin(x + pi/2) = cos(x)
+  double v = (idx & 1u) ? cs : sn;
+  if (idx & 2u) v = -v;
+  if (!want_cos && (__float_as_uint(x) >> 31)) v = -v;  // sin is odd, cos even
+  return (float)v;
+}
+
+// The large-argument path is taken with a wave-uniform branch (ballot) and a
+// select, so no divergent region enters the interpreter's dispatch switch.
 __device__ __forceinline__ bool trig_big(float x) {
   return !(__builtin_fabsf(x) <= 105615.0f) && __builtin_isfinite(x);
 }
@@ -196,7 +263,7 @@ __device__ __forceinline__ float m_sin(float x) {
   float v = fast_sincos_f32(x, 0);
   const bool big = trig_big(x);
   if (__builtin_amdgcn_ballot_w64(big) != 0) {
-    const float o = m_sin_ocml(x);
+    const float o = big_sincos_f32(x, 0);
     v = big ? o : v;
   }
   return v;
@@ -205,7 +272,7 @@ __device__ __forceinline__ float m_cos(float x) {
   float v = fast_sincos_f32(x, 1);
   const bool big = trig_big(x);
   if (__builtin_amdgcn_ballot_w64(big) != 0) {
-    const float o = m_cos_ocml(x);
+    const float o = big_sincos_f32(x, 1);
     v = big ? o : v;
   }
   return v;

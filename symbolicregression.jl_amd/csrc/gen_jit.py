@@ -117,6 +117,11 @@ def rows(expr):
     return f"_Pragma(\"unroll\") for (int r = 0; r < R; ++r) {{ {expr} }}"
 
 
+# sin / cos routines that hand arguments beyond the fast reduction back to the
+# caller (the tree is then re-evaluated by the interpreter) instead of doing
+# the large-argument reduction themselves.
+TRIG_BAIL = False
+
 # Operators emitted inline by jit.cpp (no routine).
 INLINE_BOPS = {"ADD", "SUB", "MUL"}
 INLINE_UOPS = {"NEG", "ABS", "SQUARE", "CUBE"}
@@ -128,14 +133,14 @@ def routine_list():
     for u in sorted(UOPS, key=lambda k: UOPS[k]):
         if u in INLINE_UOPS:
             continue
-        if u in ("SIN", "COS"):
+        if u in ("SIN", "COS") and TRIG_BAIL:
             body = ("float qm = 0.0f; " +
                     rows(f"float qa; s.a[r] = dev::fast_sincos_f32(s.a[r], {1 if u == 'COS' else 0}, qa); "
                          "qm = __builtin_fmaxf(qm, qa);") +
                     " const unsigned long long fl = __builtin_amdgcn_ballot_w64(!(qm <= dev::kTrigQMax));"
                     " s.s_flag = (unsigned)fl; s.s_flag_hi = (unsigned)(fl >> 32);")
             rs.append((f"u_{u.lower()}", body, True))
-        else:
+        else:  # sin / cos: the whole range, large arguments by device_ops.h big_sincos_f32
             mk = "chk = mark(s.a[r], chk); " if u in LOSSY_UOPS else ""
             rs.append((f"u_{u.lower()}", rows(f"{mk}s.a[r] = dev::uop<SRHIP_UOP_{u}>(s.a[r]);"), False))
     for b in sorted(BOPS, key=lambda k: BOPS[k]):
@@ -242,7 +247,7 @@ def build(hipcc, outdir, R):
     hp = os.path.join(outdir, f"jit_layout_r{R}.h")
     clob_v = sorted(vtemp | (vstate - {rg.CHK, rg.LANE, rg.LSUM, rg.LANE4}))
     clob_s = sorted(stemp | (sstate - {rg.S[k] for k in ("tile", "nt", "partial", "tilebytes", "woff", "fastok",
-                                                          "status")}))
+                                                          "status", "x0")}))
     with open(hp, "w") as f:
         f.write(f"// Generated by gen_jit.py (R={R}); do not edit.\n#pragma once\n")
         f.write(f"#define SR_JIT_R {R}\n")

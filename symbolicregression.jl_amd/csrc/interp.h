@@ -164,7 +164,8 @@ template <int U, typename T, int R>
 __device__ __forceinline__ void un_apply(T (&acc)[R], T& chk) {
   if constexpr ((U == SRHIP_UOP_COS || U == SRHIP_UOP_SIN) && sizeof(T) == 4) {
     // fast f32 sin/cos for all R values, one wave-uniform check for the
-    // rare |x| > 105615 that needs OCML's full reduction
+    // rare |x| > 105615 that needs the full reduction (device_ops.h
+    // big_sincos_f32)
     T v[R];
     float qmax = 0.0f;
 #pragma unroll
@@ -176,7 +177,7 @@ __device__ __forceinline__ void un_apply(T (&acc)[R], T& chk) {
     if (__builtin_amdgcn_ballot_w64(!(qmax <= dev::kTrigQMax)) != 0) {
 #pragma unroll
       for (int r = 0; r < R; ++r) {
-        const T o = U == SRHIP_UOP_COS ? dev::m_cos_ocml(acc[r]) : dev::m_sin_ocml(acc[r]);
+        const T o = dev::big_sincos_f32(acc[r], U == SRHIP_UOP_COS ? 1 : 0);
         v[r] = dev::trig_big(acc[r]) ? o : v[r];
       }
     }

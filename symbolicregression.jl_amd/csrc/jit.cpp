@@ -66,7 +66,7 @@ constexpr int S_TILE = SR_JIT_S_TILE, S_NT = SR_JIT_S_NT, S_PARTIAL = SR_JIT_S_P
 constexpr int S_TILEBYTES = SR_JIT_S_TILEBYTES, S_WOFF = SR_JIT_S_WOFF, S_STATUS = SR_JIT_S_STATUS;
 constexpr int S_FLAG = SR_JIT_S_FLAG, S_RR = SR_JIT_S_RR, S_TGT = SR_JIT_S_TGT, S_RT = SR_JIT_S_RT;
 constexpr int S_MDELTA = SR_JIT_S_MDELTA, S_FASTOK = SR_JIT_S_FASTOK, S_EPS = SR_JIT_S_EPS;
-constexpr int S_K = SR_JIT_S_K, S_PE = SR_JIT_S_PE, S_MODE = SR_JIT_S_MODE;
+constexpr int S_K = SR_JIT_S_K, S_PE = SR_JIT_S_PE, S_MODE = SR_JIT_S_MODE, S_X0 = SR_JIT_S_X0;
 constexpr int TILE = 64 * R;
 constexpr int kNumRoutines = SR_JIT_NUM_ROUTINES;
 const int kUopRoutine[SRHIP_NUM_UOPS] = SR_JIT_UOP_ROUTINE;
@@ -167,11 +167,18 @@ const Templates& templates() {
 }
 
 // ---- instruction encoder (gfx950 formats), with an assembly-text mirror ---------
+std::string hex32(uint32_t v);
+
 struct Src {
   int enc = 0;        // 9-bit operand field
   bool lit = false;   // a 32-bit literal follows
-  uint32_t val = 0;
-  std::string name;
+  uint32_t val = 0;   // constant bits (literal or inline constant)
+  // assembly text of the operand (only built when text is wanted)
+  std::string name() const {
+    if (enc >= 256) return "v" + std::to_string(enc - 256);
+    if (enc < 102) return "s" + std::to_string(enc);
+    return hex32(val);
+  }
 };
 
 bool inline_const(uint32_t b, int* enc) {
@@ -198,19 +205,18 @@ std::string hex32(uint32_t v) {
   return b;
 }
 
-Src V(int r) { return Src{256 + r, false, 0, "v" + std::to_string(r)}; }
-Src S(int r) { return Src{r, false, 0, "s" + std::to_string(r)}; }
+Src V(int r) { return Src{256 + r, false, 0}; }
+Src S(int r) { return Src{r, false, 0}; }
 Src K(uint32_t bits) {
   Src s;
   int e;
+  s.val = bits;
   if (inline_const(bits, &e)) {
     s.enc = e;
   } else {
     s.enc = 255;
     s.lit = true;
-    s.val = bits;
   }
-  s.name = hex32(bits);
   return s;
 }
 
@@ -237,41 +243,41 @@ struct Asm {
   void sop1(int op, const char* nm, int sdst, const Src& s0, const std::string& dname) {
     put(0xbe800000u | ((uint32_t)sdst << 16) | ((uint32_t)op << 8) | (uint32_t)s0.enc);
     lit(s0);
-    t(std::string(nm) + " " + dname + ", " + s0.name);
+    if (want_text) t(std::string(nm) + " " + dname + ", " + s0.name());
   }
   void sop2(int op, const char* nm, int sdst, const Src& s0, const Src& s1) {
     put(0x80000000u | ((uint32_t)op << 23) | ((uint32_t)sdst << 16) | ((uint32_t)s1.enc << 8) | (uint32_t)s0.enc);
     lit(s0.lit ? s0 : s1);
-    t(std::string(nm) + " s" + std::to_string(sdst) + ", " + s0.name + ", " + s1.name);
+    if (want_text) t(std::string(nm) + " s" + std::to_string(sdst) + ", " + s0.name() + ", " + s1.name());
   }
   void sopc(int op, const char* nm, const Src& s0, const Src& s1, const std::string& n0 = "") {
     put(0xbf000000u | ((uint32_t)op << 16) | ((uint32_t)s1.enc << 8) | (uint32_t)s0.enc);
     lit(s0.lit ? s0 : s1);
-    t(std::string(nm) + " " + (n0.empty() ? s0.name : n0) + ", " + s1.name);
+    if (want_text) t(std::string(nm) + " " + (n0.empty() ? s0.name() : n0) + ", " + s1.name());
   }
   void sopp(int op, const char* nm, int imm, bool show = true) {
     put(0xbf800000u | ((uint32_t)op << 16) | ((uint32_t)imm & 0xffffu));
-    t(show ? std::string(nm) + " " + std::to_string(imm) : std::string(nm));
+    if (want_text) t(show ? std::string(nm) + " " + std::to_string(imm) : std::string(nm));
   }
   void branch(int op, const char* nm, int l) {
     fix.push_back({w.size(), l, want_text ? lines.size() : 0});
     put(0xbf800000u | ((uint32_t)op << 16));
-    t(std::string(nm) + " @");
+    if (want_text) t(std::string(nm) + " @");
   }
   void vop1(int op, const char* nm, int vdst, const Src& s0) {
     put(0x7e000000u | ((uint32_t)vdst << 17) | ((uint32_t)op << 9) | (uint32_t)s0.enc);
     lit(s0);
-    t(std::string(nm) + " v" + std::to_string(vdst) + ", " + s0.name);
+    if (want_text) t(std::string(nm) + " v" + std::to_string(vdst) + ", " + s0.name());
   }
   void vop2(int op, const char* nm, int vdst, const Src& s0, int vsrc1, const char* tail = "") {
     put(((uint32_t)op << 25) | ((uint32_t)vdst << 17) | ((uint32_t)vsrc1 << 9) | (uint32_t)s0.enc);
     lit(s0);
-    t(std::string(nm) + " v" + std::to_string(vdst) + ", " + s0.name + ", v" + std::to_string(vsrc1) + tail);
+    if (want_text) t(std::string(nm) + " v" + std::to_string(vdst) + ", " + s0.name() + ", v" + std::to_string(vsrc1) + tail);
   }
   void vopc(int op, const char* nm, const Src& s0, int vsrc1) {
     put(0x7c000000u | ((uint32_t)op << 17) | ((uint32_t)vsrc1 << 9) | (uint32_t)s0.enc);
     lit(s0);
-    t(std::string(nm) + " vcc, " + s0.name + ", v" + std::to_string(vsrc1));
+    if (want_text) t(std::string(nm) + " vcc, " + s0.name() + ", v" + std::to_string(vsrc1));
   }
   // VOP3 (no literals on gfx9): abs / neg bit i applies to source i
   void vop3(int op, const char* nm, int vdst, const Src& s0, const Src& s1, const Src* s2, int abs, int neg) {
@@ -279,8 +285,9 @@ struct Asm {
     put(0xd0000000u | ((uint32_t)op << 16) | ((uint32_t)(abs & 7) << 8) | (uint32_t)vdst);
     put(((uint32_t)(neg & 7) << 29) | ((uint32_t)(s2 ? s2->enc : 0) << 18) | ((uint32_t)s1.enc << 9) |
         (uint32_t)s0.enc);
+    if (!want_text) return;
     auto f = [&](const Src& s, int i) {
-      std::string n = s.name;
+      std::string n = s.name();
       if (abs & (1 << i)) n = "|" + n + "|";
       if (neg & (1 << i)) n = "-" + n;
       return n;
@@ -290,7 +297,7 @@ struct Asm {
   void ds_read_b128(int vdst, int vaddr, int offset) {
     put(0xd8000000u | (0xffu << 17) | (uint32_t)(offset & 0xffff));
     put(((uint32_t)vdst << 24) | (uint32_t)vaddr);
-    t("ds_read_b128 v[" + std::to_string(vdst) + ":" + std::to_string(vdst + 3) + "], v" + std::to_string(vaddr) +
+    if (want_text) t("ds_read_b128 v[" + std::to_string(vdst) + ":" + std::to_string(vdst + 3) + "], v" + std::to_string(vaddr) +
       (offset ? " offset:" + std::to_string(offset) : ""));
   }
   void waitcnt_lgkm(int n) { sopp(0x0c, "s_waitcnt", 0xc07f | (n << 8), false); if (want_text) lines.back() = "s_waitcnt lgkmcnt(" + std::to_string(n) + ")"; }
@@ -575,7 +582,7 @@ struct Gen {
   }
 
   void call_routine(int rid) {
-    as.sop1(SOP1_GETPC, "s_getpc_b64", S_TGT, Src{0, false, 0, ""}, "s[" + std::to_string(S_TGT) + ":" +
+    as.sop1(SOP1_GETPC, "s_getpc_b64", S_TGT, Src{0, false, 0}, "s[" + std::to_string(S_TGT) + ":" +
                                                                           std::to_string(S_TGT + 1) + "]");
     if (as.want_text) as.lines.back() = "s_getpc_b64 s[" + std::to_string(S_TGT) + ":" + std::to_string(S_TGT + 1) + "]";
     // patch: s_getpc has no source operand (encoding field 0)
@@ -881,6 +888,7 @@ struct Gen {
     if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(S_RT) + ":" + std::to_string(S_RT + 1) + "]";
     if (fast) {
       as.bind(L_redo);
+      as.sop2(SOP2_ADD_U32, "s_add_u32", S_X0, S(S_X0), K(1));  // redo counter (driver output)
       as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHK, V(VCHKSAVE));
       as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(1), "s" + std::to_string(S_MODE));
       as.sop1(SOP1_MOV, "s_mov_b32", S_MDELTA, K((uint32_t)T.delta), "s" + std::to_string(S_MDELTA));
@@ -931,7 +939,7 @@ struct Module {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr;
   int32_t* d_off = nullptr;    // [nslots] code offsets
-  uint32_t* d_bail = nullptr;  // [nslots + 1]
+  uint32_t* d_bail = nullptr;  // [nslots + 2]: bail flags, bail count, PRECISE redo count
   int nslots = 0;
 };
 
@@ -1025,7 +1033,7 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
                                   hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     HIP_CHECK(hipMalloc((void**)&m->d_off, offs.size() * sizeof(int32_t)));
     HIP_CHECK(hipMemcpy(m->d_off, offs.data(), offs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    HIP_CHECK(hipMalloc((void**)&m->d_bail, (size_t)(m->nslots + 1) * sizeof(uint32_t)));
+    HIP_CHECK(hipMalloc((void**)&m->d_bail, (size_t)(m->nslots + 2) * sizeof(uint32_t)));
   } catch (...) {
     destroy(m);
     throw;
@@ -1059,7 +1067,7 @@ struct JitArgs {
 };
 
 hipError_t launch(Module* m, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream) {
-  hipError_t err = hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 1) * sizeof(uint32_t), stream);
+  hipError_t err = hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t), stream);
   if (err != hipSuccess) return err;
   JitArgs ja;
   ja.e = a;

@@ -44,7 +44,8 @@ constexpr int TILE = 64 * R;
 struct JitArgs {
   EvalArgs<float> e;
   const int32_t* code_off;  // [nlist] byte offset of each slot's tree code in the area
-  uint32_t* bail;           // [nlist] set when tree code hands a tile back; bail[nlist] counts them
+  uint32_t* bail;           // [nlist] set when tree code hands a tile back; [nlist] counts them,
+                            // [nlist + 1] counts tiles redone with the PRECISE routines
   int fast;                 // 1: trees may run their FAST-routine path (guarded)
 };
 
@@ -109,6 +110,7 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
   m = __builtin_amdgcn_readfirstlane(m);
   uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
+  uint32_t redos = 0;  // tiles redone with the PRECISE routines (counted by tree code)
   for (int k = 0; k < m; ++k) {
     const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
@@ -121,7 +123,8 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
       uint32_t la = lds_lane;
       uint32_t tile = 0, status;
       asm volatile("s_swappc_b64 s[76:77], %[tgt]"
-                   : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status)
+                   : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
+                     "+{s84}"(redos)
                    : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
                      "{s68}"(woff), "{s79}"(fastok)
                    : SR_JIT_CLOBBERS, "memory");
@@ -142,6 +145,9 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
     if (!skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if (lane == 0 && __builtin_amdgcn_readfirstlane((int)redos) != 0)
+    __hip_atomic_fetch_add(ja.bail + a.nlist + 1, (uint32_t)__builtin_amdgcn_readfirstlane((int)redos),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   __syncthreads();
   Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
   for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) dst[i] = sPart[i];

@@ -281,11 +281,12 @@ def _optimize(dataset, trees, options, rng, device, evaluator_factory) -> ConstO
             f_conv = abs(fn[k] - f[k]) <= 0.0
             g_conv = np.max(np.abs(seg(Gn, k))) <= G_TOL
             if not newton[k]:
-                dxdg = float(np.dot(dx, dg))
+                dxdg = np.float64(np.dot(dx, dg))  # IEEE arithmetic: overflow gives Inf, as in Julia
                 if dxdg > 0:
-                    Hdg = invH[k] @ dg
-                    invH[k] = (invH[k] + (dxdg + dg @ Hdg) * np.outer(dx, dx) / dxdg ** 2
-                               - (np.outer(Hdg, dx) + np.outer(dx, Hdg)) / dxdg)
+                    with np.errstate(all="ignore"):
+                        Hdg = invH[k] @ dg
+                        invH[k] = (invH[k] + (dxdg + dg @ Hdg) * np.outer(dx, dx) / (dxdg * dxdg)
+                                   - (np.outer(Hdg, dx) + np.outer(dx, Hdg)) / dxdg)
             if x_conv or f_conv or g_conv:
                 conv[k], active[k] = True, False
         keep = np.repeat(moved, sizes)

@@ -11,8 +11,19 @@ Two partitions, as SURVEY.md §8e describes:
   the loss is ΣΣ / ΣΣw — identical to the single-device result up to fp64
   summation order.
 
-The combine step is plain host logic on top of any all-reduce, so it is
-tested with the gloo backend on CPU (tests/test_distributed.py).
+Constant optimisation on a row-sharded dataset (config #5) needs the
+gradient too: `combine_grad_shards` all-reduces [Σw·ℓ, failures, Σw·∂ℓ/∂c
+of every constant, Σw] in one buffer, and `RowShardedEvaluator` plugs that
+into `optimize_constants_batch` (each rank runs the same lockstep optimiser
+on identical, all-reduced values, so every rank takes the same steps).
+
+Trees of one batch are split over ranks by `shard_trees` (strided, so every
+rank gets a similar cost mix) and put back in order by `merge_tree_shards`
+(bench.py's strong-scaling run).
+
+The combine steps are plain host logic on top of any all-reduce, so they are
+tested with the gloo backend on CPU (tests/test_distributed.py) and on the
+engine with both ranks on one GPU (tests/test_distributed_gpu.py).
 """
 from __future__ import annotations
 
@@ -26,6 +37,26 @@ def shard_range(n: int, rank: int, world: int) -> Tuple[int, int]:
     base, extra = divmod(n, world)
     begin = rank * base + min(rank, extra)
     return begin, begin + base + (1 if rank < extra else 0)
+
+
+def shard_trees(ntrees: int, rank: int, world: int) -> np.ndarray:
+    """Indices of the trees rank evaluates: every world-th tree from rank on
+    (random populations are unordered, so strided shards carry similar cost)."""
+    return np.arange(rank, ntrees, world, dtype=np.int64)
+
+
+def merge_tree_shards(parts, ntrees: int) -> np.ndarray:
+    """Per-rank result arrays (in shard_trees order, rank 0 first) back into
+    tree order."""
+    parts = list(parts)
+    world = len(parts)
+    out = np.empty(ntrees, dtype=np.result_type(*[np.asarray(p).dtype for p in parts]) if parts else np.float64)
+    for r, p in enumerate(parts):
+        idx = shard_trees(ntrees, r, world)
+        if len(p) != len(idx):
+            raise ValueError(f"rank {r} returned {len(p)} results for {len(idx)} trees")
+        out[idx] = p
+    return out
 
 
 def pack_partials(sums: np.ndarray, wsum: float, ok: np.ndarray) -> np.ndarray:
@@ -50,6 +81,68 @@ def combine_row_shards(sums: np.ndarray, wsum: float, ok: np.ndarray,
                        all_reduce_sum: Callable[[np.ndarray], np.ndarray]):
     """Combine one rank's shard partials with everyone else's."""
     return unpack_partials(all_reduce_sum(pack_partials(sums, wsum, ok)))
+
+
+def pack_grad_partials(sums: np.ndarray, grads: np.ndarray, wsum: float, ok: np.ndarray,
+                       const_off: np.ndarray) -> np.ndarray:
+    """[sum_t, fail_t per tree ..., Σw·∂ℓ/∂c per constant ..., Σw]; a failed
+    tree contributes 0 to its sums and gradients and 1 to its failure count."""
+    nt, nc = len(sums), len(grads)
+    buf = np.zeros(2 * nt + nc + 1, dtype=np.float64)
+    buf[0:2 * nt:2] = np.where(ok, sums, 0.0)
+    buf[1:2 * nt:2] = np.where(ok, 0.0, 1.0)
+    bad = np.repeat(~np.asarray(ok, dtype=bool), np.diff(const_off))
+    buf[2 * nt:2 * nt + nc] = np.where(bad, 0.0, grads)
+    buf[-1] = wsum
+    return buf
+
+
+def unpack_grad_partials(buf: np.ndarray, ntrees: int, const_off: np.ndarray):
+    nc = int(const_off[-1])
+    sums, wsum, ok = unpack_partials(np.concatenate([buf[:2 * ntrees], buf[-1:]]))
+    grads = buf[2 * ntrees:2 * ntrees + nc].copy()
+    grads[np.repeat(~ok, np.diff(const_off))] = np.nan
+    return sums, grads, wsum, ok
+
+
+def combine_grad_shards(sums, grads, wsum, ok, const_off, all_reduce_sum: Callable[[np.ndarray], np.ndarray]):
+    """Combine one rank's (Σw·ℓ, Σw·∂ℓ/∂c, Σw, ok) of its row shard with the
+    other ranks' in one all-reduce (SURVEY.md §5 "constant-gradient
+    all-reduce"): ∂L/∂c = ΣΣ w·∂ℓ/∂c / ΣΣ w, did_succeed = AND over shards."""
+    red = all_reduce_sum(pack_grad_partials(sums, grads, wsum, ok, const_off))
+    return unpack_grad_partials(red, len(sums), const_off)
+
+
+class RowShardedEvaluator:
+    """Evaluator for `optimize_constants_batch` over a row-sharded dataset:
+    the candidates are compiled on this rank's shard, loss and gradient
+    partials are all-reduced (src/ConstantOptimization.jl:12-19,43 with the
+    dataset split across GPUs). `program_factory(candidates)` returns an
+    object with set_constants / eval_loss / eval_loss_grad (srhip.Program on
+    the shard; tests pass an oracle-backed stand-in)."""
+
+    def __init__(self, prog, dev, loss, all_reduce_sum: Callable[[np.ndarray], np.ndarray], T):
+        self.prog, self.dev, self.loss, self.red, self.T = prog, dev, loss, all_reduce_sum, T
+        self.const_off = np.asarray(prog.flat.const_off)
+
+    def _set(self, consts):
+        self.prog.set_constants(np.asarray(consts).astype(self.T, copy=False))
+
+    def loss_grad(self, consts):
+        from .constant_optimization import _finish, _grad_finish
+
+        self._set(consts)
+        sums, grads, wsum, ok = self.prog.eval_loss_grad(self.dev, self.loss.kind, self.loss.params)
+        s, g, W, k = combine_grad_shards(sums, grads, wsum, ok, self.const_off, self.red)
+        return _finish(s, W, k), _grad_finish(g, W, k, self.const_off)
+
+    def loss_only(self, consts):
+        from .constant_optimization import _finish
+
+        self._set(consts)
+        sums, wsum, ok = self.prog.eval_loss(self.dev, self.loss.kind, self.loss.params)
+        s, W, k = combine_row_shards(sums, wsum, ok, self.red)
+        return _finish(s, W, k)
 
 
 def torch_all_reduce_sum(device: Optional[str] = None, group=None):
@@ -92,3 +185,28 @@ def eval_loss_row_sharded(trees, dataset, options, device: Optional[int] = None,
         out = (tsum / twsum).astype(T)
     out[~tok] = T(np.inf)
     return out, tok
+
+
+def optimize_constants_row_sharded(trees, dataset, options, rng=None, device: Optional[int] = None, group=None):
+    """optimize_constants_batch with the dataset's rows sharded over the ranks
+    of the process group: every rank uploads its shard, compiles the
+    candidates on it, and all-reduces loss and gradient partials per step
+    (RowShardedEvaluator). All ranks return the same result."""
+    import torch.distributed as dist
+
+    from .constant_optimization import optimize_constants_batch
+    from .dataset import Dataset
+    from .interface import compile_trees
+
+    rank, world = dist.get_rank(group), dist.get_world_size(group)
+    rb, re = shard_range(dataset.n, rank, world)
+    shard = Dataset(dataset.X, dataset.y, dataset.weights, row_range=(rb, re))
+    dev = shard.device(device)
+    backend = dist.get_backend(group)
+    red = torch_all_reduce_sum("cuda" if backend == "nccl" else None, group)
+
+    def factory(cands):
+        return RowShardedEvaluator(compile_trees(cands, options, dataset.T, dev.ctx.device), dev,
+                                   options.elementwise_loss, red, dataset.T)
+
+    return optimize_constants_batch(dataset, trees, options, rng=rng, evaluator_factory=factory)

@@ -65,9 +65,15 @@ class Context:
 
     def last_bailed(self) -> int:
         """Trees of the last eval whose tree code handed a tile back."""
+        return self.last_jit_events()[0]
+
+    def last_jit_events(self):
+        """(trees handed back to the interpreter, tiles redone with the
+        PRECISE routines) of the last eval."""
         n = C.c_int32(0)
-        check(lib().srhip_last_bailed(self.handle, C.byref(n)))
-        return n.value
+        r = C.c_int64(0)
+        check(lib().srhip_last_bailed(self.handle, C.byref(n), C.byref(r)))
+        return n.value, r.value
 
 
 def default_device() -> int:

@@ -10,7 +10,8 @@ import pytest
 import torch.multiprocessing as mp
 
 import srhip
-from srhip.distributed import combine_row_shards, pack_partials, shard_range, unpack_partials
+from srhip.distributed import (combine_row_shards, merge_tree_shards, pack_grad_partials, pack_partials,
+                               shard_range, shard_trees, unpack_grad_partials, unpack_partials)
 
 
 def free_port():
@@ -36,6 +37,32 @@ def test_pack_roundtrip():
     s, w, k = unpack_partials(pack_partials(sums, 10.0, ok))
     assert w == 10.0 and list(k) == [True, False, True]
     assert s[0] == 1.5 and np.isnan(s[1]) and s[2] == 3.0
+
+
+def test_tree_shards_cover_and_merge_in_order():
+    for nt in (0, 1, 5, 4096, 4097):
+        for world in (1, 2, 3, 8):
+            parts = [shard_trees(nt, r, world) for r in range(world)]
+            allidx = np.sort(np.concatenate(parts)) if parts else np.zeros(0)
+            assert np.array_equal(allidx, np.arange(nt))  # every tree exactly once
+            assert max(len(p) for p in parts) - min(len(p) for p in parts) <= 1
+            vals = merge_tree_shards([p * 10.0 for p in parts], nt)  # results computed per shard
+            assert np.array_equal(vals, np.arange(nt) * 10.0)      # land back in tree order
+    with pytest.raises(ValueError):
+        merge_tree_shards([np.zeros(3), np.zeros(3)], 5)
+
+
+def test_grad_pack_roundtrip():
+    sums = np.array([1.5, np.nan, 3.0])
+    ok = np.array([True, False, True])
+    co = np.array([0, 2, 3, 5])
+    g = np.array([0.5, -1.0, np.nan, 2.0, 4.0])
+    buf = pack_grad_partials(sums, g, 7.0, ok, co)
+    assert np.all(np.isfinite(buf))  # a failed tree's NaNs never reach the all-reduce
+    s, gg, w, k = unpack_grad_partials(buf + buf, 3, co)  # two identical shards
+    assert w == 14.0 and list(k) == [True, False, True]
+    np.testing.assert_array_equal(gg[[0, 1, 3, 4]], 2 * g[[0, 1, 3, 4]])
+    assert np.isnan(gg[2]) and np.isnan(s[1])
 
 
 def _problem():
@@ -96,3 +123,100 @@ def test_row_sharded_gloo_world2_matches_single_process():
         assert np.array_equal(k, ref_ok)
         assert abs(W - w.sum()) < 1e-9 * w.sum()
         np.testing.assert_allclose(s[k], ref_s[k], rtol=1e-12)
+
+
+class OracleShardProgram:
+    """Test stand-in for srhip.Program on one row shard: loss and
+    Σ w·∂ℓ/∂c (L2) of every tree on the CPU oracle."""
+
+    def __init__(self, cands, options, X, y):
+        self.flat = srhip.flatten(cands, options, dtype=np.float64)
+        self.X, self.y = X, y
+        self.consts = np.asarray(self.flat.consts, dtype=np.float64)
+
+    def set_constants(self, c):
+        self.consts = np.asarray(c, dtype=np.float64)
+
+    def _trees(self):
+        co = self.flat.const_off
+        for t in range(self.flat.ntrees):
+            k, a, _ = self.flat.tree(t)
+            yield t, k, a, self.consts[co[t]:co[t + 1]]
+
+    def eval_loss_grad(self, dev, kind, params):
+        import oracle
+        sums, grads, ok = [], [], []
+        for t, k, a, c in self._trees():
+            out, g, good = oracle.eval_grad_consts(k, a, c, self.X, len(c))
+            r = out - self.y
+            sums.append(float(r @ r) if good else np.nan)
+            grads.append(2.0 * (g @ r) if good else np.full(len(c), np.nan))
+            ok.append(bool(good))
+        return (np.asarray(sums), np.concatenate(grads) if grads else np.zeros(0), float(self.X.shape[1]),
+                np.asarray(ok))
+
+    def eval_loss(self, dev, kind, params):
+        s, _, w, ok = self.eval_loss_grad(dev, kind, params)
+        return s, w, ok
+
+
+def _copt_problem():
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(11)
+    X = rng.standard_normal((3, 301))
+    y = 2.5 * np.cos(1.3 * X[0]) + 0.7 * X[1]
+    trees = srhip.random_population(24, o, 3, np.float64, seed=12)
+    return o, X, y, trees
+
+
+def _copt_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(root / "symbolicregression.jl_amd"), str(root / "oracle"), str(root / "tests")]
+    import torch.distributed as dist
+
+    from srhip.distributed import RowShardedEvaluator, torch_all_reduce_sum
+    from test_distributed import OracleShardProgram, _copt_problem
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    o, X, y, trees = _copt_problem()
+    b, e = shard_range(X.shape[1], rank, world)
+    red = torch_all_reduce_sum()
+    ds = srhip.Dataset(X, y)
+
+    def factory(cands):
+        return RowShardedEvaluator(OracleShardProgram(cands, o, X[:, b:e], y[b:e]), None, o.elementwise_loss, red,
+                                   np.float64)
+
+    res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(5), evaluator_factory=factory)
+    q.put((rank, res.losses, res.converged))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_constant_optimization_row_sharded_gloo_world2():
+    """optimize_constants_batch over 2 row shards (gradients all-reduced)
+    takes the same steps as over all rows in one process."""
+    from test_constant_optimization import OracleEvaluator
+
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_copt_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    o, X, y, trees = _copt_problem()
+    ref = srhip.optimize_constants_batch(srhip.Dataset(X, y), trees, o, rng=np.random.default_rng(5),
+                                         evaluator_factory=lambda c: OracleEvaluator(c, o, X, y))
+    (_, l0, c0), (_, l1, c1) = res
+    np.testing.assert_array_equal(l0, l1)  # both ranks agree exactly
+    assert np.array_equal(c0, ref.converged)
+    np.testing.assert_allclose(l0, ref.losses, rtol=1e-7)

@@ -1,0 +1,113 @@
+"""Row-sharded product path on the engine (config #5's partition), world_size 2
+with both ranks on device 0 and the gloo backend for the all-reduce:
+
+* eval_loss_row_sharded: each rank uploads its row shard and evaluates all
+  trees on it; the combined losses / did_succeed equal the single-process
+  engine result (fp64 partial sums, summation order aside) and the oracle's;
+* optimize_constants_row_sharded: loss AND ∂L/∂c partials all-reduced per
+  step (RowShardedEvaluator); both ranks agree exactly and match the
+  single-process optimiser on the engine.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+import oracle
+import srhip
+
+pytestmark = pytest.mark.gpu
+
+
+def free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _problem(T=np.float32):
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(21)
+    X = rng.standard_normal((20, 200_003)).astype(T)
+    y = (T(2) * np.cos(X[3]) + X[0] * X[0] - T(2)).astype(T)
+    trees = srhip.random_population(700, o, 20, T, seed=22)
+    return o, X, y, trees
+
+
+def _copt_problem():
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(31)
+    X = rng.standard_normal((4, 50_001))
+    y = 2.5 * np.cos(1.3 * X[0]) + 0.7 * X[1]
+    trees = srhip.random_population(64, o, 4, np.float64, seed=32)
+    return o, X, y, trees
+
+
+def _worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(root / "symbolicregression.jl_amd"), str(root / "oracle"), str(root / "tests")]
+    os.environ["SRHIP_DEVICE"] = "0"
+    import torch.distributed as dist
+
+    from srhip.distributed import eval_loss_row_sharded, optimize_constants_row_sharded
+    from test_distributed_gpu import _copt_problem, _problem
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        o, X, y, trees = _problem()
+        losses, ok = eval_loss_row_sharded(trees, srhip.Dataset(X, y), o, device=0)
+        o2, X2, y2, trees2 = _copt_problem()
+        res = optimize_constants_row_sharded(trees2, srhip.Dataset(X2, y2), o2, rng=np.random.default_rng(5),
+                                             device=0)
+        q.put((rank, losses, ok, res.losses, res.converged))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(240)
+def test_row_sharded_engine_world2_on_one_gpu(gpu_ctx):
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=200) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    # loss evaluation: both ranks, single-process engine, oracle
+    o, X, y, trees = _problem()
+    ref_l, ref_ok = srhip.eval_loss_batch_ok(trees, srhip.Dataset(X, y), o)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    _, or_l, or_ok = oracle.eval_loss_batch(flat, X, y, dtype=np.float32, nthreads=16)
+    for _, l, k, _, _ in res:
+        assert np.array_equal(k, ref_ok) and np.array_equal(k, or_ok)
+        m = k & np.isfinite(ref_l)
+        # the shards regroup the Float32 per-tile partial sums: within the
+        # north_star's 1e-5 of the single-process engine and of the oracle
+        np.testing.assert_allclose(l[m], ref_l[m], rtol=1e-5)
+        # against the oracle's Float64-evaluated transcendentals the FAST
+        # path moves ill-conditioned trees more (tests/test_full_size.py
+        # checks those against the conditioning); the bulk agrees
+        rel = np.abs(l[m] - or_l[m]) / np.abs(or_l[m])
+        assert np.median(rel) < 1e-6 and np.mean(rel < 1e-5) > 0.9
+    np.testing.assert_array_equal(res[0][1], res[1][1])
+    # constant optimisation with all-reduced gradients
+    o2, X2, y2, trees2 = _copt_problem()
+    ref = srhip.optimize_constants_batch(srhip.Dataset(X2, y2), trees2, o2, rng=np.random.default_rng(5))
+    (_, _, _, l0, c0), (_, _, _, l1, c1) = res
+    np.testing.assert_array_equal(l0, l1)
+    np.testing.assert_array_equal(c0, c1)
+    assert np.mean(c0 == ref.converged) >= 0.95
+    both = c0 & ref.converged
+    np.testing.assert_allclose(l0[both], ref.losses[both], rtol=1e-6)
