@@ -4,21 +4,26 @@
 One step = one srhip_eval_loss call over the whole batch: 4096 random trees
 (maxsize 30, ops + - * / and cos exp) × 1M rows × 5 features, Float32, L2,
 with the dataset and the compiled trees already resident in HBM; the step
-returns the per-tree loss sums / did_succeed flags in host memory.
+returns the per-tree loss sums / did_succeed flags in host memory. Large
+Float32 batches run as tree code (csrc/jit.cpp): the program's creation
+compiles every tree to machine code (reported under setup_s / tree_code).
 
 Metric: node·row evals/sec = Σ_trees count_nodes × rows ÷ wall time
 (nominal count, no credit for early-failed trees).
 
-Multi-GPU (torchrun, one rank per GPU): trees are independent, so each rank
-evaluates its own 4096-tree batch (islands/trees sharded over GPUs) against
-its own copy of the dataset, with no collective on the data path — weak
-scaling. Timing: barrier + sync on both sides of the K timed steps, max over
-ranks; value = all ranks' node·rows ÷ that time.
+Multi-GPU (torchrun, one rank per GPU): strong scaling over trees — the same
+4096 trees are split over the N ranks (srhip.distributed.shard_trees, every
+N-th tree), each rank evaluates its share against its own copy of the
+dataset, no collective on the data path. Timing: barrier + sync on both
+sides of the K timed steps, max over ranks; value = the 4096 trees'
+node·rows ÷ that time. A weak-scaling figure (4096 trees on every rank) is
+reported beside it as `weak`.
 
 cpu_baseline: the oracle/ CPU restatement of the reference algorithm
 (recursive per-node arrays with early exit, fused leaf patterns, separate
-loss pass; the turbo=true-like vectorised build) on the host cores, threaded
-over trees, on a bounded sample of the same workload.
+loss pass) on the host cores this job may use, threaded over trees, both the
+turbo=true-like vectorised build and the turbo=false-like scalar build on
+the same bounded row sample of the same workload.
 """
 from __future__ import annotations
 
@@ -43,6 +48,24 @@ METRIC = "node\u00b7row evals/sec (Float32, 4096 trees\u00d71M rows) at 1/2/4/8 
 HBM_PEAK_GBS = 8000.0
 
 
+def available_cpus() -> int:
+    """CPUs this job may use: the cgroup CPU quota if one is set, else the
+    affinity mask (a shared GPU box shows the whole machine in os.cpu_count())."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    try:
+        quota, period = Path("/sys/fs/cgroup/cpu.max").read_text().split()[:2]
+        if quota != "max":
+            n = min(n, max(1, int(int(quota) / int(period))))
+    except (OSError, ValueError):
+        pass
+    return max(n, 1)
+
+
+def cpu_note() -> str:
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else None
+    return f"affinity {aff}, os.cpu_count() {os.cpu_count()}, cgroup-limited {available_cpus()}"
+
+
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -54,7 +77,8 @@ def parse():
     ap.add_argument("--maxsize", type=int, default=30)
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
-    ap.add_argument("--cpu-threads", type=int, default=0, help="0: min(os.cpu_count(), 16)")
+    ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
+    ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
     ap.add_argument("--no-cpu", action="store_true")
     return ap.parse_args()
 
@@ -75,6 +99,7 @@ def main():
 
     import srhip
     from srhip import constants as K
+    from srhip.distributed import shard_trees
 
     T = np.float32 if args.dtype == "f32" else np.float64
     options = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
@@ -82,7 +107,9 @@ def main():
     X = rng.standard_normal((args.nfeat, args.rows)).astype(T)
     y = (T(2) * np.cos(X[3 % args.nfeat]) + X[0] * X[0] - T(2)).astype(T)
     t0 = time.time()
-    trees = srhip.random_population(args.ntrees, options, args.nfeat, T, seed=1000 + rank, maxsize=args.maxsize)
+    # the same batch on every rank; rank r evaluates every world-th tree (strong scaling)
+    all_trees = srhip.random_population(args.ntrees, options, args.nfeat, T, seed=1000, maxsize=args.maxsize)
+    trees = [all_trees[i] for i in shard_trees(len(all_trees), rank, world)]
     t_gen = time.time() - t0
 
     ctx = srhip.get_context(local_rank)
@@ -94,12 +121,6 @@ def main():
     _, total_nodes, _ = prog.info()
     node_rows = float(total_nodes) * args.rows
 
-    def step():
-        return prog.eval_loss(ds, K.LOSS["L2"])
-
-    for _ in range(args.warmup):
-        step()
-
     def barrier():
         ctx.sync()
         if dist:
@@ -107,26 +128,42 @@ def main():
             torch.cuda.synchronize()
             tdist.barrier()
 
-    barrier()
-    kernel_ms = []
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        sums, wsum, ok = step()
-        kernel_ms.append(ctx.last_kernel_time()[0])
-    barrier()
-    elapsed = time.perf_counter() - t0
+    def timed(p, steps, warmup):
+        for _ in range(warmup):
+            p.eval_loss(ds, K.LOSS["L2"])
+        barrier()
+        kms = []
+        t_ = time.perf_counter()
+        for _ in range(steps):
+            p.eval_loss(ds, K.LOSS["L2"])
+            kms.append(ctx.last_kernel_time()[0])
+        barrier()
+        return time.perf_counter() - t_, kms
 
-    my_node_rows = node_rows * args.steps
-    if dist:
+    def reduce_max_sum(elapsed_, node_rows_):
+        if not dist:
+            return elapsed_, node_rows_
         torch, tdist = dist
-        t = torch.tensor([elapsed], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed_], dtype=torch.float64, device="cuda")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
-        nr = torch.tensor([my_node_rows], dtype=torch.float64, device="cuda")
+        nr = torch.tensor([node_rows_], dtype=torch.float64, device="cuda")
         tdist.all_reduce(nr, op=tdist.ReduceOp.SUM)
-        total_node_rows = float(nr.item())
-    else:
-        total_node_rows = my_node_rows
+        return float(t.item()), float(nr.item())
+
+    elapsed, kernel_ms = timed(prog, args.steps, args.warmup)
+    elapsed, total_node_rows = reduce_max_sum(elapsed, node_rows * args.steps)
+    tree_code = prog.jit_info()
+
+    # secondary: weak scaling (the whole batch on every rank)
+    weak = None
+    if world > 1 and not args.no_weak:
+        wprog = srhip.Program(ctx, srhip.flatten(all_trees, options, dtype=T), T)
+        _, wnodes, _ = wprog.info()
+        w_el, _ = timed(wprog, max(args.steps // 2, 3), 1)
+        w_el, w_nr = reduce_max_sum(w_el, float(wnodes) * args.rows * max(args.steps // 2, 3))
+        weak = {"value": w_nr / w_el, "unit": "node·row/s", "ntrees_per_gpu": len(all_trees),
+                "ms_per_step": w_el * 1e3 / max(args.steps // 2, 3)}
+        del wprog
 
     value = total_node_rows / elapsed
     ms_per_step = elapsed * 1e3 / args.steps
@@ -168,7 +205,7 @@ def main():
         sys.path.insert(0, str(ROOT / "oracle"))
         import oracle
 
-        threads = args.cpu_threads or min(os.cpu_count() or 1, 16)
+        threads = args.cpu_threads or available_cpus()
         fl = srhip.flatten(trees, options, dtype=T)
 
         def run_cpu(nrows, variant="simd"):
@@ -186,12 +223,12 @@ def main():
             "cores": threads,
             "kind": "port",
             "sample": f"all {len(trees)} trees x first {nrows} rows; oracle simd build (turbo=true analogue), "
-                      f"OpenMP over trees; {dt:.1f} s",
+                      f"OpenMP over trees on {threads} threads (the CPUs this job may use: {cpu_note()}); "
+                      f"{dt:.1f} s",
         }
-        # turbo=false analogue (scalar build), a smaller sample
-        ns = max(probe, nrows // 3)
-        dts, nrs = run_cpu(ns, "scalar")
-        cpu["turbo_false"] = {"value": nrs / dts, "sample": f"first {ns} rows; oracle scalar build; {dts:.1f} s"}
+        # turbo=false analogue (scalar build) on the same rows
+        dts, nrs = run_cpu(nrows, "scalar")
+        cpu["turbo_false"] = {"value": nrs / dts, "sample": f"same {nrows} rows; oracle scalar build; {dts:.1f} s"}
 
     out = {
         "metric": METRIC if T == np.float32 else "node·row evals/sec (Float64)",
@@ -202,19 +239,23 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": ms_per_step,
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong",
         "vs_baseline": None,
         "dtype": args.dtype,
         "data": "synthetic (randn X, y = 2cos(x4) + x1^2 - 2; random trees per gen_random_tree_fixed_size)",
         "config": {
             "workload": f"config#2 batched eval_loss: {args.ntrees} trees (size U{{1..{args.maxsize}}}, "
                         f"+ - * / cos exp) x {args.nfeat} feat x {args.rows} rows, L2",
-            "ntrees_per_gpu": args.ntrees,
+            "ntrees": args.ntrees,
+            "ntrees_per_gpu": len(trees),
             "rows": args.rows,
             "nfeat": args.nfeat,
             "total_nodes_per_gpu": int(total_nodes),
-            "parallelism": f"trees sharded over {world} GPU(s), no data-path collective",
+            "parallelism": f"the {args.ntrees} trees sharded over {world} GPU(s) (strong scaling), "
+                           "no data-path collective",
         },
+        "weak": weak,
+        "tree_code": tree_code,
         "roofline": roof,
         "cpu_baseline": cpu,
         "setup_s": {"tree_gen": round(t_gen, 2), "compile_upload": round(t_compile, 3)},

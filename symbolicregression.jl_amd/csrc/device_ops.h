@@ -198,7 +198,10 @@ constexpr float kTrigQMax = 33500.0f;
 // and cos (to r^17 / r^16) and one rounding to Float32 give the value the
 // oracle's Float64 sin/cos rounds to (except within ~2^-45 of a rounding
 // boundary).
-__device__ __forceinline__ float big_sincos_f32(float x, int want_cos) {
+// Out of line in the interpreters (rarely taken, behind a ballot; inline it
+// would cost the dispatch loop registers), inline in the tree compiler's
+// routines (SRHIP_INLINE_ALL: a routine cannot call).
+__device__ SR_NOINLINE float big_sincos_f32(float x, int want_cos) {
   const uint32_t ax = __float_as_uint(x) & 0x7fffffffu;
   const int e = (int)(ax >> 23) - 127;  // >= 16 on this path
   const uint64_t M = (ax & 0x7fffffu) | 0x800000u;

@@ -1,0 +1,236 @@
+# BatchedCallers.jl — the hot path's callers, batched (SURVEY.md §8 a10 / f1).
+#
+# The reference scores one candidate at a time: next_generation
+# (src/Mutate.jl:26-255) calls score_func per mutated tree inside
+# reg_evol_cycle (src/RegularizedEvolution.jl:13-155), Population(...)
+# (src/Population.jl:31-46) and finalize_scores (:134-148) score member by
+# member. This module keeps those algorithms and moves the scoring out of the
+# per-candidate loop, so that one SRHip.eval_loss_batch launch scores every
+# candidate of a step:
+#
+#   * `population_batched`      — Population(dataset; npop, nlength, options, nfeatures)
+#   * `finalize_scores_batched` — finalize_scores(dataset, pop, options)
+#   * `reg_evol_cycle_batched`  — reg_evol_cycle with fast_cycle semantics
+#     (one baby per tournament_selection_n-member subsample, replace-oldest),
+#     for several islands in lockstep: every island's babies in one launch.
+#
+# next_generation is split into `propose` (mutation choice, attempts,
+# check_constraints — everything before score_func, calling the reference's
+# own mutation functions) and `accept` (the NaN rejection and the
+# annealing / adaptive-parsimony acceptance rule after it). A candidate whose
+# mutation needs no score (simplify, optimize, do_nothing, a failed
+# constraint check) is decided in `propose`, as in the reference.
+#
+# UNTESTED AS JULIA (no Julia in the build image). The Python mirror of the
+# same lockstep loop (symbolicregression.jl_amd/srhip/search.py) runs in the
+# test suite; tests/test_julia_binding.py checks this file's references to
+# the reference's functions and to SRHip statically.
+module BatchedCallers
+
+import DynamicExpressions: Node, copy_node, count_constants, count_depth, simplify_tree, combine_operators
+import ..CoreModule: Options, Dataset, RecordType, sample_mutation
+import ..ComplexityModule: compute_complexity
+import ..LossFunctionsModule: score_func, score_func_batch, loss_to_score
+import ..CheckConstraintsModule: check_constraints
+import ..AdaptiveParsimonyModule: RunningSearchStatistics
+import ..PopMemberModule: PopMember
+import ..PopulationModule: Population
+import ..MutationFunctionsModule:
+    gen_random_tree, gen_random_tree_fixed_size, mutate_constant, mutate_operator, append_random_op,
+    prepend_random_op, insert_random_op, delete_random_op
+import ..ConstantOptimizationModule: optimize_constants
+import ..SRHip
+
+"""
+    score_batch(dataset, trees, options) -> (scores, losses)
+
+score_func (src/LossFunctions.jl:86-92) for every tree: one SRHip launch when
+the engine covers the options, else the reference, tree by tree.
+"""
+function score_batch(dataset::Dataset{T}, trees::AbstractVector{Node{T}}, options::Options) where {T}
+    if !isempty(trees) && SRHip.enabled(options)
+        try
+            losses = SRHip.eval_loss_batch(trees, dataset, options)
+            scores = [loss_to_score(l, dataset.baseline_loss, t, options) for (l, t) in zip(losses, trees)]
+            return scores, losses
+        catch e
+            e isa SRHip.Unsupported || rethrow()
+        end
+    end
+    pairs = [score_func(dataset, t, options) for t in trees]
+    return T[p[1] for p in pairs], T[p[2] for p in pairs]
+end
+
+"""
+    score_batch_minibatch(dataset, trees, options) -> (scores, losses)
+
+score_func_batch (src/LossFunctions.jl:95-115) for every tree: one row sample
+of batch_size rows (with replacement) shared by the launch; a failed
+evaluation scores (0, Inf) as in the reference.
+"""
+function score_batch_minibatch(dataset::Dataset{T}, trees::AbstractVector{Node{T}}, options::Options) where {T}
+    if !isempty(trees) && SRHip.enabled(options)
+        try
+            idx = rand(1:(dataset.n), options.batch_size)
+            losses = SRHip.eval_loss_batch(trees, dataset, options; idx=idx)
+            scores = [isfinite(l) ? loss_to_score(l, dataset.baseline_loss, t, options) : zero(T)
+                      for (l, t) in zip(losses, trees)]
+            return scores, losses
+        catch e
+            e isa SRHip.Unsupported || rethrow()
+        end
+    end
+    pairs = [score_func_batch(dataset, t, options) for t in trees]
+    return T[p[1] for p in pairs], T[p[2] for p in pairs]
+end
+
+# ---- Population / finalize_scores ---------------------------------------------------
+
+"""Population(dataset; npop, nlength, options, nfeatures) with one launch."""
+function population_batched(dataset::Dataset{T}; npop::Int, nlength::Int=3, options::Options,
+                            nfeatures::Int) where {T}
+    trees = [gen_random_tree(nlength, options, nfeatures, T) for _ in 1:npop]
+    scores, losses = score_batch(dataset, trees, options)
+    members = [PopMember(trees[i], scores[i], losses[i]; parent=-1, deterministic=options.deterministic)
+               for i in 1:npop]
+    return Population{T}(members, npop)
+end
+
+"""finalize_scores (src/Population.jl:134-148): with batching, every member is
+re-scored on the full dataset — one launch for the population."""
+function finalize_scores_batched(dataset::Dataset{T}, pop::Population, options::Options) where {T}
+    options.batching || return (pop, 0.0)
+    scores, losses = score_batch(dataset, [m.tree for m in pop.members], options)
+    for (m, s, l) in zip(pop.members, scores, losses)
+        m.score = s
+        m.loss = l
+    end
+    return (pop, pop.n * (options.batch_size / dataset.n))
+end
+
+# ---- next_generation, split around its score_func call ---------------------------------
+
+# A proposal: either decided (`member` set: no score needed) or a tree to score.
+struct Proposal{T}
+    parent::PopMember{T}
+    tree::Union{Node{T},Nothing}
+    member::Union{PopMember{T},Nothing}
+    accepted::Bool
+    num_evals::Float64
+end
+
+# the tree-producing mutations of next_generation (src/Mutate.jl:79-115,132-139),
+# through the reference's own mutation functions
+function mutate_tree(choice::Symbol, tree::Node{T}, temperature, curmaxsize::Int, options::Options,
+                     nfeatures::Int) where {T}
+    choice == :mutate_constant && return mutate_constant(tree, temperature, options)
+    choice == :mutate_operator && return mutate_operator(tree, options)
+    choice == :add_node && return rand() < 0.5 ? append_random_op(tree, options, nfeatures) :
+                                                 prepend_random_op(tree, options, nfeatures)
+    choice == :insert_node && return insert_random_op(tree, options, nfeatures)
+    choice == :delete_node && return delete_random_op(tree, options, nfeatures)
+    choice == :randomize && return gen_random_tree_fixed_size(rand(1:curmaxsize), options, nfeatures, T)
+    error("Unknown mutation choice: $choice")
+end
+
+"""Everything of next_generation before score_func (src/Mutate.jl:26-193)."""
+function propose(dataset::Dataset{T}, member::PopMember{T}, temperature, curmaxsize::Int,
+                 options::Options) where {T}
+    prev = member.tree
+    keep(tree, accepted, evals=0.0) = Proposal{T}(member, nothing,
+        PopMember(tree, member.score, member.loss; parent=member.ref, deterministic=options.deterministic),
+        accepted, evals)
+    weights = copy(options.mutation_weights)
+    weights.mutate_constant *= min(8, count_constants(prev)) / 8.0
+    if compute_complexity(prev, options) >= curmaxsize || count_depth(prev) >= options.maxdepth
+        weights.add_node = 0.0
+        weights.insert_node = 0.0
+    end
+    choice = sample_mutation(weights)
+    choice == :do_nothing && return keep(prev, true)
+    if choice == :simplify
+        return keep(combine_operators(simplify_tree(copy_node(prev), options.operators), options.operators), true)
+    end
+    if choice == :optimize
+        m, evals = optimize_constants(dataset, PopMember(copy_node(prev), member.score, member.loss;
+                                                         parent=member.ref, deterministic=options.deterministic),
+                                      options)
+        return Proposal{T}(member, nothing, m, true, evals)
+    end
+    for _ in 1:10  # max_attempts
+        tree = mutate_tree(choice, copy_node(prev), temperature, curmaxsize, options, dataset.nfeatures)
+        check_constraints(tree, options, curmaxsize) && return Proposal{T}(member, tree, nothing, false, 0.0)
+    end
+    return keep(copy_node(prev), false)  # failed constraint check: rejected
+end
+
+"""Everything of next_generation after score_func (src/Mutate.jl:207-255)."""
+function accept(p::Proposal{T}, score::T, loss::T, temperature, stats::RunningSearchStatistics,
+                options::Options) where {T}
+    member = p.parent
+    reject() = (PopMember(copy_node(member.tree), member.score, member.loss; parent=member.ref,
+                          deterministic=options.deterministic), false)
+    isnan(score) && return reject()
+    prob = 1.0
+    if options.annealing
+        prob *= exp(-(score - member.score) / (temperature * options.alpha))
+    end
+    if options.use_frequency
+        freq(c) = 0 < c <= options.maxsize ? stats.normalized_frequencies[c] : 1e-6
+        prob *= freq(compute_complexity(member.tree, options)) / freq(compute_complexity(p.tree, options))
+    end
+    prob < rand() && return reject()
+    return (PopMember(p.tree, score, loss; parent=member.ref, deterministic=options.deterministic), true)
+end
+
+# ---- reg_evol_cycle, fast_cycle semantics, islands in lockstep ------------------------
+
+"""
+    reg_evol_cycle_batched(dataset, pops, temperature, curmaxsize, stats, options) -> (pops, num_evals)
+
+One fast_cycle pass (src/RegularizedEvolution.jl:33-79) over every island
+of `pops` at once: shuffle each population, take the best of every
+tournament_selection_n-member subsample, propose one baby each, score ALL
+islands' babies in one launch, then accept and replace the oldest member
+per island, in the reference's order.
+"""
+function reg_evol_cycle_batched(dataset::Dataset{T}, pops::AbstractVector{<:Population}, temperature,
+                                curmaxsize::Int, stats::AbstractVector{RunningSearchStatistics},
+                                options::Options) where {T}
+    proposals = Vector{Vector{Proposal{T}}}(undef, length(pops))
+    for (k, pop) in enumerate(pops)
+        shuffle!(pop.members)
+        ncyc = round(Int, pop.n / options.tournament_selection_n)
+        props = Vector{Proposal{T}}(undef, ncyc)
+        Threads.@threads for i in 1:ncyc
+            sub = (1 + (i - 1) * options.tournament_selection_n):(i * options.tournament_selection_n)
+            allstar = pop.members[sub[argmin([pop.members[j].score for j in sub])]]
+            props[i] = propose(dataset, allstar, temperature, curmaxsize, options)
+        end
+        proposals[k] = props
+    end
+    # one launch for every island's babies
+    trees = Node{T}[p.tree for props in proposals for p in props if p.member === nothing]
+    scores, losses = options.batching ? score_batch_minibatch(dataset, trees, options) :
+                     score_batch(dataset, trees, options)
+    num_evals = length(trees) * (options.batching ? options.batch_size / dataset.n : 1.0)
+    j = 0
+    for (k, pop) in enumerate(pops)
+        for p in proposals[k]
+            num_evals += p.num_evals
+            baby, accepted = if p.member === nothing
+                j += 1
+                accept(p, scores[j], losses[j], temperature, stats[k], options)
+            else
+                (p.member, p.accepted)
+            end
+            oldest = argmin([m.birth for m in pop.members])
+            (accepted || !options.skip_mutation_failures) && (pop.members[oldest] = baby)
+        end
+    end
+    return pops, num_evals
+end
+
+shuffle!(v) = (for i in length(v):-1:2; j = rand(1:i); v[i], v[j] = v[j], v[i]; end; v)
+
+end # module

@@ -157,3 +157,37 @@ def test_binding_exposes_the_shim_api():
         assert re.search(rf"^function {re.escape(fn)}\(|^{re.escape(fn)}\(.*\) =", src, re.M), fn
     # the shared device-dataset table is only touched under the lock
     assert re.search(r"lock\(CTX_LOCK\) do\s+get!\(DEVICE_DATASETS", src)
+
+
+BATCHED = ROOT / "symbolicregression.jl_amd" / "julia" / "BatchedCallers.jl"
+REFERENCE_SRC = Path("/root/reference/src")
+
+
+def test_batched_callers_use_existing_functions():
+    """BatchedCallers.jl (the Julia-side candidate batching of SURVEY.md §8 f1)
+    imports the reference's own mutation / scoring functions and calls the
+    SRHip binding; every imported name must be defined in the reference
+    (checked when its sources are present, i.e. in the build container) and
+    every SRHip.* it uses must exist in SRHip.jl."""
+    src = BATCHED.read_text()
+    code = "\n".join(ln.split("#")[0] for ln in src.splitlines())
+    imported = []
+    for m in re.finditer(r"import \.\.(\w+):\s*((?:[\w!]+\s*,\s*)*[\w!]+)", code):
+        imported += [n.strip() for n in m.group(2).split(",")]
+    assert {"next_generation"} .isdisjoint(imported)  # it is split, not called
+    for need in ("mutate_constant", "mutate_operator", "append_random_op", "prepend_random_op", "insert_random_op",
+                 "delete_random_op", "check_constraints", "score_func", "loss_to_score", "optimize_constants"):
+        assert need in imported, need
+    srhip_jl = JL.read_text()
+    for call in set(re.findall(r"SRHip\.(\w+)", code)):
+        assert re.search(rf"(function {call}\(|struct {call}\b|^{call}\()", srhip_jl, re.M), f"SRHip.{call} missing"
+    for fn in ("population_batched", "finalize_scores_batched", "reg_evol_cycle_batched", "propose", "accept"):
+        assert re.search(rf"^function {fn}\(", code, re.M), fn
+    if REFERENCE_SRC.exists():
+        defs = "\n".join(p.read_text() for p in REFERENCE_SRC.glob("*.jl"))
+        dyn = {"Node", "copy_node", "count_constants", "count_depth", "simplify_tree", "combine_operators"}
+        for name in imported:
+            if name in dyn or name in ("Options", "Dataset", "RecordType", "RunningSearchStatistics", "PopMember",
+                                       "Population"):
+                continue  # DynamicExpressions (not vendored) or types
+            assert re.search(rf"function {re.escape(name)}\(", defs), f"{name} is not defined in the reference"
