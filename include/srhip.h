@@ -232,6 +232,11 @@ int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog,
  * code-object load times (ms). All zero for an interpreted program. */
 int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nfast,
                                int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load);
+/* How srhip_program_set_constants applied new constants so far: in place
+ * (the device programs' immediates overwritten, same buffers) or by a full
+ * rebuild (folding or a static verdict changed, or the first new constant set
+ * of a tree-code program, which runs interpreted from then on). */
+int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inplace, int64_t* out_rebuilt);
 /* Trees of the last eval on this context whose tree code handed a tile back
  * (a sin/cos argument beyond the fast reduction) and were re-evaluated, and
  * tiles that tree code redid with the Float64-evaluated routines (a FAST-path

@@ -146,6 +146,14 @@ struct srhip_program {
   jit::Module* jit = nullptr;
   int nlist_j = 0;
   jit::Stats jit_stats;
+  // tree code is compiled for one constant set: a program whose constants are
+  // set again (srhip_program_set_constants) runs on the interpreter
+  bool jit_allowed = true;
+  // host image of the uploaded programs: set_constants patches the device
+  // copies in place when only instruction immediates change
+  std::vector<unsigned char> h_code, h_gcode;
+  std::vector<int32_t> h_toff, h_gtoff;
+  int64_t n_inplace = 0, n_rebuild = 0;
   int opset = OPSET_FULL;      // smallest operator set covering the compiled programs
   // gradient programs (compiled on first use)
   bool grad_built = false;
@@ -245,6 +253,9 @@ void build_grad_program(srhip_program* p) {
   HIP_CHECK(hipMemcpyAsync(p->d_const_off, p->const_off.data(), p->const_off.size() * sizeof(int32_t),
                            hipMemcpyHostToDevice, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  p->h_gcode.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
+                    reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
+  p->h_gtoff = cb.tree_off;
   p->grad_built = true;
 }
 
@@ -304,7 +315,7 @@ void build_program(srhip_program* p) {
   p->nlist_j = 0;
   p->jit_stats = jit::Stats();
   if constexpr (std::is_same<T, float>::value) {
-    if (jit_wanted((int)a.size())) {
+    if (p->jit_allowed && jit_wanted((int)a.size())) {
       std::vector<int32_t> jl, rest;
       jit::Options jo;
       jo.fast = jit_fast_enabled();
@@ -344,6 +355,65 @@ void build_program(srhip_program* p) {
   if (!list.empty())
     HIP_CHECK(hipMemcpyAsync(p->d_list, list.data(), list.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipStreamSynchronize(s));
+  p->h_code.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
+                   reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
+  p->h_toff = cb.tree_off;
+}
+
+// Same instruction streams (opcodes, operands, offsets, static verdicts) up to
+// the immediates of the instructions?
+template <typename T>
+bool same_shape(const std::vector<Ins<T>>& code, const std::vector<unsigned char>& old) {
+  if (code.size() * sizeof(Ins<T>) != old.size()) return false;
+  const Ins<T>* o = reinterpret_cast<const Ins<T>*>(old.data());
+  for (size_t k = 0; k < code.size(); ++k)
+    if (code[k].code != o[k].code) return false;
+  return true;
+}
+
+// srhip_program_set_constants: recompile on the host; when only the
+// immediates moved, overwrite the device programs in place (no reallocation,
+// no list rebuild, gradient programs patched too); else rebuild.
+template <typename T>
+void update_constants(srhip_program* p) {
+  if (p->jit) {  // first new constant set of a tree-code program: interpreter from now on
+    p->jit_allowed = false;
+    ++p->n_rebuild;
+    build_program<T>(p);
+    return;
+  }
+  p->jit_allowed = false;
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->consts.data();
+  CompiledBatch<T> cb = compile_batch<T>(tr);
+  if (!same_shape(cb.code, p->h_code) || cb.tree_off != p->h_toff || cb.static_fail != p->static_fail ||
+      cb.fail_if_rows != p->fail_if_rows) {
+    ++p->n_rebuild;
+    build_program<T>(p);
+    return;
+  }
+  hipStream_t s = p->ctx->stream;
+  HIP_CHECK(hipStreamSynchronize(s));  // no launch may still read the old programs / host images
+  p->h_code.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
+                   reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
+  HIP_CHECK(hipMemcpyAsync(p->d_code, p->h_code.data(), p->h_code.size(), hipMemcpyHostToDevice, s));
+  if (p->grad_built) {
+    CompiledBatch<T> gb = compile_batch<T>(tr, /*grad=*/true);
+    if (same_shape(gb.code, p->h_gcode) && gb.tree_off == p->h_gtoff && gb.static_fail == p->g_static_fail) {
+      p->h_gcode.assign(reinterpret_cast<const unsigned char*>(gb.code.data()),
+                        reinterpret_cast<const unsigned char*>(gb.code.data() + gb.code.size()));
+      HIP_CHECK(hipMemcpyAsync(p->d_gcode, p->h_gcode.data(), p->h_gcode.size(), hipMemcpyHostToDevice, s));
+    } else {
+      p->grad_built = false;  // rebuilt on next use
+    }
+  }
+  HIP_CHECK(hipStreamSynchronize(s));
+  ++p->n_inplace;
 }
 
 void check_program_vs_dataset(const srhip_dataset* ds, const srhip_program* p) {
@@ -1064,8 +1134,8 @@ int32_t srhip_program_set_constants(srhip_program* prog, const void* consts) {
     if (cb) std::memcpy(prog->consts.data(), consts, cb);
     std::lock_guard<std::mutex> lk(prog->ctx->mu);
     HIP_CHECK(hipSetDevice(prog->ctx->device));
-    if (prog->dtype == SRHIP_F32) build_program<float>(prog);
-    else build_program<double>(prog);
+    if (prog->dtype == SRHIP_F32) update_constants<float>(prog);
+    else update_constants<double>(prog);
     return SRHIP_OK;
   });
 }
@@ -1161,6 +1231,15 @@ int32_t srhip_sync(srhip_ctx* ctx) {
 }
 
 }  // extern "C"
+
+int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inplace, int64_t* out_rebuilt) {
+  return guarded([&] {
+    if (!prog) throw Error(SRHIP_ERR_INVALID, "null program");
+    if (out_inplace) *out_inplace = prog->n_inplace;
+    if (out_rebuilt) *out_rebuilt = prog->n_rebuild;
+    return SRHIP_OK;
+  });
+}
 
 int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nfast,
                                int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load) {

@@ -241,11 +241,21 @@ BAD = ("s_swappc", "s_setpc", "s_getpc", "scratch_", "buffer_", "global_", "flat
 
 
 def extract(asm_text, name):
-    m = re.search(rf"^sr_h_{name}:.*?$(.*?)^\s*s_endpgm", asm_text, re.S | re.M)
+    m = re.search(rf"^sr_h_{name}:.*?$(.*?)^\.Lfunc_end", asm_text, re.S | re.M)
     if not m:
         raise SystemExit(f"gen_asm_interp: handler {name} not found in compiler output")
+    # the compiler may place cold blocks after the kernel's s_endpgm: every
+    # s_endpgm becomes a branch to the handler's end (the last one is dropped)
+    body = m.group(1).rstrip().splitlines()
+    while body and not body[-1].strip().split(";")[0]:
+        body.pop()
+    if body and body[-1].strip().startswith("s_endpgm"):
+        body.pop()
+    body = [("s_branch .LBBsrend" if ln.strip().startswith("s_endpgm") else ln) for ln in body]
+    if any(ln == "s_branch .LBBsrend" for ln in body):
+        body.append(".LBBsrend:")
     lines, in_marker = [], False
-    for ln in m.group(1).splitlines():
+    for ln in body:
         s = ln.strip()
         if s.startswith(";;#ASMSTART"):
             in_marker = True

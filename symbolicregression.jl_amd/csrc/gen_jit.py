@@ -140,7 +140,18 @@ def routine_list():
                     " const unsigned long long fl = __builtin_amdgcn_ballot_w64(!(qm <= dev::kTrigQMax));"
                     " s.s_flag = (unsigned)fl; s.s_flag_hi = (unsigned)(fl >> 32);")
             rs.append((f"u_{u.lower()}", body, True))
-        else:  # sin / cos: the whole range, large arguments by device_ops.h big_sincos_f32
+        elif u in ("SIN", "COS"):  # the whole range: one ballot for the rows, then big_sincos_f32
+            wc = 1 if u == "COS" else 0
+            body = (f"float v[R]; float qmax = 0.0f; "
+                    f"for (int r = 0; r < R; ++r) {{ float qa; v[r] = dev::fast_sincos_f32(s.a[r], {wc}, qa); "
+                    f"qmax = __builtin_fmaxf(qmax, qa); }} "
+                    f"if (__builtin_amdgcn_ballot_w64(!(qmax <= dev::kTrigQMax)) != 0) {{ "
+                    # one row at a time: the full reduction's registers are not multiplied by R
+                    f"for (int r = 0; r < R; ++r) if (__builtin_amdgcn_ballot_w64(dev::trig_big(s.a[r])) != 0) {{ "
+                    f"const float o = dev::big_sincos_f32(s.a[r], {wc}); v[r] = dev::trig_big(s.a[r]) ? o : v[r]; }} }} "
+                    f"for (int r = 0; r < R; ++r) s.a[r] = v[r];")
+            rs.append((f"u_{u.lower()}", body, False))
+        else:
             mk = "chk = mark(s.a[r], chk); " if u in LOSSY_UOPS else ""
             rs.append((f"u_{u.lower()}", rows(f"{mk}s.a[r] = dev::uop<SRHIP_UOP_{u}>(s.a[r]);"), False))
     for b in sorted(BOPS, key=lambda k: BOPS[k]):
@@ -149,6 +160,16 @@ def routine_list():
         mk = ("chk = mark(s.a[r], chk); " if b in LOSSY_LHS else "") + \
              ("chk = mark(s.b[r], chk); " if b in LOSSY_RHS else "")
         rs.append((f"b_{b.lower()}", rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], s.b[r]);"), False))
+    # constant-operand variants: the constant in SGPR s_k (no VGPR moves of a
+    # literal); the constant itself was checked at compile time, not marked
+    for b in sorted(BOPS, key=lambda k: BOPS[k]):
+        if b in INLINE_BOPS:
+            continue
+        imm = "const float imm = __int_as_float((int)s.s_k); "
+        mk = "chk = mark(s.a[r], chk); " if b in LOSSY_LHS else ""
+        rs.append((f"b_{b.lower()}_rc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], imm);"), False))
+        mk = "chk = mark(s.a[r], chk); " if b in LOSSY_RHS else ""
+        rs.append((f"b_{b.lower()}_lc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
     return rs
 
 
@@ -267,6 +288,10 @@ def build(hipcc, outdir, R):
         f.write("#define SR_JIT_BOP_ROUTINE {" + ", ".join(
             str(-1 if b_name.upper()[2:] in INLINE_BOPS else rid(b_name))
             for _, b_name in sorted(bop_rt.items())) + "}\n")
+        for suf in ("rc", "lc"):
+            f.write(f"#define SR_JIT_BOP_ROUTINE_{suf.upper()} {{" + ", ".join(
+                str(-1 if b_name.upper()[2:] in INLINE_BOPS else rid(f"{b_name}_{suf}"))
+                for _, b_name in sorted(bop_rt.items())) + "}\n")
         f.write(f"#define SR_JIT_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT_ROUTINE_TRIG {" + ", ".join("1" if n in trig else "0" for n in names) + "}\n")

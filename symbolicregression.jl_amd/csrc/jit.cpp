@@ -65,12 +65,15 @@ constexpr int VGT = SR_JIT_V_GT, VY = SR_JIT_V_Y, VPOOL0 = SR_JIT_V_POOL0, NPOOL
 constexpr int S_TILE = SR_JIT_S_TILE, S_NT = SR_JIT_S_NT, S_PARTIAL = SR_JIT_S_PARTIAL;
 constexpr int S_TILEBYTES = SR_JIT_S_TILEBYTES, S_WOFF = SR_JIT_S_WOFF, S_STATUS = SR_JIT_S_STATUS;
 constexpr int S_FLAG = SR_JIT_S_FLAG, S_RR = SR_JIT_S_RR, S_TGT = SR_JIT_S_TGT, S_RT = SR_JIT_S_RT;
-constexpr int S_MDELTA = SR_JIT_S_MDELTA, S_FASTOK = SR_JIT_S_FASTOK, S_EPS = SR_JIT_S_EPS;
+constexpr int S_FASTOK = SR_JIT_S_FASTOK, S_EPS = SR_JIT_S_EPS;
 constexpr int S_K = SR_JIT_S_K, S_PE = SR_JIT_S_PE, S_MODE = SR_JIT_S_MODE, S_X0 = SR_JIT_S_X0;
+constexpr int S_BASE = SR_JIT_S_X2;  // s[86:87]: base of the routine region in use (FAST or PRECISE)
 constexpr int TILE = 64 * R;
 constexpr int kNumRoutines = SR_JIT_NUM_ROUTINES;
 const int kUopRoutine[SRHIP_NUM_UOPS] = SR_JIT_UOP_ROUTINE;
 const int kBopRoutine[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE;
+const int kBopRoutineRC[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE_RC;  // rhs constant in s_k
+const int kBopRoutineLC[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE_LC;  // lhs constant in s_k
 const char* const kRoutineName[kNumRoutines] = SR_JIT_ROUTINE_NAMES;
 const int kRoutineTrig[kNumRoutines] = SR_JIT_ROUTINE_TRIG;
 
@@ -83,6 +86,7 @@ struct Tmpl {
   uint64_t area_va = 0;    // its address in the image
   uint64_t rt_va[kNumRoutines] = {};  // FAST routine addresses
   uint64_t delta = 0;      // PRECISE - FAST region offset
+  uint64_t fast0 = 0;      // FAST region start (sr_rt_fast)
   bool ok = false;
   std::string why;
 };
@@ -131,6 +135,7 @@ bool parse_tmpl(const uint8_t* img, size_t size, Tmpl* t) {
     if (prec_va[k] - t->rt_va[k] != prec0 - fast0) { t->why = "FAST / PRECISE routine layouts differ"; return false; }
   }
   t->delta = prec0 - fast0;
+  t->fast0 = fast0;
   const Elf64_Shdr* text = nullptr;
   for (auto& s : sh)
     if (s.sh_type == SHT_PROGBITS && (s.sh_flags & SHF_EXECINSTR) && code_va >= s.sh_addr &&
@@ -325,7 +330,7 @@ enum : int {
   VOP3_ADD_F32 = 0x101, VOP3_MIN_F32 = 0x10a, VOP3_MAX_F32 = 0x10b, VOP3_FMA_F32 = 0x1cb,
   VOPC_LT_F32 = 0x41, VOPC_LE_F32 = 0x43, VOPC_GT_F32 = 0x44, VOPC_U_F32 = 0x48, VOPC_GT_I32 = 0xc4,
   SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
-  SOP2_ADD_U32 = 0x00, SOP2_SUB_I32 = 0x03, SOP2_ADDC_U32 = 0x04, SOP2_CSELECT = 0x0a,
+  SOP2_ADD_U32 = 0x00, SOP2_SUB_U32 = 0x01, SOP2_SUB_I32 = 0x03, SOP2_SUBB_U32 = 0x05, SOP2_ADDC_U32 = 0x04, SOP2_CSELECT = 0x0a,
   SOPC_EQ_U32 = 0x06, SOPC_LG_U32 = 0x07, SOPC_GE_U32 = 0x09, SOPC_LT_U32 = 0x0a, SOPC_LG_U64 = 0x13,
   SOPP_BRANCH = 0x02, SOPP_SCC0 = 0x04, SOPP_SCC1 = 0x05, SOPP_VCCNZ = 0x07,
 };
@@ -342,6 +347,7 @@ struct IrOp {
   int op = 0;
   Opnd a, b;
   int rid = -1;      // routine, -1: inline
+  int krid = -1;     // constant-operand routine variant (constant in s_k), -1: none
   bool taint = false, zs = false;
   int consumer = -1, cpos = 0;
 };
@@ -425,7 +431,7 @@ struct Gen {
   std::vector<IrOp> ops;
   Opnd root;
   bool fast = false;    // this tree has a guarded FAST path
-  bool g_can = false, g_min = false, g_exp = false, has_trig = false;
+  bool g_can = false, g_min = false, g_exp = false, has_trig = false, has_call = false;
   // allocation state
   enum { L_NONE = -1, L_A = 100, L_B = 101 };
   std::vector<int> loc;          // per value
@@ -453,6 +459,10 @@ struct Gen {
       if (!is_inline(o)) {
         o.rid = o.un ? kUopRoutine[o.op] : kBopRoutine[o.op];
         if (o.rid < 0) { why = "operator without routine"; return false; }
+        has_call = true;
+        // a constant operand rides in s_k: the routine variant takes the other one in A
+        if (!o.un && o.b.k == O_C && o.a.k != O_C && kBopRoutineRC[o.op] >= 0) o.krid = kBopRoutineRC[o.op];
+        if (!o.un && o.a.k == O_C && o.b.k != O_C && kBopRoutineLC[o.op] >= 0) o.krid = kBopRoutineLC[o.op];
         if (kRoutineTrig[o.rid]) has_trig = true;
       }
       for (int s = 0; s < 2; ++s) {
@@ -581,17 +591,23 @@ struct Gen {
     return true;
   }
 
-  void call_routine(int rid) {
-    as.sop1(SOP1_GETPC, "s_getpc_b64", S_TGT, Src{0, false, 0}, "s[" + std::to_string(S_TGT) + ":" +
-                                                                          std::to_string(S_TGT + 1) + "]");
-    if (as.want_text) as.lines.back() = "s_getpc_b64 s[" + std::to_string(S_TGT) + ":" + std::to_string(S_TGT + 1) + "]";
-    // patch: s_getpc has no source operand (encoding field 0)
+  // s[86:87] = the FAST routine region (set once per tree entry); a PRECISE
+  // tile adds the region offset D to it, the next FAST tile takes it off
+  void set_base() {
+    as.sop1(SOP1_GETPC, "s_getpc_b64", S_BASE, Src{0, false, 0}, "");
+    if (as.want_text) as.lines.back() = "s_getpc_b64 s[" + std::to_string(S_BASE) + ":" + std::to_string(S_BASE + 1) + "]";
     const uint64_t pc_next = cur_va();
-    const int64_t rel = (int64_t)(T.rt_va[rid] - pc_next);
-    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TGT, S(S_TGT), K((uint32_t)(uint64_t)rel));
-    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_TGT + 1, S(S_TGT + 1), K((uint32_t)((uint64_t)rel >> 32)));
-    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TGT, S(S_TGT), S(S_MDELTA));
-    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_TGT + 1, S(S_TGT + 1), K(0));
+    const int64_t rel = (int64_t)(T.fast0 - pc_next);
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_BASE, S(S_BASE), K((uint32_t)(uint64_t)rel));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_BASE + 1, S(S_BASE + 1), K((uint32_t)((uint64_t)rel >> 32)));
+  }
+  void shift_base(bool up) {
+    as.sop2(up ? SOP2_ADD_U32 : SOP2_SUB_U32, up ? "s_add_u32" : "s_sub_u32", S_BASE, S(S_BASE), K((uint32_t)T.delta));
+    as.sop2(up ? SOP2_ADDC_U32 : SOP2_SUBB_U32, up ? "s_addc_u32" : "s_subb_u32", S_BASE + 1, S(S_BASE + 1), K(0));
+  }
+  void call_routine(int rid) {
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TGT, S(S_BASE), K((uint32_t)(T.rt_va[rid] - T.fast0)));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_TGT + 1, S(S_BASE + 1), K(0));
     as.sop1(SOP1_SWAPPC, "s_swappc_b64", S_RR, S(S_TGT), "s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "]");
     if (as.want_text)
       as.lines.back() = "s_swappc_b64 s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "], s[" +
@@ -605,11 +621,13 @@ struct Gen {
 
   bool emit_call(int i) {
     IrOp& o = ops[i];
+    if (o.krid >= 0) return emit_call_k(i);
     const int va_ = o.a.k == O_VAL ? o.a.v : -1;
     const int vb_ = (!o.un && o.b.k == O_VAL) ? o.b.v : -1;
     wait_for(o.a);
     if (!o.un) wait_for(o.b);
-    if (!evict(L_A, va_, vb_) || !evict(L_B, va_, vb_)) return false;
+    // routines keep B: a unary call leaves its owner there
+    if (!evict(L_A, va_, vb_) || (!o.un && !evict(L_B, va_, vb_))) return false;
     // move the operands into A (lhs) and B (rhs)
     auto srcs = [&](const Opnd& q, Src (&s)[R]) {
       for (int e = 0; e < R; ++e) s[e] = opsrc(q, e);
@@ -640,7 +658,8 @@ struct Gen {
     if (vb_ >= 0) release_val(vb_);
     if (o.a.k == O_X) release_x(o.a.v, i);
     if (!o.un && o.b.k == O_X) release_x(o.b.v, i);
-    a_owner = b_owner = -1;
+    a_owner = -1;
+    if (!o.un) b_owner = -1;
     if (fast && o.un && o.op == SRHIP_UOP_EXP)
       for (int e = 0; e < R; ++e) {
         const Src g = V(VGEXP), x = V(VA + e);
@@ -650,6 +669,33 @@ struct Gen {
     loc[i] = L_A;
     a_owner = i;
     if (fast && o.taint && o.zs && !o.un && o.op == SRHIP_BOP_DIV) guard_min(VA);
+    return true;
+  }
+
+  // a binary operator with one constant operand: the constant in s_k, the
+  // other operand in A, B untouched
+  bool emit_call_k(int i) {
+    IrOp& o = ops[i];
+    const bool kr = o.b.k == O_C;
+    const Opnd& q = kr ? o.a : o.b;
+    const int vq = q.k == O_VAL ? q.v : -1;
+    wait_for(q);
+    if (!evict(L_A, vq, -1)) return false;
+    const int lq = vq >= 0 ? loc[vq] : L_NONE;
+    if (lq != L_A) {
+      Src sq[R];
+      for (int e = 0; e < R; ++e) sq[e] = opsrc(q, e);
+      mov_block(VA, sq);
+    }
+    if (vq >= 0) release_val(vq);
+    if (q.k == O_X) release_x(q.v, i);
+    if (vq >= 0 && lq == L_B) b_owner = -1;
+    a_owner = -1;
+    as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(kr ? o.b.c : o.a.c), "s" + std::to_string(S_K));
+    call_routine(o.krid);
+    loc[i] = L_A;
+    a_owner = i;
+    if (fast && o.taint && o.zs && o.op == SRHIP_BOP_DIV) guard_min(VA);
     return true;
   }
 
@@ -700,7 +746,7 @@ struct Gen {
     // comes in between, else a freed or free pool block
     int dst = L_NONE;
     if (o.consumer >= 0 && ops[o.consumer].rid >= 0 && next_call[i + 1] == o.consumer) {
-      const bool lhs = o.cpos == 0;
+      const bool lhs = o.cpos == 0 || ops[o.consumer].krid >= 0;
       if (lhs && a_owner < 0) dst = L_A;
       if (!lhs && b_owner < 0) dst = L_B;
     }
@@ -765,13 +811,16 @@ struct Gen {
     // ---- prologue
     as.sop1(SOP1_MOV, "s_mov_b32", S_STATUS, K(0), "s" + std::to_string(S_STATUS));
     if (g_can) as.sop1(SOP1_MOV, "s_mov_b32", S_EPS, K(0x38800000u), "s" + std::to_string(S_EPS));  // 2^-14
+    if (has_call) set_base();
     if (fast) {
       as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_FASTOK), K(0));
       as.sop2(SOP2_CSELECT, "s_cselect_b32", S_MODE, K(1), K(0));
-      as.sop2(SOP2_CSELECT, "s_cselect_b32", S_MDELTA, K(D), K(0));
+      as.sop2(SOP2_CSELECT, "s_cselect_b32", S_K, K(D), K(0));
+      as.sop2(SOP2_ADD_U32, "s_add_u32", S_BASE, S(S_BASE), S(S_K));
+      as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_BASE + 1, S(S_BASE + 1), K(0));
     } else {
       as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(1), "s" + std::to_string(S_MODE));
-      as.sop1(SOP1_MOV, "s_mov_b32", S_MDELTA, K(D), "s" + std::to_string(S_MDELTA));
+      if (has_call) shift_base(true);
     }
     as.sopc(SOPC_GE_U32, "s_cmp_ge_u32", S(S_TILE), S(S_NT));
     as.branch(SOPP_SCC1, "s_cbranch_scc1", L_done);
@@ -833,25 +882,14 @@ struct Gen {
       }
       as.bind(L_skip);
     }
-    // ---- L2 loss of the tile (eval_kernel.h tile_loss order)
+    // ---- L2 loss of the tile: the residuals here, their squares in emit_tail
     for (int e = 0; e < R; ++e) as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", VY + e, V(rreg + e), VY + e);
-    for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VY + e), VY + e);
     return true;
   }
 
   // second half of the tile: weights (s_woff != 0), mask, sums, loop
-  void emit_tail() {
-    {
-      const int L_now = as.label();
-      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
-      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_now);
-      as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VGT, S(S_WOFF), VLANE);
-      as.ds_read_b128(VGT, VGT, 0);
-      as.waitcnt_lgkm(0);
-      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VGT + e), VY + e);
-      as.bind(L_now);
-    }
-    // the last, partial tile: rows past `partial` add 0
+  // the last, partial tile: rows past `partial` add 0 (block `reg` zeroed there)
+  void emit_mask(int reg) {
     const int L_nomask = as.label();
     as.sop2(SOP2_ADD_U32, "s_add_u32", S_PE, S(S_TILE), K(1));
     as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_PE), S(S_NT));
@@ -861,22 +899,49 @@ struct Gen {
     for (int e = 0; e < R; ++e) {
       as.sop2(SOP2_SUB_I32, "s_sub_i32", S_PE, S(S_PARTIAL), K((uint32_t)e));
       as.vopc(VOPC_GT_I32, "v_cmp_gt_i32_e32", S(S_PE), VLANE4);
-      as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", VY + e, K(0), VY + e, ", vcc");
+      as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", reg + e, K(0), reg + e, ", vcc");
     }
     as.bind(L_nomask);
-    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 2);
-    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY + 1, V(VY + 1), VY + 3);
-    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 1);
-    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VLSUM, V(VLSUM), VY);
+  }
+
+  // second half of the tile: squares (weighted when s_woff != 0), mask, sums, loop
+  void emit_tail() {
+    {
+      const int L_unw = as.label(), L_sum = as.label();
+      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
+      // weighted: w * r^2 per row (eval_kernel.h tile_loss), masked, then summed
+      as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VGT, S(S_WOFF), VLANE);
+      as.ds_read_b128(VGT, VGT, 0);
+      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VY + e), VY + e);
+      as.waitcnt_lgkm(0);
+      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VGT + e), VY + e);
+      emit_mask(VY);
+      as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 2);
+      as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY + 1, V(VY + 1), VY + 3);
+      as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 1);
+      as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VLSUM, V(VLSUM), VY);
+      as.branch(SOPP_BRANCH, "s_branch", L_sum);
+      // unweighted: the residuals masked, squared and accumulated by fma
+      as.bind(L_unw);
+      emit_mask(VY);
+      for (int e = 0; e < R; ++e) {
+        const Src r = V(VY + e), l = V(VLSUM);
+        as.vop3(VOP3_FMA_F32, "v_fma_f32", VLSUM, r, r, &l, 0, 0);
+      }
+      as.bind(L_sum);
+    }
     // a failed tile ends the tree
     as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
     as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
-    if (fast) {  // the next tile starts FAST again
+    if (fast) {  // after a redone tile, the next tile starts FAST again
       const int L_keep = as.label();
       as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_FASTOK), K(0));
       as.branch(SOPP_SCC1, "s_cbranch_scc1", L_keep);
+      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_MODE), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_keep);
       as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(0), "s" + std::to_string(S_MODE));
-      as.sop1(SOP1_MOV, "s_mov_b32", S_MDELTA, K(0), "s" + std::to_string(S_MDELTA));
+      shift_base(false);
       as.bind(L_keep);
     }
     as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VLANE, S(S_TILEBYTES), VLANE);
@@ -891,7 +956,7 @@ struct Gen {
       as.sop2(SOP2_ADD_U32, "s_add_u32", S_X0, S(S_X0), K(1));  // redo counter (driver output)
       as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHK, V(VCHKSAVE));
       as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(1), "s" + std::to_string(S_MODE));
-      as.sop1(SOP1_MOV, "s_mov_b32", S_MDELTA, K((uint32_t)T.delta), "s" + std::to_string(S_MDELTA));
+      shift_base(true);
       as.branch(SOPP_BRANCH, "s_branch", L_tile);
     }
     if (has_trig) {

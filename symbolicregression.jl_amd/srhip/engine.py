@@ -178,6 +178,12 @@ class Program:
                                            C.byref(ml)))
         return dict(ntrees=nt.value, nfast=nf.value, code_bytes=nb.value, ms_codegen=mc.value, ms_load=ml.value)
 
+    def update_stats(self):
+        """How set_constants applied new constants: {"inplace": n, "rebuilt": n}."""
+        a, b = C.c_int64(), C.c_int64()
+        check(lib().srhip_program_update_stats(self.handle, C.byref(a), C.byref(b)))
+        return dict(inplace=a.value, rebuilt=b.value)
+
     def set_constants(self, consts: np.ndarray):
         c = np.ascontiguousarray(consts, dtype=self.dtype)
         if c.shape != (int(self.flat.const_off[-1]),):

@@ -137,3 +137,57 @@ def test_engine_optimizer_random_population(gpu_ctx):
     m = np.isfinite(before)
     assert np.all(after[m] <= before[m] * (1 + 1e-4) + 1e-9)
     assert res.converged.any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T,n", [(np.float32, 600), (np.float64, 200)])
+def test_set_constants_in_place(gpu_ctx, T, n):
+    """srhip_program_set_constants overwrites the device programs' immediates
+    in place (same folding / static verdicts) and the losses, gradients and
+    did_succeed equal those of a program built from the new constants. A
+    tree-code program (600 Float32 trees, SRHIP_JIT=1) is rebuilt once and
+    runs interpreted from then on."""
+    import os
+    from srhip import constants as K
+
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(n, o, 5, T, seed=11)
+    rng = np.random.default_rng(12)
+    X = rng.standard_normal((5, 3001)).astype(T)
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(T)
+    ctx = gpu_ctx
+    ds = srhip.DeviceDataset(ctx, X, y)
+    flat = srhip.flatten(trees, o, dtype=T)
+    old = os.environ.get("SRHIP_JIT")
+    os.environ["SRHIP_JIT"] = "1"
+    try:
+        prog = srhip.Program(ctx, flat, T)
+        jit0 = prog.jit_info()["ntrees"]
+        prog.eval_loss_grad(ds, K.LOSS["L2"])  # gradient programs built
+        c0 = np.asarray(flat.consts, dtype=T)
+        for k in range(3):
+            c = (c0 * T(1 + 0.01 * (k + 1)) + T(0.001 * k)).astype(T)
+            prog.set_constants(c)
+            fresh_flat = srhip.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off, c, flat.nodes)
+            os.environ["SRHIP_JIT"] = "0"
+            fresh_i = srhip.Program(ctx, fresh_flat, T)
+            os.environ["SRHIP_JIT"] = "1"
+            s1, w1, ok1 = prog.eval_loss(ds, K.LOSS["L2"])
+            s2, w2, ok2 = fresh_i.eval_loss(ds, K.LOSS["L2"])
+            assert np.array_equal(ok1, ok2)
+            np.testing.assert_array_equal(s1[ok1], s2[ok2])
+            g1 = prog.eval_loss_grad(ds, K.LOSS["L2"])
+            g2 = fresh_i.eval_loss_grad(ds, K.LOSS["L2"])
+            for a, b in zip(g1, g2):
+                np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+        st = prog.update_stats()
+        assert prog.jit_info()["ntrees"] == 0
+        if jit0:
+            assert st["rebuilt"] == 1 and st["inplace"] == 2
+        else:
+            assert st["rebuilt"] == 0 and st["inplace"] == 3
+    finally:
+        if old is None:
+            os.environ.pop("SRHIP_JIT", None)
+        else:
+            os.environ["SRHIP_JIT"] = old
