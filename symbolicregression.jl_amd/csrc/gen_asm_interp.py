@@ -273,6 +273,9 @@ def extract(asm_text, name):
             if bad in s:
                 raise SystemExit(f"gen_asm_interp: handler {name} contains '{bad}': {s}")
         lines.append(s)
+    # a branch to the very next line (left where a trailing s_endpgm was) goes
+    lines = [s for k, s in enumerate(lines)
+             if not (s.startswith("s_branch ") and k + 1 < len(lines) and lines[k + 1] == s.split()[1] + ":")]
     # handler-local labels -> unique per handler (and per asm instance via %=)
     lbl = {}
     for s in lines:

@@ -27,6 +27,7 @@ Usage: gen_jit.py <hipcc> <outdir> [R]
 """
 import os
 import re
+import re
 import subprocess
 import sys
 import tempfile
@@ -151,6 +152,10 @@ def routine_list():
                     f"const float o = dev::big_sincos_f32(s.a[r], {wc}); v[r] = dev::trig_big(s.a[r]) ? o : v[r]; }} }} "
                     f"for (int r = 0; r < R; ++r) s.a[r] = v[r];")
             rs.append((f"u_{u.lower()}", body, False))
+            # the complete routine under another name: the hand-scheduled FAST
+            # body (manual_trig) branches to it when an argument needs more
+            # than the fast reduction
+            rs.append((f"u_{u.lower()}_full", body, False))
         else:
             mk = "chk = mark(s.a[r], chk); " if u in LOSSY_UOPS else ""
             rs.append((f"u_{u.lower()}", rows(f"{mk}s.a[r] = dev::uop<SRHIP_UOP_{u}>(s.a[r]);"), False))
@@ -171,6 +176,113 @@ def routine_list():
         mk = "chk = mark(s.a[r], chk); " if b in LOSSY_RHS else ""
         rs.append((f"b_{b.lower()}_lc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
     return rs
+
+
+def manual_trig(kind):
+    """FAST sin / cos for the 4 rows of A, hand-scheduled: the same operations
+    (bit for bit) as hipcc's code for dev::fast_sincos_f32 — reduction by pi
+    (three-part pi/2), odd polynomial, sign from the parity of n — with the
+    two row pairs interleaved on packed f32 instructions, n rounded with the
+    1.5*2^23 shift (its low mantissa bit is n's parity) and no s_nop. Any
+    |t| > kTrigQMax (before rounding: a superset of the rows the full
+    routine treats specially) branches to the full routine, which starts
+    over from A (untouched until the last instructions)."""
+    cos = kind == "cos"
+    L = ["s_mov_b32 s0, 0x3ea2f983", "s_mov_b32 s20, 0x4702dc00"]  # 1/pi, kTrigQMax = 33500
+    if cos:  # t = x/pi - 1/2
+        L += ["v_pk_fma_f32 v[0:1], v[32:33], s[0:1], -0.5 op_sel_hi:[1,0,0]",
+              "v_pk_fma_f32 v[2:3], v[34:35], s[0:1], -0.5 op_sel_hi:[1,0,0]"]
+    else:    # t = x/pi
+        L += ["v_pk_mul_f32 v[0:1], v[32:33], s[0:1] op_sel_hi:[1,0]",
+              "v_pk_mul_f32 v[2:3], v[34:35], s[0:1] op_sel_hi:[1,0]"]
+    L += ["s_mov_b32 s2, 0x4b400000",                       # 1.5 * 2^23
+          "v_max3_f32 v24, |v0|, |v1|, |v2|",
+          "v_max_f32_e64 v24, v24, |v3|",
+          "v_cmp_lt_f32_e32 vcc, s20, v24",
+          "s_mov_b32 s4, 0xcb400000",
+          "v_pk_add_f32 v[4:5], v[0:1], s[2:3] op_sel_hi:[1,0]",   # t + 1.5*2^23: n in the low bits
+          "v_pk_add_f32 v[6:7], v[2:3], s[2:3] op_sel_hi:[1,0]",
+          "s_cbranch_vccnz @FULL@",
+          "v_pk_add_f32 v[8:9], v[4:5], s[4:5] op_sel_hi:[1,0]",   # n = rint(t)
+          "v_pk_add_f32 v[10:11], v[6:7], s[4:5] op_sel_hi:[1,0]",
+          "s_mov_b32 s6, 0xbfc90fd8"]
+    if cos:  # m = 2n + 1
+        L += ["v_pk_fma_f32 v[8:9], v[8:9], 2.0, 1.0 op_sel_hi:[1,0,0]",
+              "v_pk_fma_f32 v[10:11], v[10:11], 2.0, 1.0 op_sel_hi:[1,0,0]"]
+    else:    # m = 2n
+        L += ["v_pk_add_f32 v[8:9], v[8:9], v[8:9]",
+              "v_pk_add_f32 v[10:11], v[10:11], v[10:11]"]
+    L += ["s_mov_b32 s8, 0xb4a8885a",
+          "v_pk_fma_f32 v[12:13], v[8:9], s[6:7], v[32:33] op_sel_hi:[1,0,1]",   # r = x - m*pi/2 (3 parts)
+          "v_pk_fma_f32 v[14:15], v[10:11], s[6:7], v[34:35] op_sel_hi:[1,0,1]",
+          "s_mov_b32 s10, 0xa7c234c4",
+          "v_pk_fma_f32 v[12:13], v[8:9], s[8:9], v[12:13] op_sel_hi:[1,0,1]",
+          "v_pk_fma_f32 v[14:15], v[10:11], s[8:9], v[14:15] op_sel_hi:[1,0,1]",
+          "s_mov_b32 s12, 0x362ee8a0",
+          "v_pk_fma_f32 v[12:13], v[8:9], s[10:11], v[12:13] op_sel_hi:[1,0,1]",
+          "v_pk_fma_f32 v[14:15], v[10:11], s[10:11], v[14:15] op_sel_hi:[1,0,1]",
+          "v_mov_b32_e32 v28, 0xb94fb8ba",
+          "v_pk_mul_f32 v[16:17], v[12:13], v[12:13]",                          # s = r^2
+          "v_pk_mul_f32 v[18:19], v[14:15], v[14:15]",
+          "s_mov_b32 s16, 0x3c08876e",
+          "v_pk_fma_f32 v[20:21], v[16:17], s[12:13], v[28:29] op_sel_hi:[1,0,0]",
+          "v_pk_fma_f32 v[22:23], v[18:19], s[12:13], v[28:29] op_sel_hi:[1,0,0]",
+          "s_mov_b32 s18, 0xbe2aaaa6",
+          "v_pk_fma_f32 v[20:21], v[20:21], v[16:17], s[16:17] op_sel_hi:[1,1,0]",
+          "v_pk_fma_f32 v[22:23], v[22:23], v[18:19], s[16:17] op_sel_hi:[1,1,0]",
+          "v_lshlrev_b32_e32 v24, 31, v4",                                     # (-1)^n
+          "v_pk_fma_f32 v[20:21], v[20:21], v[16:17], s[18:19] op_sel_hi:[1,1,0]",
+          "v_pk_fma_f32 v[22:23], v[22:23], v[18:19], s[18:19] op_sel_hi:[1,1,0]",
+          "v_lshlrev_b32_e32 v25, 31, v5",
+          "v_pk_mul_f32 v[20:21], v[16:17], v[20:21]",
+          "v_pk_mul_f32 v[22:23], v[18:19], v[22:23]",
+          "v_lshlrev_b32_e32 v26, 31, v6"]
+    neg = " neg_lo:[0,1,1] neg_hi:[0,1,1]" if cos else ""
+    L += [f"v_pk_fma_f32 v[20:21], v[20:21], v[12:13], v[12:13]{neg}",
+          f"v_pk_fma_f32 v[22:23], v[22:23], v[14:15], v[14:15]{neg}",
+          "v_lshlrev_b32_e32 v27, 31, v7",
+          "v_xor_b32_e32 v32, v24, v20",
+          "v_xor_b32_e32 v33, v25, v21",
+          "v_xor_b32_e32 v34, v26, v22",
+          "v_xor_b32_e32 v35, v27, v23"]
+    return L
+
+
+def manual_div_rk(rg):
+    """a / c for a constant divisor c (s_k) through its correctly rounded
+    reciprocal y = RN(1/c) (s_x1, computed by the host): q = a*y,
+    r = fma(-c, q, a), q' = fma(r, y, q) — the IEEE quotient whenever |a| and
+    |c| lie in [2^-60, 2^60] (tools/check_div_const.c: 1.7e10 quotients, no
+    mismatch; the host only uses this routine for such c). A row outside
+    that range (0, Inf, NaN, extreme exponents) sends all four to the IEEE
+    routine b_div_rc."""
+    k, y = rg.S["k"], rg.S["x1"]
+    return ["v_max3_f32 v0, |v32|, |v33|, |v34|",
+            "v_min3_f32 v1, |v32|, |v33|, |v34|",
+            "s_mov_b32 s0, 0x5d800000",           # 2^60
+            "v_max_f32_e64 v0, v0, |v35|",
+            "v_min_f32_e64 v1, v1, |v35|",
+            "s_mov_b32 s1, 0x21800000",           # 2^-60
+            "v_cmp_gt_f32_e64 s[2:3], s0, v0",
+            "v_cmp_lt_f32_e64 s[4:5], s1, v1",
+            "s_and_b64 s[2:3], s[2:3], s[4:5]",
+            "s_andn2_b64 s[2:3], exec, s[2:3]",
+            "s_cbranch_scc1 .Lsrdk_fb_%=",
+            f"v_mul_f32_e32 v4, s{y}, v32",
+            f"v_mul_f32_e32 v5, s{y}, v33",
+            f"v_mul_f32_e32 v6, s{y}, v34",
+            f"v_mul_f32_e32 v7, s{y}, v35",
+            f"v_fma_f32 v8, -s{k}, v4, v32",
+            f"v_fma_f32 v9, -s{k}, v5, v33",
+            f"v_fma_f32 v10, -s{k}, v6, v34",
+            f"v_fma_f32 v11, -s{k}, v7, v35",
+            f"v_fma_f32 v32, v8, s{y}, v4",
+            f"v_fma_f32 v33, v9, s{y}, v5",
+            f"v_fma_f32 v34, v10, s{y}, v6",
+            f"v_fma_f32 v35, v11, s{y}, v7",
+            f"s_setpc_b64 s[{rg.S['rr']}:{rg.S['rr'] + 1}]",
+            ".Lsrdk_fb_%=:",
+            "s_branch @DIVRC@"]
 
 
 def compile_bodies(hipcc, rg, routines, extra):
@@ -213,6 +325,15 @@ def build(hipcc, outdir, R):
     fast = compile_bodies(hipcc, rg, routines, ["-DSR_PRECISE_TRANSC=0"])
     prec = compile_bodies(hipcc, rg, routines, [])
     names = [n for n, _, _ in routines if n in fast and n in prec]
+    manual = set()
+    if "b_div_rc" in names:  # hand-written, the same in both regions (IEEE exact)
+        fast["b_div_rk"] = prec["b_div_rk"] = manual_div_rk(rg)
+        names.insert(names.index("b_div_rc") + 1, "b_div_rk")
+    if os.environ.get("SR_JIT_MANUAL_TRIG", "1") != "0":
+        for k in ("sin", "cos"):
+            if f"u_{k}_full" in names:
+                fast[f"u_{k}"] = manual_trig(k)
+                manual.add(f"u_{k}")
     trig = {n for n, _, t in routines if t}
     vstate = set(range(rg.A, rg.VEND))
     sstate = {r for _, r in rg.sregs()}
@@ -239,8 +360,13 @@ def build(hipcc, outdir, R):
 
     fb = {n: with_ret(fast[n], n, "f") for n in names}
     pb = {n: with_ret(prec[n], n, "p") for n in names}
-    fs = label_sizes(fb, names)
-    ps = label_sizes(pb, names)
+    def sized(bodies):
+        return {n: [l.replace("@FULL@", f".Lsr_start_{n}_full_%=").replace("@DIVRC@", ".Lsr_start_b_div_rc_%=")
+                    for l in b] for n, b in bodies.items()}
+    fs, ps = label_sizes(sized(fb), names), label_sizes(sized(pb), names)
+    fb = {n: [l.replace("@FULL@", f".Lsrent_fast_{n}_full").replace("@DIVRC@", ".Lsrent_fast_b_div_rc")
+              for l in b] for n, b in fb.items()}
+    pb = {n: [l.replace("@DIVRC@", ".Lsrent_prec_b_div_rc") for l in b] for n, b in pb.items()}
     slot = {n: (max(fs[n], ps[n]) + 63) // 64 * 64 for n in names}
     text = ["s_endpgm"]
     for region, bodies, sizes in (("fast", fb, fs), ("prec", pb, ps)):
@@ -250,6 +376,7 @@ def build(hipcc, outdir, R):
         for n in names:
             text.append(f".globl sr_rt_{region}_{n}")
             text.append(f"sr_rt_{region}_{n}:")
+            text.append(f".Lsrent_{region}_{n}:")  # local entry label (branch target)
             text += bodies[n]
             pad = slot[n] - sizes[n]
             assert pad % 4 == 0
@@ -295,6 +422,14 @@ def build(hipcc, outdir, R):
         f.write(f"#define SR_JIT_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT_ROUTINE_TRIG {" + ", ".join("1" if n in trig else "0" for n in names) + "}\n")
+        # routines whose FAST and PRECISE bodies are the same code (labels aside)
+        # and small: tree code may copy them in place of a call (jit.cpp)
+        def norm(lines):
+            return [re.sub(r"_[fp]\b", "", l) for l in lines]
+        inl = [n for n in names if norm(fb[n]) == norm(pb[n]) and fs[n] <= 512 and
+               not any(k in l for l in fb[n][:-1] for k in ("s_getpc", "s_setpc", "s_swappc", "s_endpgm"))]
+        f.write("#define SR_JIT_ROUTINE_INLINE {" + ", ".join("1" if n in inl else "0" for n in names) + "}\n")
+        f.write("#define SR_JIT_ROUTINE_BODY_BYTES {" + ", ".join(str(fs[n] - 4) for n in names) + "}\n")
         f.write("#define SR_JIT_CLOBBERS " + ", ".join([f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s]
                                                           + ['"vcc"', '"scc"', '"m0"']) + "\n")
         f.write(f"// routine VGPR temps v{min(vtemp)}..v{max(vtemp)}, SGPR temps {sorted(stemp)}\n")

@@ -31,6 +31,7 @@
 
 #include <algorithm>
 #include <chrono>
+#include <cmath>
 #include <cstdarg>
 #include <cstdio>
 #include <cstdlib>
@@ -67,7 +68,8 @@ constexpr int S_TILEBYTES = SR_JIT_S_TILEBYTES, S_WOFF = SR_JIT_S_WOFF, S_STATUS
 constexpr int S_FLAG = SR_JIT_S_FLAG, S_RR = SR_JIT_S_RR, S_TGT = SR_JIT_S_TGT, S_RT = SR_JIT_S_RT;
 constexpr int S_FASTOK = SR_JIT_S_FASTOK, S_EPS = SR_JIT_S_EPS;
 constexpr int S_K = SR_JIT_S_K, S_PE = SR_JIT_S_PE, S_MODE = SR_JIT_S_MODE, S_X0 = SR_JIT_S_X0;
-constexpr int S_BASE = SR_JIT_S_X2;  // s[86:87]: base of the routine region in use (FAST or PRECISE)
+constexpr int S_BASE = SR_JIT_S_X2;
+constexpr int S_RECIP = SR_JIT_S_X1;  // RN(1/c) of a constant divisor (routine b_div_rk)  // s[86:87]: base of the routine region in use (FAST or PRECISE)
 constexpr int TILE = 64 * R;
 constexpr int kNumRoutines = SR_JIT_NUM_ROUTINES;
 const int kUopRoutine[SRHIP_NUM_UOPS] = SR_JIT_UOP_ROUTINE;
@@ -76,6 +78,8 @@ const int kBopRoutineRC[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE_RC;  // rhs constan
 const int kBopRoutineLC[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE_LC;  // lhs constant in s_k
 const char* const kRoutineName[kNumRoutines] = SR_JIT_ROUTINE_NAMES;
 const int kRoutineTrig[kNumRoutines] = SR_JIT_ROUTINE_TRIG;
+const int kRoutineInline[kNumRoutines] = SR_JIT_ROUTINE_INLINE;        // same FAST / PRECISE code, small
+const int kRoutineBodyBytes[kNumRoutines] = SR_JIT_ROUTINE_BODY_BYTES;  // up to the return
 
 // ---- the code-object template ---------------------------------------------------
 struct Tmpl {
@@ -87,6 +91,7 @@ struct Tmpl {
   uint64_t rt_va[kNumRoutines] = {};  // FAST routine addresses
   uint64_t delta = 0;      // PRECISE - FAST region offset
   uint64_t fast0 = 0;      // FAST region start (sr_rt_fast)
+  std::vector<uint32_t> body[kNumRoutines];  // inlinable routine bodies (without the return)
   bool ok = false;
   std::string why;
 };
@@ -143,6 +148,18 @@ bool parse_tmpl(const uint8_t* img, size_t size, Tmpl* t) {
       text = &s;
   if (!text) { t->why = "code area outside .text"; return false; }
   t->area_va = code_va;
+  for (int k = 0; k < kNumRoutines; ++k) {
+    if (!kRoutineInline[k]) continue;
+    const uint64_t va = t->rt_va[k];
+    const size_t nb = (size_t)kRoutineBodyBytes[k];
+    if (va < text->sh_addr || va + nb + 4 > text->sh_addr + text->sh_size || nb % 4) continue;
+    const size_t off = (size_t)(va - text->sh_addr + text->sh_offset);
+    uint32_t ret;
+    std::memcpy(&ret, img + off + nb, 4);
+    if (ret != (0xbe801d00u | (uint32_t)S_RR)) { t->why = "routine body does not end in its return"; return false; }
+    t->body[k].resize(nb / 4);
+    std::memcpy(t->body[k].data(), img + off, nb);
+  }
   t->area_off = (size_t)(code_va - text->sh_addr + text->sh_offset);
   // the area function: s_endpgm, the area, the compiler's closing s_endpgm
   const uint64_t end = area_fn_va + area_fn_size;
@@ -263,6 +280,10 @@ struct Asm {
   void sopp(int op, const char* nm, int imm, bool show = true) {
     put(0xbf800000u | ((uint32_t)op << 16) | ((uint32_t)imm & 0xffffu));
     if (want_text) t(show ? std::string(nm) + " " + std::to_string(imm) : std::string(nm));
+  }
+  void raw(uint32_t x) {
+    put(x);
+    if (want_text) t(".long " + hex32(x));
   }
   void branch(int op, const char* nm, int l) {
     fix.push_back({w.size(), l, want_text ? lines.size() : 0});
@@ -446,7 +467,30 @@ struct Gen {
   int L_tile = -1, L_done = -1, L_redo = -1, L_bail = -1;
   std::string why;
 
-  Gen(Asm& a, const Tmpl& t, uint64_t va, bool f) : as(a), T(t), base_va(va), fast_opt(f) {}
+  // SRHIP_JIT_TRIG_FULL=1 (tests): sin / cos through the complete compiled
+  // routines instead of the hand-scheduled FAST bodies
+  bool trig_full = false;
+  static int div_rk() {
+    static const int r = [] {
+      for (int k = 0; k < kNumRoutines; ++k)
+        if (std::string(kRoutineName[k]) == "b_div_rk") return k;
+      return -1;
+    }();
+    return r;
+  }
+  static int full_routine(int rid) {
+    const std::string want = std::string(kRoutineName[rid]) + "_full";
+    for (int k = 0; k < kNumRoutines; ++k)
+      if (want == kRoutineName[k]) return k;
+    return rid;
+  }
+  bool inline_ok = false;  // copy mode-independent small routines into the tree code
+  Gen(Asm& a, const Tmpl& t, uint64_t va, bool f) : as(a), T(t), base_va(va), fast_opt(f) {
+    const char* e = std::getenv("SRHIP_JIT_INLINE");  // measured no faster: off by default
+    inline_ok = e && e[0] == '1';
+    const char* tf = std::getenv("SRHIP_JIT_TRIG_FULL");
+    trig_full = tf && tf[0] == '1';
+  }
 
   uint64_t cur_va() const { return base_va + as.bytes(); }
   int reg_of_loc(int l) const { return l == L_A ? VA : l == L_B ? VB : VPOOL0 + R * l; }
@@ -459,6 +503,7 @@ struct Gen {
       if (!is_inline(o)) {
         o.rid = o.un ? kUopRoutine[o.op] : kBopRoutine[o.op];
         if (o.rid < 0) { why = "operator without routine"; return false; }
+        if (trig_full && o.un && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS)) o.rid = full_routine(o.rid);
         has_call = true;
         // a constant operand rides in s_k: the routine variant takes the other one in A
         if (!o.un && o.b.k == O_C && o.a.k != O_C && kBopRoutineRC[o.op] >= 0) o.krid = kBopRoutineRC[o.op];
@@ -606,6 +651,11 @@ struct Gen {
     as.sop2(up ? SOP2_ADDC_U32 : SOP2_SUBB_U32, up ? "s_addc_u32" : "s_subb_u32", S_BASE + 1, S(S_BASE + 1), K(0));
   }
   void call_routine(int rid) {
+    if (inline_ok && !T.body[rid].empty()) {  // a copy of the body instead of the call
+      for (uint32_t w : T.body[rid]) as.raw(w);
+      as.sopp(0x00, "s_nop", 0);  // a trans result read right after the body
+      return;
+    }
     as.sop2(SOP2_ADD_U32, "s_add_u32", S_TGT, S(S_BASE), K((uint32_t)(T.rt_va[rid] - T.fast0)));
     as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_TGT + 1, S(S_BASE + 1), K(0));
     as.sop1(SOP1_SWAPPC, "s_swappc_b64", S_RR, S(S_TGT), "s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "]");
@@ -691,8 +741,22 @@ struct Gen {
     if (q.k == O_X) release_x(q.v, i);
     if (vq >= 0 && lq == L_B) b_owner = -1;
     a_owner = -1;
-    as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(kr ? o.b.c : o.a.c), "s" + std::to_string(S_K));
-    call_routine(o.krid);
+    const uint32_t cb = kr ? o.b.c : o.a.c;
+    as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(cb), "s" + std::to_string(S_K));
+    int rid = o.krid;
+    float cf;
+    std::memcpy(&cf, &cb, 4);
+    const float ac = std::fabs(cf);
+    if (kr && o.op == SRHIP_BOP_DIV && div_rk() >= 0 && ac >= 0x1p-60f && ac <= 0x1p60f) {
+      // the reciprocal-and-correction routine (IEEE exact for admitted a; gen_jit.py manual_div_rk)
+      const volatile float one = 1.0f;
+      const float y = one / cf;  // correctly rounded (SSE division, no contraction)
+      uint32_t yb;
+      std::memcpy(&yb, &y, 4);
+      as.sop1(SOP1_MOV, "s_mov_b32", S_RECIP, K(yb), "s" + std::to_string(S_RECIP));
+      rid = div_rk();
+    }
+    call_routine(rid);
     loc[i] = L_A;
     a_owner = i;
     if (fast && o.taint && o.zs && o.op == SRHIP_BOP_DIV) guard_min(VA);
@@ -899,6 +963,7 @@ struct Gen {
     for (int e = 0; e < R; ++e) {
       as.sop2(SOP2_SUB_I32, "s_sub_i32", S_PE, S(S_PARTIAL), K((uint32_t)e));
       as.vopc(VOPC_GT_I32, "v_cmp_gt_i32_e32", S(S_PE), VLANE4);
+      as.sopp(0x00, "s_nop", 1);  // VALU-written VCC read as a VALU mask: 2 wait states
       as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", reg + e, K(0), reg + e, ", vcc");
     }
     as.bind(L_nomask);
@@ -1142,8 +1207,10 @@ hipError_t launch(Module* m, const EvalPlan& plan, const EvalArgs<float>& a, boo
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
+  // SRHIP_JIT_LDS_PAD (experiments): extra LDS per workgroup, i.e. fewer resident waves
+  static const unsigned pad = [] { const char* e = std::getenv("SRHIP_JIT_LDS_PAD"); return e ? (unsigned)std::atoi(e) : 0u; }();
   return hipModuleLaunchKernel(a.w ? m->fn_w : m->fn, grid, 1, 1, (unsigned)plan.threads, 1, 1,
-                               (unsigned)plan.lds_bytes, stream, nullptr, cfg);
+                               (unsigned)plan.lds_bytes + pad, stream, nullptr, cfg);
 }
 
 }  // namespace jit

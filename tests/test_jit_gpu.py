@@ -171,3 +171,53 @@ def test_large_argument_sin_cos_correctly_rounded(gpu_ctx, op):
     s_j, w_j, ok_j, info, bailed = run([tree] * 600, o, X, ref, jit="1", fast="1")
     assert info["ntrees"] == 600 and bailed == 0 and ok_j.all()
     assert np.all(s_j <= 2e-12 * n), s_j.max()
+
+
+def test_hand_scheduled_trig_equals_compiled(gpu_ctx):
+    """The hand-scheduled FAST sin/cos bodies (gen_jit.py manual_trig) compute
+    bit for bit what hipcc's code for the same routine computes
+    (SRHIP_JIT_TRIG_FULL=1 routes every sin/cos through the compiled one)."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["sin", "cos", "exp"])
+    trees = srhip.random_population(1500, o, 5, np.float32, seed=21)
+    rng = np.random.default_rng(22)
+    X = (rng.standard_normal((5, 40_000)) * rng.choice([1.0, 30.0, 3000.0], (5, 40_000))).astype(np.float32)
+    y = (np.float32(2) * np.cos(X[3]) + X[0] * X[0] - np.float32(2)).astype(np.float32)
+    s_m, w_m, ok_m, info_m, _ = run(trees, o, X, y, jit="1", fast="1")
+    with env(SRHIP_JIT_TRIG_FULL="1"):
+        s_f, w_f, ok_f, info_f, _ = run(trees, o, X, y, jit="1", fast="1")
+    assert info_m["ntrees"] == info_f["ntrees"] > 1000 and info_m["nfast"] > 500
+    assert np.array_equal(ok_m, ok_f)
+    assert np.array_equal(s_m[ok_m], s_f[ok_f])
+
+
+@pytest.mark.parametrize("fast", ["0", "1"])
+def test_constant_divisor_is_ieee_exact(gpu_ctx, fast):
+    """x0 / c through the reciprocal routine (admitted |c|) or the IEEE one:
+    every row equals numpy's Float32 quotient bit for bit — the tree
+    (x0 / c_j) - x_j, with x_j = x0 / c_j precomputed, has loss exactly 0."""
+    rng = np.random.default_rng(31)
+    n, F = 20_000, 41
+    a = (rng.uniform(1, 2, n) * np.exp2(rng.integers(-60, 61, n))).astype(np.float32)
+    a *= rng.choice([-1, 1], n).astype(np.float32)
+    a[:50] = 0
+    a[50:100] = np.float32(2.0 ** -59)
+    for rep in range(6):
+        e = rng.integers(-62, 63, F - 1)
+        c = (rng.uniform(1, 2, F - 1) * np.exp2(e) * rng.choice([-1, 1], F - 1)).astype(np.float32)
+        if rep == 0:
+            c[:8] = np.float32([3, 7, 0.1, -1.7, float.fromhex("0x1.fffffep0"), 2.0 ** 60, 2.0 ** -60,
+                                float.fromhex("0x1.000002p0")])
+        X = np.empty((F, n), np.float32)
+        X[0] = a
+        with np.errstate(all="ignore"):
+            X[1:] = a[None, :] / c[:, None]
+        m = np.isfinite(X).all(axis=0) & (np.abs(X[1:]) < np.float32(1e37)).all(axis=0)
+        X = X[:, m]
+        o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+        trees = [o.make_binary("-", o.make_binary("/", srhip.Node(feature=1), srhip.Node(val=np.float32(cj))),
+                               srhip.Node(feature=j + 2)) for j, cj in enumerate(c)]
+        y = np.zeros(X.shape[1], np.float32)
+        s, w, ok, info, _ = run(trees, o, X, y, jit="1", fast=fast)
+        assert info["ntrees"] == len(trees) and ok.all()
+        bad = np.flatnonzero(s != 0)
+        assert bad.size == 0, (c[bad[:5]], s[bad[:5]])

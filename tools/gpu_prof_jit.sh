@@ -1,12 +1,21 @@
 #!/bin/bash
-# rocprofv3 passes over tools/prof_target.py (MODE=jit|interp|jit-precise)
+# rocprofv3 passes over tools/prof_target.py (MODE=jit|interp|jit-precise):
+# a kernel trace of 20 warm evaluations, then PMC passes (one run each).
 cd "$GRAFT_REPO_ROOT"
 export TMPDIR=/tmp
 OUT=gpurun_out/prof_${TAG:-jit}
 mkdir -p $OUT
 export MODE=${MODE:-jit}
-timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 tools/prof_target.py 10 > $OUT/log.txt 2>&1 || exit $?
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_BRANCH --output-format csv -d $OUT/pmc1 -o pmc1 -- python3 tools/prof_target.py 3 >> $OUT/log.txt 2>&1 || exit $?
-timeout -s KILL 90 rocprofv3 --pmc SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE GRBM_GUI_ACTIVE --output-format csv -d $OUT/pmc2 -o pmc2 -- python3 tools/prof_target.py 3 >> $OUT/log.txt 2>&1 || exit $?
-timeout -s KILL 90 rocprofv3 --pmc SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_IFETCH SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INST_CYCLES_SALU --output-format csv -d $OUT/pmc3 -o pmc3 -- python3 tools/prof_target.py 3 >> $OUT/log.txt 2>&1 || exit $?
-find $OUT -name "*.csv" | head -20
+timeout -k 10 120 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- python3 tools/prof_target.py 20 > $OUT/log.txt 2>&1 || exit $?
+P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_BRANCH"
+P2="SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_IFETCH SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES"
+P3="SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_LEVEL_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F32"
+P4="SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE GRBM_GUI_ACTIVE"
+P5="FETCH_SIZE"
+P6="WRITE_SIZE"
+i=0
+for P in "$P1" "$P2" "$P3" "$P4" "$P5" "$P6"; do
+  i=$((i+1))
+  timeout -s KILL 90 rocprofv3 --pmc $P --output-format csv -d $OUT/pmc$i -o pmc$i -- python3 tools/prof_target.py 3 >> $OUT/log.txt 2>&1 || exit $?
+done
+python3 tools/pmc_summary.py $OUT > $OUT/summary.json && cat $OUT/summary.json

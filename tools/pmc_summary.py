@@ -1,0 +1,42 @@
+"""Per-dispatch averages of the PMC passes of tools/gpu_prof_jit.sh for the
+tree-code kernel (sr_jit_eval*) or the interpreter's eval kernel, plus the
+kernel trace's average duration, and the derived ratios DESIGN.md quotes."""
+import csv
+import glob
+import json
+import os
+import sys
+from collections import defaultdict
+
+out = sys.argv[1]
+want = os.environ.get("KERNEL", "sr_jit_eval")
+vals = defaultdict(list)
+for f in glob.glob(os.path.join(out, "pmc*", "*counter_collection.csv")):
+    per = defaultdict(lambda: defaultdict(float))
+    for r in csv.DictReader(open(f)):
+        if want in r["Kernel_Name"]:
+            per[r["Dispatch_Id"]][r["Counter_Name"]] += float(r["Counter_Value"])
+    for d in per.values():
+        for k, v in d.items():
+            vals[k].append(v)
+avg = {k: sum(v) / len(v) for k, v in vals.items()}
+kt = glob.glob(os.path.join(out, "kt", "*kernel_stats.csv"))
+dur = None
+if kt:
+    for r in csv.DictReader(open(kt[0])):
+        if want in r["Name"]:
+            dur = float(r["AverageNs"]) / 1e6
+res = {"kernel": want, "avg_ms_kernel_trace": dur, "counters_per_dispatch": avg}
+if "SQ_WAVE_CYCLES" in avg:
+    wc = avg["SQ_WAVE_CYCLES"]
+    for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS",
+              "SQ_ACTIVE_INST_SCA", "SQ_ACTIVE_INST_MISC", "SQ_ACTIVE_INST_VALU"):
+        if k in avg:
+            res[f"{k}/WAVE_CYCLES"] = avg[k] / wc
+if "GRBM_GUI_ACTIVE" in avg and "SQ_INSTS_VALU" in avg:
+    cyc = avg["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs
+    res["gpu_cycles"] = cyc
+    res["valu_busy_2cyc"] = avg["SQ_INSTS_VALU"] * 2 / (cyc * 1024)
+if "FETCH_SIZE" in avg:
+    res["hbm_bytes"] = (avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0)) * 1024
+print(json.dumps(res, indent=1))
