@@ -69,8 +69,8 @@ def cpu_note() -> str:
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--ntrees", type=int, default=4096)
     ap.add_argument("--rows", type=int, default=1_000_000)
     ap.add_argument("--nfeat", type=int, default=5)

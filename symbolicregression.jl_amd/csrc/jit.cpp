@@ -349,6 +349,7 @@ enum : int {
   VOP2_MIN_F32 = 0x0a, VOP2_MAX_F32 = 0x0b, VOP2_AND_B32 = 0x13, VOP2_XOR_B32 = 0x15, VOP2_ADD_U32 = 0x34,
   VOP1_MOV = 0x01,
   VOP3_ADD_F32 = 0x101, VOP3_MIN_F32 = 0x10a, VOP3_MAX_F32 = 0x10b, VOP3_FMA_F32 = 0x1cb,
+  VOP3_MIN3_F32 = 0x1d0, VOP3_MAX3_F32 = 0x1d3,
   VOPC_LT_F32 = 0x41, VOPC_LE_F32 = 0x43, VOPC_GT_F32 = 0x44, VOPC_U_F32 = 0x48, VOPC_GT_I32 = 0xc4,
   SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
   SOP2_ADD_U32 = 0x00, SOP2_SUB_U32 = 0x01, SOP2_SUB_I32 = 0x03, SOP2_SUBB_U32 = 0x05, SOP2_ADDC_U32 = 0x04, SOP2_CSELECT = 0x0a,
@@ -460,6 +461,8 @@ struct Gen {
   int a_owner = -1, b_owner = -1;
   int xblk[256];
   int xlast[256];
+  bool xinl[256];                // feature read by an inline operator or as the root
+  bool xdirect = false;          // call operands that are features: ds_read straight into A / B
   std::vector<int> feats;        // features in first-use order
   int load_idx[256];             // load number (0 = y)
   int nloads = 0, waited = 0;
@@ -488,6 +491,8 @@ struct Gen {
   Gen(Asm& a, const Tmpl& t, uint64_t va, bool f) : as(a), T(t), base_va(va), fast_opt(f) {
     const char* e = std::getenv("SRHIP_JIT_INLINE");  // measured no faster: off by default
     inline_ok = e && e[0] == '1';
+    const char* xd = std::getenv("SRHIP_JIT_XDIRECT");
+    xdirect = !(xd && xd[0] == '0');  // measured 1 % faster on config #2
     const char* tf = std::getenv("SRHIP_JIT_TRIG_FULL");
     trig_full = tf && tf[0] == '1';
   }
@@ -559,7 +564,7 @@ struct Gen {
       }
     }
     // features: first use order, last use
-    for (int f = 0; f < 256; ++f) { xblk[f] = -1; xlast[f] = -1; load_idx[f] = -1; }
+    for (int f = 0; f < 256; ++f) { xblk[f] = -1; xlast[f] = -1; load_idx[f] = -1; xinl[f] = false; }
     auto usef = [&](const Opnd& q, int i) {
       if (q.k != O_X) return true;
       if (q.v < 0 || q.v > 255) return false;
@@ -570,8 +575,19 @@ struct Gen {
     for (int i = 0; i < n; ++i) {
       if (!usef(ops[i].a, i)) return false;
       if (!ops[i].un && !usef(ops[i].b, i)) return false;
+      if (ops[i].rid < 0 || !xdirect) {
+        if (ops[i].a.k == O_X) xinl[ops[i].a.v] = true;
+        if (!ops[i].un && ops[i].b.k == O_X) xinl[ops[i].b.v] = true;
+      }
     }
     if (!usef(root, n)) return false;
+    if (root.k == O_X) xinl[root.v] = true;
+    {
+      std::vector<int> pre;
+      for (int f : feats)
+        if (xinl[f]) pre.push_back(f);
+      feats = pre;  // the features preloaded into register blocks at the tile start
+    }
     if ((int)feats.size() > NPOOL) { why = "more features than register blocks"; return false; }
     for (int f : feats)
       if ((1 + f) * TILE * 4 + 3 * 4 * 64 > 65535) { why = "feature offset beyond the DS immediate"; return false; }
@@ -614,6 +630,24 @@ struct Gen {
   void mov_block_reg(int dst, int srcreg) {
     for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", dst + e, V(srcreg + e));
   }
+  // a call operand into block `dst` (A or B): features not preloaded (or all
+  // of them with xdirect) are read from the LDS tile, other operands moved
+  bool load_x_direct(const Opnd& q) const { return q.k == O_X && (xdirect || xblk[q.v] < 0); }
+  void operand_to(int dst, const Opnd& q, bool* issued) {
+    if (load_x_direct(q)) {
+      as.ds_read_b128(dst, VLANE, (1 + q.v) * TILE * 4);
+      ++nloads;
+      *issued = true;
+      return;
+    }
+    Src sq[R];
+    for (int e = 0; e < R; ++e) sq[e] = opsrc(q, e);
+    mov_block(dst, sq);
+  }
+  void wait_direct(bool issued) {
+    if (issued) { as.waitcnt_lgkm(0); waited = nloads; }
+  }
+
   // value v leaves its location (its last use)
   void release_val(int v) {
     const int l = loc[v];
@@ -679,30 +713,26 @@ struct Gen {
     // routines keep B: a unary call leaves its owner there
     if (!evict(L_A, va_, vb_) || (!o.un && !evict(L_B, va_, vb_))) return false;
     // move the operands into A (lhs) and B (rhs)
-    auto srcs = [&](const Opnd& q, Src (&s)[R]) {
-      for (int e = 0; e < R; ++e) s[e] = opsrc(q, e);
-    };
     const int la = va_ >= 0 ? loc[va_] : L_NONE;
     const int lb = vb_ >= 0 ? loc[vb_] : L_NONE;
-    Src sa[R], sb[R];
+    bool issued = false;
     if (o.un) {
-      if (la != L_A) { srcs(o.a, sa); mov_block(VA, sa); }
+      if (la != L_A) operand_to(VA, o.a, &issued);
     } else if (la == L_B && lb == L_A) {
       mov_block_reg(VGT, VA);
       mov_block_reg(VA, VB);
       mov_block_reg(VB, VGT);
     } else if (la == L_B) {
       mov_block_reg(VA, VB);
-      srcs(o.b, sb);
-      mov_block(VB, sb);
+      operand_to(VB, o.b, &issued);
     } else if (lb == L_A) {
       mov_block_reg(VB, VA);
-      srcs(o.a, sa);
-      mov_block(VA, sa);
+      operand_to(VA, o.a, &issued);
     } else {
-      if (la != L_A) { srcs(o.a, sa); mov_block(VA, sa); }
-      if (lb != L_B) { srcs(o.b, sb); mov_block(VB, sb); }
+      if (la != L_A) operand_to(VA, o.a, &issued);
+      if (lb != L_B) operand_to(VB, o.b, &issued);
     }
+    wait_direct(issued);
     // the operands are consumed
     if (va_ >= 0) release_val(va_);
     if (vb_ >= 0) release_val(vb_);
@@ -710,10 +740,10 @@ struct Gen {
     if (!o.un && o.b.k == O_X) release_x(o.b.v, i);
     a_owner = -1;
     if (!o.un) b_owner = -1;
-    if (fast && o.un && o.op == SRHIP_UOP_EXP)
-      for (int e = 0; e < R; ++e) {
-        const Src g = V(VGEXP), x = V(VA + e);
-        as.vop3(VOP3_MAX_F32, "v_max_f32_e64", VGEXP, g, x, nullptr, 2, 0);
+    if (fast && o.un && o.op == SRHIP_UOP_EXP)  // max |x| over the rows, two per instruction
+      for (int e = 0; e < R; e += 2) {
+        const Src g = V(VGEXP), x0 = V(VA + e), x1 = V(VA + e + 1);
+        as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGEXP, g, x0, &x1, 6, 0);
       }
     call_routine(o.rid);
     loc[i] = L_A;
@@ -733,9 +763,9 @@ struct Gen {
     if (!evict(L_A, vq, -1)) return false;
     const int lq = vq >= 0 ? loc[vq] : L_NONE;
     if (lq != L_A) {
-      Src sq[R];
-      for (int e = 0; e < R; ++e) sq[e] = opsrc(q, e);
-      mov_block(VA, sq);
+      bool issued = false;
+      operand_to(VA, q, &issued);
+      wait_direct(issued);
     }
     if (vq >= 0) release_val(vq);
     if (q.k == O_X) release_x(q.v, i);
@@ -764,9 +794,9 @@ struct Gen {
   }
 
   void guard_min(int reg) {
-    for (int e = 0; e < R; ++e) {
-      const Src g = V(VGMIN), x = V(reg + e);
-      as.vop3(VOP3_MIN_F32, "v_min_f32_e64", VGMIN, g, x, nullptr, 2, 0);
+    for (int e = 0; e < R; e += 2) {
+      const Src g = V(VGMIN), x0 = V(reg + e), x1 = V(reg + e + 1);
+      as.vop3(VOP3_MIN3_F32, "v_min3_f32", VGMIN, g, x0, &x1, 6, 0);
     }
   }
 
@@ -852,12 +882,16 @@ struct Gen {
     if (dst == L_A) a_owner = i;
     else if (dst == L_B) b_owner = i;
     else pool_owner[dst] = i;
-    if (gcan)
+    if (gcan) {
       for (int e = 0; e < R; ++e) {
         const Src t_ = V(VGT + e), eps = S(S_EPS), r = V(d + e);
         as.vop3(VOP3_FMA_F32, "v_fma_f32", VGT + e, t_, eps, &r, 4, 4);
-        as.vop2(VOP2_MAX_F32, "v_max_f32_e32", VGCAN, V(VGT + e), VGCAN);
       }
+      for (int e = 0; e < R; e += 2) {
+        const Src g = V(VGCAN), t0 = V(VGT + e), t1 = V(VGT + e + 1);
+        as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGCAN, g, t0, &t1, 0, 0);
+      }
+    }
     if (gmin) guard_min(d);
     return true;
   }
@@ -890,7 +924,7 @@ struct Gen {
     as.branch(SOPP_SCC1, "s_cbranch_scc1", L_done);
     // ---- tile
     as.bind(L_tile);
-    as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHKSAVE, V(VCHK));
+    if (fast || has_trig) as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHKSAVE, V(VCHK));  // for a redo / bail
     if (g_can) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGCAN, K(0xbf800000u));   // -1
     if (g_min) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGMIN, K(0x3f800000u));   // 1
     if (g_exp) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGEXP, K(0));
