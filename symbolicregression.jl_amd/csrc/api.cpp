@@ -162,7 +162,9 @@ struct srhip_program {
   int32_t* d_gtree_off = nullptr;
   int32_t* d_gitems = nullptr;  // work items (tree | group << 24): shallow then deep
   int32_t* d_const_off = nullptr;
-  int ngitems_a = 0, ngitems_b = 0;
+  // work items by pass: shallow items carrying 1, 2 or kGradG tangents, then deep ones
+  int ngitems[4] = {0, 0, 0, 0};
+  int g_opset = OPSET_FULL;
   // byte capacities of the device buffers above (kept across rebuilds)
   size_t code_cap = 0, toff_cap = 0, list_cap = 0;
   size_t gcode_cap = 0, gtoff_cap = 0, gitems_cap = 0, gconst_cap = 0;
@@ -220,24 +222,35 @@ void build_grad_program(srhip_program* p) {
   CompiledBatch<T> cb = compile_batch<T>(tr, /*grad=*/true);
   if (p->ntrees >= (1 << 24)) throw Error(SRHIP_ERR_UNSUPPORTED, "too many trees for gradient work items");
   p->g_static_fail = cb.static_fail;
-  std::vector<std::pair<int, int32_t>> a, b;  // (cost, item)
+  p->g_opset = OPSET_BASIC;
+  for (const Ins<T>& ins : cb.code) {
+    const int opc = (int)(ins.code & 0xffu);
+    if (opc >= OP_BIN0 ? !opset_has_bop(OPSET_BASIC, (opc - OP_BIN0) % SRHIP_NUM_BOPS)
+                       : opc >= OP_UN0 && !opset_has_uop(OPSET_BASIC, opc - OP_UN0))
+      p->g_opset = OPSET_FULL;
+  }
+  // a work item carries the tangents of its group only: groups of 1 and 2
+  // constants run in kernels with fewer tangents (and more rows per lane)
+  std::vector<std::pair<int, int32_t>> cls[4];  // (cost, item)
   for (int t = 0; t < p->ntrees; ++t) {
     if (cb.tree_off[t] < 0) continue;
     const int nc = p->const_off[t + 1] - p->const_off[t];
     const int ngroups = std::max(1, (nc + kGradG - 1) / kGradG);
-    for (int gi = 0; gi < ngroups; ++gi)
-      (cb.need[t] <= 4 ? a : b).push_back({cb.cost[t], (int32_t)(t | (gi << 24))});
+    for (int gi = 0; gi < ngroups; ++gi) {
+      const int ntan = std::min(kGradG, nc - gi * kGradG);
+      const int k = cb.need[t] > 4 ? 3 : ntan <= 1 ? 0 : ntan <= 2 ? 1 : 2;
+      cls[k].push_back({cb.cost[t], (int32_t)(t | (gi << 24))});
+    }
   }
   auto by_cost = [](const std::pair<int, int32_t>& x, const std::pair<int, int32_t>& y) {
     return x.first != y.first ? x.first > y.first : x.second < y.second;
   };
-  std::stable_sort(a.begin(), a.end(), by_cost);
-  std::stable_sort(b.begin(), b.end(), by_cost);
   std::vector<int32_t> items;
-  for (auto& q : a) items.push_back(q.second);
-  for (auto& q : b) items.push_back(q.second);
-  p->ngitems_a = (int)a.size();
-  p->ngitems_b = (int)b.size();
+  for (int k = 0; k < 4; ++k) {
+    std::stable_sort(cls[k].begin(), cls[k].end(), by_cost);
+    for (auto& q : cls[k]) items.push_back(q.second);
+    p->ngitems[k] = (int)cls[k].size();
+  }
   std::vector<int32_t> toff(cb.tree_off);
   for (auto& v : toff) v = std::max(v, 0);
   hipStream_t s = p->ctx->stream;
@@ -709,16 +722,21 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
   c->sums.ensure(std::max<size_t>(nt, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(nt, 1));
   c->dloss.ensure(std::max<size_t>(nconst, 1) * sizeof(double));
-  for (int pass = 0; pass < 2; ++pass) {
-    const int nitems = pass == 0 ? p->ngitems_a : p->ngitems_b;
+  int first = 0;
+  for (int pass = 0; pass < 4; ++pass) {
+    const int nitems = p->ngitems[pass];
+    const int item0 = first;
+    first += nitems;
     if (nitems == 0 || ds->rows == 0) continue;
+    const bool deep = pass == 3;
+    const int G = pass == 0 ? 1 : pass == 1 ? 2 : kGradG;
     EvalPlan plan;
-    if (!plan_grad(p->dtype, pass == 1, mode, ds->w != nullptr, ds->nfeat, ds->rows, nitems, &plan))
+    if (!plan_grad(p->dtype, deep, G, mode, ds->w != nullptr, ds->nfeat, ds->rows, nitems, &plan))
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(ds->nfeat) + " features does not fit in LDS");
     GradArgs<T> a;
     a.prog = static_cast<const Ins<T>*>(p->d_gcode);
     a.tree_off = p->d_gtree_off;
-    a.items = p->d_gitems + (pass == 0 ? 0 : p->ngitems_a);
+    a.items = p->d_gitems + item0;
     a.nitems = nitems;
     a.const_off = p->d_const_off;
     a.X = static_cast<const T*>(ds->X);
@@ -733,7 +751,9 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
     a.nrg = plan.nrg;
     a.loss = loss;
     a.lparam = (T)lparam;
-    c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * (2 + kGradG) * sizeof(T));
+    a.G = G;
+    a.opset = deep ? OPSET_FULL : p->g_opset;
+    c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * (2 + G) * sizeof(T));
     a.partial = static_cast<T*>(c->partial.p);
     a.out_value = out_value;
     a.out_grad = out_grad;
@@ -748,6 +768,10 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
     HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
     c->last_ms += ms;
     c->last_launches += 1;
+    static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
+    if (dbg)
+      std::fprintf(stderr, "srhip grad pass %d: %d items, G=%d, R=%d, opset %d, %.3f ms (grid %d x %d, %d tiles/wg)\n",
+                   pass, nitems, G, plan.R, a.opset, ms, plan.nrg, plan.ntg, plan.ntiles);
   }
 }
 
@@ -759,7 +783,7 @@ void collect_grad_results(srhip_ctx* c, const srhip_program* p, int64_t rows, do
   c->h_sum.assign(nt, 0.0);
   c->h_ok.assign(nt, 1);
   std::vector<double> hd(nconst, 0.0);
-  if (rows > 0 && nt > 0 && (p->ngitems_a + p->ngitems_b) > 0) {
+  if (rows > 0 && nt > 0 && (p->ngitems[0] + p->ngitems[1] + p->ngitems[2] + p->ngitems[3]) > 0) {
     HIP_CHECK(hipMemcpyAsync(c->h_sum.data(), c->sums.p, nt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
     HIP_CHECK(hipMemcpyAsync(c->h_ok.data(), c->oks.p, nt, hipMemcpyDeviceToHost, c->stream));
     if (nconst > 0)

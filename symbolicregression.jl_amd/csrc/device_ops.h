@@ -280,6 +280,30 @@ __device__ __forceinline__ float m_cos(float x) {
   }
   return v;
 }
+// Float32 sin / cos for derivatives: the single-precision path of
+// fast_sincos_f32 (<= 2 ulp) whatever SR_PRECISE_TRANSC says — a derivative
+// value is not subject to the did_succeed parity that makes the forward
+// values Float64-evaluated — with the large-argument path behind a ballot.
+__device__ __forceinline__ float d_sincos_f32(float x, int want_cos) {
+  const float n = want_cos ? __builtin_rintf(__builtin_fmaf(x, 0.318309873f, -0.5f))
+                           : __builtin_rintf(x * 0.318309873f);
+  const float m = want_cos ? __builtin_fmaf(n, 2.0f, 1.0f) : n + n;
+  float r = __builtin_fmaf(m, -1.57079601e+00f, x);
+  r = __builtin_fmaf(m, -3.13916473e-07f, r);
+  r = __builtin_fmaf(m, -5.39030253e-15f, r);
+  const float s = r * r;
+  float p = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.606342605e-06f, s, -1.980987436e-04f), s,
+                                          8.333070204e-03f), s, -1.666665971e-01f);
+  p = p * s;
+  float v = want_cos ? __builtin_fmaf(p, -r, -r) : __builtin_fmaf(p, r, r);
+  v = __int_as_float(__float_as_int(v) ^ ((int)n << 31));
+  const bool big = trig_big(x);
+  if (__builtin_amdgcn_ballot_w64(big) != 0) {
+    const float o = big_sincos_f32(x, want_cos);
+    v = big ? o : v;
+  }
+  return v;
+}
 __device__ __forceinline__ double m_sin(double x) { return m_sin_ocml(x); }
 __device__ __forceinline__ double m_cos(double x) { return m_cos_ocml(x); }
 
@@ -418,7 +442,16 @@ __device__ __forceinline__ void bop_d(T x, T y, T& f, T& fx, T& fy) {
   if constexpr (OP == SRHIP_BOP_ADD) { fx = T(1); fy = T(1); }
   else if constexpr (OP == SRHIP_BOP_SUB) { fx = T(1); fy = T(-1); }
   else if constexpr (OP == SRHIP_BOP_MUL) { fx = y; fy = x; }
-  else if constexpr (OP == SRHIP_BOP_DIV) { fx = T(1) / y; fy = -x / (y * y); }
+  else if constexpr (OP == SRHIP_BOP_DIV) {
+    if constexpr (sizeof(T) == 4) {  // v_rcp_f32 (1 ulp): derivatives need no IEEE quotient
+      const T ry = __builtin_amdgcn_rcpf(y);
+      fx = ry;
+      fy = -f * ry;
+    } else {
+      fx = T(1) / y;
+      fy = -x / (y * y);
+    }
+  }
   else if constexpr (OP == SRHIP_BOP_POW) {
     fx = y * safe_pow(x, y - T(1));
     fy = x > T(0) ? f * m_log(x) : T(0);
@@ -441,8 +474,13 @@ __device__ __forceinline__ void uop_d(T x, T& f, T& fx) {
   else if constexpr (OP == SRHIP_UOP_LOG10) fx = T(1) / (x * T(2.30258509299404568402));
   else if constexpr (OP == SRHIP_UOP_LOG1P) fx = T(1) / (T(1) + x);
   else if constexpr (OP == SRHIP_UOP_SQRT) fx = T(0.5) / f;
-  else if constexpr (OP == SRHIP_UOP_SIN) fx = m_cos(x);
-  else if constexpr (OP == SRHIP_UOP_COS) fx = -m_sin(x);
+  else if constexpr (OP == SRHIP_UOP_SIN) {
+    if constexpr (sizeof(T) == 4) fx = d_sincos_f32(x, 1);
+    else fx = m_cos(x);
+  } else if constexpr (OP == SRHIP_UOP_COS) {
+    if constexpr (sizeof(T) == 4) fx = -d_sincos_f32(x, 0);
+    else fx = -m_sin(x);
+  }
   else if constexpr (OP == SRHIP_UOP_TAN) { T c = m_cos(x); fx = T(1) / (c * c); }
   else if constexpr (OP == SRHIP_UOP_SINH) fx = m_cosh(x);
   else if constexpr (OP == SRHIP_UOP_COSH) fx = m_sinh(x);

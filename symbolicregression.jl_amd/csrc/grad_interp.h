@@ -93,15 +93,15 @@ __device__ __forceinline__ void bin_grad(Dual<T, R, G>& a, const Dual<T, R, G>& 
     if constexpr (K < D) t = slot[K];                                    \
     break;
 #define SRG_UN(U) \
-  case OP_UN0 + U: un_grad<U, T, R, G>(a, chk); break;
+  case OP_UN0 + U: if constexpr (opset_has_uop(SET, U)) un_grad<U, T, R, G>(a, chk); break;
 #define SRG_BV(V, B) \
-  case bin_opcode(V, B): bin_grad<V, B, T, R, G>(a, t, sXt, rs, lane, f, imm, jc, chk); break;
+  case bin_opcode(V, B): if constexpr (opset_has_bop(SET, B)) bin_grad<V, B, T, R, G>(a, t, sXt, rs, lane, f, imm, jc, chk); break;
 #define SRG_BIN(B) SRG_BV(V_AX, B) SRG_BV(V_XA, B) SRG_BV(V_AC, B) SRG_BV(V_CA, B) \
   SRG_BV(V_AT, B) SRG_BV(V_TA, B) SRG_BV(V_XX, B) SRG_BV(V_XC, B) SRG_BV(V_CX, B)
 
 // Run one tree's program over one row tile with tangents for constants
 // g0 .. g0+G-1; the result is left in a.
-template <typename T, int R, int D, int G>
+template <typename T, int R, int D, int G, int SET>
 __device__ __forceinline__ void run_program_grad(CIns<T>* __restrict__ p,
                                                  const T* __restrict__ sXt, int rs, int lane,
                                                  int g0, Dual<T, R, G>& a, T& chk) {

@@ -18,9 +18,8 @@ namespace {
 
 using namespace interp;
 
-template <typename T, int R, int D, int MODE, bool W>
+template <typename T, int R, int D, int MODE, bool W, int G, int SET>
 __global__ void __launch_bounds__(256) grad_kernel(GradArgs<T> a) {
-  constexpr int G = kGradG;
   constexpr int S = 2 + G;
   constexpr int TILE = 64 * R;
   using V = typename V16<T>::type;
@@ -64,7 +63,7 @@ __global__ void __launch_bounds__(256) grad_kernel(GradArgs<T> a) {
     if (s >= a.nitems) continue;
     const int item = __builtin_amdgcn_readfirstlane(a.items[s]);
     const int t = item & 0xffffff;
-    const int g0 = (item >> 24) * G;
+    const int g0 = (item >> 24) * kGradG;  // groups are kGradG constants; G of them carried
     CIns<T>* p = const_prog(a.prog + __builtin_amdgcn_readfirstlane(a.tree_off[t]));
     const int cbase = __builtin_amdgcn_readfirstlane(a.const_off[t]);
     const int nc = __builtin_amdgcn_readfirstlane(a.const_off[t + 1]) - cbase;
@@ -74,7 +73,7 @@ __global__ void __launch_bounds__(256) grad_kernel(GradArgs<T> a) {
     for (int tl = 0; tl < nt_valid; ++tl) {
       const T* sXt = sX + tl * TILE;
       Dual<T, R, G> d;
-      run_program_grad<T, R, D, G>(p, sXt, rows, lane, g0, d, acc[1]);
+      run_program_grad<T, R, D, G, SET>(p, sXt, rows, lane, g0, d, acc[1]);
 #pragma unroll
       for (int r = 0; r < R; ++r) acc[1] = mark(d.v[r], acc[1]);
       if constexpr (MODE == GRAD_OUT) {
@@ -114,11 +113,11 @@ __global__ void __launch_bounds__(256) grad_kernel(GradArgs<T> a) {
   for (int i = threadIdx.x; i < a.tpb * S; i += blockDim.x) dst[i] = sPart[i];
 }
 
-template <typename T>
+template <typename T, int G>
 __global__ void __launch_bounds__(256) grad_finalize_kernel(GradArgs<T> a, double* __restrict__ out_sum,
                                                             uint8_t* __restrict__ out_ok,
                                                             double* __restrict__ out_dloss) {
-  constexpr int S = 2 + kGradG;
+  constexpr int S = 2 + G;
   __shared__ double sh[4][S][64];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
@@ -150,54 +149,65 @@ __global__ void __launch_bounds__(256) grad_finalize_kernel(GradArgs<T> a, doubl
       }
       const int cb = a.const_off[t];
       const int nc = a.const_off[t + 1] - cb;
-      for (int j = 0; j < kGradG; ++j)
+      for (int j = 0; j < G; ++j)
         if (g0 + j < nc) out_dloss[cb + g0 + j] = ok ? acc[2 + j] : __builtin_nan("");
     }
   }
 }
 
-template <typename T, int R, int D, int MODE, bool W>
+template <typename T, int R, int D, int MODE, bool W, int G, int SET>
 hipError_t launch_grad_one(const EvalPlan& plan, const GradArgs<T>& a, hipStream_t stream) {
   // raise the dynamic-LDS ceiling once per kernel instantiation: a function-
   // local static is initialised exactly once even with concurrent callers
   static const hipError_t attr_err = hipFuncSetAttribute(
-      reinterpret_cast<const void*>(&grad_kernel<T, R, D, MODE, W>), hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      reinterpret_cast<const void*>(&grad_kernel<T, R, D, MODE, W, G, SET>), hipFuncAttributeMaxDynamicSharedMemorySize,
+      160 * 1024);
   if (attr_err != hipSuccess) return attr_err;
   const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
-  hipLaunchKernelGGL((grad_kernel<T, R, D, MODE, W>), dim3(grid), dim3(plan.threads), plan.lds_bytes,
+  hipLaunchKernelGGL((grad_kernel<T, R, D, MODE, W, G, SET>), dim3(grid), dim3(plan.threads), plan.lds_bytes,
                      stream, a);
   return hipGetLastError();
 }
 
-template <typename T, int R, int D>
+template <typename T, int R, int D, int G, int SET>
 hipError_t launch_grad_rd(const EvalPlan& plan, const GradArgs<T>& a, int mode, hipStream_t stream) {
-  if (mode == GRAD_OUT) return launch_grad_one<T, R, D, GRAD_OUT, false>(plan, a, stream);
-  if (a.w) return launch_grad_one<T, R, D, GRAD_LOSS, true>(plan, a, stream);
-  return launch_grad_one<T, R, D, GRAD_LOSS, false>(plan, a, stream);
+  if (mode == GRAD_OUT) return launch_grad_one<T, R, D, GRAD_OUT, false, G, SET>(plan, a, stream);
+  if (a.w) return launch_grad_one<T, R, D, GRAD_LOSS, true, G, SET>(plan, a, stream);
+  return launch_grad_one<T, R, D, GRAD_LOSS, false, G, SET>(plan, a, stream);
 }
 
-// gradient variants: rows per lane R and stack slots D
-inline int grad_R(int dtype, bool deep) { return dtype == SRHIP_F32 ? (deep ? 1 : 2) : 1; }
+// gradient variants: rows per lane R (fewer tangents leave room for more
+// rows) and stack slots D
+inline int grad_R(int dtype, bool deep, int G) {
+  if (dtype != SRHIP_F32 || deep) return 1;
+  return G <= 2 ? 4 : 2;
+}
+
+template <typename T, int G>
+hipError_t launch_grad_g(const EvalPlan& plan, const GradArgs<T>& a, int mode, hipStream_t stream) {
+  constexpr int RS = sizeof(T) == 4 ? (G <= 2 ? 4 : 2) : 1;  // grad_R, shallow
+  if (plan.D == 4) {
+    if (a.opset == OPSET_BASIC) return launch_grad_rd<T, RS, 4, G, OPSET_BASIC>(plan, a, mode, stream);
+    return launch_grad_rd<T, RS, 4, G, OPSET_FULL>(plan, a, mode, stream);
+  }
+  return launch_grad_rd<T, 1, kMaxSlots, G, OPSET_FULL>(plan, a, mode, stream);
+}
 
 }  // namespace
 
-bool plan_grad(int dtype, bool deep, int mode, bool weighted, int nfeat, int64_t n, int nitems,
+bool plan_grad(int dtype, bool deep, int G, int mode, bool weighted, int nfeat, int64_t n, int nitems,
                EvalPlan* p) {
   const size_t esz = dtype == SRHIP_F32 ? 4 : 8;
   const int narr = nfeat + (mode == GRAD_LOSS ? (weighted ? 2 : 1) : 0);
-  return plan_geometry(esz, grad_R(dtype, deep), deep ? kMaxSlots : 4, narr, (2 + kGradG) * esz, n,
-                       nitems, p);
+  return plan_geometry(esz, grad_R(dtype, deep, G), deep ? kMaxSlots : 4, narr, (2 + G) * esz, n, nitems, p);
 }
 
 template <typename T>
 hipError_t launch_grad(const EvalPlan& plan, const GradArgs<T>& a, int mode, hipStream_t stream) {
-  if constexpr (sizeof(T) == 4) {
-    if (plan.D == 4) return launch_grad_rd<T, 2, 4>(plan, a, mode, stream);
-    return launch_grad_rd<T, 1, kMaxSlots>(plan, a, mode, stream);
-  } else {
-    if (plan.D == 4) return launch_grad_rd<T, 1, 4>(plan, a, mode, stream);
-    return launch_grad_rd<T, 1, kMaxSlots>(plan, a, mode, stream);
-  }
+  if (plan.D != 4) return launch_grad_g<T, kGradG>(plan, a, mode, stream);  // deep programs: one variant
+  if (a.G == 1) return launch_grad_g<T, 1>(plan, a, mode, stream);
+  if (a.G == 2) return launch_grad_g<T, 2>(plan, a, mode, stream);
+  return launch_grad_g<T, kGradG>(plan, a, mode, stream);
 }
 
 template <typename T>
@@ -205,8 +215,13 @@ hipError_t launch_grad_finalize(const GradArgs<T>& a, double* out_sum, uint8_t* 
                                 hipStream_t stream) {
   const int npos = a.ntg * a.tpb;
   const unsigned grid = (unsigned)((npos + 63) / 64);
-  hipLaunchKernelGGL((grad_finalize_kernel<T>), dim3(grid), dim3(256), 0, stream, a, out_sum, out_ok,
-                     out_dloss);
+  if (a.G == 1)
+    hipLaunchKernelGGL((grad_finalize_kernel<T, 1>), dim3(grid), dim3(256), 0, stream, a, out_sum, out_ok, out_dloss);
+  else if (a.G == 2)
+    hipLaunchKernelGGL((grad_finalize_kernel<T, 2>), dim3(grid), dim3(256), 0, stream, a, out_sum, out_ok, out_dloss);
+  else
+    hipLaunchKernelGGL((grad_finalize_kernel<T, kGradG>), dim3(grid), dim3(256), 0, stream, a, out_sum, out_ok,
+                       out_dloss);
   return hipGetLastError();
 }
 

@@ -91,13 +91,15 @@ struct GradArgs {
   int ntiles, ntg, tpb, nrg;
   int loss;
   T lparam;
-  T* partial;               // [nrg][ntg*tpb][2 + kGradG]
+  int G;                    // tangents carried by this launch (1, 2 or kGradG)
+  int opset;                // OPSET_BASIC: the programs use only the basic operators
+  T* partial;               // [nrg][ntg*tpb][2 + G]
   T* out_value;             // GRAD_OUT: [ntrees][out_stride]
   T* out_grad;              // GRAD_OUT: [total consts][out_stride]
   int64_t out_stride;
 };
 
-bool plan_grad(int dtype, bool deep, int mode, bool weighted, int nfeat, int64_t n,
+bool plan_grad(int dtype, bool deep, int G, int mode, bool weighted, int nfeat, int64_t n,
                int nitems, EvalPlan* plan);
 template <typename T>
 hipError_t launch_grad(const EvalPlan& plan, const GradArgs<T>& a, int mode, hipStream_t stream);
