@@ -132,22 +132,30 @@ def optimize_constants_batch(dataset: Dataset, trees: Sequence[Node], options: O
 
 
 def _optimize(dataset, trees, options, rng, device, evaluator_factory) -> ConstOptResult:
-    T = np.dtype(dataset.T).type
-    iterations = int(getattr(options, "optimizer_iterations", 8))
-    nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
     algorithm = getattr(options, "optimizer_algorithm", "BFGS")
     if algorithm == "NelderMead":
-        from ._lib import Unsupported
-
-        raise Unsupported(-2, "NelderMead is derivative-free; the engine batches BFGS/Newton only")
+        # one constant: Newton whatever the option says (:32-33); more: NelderMead (:35-36)
+        multi = np.array([len(get_constants(t)) > 1 for t in trees], dtype=bool)
+        out = ConstOptResult(np.full(len(trees), np.inf), np.zeros(len(trees), dtype=bool), np.zeros(len(trees)))
+        for sel, fn in ((~multi, _optimize_gradient), (multi, _optimize_nelder_mead)):
+            idx = np.nonzero(sel)[0]
+            if idx.size == 0:
+                continue
+            r = fn(dataset, [trees[i] for i in idx], options, rng, device, evaluator_factory)
+            out.losses[idx], out.converged[idx], out.num_evals[idx] = r.losses, r.converged, r.num_evals
+        return out
     if algorithm != "BFGS":
         raise ValueError("Optimization function not implemented.")  # :39-41
+    return _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory)
 
-    ntrees = len(trees)
-    x0s = [np.asarray(get_constants(t), dtype=T) for t in trees]
+
+def _starts(trees, T, nrestarts, rng):
+    """Candidates: x0 and `nrestarts` perturbed copies x0 .* (1 + randn/2) per
+    tree with constants (:42-54)."""
     cand_tree: List[int] = []
     cand_x: List[np.ndarray] = []
-    for i, x0 in enumerate(x0s):
+    for i, t in enumerate(trees):
+        x0 = np.asarray(get_constants(t), dtype=T)
         if x0.size == 0:
             continue
         cand_tree.append(i)
@@ -155,6 +163,17 @@ def _optimize(dataset, trees, options, rng, device, evaluator_factory) -> ConstO
         for _ in range(nrestarts):  # :47
             cand_tree.append(i)
             cand_x.append((x0 * (T(1) + T(0.5) * rng.standard_normal(x0.size).astype(T))).astype(T))
+    return cand_tree, cand_x
+
+
+def _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory) -> ConstOptResult:
+    """BFGS (Newton for one constant) with BackTracking, all starts in lockstep."""
+    T = np.dtype(dataset.T).type
+    iterations = int(getattr(options, "optimizer_iterations", 8))
+    nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
+
+    ntrees = len(trees)
+    cand_tree, cand_x = _starts(trees, T, nrestarts, rng)
     losses = np.full(ntrees, np.inf)
     converged_out = np.zeros(ntrees, dtype=bool)
     num_evals = np.zeros(ntrees)
@@ -303,6 +322,177 @@ def _optimize(dataset, trees, options, rng, device, evaluator_factory) -> ConstO
     for i, k in best.items():
         if conv[k]:
             set_constants(trees[i], [T(v) for v in seg(X, k)])
+            converged_out[i] = True
+            num_evals[i] += 1
+    return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory), converged_out,
+                          num_evals)
+
+
+NM_INITIAL_A, NM_INITIAL_B = 0.025, 0.5  # Optim.AffineSimplexer defaults
+
+
+def _optimize_nelder_mead(dataset, trees, options, rng, device, evaluator_factory) -> ConstOptResult:
+    """Optim.NelderMead for trees of two or more constants (:35-36), every
+    start of every tree in lockstep. Optim is not vendored in the reference;
+    this restates its published algorithm (Optim.jl, nelder_mead.jl): the
+    affine initial simplex x0 + (a + b·x0_j)·e_j (a = 0.025, b = 0.5), the
+    adaptive parameters of Gao & Han (α = 1, β = 1 + 2/n, γ = 0.75 - 1/(2n),
+    δ = 1 - 1/n), reflection / expansion / outside and inside contraction /
+    shrink, convergence when the population standard deviation of the simplex
+    losses is <= g_abstol (1e-8), and the final minimiser = the centroid of
+    the best n vertices if its loss beats the best vertex. Launches per
+    iteration: one for the reflections, one for the expansion / contraction
+    points, one for the shrinks (all vertices); vertices live in T."""
+    T = np.dtype(dataset.T).type
+    iterations = int(getattr(options, "optimizer_iterations", 8))
+    nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
+    ntrees = len(trees)
+    cand_tree, cand_x = _starts(trees, T, nrestarts, rng)
+    converged_out = np.zeros(ntrees, dtype=bool)
+    num_evals = np.zeros(ntrees)
+    if not cand_tree:
+        return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory),
+                              converged_out, num_evals)
+
+    def make(ts):
+        return evaluator_factory(ts) if evaluator_factory is not None else EngineEvaluator(ts, dataset, options, device)
+
+    cands = []
+    for i, x in zip(cand_tree, cand_x):
+        c = trees[i].copy()
+        set_constants(c, list(x))
+        cands.append(c)
+    nc = len(cands)
+    sizes = [x.size for x in cand_x]
+    point_ev = make(cands)                                              # one point per start
+    simplex_ev = make([c for k, c in enumerate(cands) for _ in range(sizes[k] + 1)])  # every vertex
+
+    # initial simplex (AffineSimplexer) and its losses: one launch
+    simplex = []
+    for x0 in cand_x:
+        v = np.repeat(x0[None, :], x0.size + 1, axis=0).astype(T)
+        for j in range(x0.size):
+            v[j + 1, j] = T((1.0 + NM_INITIAL_B) * float(v[j + 1, j]) + NM_INITIAL_A)
+        simplex.append(v)
+
+    def eval_simplices():
+        fl = simplex_ev.loss_only(np.concatenate([v.reshape(-1) for v in simplex]))
+        out, o = [], 0
+        for k in range(nc):
+            out.append(np.asarray(fl[o:o + sizes[k] + 1], dtype=np.float64))
+            o += sizes[k] + 1
+        return out
+
+    def eval_points(pts):
+        return np.asarray(point_ev.loss_only(np.concatenate(pts)), dtype=np.float64)
+
+    def nm_x(fs):  # sqrt(var(f) * n/m), var with m-1: the population standard deviation
+        with np.errstate(invalid="ignore"):
+            return float(np.sqrt(np.mean((fs - fs.mean()) ** 2)))
+
+    def centroid(v, h):
+        return np.delete(v, h, axis=0).astype(np.float64).mean(axis=0)
+
+    fsx = eval_simplices()
+    f_calls = np.array([s + 1.0 for s in sizes])
+    order = [np.argsort(f, kind="stable") for f in fsx]
+    conv = np.zeros(nc, dtype=bool)
+    active = np.ones(nc, dtype=bool)
+    params = []
+    for n in sizes:
+        params.append((1.0, 1.0 + 2.0 / n, 0.75 - 1.0 / (2.0 * n), 1.0 - 1.0 / n))
+
+    for _ in range(iterations):
+        if not active.any():
+            break
+        # 1. reflections
+        xc, xh, xr = [None] * nc, [None] * nc, [None] * nc
+        for k in range(nc):
+            m = sizes[k] + 1
+            xc[k] = centroid(simplex[k], order[k][m - 1])
+            xh[k] = simplex[k][order[k][m - 1]].astype(np.float64)
+            xr[k] = (xc[k] + params[k][0] * (xc[k] - xh[k])).astype(T) if active[k] else simplex[k][0]
+        fr = eval_points(xr)
+        f_calls += active
+        # 2. expansion / contraction points
+        second = np.zeros(nc, dtype=int)  # 0 none, 1 expand, 2 outside, 3 inside
+        xs = [simplex[k][0] for k in range(nc)]
+        shrink = np.zeros(nc, dtype=bool)
+        for k in np.nonzero(active)[0]:
+            m = sizes[k] + 1
+            f, o = fsx[k], order[k]
+            al, be, ga, de = params[k]
+            xrf = xr[k].astype(np.float64)
+            if fr[k] < f[o[0]]:
+                second[k], xs[k] = 1, (xc[k] + be * (xrf - xc[k])).astype(T)
+            elif fr[k] < f[o[m - 2]]:
+                simplex[k][o[m - 1]], f[o[m - 1]] = xr[k], fr[k]
+                order[k] = np.argsort(f, kind="stable")
+            elif fr[k] < f[o[m - 1]]:
+                second[k], xs[k] = 2, (xc[k] + ga * (xrf - xc[k])).astype(T)
+            else:
+                second[k], xs[k] = 3, (xc[k] - ga * (xrf - xc[k])).astype(T)
+        if second.any():
+            fs2 = eval_points(xs)
+            f_calls += second > 0
+            for k in np.nonzero(second)[0]:
+                m = sizes[k] + 1
+                f, o = fsx[k], order[k]
+                h = o[m - 1]
+                if second[k] == 1:
+                    if fs2[k] < fr[k]:
+                        simplex[k][h], f[h] = xs[k], fs2[k]
+                    else:
+                        simplex[k][h], f[h] = xr[k], fr[k]
+                    order[k] = np.concatenate([[h], o[:m - 1]])  # the new vertex is the lowest
+                elif (second[k] == 2 and fs2[k] < fr[k]) or (second[k] == 3 and fs2[k] < f[h]):
+                    simplex[k][h], f[h] = xs[k], fs2[k]
+                    order[k] = np.argsort(f, kind="stable")
+                else:
+                    shrink[k] = True
+        # 3. shrinks towards the lowest vertex: every other vertex re-evaluated
+        if shrink.any():
+            for k in np.nonzero(shrink)[0]:
+                lo = simplex[k][order[k][0]].astype(np.float64)
+                de = params[k][3]
+                for i in order[k][1:]:
+                    simplex[k][i] = (lo + de * (simplex[k][i].astype(np.float64) - lo)).astype(T)
+            fall = eval_simplices()
+            for k in np.nonzero(shrink)[0]:
+                f = fsx[k]
+                for i in order[k][1:]:
+                    f[i] = fall[k][i]
+                f_calls[k] += sizes[k]
+                order[k] = np.argsort(f, kind="stable")
+        for k in np.nonzero(active)[0]:
+            if nm_x(fsx[k]) <= G_TOL:
+                conv[k], active[k] = True, False
+
+    # after the loop: the centroid of the best n vertices against the best vertex
+    xcen = []
+    for k in range(nc):
+        order[k] = np.argsort(fsx[k], kind="stable")
+        xcen.append(centroid(simplex[k], order[k][-1]).astype(T))
+    fcen = eval_points(xcen)
+    f_calls += 1
+    xmin, fmin = [], np.zeros(nc)
+    for k in range(nc):
+        i = int(np.argmin(np.where(np.isnan(fsx[k]), np.inf, fsx[k])))
+        if fcen[k] < fsx[k][i]:
+            xmin.append(xcen[k])
+            fmin[k] = fcen[k]
+        else:
+            xmin.append(simplex[k][i].copy())
+            fmin[k] = fsx[k][i]
+
+    best = {}
+    for k, i in enumerate(cand_tree):
+        num_evals[i] += f_calls[k]
+        if i not in best or fmin[k] < fmin[best[i]]:  # tmpresult.minimum < result.minimum (:51)
+            best[i] = k
+    for i, k in best.items():
+        if conv[k]:
+            set_constants(trees[i], [T(v) for v in xmin[k]])
             converged_out[i] = True
             num_evals[i] += 1
     return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory), converged_out,

@@ -67,7 +67,7 @@ def test_recovers_constants_on_oracle():
                                          evaluator_factory=oracle_factory(o, X, y))
     assert res.converged[0] and res.converged[1]
     assert np.allclose(srhip.get_constants(trees[0]), [2.0, 1.0, -2.0], atol=1e-6)
-    assert np.allclose(srhip.get_constants(trees[1]), [2.0, 2.0], atol=1e-6)  # Newton path (1 constant)
+    assert np.allclose(srhip.get_constants(trees[1]), [2.0, 2.0], atol=1e-6)  # BFGS, 2 constants
     assert res.losses[0] < 1e-10 and res.losses[1] < 1e-10
     assert not res.converged[2] and res.num_evals[2] == 0  # no constants: untouched (:27-29)
     assert res.num_evals[0] > 3 and res.num_evals[1] > 3
@@ -96,11 +96,78 @@ def test_failing_tree_stays_failed():
     assert srhip.get_constants(t) == [40.0]
 
 
-def test_nelder_mead_is_unsupported():
+def test_nelder_mead_recovers_constants_on_oracle():
+    """optimizer_algorithm = "NelderMead" (ConstantOptimization.jl:35-36): the
+    3- and 2-constant trees go through the batched Nelder-Mead, a 1-constant
+    tree still through Newton (:32-33)."""
     o, X, y, trees = problem()
+    B, U = o.make_binary, o.make_unary
+    x1, x4 = Node("x1"), Node("x4")
+    single = B("-", B("+", B("+", U("cos", x4), U("cos", x4)), B("*", x1, x1)), Node(val=1.5))
+    trees.append(single)
     o.optimizer_algorithm = "NelderMead"
-    with pytest.raises(srhip.Unsupported):
-        srhip.optimize_constants_batch(srhip.Dataset(X, y), trees, o)
+    o.optimizer_iterations = 600
+    ds = srhip.Dataset(X, y)
+    res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(0),
+                                         evaluator_factory=oracle_factory(o, X, y))
+    assert res.converged[0] and res.converged[1] and res.converged[3]
+    assert np.allclose(srhip.get_constants(trees[0]), [2.0, 1.0, -2.0], atol=1e-3)
+    assert np.allclose(srhip.get_constants(trees[1]), [2.0, 2.0], atol=1e-3)
+    assert np.allclose(srhip.get_constants(trees[3]), [2.0], atol=1e-9)  # Newton: exact
+    assert res.losses[0] < 1e-6 and res.losses[3] < 1e-12
+    assert res.num_evals[0] > 3 * 8  # 3 starts, each at least its simplex and a few iterations
+
+
+def test_nelder_mead_default_iterations_never_worse():
+    """8 iterations (Options.jl optimizer_iterations): a converged start only
+    replaces x0 when its loss is the minimum; else x0 stays (:56-63)."""
+    o, X, y, _ = problem()
+    o.optimizer_algorithm = "NelderMead"
+    pop = srhip.random_population(40, o, 5, np.float64, seed=11, maxsize=15)
+    pop = [t for t in pop if len(srhip.get_constants(t)) >= 2]
+    assert len(pop) >= 5
+    x0 = [list(srhip.get_constants(t)) for t in pop]
+    ev = OracleEvaluator([t.copy() for t in pop], o, X, y)
+    f0 = ev.loss_only(np.concatenate([np.asarray(c, dtype=np.float64) for c in x0]))
+    ds = srhip.Dataset(X, y)
+    res = srhip.optimize_constants_batch(ds, pop, o, rng=np.random.default_rng(3),
+                                         evaluator_factory=oracle_factory(o, X, y))
+    for i, t in enumerate(pop):
+        if res.converged[i]:  # the simplex minimum never exceeds its x0 vertex
+            assert res.losses[i] <= f0[i] * (1 + 1e-12) or not np.isfinite(f0[i])
+        else:
+            assert srhip.get_constants(t) == x0[i]
+            assert res.losses[i] == f0[i] or not np.isfinite(f0[i])
+        assert res.num_evals[i] >= 3 * (len(x0[i]) + 1)
+
+
+def test_unknown_algorithm_raises():
+    o, X, y, trees = problem()
+    o.optimizer_algorithm = "LBFGS"
+    with pytest.raises(ValueError):
+        srhip.optimize_constants_batch(srhip.Dataset(X, y), trees, o,
+                                       evaluator_factory=oracle_factory(o, X, y))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("T", [np.float64, np.float32])
+def test_engine_nelder_mead(gpu_ctx, T):
+    """The batched Nelder-Mead on the engine (loss-only launches: points and
+    whole simplices) recovers the known constants like the oracle-driven run."""
+    o, X, y, trees = problem(T)
+    _, _, _, trees_ref = problem(T)
+    for oo in (o,):
+        oo.optimizer_algorithm = "NelderMead"
+        oo.optimizer_iterations = 600
+    ds = srhip.Dataset(X, y)
+    res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(0))
+    ref = srhip.optimize_constants_batch(ds, trees_ref, o, rng=np.random.default_rng(0),
+                                         evaluator_factory=oracle_factory(o, X, y))
+    atol = 1e-3 if T == np.float64 else 5e-3
+    assert res.converged[0] and ref.converged[0]
+    assert np.allclose(srhip.get_constants(trees[0]), [2.0, 1.0, -2.0], atol=atol)
+    assert np.allclose(srhip.get_constants(trees[0]), srhip.get_constants(trees_ref[0]), atol=2 * atol)
+    assert res.losses[0] < (1e-6 if T == np.float64 else 1e-4)
 
 
 @pytest.mark.gpu
