@@ -237,6 +237,13 @@ int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, i
  * rebuild (folding or a static verdict changed, or the first new constant set
  * of a tree-code program, which runs interpreted from then on). */
 int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inplace, int64_t* out_rebuilt);
+/* Gradient tree code of this program (reverse-mode ∂L/∂c for
+ * srhip_eval_loss_grad with the L2 loss, built on the first gradient call):
+ * trees compiled, trees left to the forward-mode interpreter, code bytes,
+ * codegen and load times (ms). All zero before the first gradient call or for
+ * Float64 programs. */
+int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nrejected,
+                                    int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load);
 /* Trees of the last eval on this context whose tree code handed a tile back
  * (a sin/cos argument beyond the fast reduction) and were re-evaluated, and
  * tiles that tree code redid with the Float64-evaluated routines (a FAST-path
@@ -249,6 +256,11 @@ int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* ou
 int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_bytes, int64_t* inout_nbytes,
                           char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
                           int64_t* inout_noffsets);
+/* Testing hook, same contract: the gradient tree code (reverse-mode ∂L/∂c,
+ * the fast path of srhip_eval_loss_grad) of Float32 trees. */
+int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int64_t* inout_nbytes,
+                               char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
+                               int64_t* inout_noffsets);
 
 /* ---- instrumentation ----------------------------------------------------
  * Device time (ms, HIP events on the context's stream) of the evaluation

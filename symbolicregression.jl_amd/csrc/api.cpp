@@ -105,6 +105,7 @@ struct srhip_ctx {
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
   DevBuf ti_rec;  // threaded-interpreter records of the shallow f32 list
   DevBuf bail_list, bail_fail;  // trees whose tree code handed a tile back, and their flags
+  DevBuf gpart;  // [nrg][nconst] per-row-group ∂L/∂c of the gradient tree code
   std::vector<double> h_sum;
   std::vector<uint8_t> h_ok;
 };
@@ -165,6 +166,17 @@ struct srhip_program {
   // work items by pass: shallow items carrying 1, 2 or kGradG tangents, then deep ones
   int ngitems[4] = {0, 0, 0, 0};
   int g_opset = OPSET_FULL;
+  // gradient tree code (jit_grad.cpp) of the Float32 trees it can compile;
+  // with it, the interpreter runs the remaining trees' items (ngitems_rest,
+  // stored after the ngitems[] items in d_gitems)
+  jit::GradModule* gjit = nullptr;
+  jit::GradStats gjit_stats;
+  int ngitems_rest[4] = {0, 0, 0, 0};
+  int32_t* d_gjit_list = nullptr;   // [nslots] tree of each gradient-code slot
+  int32_t* d_gjit_cidx = nullptr;   // constants of those trees
+  int ngjit_cidx = 0;
+  float* d_gconsts = nullptr;       // the constants as Float32 (+16 padding)
+  size_t gjl_cap = 0, gjc_cap = 0, gcs_cap = 0;
   // byte capacities of the device buffers above (kept across rebuilds)
   size_t code_cap = 0, toff_cap = 0, list_cap = 0;
   size_t gcode_cap = 0, gtoff_cap = 0, gitems_cap = 0, gconst_cap = 0;
@@ -185,12 +197,39 @@ void ensure_dev(void** ptr, size_t* cap, size_t bytes) {
 }
 
 void free_grad_device(srhip_program* p) {
-  for (void* q : {p->d_gcode, (void*)p->d_gtree_off, (void*)p->d_gitems, (void*)p->d_const_off})
+  for (void* q : {p->d_gcode, (void*)p->d_gtree_off, (void*)p->d_gitems, (void*)p->d_const_off,
+                  (void*)p->d_gjit_list, (void*)p->d_gjit_cidx, (void*)p->d_gconsts})
     if (q) (void)hipFree(q);
   p->d_gcode = nullptr;
   p->d_gtree_off = p->d_gitems = p->d_const_off = nullptr;
+  p->d_gjit_list = p->d_gjit_cidx = nullptr;
+  p->d_gconsts = nullptr;
   p->gcode_cap = p->gtoff_cap = p->gitems_cap = p->gconst_cap = 0;
+  p->gjl_cap = p->gjc_cap = p->gcs_cap = 0;
+  jit::destroy_grad(p->gjit);
+  p->gjit = nullptr;
   p->grad_built = false;
+}
+
+// Gradient tree code on/off: SRHIP_GJIT=0 never, =1 for every Float32
+// program, default for programs of at least 256 trees (loading a code object
+// costs about a millisecond).
+bool gjit_wanted(int ntrees) {
+  if (!jit::available() || ntrees == 0) return false;
+  const char* e = std::getenv("SRHIP_GJIT");
+  if (e && e[0] == '0') return false;
+  if (e && e[0] == '1') return true;
+  return ntrees >= 256;
+}
+
+// the Float32 constants the gradient tree code reads (s_load), 16 floats of padding
+void upload_gconsts(srhip_program* p) {
+  const size_t nconst = p->const_off.back();
+  std::vector<float> h(nconst + 16, 0.0f);
+  if (nconst) std::memcpy(h.data(), p->consts.data(), nconst * sizeof(float));
+  ensure_dev((void**)&p->d_gconsts, &p->gcs_cap, h.size() * sizeof(float));
+  HIP_CHECK(hipMemcpyAsync(p->d_gconsts, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, p->ctx->stream));
+  HIP_CHECK(hipStreamSynchronize(p->ctx->stream));
 }
 
 void free_program_device(srhip_program* p) {
@@ -229,27 +268,54 @@ void build_grad_program(srhip_program* p) {
                        : opc >= OP_UN0 && !opset_has_uop(OPSET_BASIC, opc - OP_UN0))
       p->g_opset = OPSET_FULL;
   }
-  // a work item carries the tangents of its group only: groups of 1 and 2
-  // constants run in kernels with fewer tangents (and more rows per lane)
-  std::vector<std::pair<int, int32_t>> cls[4];  // (cost, item)
-  for (int t = 0; t < p->ntrees; ++t) {
-    if (cb.tree_off[t] < 0) continue;
-    const int nc = p->const_off[t + 1] - p->const_off[t];
-    const int ngroups = std::max(1, (nc + kGradG - 1) / kGradG);
-    for (int gi = 0; gi < ngroups; ++gi) {
-      const int ntan = std::min(kGradG, nc - gi * kGradG);
-      const int k = cb.need[t] > 4 ? 3 : ntan <= 1 ? 0 : ntan <= 2 ? 1 : 2;
-      cls[k].push_back({cb.cost[t], (int32_t)(t | (gi << 24))});
+  // gradient tree code for the Float32 trees it can compile (cost-sorted slots)
+  jit::destroy_grad(p->gjit);
+  p->gjit = nullptr;
+  p->gjit_stats = jit::GradStats();
+  std::vector<uint8_t> in_jit(p->ntrees, 0);
+  std::vector<int32_t> gjl, gcidx;
+  if constexpr (std::is_same<T, float>::value) {
+    std::vector<int32_t> cand;
+    for (int t = 0; t < p->ntrees; ++t)
+      if (cb.tree_off[t] >= 0) cand.push_back(t);
+    if (gjit_wanted((int)cand.size())) {
+      std::stable_sort(cand.begin(), cand.end(), [&](int32_t x, int32_t y) {
+        return cb.cost[x] != cb.cost[y] ? cb.cost[x] > cb.cost[y] : x < y;
+      });
+      std::vector<int32_t> rest;
+      p->gjit = jit::build_grad(cb, p->const_off, cand, gjl, rest, &p->gjit_stats);
+      if (p->gjit)
+        for (int32_t t : gjl) {
+          in_jit[t] = 1;
+          for (int k = p->const_off[t]; k < p->const_off[t + 1]; ++k) gcidx.push_back(k);
+        }
+      else
+        gjl.clear();
     }
   }
+  // a work item carries the tangents of its group only: groups of 1 and 2
+  // constants run in kernels with fewer tangents (and more rows per lane)
   auto by_cost = [](const std::pair<int, int32_t>& x, const std::pair<int, int32_t>& y) {
     return x.first != y.first ? x.first > y.first : x.second < y.second;
   };
   std::vector<int32_t> items;
-  for (int k = 0; k < 4; ++k) {
-    std::stable_sort(cls[k].begin(), cls[k].end(), by_cost);
-    for (auto& q : cls[k]) items.push_back(q.second);
-    p->ngitems[k] = (int)cls[k].size();
+  for (int rest_only = 0; rest_only < 2; ++rest_only) {
+    std::vector<std::pair<int, int32_t>> cls[4];  // (cost, item)
+    for (int t = 0; t < p->ntrees; ++t) {
+      if (cb.tree_off[t] < 0 || (rest_only && in_jit[t])) continue;
+      const int nc = p->const_off[t + 1] - p->const_off[t];
+      const int ngroups = std::max(1, (nc + kGradG - 1) / kGradG);
+      for (int gi = 0; gi < ngroups; ++gi) {
+        const int ntan = std::min(kGradG, nc - gi * kGradG);
+        const int k = cb.need[t] > 4 ? 3 : ntan <= 1 ? 0 : ntan <= 2 ? 1 : 2;
+        cls[k].push_back({cb.cost[t], (int32_t)(t | (gi << 24))});
+      }
+    }
+    for (int k = 0; k < 4; ++k) {
+      std::stable_sort(cls[k].begin(), cls[k].end(), by_cost);
+      for (auto& q : cls[k]) items.push_back(q.second);
+      (rest_only ? p->ngitems_rest : p->ngitems)[k] = (int)cls[k].size();
+    }
   }
   std::vector<int32_t> toff(cb.tree_off);
   for (auto& v : toff) v = std::max(v, 0);
@@ -265,7 +331,16 @@ void build_grad_program(srhip_program* p) {
     HIP_CHECK(hipMemcpyAsync(p->d_gitems, items.data(), items.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
   HIP_CHECK(hipMemcpyAsync(p->d_const_off, p->const_off.data(), p->const_off.size() * sizeof(int32_t),
                            hipMemcpyHostToDevice, s));
+  p->ngjit_cidx = (int)gcidx.size();
+  if (p->gjit) {
+    ensure_dev((void**)&p->d_gjit_list, &p->gjl_cap, gjl.size() * sizeof(int32_t));
+    HIP_CHECK(hipMemcpyAsync(p->d_gjit_list, gjl.data(), gjl.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+    ensure_dev((void**)&p->d_gjit_cidx, &p->gjc_cap, std::max<size_t>(gcidx.size(), 1) * sizeof(int32_t));
+    if (!gcidx.empty())
+      HIP_CHECK(hipMemcpyAsync(p->d_gjit_cidx, gcidx.data(), gcidx.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
+  }
   HIP_CHECK(hipStreamSynchronize(s));
+  if (p->gjit) upload_gconsts(p);
   p->h_gcode.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
                     reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   p->h_gtoff = cb.tree_off;
@@ -421,6 +496,7 @@ void update_constants(srhip_program* p) {
       p->h_gcode.assign(reinterpret_cast<const unsigned char*>(gb.code.data()),
                         reinterpret_cast<const unsigned char*>(gb.code.data() + gb.code.size()));
       HIP_CHECK(hipMemcpyAsync(p->d_gcode, p->h_gcode.data(), p->h_gcode.size(), hipMemcpyHostToDevice, s));
+      if (p->gjit) upload_gconsts(p);
     } else {
       p->grad_built = false;  // rebuilt on next use
     }
@@ -722,9 +798,74 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
   c->sums.ensure(std::max<size_t>(nt, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(nt, 1));
   c->dloss.ensure(std::max<size_t>(nconst, 1) * sizeof(double));
+  // gradient tree code (L2 loss, ∂L/∂c) for the trees it holds; the
+  // interpreter items of the other trees follow
+  bool use_gjit = false;
+  if constexpr (std::is_same<T, float>::value) {
+    if (p->gjit && mode == GRAD_LOSS && loss == SRHIP_LOSS_L2 && ds->rows > 0) {
+      const int nparts = jit::grad_nparts(p->gjit);
+      const int narr = 1 + ds->nfeat + (ds->w ? 1 : 0);
+      std::vector<EvalPlan> plans(nparts);
+      use_gjit = true;
+      for (int k = 0; k < nparts && use_gjit; ++k) {
+        int s0, nsl;
+        jit::grad_part(p->gjit, k, &s0, &nsl);
+        use_gjit = plan_geometry(4, 4, kShallowSlots, narr, 2 * 4, ds->rows, nsl, &plans[k]) &&
+                   plans[k].lds_bytes + jit::grad_lds_extra() <= 160 * 1024 && plans[k].nrg == plans[0].nrg;
+      }
+      if (use_gjit) {
+        const int nsl_all = jit::grad_nslots(p->gjit);
+        c->fail.ensure((size_t)nsl_all * sizeof(uint32_t));
+        HIP_CHECK(hipMemsetAsync(c->fail.p, 0, (size_t)nsl_all * sizeof(uint32_t), s));
+        c->gpart.ensure(std::max<size_t>((size_t)plans[0].nrg * nconst, 1) * sizeof(float));
+        for (int k = 0; k < nparts; ++k) {
+          int s0, nsl;
+          jit::grad_part(p->gjit, k, &s0, &nsl);
+          const EvalPlan& plan = plans[k];
+          EvalArgs<float> a;
+          std::memset(&a, 0, sizeof(a));
+          a.list = p->d_gjit_list + s0;
+          a.fail = static_cast<uint32_t*>(c->fail.p) + s0;
+          a.nlist = nsl;
+          a.X = static_cast<const float*>(ds->X);
+          a.y = static_cast<const float*>(ds->y);
+          a.w = static_cast<const float*>(ds->w);
+          a.n = ds->rows;
+          a.n_pad = ds->n_pad;
+          a.nfeat = ds->nfeat;
+          a.ntiles = plan.ntiles;
+          a.ntg = plan.ntg;
+          a.tpb = plan.tpb;
+          a.nrg = plan.nrg;
+          a.loss = loss;
+          c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<float>));
+          a.partial = static_cast<Part<float>*>(c->partial.p);
+          HIP_CHECK(hipEventRecord(c->ev[0], s));
+          HIP_CHECK(jit::launch_grad_code(p->gjit, k, plan, a, p->d_gconsts, static_cast<float*>(c->gpart.p), nconst,
+                                          s));
+          HIP_CHECK(hipEventRecord(c->ev[1], s));
+          HIP_CHECK(launch_finalize<float>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
+          HIP_CHECK(hipEventSynchronize(c->ev[1]));
+          float ms = 0.f;
+          HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
+          c->last_ms += ms;
+          c->last_launches += 1;
+          static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
+          if (dbg)
+            std::fprintf(stderr, "srhip grad tree code part %d: %d trees, %.3f ms (grid %d x %d, %d tiles/wg)\n", k,
+                         nsl, ms, plan.nrg, plan.ntg, plan.ntiles);
+        }
+        HIP_CHECK(launch_gconst_finalize(static_cast<const float*>(c->gpart.p), plans[0].nrg, nconst,
+                                         p->d_gjit_cidx, p->ngjit_cidx, static_cast<double*>(c->dloss.p), s));
+      }
+    }
+  }
+  const int* ngi = use_gjit ? p->ngitems_rest : p->ngitems;
   int first = 0;
+  if (use_gjit)
+    for (int k = 0; k < 4; ++k) first += p->ngitems[k];
   for (int pass = 0; pass < 4; ++pass) {
-    const int nitems = p->ngitems[pass];
+    const int nitems = ngi[pass];
     const int item0 = first;
     first += nitems;
     if (nitems == 0 || ds->rows == 0) continue;
@@ -1265,6 +1406,20 @@ int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inpla
   });
 }
 
+int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nrejected,
+                                    int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load) {
+  return guarded([&] {
+    if (!prog) throw Error(SRHIP_ERR_INVALID, "null program");
+    const bool on = prog->gjit != nullptr;
+    if (out_ntrees) *out_ntrees = on ? prog->gjit_stats.ntrees : 0;
+    if (out_nrejected) *out_nrejected = on ? prog->gjit_stats.nrejected : 0;
+    if (out_code_bytes) *out_code_bytes = on ? (int64_t)prog->gjit_stats.code_bytes : 0;
+    if (out_ms_codegen) *out_ms_codegen = on ? prog->gjit_stats.ms_codegen : 0.0;
+    if (out_ms_load) *out_ms_load = on ? prog->gjit_stats.ms_load : 0.0;
+    return SRHIP_OK;
+  });
+}
+
 int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nfast,
                                int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load) {
   return guarded([&] {
@@ -1288,23 +1443,31 @@ int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* ou
   });
 }
 
-int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_bytes, int64_t* inout_nbytes,
-                          char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
-                          int64_t* inout_noffsets) {
+namespace {
+int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes, int64_t* inout_nbytes,
+                         char* out_text, int64_t* inout_ntext, int32_t* out_offsets, int64_t* inout_noffsets) {
   return guarded([&] {
     if (!trees || !inout_nbytes || !inout_ntext || !inout_noffsets) throw Error(SRHIP_ERR_INVALID, "null argument");
     if (!jit::available()) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("tree compiler: ") + jit::unavailable_reason());
-    CompiledBatch<float> cb = compile_batch<float>(*trees);
-    std::vector<int32_t> cand;
-    for (int t = 0; t < cb.ntrees; ++t)
-      if (cb.tree_off[t] >= 0 && cb.need[t] <= kShallowSlots) cand.push_back(t);
-    jit::Options jo;
-    jo.fast = fast != 0;
-    jo.text = true;
     std::vector<uint8_t> bytes;
     std::string text;
     std::vector<int32_t> offs;
-    jit::compile_only(cb, cand, jo, &bytes, &text, &offs, nullptr);
+    if (mode == 2) {  // gradient tree code
+      CompiledBatch<float> cb = compile_batch<float>(*trees, /*grad=*/true);
+      std::vector<int32_t> cand, coff(trees->const_off, trees->const_off + trees->ntrees + 1);
+      for (int t = 0; t < cb.ntrees; ++t)
+        if (cb.tree_off[t] >= 0) cand.push_back(t);
+      jit::compile_grad_only(cb, coff, cand, &bytes, &text, &offs, nullptr);
+    } else {
+      CompiledBatch<float> cb = compile_batch<float>(*trees);
+      std::vector<int32_t> cand;
+      for (int t = 0; t < cb.ntrees; ++t)
+        if (cb.tree_off[t] >= 0 && cb.need[t] <= kShallowSlots) cand.push_back(t);
+      jit::Options jo;
+      jo.fast = mode != 0;
+      jo.text = true;
+      jit::compile_only(cb, cand, jo, &bytes, &text, &offs, nullptr);
+    }
     if ((int64_t)bytes.size() > *inout_nbytes || (int64_t)text.size() + 1 > *inout_ntext ||
         (int64_t)offs.size() > *inout_noffsets) {
       *inout_nbytes = (int64_t)bytes.size();
@@ -1320,4 +1483,18 @@ int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_b
     *inout_noffsets = (int64_t)offs.size();
     return SRHIP_OK;
   });
+}
+}  // namespace
+
+int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_bytes, int64_t* inout_nbytes,
+                          char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
+                          int64_t* inout_noffsets) {
+  return jit_compile_hook(trees, fast ? 1 : 0, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets,
+                          inout_noffsets);
+}
+
+int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int64_t* inout_nbytes,
+                               char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
+                               int64_t* inout_noffsets) {
+  return jit_compile_hook(trees, 2, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets, inout_noffsets);
 }

@@ -432,6 +432,20 @@ def build(hipcc, outdir, R):
         f.write("#define SR_JIT_ROUTINE_BODY_BYTES {" + ", ".join(str(fs[n] - 4) for n in names) + "}\n")
         f.write("#define SR_JIT_CLOBBERS " + ", ".join([f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s]
                                                           + ['"vcc"', '"scc"', '"m0"']) + "\n")
+        # gradient tree code (jit_grad.cpp): the same routines, a larger value
+        # pool, per-constant accumulators, constants in SGPRs
+        g = dict(VSCR=44, GPOOL0=56, GNPOOL=20, GACC=136, NGACC=16, SC0=24, SCPTR=78)
+        assert g["GPOOL0"] + 4 * g["GNPOOL"] == g["GACC"]
+        assert max(stemp) < g["SC0"] and g["SC0"] % 4 == 0
+        for k, v in g.items():
+            f.write(f"#define SR_JIT_G_{k} {v}\n")
+        gin_v = {rg.CHK, rg.LANE, rg.LSUM, rg.LANE4, g["VSCR"]}
+        gclob_v = sorted((vtemp | set(range(rg.A, g["GACC"] + g["NGACC"]))) - gin_v)
+        gin_s = {rg.S[k] for k in ("tile", "nt", "partial", "tilebytes", "woff", "status")} | \
+            {g["SCPTR"], g["SCPTR"] + 1}
+        gclob_s = sorted((stemp | sstate | set(range(g["SC0"], g["SC0"] + g["NGACC"]))) - gin_s)
+        f.write("#define SR_JIT_GRAD_CLOBBERS " + ", ".join([f'"v{r}"' for r in gclob_v] + [f'"s{r}"' for r in gclob_s]
+                                                               + ['"vcc"', '"scc"', '"m0"']) + "\n")
         f.write(f"// routine VGPR temps v{min(vtemp)}..v{max(vtemp)}, SGPR temps {sorted(stemp)}\n")
         f.write("// routine sizes (fast / precise bytes): " +
                 ", ".join(f"{n} {fs[n]}/{ps[n]}" for n in names) + "\n")

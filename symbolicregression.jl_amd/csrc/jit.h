@@ -58,5 +58,38 @@ hipError_t launch(Module* m, const EvalPlan& plan, const EvalArgs<float>& a, boo
 bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt,
                   std::vector<uint8_t>* bytes, std::string* text, std::vector<int32_t>* offsets, Stats* st);
 
+// ---- gradient tree code (jit_grad.cpp) ----------------------------------------------
+// Reverse-mode ∂L/∂c of every constant of a tree in one pass (L2 loss), for
+// gradient programs (compile_batch(..., grad = true)) of Float32 trees whose
+// operators are + - * / neg abs square cube exp sin cos and that have at
+// most SR_JIT_G_NGACC constants. Constants are read from a device array at
+// run time: new constant sets need no new code.
+struct GradModule;
+struct GradStats {
+  int ntrees = 0;
+  int nrejected = 0;
+  int nparts = 0;          // code objects (one launch each)
+  size_t code_bytes = 0;
+  double ms_codegen = 0.0, ms_load = 0.0;
+};
+GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
+                       const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list, std::vector<int32_t>& rest,
+                       GradStats* st);
+void destroy_grad(GradModule* m);
+int grad_nslots(const GradModule* m);
+// the module's code objects: consecutive slot ranges, one launch each
+int grad_nparts(const GradModule* m);
+void grad_part(const GradModule* m, int k, int* slot0, int* nslots);
+// LDS the gradient driver needs beyond the eval plan's (per-wave accumulator scratch)
+size_t grad_lds_extra();
+// Launch part `part` over its slots (EvalArgs as for launch(): list / fail /
+// partial of the slots); consts = the program's constants (+16 readable
+// floats of padding), gpart = [nrg][nconst] per-row-group ∂L/∂c partials.
+hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const EvalArgs<float>& a,
+                            const float* consts, float* gpart, int nconst, hipStream_t stream);
+bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
+                       const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
+                       std::vector<int32_t>* offsets, GradStats* st);
+
 }  // namespace jit
 }  // namespace srhip

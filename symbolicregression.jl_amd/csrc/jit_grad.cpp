@@ -1,0 +1,967 @@
+// jit_grad.cpp — gradient tree code: every tree of a Float32 gradient program
+// becomes straight-line gfx950 machine code that computes, per tile of 256
+// rows, the forward values, the L2 loss and the REVERSE-mode adjoints of its
+// constants: Σ_rows w·ℓ'(r)·∂ŷ/∂c_j for every constant c_j of the tree in one
+// pass, whatever the constant count.
+//
+// It replaces, for the batched constant optimiser (srhip_eval_loss_grad), the
+// forward-mode interpreter of grad_kernels.hip, which carries 1-4 tangents per
+// pass and so re-runs the whole tree once per group of four constants with a
+// switch dispatch per node. Reference: ConstantOptimization.jl:12-65 (the
+// loss whose gradient BFGS needs), InterfaceDynamicExpressions.jl:105-107
+// (eval_grad_tree_array(...; variable=false)).
+//
+// Tree code layout (driver: sr_jit_grad in jit_template.hip):
+//   prologue   s_load of the tree's constants into s[SC0 ..] (they are never
+//              literals, so new constant sets need no new code), accumulators
+//              zeroed, routine base
+//   tile loop  forward: values in pool blocks of 4 VGPRs (R = 4 rows per
+//              lane), + - * neg abs square cube inline, / exp sin cos by the
+//              PRECISE routines of gen_jit.py (same code as the loss tree
+//              code and the interpreters: did_succeed and values identical);
+//              every value the reverse pass needs stays in its block;
+//              root mark, a failed tile ends the tree;
+//              loss: r = ŷ - y masked past the last row, Σ w·r², seed 2·w·r;
+//              reverse: adjoints in pool blocks, one per value, sign carried
+//              as a flag (neg / sub cost nothing); a constant's adjoint is
+//              summed over the lane's rows into its accumulator VGPR; sin /
+//              cos derivatives call the FAST cos / sin routines (<= 2 ulp),
+//              1/b by v_rcp_f32 (the interpreter's rules, device_ops.h uop_d /
+//              bop_d); subtrees without constants get no reverse code at all
+//   epilogue   accumulators to the wave's LDS scratch, return
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+
+#include "jit.h"
+#include "jit_asm.h"
+
+#define HIP_CHECK(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw Error(SRHIP_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));  \
+  } while (0)
+
+namespace srhip {
+namespace jit {
+namespace {
+
+using namespace detail;
+
+constexpr int VSCR = SR_JIT_G_VSCR, GPOOL0 = SR_JIT_G_GPOOL0, GNPOOL = SR_JIT_G_GNPOOL;
+constexpr int GACC = SR_JIT_G_GACC, NGACC = SR_JIT_G_NGACC, SC0 = SR_JIT_G_SC0, SCPTR = SR_JIT_G_SCPTR;
+// scratch VGPRs of tree code (routine temps: free between calls)
+constexpr int XS0 = 0, XS1 = 4;   // feature values read in the reverse pass
+constexpr int TS = 8;             // 2 registers: row sums
+constexpr int TP = 12, TR = 16, TQ = 20;  // product / reciprocal / quotient-adjoint blocks
+enum : int { VOP1_RCP_F32 = 0x22, VOPC_NEQ_F32 = 0x4d, VOP3_MUL_F32 = 0x105 };
+
+// ---- IR: the accumulator machine of a gradient program, renamed ----------------
+enum { G_VAL = 0, G_X = 1, G_C = 2 };
+struct GOpnd {
+  int k = G_VAL;
+  int v = -1;   // value id (G_VAL) or feature (G_X)
+  int ci = -1;  // constant index within the tree (G_C)
+};
+enum { K_UN = 0, K_BIN = 1, K_MAT = 2 };  // K_MAT: a constant broadcast into a block
+struct GOp {
+  int kind = K_UN;
+  int op = 0;
+  GOpnd a, b;
+  int rid = -1, krid = -1;
+  int consumer = -1;
+};
+
+constexpr uint32_t kGradUops = (1u << SRHIP_UOP_NEG) | (1u << SRHIP_UOP_ABS) | (1u << SRHIP_UOP_SQUARE) |
+                               (1u << SRHIP_UOP_CUBE) | (1u << SRHIP_UOP_EXP) | (1u << SRHIP_UOP_SIN) |
+                               (1u << SRHIP_UOP_COS);
+constexpr uint32_t kGradBops = (1u << SRHIP_BOP_ADD) | (1u << SRHIP_BOP_SUB) | (1u << SRHIP_BOP_MUL) |
+                               (1u << SRHIP_BOP_DIV);
+
+bool g_inline(const GOp& o) {
+  if (o.kind == K_MAT) return true;
+  return o.kind == K_UN ? (o.op == SRHIP_UOP_NEG || o.op == SRHIP_UOP_ABS || o.op == SRHIP_UOP_SQUARE ||
+                           o.op == SRHIP_UOP_CUBE)
+                        : (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB || o.op == SRHIP_BOP_MUL);
+}
+
+bool build_gir(const Ins<float>* p, std::vector<GOp>& ops, GOpnd& root, std::string* why) {
+  ops.clear();
+  GOpnd acc, tmp, slot[kMaxSlots];
+  auto val = [&](const GOp& o) {
+    ops.push_back(o);
+    GOpnd r;
+    r.k = G_VAL;
+    r.v = (int)ops.size() - 1;
+    return r;
+  };
+  auto mat = [&](const GOpnd& c) {  // a constant operand that must live in a block
+    GOp m;
+    m.kind = K_MAT;
+    m.a = c;
+    return val(m);
+  };
+  for (int pc = 0;; ++pc) {
+    if (pc > 4096) { *why = "program too long"; return false; }
+    const uint32_t code = p[pc].code;
+    const int opc = (int)(code & 0xffu);
+    const int slotf = (int)((code >> 8) & 0xffu);
+    const int f = (int)(code >> 16);
+    auto X = [&](int ff) { GOpnd o; o.k = G_X; o.v = ff; return o; };
+    auto C = [&]() { GOpnd o; o.k = G_C; o.ci = slotf; return o; };
+    if (opc == OP_END) { root = acc; return true; }
+    if (opc == OP_LDX) { acc = X(f); continue; }
+    if (opc == OP_LDC) { acc = C(); continue; }
+    if (opc >= OP_PUSH0 && opc < OP_PUSH0 + kMaxSlots) { slot[opc - OP_PUSH0] = acc; continue; }
+    if (opc >= OP_POP0 && opc < OP_POP0 + kMaxSlots) { tmp = slot[opc - OP_POP0]; continue; }
+    if (opc >= OP_UN0 && opc < OP_BIN0) {
+      GOp o;
+      o.kind = K_UN;
+      o.op = opc - OP_UN0;
+      if (!((kGradUops >> o.op) & 1u)) { *why = "unary operator without gradient code"; return false; }
+      o.a = acc.k == G_C ? mat(acc) : acc;
+      acc = val(o);
+      continue;
+    }
+    const int v = (opc - OP_BIN0) / SRHIP_NUM_BOPS;
+    GOp o;
+    o.kind = K_BIN;
+    o.op = (opc - OP_BIN0) % SRHIP_NUM_BOPS;
+    if (!((kGradBops >> o.op) & 1u)) { *why = "binary operator without gradient code"; return false; }
+    float imm = p[pc].imm;
+    uint32_t g;
+    std::memcpy(&g, &imm, 4);
+    switch (v) {
+      case V_AX: o.a = acc; o.b = X(f); break;
+      case V_XA: o.a = X(f); o.b = acc; break;
+      case V_AC: o.a = acc; o.b = C(); break;
+      case V_CA: o.a = C(); o.b = acc; break;
+      case V_AT: o.a = acc; o.b = tmp; break;
+      case V_TA: o.a = tmp; o.b = acc; break;
+      case V_XX: o.a = X(f); o.b = X((int)g); break;
+      case V_XC: o.a = X(f); o.b = C(); break;
+      case V_CX: o.a = C(); o.b = X(f); break;
+      default: *why = "bad variant"; return false;
+    }
+    if (o.a.k == G_C && o.b.k == G_C) o.a = mat(o.a);
+    acc = val(o);
+  }
+}
+
+// ---- code generation of one tree ---------------------------------------------------
+struct GradGen {
+  Asm& as;
+  const Tmpl& T;
+  uint64_t base_va;
+  std::vector<GOp> ops;
+  GOpnd root;
+  int nc = 0;              // constants of the tree
+  std::string why;
+  int n = 0;
+  std::vector<uint8_t> hasc;      // value's subtree holds a constant: it needs an adjoint
+  std::vector<int> last;          // last step (forward i, loss n, reverse 2n-i) that reads the value
+  std::vector<int> loc;           // pool block of each value, -1 none
+  int owner[GNPOOL];              // pool block: -1 free, value id, 1000 + feature (forward), 2000 + k adjoint
+  int refs[GNPOOL];               // adjoint references of a block
+  struct Adj { int reg = -1; int blk = -2; bool neg = false; };  // blk -1: the seed block Y
+  std::vector<Adj> adj;
+  int xblk[256], xlast[256], load_idx[256];
+  bool xinl[256];
+  std::vector<int> feats;
+  int nloads = 0, waited = 0;
+  bool has_call = false;
+  int L_tile = -1, L_done = -1;
+
+  GradGen(Asm& a, const Tmpl& t, uint64_t va) : as(a), T(t), base_va(va) {}
+  uint64_t cur_va() const { return base_va + as.bytes(); }
+  static int blk_reg(int k) { return GPOOL0 + R * k; }
+  int bstep(int i) const { return 2 * n - i; }  // reverse steps n+1 .. 2n (n: the loss)
+  bool needs_adj(const GOpnd& q) const { return q.k == G_C || (q.k == G_VAL && hasc[q.v]); }
+
+  bool analyze() {
+    n = (int)ops.size();
+    hasc.assign(n, 0);
+    last.assign(n, -1);
+    loc.assign(n, -1);
+    adj.assign(n, Adj());
+    for (int i = 0; i < n; ++i) {
+      GOp& o = ops[i];
+      auto hc = [&](const GOpnd& q) { return q.k == G_C || (q.k == G_VAL && hasc[q.v]); };
+      hasc[i] = o.kind == K_MAT || hc(o.a) || (o.kind == K_BIN && hc(o.b));
+      if (o.a.k == G_C && o.kind != K_MAT && o.a.ci >= nc) { why = "constant index out of range"; return false; }
+      if (o.kind == K_BIN && o.b.k == G_C && o.b.ci >= nc) { why = "constant index out of range"; return false; }
+      if (!g_inline(o)) {
+        o.rid = o.kind == K_UN ? kUopRoutine[o.op] : kBopRoutine[o.op];
+        if (o.rid < 0) { why = "operator without routine"; return false; }
+        if (o.kind == K_BIN && o.b.k == G_C && o.a.k != G_C) o.krid = kBopRoutineRC[o.op];
+        if (o.kind == K_BIN && o.a.k == G_C && o.b.k != G_C) o.krid = kBopRoutineLC[o.op];
+        has_call = true;
+      }
+      for (int s = 0; s < 2; ++s) {
+        const GOpnd& q = s ? o.b : o.a;
+        if (s && o.kind != K_BIN) break;
+        if (q.k == G_VAL) { ops[q.v].consumer = i; last[q.v] = std::max(last[q.v], i); }
+      }
+    }
+    if (root.k == G_C && root.ci >= nc) { why = "constant index out of range"; return false; }
+    // reverse-pass reads of saved values (operands and own results)
+    for (int i = 0; i < n; ++i) {
+      const GOp& o = ops[i];
+      if (!hasc[i] || o.kind == K_MAT) continue;
+      auto use = [&](const GOpnd& q) {
+        if (q.k == G_VAL) last[q.v] = std::max(last[q.v], bstep(i));
+      };
+      if (o.kind == K_BIN) {
+        const bool aa = needs_adj(o.a), ab = needs_adj(o.b);
+        if (o.op == SRHIP_BOP_MUL) {
+          if (ab) use(o.a);
+          if (aa) use(o.b);
+        } else if (o.op == SRHIP_BOP_DIV) {
+          use(o.b);
+          if (ab) last[i] = std::max(last[i], bstep(i));  // the quotient
+        }
+      } else {
+        if (o.op == SRHIP_UOP_EXP) last[i] = std::max(last[i], bstep(i));
+        else if (o.op != SRHIP_UOP_NEG) use(o.a);
+      }
+    }
+    if (root.k == G_VAL) last[root.v] = std::max(last[root.v], n);  // read by the loss step
+    // features: those read by inline operators (or as the root) are preloaded per tile
+    for (int f = 0; f < 256; ++f) { xblk[f] = -1; xlast[f] = -1; load_idx[f] = -1; xinl[f] = false; }
+    auto usef = [&](const GOpnd& q, int i, bool inl) {
+      if (q.k != G_X) return true;
+      if (q.v < 0 || q.v > 255) return false;
+      if (inl) {
+        if (!xinl[q.v]) feats.push_back(q.v);
+        xinl[q.v] = true;
+        xlast[q.v] = std::max(xlast[q.v], i);
+      }
+      return true;
+    };
+    for (int i = 0; i < n; ++i) {
+      const bool inl = g_inline(ops[i]);
+      if (!usef(ops[i].a, i, inl)) { why = "feature index"; return false; }
+      if (ops[i].kind == K_BIN && !usef(ops[i].b, i, inl)) { why = "feature index"; return false; }
+    }
+    if (!usef(root, n, true)) { why = "feature index"; return false; }
+    for (int f = 0; f < 256; ++f)
+      if (xlast[f] >= 0 && (1 + f) * TILE * 4 + 3 * 4 * 64 > 65535) { why = "feature offset beyond the DS immediate"; return false; }
+    if ((int)feats.size() > GNPOOL) { why = "more features than register blocks"; return false; }
+    return true;
+  }
+
+  // ---- pool
+  int free_block() const {
+    for (int k = 0; k < GNPOOL; ++k)
+      if (owner[k] == -1) return k;
+    return -1;
+  }
+  void free_values_at(int step) {
+    for (int v = 0; v < n; ++v)
+      if (last[v] == step && loc[v] >= 0 && owner[loc[v]] == v) { owner[loc[v]] = -1; loc[v] = -1; }
+  }
+  void free_feats_at(int step) {
+    for (int f : feats)
+      if (xlast[f] == step && xblk[f] >= 0 && owner[xblk[f]] == 1000 + f) owner[xblk[f]] = -1;
+  }
+  int new_adj_block(int v) {
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted (adjoints)"; return -1; }
+    owner[k] = 2000 + v;
+    refs[k] = 1;
+    return k;
+  }
+  void release_adj(const Adj& a) {
+    if (a.blk < 0) return;
+    if (--refs[a.blk] == 0) owner[a.blk] = -1;
+  }
+  void share_adj(int v, const Adj& g, bool flip) {
+    Adj a = g;
+    a.neg = g.neg != flip;
+    if (a.blk >= 0) ++refs[a.blk];
+    adj[v] = a;
+  }
+
+  // ---- emission helpers
+  void wait_for_feat(int f) {
+    const int li = load_idx[f];
+    if (li >= waited) {
+      as.waitcnt_lgkm(nloads - 1 - li);
+      waited = li + 1;
+    }
+  }
+  void wait_all() {
+    if (waited < nloads) { as.waitcnt_lgkm(0); waited = nloads; }
+  }
+  Src fsrc(const GOpnd& q, int e) const {  // forward operand source
+    if (q.k == G_C) return S(SC0 + q.ci);
+    if (q.k == G_X) return V(blk_reg(xblk[q.v]) + e);
+    return V(blk_reg(loc[q.v]) + e);
+  }
+  void read_feat(int dst, int f) {  // a feature block straight from the LDS tile
+    as.ds_read_b128(dst, VLANE, (1 + f) * TILE * 4);
+    as.waitcnt_lgkm(0);
+    waited = nloads;
+  }
+  void routine(int rid, bool precise) {
+    uint64_t off = T.rt_va[rid] - T.fast0 + (precise ? T.delta : 0);
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TGT, S(S_BASE), K((uint32_t)off));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_TGT + 1, S(S_BASE + 1), K((uint32_t)(off >> 32)));
+    as.sop1(SOP1_SWAPPC, "s_swappc_b64", S_RR, S(S_TGT), "s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "]");
+    if (as.want_text)
+      as.lines.back() = "s_swappc_b64 s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "], s[" +
+                        std::to_string(S_TGT) + ":" + std::to_string(S_TGT + 1) + "]";
+  }
+  void set_base() {
+    as.sop1(SOP1_GETPC, "s_getpc_b64", S_BASE, Src{0, false, 0}, "");
+    if (as.want_text) as.lines.back() = "s_getpc_b64 s[" + std::to_string(S_BASE) + ":" + std::to_string(S_BASE + 1) + "]";
+    const uint64_t pc_next = cur_va();
+    const int64_t rel = (int64_t)(T.fast0 - pc_next);
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_BASE, S(S_BASE), K((uint32_t)(uint64_t)rel));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_BASE + 1, S(S_BASE + 1), K((uint32_t)((uint64_t)rel >> 32)));
+  }
+  void mov4(int dst, int src) {
+    for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", dst + e, V(src + e));
+  }
+  // d = x * y (y a VGPR unless x is one)
+  void vmul(int d, const Src& x, const Src& y) {
+    if (y.enc >= 256) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d, x, y.enc - 256);
+    else as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d, y, x.enc - 256);
+  }
+  // acc_ci ±= Σ_e blk_e
+  void acc_add(int ci, int reg, bool neg) {
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", TS, V(reg), reg + 1);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", TS + 1, V(reg + 2), reg + 3);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", TS, V(TS), TS + 1);
+    if (neg) as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", GACC + ci, V(GACC + ci), TS);
+    else as.vop2(VOP2_ADD_F32, "v_add_f32_e32", GACC + ci, V(GACC + ci), TS);
+  }
+
+  // ---- forward
+  bool emit_mat(int i) {
+    const GOp& o = ops[i];
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted"; return false; }
+    for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", blk_reg(k) + e, S(SC0 + o.a.ci));
+    owner[k] = i;
+    loc[i] = k;
+    return true;
+  }
+  bool emit_inline(int i) {
+    const GOp& o = ops[i];
+    if (o.a.k == G_X) wait_for_feat(o.a.v);
+    if (o.kind == K_BIN && o.b.k == G_X) wait_for_feat(o.b.v);
+    Src a[R], b[R];
+    for (int e = 0; e < R; ++e) {
+      a[e] = fsrc(o.a, e);
+      if (o.kind == K_BIN) b[e] = fsrc(o.b, e);
+    }
+    // blocks dying here may hold the result (rows are independent)
+    free_values_at(i);
+    free_feats_at(i);
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted"; return false; }
+    const int d = blk_reg(k);
+    for (int e = 0; e < R; ++e) {
+      if (o.kind == K_UN) {
+        const int ar = a[e].enc - 256;
+        switch (o.op) {
+          case SRHIP_UOP_NEG: as.vop2(VOP2_XOR_B32, "v_xor_b32_e32", d + e, K(0x80000000u), ar); break;
+          case SRHIP_UOP_ABS: as.vop2(VOP2_AND_B32, "v_and_b32_e32", d + e, K(0x7fffffffu), ar); break;
+          case SRHIP_UOP_SQUARE: as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, a[e], ar); break;
+          default: {  // CUBE = (x*x)*x
+            const int tt = (d + e == ar) ? VGT + e : d + e;
+            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", tt, a[e], ar);
+            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, V(tt), ar);
+          }
+        }
+      } else {
+        const bool cb = o.b.k == G_C;
+        switch (o.op) {
+          case SRHIP_BOP_ADD:
+          case SRHIP_BOP_MUL: {
+            const int opc = o.op == SRHIP_BOP_ADD ? VOP2_ADD_F32 : VOP2_MUL_F32;
+            const char* nm = o.op == SRHIP_BOP_ADD ? "v_add_f32_e32" : "v_mul_f32_e32";
+            if (cb) as.vop2(opc, nm, d + e, b[e], a[e].enc - 256);
+            else as.vop2(opc, nm, d + e, a[e], b[e].enc - 256);
+            break;
+          }
+          default:  // SUB
+            if (cb) as.vop2(VOP2_SUBREV_F32, "v_subrev_f32_e32", d + e, b[e], a[e].enc - 256);
+            else as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", d + e, a[e], b[e].enc - 256);
+        }
+      }
+    }
+    owner[k] = i;
+    loc[i] = k;
+    return true;
+  }
+  void operand_to(int dst, const GOpnd& q) {
+    if (q.k == G_X) { read_feat(dst, q.v); return; }
+    mov4(dst, blk_reg(loc[q.v]));
+  }
+  bool emit_call(int i) {
+    const GOp& o = ops[i];
+    if (o.krid >= 0) {
+      const bool kr = o.b.k == G_C;
+      operand_to(VA, kr ? o.a : o.b);
+      as.sop1(SOP1_MOV, "s_mov_b32", S_K, S(SC0 + (kr ? o.b.ci : o.a.ci)), "s" + std::to_string(S_K));
+      free_values_at(i);
+      routine(o.krid, true);
+    } else {
+      operand_to(VA, o.a);
+      if (o.kind == K_BIN) operand_to(VB, o.b);
+      free_values_at(i);
+      routine(o.rid, true);
+    }
+    free_feats_at(i);
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted"; return false; }
+    mov4(blk_reg(k), VA);
+    owner[k] = i;
+    loc[i] = k;
+    return true;
+  }
+
+  // ---- reverse: the adjoint of op i's operands from its own
+  bool emit_reverse(int i) {
+    const GOp& o = ops[i];
+    const Adj g = adj[i];
+    if (g.reg < 0) { why = "internal: adjoint missing"; return false; }
+    auto gv = [&](int e) { return V(g.reg + e); };
+    // value of an operand in the reverse pass (features re-read from LDS)
+    auto rsrc = [&](const GOpnd& q, int scratch, int e) {
+      if (q.k == G_C) return S(SC0 + q.ci);
+      if (q.k == G_X) return V(scratch + e);
+      return V(blk_reg(loc[q.v]) + e);
+    };
+    auto fetch = [&](const GOpnd& q, int scratch) {
+      if (q.k == G_X) read_feat(scratch, q.v);
+    };
+    // adjoint of operand q = (products already in block `reg`) with sign `neg`
+    auto give = [&](const GOpnd& q, int reg, bool neg, int blk) {
+      if (q.k == G_C) { acc_add(q.ci, reg, neg); return; }
+      Adj a;
+      a.reg = reg;
+      a.blk = blk;
+      a.neg = neg;
+      adj[q.v] = a;
+    };
+    // a block for the adjoint of q (pool if q is a value, scratch `tmp` for a constant)
+    auto dest = [&](const GOpnd& q, int tmp, int* blk) {
+      *blk = -2;
+      if (q.k != G_VAL) return tmp;
+      const int k = new_adj_block(q.v);
+      if (k < 0) return -1;
+      *blk = k;
+      return blk_reg(k);
+    };
+    if (o.kind == K_MAT) {
+      acc_add(o.a.ci, g.reg, g.neg);
+    } else if (o.kind == K_BIN) {
+      const bool aa = needs_adj(o.a), ab = needs_adj(o.b);
+      switch (o.op) {
+        case SRHIP_BOP_ADD:
+        case SRHIP_BOP_SUB:
+          if (aa) {
+            if (o.a.k == G_C) acc_add(o.a.ci, g.reg, g.neg);
+            else share_adj(o.a.v, g, false);
+          }
+          if (ab) {
+            const bool fl = o.op == SRHIP_BOP_SUB;
+            if (o.b.k == G_C) acc_add(o.b.ci, g.reg, g.neg != fl);
+            else share_adj(o.b.v, g, fl);
+          }
+          break;
+        case SRHIP_BOP_MUL: {
+          fetch(o.a, XS0);
+          fetch(o.b, XS1);
+          if (aa) {
+            int blk;
+            const int d = dest(o.a, TP, &blk);
+            if (d < 0) return false;
+            for (int e = 0; e < R; ++e) vmul(d + e, rsrc(o.b, XS1, e), gv(e));
+            give(o.a, d, g.neg, blk);
+          }
+          if (ab) {
+            int blk;
+            const int d = dest(o.b, TP, &blk);
+            if (d < 0) return false;
+            for (int e = 0; e < R; ++e) vmul(d + e, rsrc(o.a, XS0, e), gv(e));
+            give(o.b, d, g.neg, blk);
+          }
+          break;
+        }
+        default: {  // DIV: q = a / b; ∂a = g / b, ∂b = -(g / b) q
+          fetch(o.b, XS1);
+          for (int e = 0; e < R; ++e) as.vop1(VOP1_RCP_F32, "v_rcp_f32_e32", TR + e, rsrc(o.b, XS1, e));
+          int blk_a = -2;
+          const int ra = (aa && o.a.k == G_VAL) ? dest(o.a, TQ, &blk_a) : TQ;
+          if (ra < 0) return false;
+          for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", ra + e, gv(e), TR + e);
+          if (aa) give(o.a, ra, g.neg, blk_a);
+          if (ab) {
+            int blk;
+            const int d = dest(o.b, TP, &blk);
+            if (d < 0) return false;
+            const int qreg = blk_reg(loc[i]);
+            for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, V(ra + e), qreg + e);
+            give(o.b, d, !g.neg, blk);
+          }
+        }
+      }
+    } else {
+      // unary: the operand is a value (constants were materialised) or a feature
+      if (!needs_adj(o.a)) { release_adj(g); return true; }
+      int blk;
+      switch (o.op) {
+        case SRHIP_UOP_NEG:
+          share_adj(o.a.v, g, true);
+          break;
+        case SRHIP_UOP_EXP: {
+          const int d = dest(o.a, TP, &blk);
+          if (d < 0) return false;
+          const int er = blk_reg(loc[i]);
+          for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), er + e);
+          give(o.a, d, g.neg, blk);
+          break;
+        }
+        case SRHIP_UOP_SQUARE:
+        case SRHIP_UOP_CUBE: {
+          const int d = dest(o.a, TP, &blk);
+          if (d < 0) return false;
+          const int ar = blk_reg(loc[o.a.v]);
+          for (int e = 0; e < R; ++e) {
+            if (o.op == SRHIP_UOP_SQUARE) {
+              as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, K(0x40000000u), ar + e);  // 2x
+            } else {
+              as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, K(0x40400000u), ar + e);  // 3x
+              as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, V(d + e), ar + e);        // (3x)x
+            }
+            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
+          }
+          give(o.a, d, g.neg, blk);
+          break;
+        }
+        case SRHIP_UOP_ABS: {  // sign(a) (0 at 0) times g
+          const int d = dest(o.a, TP, &blk);
+          if (d < 0) return false;
+          const int ar = blk_reg(loc[o.a.v]);
+          for (int e = 0; e < R; ++e) {
+            as.vop2(VOP2_AND_B32, "v_and_b32_e32", d + e, K(0x80000000u), ar + e);
+            as.vop2(VOP2_XOR_B32, "v_xor_b32_e32", d + e, gv(e), d + e);
+            as.vopc(VOPC_NEQ_F32, "v_cmp_neq_f32_e32", K(0), ar + e);
+            as.sopp(0x00, "s_nop", 1);
+            as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", d + e, K(0), d + e, ", vcc");
+          }
+          give(o.a, d, g.neg, blk);
+          break;
+        }
+        default: {  // SIN: g cos(a); COS: -g sin(a) — the FAST routines, <= 2 ulp
+          const bool is_sin = o.op == SRHIP_UOP_SIN;
+          mov4(VA, blk_reg(loc[o.a.v]));
+          routine(kUopRoutine[is_sin ? SRHIP_UOP_COS : SRHIP_UOP_SIN], false);
+          const int d = dest(o.a, TP, &blk);
+          if (d < 0) return false;
+          for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), VA + e);
+          give(o.a, d, g.neg != !is_sin, blk);
+        }
+      }
+    }
+    release_adj(g);
+    return true;
+  }
+
+  // the last, partial tile: rows past `partial` get 0 in block `reg`
+  void emit_mask(int reg) {
+    const int L_nomask = as.label();
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_PE, S(S_TILE), K(1));
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_PE), S(S_NT));
+    as.branch(SOPP_SCC0, "s_cbranch_scc0", L_nomask);
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_PARTIAL), K((uint32_t)TILE));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_nomask);
+    for (int e = 0; e < R; ++e) {
+      as.sop2(SOP2_SUB_I32, "s_sub_i32", S_PE, S(S_PARTIAL), K((uint32_t)e));
+      as.vopc(VOPC_GT_I32, "v_cmp_gt_i32_e32", S(S_PE), VLANE4);
+      as.sopp(0x00, "s_nop", 1);
+      as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", reg + e, K(0), reg + e, ", vcc");
+    }
+    as.bind(L_nomask);
+  }
+
+  bool emit_tree() {
+    if (!analyze()) return false;
+    for (int k = 0; k < GNPOOL; ++k) { owner[k] = -1; refs[k] = 0; }
+    L_tile = as.label();
+    L_done = as.label();
+    // ---- prologue
+    as.sop1(SOP1_MOV, "s_mov_b32", S_STATUS, K(0), "s" + std::to_string(S_STATUS));
+    if (nc > 0) {
+      const int op = nc <= 1 ? 0 : nc <= 2 ? 1 : nc <= 4 ? 2 : nc <= 8 ? 3 : 4;
+      static const char* nm[] = {"s_load_dword", "s_load_dwordx2", "s_load_dwordx4", "s_load_dwordx8", "s_load_dwordx16"};
+      static const int cnt[] = {1, 2, 4, 8, 16};
+      as.put(0xc0020000u | ((uint32_t)op << 18) | ((uint32_t)SC0 << 6) | (uint32_t)(SCPTR >> 1));
+      as.put(0u);
+      if (as.want_text)
+        as.lines.push_back(std::string(nm[op]) + " " +
+                           (cnt[op] == 1 ? "s" + std::to_string(SC0)
+                                         : "s[" + std::to_string(SC0) + ":" + std::to_string(SC0 + cnt[op] - 1) + "]") +
+                           ", s[" + std::to_string(SCPTR) + ":" + std::to_string(SCPTR + 1) + "], 0x0");
+    }
+    bool trig = false;
+    for (const GOp& o : ops)
+      if (o.kind == K_UN && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS)) trig = true;
+    if (has_call || trig) set_base();
+    for (int j = 0; j < nc; ++j) as.vop1(VOP1_MOV, "v_mov_b32_e32", GACC + j, K(0));
+    if (nc > 0) as.waitcnt_lgkm(0);
+    as.sopc(SOPC_GE_U32, "s_cmp_ge_u32", S(S_TILE), S(S_NT));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_done);
+    // ---- tile: forward
+    as.bind(L_tile);
+    nloads = 0;
+    waited = 0;
+    as.ds_read_b128(VY, VLANE, 0);
+    ++nloads;
+    for (size_t j = 0; j < feats.size(); ++j) {
+      const int f = feats[j];
+      xblk[f] = (int)j;
+      owner[j] = 1000 + f;
+      load_idx[f] = nloads++;
+      as.ds_read_b128(blk_reg((int)j), VLANE, (1 + f) * TILE * 4);
+    }
+    for (int i = 0; i < n; ++i) {
+      const GOp& o = ops[i];
+      bool ok;
+      if (o.kind == K_MAT) ok = emit_mat(i);
+      else if (g_inline(o)) ok = emit_inline(i);
+      else ok = emit_call(i);
+      if (!ok) return false;
+    }
+    // root value → rreg
+    int rreg;
+    if (root.k == G_VAL) rreg = blk_reg(loc[root.v]);
+    else if (root.k == G_X) { wait_for_feat(root.v); rreg = blk_reg(xblk[root.v]); }
+    else {
+      for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGT + e, S(SC0 + root.ci));
+      rreg = VGT;
+    }
+    for (int e = 0; e < R; ++e) {
+      const Src r = V(rreg + e), z = K(0), c = V(VCHK);
+      as.vop3(VOP3_FMA_F32, "v_fma_f32", VCHK, r, z, &c, 0, 0);
+    }
+    wait_all();
+    // a failed tile ends the tree (no reverse pass)
+    as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
+    as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
+    // ---- loss of the tile and the seed 2·w·r (masked rows: r = 0)
+    for (int e = 0; e < R; ++e) as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", VY + e, V(rreg + e), VY + e);
+    free_values_at(n);
+    free_feats_at(n);
+    emit_mask(VY);
+    {
+      const int L_unw = as.label(), L_seed = as.label();
+      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
+      as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VGT, S(S_WOFF), VLANE);
+      as.ds_read_b128(VGT, VGT, 0);
+      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", TP + e, V(VY + e), VY + e);
+      as.waitcnt_lgkm(0);
+      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", TP + e, V(VGT + e), TP + e);
+      as.vop2(VOP2_ADD_F32, "v_add_f32_e32", TP, V(TP), TP + 2);
+      as.vop2(VOP2_ADD_F32, "v_add_f32_e32", TP + 1, V(TP + 1), TP + 3);
+      as.vop2(VOP2_ADD_F32, "v_add_f32_e32", TP, V(TP), TP + 1);
+      as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VLSUM, V(VLSUM), TP);
+      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VGT + e), VY + e);
+      as.branch(SOPP_BRANCH, "s_branch", L_seed);
+      as.bind(L_unw);
+      for (int e = 0; e < R; ++e) {
+        const Src r = V(VY + e), l = V(VLSUM);
+        as.vop3(VOP3_FMA_F32, "v_fma_f32", VLSUM, r, r, &l, 0, 0);
+      }
+      as.bind(L_seed);
+      for (int e = 0; e < R; ++e) as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY + e, V(VY + e), VY + e);
+    }
+    // ---- reverse pass
+    if (root.k == G_C) acc_add(root.ci, VY, false);
+    else if (root.k == G_VAL && hasc[root.v]) {
+      Adj s;
+      s.reg = VY;
+      s.blk = -1;
+      adj[root.v] = s;
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      if (hasc[i] && !emit_reverse(i)) return false;
+      free_values_at(bstep(i));
+    }
+    for (int k = 0; k < GNPOOL; ++k)
+      if (owner[k] != -1) { why = "internal: block live after the reverse pass"; return false; }
+    // ---- next tile
+    as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VLANE, S(S_TILEBYTES), VLANE);
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TILE, S(S_TILE), K(1));
+    as.sopc(SOPC_LT_U32, "s_cmp_lt_u32", S(S_TILE), S(S_NT));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_tile);
+    // ---- epilogue: accumulators to the wave's scratch, return
+    as.bind(L_done);
+    for (int j = 0; j < nc; ++j) {
+      as.put(0xd81a0000u | (uint32_t)((j * 256) & 0xffff));
+      as.put(((uint32_t)(GACC + j) << 8) | (uint32_t)VSCR);
+      if (as.want_text)
+        as.lines.push_back("ds_write_b32 v" + std::to_string(VSCR) + ", v" + std::to_string(GACC + j) +
+                           (j ? " offset:" + std::to_string(j * 256) : ""));
+    }
+    if (nc > 0) as.waitcnt_lgkm(0);
+    as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(S_RT), "");
+    if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(S_RT) + ":" + std::to_string(S_RT + 1) + "]";
+    return true;
+  }
+};
+
+bool gen_grad_tree(const Ins<float>* prog, int nc, const Tmpl& T, bool text, std::vector<uint32_t>& out,
+                   std::vector<std::string>* lines, int32_t* off, std::string* why) {
+  if (nc > NGACC) { *why = "more constants than accumulators"; return false; }
+  std::vector<GOp> ir;
+  GOpnd root;
+  if (!build_gir(prog, ir, root, why)) return false;
+  const size_t start = (out.size() + 15) / 16 * 16;
+  Asm as;
+  as.want_text = text;
+  GradGen g(as, T, T.area_va + start * 4);
+  g.ops = ir;
+  g.root = root;
+  g.nc = nc;
+  if (!g.emit_tree()) { *why = g.why; return false; }
+  as.finish();
+  while (out.size() < start) {
+    out.push_back(0xbf800000u);
+    if (lines) lines->push_back("s_nop 0");
+  }
+  out.insert(out.end(), as.w.begin(), as.w.end());
+  if (lines) {
+    lines->push_back("; gradient tree code at " + std::to_string(start * 4));
+    lines->insert(lines->end(), as.lines.begin(), as.lines.end());
+  }
+  *off = (int32_t)(start * 4);
+  return true;
+}
+
+// Trees that compile are appended to ok_trees / offs; a tree that does not
+// compile goes to `rest`; a tree that no longer fits in the area ends the
+// call (returns its position in cand, or cand.size() when all were done).
+size_t grad_codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
+                    const std::vector<int32_t>& cand, size_t from, bool text, std::vector<uint32_t>& words,
+                    std::vector<std::string>* lines, std::vector<int32_t>& offs, std::vector<int32_t>& ok_trees,
+                    std::vector<int32_t>& rest, GradStats* st, const Tmpl& T) {
+  for (size_t k = from; k < cand.size(); ++k) {
+    const int32_t t = cand[k];
+    int32_t off = -1;
+    std::string why;
+    const size_t before = words.size();
+    const size_t lbefore = lines ? lines->size() : 0;
+    const int nc = const_off[t + 1] - const_off[t];
+    const bool okc = cb.tree_off[t] >= 0 && gen_grad_tree(&cb.code[cb.tree_off[t]], nc, T, text, words, lines, &off, &why);
+    if (okc && words.size() * 4 > T.area_bytes) {  // area full: the next part takes it
+      words.resize(before);
+      if (lines) lines->resize(lbefore);
+      return k;
+    }
+    if (okc) {
+      ok_trees.push_back(t);
+      offs.push_back(off);
+      if (st) st->ntrees++;
+    } else {
+      words.resize(before);
+      if (lines) lines->resize(lbefore);
+      rest.push_back(t);
+      if (st) st->nrejected++;
+      static const bool dbg = std::getenv("SRHIP_JIT_DEBUG") != nullptr;
+      if (dbg) std::fprintf(stderr, "jit-grad: tree %d not compiled: %s\n", t, why.c_str());
+    }
+  }
+  return cand.size();
+}
+
+}  // namespace
+
+// One loaded code object per part: a batch whose code exceeds one code area
+// (8 MiB) is split into consecutive slot ranges, one launch each.
+struct GradPart {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr, fn_w = nullptr;
+  int32_t* d_off = nullptr;    // [nslots] code offsets
+  int32_t* d_cbase = nullptr;  // [nslots] first constant of the slot's tree
+  int32_t* d_ncon = nullptr;   // [nslots] its constant count
+  int slot0 = 0, nslots = 0;
+};
+struct GradModule {
+  std::vector<GradPart> parts;
+  int nslots = 0;
+};
+
+namespace {
+constexpr int kMaxGradParts = 8;
+
+void load_part(GradPart& pt, const Tmpl& T, const std::vector<uint32_t>& words, const std::vector<int32_t>& offs,
+               const std::vector<int32_t>& slots, const std::vector<int32_t>& const_off) {
+  std::vector<uint8_t> img(T.img, T.img + T.size);
+  std::memcpy(img.data() + T.area_off, words.data(), words.size() * 4);
+  std::vector<int32_t> cbase(slots.size()), ncon(slots.size());
+  for (size_t k = 0; k < slots.size(); ++k) {
+    cbase[k] = const_off[slots[k]];
+    ncon[k] = const_off[slots[k] + 1] - cbase[k];
+  }
+  HIP_CHECK(hipModuleLoadData(&pt.mod, img.data()));
+  HIP_CHECK(hipModuleGetFunction(&pt.fn, pt.mod, "sr_jit_grad"));
+  HIP_CHECK(hipModuleGetFunction(&pt.fn_w, pt.mod, "sr_jit_grad_w"));
+  for (hipFunction_t f : {pt.fn, pt.fn_w})
+    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                  160 * 1024));
+  const std::pair<int32_t**, const std::vector<int32_t>*> arrays[] = {
+      {&pt.d_off, &offs}, {&pt.d_cbase, &cbase}, {&pt.d_ncon, &ncon}};
+  for (const auto& q : arrays) {
+    HIP_CHECK(hipMalloc((void**)q.first, q.second->size() * sizeof(int32_t)));
+    HIP_CHECK(hipMemcpy(*q.first, q.second->data(), q.second->size() * sizeof(int32_t), hipMemcpyHostToDevice));
+  }
+}
+}  // namespace
+
+GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
+                       const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list, std::vector<int32_t>& rest,
+                       GradStats* st) {
+  const Templates& TT = templates();
+  if (!TT.ok) { rest = cand; return nullptr; }
+  auto t0 = std::chrono::steady_clock::now();
+  struct Chunk { std::vector<uint32_t> words; std::vector<int32_t> offs, slots; const Tmpl* T; };
+  std::vector<Chunk> chunks;
+  size_t pos = 0;
+  size_t bytes = 0;
+  while (pos < cand.size()) {
+    Chunk ch;
+    ch.T = &TT.large;
+    const size_t next = grad_codegen(cb, const_off, cand, pos, false, ch.words, nullptr, ch.offs, ch.slots, rest, st,
+                                     TT.large);
+    if (next == pos) { rest.push_back(cand[pos]); if (st) st->nrejected++; pos = next + 1; continue; }  // one tree > area
+    if ((int)chunks.size() + 1 == kMaxGradParts && next < cand.size()) {  // the rest stays interpreted
+      for (size_t k = next; k < cand.size(); ++k) rest.push_back(cand[k]);
+      if (st) st->nrejected += (int)(cand.size() - next);
+      pos = cand.size();
+    } else {
+      pos = next;
+    }
+    if (ch.slots.empty()) continue;
+    if (ch.words.size() * 4 <= TT.small.area_bytes) {  // relayout for the small template's addresses
+      Chunk sm;
+      sm.T = &TT.small;
+      std::vector<int32_t> rs;
+      grad_codegen(cb, const_off, ch.slots, 0, false, sm.words, nullptr, sm.offs, sm.slots, rs, nullptr, TT.small);
+      if (sm.slots != ch.slots) throw Error(SRHIP_ERR_INVALID, "jit-grad: small-template relayout differs");
+      ch = std::move(sm);
+    }
+    bytes += ch.words.size() * 4;
+    chunks.push_back(std::move(ch));
+  }
+  if (chunks.empty()) return nullptr;
+  auto t1 = std::chrono::steady_clock::now();
+  GradModule* m = new GradModule();
+  try {
+    for (Chunk& ch : chunks) {
+      GradPart pt;
+      pt.slot0 = m->nslots;
+      pt.nslots = (int)ch.slots.size();
+      m->parts.push_back(pt);
+      load_part(m->parts.back(), *ch.T, ch.words, ch.offs, ch.slots, const_off);
+      m->nslots += pt.nslots;
+      jit_list.insert(jit_list.end(), ch.slots.begin(), ch.slots.end());
+    }
+  } catch (...) {
+    destroy_grad(m);
+    throw;
+  }
+  auto t2 = std::chrono::steady_clock::now();
+  if (st) {
+    st->ms_codegen = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    st->ms_load = std::chrono::duration<double, std::milli>(t2 - t1).count();
+    st->code_bytes = bytes;
+    st->nparts = (int)chunks.size();
+  }
+  return m;
+}
+
+void destroy_grad(GradModule* m) {
+  if (!m) return;
+  for (GradPart& pt : m->parts) {
+    for (void* q : {(void*)pt.d_off, (void*)pt.d_cbase, (void*)pt.d_ncon})
+      if (q) (void)hipFree(q);
+    if (pt.mod) (void)hipModuleUnload(pt.mod);
+  }
+  delete m;
+}
+
+int grad_nslots(const GradModule* m) { return m ? m->nslots : 0; }
+int grad_nparts(const GradModule* m) { return m ? (int)m->parts.size() : 0; }
+void grad_part(const GradModule* m, int k, int* slot0, int* nslots) {
+  *slot0 = m->parts[k].slot0;
+  *nslots = m->parts[k].nslots;
+}
+
+size_t grad_lds_extra() { return (size_t)4 * NGACC * 64 * sizeof(float) + 16; }
+
+struct JitGradArgs {
+  EvalArgs<float> e;
+  const int32_t* code_off;
+  const float* consts;
+  const int32_t* cbase;
+  const int32_t* ncon;
+  float* gpart;
+  int nconst;
+};
+
+hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const EvalArgs<float>& a,
+                            const float* consts, float* gpart, int nconst, hipStream_t stream) {
+  if (plan.threads != 256) return hipErrorInvalidValue;  // the scratch holds 4 waves
+  const GradPart& pt = m->parts[part];
+  if (a.nlist != pt.nslots) return hipErrorInvalidValue;
+  JitGradArgs ja;
+  ja.e = a;
+  ja.code_off = pt.d_off;
+  ja.consts = consts;
+  ja.cbase = pt.d_cbase;
+  ja.ncon = pt.d_ncon;
+  ja.gpart = gpart;
+  ja.nconst = nconst;
+  size_t sz = sizeof(ja);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
+  return hipModuleLaunchKernel(a.w ? pt.fn_w : pt.fn, grid, 1, 1, (unsigned)plan.threads, 1, 1,
+                               (unsigned)(plan.lds_bytes + grad_lds_extra()), stream, nullptr, cfg);
+}
+
+bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
+                       const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
+                       std::vector<int32_t>* offsets, GradStats* st) {
+  const Templates& TT = templates();
+  if (!TT.ok) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("jit templates unavailable: ") + TT.why);
+  std::vector<uint32_t> words;
+  std::vector<std::string> lines;
+  std::vector<int32_t> offs, okt, rest;
+  grad_codegen(cb, const_off, cand, 0, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, st, TT.large);
+  if (bytes) {
+    bytes->resize(words.size() * 4);
+    std::memcpy(bytes->data(), words.data(), bytes->size());
+  }
+  if (text) {
+    text->clear();
+    for (auto& l : lines) { *text += l; *text += '\n'; }
+  }
+  if (offsets) {
+    offsets->clear();
+    for (size_t k = 0; k < okt.size(); ++k) {
+      offsets->push_back(okt[k]);
+      offsets->push_back(offs[k]);
+    }
+  }
+  return !okt.empty();
+}
+
+}  // namespace jit
+}  // namespace srhip

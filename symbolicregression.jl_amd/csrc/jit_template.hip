@@ -155,3 +155,122 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
 
 extern "C" __global__ void __launch_bounds__(256) sr_jit_eval(JitArgs ja) { jit_eval_body<false>(ja); }
 extern "C" __global__ void __launch_bounds__(256) sr_jit_eval_w(JitArgs ja) { jit_eval_body<true>(ja); }
+
+// ---- gradient tree code (jit_grad.cpp) ---------------------------------------------
+// One workgroup = (row group, tree group) as above; each tree's code runs the
+// forward pass and the reverse (adjoint) pass of every tile and leaves, per
+// lane, Σ w·ℓ in LSUM, the marker in CHK and Σ ∂(w·ℓ)/∂c_j of its constants
+// in LDS scratch (sScr[wave][j][lane], written by the tree code at its end);
+// the driver reduces them over the wave into the per-row-group partials.
+struct JitGradArgs {
+  EvalArgs<float> e;        // rows, tiles, list / fail / partial as for sr_jit_eval
+  const int32_t* code_off;  // [nlist] byte offset of each slot's gradient code
+  const float* consts;      // [total constants + 16] the program's constants
+  const int32_t* cbase;     // [nlist] first constant of the slot's tree
+  const int32_t* ncon;      // [nlist] its constant count (<= SR_JIT_G_NGACC)
+  float* gpart;             // [nrg][nconst] per-row-group Σ w·ℓ'·∂ŷ/∂c
+  int nconst;
+};
+
+template <bool W>
+__device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
+  const EvalArgs<float>& a = ja.e;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* sX = reinterpret_cast<float*>(smem);
+  const int narr = 1 + a.nfeat + (W ? 1 : 0);
+  const int rows = a.ntiles * TILE;
+  Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
+  float* sScr = reinterpret_cast<float*>(sPart + ((a.tpb + 1) & ~1));
+  const int rg = blockIdx.x / a.ntg;
+  const int g = blockIdx.x - rg * a.ntg;
+  const int64_t row0 = (int64_t)rg * rows;
+  {
+    constexpr int V = TILE / 4;
+    const int total = a.ntiles * narr * V;
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int v = idx % V;
+      const int tk = idx / V;
+      const int k = tk % narr;
+      const int t = tk / narr;
+      const float* src = k == 0 ? a.y : (k <= a.nfeat ? a.X + (size_t)(k - 1) * a.n_pad : a.w);
+      reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
+          reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
+    }
+    for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) sPart[i] = Part<float>{0.0f, 0.0f};
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int64_t rem = a.n - row0;
+  const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE - 1) / TILE);
+  const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nwaves = (int)(blockDim.x >> 6);
+  auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
+  auto sld = [&](const int32_t* p, int s) {
+    return __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(p))[s]);
+  };
+  auto ld_flag = [&](int slot) { return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  uint64_t area;
+  asm volatile(
+      "s_getpc_b64 s[88:89]\n"
+      "s_add_u32 s88, s88, sr_jit_code@rel32@lo+4\n"
+      "s_addc_u32 s89, s89, sr_jit_code@rel32@hi+12"
+      : "={s[88:89]}"(area));
+  const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)sX) +
+                            (uint32_t)lane * 16u;
+  float* myScr = sScr + (size_t)wave * (SR_JIT_G_NGACC * 64);
+  const uint32_t scr_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)myScr) +
+                            (uint32_t)lane * 4u;
+  const uint32_t tilebytes = (uint32_t)(narr * TILE * 4);
+  const uint32_t woff = W ? (uint32_t)((1 + a.nfeat) * TILE * 4) : 0u;
+  const uint32_t lane4 = (uint32_t)lane * R;
+  const uint32_t partial = (uint32_t)last_valid;
+  const uint32_t nt_u = (uint32_t)nt_valid;
+
+  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
+  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
+  m = __builtin_amdgcn_readfirstlane(m);
+  uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
+  float* gdst = ja.gpart + (size_t)rg * (size_t)ja.nconst;
+  for (int k = 0; k < m; ++k) {
+    const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
+    const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
+    const bool more = k + 1 < m;
+    const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
+    if (more) fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
+    const int cb = sld(ja.cbase, s);
+    const int nc = sld(ja.ncon, s);
+    float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
+    if (!skip) {
+      const uint64_t target = area + (uint32_t)sld(ja.code_off, s);
+      const uint64_t cptr = reinterpret_cast<uint64_t>(ja.consts + cb);
+      uint32_t la = lds_lane;
+      uint32_t tile = 0, status;
+      asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                   : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status)
+                   : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+                     "{s68}"(woff), "{s[78:79]}"(cptr), "{v44}"(scr_lane)
+                   : SR_JIT_GRAD_CLOBBERS, "memory");
+      (void)status;
+    }
+    lsum = wave_sum(lsum);
+    chk = wave_sum(chk);
+    if (lane == 0) sPart[i] = Part<float>{lsum, chk};
+    if (!skip && chk != chk && lane == 0)
+      __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // per-constant partials: the tree code left them in this wave's scratch
+    // (a skipped or failed tree's values are never read: finalize marks it failed)
+    for (int j = 0; j < nc; ++j) {
+      float v = skip ? 0.0f : myScr[j * 64 + lane];
+      v = wave_sum(v);
+      if (lane == 0) gdst[cb + j] = v;
+    }
+  }
+  __syncthreads();
+  Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
+  for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) dst[i] = sPart[i];
+}
+
+extern "C" __global__ void __launch_bounds__(256) sr_jit_grad(JitGradArgs ja) { jit_grad_body<false>(ja); }
+extern "C" __global__ void __launch_bounds__(256) sr_jit_grad_w(JitGradArgs ja) { jit_grad_body<true>(ja); }

@@ -107,6 +107,11 @@ template <typename T>
 hipError_t launch_grad_finalize(const GradArgs<T>& a, double* out_sum, uint8_t* out_ok,
                                 double* out_dloss, hipStream_t stream);
 
+// Σ over row groups of the gradient tree code's per-constant partials:
+// out[cidx[k]] = Σ_rg gpart[rg][cidx[k]] in fp64 (jit_grad.cpp).
+hipError_t launch_gconst_finalize(const float* gpart, int nrg, int nconst, const int32_t* cidx, int ncidx,
+                                  double* out, hipStream_t stream);
+
 template <typename T>
 hipError_t launch_eval(const EvalPlan& plan, const EvalArgs<T>& a, int mode,
                        hipStream_t stream);

@@ -196,6 +196,33 @@ hipError_t launch_finalize(const EvalArgs<T>& a, double* out_sum, uint8_t* out_o
   return hipGetLastError();
 }
 
+namespace {
+// one wave per 64 constants, the four waves of a workgroup split the row groups
+__global__ void __launch_bounds__(256) gconst_finalize_kernel(const float* __restrict__ gpart, int nrg, int nconst,
+                                                              const int32_t* __restrict__ cidx, int ncidx,
+                                                              double* __restrict__ out) {
+  __shared__ double sh[4][64];
+  const int lane = threadIdx.x & 63;
+  const int w = threadIdx.x >> 6;
+  const int idx = blockIdx.x * 64 + lane;
+  const int k = idx < ncidx ? cidx[idx] : -1;
+  double acc = 0.0;
+  if (k >= 0)
+    for (int rg = w; rg < nrg; rg += 4) acc += (double)gpart[(size_t)rg * nconst + k];
+  sh[w][lane] = acc;
+  __syncthreads();
+  if (w == 0 && k >= 0) out[k] = (sh[0][lane] + sh[1][lane]) + (sh[2][lane] + sh[3][lane]);
+}
+}  // namespace
+
+hipError_t launch_gconst_finalize(const float* gpart, int nrg, int nconst, const int32_t* cidx, int ncidx,
+                                  double* out, hipStream_t stream) {
+  if (ncidx <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gconst_finalize_kernel, dim3((unsigned)((ncidx + 63) / 64)), dim3(256), 0, stream, gpart, nrg,
+                     nconst, cidx, ncidx, out);
+  return hipGetLastError();
+}
+
 template <typename T>
 hipError_t launch_pack_x(const T* src, int layout, int64_t src_stride, int64_t rows, int nfeat,
                          int64_t n_pad, T* dst, int* bad, hipStream_t stream) {

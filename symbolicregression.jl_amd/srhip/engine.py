@@ -178,6 +178,16 @@ class Program:
                                            C.byref(ml)))
         return dict(ntrees=nt.value, nfast=nf.value, code_bytes=nb.value, ms_codegen=mc.value, ms_load=ml.value)
 
+    def grad_jit_info(self):
+        """Gradient tree code of this program (srhip_program_grad_jit_info)."""
+        nt, nr = C.c_int32(), C.c_int32()
+        nb = C.c_int64()
+        mc, ml = C.c_double(), C.c_double()
+        check(lib().srhip_program_grad_jit_info(self.handle, C.byref(nt), C.byref(nr), C.byref(nb), C.byref(mc),
+                                                C.byref(ml)))
+        return dict(ntrees=nt.value, nrejected=nr.value, code_bytes=nb.value, ms_codegen=mc.value,
+                    ms_load=ml.value)
+
     def update_stats(self):
         """How set_constants applied new constants: {"inplace": n, "rebuilt": n}."""
         a, b = C.c_int64(), C.c_int64()
@@ -252,20 +262,28 @@ def _trees_struct(flat: FlatTrees, consts: np.ndarray) -> Trees:
     )
 
 
-def jit_compile(flat: FlatTrees, fast: bool = True):
-    """Tree compiler without a device (srhip_jit_compile): (code bytes,
-    assembly text, {tree id: byte offset})."""
+def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False):
+    """Tree compiler without a device (srhip_jit_compile, or with grad=True
+    srhip_jit_compile_grad: the reverse-mode gradient tree code): (code
+    bytes, assembly text, {tree id: byte offset})."""
     consts = np.ascontiguousarray(flat.consts, dtype=np.float32)
     tr = _trees_struct(flat, consts)
     nb, nt, no = C.c_int64(0), C.c_int64(0), C.c_int64(0)
-    rc = lib().srhip_jit_compile(C.byref(tr), int(fast), None, C.byref(nb), None, C.byref(nt), None, C.byref(no))
+
+    def call(*bufs):
+        if grad:
+            return lib().srhip_jit_compile_grad(C.byref(tr), bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
+                                                C.byref(no))
+        return lib().srhip_jit_compile(C.byref(tr), int(fast), bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
+                                       C.byref(no))
+
+    rc = call(None, None, None)
     if rc != -1:
         check(rc)
     buf = np.zeros(max(nb.value, 1), dtype=np.uint8)
     txt = C.create_string_buffer(max(nt.value, 1))
     offs = np.zeros(max(no.value, 1), dtype=np.int32)
-    check(lib().srhip_jit_compile(C.byref(tr), int(fast), _p(buf), C.byref(nb), txt, C.byref(nt), _p(offs),
-                                  C.byref(no)))
+    check(call(_p(buf), txt, _p(offs)))
     pairs = offs[: no.value].reshape(-1, 2)
     return bytes(buf[: nb.value]), txt.value.decode(), {int(t): int(o) for t, o in pairs}
 

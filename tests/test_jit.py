@@ -63,3 +63,37 @@ def test_every_tree_of_config2_compiles():
     assert len(offs) >= 990
     assert all(v % 64 == 0 for v in offs.values())
     print(f"{len(offs)} trees, {len(code) / len(offs):.0f} bytes per tree")
+
+
+GRAD_OPSETS = [
+    (["+", "-", "*", "/"], ["cos", "exp"]),  # config #5
+    (["+", "-", "*", "/"], ["sin", "cos", "exp", "neg", "square", "cube", "abs"]),
+]
+
+
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.parametrize("k", range(len(GRAD_OPSETS)))
+def test_gradient_machine_code_equals_llvm_mc(k):
+    """The reverse-mode gradient tree code (csrc/jit_grad.cpp): same check."""
+    b_ops, u_ops = GRAD_OPSETS[k]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    trees = srhip.random_population(300, o, 7, np.float32, seed=21 + k)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    code, text, offs = jit_compile(flat, grad=True)
+    assert len(offs) >= 0.9 * len(trees), f"only {len(offs)} of {len(trees)} trees compiled"
+    ref = assemble(text)
+    assert len(ref) == len(code)
+    if ref != code:
+        a = np.frombuffer(code, dtype=np.uint32)
+        r = np.frombuffer(ref, dtype=np.uint32)
+        i = int(np.flatnonzero(a != r)[0])
+        raise AssertionError(f"word {i}: jit {a[i]:#010x} vs llvm-mc {r[i]:#010x}")
+
+
+def test_gradient_code_covers_config5_trees():
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(2000, o, 20, np.float32, seed=5)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    code, _, offs = jit_compile(flat, grad=True)
+    assert len(offs) >= 0.97 * len(trees), f"{len(offs)} of {len(trees)}"
+    print(f"{len(offs)} of {len(trees)} trees, {len(code) / len(offs):.0f} bytes per tree")
