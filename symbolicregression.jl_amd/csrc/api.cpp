@@ -158,6 +158,7 @@ struct srhip_program {
   int opset = OPSET_FULL;      // smallest operator set covering the compiled programs
   // gradient programs (compiled on first use)
   bool grad_built = false;
+  bool grad_stale = false;  // constants changed since the gradient programs were patched
   std::vector<uint8_t> g_static_fail;
   void* d_gcode = nullptr;
   int32_t* d_gtree_off = nullptr;
@@ -249,7 +250,39 @@ void free_program_device(srhip_program* p) {
 // Gradient programs: compiled without folding, one work item per (tree,
 // tangent group of kGradG constants), cost-sorted.
 template <typename T>
+bool same_shape(const std::vector<Ins<T>>& code, const std::vector<unsigned char>& old);
+
+// New constants for built gradient programs: immediates patched in place when
+// the programs keep their shape, else a rebuild. Deferred from set_constants
+// to the next gradient call (a line search sets constants many times between
+// two gradient calls).
+template <typename T>
+void patch_grad_constants(srhip_program* p) {
+  p->grad_stale = false;
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->consts.data();
+  CompiledBatch<T> gb = compile_batch<T>(tr, /*grad=*/true);
+  if (same_shape(gb.code, p->h_gcode) && gb.tree_off == p->h_gtoff && gb.static_fail == p->g_static_fail) {
+    hipStream_t s = p->ctx->stream;
+    HIP_CHECK(hipStreamSynchronize(s));
+    p->h_gcode.assign(reinterpret_cast<const unsigned char*>(gb.code.data()),
+                      reinterpret_cast<const unsigned char*>(gb.code.data() + gb.code.size()));
+    HIP_CHECK(hipMemcpyAsync(p->d_gcode, p->h_gcode.data(), p->h_gcode.size(), hipMemcpyHostToDevice, s));
+    HIP_CHECK(hipStreamSynchronize(s));
+    if (p->gjit) upload_gconsts(p);
+  } else {
+    p->grad_built = false;  // rebuilt below
+  }
+}
+
+template <typename T>
 void build_grad_program(srhip_program* p) {
+  if (p->grad_built && p->grad_stale) patch_grad_constants<T>(p);
   if (p->grad_built) return;
   srhip_trees tr;
   tr.ntrees = p->ntrees;
@@ -345,6 +378,7 @@ void build_grad_program(srhip_program* p) {
                     reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   p->h_gtoff = cb.tree_off;
   p->grad_built = true;
+  p->grad_stale = false;
 }
 
 // Tree code (jit.cpp) on/off: SRHIP_JIT=0 never, =1 for every Float32
@@ -467,7 +501,12 @@ void update_constants(srhip_program* p) {
   if (p->jit) {  // first new constant set of a tree-code program: interpreter from now on
     p->jit_allowed = false;
     ++p->n_rebuild;
+    const bool had_grad = p->grad_built;
     build_program<T>(p);
+    if (had_grad) {  // same trees: the gradient programs (and their tree code) only need the constants
+      p->grad_built = true;
+      p->grad_stale = true;
+    }
     return;
   }
   p->jit_allowed = false;
@@ -490,17 +529,7 @@ void update_constants(srhip_program* p) {
   p->h_code.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
                    reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   HIP_CHECK(hipMemcpyAsync(p->d_code, p->h_code.data(), p->h_code.size(), hipMemcpyHostToDevice, s));
-  if (p->grad_built) {
-    CompiledBatch<T> gb = compile_batch<T>(tr, /*grad=*/true);
-    if (same_shape(gb.code, p->h_gcode) && gb.tree_off == p->h_gtoff && gb.static_fail == p->g_static_fail) {
-      p->h_gcode.assign(reinterpret_cast<const unsigned char*>(gb.code.data()),
-                        reinterpret_cast<const unsigned char*>(gb.code.data() + gb.code.size()));
-      HIP_CHECK(hipMemcpyAsync(p->d_gcode, p->h_gcode.data(), p->h_gcode.size(), hipMemcpyHostToDevice, s));
-      if (p->gjit) upload_gconsts(p);
-    } else {
-      p->grad_built = false;  // rebuilt on next use
-    }
-  }
+  if (p->grad_built) p->grad_stale = true;  // patched by the next gradient call (patch_grad_constants)
   HIP_CHECK(hipStreamSynchronize(s));
   ++p->n_inplace;
 }

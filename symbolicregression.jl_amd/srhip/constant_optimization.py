@@ -32,7 +32,7 @@ import numpy as np
 
 from .dataset import Dataset
 from .interface import eval_loss_batch
-from .node import Node, get_constants, set_constants
+from .node import FlatTrees, Node, flatten, get_constants, set_constants
 from .options import Options
 
 # Optim.Options defaults the reference inherits (g_abstol = 1e-8; x/f tolerances 0).
@@ -43,6 +43,9 @@ G_TOL = 1e-8
 # longer changes x in Float64; a candidate still failing Armijo then is a failed
 # line search (LineSearchException → Optim stops, not converged).
 C1, RHO_HI, RHO_LO, LS_ITERATIONS = 1e-4, 0.5, 0.1, 60
+# a line-search round with fewer than 1/SUBSET_FRACTION of the candidates still
+# shrinking moves them to a program of their own
+SUBSET_FRACTION = 10
 
 
 @dataclass
@@ -60,17 +63,31 @@ class EngineEvaluator:
     """Loss / loss+gradient of all candidates in one launch each, through the
     C ABI (srhip_program_set_constants + srhip_eval_loss[_grad])."""
 
-    def __init__(self, candidates: Sequence[Node], dataset: Dataset, options: Options,
-                 device: Optional[int] = None):
+    def __init__(self, candidates, dataset: Dataset, options: Options, device: Optional[int] = None):
+        """candidates: a list of Node, or a FlatTrees batch (no Python trees)."""
+        from .engine import Program
         from .interface import compile_trees
 
         self.dev = dataset.device(device)
-        self.prog = compile_trees(candidates, options, dataset.T, self.dev.ctx.device)
+        if isinstance(candidates, FlatTrees):
+            self.prog = Program(self.dev.ctx, candidates, dataset.T)
+        else:
+            self.prog = compile_trees(candidates, options, dataset.T, self.dev.ctx.device)
         self.loss = options.elementwise_loss
         self.T = dataset.T
 
     def _set(self, consts: np.ndarray) -> None:
         self.prog.set_constants(consts.astype(self.T, copy=False))
+
+    def subset(self, idx) -> "EngineEvaluator":
+        """An evaluator of candidates idx only (a small program: its launches
+        and constant updates cost little when few candidates are left)."""
+        sub = EngineEvaluator.__new__(EngineEvaluator)
+        from .engine import Program
+
+        sub.dev, sub.loss, sub.T = self.dev, self.loss, self.T
+        sub.prog = Program(self.dev.ctx, self.prog.flat.take(idx), self.T)
+        return sub
 
     def loss_grad(self, consts: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
         self._set(consts)
@@ -120,6 +137,26 @@ def _backtrack_step(a1, a2, phi0, dphi0, phix0, phix1, first: bool) -> float:
     return max(at, lo)
 
 
+def _backtrack_steps(a1, a2, phi0, dphi0, phix0, phix1, first):
+    """_backtrack_step for arrays of candidates (NaN/Inf arithmetic as IEEE)."""
+    with np.errstate(all="ignore"):
+        den = 2.0 * (phix1 - phi0 - dphi0 * a2)
+        at_q = np.where(den != 0, -(dphi0 * a2 * a2) / den, np.nan)
+        div = 1.0 / (a1 * a1 * a2 * a2 * (a2 - a1))
+        r1 = phix1 - phi0 - dphi0 * a2
+        r0 = phix0 - phi0 - dphi0 * a1
+        a = (a1 * a1 * r1 - a2 * a2 * r0) * div
+        b = (-a1 ** 3 * r1 + a2 ** 3 * r0) * div
+        lin = np.abs(a) <= 1e-12 * np.maximum(1.0, np.abs(b))
+        at_l = np.where(b != 0, dphi0 / (2.0 * b), np.nan)
+        d = np.maximum(b * b - 3.0 * a * dphi0, 0.0)
+        at_c = (-b + np.sqrt(d)) / (3.0 * a)
+        at = np.where(first, at_q, np.where(lin, at_l, at_c))
+        hi, lo = a2 * RHO_HI, a2 * RHO_LO
+        at = np.where(np.isfinite(at), np.minimum(at, hi), hi)  # NaNMath.min
+        return np.maximum(at, lo)
+
+
 def optimize_constants_batch(dataset: Dataset, trees: Sequence[Node], options: Options,
                              rng: Optional[np.random.Generator] = None, device: Optional[int] = None,
                              evaluator_factory: Optional[Callable] = None) -> ConstOptResult:
@@ -149,13 +186,14 @@ def _optimize(dataset, trees, options, rng, device, evaluator_factory) -> ConstO
     return _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory)
 
 
-def _starts(trees, T, nrestarts, rng):
+def _starts(flat: FlatTrees, T, nrestarts, rng):
     """Candidates: x0 and `nrestarts` perturbed copies x0 .* (1 + randn/2) per
     tree with constants (:42-54)."""
     cand_tree: List[int] = []
     cand_x: List[np.ndarray] = []
-    for i, t in enumerate(trees):
-        x0 = np.asarray(get_constants(t), dtype=T)
+    co = flat.const_off
+    for i in range(flat.ntrees):
+        x0 = np.asarray(flat.consts[co[i]:co[i + 1]], dtype=T)
         if x0.size == 0:
             continue
         cand_tree.append(i)
@@ -173,69 +211,70 @@ def _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory) 
     nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
 
     ntrees = len(trees)
-    cand_tree, cand_x = _starts(trees, T, nrestarts, rng)
+    flat = flatten(trees, options, dtype=T)
+    cand_tree, cand_x = _starts(flat, T, nrestarts, rng)
     losses = np.full(ntrees, np.inf)
     converged_out = np.zeros(ntrees, dtype=bool)
     num_evals = np.zeros(ntrees)
     if not cand_tree:
-        return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory)
+        return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat)
                               if ntrees else losses, converged_out, num_evals)
+    ev = _make_evaluator(trees, flat, cand_tree, cand_x, dataset, options, device, evaluator_factory)
 
-    cands = []
-    for i, x in zip(cand_tree, cand_x):
-        c = trees[i].copy()
-        set_constants(c, list(x))
-        cands.append(c)
-    ev = (evaluator_factory(cands) if evaluator_factory is not None
-          else EngineEvaluator(cands, dataset, options, device))
-
-    nc = len(cands)
+    nc = len(cand_tree)
     sizes = np.array([x.size for x in cand_x])
     off = np.concatenate([[0], np.cumsum(sizes)])
+    starts = off[:-1]
     X = np.concatenate(cand_x).astype(T)
     newton = sizes == 1
     f_calls = np.zeros(nc)
+    # candidates grouped by constant count: the BFGS algebra runs batched per group
+    groups = {int(sz): np.nonzero(sizes == sz)[0] for sz in np.unique(sizes) if sz > 1}
+    gidx = {sz: starts[ks][:, None] + np.arange(sz)[None, :] for sz, ks in groups.items()}  # flat positions
+    invH = {sz: np.repeat(np.eye(sz)[None], len(ks), axis=0) for sz, ks in groups.items()}
 
-    def seg(v, k):
-        return v[off[k]:off[k + 1]]
+    def segsum(v):
+        return np.add.reduceat(v, starts)
+
+    def segmax_abs(v):
+        return np.maximum.reduceat(np.abs(v), starts)
 
     f, G = ev.loss_grad(X)
     f_calls += 1
-    invH = [np.eye(s) for s in sizes]
     active = np.isfinite(f)
-    conv = np.zeros(nc, dtype=bool)
-    for k in range(nc):
-        if active[k] and np.max(np.abs(seg(G, k))) <= G_TOL:  # converged at x0
-            conv[k], active[k] = True, False
+    with np.errstate(invalid="ignore"):
+        conv = active & (segmax_abs(G) <= G_TOL)  # converged at x0
+    active &= ~conv
 
     for _ in range(iterations):
         if not active.any():
             break
         # search directions
         S = np.zeros_like(X, dtype=np.float64)
-        if (newton & active).any():
-            h = np.zeros(nc)
-            step = np.where(newton & active, np.cbrt(np.finfo(T).eps) * np.maximum(1.0, np.abs(X[off[:-1]])), 0)
-            Xp, Xm = X.astype(np.float64).copy(), X.astype(np.float64).copy()
-            for k in np.nonzero(newton & active)[0]:
-                Xp[off[k]] += step[k]
-                Xm[off[k]] -= step[k]
+        nw = newton & active
+        if nw.any():
+            step = np.where(nw, np.cbrt(np.finfo(T).eps) * np.maximum(1.0, np.abs(X[starts].astype(np.float64))), 0)
+            Xp, Xm = X.astype(np.float64), X.astype(np.float64)
+            Xp[starts[nw]] += step[nw]
+            Xm[starts[nw]] -= step[nw]
             _, Gp = ev.loss_grad(Xp.astype(T))
             _, Gm = ev.loss_grad(Xm.astype(T))
-            for k in np.nonzero(newton & active)[0]:
-                h[k] = (Gp[off[k]] - Gm[off[k]]) / (2 * step[k])
-        for k in np.nonzero(active)[0]:
-            g = seg(G, k)
-            if newton[k]:
-                hk = abs(h[k]) if np.isfinite(h[k]) and abs(h[k]) > np.finfo(T).eps else 1.0
-                s = -g / hk
-            else:
-                s = -invH[k] @ g
-                if not np.dot(g, s) < 0:  # not a descent direction: restart from I
-                    invH[k] = np.eye(sizes[k])
-                    s = -g
-            S[off[k]:off[k + 1]] = s
-        dphi0 = np.array([np.dot(seg(G, k), seg(S, k)) if active[k] else 0.0 for k in range(nc)])
+            h = (Gp[starts] - Gm[starts]) / np.where(nw, 2 * step, 1.0)
+            hk = np.where(np.isfinite(h) & (np.abs(h) > np.finfo(T).eps), np.abs(h), 1.0)
+            S[starts[nw]] = -G[starts[nw]] / hk[nw]
+        for sz, ks in groups.items():
+            act = active[ks]
+            if not act.any():
+                continue
+            g = G[gidx[sz]]
+            sd = -np.einsum("mij,mj->mi", invH[sz], g)
+            bad = ~(np.einsum("mi,mi->m", g, sd) < 0)  # not a descent direction: restart from I
+            if (bad & act).any():
+                invH[sz][bad & act] = np.eye(sz)
+                sd[bad] = -g[bad]
+            S[gidx[sz][act]] = sd[act]
+        with np.errstate(invalid="ignore", over="ignore"):
+            dphi0 = np.where(active, segsum(G * S), 0.0)
         # a NaN gradient (or no descent at all) ends the run: Optim's x would turn NaN
         active &= np.isfinite(dphi0) & (dphi0 < 0)
 
@@ -245,42 +284,48 @@ def _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory) 
         phix0 = f.copy()
         searching = active.copy()
         Xbase = X.astype(np.float64)
-        alpha_full = np.repeat(a2, sizes)
-        trial = ev.loss_only((Xbase + alpha_full * S).astype(T))
+        trial = ev.loss_only((Xbase + S).astype(T))
         f_calls += searching
         phix1 = np.where(searching, trial, f)
         finite_left = np.where(searching, int(-np.log2(np.finfo(T).eps)), 0)
         first = np.ones(nc, dtype=bool)
         ls_iter = np.zeros(nc, dtype=int)
+        sub = None  # (candidates, evaluator, flat positions) once few are left searching
         while True:
-            shrink = np.zeros(nc, dtype=bool)
-            for k in np.nonzero(searching)[0]:
-                if not np.isfinite(phix1[k]):
-                    if finite_left[k] > 0:  # halve until the loss is finite
-                        finite_left[k] -= 1
-                        a1[k] = a2[k]
-                        a2[k] *= 0.5
-                        shrink[k] = True
-                    else:
-                        searching[k] = False
-                    continue
-                if phix1[k] <= f[k] + C1 * a2[k] * dphi0[k]:
-                    searching[k] = False
-                    continue
-                if ls_iter[k] >= LS_ITERATIONS:  # failed line search: stays at x
-                    searching[k] = False
-                    phix1[k] = np.inf
-                    continue
-                ls_iter[k] += 1
-                at = _backtrack_step(a1[k], a2[k], f[k], dphi0[k], phix0[k], phix1[k], first[k])
-                first[k] = False
-                a1[k] = a2[k]
-                a2[k] = at
-                shrink[k] = True
+            fin = np.isfinite(phix1)
+            halve = searching & ~fin & (finite_left > 0)  # halve until the loss is finite
+            searching &= fin | halve
+            with np.errstate(invalid="ignore"):
+                armijo = searching & fin & (phix1 <= f + C1 * a2 * dphi0)
+            searching &= ~armijo
+            failed = searching & fin & (ls_iter >= LS_ITERATIONS)  # failed line search: stays at x
+            searching &= ~failed
+            phix1 = np.where(failed, np.inf, phix1)
+            step = searching & fin
+            finite_left = np.where(halve, finite_left - 1, finite_left)
+            ls_iter = np.where(step, ls_iter + 1, ls_iter)
+            at = _backtrack_steps(a1, a2, f, dphi0, phix0, phix1, first)
+            shrink = halve | step
+            a1 = np.where(shrink, a2, a1)
+            a2 = np.where(halve, a2 * 0.5, np.where(step, at, a2))
+            first = np.where(step, False, first)
             if not shrink.any():
                 break
             alpha_full = np.repeat(a2, sizes)
-            trial = ev.loss_only(np.where(np.repeat(shrink, sizes), Xbase + alpha_full * S, Xbase).astype(T))
+            Xt = np.where(np.repeat(shrink, sizes), Xbase + alpha_full * S, Xbase).astype(T)
+            if sub is None and hasattr(ev, "subset") and shrink.sum() * SUBSET_FRACTION < nc:
+                # the stragglers (a line search that keeps shrinking) continue on their own
+                # program: the full batch's launches and constant updates cost the same for
+                # 10 or 10⁴ candidates
+                ks = np.nonzero(searching | halve)[0]
+                pos = np.concatenate([np.arange(off[k], off[k + 1]) for k in ks])
+                sub = (ks, ev.subset(ks), pos)
+            if sub is not None:
+                ks, sev, pos = sub
+                trial = np.full(nc, np.inf)
+                trial[ks] = sev.loss_only(Xt[pos])
+            else:
+                trial = ev.loss_only(Xt)
             f_calls += shrink
             phix0 = np.where(shrink, phix1, phix0)
             phix1 = np.where(shrink, trial, phix1)
@@ -290,28 +335,42 @@ def _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory) 
         Xn = np.where(np.repeat(moved, sizes), Xbase + np.repeat(a2, sizes) * S, Xbase).astype(T)
         fn, Gn = ev.loss_grad(Xn)
         f_calls += moved
-        for k in np.nonzero(active)[0]:
-            if not moved[k] or not np.isfinite(fn[k]):
-                active[k] = False
-                continue
-            dx = seg(Xn, k).astype(np.float64) - seg(X, k).astype(np.float64)
-            dg = seg(Gn, k) - seg(G, k)
-            x_conv = np.max(np.abs(dx)) <= 0.0
-            f_conv = abs(fn[k] - f[k]) <= 0.0
-            g_conv = np.max(np.abs(seg(Gn, k))) <= G_TOL
-            if not newton[k]:
-                dxdg = np.float64(np.dot(dx, dg))  # IEEE arithmetic: overflow gives Inf, as in Julia
-                if dxdg > 0:
-                    with np.errstate(all="ignore"):
-                        Hdg = invH[k] @ dg
-                        invH[k] = (invH[k] + (dxdg + dg @ Hdg) * np.outer(dx, dx) / (dxdg * dxdg)
-                                   - (np.outer(Hdg, dx) + np.outer(dx, Hdg)) / dxdg)
-            if x_conv or f_conv or g_conv:
-                conv[k], active[k] = True, False
+        upd = active & moved & np.isfinite(fn)
+        active &= upd
+        dx_all = Xn.astype(np.float64) - X.astype(np.float64)
+        dg_all = Gn - G
+        with np.errstate(invalid="ignore", over="ignore"):
+            x_conv = segmax_abs(dx_all) <= 0.0
+            f_conv = np.abs(fn - f) <= 0.0
+            g_conv = segmax_abs(Gn) <= G_TOL
+        with np.errstate(all="ignore"):  # IEEE arithmetic: overflow gives Inf, as in Julia
+            for sz, ks in groups.items():
+                u = upd[ks]
+                if not u.any():
+                    continue
+                dx, dg = dx_all[gidx[sz]], dg_all[gidx[sz]]
+                dxdg = np.einsum("mi,mi->m", dx, dg)
+                u &= dxdg > 0
+                if not u.any():
+                    continue
+                H = invH[sz][u]
+                dxu, dgu, d = dx[u], dg[u], dxdg[u]
+                Hdg = np.einsum("mij,mj->mi", H, dgu)
+                outer_dx = dxu[:, :, None] * dxu[:, None, :]
+                coef = (d + np.einsum("mi,mi->m", dgu, Hdg)) / (d * d)
+                invH[sz][u] = (H + coef[:, None, None] * outer_dx
+                               - (Hdg[:, :, None] * dxu[:, None, :] + dxu[:, :, None] * Hdg[:, None, :])
+                               / d[:, None, None])
+        done = upd & (x_conv | f_conv | g_conv)
+        conv |= done
+        active &= ~done
         keep = np.repeat(moved, sizes)
         X = np.where(keep, Xn, X).astype(T)
         G = np.where(keep, Gn, G)
         f = np.where(moved & np.isfinite(fn), fn, f)
+
+    def seg(v, k):
+        return v[off[k]:off[k + 1]]
 
     # best start per tree (:51-53), then the converged check (:56-63)
     best = {}
@@ -321,11 +380,29 @@ def _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory) 
             best[i] = k
     for i, k in best.items():
         if conv[k]:
-            set_constants(trees[i], [T(v) for v in seg(X, k)])
+            vals = seg(X, k).astype(T)
+            set_constants(trees[i], [T(v) for v in vals])
+            flat.consts[flat.const_off[i]:flat.const_off[i + 1]] = vals
             converged_out[i] = True
             num_evals[i] += 1
-    return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory), converged_out,
+    return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat), converged_out,
                           num_evals)
+
+
+def _make_evaluator(trees, flat, cand_tree, cand_x, dataset, options, device, factory, repeat=None):
+    """The evaluator of the candidates (start k = tree cand_tree[k] with
+    constants cand_x[k]); `repeat[k]` copies of each when given. The engine
+    takes the flattened batch directly; a test factory gets Node copies."""
+    idx = np.asarray(cand_tree) if repeat is None else np.repeat(cand_tree, repeat)
+    xs = cand_x if repeat is None else [x for x, r in zip(cand_x, repeat) for _ in range(r)]
+    if factory is None:
+        return EngineEvaluator(flat.take(idx, np.concatenate(xs)), dataset, options, device)
+    cands = []
+    for i, x in zip(idx, xs):
+        c = trees[i].copy()
+        set_constants(c, list(x))
+        cands.append(c)
+    return factory(cands)
 
 
 NM_INITIAL_A, NM_INITIAL_B = 0.025, 0.5  # Optim.AffineSimplexer defaults
@@ -347,25 +424,18 @@ def _optimize_nelder_mead(dataset, trees, options, rng, device, evaluator_factor
     iterations = int(getattr(options, "optimizer_iterations", 8))
     nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
     ntrees = len(trees)
-    cand_tree, cand_x = _starts(trees, T, nrestarts, rng)
+    flat = flatten(trees, options, dtype=T)
+    cand_tree, cand_x = _starts(flat, T, nrestarts, rng)
     converged_out = np.zeros(ntrees, dtype=bool)
     num_evals = np.zeros(ntrees)
     if not cand_tree:
-        return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory),
+        return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat),
                               converged_out, num_evals)
-
-    def make(ts):
-        return evaluator_factory(ts) if evaluator_factory is not None else EngineEvaluator(ts, dataset, options, device)
-
-    cands = []
-    for i, x in zip(cand_tree, cand_x):
-        c = trees[i].copy()
-        set_constants(c, list(x))
-        cands.append(c)
-    nc = len(cands)
+    nc = len(cand_tree)
     sizes = [x.size for x in cand_x]
-    point_ev = make(cands)                                              # one point per start
-    simplex_ev = make([c for k, c in enumerate(cands) for _ in range(sizes[k] + 1)])  # every vertex
+    point_ev = _make_evaluator(trees, flat, cand_tree, cand_x, dataset, options, device, evaluator_factory)
+    simplex_ev = _make_evaluator(trees, flat, cand_tree, cand_x, dataset, options, device, evaluator_factory,
+                                 repeat=[sz + 1 for sz in sizes])  # every vertex
 
     # initial simplex (AffineSimplexer) and its losses: one launch
     simplex = []
@@ -492,18 +562,25 @@ def _optimize_nelder_mead(dataset, trees, options, rng, device, evaluator_factor
             best[i] = k
     for i, k in best.items():
         if conv[k]:
-            set_constants(trees[i], [T(v) for v in xmin[k]])
+            vals = np.asarray(xmin[k], dtype=T)
+            set_constants(trees[i], [T(v) for v in vals])
+            flat.consts[flat.const_off[i]:flat.const_off[i + 1]] = vals
             converged_out[i] = True
             num_evals[i] += 1
-    return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory), converged_out,
+    return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat), converged_out,
                           num_evals)
 
 
-def _final_losses(trees, dataset, options, device, factory) -> np.ndarray:
+def _final_losses(trees, dataset, options, device, factory, flat=None) -> np.ndarray:
     """Losses of the trees as they stand (one launch; the reference's
     score_func re-score of a converged member, :58)."""
     if factory is None:
-        return np.asarray(eval_loss_batch(trees, dataset, options, device=device), dtype=np.float64)
+        prog = None
+        if flat is not None:
+            from .engine import Program
+
+            prog = Program(dataset.device(device).ctx, flat, dataset.T)
+        return np.asarray(eval_loss_batch(trees, dataset, options, device=device, program=prog), dtype=np.float64)
     ev = factory(list(trees))
     consts = [np.asarray(get_constants(t), dtype=np.float64) for t in trees]
     X = np.concatenate(consts) if consts else np.zeros(0)

@@ -169,6 +169,26 @@ class FlatTrees:
         cb, ce = self.const_off[t], self.const_off[t + 1]
         return self.kind[b:e], self.arg[b:e], self.consts[cb:ce]
 
+    def take(self, idx, consts=None) -> "FlatTrees":
+        """The trees idx (repeats allowed) as a new batch; `consts` replaces
+        their concatenated constants (default: the trees' own)."""
+        idx = np.asarray(idx, dtype=np.int64)
+
+        def gather(off, arr):
+            lens = np.diff(off)[idx]
+            new_off = np.concatenate([[0], np.cumsum(lens)]).astype(np.int32)
+            pos = np.repeat(off[:-1][idx] - new_off[:-1], lens) + np.arange(new_off[-1])
+            return new_off, arr[pos]
+
+        node_off, kind = gather(self.node_off, self.kind)
+        _, arg = gather(self.node_off, self.arg)
+        const_off, cs = gather(self.const_off, self.consts)
+        if consts is not None:
+            cs = np.asarray(consts, dtype=self.consts.dtype)
+            if cs.shape != (const_off[-1],):
+                raise ValueError("constant vector has the wrong length")
+        return FlatTrees(node_off, kind, arg, const_off, cs, self.nodes[idx])
+
 
 def flatten(trees: Iterable[Node], options, dtype=np.float32) -> FlatTrees:
     """Post-order flattening. Operator indices are mapped through the
