@@ -223,6 +223,16 @@ bool gjit_wanted(int ntrees) {
   return ntrees >= 256;
 }
 
+// LDS for the row tiles of a gradient tree-code workgroup (SRHIP_GJIT_LDS, KiB:
+// experiments); more tiles per workgroup amortise each tree's call over more rows
+size_t gjit_tile_budget() {
+  static const size_t b = [] {
+    const char* e = std::getenv("SRHIP_GJIT_LDS");
+    return (size_t)(e ? std::atoi(e) : 40) * 1024;
+  }();
+  return b;
+}
+
 // the Float32 constants the gradient tree code reads (s_load), 16 floats of padding
 void upload_gconsts(srhip_program* p) {
   const size_t nconst = p->const_off.back();
@@ -839,7 +849,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
       for (int k = 0; k < nparts && use_gjit; ++k) {
         int s0, nsl;
         jit::grad_part(p->gjit, k, &s0, &nsl);
-        use_gjit = plan_geometry(4, 4, kShallowSlots, narr, 2 * 4, ds->rows, nsl, &plans[k]) &&
+        use_gjit = plan_geometry(4, 4, kShallowSlots, narr, 2 * 4, ds->rows, nsl, &plans[k], gjit_tile_budget()) &&
                    plans[k].lds_bytes + jit::grad_lds_extra() <= 160 * 1024 && plans[k].nrg == plans[0].nrg;
       }
       if (use_gjit) {

@@ -70,7 +70,7 @@ bool plan_eval(int dtype, bool deep, int opset, int mode, bool weighted, int nfe
                int64_t n, int nlist, EvalPlan* plan);
 // Same, for explicit R / D / LDS arrays / partial bytes per tree slot.
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n,
-                   int nlist, EvalPlan* plan);
+                   int nlist, EvalPlan* plan, size_t tile_budget = 40 * 1024);
 
 // ---- constant gradients (grad_kernels.hip) -----------------------------------
 constexpr int kGradG = 4;  // tangents per pass (constants per "tangent group")

@@ -139,14 +139,14 @@ hipError_t launch_ti_records(const Ins<float>* prog, const int32_t* list_off, in
 }
 
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n, int nlist,
-                   EvalPlan* p) {
+                   EvalPlan* p, size_t tile_budget) {
   p->R = R;
   p->D = D;
   p->opset = OPSET_FULL;
   p->tile = 64 * R;
   p->threads = 256;
   const size_t per_tile = (size_t)narr * p->tile * esz;
-  const size_t budget = 40 * 1024;
+  const size_t budget = tile_budget;
 #ifndef SR_NTMAX
 #define SR_NTMAX 16
 #endif
