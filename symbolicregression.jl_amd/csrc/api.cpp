@@ -228,7 +228,7 @@ bool gjit_wanted(int ntrees) {
 size_t gjit_tile_budget() {
   static const size_t b = [] {
     const char* e = std::getenv("SRHIP_GJIT_LDS");
-    return (size_t)(e ? std::atoi(e) : 40) * 1024;
+    return (size_t)(e ? std::atoi(e) : 52) * 1024;
   }();
   return b;
 }
@@ -849,8 +849,10 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
       for (int k = 0; k < nparts && use_gjit; ++k) {
         int s0, nsl;
         jit::grad_part(p->gjit, k, &s0, &nsl);
-        use_gjit = plan_geometry(4, 4, kShallowSlots, narr, 2 * 4, ds->rows, nsl, &plans[k], gjit_tile_budget()) &&
-                   plans[k].lds_bytes + jit::grad_lds_extra() <= 160 * 1024 && plans[k].nrg == plans[0].nrg;
+        // partials go straight to global memory: LDS holds the row tiles only (1 byte per slot below
+        // keeps plan_geometry's slot bound out of the way)
+        use_gjit = plan_geometry(4, 4, kShallowSlots, narr, 1, ds->rows, nsl, &plans[k], gjit_tile_budget()) &&
+                   plans[k].nrg == plans[0].nrg;
       }
       if (use_gjit) {
         const int nsl_all = jit::grad_nslots(p->gjit);

@@ -434,15 +434,15 @@ def build(hipcc, outdir, R):
                                                           + ['"vcc"', '"scc"', '"m0"']) + "\n")
         # gradient tree code (jit_grad.cpp): the same routines, a larger value
         # pool, per-constant accumulators, constants in SGPRs
-        g = dict(VSCR=44, GPOOL0=56, GNPOOL=20, GACC=136, NGACC=16, SC0=24, SCPTR=78)
+        g = dict(GPOOL0=56, GNPOOL=20, GACC=136, NGACC=16, SC0=24, SCPTR=78, SGPTR=84)
         assert g["GPOOL0"] + 4 * g["GNPOOL"] == g["GACC"]
         assert max(stemp) < g["SC0"] and g["SC0"] % 4 == 0
         for k, v in g.items():
             f.write(f"#define SR_JIT_G_{k} {v}\n")
-        gin_v = {rg.CHK, rg.LANE, rg.LSUM, rg.LANE4, g["VSCR"]}
+        gin_v = {rg.CHK, rg.LANE, rg.LSUM, rg.LANE4}
         gclob_v = sorted((vtemp | set(range(rg.A, g["GACC"] + g["NGACC"]))) - gin_v)
         gin_s = {rg.S[k] for k in ("tile", "nt", "partial", "tilebytes", "woff", "status")} | \
-            {g["SCPTR"], g["SCPTR"] + 1}
+            {g["SCPTR"], g["SCPTR"] + 1, g["SGPTR"], g["SGPTR"] + 1}
         gclob_s = sorted((stemp | sstate | set(range(g["SC0"], g["SC0"] + g["NGACC"]))) - gin_s)
         f.write("#define SR_JIT_GRAD_CLOBBERS " + ", ".join([f'"v{r}"' for r in gclob_v] + [f'"s{r}"' for r in gclob_s]
                                                                + ['"vcc"', '"scc"', '"m0"']) + "\n")

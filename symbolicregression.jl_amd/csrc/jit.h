@@ -80,8 +80,6 @@ int grad_nslots(const GradModule* m);
 // the module's code objects: consecutive slot ranges, one launch each
 int grad_nparts(const GradModule* m);
 void grad_part(const GradModule* m, int k, int* slot0, int* nslots);
-// LDS the gradient driver needs beyond the eval plan's (per-wave accumulator scratch)
-size_t grad_lds_extra();
 // Launch part `part` over its slots (EvalArgs as for launch(): list / fail /
 // partial of the slots); consts = the program's constants (+16 readable
 // floats of padding), gpart = [nrg][nconst] per-row-group ∂L/∂c partials.

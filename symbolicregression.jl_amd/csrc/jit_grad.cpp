@@ -49,8 +49,9 @@ namespace {
 
 using namespace detail;
 
-constexpr int VSCR = SR_JIT_G_VSCR, GPOOL0 = SR_JIT_G_GPOOL0, GNPOOL = SR_JIT_G_GNPOOL;
+constexpr int GPOOL0 = SR_JIT_G_GPOOL0, GNPOOL = SR_JIT_G_GNPOOL;
 constexpr int GACC = SR_JIT_G_GACC, NGACC = SR_JIT_G_NGACC, SC0 = SR_JIT_G_SC0, SCPTR = SR_JIT_G_SCPTR;
+constexpr int SGPTR = SR_JIT_G_SGPTR;  // s[84:85]: this row group's ∂L/∂c partials of the tree
 // scratch VGPRs of tree code (routine temps: free between calls)
 constexpr int XS0 = 0, XS1 = 4;   // feature values read in the reverse pass
 constexpr int TS = 8;             // 2 registers: row sums
@@ -701,16 +702,48 @@ struct GradGen {
     as.sop2(SOP2_ADD_U32, "s_add_u32", S_TILE, S(S_TILE), K(1));
     as.sopc(SOPC_LT_U32, "s_cmp_lt_u32", S(S_TILE), S(S_NT));
     as.branch(SOPP_SCC1, "s_cbranch_scc1", L_tile);
-    // ---- epilogue: accumulators to the wave's scratch, return
+    // ---- epilogue: each accumulator summed over the wave (DPP, the order of
+    // interp.h wave_sum: lane 63 holds the sum) and stored to this row
+    // group's partial of its constant; return
     as.bind(L_done);
-    for (int j = 0; j < nc; ++j) {
-      as.put(0xd81a0000u | (uint32_t)((j * 256) & 0xffff));
-      as.put(((uint32_t)(GACC + j) << 8) | (uint32_t)VSCR);
-      if (as.want_text)
-        as.lines.push_back("ds_write_b32 v" + std::to_string(VSCR) + ", v" + std::to_string(GACC + j) +
-                           (j ? " offset:" + std::to_string(j * 256) : ""));
+    if (nc > 0) {
+      as.vop1(VOP1_MOV, "v_mov_b32_e32", TS + 1, K(0));
+      // a DPP source must not be written by the 2 VALU instructions before:
+      // the six steps run interleaved over the constants, padded with s_nop
+      static const struct { uint32_t ctrl, row; const char* txt; } steps[] = {
+          {0x0b1, 0xf, "quad_perm:[1,0,3,2] row_mask:0xf"}, {0x04e, 0xf, "quad_perm:[2,3,0,1] row_mask:0xf"},
+          {0x141, 0xf, "row_half_mirror row_mask:0xf"},     {0x140, 0xf, "row_mirror row_mask:0xf"},
+          {0x142, 0xa, "row_bcast:15 row_mask:0xa"},        {0x143, 0xc, "row_bcast:31 row_mask:0xc"}};
+      as.sopp(0x00, "s_nop", 1);
+      for (const auto& st : steps) {
+        if (nc < 3) as.sopp(0x00, "s_nop", 2 - nc);
+        for (int j = 0; j < nc; ++j) {
+          const int a = GACC + j;
+          as.put(((uint32_t)VOP2_ADD_F32 << 25) | ((uint32_t)a << 17) | ((uint32_t)a << 9) | 0xfau);
+          as.put((uint32_t)a | (st.ctrl << 8) | (0xfu << 24) | (st.row << 28));
+          if (as.want_text)
+            as.lines.push_back("v_add_f32_dpp v" + std::to_string(a) + ", v" + std::to_string(a) + ", v" +
+                               std::to_string(a) + " " + st.txt + " bank_mask:0xf");
+        }
+      }
+      as.sopp(0x00, "s_nop", 1);
     }
-    if (nc > 0) as.waitcnt_lgkm(0);
+    for (int j = 0; j < nc; ++j) {
+      const int a = GACC + j;
+      // lane 63 holds the sum: v_readlane_b32 s20, v_a, 63 (s20: a routine temporary, free here)
+      as.put(0xd2890000u | 20u);
+      as.put((uint32_t)(256 + a) | (191u << 9));
+      if (as.want_text) as.lines.push_back("v_readlane_b32 s20, v" + std::to_string(a) + ", 63");
+      as.sopp(0x00, "s_nop", 4);
+      as.vop1(VOP1_MOV, "v_mov_b32_e32", TS, S(20));
+      // global_store_dword v[TS+1] (= 0), v[TS], s[SGPTR:SGPTR+1] offset:4j
+      as.put(0xdc708000u | (uint32_t)((4 * j) & 0x1fff));
+      as.put((uint32_t)(TS + 1) | ((uint32_t)TS << 8) | ((uint32_t)SGPTR << 16));
+      if (as.want_text)
+        as.lines.push_back("global_store_dword v" + std::to_string(TS + 1) + ", v" + std::to_string(TS) + ", s[" +
+                           std::to_string(SGPTR) + ":" + std::to_string(SGPTR + 1) + "]" +
+                           (j ? " offset:" + std::to_string(4 * j) : ""));
+    }
     as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(S_RT), "");
     if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(S_RT) + ":" + std::to_string(S_RT + 1) + "]";
     return true;
@@ -904,7 +937,6 @@ void grad_part(const GradModule* m, int k, int* slot0, int* nslots) {
   *nslots = m->parts[k].nslots;
 }
 
-size_t grad_lds_extra() { return (size_t)4 * NGACC * 64 * sizeof(float) + 16; }
 
 struct JitGradArgs {
   EvalArgs<float> e;
@@ -932,8 +964,11 @@ hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
-  return hipModuleLaunchKernel(a.w ? pt.fn_w : pt.fn, grid, 1, 1, (unsigned)plan.threads, 1, 1,
-                               (unsigned)(plan.lds_bytes + grad_lds_extra()), stream, nullptr, cfg);
+  // LDS: the row tiles only (partials and ∂L/∂c go straight to global memory)
+  const size_t narr = 1 + (size_t)a.nfeat + (a.w ? 1 : 0);
+  const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + 16;
+  return hipModuleLaunchKernel(a.w ? pt.fn_w : pt.fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds,
+                               stream, nullptr, cfg);
 }
 
 bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,

@@ -158,10 +158,10 @@ extern "C" __global__ void __launch_bounds__(256) sr_jit_eval_w(JitArgs ja) { ji
 
 // ---- gradient tree code (jit_grad.cpp) ---------------------------------------------
 // One workgroup = (row group, tree group) as above; each tree's code runs the
-// forward pass and the reverse (adjoint) pass of every tile and leaves, per
-// lane, Σ w·ℓ in LSUM, the marker in CHK and Σ ∂(w·ℓ)/∂c_j of its constants
-// in LDS scratch (sScr[wave][j][lane], written by the tree code at its end);
-// the driver reduces them over the wave into the per-row-group partials.
+// forward pass and the reverse (adjoint) pass of every tile, leaves Σ w·ℓ in
+// LSUM and the marker in CHK, and itself stores Σ w·ℓ'·∂ŷ/∂c_j of each of its
+// constants (summed over the wave) to this row group's partials. LDS holds
+// the row tiles only, so two or more tiles of a wide dataset fit.
 struct JitGradArgs {
   EvalArgs<float> e;        // rows, tiles, list / fail / partial as for sr_jit_eval
   const int32_t* code_off;  // [nlist] byte offset of each slot's gradient code
@@ -178,11 +178,9 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sX = reinterpret_cast<float*>(smem);
   const int narr = 1 + a.nfeat + (W ? 1 : 0);
-  const int rows = a.ntiles * TILE;
-  Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
-  float* sScr = reinterpret_cast<float*>(sPart + ((a.tpb + 1) & ~1));
   const int rg = blockIdx.x / a.ntg;
   const int g = blockIdx.x - rg * a.ntg;
+  const int rows = a.ntiles * TILE;
   const int64_t row0 = (int64_t)rg * rows;
   {
     constexpr int V = TILE / 4;
@@ -196,7 +194,6 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
       reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
           reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
     }
-    for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) sPart[i] = Part<float>{0.0f, 0.0f};
   }
   __syncthreads();
 
@@ -219,9 +216,6 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
       : "={s[88:89]}"(area));
   const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)sX) +
                             (uint32_t)lane * 16u;
-  float* myScr = sScr + (size_t)wave * (SR_JIT_G_NGACC * 64);
-  const uint32_t scr_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)myScr) +
-                            (uint32_t)lane * 4u;
   const uint32_t tilebytes = (uint32_t)(narr * TILE * 4);
   const uint32_t woff = W ? (uint32_t)((1 + a.nfeat) * TILE * 4) : 0u;
   const uint32_t lane4 = (uint32_t)lane * R;
@@ -233,43 +227,35 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   m = __builtin_amdgcn_readfirstlane(m);
   uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
   float* gdst = ja.gpart + (size_t)rg * (size_t)ja.nconst;
+  Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
   for (int k = 0; k < m; ++k) {
     const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
     const bool more = k + 1 < m;
     const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
     if (more) fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
-    const int cb = sld(ja.cbase, s);
-    const int nc = sld(ja.ncon, s);
     float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
     if (!skip) {
+      const int cb = sld(ja.cbase, s);
       const uint64_t target = area + (uint32_t)sld(ja.code_off, s);
       const uint64_t cptr = reinterpret_cast<uint64_t>(ja.consts + cb);
+      const uint64_t gptr = reinterpret_cast<uint64_t>(gdst + cb);
       uint32_t la = lds_lane;
       uint32_t tile = 0, status;
       asm volatile("s_swappc_b64 s[76:77], %[tgt]"
                    : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status)
                    : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
-                     "{s68}"(woff), "{s[78:79]}"(cptr), "{v44}"(scr_lane)
+                     "{s68}"(woff), "{s[78:79]}"(cptr), "{s[84:85]}"(gptr)
                    : SR_JIT_GRAD_CLOBBERS, "memory");
       (void)status;
     }
+    // a skipped tree writes no ∂L/∂c partials: finalize marks it failed
     lsum = wave_sum(lsum);
     chk = wave_sum(chk);
-    if (lane == 0) sPart[i] = Part<float>{lsum, chk};
+    if (lane == 0) dst[i] = Part<float>{lsum, chk};
     if (!skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    // per-constant partials: the tree code left them in this wave's scratch
-    // (a skipped or failed tree's values are never read: finalize marks it failed)
-    for (int j = 0; j < nc; ++j) {
-      float v = skip ? 0.0f : myScr[j * 64 + lane];
-      v = wave_sum(v);
-      if (lane == 0) gdst[cb + j] = v;
-    }
   }
-  __syncthreads();
-  Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
-  for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) dst[i] = sPart[i];
 }
 
 extern "C" __global__ void __launch_bounds__(256) sr_jit_grad(JitGradArgs ja) { jit_grad_body<false>(ja); }
