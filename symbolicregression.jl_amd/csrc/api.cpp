@@ -401,6 +401,14 @@ bool jit_wanted(int nshallow) {
   if (e && e[0] == '1') return true;
   return nshallow >= 512;
 }
+// LDS for the row tiles of a tree-code workgroup (SRHIP_EVAL_LDS, KiB)
+size_t jit_tile_budget() {
+  static const size_t b = [] {
+    const char* e = std::getenv("SRHIP_EVAL_LDS");
+    return (size_t)(e ? std::atoi(e) : 40) * 1024;
+  }();
+  return b;
+}
 bool jit_fast_enabled() {
   const char* e = std::getenv("SRHIP_JIT_FAST");
   return !(e && e[0] == '0');
@@ -673,7 +681,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     EvalPlan plan;
     if (pass == -1) {
       const int narr = 1 + nfeat + (w ? 1 : 0);
-      if (!plan_geometry(4, 4, kShallowSlots, narr, 2 * 4, rows, nlist, &plan))
+      if (!plan_geometry(4, 4, kShallowSlots, narr, 2 * 4, rows, nlist, &plan, jit_tile_budget()))
         throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
     } else if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan)) {
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");

@@ -382,7 +382,11 @@ struct Gen {
     as.sop2(up ? SOP2_ADDC_U32 : SOP2_SUBB_U32, up ? "s_addc_u32" : "s_subb_u32", S_BASE + 1, S(S_BASE + 1), K(0));
   }
   void call_routine(int rid) {
-    if (inline_ok && !T.body[rid].empty()) {  // a copy of the body instead of the call
+    static const size_t inline_max = [] {  // SRHIP_JIT_INLINE_MAX: only bodies up to this many bytes
+      const char* e = std::getenv("SRHIP_JIT_INLINE_MAX");
+      return e ? (size_t)std::atoi(e) : (size_t)1 << 30;
+    }();
+    if (inline_ok && !T.body[rid].empty() && T.body[rid].size() * 4 <= inline_max) {  // a copy of the body
       for (uint32_t w : T.body[rid]) as.raw(w);
       as.sopp(0x00, "s_nop", 0);  // a trans result read right after the body
       return;

@@ -110,23 +110,29 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
   m = __builtin_amdgcn_readfirstlane(m);
   uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
+  // the next slot's code offset is loaded one tree ahead, like its flag
+  int32_t cnext = m > 0 ? code_of(slot_of(wave)) : 0;
   uint32_t redos = 0;  // tiles redone with the PRECISE routines (counted by tree code)
   for (int k = 0; k < m; ++k) {
     const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
     const bool more = k + 1 < m;
     const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
-    if (more) fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
+    const int32_t coff = cnext;
+    if (more) {
+      fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
+      cnext = code_of(slot_of(wave + (k + 1) * nwaves));
+    }
     float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
     if (!skip) {
-      const uint64_t target = area + (uint32_t)code_of(s);
+      const uint64_t target = area + (uint32_t)coff;
       uint32_t la = lds_lane;
       uint32_t tile = 0, status;
       asm volatile("s_swappc_b64 s[76:77], %[tgt]"
                    : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
                      "+{s84}"(redos)
-                   : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
-                     "{s68}"(woff), "{s79}"(fastok)
+                   : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial),
+                     "{s67}"(tilebytes), "{s68}"(woff), "{s79}"(fastok)
                    : SR_JIT_CLOBBERS, "memory");
       if (__builtin_amdgcn_readfirstlane((int)status) != 0) {
         // a tile the routines cannot do (sin/cos argument beyond the fast
@@ -139,8 +145,9 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
         }
       }
     }
+    // the marker only has to say whether some row failed: a ballot, not a sum
     lsum = wave_sum(lsum);
-    chk = wave_sum(chk);
+    chk = __builtin_amdgcn_ballot_w64(chk != chk) != 0 ? __builtin_nanf("") : 0.0f;
     if (lane == 0) sPart[i] = Part<float>{lsum, chk};
     if (!skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -251,7 +258,7 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
     }
     // a skipped tree writes no ∂L/∂c partials: finalize marks it failed
     lsum = wave_sum(lsum);
-    chk = wave_sum(chk);
+    chk = __builtin_amdgcn_ballot_w64(chk != chk) != 0 ? __builtin_nanf("") : 0.0f;
     if (lane == 0) dst[i] = Part<float>{lsum, chk};
     if (!skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

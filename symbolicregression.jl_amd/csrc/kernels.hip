@@ -4,6 +4,8 @@
 // eval_kernel.h (instantiated by eval_f32.hip / eval_f64.hip).
 #include <hip/hip_runtime.h>
 
+#include <cstdlib>
+
 #include "kernels.h"
 
 #include <algorithm>
@@ -162,6 +164,25 @@ bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_
   int ntg = (target_wg + p->nrg - 1) / p->nrg;
   const int max_groups = (nlist + 3) / 4;  // at least ~4 trees (one per wave) per group
   if (ntg > max_groups) ntg = max_groups;
+  // XCD affinity: workgroups are dealt round-robin to the 8 XCDs, and block b
+  // runs tree group b % ntg, so with ntg a divisor or multiple of 8 every XCD
+  // runs a fixed subset of the tree groups and its L2 keeps only their code /
+  // programs. SRHIP_XCD_NTG=1 turns it on; measured neutral on config #2
+  // (3.40 vs 3.41 ms, profiles/r02i_evalknobs.txt), so off by default.
+  static const bool xcd = [] {
+    const char* e = std::getenv("SRHIP_XCD_NTG");
+    return e && e[0] == '1';
+  }();
+  if (xcd && ntg > 1) {
+    if (ntg <= 8) {
+      int q = 1;
+      while (q < ntg) q *= 2;
+      ntg = q;
+    } else {
+      ntg = (ntg + 4) / 8 * 8;
+    }
+    if (ntg > max_groups) ntg = std::max(1, max_groups);
+  }
   // the group's partial slots live in LDS next to the row tile: with many
   // trees and few tree groups (huge row counts) they bound the group size
   const size_t lds_cap = 160 * 1024 - 16;

@@ -1,0 +1,10 @@
+#!/bin/bash
+cd "$GRAFT_REPO_ROOT"; mkdir -p gpurun_out
+SRHIP_JIT_COOP=1 timeout -k 10 300 python -u -m pytest tests/test_jit_gpu.py tests/test_full_size.py -m gpu -q --timeout 120 --timeout-method thread > gpurun_out/pytest_coop.log 2>&1
+rc=$?; tail -3 gpurun_out/pytest_coop.log; if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
+run() { echo "== $*"; env "$@" timeout -k 10 200 python3 bench.py --no-cpu --steps 20 --warmup 5 > gpurun_out/coop.log 2>&1 || exit $?;
+        tail -1 gpurun_out/coop.log | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('kernel_ms', round(d['roofline']['kernel_ms'],3), 'frac', round(d['roofline']['frac'],4))"; }
+run SRHIP_JIT_COOP=0
+run SRHIP_JIT_COOP=1
+run SRHIP_JIT_COOP=0
+run SRHIP_JIT_COOP=1
