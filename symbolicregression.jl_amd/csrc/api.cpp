@@ -401,6 +401,16 @@ bool jit_wanted(int nshallow) {
   if (e && e[0] == '1') return true;
   return nshallow >= 512;
 }
+// Tree code: SRHIP_JIT_CONTIG=1 gives tree group g the contiguous slots
+// [g*tpb, (g+1)*tpb) of the cost-sorted list (its code one contiguous range).
+// Measured slower than the snake deal (config #2 3.39 -> 3.63 ms, config #5
+// gradient 49.6 -> 60.9 ms: the expensive trees end up in a few groups;
+// profiles/r02i_evalknobs.txt), so off by default.
+bool jit_contig() {
+  const char* e = std::getenv("SRHIP_JIT_CONTIG");  // read per launch: A/B measurements
+  return e && e[0] == '1';
+}
+
 // LDS for the row tiles of a tree-code workgroup (SRHIP_EVAL_LDS, KiB)
 size_t jit_tile_budget() {
   static const size_t b = [] {
@@ -617,6 +627,7 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
     if (!plan_eval(p->dtype, false, OPSET_FULL, MODE_LOSS, ja.w != nullptr, nfeat, rows, nb, &plan))
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile does not fit in LDS");
     EvalArgs<T> a = ja;
+    a.contig = 0;  // the interpreter kernel deals its slots in snake order
     a.list = static_cast<const int32_t*>(c->bail_list.p);
     a.list_off = a.list + nb;
     a.fail = static_cast<uint32_t*>(c->bail_fail.p);
@@ -673,15 +684,36 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   const bool use_jit = std::is_same<T, float>::value && p->jit && p->nlist_j > 0 && mode == MODE_LOSS &&
                        loss == SRHIP_LOSS_L2;
   const int nj = use_jit ? p->nlist_j : 0;
-  for (int pass = -1; pass < 2; ++pass) {
-    if (pass == -1 && nj == 0) continue;
-    const int s0 = pass == -1 ? 0 : pass == 0 ? nj : p->nlist_a;
-    const int nlist = pass == -1 ? nj : pass == 0 ? p->nlist_a - nj : p->nlist_b;
-    if (nlist == 0 || rows == 0) continue;
+  // launches: the tree-code parts (pass -1, one per code object), the shallow
+  // interpreter (0), the deep interpreter (1)
+  struct Launch { int pass, s0, nlist, part; };
+  std::vector<Launch> launches;
+  if (nj > 0) {
+    if constexpr (std::is_same<T, float>::value) {
+      HIP_CHECK(jit::reset_flags(p->jit, s));
+      for (int k = 0; k < jit::nparts(p->jit); ++k) {
+        int s0, nsl;
+        jit::part(p->jit, k, &s0, &nsl);
+        launches.push_back({-1, s0, nsl, k});
+      }
+    }
+  }
+  launches.push_back({0, nj, p->nlist_a - nj, -1});
+  launches.push_back({1, p->nlist_a, p->nlist_b, -1});
+  for (size_t li = 0; li < launches.size(); ++li) {
+    const int pass = launches[li].pass;
+    const int s0 = launches[li].s0;
+    const int nlist = launches[li].nlist;
+    const bool last_jit = pass == -1 && (li + 1 == launches.size() || launches[li + 1].pass != -1);
+    if (nlist == 0 || rows == 0) {
+      if (last_jit) throw Error(SRHIP_ERR_INVALID, "empty tree-code part");
+      continue;
+    }
     EvalPlan plan;
     if (pass == -1) {
       const int narr = 1 + nfeat + (w ? 1 : 0);
-      if (!plan_geometry(4, 4, kShallowSlots, narr, 2 * 4, rows, nlist, &plan, jit_tile_budget()))
+      // partials go to global memory: LDS holds the tiles (1 byte per slot keeps the slot bound away)
+      if (!plan_geometry(4, 4, kShallowSlots, narr, 1, rows, nlist, &plan, jit_tile_budget(), 52 * 1024))
         throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
     } else if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan)) {
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
@@ -713,6 +745,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.nrg = plan.nrg;
     a.loss = loss;
     a.rotate = rotate_enabled() ? 1 : 0;
+    a.contig = (pass == -1 && jit_contig()) ? 1 : 0;
     a.lparam = (T)lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);
@@ -720,7 +753,8 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.out_stride = out_stride;
     HIP_CHECK(hipEventRecord(c->ev[0], s));
     if (pass == -1) {
-      if constexpr (std::is_same<T, float>::value) HIP_CHECK(jit::launch(p->jit, plan, a, jit_fast_enabled(), s));
+      if constexpr (std::is_same<T, float>::value)
+        HIP_CHECK(jit::launch(p->jit, launches[li].part, plan, a, jit_fast_enabled(), s));
     } else {
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
@@ -736,7 +770,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
       std::fprintf(stderr, "srhip pass %s: %d trees, %.3f ms (grid %d x %d, %d tiles/wg)\n",
                    pass == -1 ? "tree-code" : pass == 0 ? "shallow" : "deep", nlist, ms, plan.nrg, plan.ntg,
                    plan.ntiles);
-    if (pass == -1) rerun_bailed<T>(c, p, a, plan, nfeat, rows, loss, lparam);
+    if (last_jit) rerun_bailed<T>(c, p, a, plan, nfeat, rows, loss, lparam);
   }
 }
 
@@ -887,6 +921,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
           a.tpb = plan.tpb;
           a.nrg = plan.nrg;
           a.loss = loss;
+          a.contig = jit_contig() ? 1 : 0;
           c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<float>));
           a.partial = static_cast<Part<float>*>(c->partial.p);
           HIP_CHECK(hipEventRecord(c->ev[0], s));

@@ -800,21 +800,32 @@ static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool 
   return true;
 }
 
-struct Module {
+// One loaded code object per part: a batch whose code exceeds one code area
+// (8 MiB) is split into consecutive slot ranges, one launch each.
+struct ModulePart {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr;
-  int32_t* d_off = nullptr;    // [nslots] code offsets
-  uint32_t* d_bail = nullptr;  // [nslots + 2]: bail flags, bail count, PRECISE redo count
+  int32_t* d_off = nullptr;  // [nslots] code offsets
+  int slot0 = 0, nslots = 0;
+};
+struct Module {
+  std::vector<ModulePart> parts;
+  uint32_t* d_bail = nullptr;  // [nslots + 2]: bail flags of all slots, bail count, PRECISE redo count
   int nslots = 0;
 };
 
 bool available() { return templates().ok; }
 const char* unavailable_reason() { return templates().why.c_str(); }
 
-static bool codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt,
-                    std::vector<uint32_t>& words, std::vector<std::string>* lines, std::vector<int32_t>& offs,
-                    std::vector<int32_t>& ok_trees, std::vector<int32_t>& rest, Stats* st, const Tmpl& T) {
-  for (int32_t t : cand) {
+// Trees that compile are appended to ok_trees / offs, the others to `rest`; a
+// tree that no longer fits in the area ends the call (returns its position in
+// cand; cand.size() when all were done).
+static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, size_t from,
+                      const Options& opt, std::vector<uint32_t>& words, std::vector<std::string>* lines,
+                      std::vector<int32_t>& offs, std::vector<int32_t>& ok_trees, std::vector<int32_t>& rest,
+                      Stats* st, const Tmpl& T) {
+  for (size_t k = from; k < cand.size(); ++k) {
+    const int32_t t = cand[k];
     int32_t off = -1;
     bool f = false;
     std::string why;
@@ -822,12 +833,16 @@ static bool codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& 
     const size_t lbefore = lines ? lines->size() : 0;
     const bool okc = cb.tree_off[t] >= 0 &&
                      gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, opt.text, words, lines, T.area_va, &off, &f, &why);
-    if (okc && words.size() * 4 <= T.area_bytes) {
+    if (okc && words.size() * 4 > T.area_bytes) {  // area full: the next part takes it
+      words.resize(before);
+      if (lines) lines->resize(lbefore);
+      return k;
+    }
+    if (okc) {
       ok_trees.push_back(t);
       offs.push_back(off);
       if (st) { st->ntrees++; st->nfast += f ? 1 : 0; }
     } else {
-      if (okc) why = "code area full";
       words.resize(before);
       if (lines) lines->resize(lbefore);
       rest.push_back(t);
@@ -836,8 +851,7 @@ static bool codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& 
       if (dbg) std::fprintf(stderr, "jit: tree %d not compiled: %s\n", t, why.c_str());
     }
   }
-  if (st) st->code_bytes = words.size() * 4;
-  return !ok_trees.empty();
+  return cand.size();
 }
 
 bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt,
@@ -847,7 +861,7 @@ bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& ca
   std::vector<uint32_t> words;
   std::vector<std::string> lines;
   std::vector<int32_t> offs, okt, rest;
-  codegen(cb, cand, opt, words, opt.text ? &lines : nullptr, offs, okt, rest, st, TT.large);
+  codegen(cb, cand, 0, opt, words, opt.text ? &lines : nullptr, offs, okt, rest, st, TT.large);
   if (bytes) {
     bytes->resize(words.size() * 4);
     std::memcpy(bytes->data(), words.data(), bytes->size());
@@ -871,33 +885,62 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
   const Templates& TT = templates();
   if (!TT.ok) { rest = cand; return nullptr; }
   auto t0 = std::chrono::steady_clock::now();
-  std::vector<uint32_t> words;
-  std::vector<int32_t> offs;
-  codegen(cb, cand, opt, words, nullptr, offs, jit_list, rest, st, TT.large);
-  if (jit_list.empty()) return nullptr;
-  const Tmpl& T = words.size() * 4 <= TT.small.area_bytes ? TT.small : TT.large;
-  if (&T == &TT.small) {  // the code was laid out for the large template's addresses: redo
-    words.clear();
-    offs.clear();
-    std::vector<int32_t> jl, rs;
-    codegen(cb, jit_list, opt, words, nullptr, offs, jl, rs, nullptr, T);
-    if (jl.size() != jit_list.size()) throw Error(SRHIP_ERR_INVALID, "jit: small-template relayout differs");
+  constexpr int kMaxParts = 8;
+  struct Chunk { std::vector<uint32_t> words; std::vector<int32_t> offs, slots; const Tmpl* T; };
+  std::vector<Chunk> chunks;
+  size_t pos = 0, bytes = 0;
+  while (pos < cand.size()) {
+    Chunk ch;
+    ch.T = &TT.large;
+    const size_t next = codegen(cb, cand, pos, opt, ch.words, nullptr, ch.offs, ch.slots, rest, st, TT.large);
+    if (next == pos) {  // one tree larger than the area
+      rest.push_back(cand[pos]);
+      if (st) st->nrejected++;
+      pos = next + 1;
+      continue;
+    }
+    if ((int)chunks.size() + 1 == kMaxParts && next < cand.size()) {  // the rest stays interpreted
+      for (size_t k = next; k < cand.size(); ++k) rest.push_back(cand[k]);
+      if (st) st->nrejected += (int)(cand.size() - next);
+      pos = cand.size();
+    } else {
+      pos = next;
+    }
+    if (ch.slots.empty()) continue;
+    if (ch.words.size() * 4 <= TT.small.area_bytes) {  // relayout for the small template's addresses
+      Chunk sm;
+      sm.T = &TT.small;
+      std::vector<int32_t> rs;
+      codegen(cb, ch.slots, 0, opt, sm.words, nullptr, sm.offs, sm.slots, rs, nullptr, TT.small);
+      if (sm.slots != ch.slots) throw Error(SRHIP_ERR_INVALID, "jit: small-template relayout differs");
+      ch = std::move(sm);
+    }
+    bytes += ch.words.size() * 4;
+    chunks.push_back(std::move(ch));
   }
-  std::vector<uint8_t> img(T.img, T.img + T.size);
-  std::memcpy(img.data() + T.area_off, words.data(), words.size() * 4);
+  if (chunks.empty()) return nullptr;
   auto t1 = std::chrono::steady_clock::now();
   Module* m = new Module();
-  m->nslots = (int)jit_list.size();
   try {
-    HIP_CHECK(hipModuleLoadData(&m->mod, img.data()));
-    HIP_CHECK(hipModuleGetFunction(&m->fn, m->mod, "sr_jit_eval"));
-    HIP_CHECK(hipModuleGetFunction(&m->fn_w, m->mod, "sr_jit_eval_w"));
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(m->fn), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                  160 * 1024));
-    HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(m->fn_w),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    HIP_CHECK(hipMalloc((void**)&m->d_off, offs.size() * sizeof(int32_t)));
-    HIP_CHECK(hipMemcpy(m->d_off, offs.data(), offs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    for (Chunk& ch : chunks) {
+      ModulePart pt;
+      pt.slot0 = m->nslots;
+      pt.nslots = (int)ch.slots.size();
+      m->parts.push_back(pt);
+      ModulePart& q = m->parts.back();
+      std::vector<uint8_t> img(ch.T->img, ch.T->img + ch.T->size);
+      std::memcpy(img.data() + ch.T->area_off, ch.words.data(), ch.words.size() * 4);
+      HIP_CHECK(hipModuleLoadData(&q.mod, img.data()));
+      HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, "sr_jit_eval"));
+      HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, "sr_jit_eval_w"));
+      for (hipFunction_t f : {q.fn, q.fn_w})
+        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+      HIP_CHECK(hipMalloc((void**)&q.d_off, ch.offs.size() * sizeof(int32_t)));
+      HIP_CHECK(hipMemcpy(q.d_off, ch.offs.data(), ch.offs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      m->nslots += pt.nslots;
+      jit_list.insert(jit_list.end(), ch.slots.begin(), ch.slots.end());
+    }
     HIP_CHECK(hipMalloc((void**)&m->d_bail, (size_t)(m->nslots + 2) * sizeof(uint32_t)));
   } catch (...) {
     destroy(m);
@@ -907,45 +950,66 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
   if (st) {
     st->ms_codegen = std::chrono::duration<double, std::milli>(t1 - t0).count();
     st->ms_load = std::chrono::duration<double, std::milli>(t2 - t1).count();
-    st->code_bytes = words.size() * 4;
+    st->code_bytes = bytes;
+    st->nparts = (int)chunks.size();
   }
   return m;
 }
 
 void destroy(Module* m) {
   if (!m) return;
-  if (m->d_off) (void)hipFree(m->d_off);
+  for (ModulePart& q : m->parts) {
+    if (q.d_off) (void)hipFree(q.d_off);
+    if (q.mod) (void)hipModuleUnload(q.mod);
+  }
   if (m->d_bail) (void)hipFree(m->d_bail);
-  if (m->mod) (void)hipModuleUnload(m->mod);
   delete m;
 }
 
-const int32_t* code_off(const Module* m) { return m->d_off; }
 uint32_t* bail_flags(Module* m) { return m->d_bail; }
 int nslots(const Module* m) { return m->nslots; }
+int nparts(const Module* m) { return m ? (int)m->parts.size() : 0; }
+void part(const Module* m, int k, int* slot0, int* nslots) {
+  *slot0 = m->parts[k].slot0;
+  *nslots = m->parts[k].nslots;
+}
 
 struct JitArgs {
   EvalArgs<float> e;
   const int32_t* code_off;
   uint32_t* bail;
+  uint32_t* counters;
   int fast;
+  int part_lds;
 };
 
-hipError_t launch(Module* m, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream) {
-  hipError_t err = hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t), stream);
-  if (err != hipSuccess) return err;
+hipError_t reset_flags(Module* m, hipStream_t stream) {
+  return hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t), stream);
+}
+
+hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream) {
+  const ModulePart& q = m->parts[k];
+  if (a.nlist != q.nslots) return hipErrorInvalidValue;
   JitArgs ja;
   ja.e = a;
-  ja.code_off = m->d_off;
-  ja.bail = m->d_bail;
+  ja.code_off = q.d_off;
+  ja.bail = m->d_bail + q.slot0;
+  ja.counters = m->d_bail + m->nslots;
   ja.fast = fast ? 1 : 0;
+  // partials in LDS when they take little room next to the tiles (measured
+  // faster on config #2: one coalesced write-out instead of a store per tree)
+  const size_t part_bytes = (size_t)a.tpb * sizeof(Part<float>);
+  ja.part_lds = part_bytes <= 8192 ? 1 : 0;
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
   // SRHIP_JIT_LDS_PAD (experiments): extra LDS per workgroup, i.e. fewer resident waves
   static const unsigned pad = [] { const char* e = std::getenv("SRHIP_JIT_LDS_PAD"); return e ? (unsigned)std::atoi(e) : 0u; }();
-  return hipModuleLaunchKernel(a.w ? m->fn_w : m->fn, grid, 1, 1, (unsigned)plan.threads, 1, 1,
-                               (unsigned)plan.lds_bytes + pad, stream, nullptr, cfg);
+  // LDS: the row tiles (+ the partials when part_lds)
+  const size_t narr = 1 + (size_t)a.nfeat + (a.w ? 1 : 0);
+  const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + (ja.part_lds ? part_bytes : 0) + 16;
+  return hipModuleLaunchKernel(a.w ? q.fn_w : q.fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds + pad,
+                               stream, nullptr, cfg);
 }
 
 }  // namespace jit

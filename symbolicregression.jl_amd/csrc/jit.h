@@ -26,6 +26,7 @@ struct Stats {
   int ntrees = 0;          // trees compiled to code
   int nfast = 0;           // of which have a guarded FAST path
   int nrejected = 0;       // trees left to the interpreter (register pool exhausted, ...)
+  int nparts = 0;          // code objects (one launch each)
   size_t code_bytes = 0;
   double ms_codegen = 0.0, ms_load = 0.0;
 };
@@ -43,15 +44,18 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
               std::vector<int32_t>& rest, const Options& opt, Stats* st);
 void destroy(Module* m);
 
-// Per-slot code offsets of the module, in jit_list order (device array).
-const int32_t* code_off(const Module* m);
-// bail flags + counter: [nslots + 1] uint32 (device), cleared by launch
+// bail flags of all slots + bail count + PRECISE redo count: [nslots + 2]
+// uint32 (device), cleared by reset_flags
 uint32_t* bail_flags(Module* m);
 int nslots(const Module* m);
+// the module's code objects: consecutive slot ranges (jit_list order), one launch each
+int nparts(const Module* m);
+void part(const Module* m, int k, int* slot0, int* nslots);
+hipError_t reset_flags(Module* m, hipStream_t stream);
 
-// Launch the driver over the module's trees (EvalArgs as for eval_kernel:
-// list / list_off / fail / partial of the module's slots).
-hipError_t launch(Module* m, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream);
+// Launch part k's driver over its slots (EvalArgs as for eval_kernel: list /
+// list_off / fail / partial of the part's slots).
+hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream);
 
 // Test hook: compile without loading; returns bytes and (opt.text) the
 // assembly text of the whole area image.

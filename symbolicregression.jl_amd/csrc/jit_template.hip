@@ -44,9 +44,11 @@ constexpr int TILE = 64 * R;
 struct JitArgs {
   EvalArgs<float> e;
   const int32_t* code_off;  // [nlist] byte offset of each slot's tree code in the area
-  uint32_t* bail;           // [nlist] set when tree code hands a tile back; [nlist] counts them,
-                            // [nlist + 1] counts tiles redone with the PRECISE routines
+  uint32_t* bail;           // [nlist] set when tree code hands a tile back
+  uint32_t* counters;       // [0] counts those slots, [1] tiles redone with the PRECISE routines
   int fast;                 // 1: trees may run their FAST-routine path (guarded)
+  int part_lds;             // 1: per-tree partials gathered in LDS (after the tiles) and
+                            //    written out together at the end; 0: straight to global memory
 };
 
 template <bool W>
@@ -56,10 +58,14 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   float* sX = reinterpret_cast<float*>(smem);
   const int narr = 1 + a.nfeat + (W ? 1 : 0);
   const int rows = a.ntiles * TILE;
-  Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
   const int rg = blockIdx.x / a.ntg;
   const int g = blockIdx.x - rg * a.ntg;
   const int64_t row0 = (int64_t)rg * rows;
+  // per-tree partials: gathered in LDS after the tiles when the host made room
+  // for them (few trees per group), else stored straight to global memory
+  Part<float>* gdst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
+  Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
+  Part<float>* dst = ja.part_lds ? sPart : gdst;
 
   // 1. stage the row group tile-major: tile t, array k (0 = y, 1.. = x_{k-1}, last = w)
   {
@@ -74,7 +80,6 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
       reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
           reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
     }
-    for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) sPart[i] = Part<float>{0.0f, 0.0f};
   }
   __syncthreads();
 
@@ -84,7 +89,7 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nwaves = (int)(blockDim.x >> 6);
-  auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
+  auto slot_of = [&](int i) { return a.contig ? g * a.tpb + i : i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
   auto code_of = [&](int s) {
     return __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(ja.code_off))[s]);
   };
@@ -141,23 +146,24 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
         chk = __builtin_nanf("");
         if (lane == 0) {
           __hip_atomic_store(ja.bail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-          __hip_atomic_fetch_add(ja.bail + a.nlist, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          __hip_atomic_fetch_add(ja.counters, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
     }
     // the marker only has to say whether some row failed: a ballot, not a sum
     lsum = wave_sum(lsum);
     chk = __builtin_amdgcn_ballot_w64(chk != chk) != 0 ? __builtin_nanf("") : 0.0f;
-    if (lane == 0) sPart[i] = Part<float>{lsum, chk};
+    if (lane == 0) dst[i] = Part<float>{lsum, chk};
     if (!skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (lane == 0 && __builtin_amdgcn_readfirstlane((int)redos) != 0)
-    __hip_atomic_fetch_add(ja.bail + a.nlist + 1, (uint32_t)__builtin_amdgcn_readfirstlane((int)redos),
+    __hip_atomic_fetch_add(ja.counters + 1, (uint32_t)__builtin_amdgcn_readfirstlane((int)redos),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  __syncthreads();
-  Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
-  for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) dst[i] = sPart[i];
+  if (ja.part_lds) {  // slots no wave ran keep whatever: finalize ignores them
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) gdst[i] = sPart[i];
+  }
 }
 
 extern "C" __global__ void __launch_bounds__(256) sr_jit_eval(JitArgs ja) { jit_eval_body<false>(ja); }
@@ -210,7 +216,7 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nwaves = (int)(blockDim.x >> 6);
-  auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
+  auto slot_of = [&](int i) { return a.contig ? g * a.tpb + i : i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
   auto sld = [&](const int32_t* p, int s) {
     return __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(p))[s]);
   };

@@ -39,6 +39,8 @@ struct EvalArgs {
   int nrg;                 // row groups
   int loss;
   int rotate;              // MODE_LOSS: start each wave's tree sequence at row-group-dependent offsets
+  int contig;              // tree group g holds list slots [g*tpb, (g+1)*tpb) (tree code: a group's
+                           // code is one contiguous range); 0: slots dealt in snake order
   T lparam;
   Part<T>* partial;        // [nrg][ntg*tpb]
   T* out;                  // MODE_OUT: [ntrees][out_stride]
@@ -70,7 +72,7 @@ bool plan_eval(int dtype, bool deep, int opset, int mode, bool weighted, int nfe
                int64_t n, int nlist, EvalPlan* plan);
 // Same, for explicit R / D / LDS arrays / partial bytes per tree slot.
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n,
-                   int nlist, EvalPlan* plan, size_t tile_budget = 40 * 1024);
+                   int nlist, EvalPlan* plan, size_t tile_budget = 40 * 1024, size_t two_tile_cap = 0);
 
 // ---- constant gradients (grad_kernels.hip) -----------------------------------
 constexpr int kGradG = 4;  // tangents per pass (constants per "tangent group")

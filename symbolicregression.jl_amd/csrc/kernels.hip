@@ -38,7 +38,7 @@ __global__ void __launch_bounds__(256) finalize_kernel(EvalArgs<T> a, double* __
     c = (sc[0][lane] + sc[1][lane]) + (sc[2][lane] + sc[3][lane]);
     const int g = pos / a.tpb;
     const int i = pos - g * a.tpb;
-    const int sidx = i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
+    const int sidx = a.contig ? g * a.tpb + i : i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
     if (sidx < a.nlist) {
       const int t = a.list[sidx];
       const bool ok = !__builtin_isnan(c);
@@ -141,7 +141,7 @@ hipError_t launch_ti_records(const Ins<float>* prog, const int32_t* list_off, in
 }
 
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n, int nlist,
-                   EvalPlan* p, size_t tile_budget) {
+                   EvalPlan* p, size_t tile_budget, size_t two_tile_cap) {
   p->R = R;
   p->D = D;
   p->opset = OPSET_FULL;
@@ -156,6 +156,9 @@ bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_
   while (nt * 2 <= SR_NTMAX && (int64_t)nt * 2 * p->tile <= 8192 && per_tile * nt * 2 <= budget &&
          (int64_t)nt * p->tile < n)
     nt *= 2;
+  // at least two tiles when two fit in two_tile_cap: a tree call covers twice
+  // the rows (wide datasets, whose single tile already fills the budget)
+  if (nt == 1 && two_tile_cap && per_tile * 2 <= two_tile_cap && (int64_t)p->tile < n) nt = 2;
   p->ntiles = nt;
   p->rows_wg = nt * p->tile;
   p->nrg = (int)((n + p->rows_wg - 1) / p->rows_wg);
