@@ -258,3 +258,39 @@ def test_set_constants_in_place(gpu_ctx, T, n):
             os.environ.pop("SRHIP_JIT", None)
         else:
             os.environ["SRHIP_JIT"] = old
+
+
+def test_vectorised_backtrack_step_matches_scalar():
+    """_backtrack_steps (all candidates at once) equals _backtrack_step (the
+    LineSearches BackTracking order-3 interpolation) element by element."""
+    from srhip.constant_optimization import _backtrack_step, _backtrack_steps
+
+    rng = np.random.default_rng(4)
+    n = 2000
+    a1 = rng.uniform(0.01, 1, n)
+    a2 = a1 * rng.uniform(0.1, 0.9, n)
+    phi0 = rng.standard_normal(n)
+    dphi0 = -np.abs(rng.standard_normal(n))
+    phix0 = phi0 + np.abs(rng.standard_normal(n))
+    phix1 = phi0 + rng.standard_normal(n)
+    phix1[::17] = np.inf
+    phix1[::29] = phi0[::29] + dphi0[::29] * a2[::29]  # den == 0 on the first shrink
+    first = rng.random(n) < 0.5
+    vec = _backtrack_steps(a1, a2, phi0, dphi0, phix0, phix1, first)
+    with np.errstate(all="ignore"):
+        ref = np.array([_backtrack_step(a1[k], a2[k], phi0[k], dphi0[k], phix0[k], phix1[k], first[k])
+                        for k in range(n)])
+    np.testing.assert_allclose(vec, ref, rtol=1e-14)  # a1**3 on arrays may round differently by an ulp
+
+
+def test_flat_take_matches_flatten():
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(60, o, 4, np.float32, seed=2)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    idx = [5, 5, 0, 59, 17, 5]
+    got = flat.take(idx)
+    ref = srhip.flatten([trees[i] for i in idx], o, dtype=np.float32)
+    for k in ("node_off", "kind", "arg", "const_off", "consts", "nodes"):
+        np.testing.assert_array_equal(getattr(got, k), getattr(ref, k))
+    c = np.arange(ref.const_off[-1], dtype=np.float32)
+    np.testing.assert_array_equal(flat.take(idx, c).consts, c)
