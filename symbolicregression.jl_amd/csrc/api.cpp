@@ -411,6 +411,12 @@ bool jit_contig() {
   return e && e[0] == '1';
 }
 
+// Tree code: every tree group of a row group on one XCD (SRHIP_RG_XCD=1)
+bool rg_xcd() {
+  const char* e = std::getenv("SRHIP_RG_XCD");  // read per launch: A/B measurements
+  return e && e[0] == '1';
+}
+
 // LDS for the row tiles of a tree-code workgroup (SRHIP_EVAL_LDS, KiB)
 size_t jit_tile_budget() {
   static const size_t b = [] {
@@ -628,6 +634,7 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile does not fit in LDS");
     EvalArgs<T> a = ja;
     a.contig = 0;  // the interpreter kernel deals its slots in snake order
+    a.rotate = 0;
     a.list = static_cast<const int32_t*>(c->bail_list.p);
     a.list_off = a.list + nb;
     a.fail = static_cast<uint32_t*>(c->bail_fail.p);
@@ -746,6 +753,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.loss = loss;
     a.rotate = rotate_enabled() ? 1 : 0;
     a.contig = (pass == -1 && jit_contig()) ? 1 : 0;
+    if (pass == -1 && rg_xcd()) a.rotate = 2;  // tree code: row groups per XCD (experiment)
     a.lparam = (T)lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);
@@ -922,6 +930,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
           a.nrg = plan.nrg;
           a.loss = loss;
           a.contig = jit_contig() ? 1 : 0;
+          a.rotate = rg_xcd() ? 2 : 0;
           c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<float>));
           a.partial = static_cast<Part<float>*>(c->partial.p);
           HIP_CHECK(hipEventRecord(c->ev[0], s));

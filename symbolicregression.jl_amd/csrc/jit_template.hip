@@ -41,6 +41,25 @@ constexpr int R = SR_JIT_R;
 constexpr int TILE = 64 * R;
 }  // namespace
 
+// Block → (row group, tree group). Default: rg = b / ntg, g = b % ntg.
+// a.rotate == 2 (SRHIP_RG_XCD=1, experiment): blocks are dealt round-robin
+// over the 8 XCDs (b % 8 share one), so rg = (b/8 / ntg)·8 + b % 8 and
+// g = (b/8) % ntg put every tree group of a row group on the same XCD (its X
+// tile is read from HBM once per XCD); the grid is padded to whole octets of
+// row groups and the padding blocks return at once.
+__device__ __forceinline__ bool block_of(const EvalArgs<float>& a, int& rg, int& g) {
+  const int b = blockIdx.x;
+  if (a.rotate == 2) {
+    const int k = b >> 3;
+    rg = (k / a.ntg) * 8 + (b & 7);
+    g = k % a.ntg;
+    return rg < a.nrg;
+  }
+  rg = b / a.ntg;
+  g = b - rg * a.ntg;
+  return true;
+}
+
 struct JitArgs {
   EvalArgs<float> e;
   const int32_t* code_off;  // [nlist] byte offset of each slot's tree code in the area
@@ -58,8 +77,8 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   float* sX = reinterpret_cast<float*>(smem);
   const int narr = 1 + a.nfeat + (W ? 1 : 0);
   const int rows = a.ntiles * TILE;
-  const int rg = blockIdx.x / a.ntg;
-  const int g = blockIdx.x - rg * a.ntg;
+  int rg, g;
+  if (!block_of(a, rg, g)) return;
   const int64_t row0 = (int64_t)rg * rows;
   // per-tree partials: gathered in LDS after the tiles when the host made room
   // for them (few trees per group), else stored straight to global memory
@@ -191,8 +210,8 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sX = reinterpret_cast<float*>(smem);
   const int narr = 1 + a.nfeat + (W ? 1 : 0);
-  const int rg = blockIdx.x / a.ntg;
-  const int g = blockIdx.x - rg * a.ntg;
+  int rg, g;
+  if (!block_of(a, rg, g)) return;
   const int rows = a.ntiles * TILE;
   const int64_t row0 = (int64_t)rg * rows;
   {

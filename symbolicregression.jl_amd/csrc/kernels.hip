@@ -156,6 +156,11 @@ bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_
   while (nt * 2 <= SR_NTMAX && (int64_t)nt * 2 * p->tile <= 8192 && per_tile * nt * 2 <= budget &&
          (int64_t)nt * p->tile < n)
     nt *= 2;
+  // SRHIP_TREE_NT (experiments): tiles per workgroup of tree code, any count
+  if (two_tile_cap) {
+    static const int force = [] { const char* e = std::getenv("SRHIP_TREE_NT"); return e ? std::atoi(e) : 0; }();
+    if (force > 0 && per_tile * force <= 150 * 1024) nt = force;
+  }
   // at least two tiles when two fit in two_tile_cap: a tree call covers twice
   // the rows (wide datasets, whose single tile already fills the budget)
   if (nt == 1 && two_tile_cap && per_tile * 2 <= two_tile_cap && (int64_t)p->tile < n) nt = 2;
