@@ -97,6 +97,17 @@ struct srhip_ctx {
   hipStream_t stream = nullptr;
   std::mutex mu;
   hipEvent_t ev[4] = {nullptr, nullptr, nullptr, nullptr};
+  // kernel timing of the current call: event pairs recorded around each launch
+  // and read after the call's one stream synchronisation (timing_finish)
+  std::vector<hipEvent_t> tev;
+  int tpairs = 0;
+  bool timing_pending = false;
+  bool cnt_pending = false;    // tree-code bail / PRECISE-redo counters copied to pin_cnt
+  // pinned host copies of the per-tree results 
+  double* pin_sum = nullptr;
+  uint8_t* pin_ok = nullptr;
+  size_t pin_cap = 0;
+  uint32_t* pin_cnt = nullptr;  // [2]
   double last_ms = 0.0;
   int last_launches = 0;
   int last_bailed = 0;  // trees re-evaluated after their tree code handed a tile back
@@ -195,6 +206,48 @@ void ensure_dev(void** ptr, size_t* cap, size_t bytes) {
   *cap = 0;
   HIP_CHECK(hipMalloc(ptr, bytes));
   *cap = bytes;
+}
+
+// ---- per-call kernel timing (no synchronisation per launch) -----------------------
+void timing_reset(srhip_ctx* c) {
+  c->last_ms = 0.0;
+  c->last_launches = 0;
+  c->last_bailed = 0;
+  c->last_redone = 0;
+  c->tpairs = 0;
+  c->timing_pending = false;
+  c->cnt_pending = false;
+}
+int timed_begin(srhip_ctx* c, hipStream_t s) {
+  while (c->tev.size() < 2 * (size_t)(c->tpairs + 1)) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreate(&e));
+    c->tev.push_back(e);
+  }
+  HIP_CHECK(hipEventRecord(c->tev[2 * (size_t)c->tpairs], s));
+  return c->tpairs++;
+}
+void timed_end(srhip_ctx* c, hipStream_t s, int k) {
+  HIP_CHECK(hipEventRecord(c->tev[2 * (size_t)k + 1], s));
+  c->timing_pending = true;
+  c->last_launches += 1;
+}
+// after the stream is synchronised: kernel times and the copied-back counters
+void timing_finish(srhip_ctx* c) {
+  if (c->timing_pending) {
+    double tot = 0.0;
+    for (int k = 0; k < c->tpairs; ++k) {
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, c->tev[2 * (size_t)k], c->tev[2 * (size_t)k + 1]));
+      tot += ms;
+    }
+    c->last_ms = tot;
+    c->timing_pending = false;
+  }
+  if (c->cnt_pending) {
+    c->last_redone = c->pin_cnt[1];
+    c->cnt_pending = false;
+  }
 }
 
 void free_grad_device(srhip_program* p) {
@@ -604,6 +657,11 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
   if constexpr (std::is_same<T, float>::value) {
     hipStream_t s = c->stream;
     const int nj = p->nlist_j;
+    if (!jit::can_bail()) {  // no routine hands a tile back: only the counters, read with the results
+      HIP_CHECK(hipMemcpyAsync(c->pin_cnt, jit::bail_flags(p->jit) + nj, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+      c->cnt_pending = true;
+      return;
+    }
     std::vector<uint32_t> flags((size_t)nj + 2);
     HIP_CHECK(hipMemcpyAsync(flags.data(), jit::bail_flags(p->jit), flags.size() * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, s));
@@ -654,18 +712,12 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
     a.lparam = (T)lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);
-    HIP_CHECK(hipEventRecord(c->ev[2], s));
+    const int tk = timed_begin(c, s);
     HIP_CHECK(launch_eval<T>(plan, a, MODE_LOSS, s));
-    HIP_CHECK(hipEventRecord(c->ev[3], s));
+    timed_end(c, s, tk);
     HIP_CHECK(launch_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
-    HIP_CHECK(hipEventSynchronize(c->ev[3]));
-    float ms = 0.f;
-    HIP_CHECK(hipEventElapsedTime(&ms, c->ev[2], c->ev[3]));
-    c->last_ms += ms;
-    c->last_launches += 1;
     c->last_bailed = nb;
-    if (std::getenv("SRHIP_DEBUG_PASSES"))
-      std::fprintf(stderr, "srhip pass bail-rerun: %d trees, %.3f ms\n", nb, ms);
+    if (std::getenv("SRHIP_DEBUG_PASSES")) std::fprintf(stderr, "srhip pass bail-rerun: %d trees\n", nb);
   }
 }
 
@@ -676,10 +728,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
               const T* w, int64_t rows, int64_t n_pad, int nfeat, int loss, double lparam,
               T* out, int64_t out_stride) {
   hipStream_t s = c->stream;
-  c->last_ms = 0.0;
-  c->last_launches = 0;
-  c->last_bailed = 0;
-  c->last_redone = 0;
+  timing_reset(c);
   c->sums.ensure(std::max<size_t>(p->ntrees, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(p->ntrees, 1));
   const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
@@ -759,50 +808,74 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.partial = static_cast<Part<T>*>(c->partial.p);
     a.out = out;
     a.out_stride = out_stride;
-    HIP_CHECK(hipEventRecord(c->ev[0], s));
+    const int tk = timed_begin(c, s);
     if (pass == -1) {
       if constexpr (std::is_same<T, float>::value)
         HIP_CHECK(jit::launch(p->jit, launches[li].part, plan, a, jit_fast_enabled(), s));
     } else {
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
-    HIP_CHECK(hipEventRecord(c->ev[1], s));
+    timed_end(c, s, tk);
     HIP_CHECK(launch_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
-    HIP_CHECK(hipEventSynchronize(c->ev[1]));
-    float ms = 0.f;
-    HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-    c->last_ms += ms;
-    c->last_launches += 1;
     static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
-    if (dbg)
+    if (dbg) {  // debugging only: wait for the launch to report its time
+      HIP_CHECK(hipStreamSynchronize(s));
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, c->tev[2 * (size_t)tk], c->tev[2 * (size_t)tk + 1]));
       std::fprintf(stderr, "srhip pass %s: %d trees, %.3f ms (grid %d x %d, %d tiles/wg)\n",
                    pass == -1 ? "tree-code" : pass == 0 ? "shallow" : "deep", nlist, ms, plan.nrg, plan.ntg,
                    plan.ntiles);
+    }
     if (last_jit) rerun_bailed<T>(c, p, a, plan, nfeat, rows, loss, lparam);
+  }
+}
+
+// Copy per-tree results to the caller, applying the static verdicts.
+void ensure_pinned(srhip_ctx* c, size_t nt) {
+  if (nt <= c->pin_cap) return;
+  if (c->pin_sum) (void)hipHostFree(c->pin_sum);
+  if (c->pin_ok) (void)hipHostFree(c->pin_ok);
+  c->pin_sum = nullptr;
+  c->pin_ok = nullptr;
+  c->pin_cap = 0;
+  HIP_CHECK(hipHostMalloc((void**)&c->pin_sum, nt * sizeof(double), hipHostMallocDefault));
+  HIP_CHECK(hipHostMalloc((void**)&c->pin_ok, nt, hipHostMallocDefault));
+  c->pin_cap = nt;
+}
+
+// the per-tree results to pinned host memory (asynchronous)
+bool enqueue_result_copies(srhip_ctx* c, const srhip_program* p, int64_t rows) {
+  const int nt = p->ntrees;
+  if (!(rows > 0 && nt > 0 && (p->nlist_a + p->nlist_b) > 0)) return false;
+  HIP_CHECK(hipMemcpyAsync(c->pin_sum, c->sums.p, nt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
+  HIP_CHECK(hipMemcpyAsync(c->pin_ok, c->oks.p, nt, hipMemcpyDeviceToHost, c->stream));
+  return true;
+}
+
+// wait for the call, then the per-tree results with the static verdicts applied
+void finish_results(srhip_ctx* c, const srhip_program* p, int64_t rows, bool copied, double* out_sum,
+                    uint8_t* out_ok) {
+  HIP_CHECK(hipStreamSynchronize(c->stream));
+  timing_finish(c);
+  const int nt = p->ntrees;
+  for (int t = 0; t < nt; ++t) {
+    bool ok;
+    double sm;
+    if (p->static_fail[t]) { ok = false; sm = NAN; }
+    else if (p->fail_if_rows[t]) { ok = rows == 0; sm = rows == 0 ? 0.0 : NAN; }
+    else if (rows == 0 || !copied) { ok = true; sm = 0.0; }
+    else { ok = c->pin_ok[t] != 0; sm = c->pin_sum[t]; }
+    if (out_sum) out_sum[t] = sm;
+    if (out_ok) out_ok[t] = ok ? 1 : 0;
   }
 }
 
 // Copy per-tree results to the caller, applying the static verdicts.
 void collect_results(srhip_ctx* c, const srhip_program* p, int64_t rows, double* out_sum,
                      uint8_t* out_ok) {
-  const int nt = p->ntrees;
-  c->h_sum.assign(nt, 0.0);
-  c->h_ok.assign(nt, 1);
-  if (rows > 0 && nt > 0 && (p->nlist_a + p->nlist_b) > 0) {
-    HIP_CHECK(hipMemcpyAsync(c->h_sum.data(), c->sums.p, nt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
-    HIP_CHECK(hipMemcpyAsync(c->h_ok.data(), c->oks.p, nt, hipMemcpyDeviceToHost, c->stream));
-  }
-  HIP_CHECK(hipStreamSynchronize(c->stream));
-  for (int t = 0; t < nt; ++t) {
-    bool ok;
-    double sm;
-    if (p->static_fail[t]) { ok = false; sm = NAN; }
-    else if (p->fail_if_rows[t]) { ok = rows == 0; sm = rows == 0 ? 0.0 : NAN; }
-    else if (rows == 0) { ok = true; sm = 0.0; }
-    else { ok = c->h_ok[t] != 0; sm = c->h_sum[t]; }
-    if (out_sum) out_sum[t] = sm;
-    if (out_ok) out_ok[t] = ok ? 1 : 0;
-  }
+  ensure_pinned(c, std::max(p->ntrees, 1));
+  const bool copied = enqueue_result_copies(c, p, rows);
+  finish_results(c, p, rows, copied, out_sum, out_ok);
 }
 
 template <typename T>
@@ -844,8 +917,7 @@ int eval_loss_impl(srhip_dataset* ds, const srhip_program* p, int loss, const do
     rows = nidx;
     n_pad = gp;
   }
-  run_eval<T>(c, p, MODE_LOSS, X, y, w, rows, n_pad, ds->nfeat, loss, params ? params[0] : 0.0,
-              nullptr, 0);
+  run_eval<T>(c, p, MODE_LOSS, X, y, w, rows, n_pad, ds->nfeat, loss, params ? params[0] : 0.0, nullptr, 0);
   collect_results(c, p, rows, out_sum, out_ok);
   if (out_wsum) *out_wsum = wsum;
   return SRHIP_OK;
@@ -878,10 +950,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
               T* out_value, T* out_grad, int64_t out_stride) {
   build_grad_program<T>(p);
   hipStream_t s = c->stream;
-  c->last_ms = 0.0;
-  c->last_launches = 0;
-  c->last_bailed = 0;
-  c->last_redone = 0;
+  timing_reset(c);
   const int nt = p->ntrees;
   const int nconst = p->const_off.back();
   c->sums.ensure(std::max<size_t>(nt, 1) * sizeof(double));
@@ -933,20 +1002,19 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
           a.rotate = rg_xcd() ? 2 : 0;
           c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<float>));
           a.partial = static_cast<Part<float>*>(c->partial.p);
-          HIP_CHECK(hipEventRecord(c->ev[0], s));
+          const int tk = timed_begin(c, s);
           HIP_CHECK(jit::launch_grad_code(p->gjit, k, plan, a, p->d_gconsts, static_cast<float*>(c->gpart.p), nconst,
                                           s));
-          HIP_CHECK(hipEventRecord(c->ev[1], s));
+          timed_end(c, s, tk);
           HIP_CHECK(launch_finalize<float>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
-          HIP_CHECK(hipEventSynchronize(c->ev[1]));
-          float ms = 0.f;
-          HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-          c->last_ms += ms;
-          c->last_launches += 1;
           static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
-          if (dbg)
+          if (dbg) {
+            HIP_CHECK(hipStreamSynchronize(s));
+            float ms = 0.f;
+            HIP_CHECK(hipEventElapsedTime(&ms, c->tev[2 * (size_t)tk], c->tev[2 * (size_t)tk + 1]));
             std::fprintf(stderr, "srhip grad tree code part %d: %d trees, %.3f ms (grid %d x %d, %d tiles/wg)\n", k,
                          nsl, ms, plan.nrg, plan.ntg, plan.ntiles);
+          }
         }
         HIP_CHECK(launch_gconst_finalize(static_cast<const float*>(c->gpart.p), plans[0].nrg, nconst,
                                          p->d_gjit_cidx, p->ngjit_cidx, static_cast<double*>(c->dloss.p), s));
@@ -992,20 +1060,19 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
     a.out_value = out_value;
     a.out_grad = out_grad;
     a.out_stride = out_stride;
-    HIP_CHECK(hipEventRecord(c->ev[0], s));
+    const int tk = timed_begin(c, s);
     HIP_CHECK(launch_grad<T>(plan, a, mode, s));
-    HIP_CHECK(hipEventRecord(c->ev[1], s));
+    timed_end(c, s, tk);
     HIP_CHECK(launch_grad_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p),
                                       static_cast<double*>(c->dloss.p), s));
-    HIP_CHECK(hipEventSynchronize(c->ev[1]));
-    float ms = 0.f;
-    HIP_CHECK(hipEventElapsedTime(&ms, c->ev[0], c->ev[1]));
-    c->last_ms += ms;
-    c->last_launches += 1;
     static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
-    if (dbg)
+    if (dbg) {
+      HIP_CHECK(hipStreamSynchronize(s));
+      float ms = 0.f;
+      HIP_CHECK(hipEventElapsedTime(&ms, c->tev[2 * (size_t)tk], c->tev[2 * (size_t)tk + 1]));
       std::fprintf(stderr, "srhip grad pass %d: %d items, G=%d, R=%d, opset %d, %.3f ms (grid %d x %d, %d tiles/wg)\n",
                    pass, nitems, G, plan.R, a.opset, ms, plan.nrg, plan.ntg, plan.ntiles);
+    }
   }
 }
 
@@ -1024,6 +1091,7 @@ void collect_grad_results(srhip_ctx* c, const srhip_program* p, int64_t rows, do
       HIP_CHECK(hipMemcpyAsync(hd.data(), c->dloss.p, nconst * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   }
   HIP_CHECK(hipStreamSynchronize(c->stream));
+  timing_finish(c);
   for (int t = 0; t < nt; ++t) {
     const bool fail = p->g_static_fail[t] || (rows > 0 && !c->h_ok[t]);
     if (out_ok) out_ok[t] = fail ? 0 : 1;
@@ -1143,6 +1211,7 @@ int32_t srhip_open(int32_t device, srhip_ctx** out_ctx) {
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->pin_cnt, 2 * sizeof(uint32_t), hipHostMallocDefault);
     if (e != hipSuccess) {
       delete c;
       throw Error(SRHIP_ERR_DEVICE, std::string("stream/event creation: ") + hipGetErrorString(e));
@@ -1169,6 +1238,11 @@ int32_t srhip_close(srhip_ctx* ctx) {
     ctx->bail_fail.release();
     for (auto& e : ctx->ev)
       if (e) (void)hipEventDestroy(e);
+    for (auto& e : ctx->tev)
+      if (e) (void)hipEventDestroy(e);
+    for (void* h : {(void*)ctx->pin_sum, (void*)ctx->pin_ok, (void*)ctx->pin_cnt})
+      if (h) (void)hipHostFree(h);
+    ctx->gpart.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return SRHIP_OK;
@@ -1473,6 +1547,13 @@ int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog,
 int32_t srhip_last_kernel_time(const srhip_ctx* ctx, double* out_ms, int32_t* out_launches) {
   return guarded([&] {
     if (!ctx) throw Error(SRHIP_ERR_INVALID, "null ctx");
+    auto* c = const_cast<srhip_ctx*>(ctx);
+    if (c->timing_pending || c->cnt_pending) {  // a call that returned before its results were read
+      std::lock_guard<std::mutex> lk(c->mu);
+      HIP_CHECK(hipSetDevice(c->device));
+      HIP_CHECK(hipStreamSynchronize(c->stream));
+      timing_finish(c);
+    }
     if (out_ms) *out_ms = ctx->last_ms;
     if (out_launches) *out_launches = ctx->last_launches;
     return SRHIP_OK;
@@ -1530,6 +1611,13 @@ int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, i
 int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* out_redone) {
   return guarded([&] {
     if (!ctx || !out_ntrees) throw Error(SRHIP_ERR_INVALID, "null argument");
+    auto* c = const_cast<srhip_ctx*>(ctx);
+    if (c->timing_pending || c->cnt_pending) {
+      std::lock_guard<std::mutex> lk(c->mu);
+      HIP_CHECK(hipSetDevice(c->device));
+      HIP_CHECK(hipStreamSynchronize(c->stream));
+      timing_finish(c);
+    }
     *out_ntrees = ctx->last_bailed;
     if (out_redone) *out_redone = ctx->last_redone;
     return SRHIP_OK;

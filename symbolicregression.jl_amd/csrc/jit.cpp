@@ -815,6 +815,11 @@ struct Module {
 };
 
 bool available() { return templates().ok; }
+bool can_bail() {
+  for (int k = 0; k < kNumRoutines; ++k)
+    if (kRoutineTrig[k]) return true;
+  return false;
+}
 const char* unavailable_reason() { return templates().why.c_str(); }
 
 // Trees that compile are appended to ok_trees / offs, the others to `rest`; a

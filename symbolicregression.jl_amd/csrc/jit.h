@@ -34,6 +34,9 @@ struct Stats {
 // The embedded template could be parsed (false: no tree compiler, the
 // interpreter runs everything).
 bool available();
+// some routine can hand a tile back to the interpreter (sin/cos built with
+// TRIG_BAIL in gen_jit.py); false: the bail flags never need reading
+bool can_bail();
 const char* unavailable_reason();
 
 // Compile the trees `cand` (tree ids, in list order) of `cb`. Trees that
