@@ -159,12 +159,16 @@ def routine_list():
         else:
             mk = "chk = mark(s.a[r], chk); " if u in LOSSY_UOPS else ""
             rs.append((f"u_{u.lower()}", rows(f"{mk}s.a[r] = dev::uop<SRHIP_UOP_{u}>(s.a[r]);"), False))
+            if u == "EXP":  # the compiled body beside the hand-scheduled one (tests: SRHIP_JIT_MANUAL=0)
+                rs.append(("u_exp_full", rows(f"{mk}s.a[r] = dev::uop<SRHIP_UOP_{u}>(s.a[r]);"), False))
     for b in sorted(BOPS, key=lambda k: BOPS[k]):
         if b in INLINE_BOPS:
             continue
         mk = ("chk = mark(s.a[r], chk); " if b in LOSSY_LHS else "") + \
              ("chk = mark(s.b[r], chk); " if b in LOSSY_RHS else "")
         rs.append((f"b_{b.lower()}", rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], s.b[r]);"), False))
+        if b == "DIV":  # the compiled IEEE division, where manual_div sends rows out of its range
+            rs.append(("b_div_full", rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], s.b[r]);"), False))
     # constant-operand variants: the constant in SGPR s_k (no VGPR moves of a
     # literal); the constant itself was checked at compile time, not marked
     for b in sorted(BOPS, key=lambda k: BOPS[k]):
@@ -175,6 +179,8 @@ def routine_list():
         rs.append((f"b_{b.lower()}_rc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], imm);"), False))
         mk = "chk = mark(s.a[r], chk); " if b in LOSSY_RHS else ""
         rs.append((f"b_{b.lower()}_lc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
+        if b == "DIV":
+            rs.append(("b_div_lc_full", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
     return rs
 
 
@@ -285,6 +291,137 @@ def manual_div_rk(rg):
             "s_branch @DIVRC@"]
 
 
+def manual_exp():
+    """FAST exp for the 4 rows of A, bit for bit hipcc's Float32 exp
+    (SR_PRECISE_TRANSC=0: clamp to [-104, 89], n = rint(c*log2e),
+    f = fma(c, log2e, -n) + c*log2e_lo, ldexp(v_exp_f32(f), n)) on every tile
+    the FAST path keeps. Tree code runs this body only under its exp guard
+    (jit.cpp: a tile with some |x| > 87, or a non-finite x, which the input
+    mark catches, is redone with the PRECISE routines), so for a kept tile
+    |x| <= 87: the clamp is the identity, rint(t) is (t + 1.5*2^23) - 1.5*2^23
+    (round to nearest even, |t| < 2^22), and 2^f * 2^n is a normal number,
+    i.e. its bits are those of 2^f plus n << 23 — the low bits of
+    t + 1.5*2^23 shifted left by 23. Two rows per v_pk_*_f32 instruction.
+    The input is marked (chk) as in the compiled body: (x0, x1)*0 + (x2, x3)
+    is finite iff the four rows are."""
+    return ["s_mov_b32 s2, 0x3fb8aa3b",            # log2(e)
+            "s_mov_b32 s4, 0x4b400000",            # 1.5 * 2^23
+            "v_pk_mul_f32 v[0:1], v[32:33], s[2:3] op_sel_hi:[1,0]",   # t = x*log2e
+            "v_pk_mul_f32 v[2:3], v[34:35], s[2:3] op_sel_hi:[1,0]",
+            "s_mov_b32 s6, 0x32a57060",            # log2(e) - RN32(log2(e))
+            "v_pk_add_f32 v[4:5], v[0:1], s[4:5] op_sel_hi:[1,0]",     # s = t + 1.5*2^23: n in the low bits
+            "v_pk_add_f32 v[6:7], v[2:3], s[4:5] op_sel_hi:[1,0]",
+            "v_pk_add_f32 v[0:1], v[4:5], s[4:5] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]",   # n = rint(t)
+            "v_pk_add_f32 v[2:3], v[6:7], s[4:5] op_sel_hi:[1,0] neg_lo:[0,1] neg_hi:[0,1]",
+            "v_pk_fma_f32 v[8:9], v[32:33], s[2:3], v[0:1] op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]",
+            "v_pk_fma_f32 v[10:11], v[34:35], s[2:3], v[2:3] op_sel_hi:[1,0,1] neg_lo:[0,0,1] neg_hi:[0,0,1]",
+            "v_pk_fma_f32 v[8:9], s[6:7], v[32:33], v[8:9] op_sel_hi:[0,1,1]",
+            "v_pk_fma_f32 v[10:11], s[6:7], v[34:35], v[10:11] op_sel_hi:[0,1,1]",
+            "v_exp_f32_e32 v8, v8",
+            "v_exp_f32_e32 v9, v9",
+            "v_exp_f32_e32 v10, v10",
+            "v_exp_f32_e32 v11, v11",
+            "v_pk_fma_f32 v[12:13], v[32:33], 0, v[34:35] op_sel_hi:[1,0,1]",
+            "v_fmac_f32_e32 v40, 0, v12",
+            "v_fmac_f32_e32 v40, 0, v13",
+            "v_lshl_add_u32 v32, v4, 23, v8",
+            "v_lshl_add_u32 v33, v5, 23, v9",
+            "v_lshl_add_u32 v34, v6, 23, v10",
+            "v_lshl_add_u32 v35, v7, 23, v11"]
+
+
+def manual_div(rg):
+    """a / b (A / B) for the 4 rows: when every |a| and |b| lies in
+    [2^-45, 2^45], v_div_scale_f32 leaves both unchanged (no exponent
+    difference of 96, no denormal reciprocal or quotient), v_div_fmas_f32 is a
+    plain fma and v_div_fixup_f32 returns its input, so hipcc's IEEE sequence
+    reduces to rcp, e = 1 - b*r, r += e*r, q = a*r, e = a - b*q, q += e*r,
+    e = a - b*q, q += e*r — the same roundings, here two rows per v_pk_*_f32
+    instruction. b is marked as in the compiled body. Rows out of the range
+    (0, Inf, NaN, extreme exponents) send all four to the compiled routine
+    (b_div_full)."""
+    neg0 = " neg_lo:[1,0,0] neg_hi:[1,0,0]"
+    return ["v_max3_f32 v0, |v32|, |v33|, |v34|",
+            "v_min3_f32 v1, |v32|, |v33|, |v34|",
+            "v_max3_f32 v0, v0, |v35|, |v36|",
+            "v_min3_f32 v1, v1, |v35|, |v36|",
+            "v_max3_f32 v0, v0, |v37|, |v38|",
+            "v_min3_f32 v1, v1, |v37|, |v38|",
+            "s_mov_b32 s0, 0x56000000",           # 2^45
+            "v_max_f32_e64 v0, v0, |v39|",
+            "v_min_f32_e64 v1, v1, |v39|",
+            "s_mov_b32 s1, 0x29000000",           # 2^-45
+            "v_cmp_gt_f32_e64 s[2:3], s0, v0",
+            "v_cmp_lt_f32_e64 s[4:5], s1, v1",
+            "s_and_b64 s[2:3], s[2:3], s[4:5]",
+            "s_andn2_b64 s[2:3], exec, s[2:3]",
+            "s_cbranch_scc1 @DIVFULL@",
+            "v_rcp_f32_e32 v2, v36",
+            "v_rcp_f32_e32 v3, v37",
+            "v_rcp_f32_e32 v4, v38",
+            "v_rcp_f32_e32 v5, v39",
+            "v_pk_fma_f32 v[6:7], v[36:37], v[2:3], 1.0 op_sel_hi:[1,1,0]" + neg0,
+            "v_pk_fma_f32 v[8:9], v[38:39], v[4:5], 1.0 op_sel_hi:[1,1,0]" + neg0,
+            "v_pk_fma_f32 v[2:3], v[6:7], v[2:3], v[2:3]",
+            "v_pk_fma_f32 v[4:5], v[8:9], v[4:5], v[4:5]",
+            "v_pk_mul_f32 v[10:11], v[32:33], v[2:3]",
+            "v_pk_mul_f32 v[12:13], v[34:35], v[4:5]",
+            "v_pk_fma_f32 v[6:7], v[36:37], v[10:11], v[32:33]" + neg0,
+            "v_pk_fma_f32 v[8:9], v[38:39], v[12:13], v[34:35]" + neg0,
+            "v_pk_fma_f32 v[10:11], v[6:7], v[2:3], v[10:11]",
+            "v_pk_fma_f32 v[12:13], v[8:9], v[4:5], v[12:13]",
+            "v_pk_fma_f32 v[14:15], v[36:37], 0, v[38:39] op_sel_hi:[1,0,1]",
+            "v_pk_fma_f32 v[6:7], v[36:37], v[10:11], v[32:33]" + neg0,
+            "v_pk_fma_f32 v[8:9], v[38:39], v[12:13], v[34:35]" + neg0,
+            "v_fmac_f32_e32 v40, 0, v14",
+            "v_fmac_f32_e32 v40, 0, v15",
+            "v_pk_fma_f32 v[32:33], v[6:7], v[2:3], v[10:11]",
+            "v_pk_fma_f32 v[34:35], v[8:9], v[4:5], v[12:13]"]
+
+
+def manual_div_lc(rg):
+    """c / a for the constant c in s_k (the odd half of an SGPR pair, so the
+    packed instructions pick it with op_sel) and the 4 rows of A: manual_div's
+    sequence with c as the numerator, under the same range condition on c and
+    every |a|; otherwise the compiled routine (b_div_lc_full)."""
+    k = rg.S["k"]
+    assert k % 2 == 1
+    cp = f"s[{k - 1}:{k}]"
+    neg0 = " neg_lo:[1,0,0] neg_hi:[1,0,0]"
+    return [f"v_max3_f32 v0, |v32|, |v33|, |s{k}|",
+            f"v_min3_f32 v1, |v32|, |v33|, |s{k}|",
+            "v_max3_f32 v0, v0, |v34|, |v35|",
+            "v_min3_f32 v1, v1, |v34|, |v35|",
+            "s_mov_b32 s0, 0x56000000",           # 2^45
+            "s_mov_b32 s1, 0x29000000",           # 2^-45
+            "v_cmp_gt_f32_e64 s[2:3], s0, v0",
+            "v_cmp_lt_f32_e64 s[4:5], s1, v1",
+            "s_and_b64 s[2:3], s[2:3], s[4:5]",
+            "s_andn2_b64 s[2:3], exec, s[2:3]",
+            "s_cbranch_scc1 @LCFULL@",
+            "v_rcp_f32_e32 v2, v32",
+            "v_rcp_f32_e32 v3, v33",
+            "v_rcp_f32_e32 v4, v34",
+            "v_rcp_f32_e32 v5, v35",
+            "v_pk_fma_f32 v[6:7], v[32:33], v[2:3], 1.0 op_sel_hi:[1,1,0]" + neg0,
+            "v_pk_fma_f32 v[8:9], v[34:35], v[4:5], 1.0 op_sel_hi:[1,1,0]" + neg0,
+            "v_pk_fma_f32 v[2:3], v[6:7], v[2:3], v[2:3]",
+            "v_pk_fma_f32 v[4:5], v[8:9], v[4:5], v[4:5]",
+            f"v_pk_mul_f32 v[10:11], {cp}, v[2:3] op_sel:[1,0]",
+            f"v_pk_mul_f32 v[12:13], {cp}, v[4:5] op_sel:[1,0]",
+            f"v_pk_fma_f32 v[6:7], v[32:33], v[10:11], {cp} op_sel:[0,0,1]" + neg0,
+            f"v_pk_fma_f32 v[8:9], v[34:35], v[12:13], {cp} op_sel:[0,0,1]" + neg0,
+            "v_pk_fma_f32 v[10:11], v[6:7], v[2:3], v[10:11]",
+            "v_pk_fma_f32 v[12:13], v[8:9], v[4:5], v[12:13]",
+            "v_pk_fma_f32 v[14:15], v[32:33], 0, v[34:35] op_sel_hi:[1,0,1]",
+            f"v_pk_fma_f32 v[6:7], v[32:33], v[10:11], {cp} op_sel:[0,0,1]" + neg0,
+            f"v_pk_fma_f32 v[8:9], v[34:35], v[12:13], {cp} op_sel:[0,0,1]" + neg0,
+            "v_fmac_f32_e32 v40, 0, v14",
+            "v_fmac_f32_e32 v40, 0, v15",
+            "v_pk_fma_f32 v[32:33], v[6:7], v[2:3], v[10:11]",
+            "v_pk_fma_f32 v[34:35], v[8:9], v[4:5], v[12:13]"]
+
+
 def compile_bodies(hipcc, rg, routines, extra):
     src = snippet_source(rg, [(n, b) for n, b, _ in routines])
     with tempfile.TemporaryDirectory() as td:
@@ -329,6 +466,15 @@ def build(hipcc, outdir, R):
     if "b_div_rc" in names:  # hand-written, the same in both regions (IEEE exact)
         fast["b_div_rk"] = prec["b_div_rk"] = manual_div_rk(rg)
         names.insert(names.index("b_div_rc") + 1, "b_div_rk")
+    if os.environ.get("SR_JIT_MANUAL_DIV", "1") != "0" and "b_div_full" in names:
+        fast["b_div"] = prec["b_div"] = manual_div(rg)  # exact: the same in both regions
+        manual.add("b_div")
+        if "b_div_lc_full" in names:
+            fast["b_div_lc"] = prec["b_div_lc"] = manual_div_lc(rg)
+            manual.add("b_div_lc")
+    if os.environ.get("SR_JIT_MANUAL_EXP", "1") != "0" and "u_exp" in names:
+        fast["u_exp"] = manual_exp()
+        manual.add("u_exp")
     if os.environ.get("SR_JIT_MANUAL_TRIG", "1") != "0":
         for k in ("sin", "cos"):
             if f"u_{k}_full" in names:
@@ -362,11 +508,14 @@ def build(hipcc, outdir, R):
     pb = {n: with_ret(prec[n], n, "p") for n in names}
     def sized(bodies):
         return {n: [l.replace("@FULL@", f".Lsr_start_{n}_full_%=").replace("@DIVRC@", ".Lsr_start_b_div_rc_%=")
+                    .replace("@DIVFULL@", ".Lsr_start_b_div_full_%=").replace("@LCFULL@", ".Lsr_start_b_div_lc_full_%=")
                     for l in b] for n, b in bodies.items()}
     fs, ps = label_sizes(sized(fb), names), label_sizes(sized(pb), names)
     fb = {n: [l.replace("@FULL@", f".Lsrent_fast_{n}_full").replace("@DIVRC@", ".Lsrent_fast_b_div_rc")
+              .replace("@DIVFULL@", ".Lsrent_fast_b_div_full").replace("@LCFULL@", ".Lsrent_fast_b_div_lc_full")
               for l in b] for n, b in fb.items()}
-    pb = {n: [l.replace("@DIVRC@", ".Lsrent_prec_b_div_rc") for l in b] for n, b in pb.items()}
+    pb = {n: [l.replace("@DIVRC@", ".Lsrent_prec_b_div_rc").replace("@DIVFULL@", ".Lsrent_prec_b_div_full")
+              .replace("@LCFULL@", ".Lsrent_prec_b_div_lc_full") for l in b] for n, b in pb.items()}
     slot = {n: (max(fs[n], ps[n]) + 63) // 64 * 64 for n in names}
     text = ["s_endpgm"]
     for region, bodies, sizes in (("fast", fb, fs), ("prec", pb, ps)):

@@ -170,6 +170,9 @@ struct Gen {
   // SRHIP_JIT_TRIG_FULL=1 (tests): sin / cos through the complete compiled
   // routines instead of the hand-scheduled FAST bodies
   bool trig_full = false;
+  // SRHIP_JIT_MANUAL=0 (tests): sin, cos, exp and / through the compiled
+  // routines instead of the hand-scheduled packed bodies (gen_jit.py manual_*)
+  bool manual_off = false;
   static int div_rk() {
     static const int r = [] {
       for (int k = 0; k < kNumRoutines; ++k)
@@ -185,13 +188,22 @@ struct Gen {
     return rid;
   }
   bool inline_ok = false;  // copy mode-independent small routines into the tree code
+  // + - * (and square / cube, residuals, the root check) two rows per
+  // instruction on v_pk_*_f32; block moves on v_pk_mov_b32
+  bool packed = true, pkmov = true;
   Gen(Asm& a, const Tmpl& t, uint64_t va, bool f) : as(a), T(t), base_va(va), fast_opt(f) {
     const char* e = std::getenv("SRHIP_JIT_INLINE");  // measured no faster: off by default
     inline_ok = e && e[0] == '1';
     const char* xd = std::getenv("SRHIP_JIT_XDIRECT");
     xdirect = !(xd && xd[0] == '0');  // measured 1 % faster on config #2
+    const char* pk = std::getenv("SRHIP_JIT_PACKED");
+    packed = !(pk && pk[0] == '0');
+    const char* pm = std::getenv("SRHIP_JIT_PKMOV");
+    pkmov = !(pm && pm[0] == '0');
     const char* tf = std::getenv("SRHIP_JIT_TRIG_FULL");
     trig_full = tf && tf[0] == '1';
+    const char* mo = std::getenv("SRHIP_JIT_MANUAL");
+    manual_off = mo && mo[0] == '0';
   }
 
   uint64_t cur_va() const { return base_va + as.bytes(); }
@@ -206,10 +218,14 @@ struct Gen {
         o.rid = o.un ? kUopRoutine[o.op] : kBopRoutine[o.op];
         if (o.rid < 0) { why = "operator without routine"; return false; }
         if (trig_full && o.un && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS)) o.rid = full_routine(o.rid);
+        if (manual_off && ((o.un && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS || o.op == SRHIP_UOP_EXP)) ||
+                           (!o.un && o.op == SRHIP_BOP_DIV)))
+          o.rid = full_routine(o.rid);
         has_call = true;
         // a constant operand rides in s_k: the routine variant takes the other one in A
         if (!o.un && o.b.k == O_C && o.a.k != O_C && kBopRoutineRC[o.op] >= 0) o.krid = kBopRoutineRC[o.op];
         if (!o.un && o.a.k == O_C && o.b.k != O_C && kBopRoutineLC[o.op] >= 0) o.krid = kBopRoutineLC[o.op];
+        if (manual_off && o.krid >= 0 && !o.un && o.op == SRHIP_BOP_DIV) o.krid = full_routine(o.krid);
         if (kRoutineTrig[o.rid]) has_trig = true;
       }
       for (int s = 0; s < 2; ++s) {
@@ -322,10 +338,32 @@ struct Gen {
     return -1;
   }
   void mov_block(int dst, const Src (&src)[R]) {
+    bool blk = src[0].enc >= 256;
+    for (int e = 1; e < R; ++e) blk = blk && src[e].enc == src[0].enc + e;
+    if (blk) { mov_block_reg(dst, src[0].enc - 256); return; }
     for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", dst + e, src[e]);
   }
   void mov_block_reg(int dst, int srcreg) {
+    if (pkmov) {
+      for (int e = 0; e < R; e += 2)
+        as.vop3p(VOP3P_MOV_B32, "v_pk_mov_b32", dst + e, V(srcreg + e), V(srcreg + e), nullptr, 2, 7, 0, 0);
+      return;
+    }
     for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", dst + e, V(srcreg + e));
+  }
+  // a source of a packed instruction for rows e, e+1: a VGPR pair, an inline
+  // constant, or the constant in s[20:21] (pk_const puts it there first)
+  static Src pks(const Src& s) { return s.lit ? S(S_PKC) : s; }
+  void pk_const(const Src& s) {
+    if (s.lit) as.sop1(SOP1_MOV, "s_mov_b32", S_PKC, K(s.val), "s" + std::to_string(S_PKC));
+  }
+  // block d = a (op) b, two rows per instruction; a constant feeds both halves
+  void pk_block(int opc, const char* nm, int d, const Src (&a)[R], const Src (&b)[R], bool negb) {
+    pk_const(a[0]);
+    pk_const(b[0]);
+    const int hi = 4 | (a[0].enc >= 256 ? 1 : 0) | (b[0].enc >= 256 ? 2 : 0);
+    for (int e = 0; e < R; e += 2)
+      as.vop3p(opc, nm, d + e, pks(a[e]), pks(b[e]), nullptr, 0, hi, negb ? 2 : 0, negb ? 2 : 0);
   }
   // a call operand into block `dst` (A or B): features not preloaded (or all
   // of them with xdirect) are read from the LDS tile, other operands moved
@@ -548,7 +586,25 @@ struct Gen {
     if (dst == L_NONE) dst = freed >= 0 ? freed : free_block();
     if (dst == L_NONE) { why = "register pool exhausted"; return false; }
     const int d = reg_of_loc(dst);
-    for (int e = 0; e < R; ++e) {
+    const bool ca = o.a.k == O_C, cb = !o.un && o.b.k == O_C;
+    const bool pk_bin = packed && !o.un && !(ca && cb) &&
+                        (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB || o.op == SRHIP_BOP_MUL);
+    const bool pk_un = packed && o.un && !ca && (o.op == SRHIP_UOP_SQUARE || o.op == SRHIP_UOP_CUBE);
+    if (pk_bin) {
+      if (o.op == SRHIP_BOP_MUL) pk_block(VOP3P_MUL_F32, "v_pk_mul_f32", d, a, b, false);
+      else pk_block(VOP3P_ADD_F32, "v_pk_add_f32", d, a, b, o.op == SRHIP_BOP_SUB);
+    } else if (pk_un) {
+      if (o.op == SRHIP_UOP_SQUARE) {
+        pk_block(VOP3P_MUL_F32, "v_pk_mul_f32", d, a, a, false);
+      } else {  // CUBE = (x*x)*x
+        const int tt = (d == a[0].enc - 256) ? VGT : d;
+        Src t2[R];
+        for (int e = 0; e < R; ++e) t2[e] = V(tt + e);
+        pk_block(VOP3P_MUL_F32, "v_pk_mul_f32", tt, a, a, false);
+        pk_block(VOP3P_MUL_F32, "v_pk_mul_f32", d, t2, a, false);
+      }
+    }
+    for (int e = 0; e < R && !pk_bin && !pk_un; ++e) {
       if (o.un) {
         switch (o.op) {
           case SRHIP_UOP_NEG: as.vop2(VOP2_XOR_B32, "v_xor_b32_e32", d + e, K(0x80000000u), a[e].enc - 256); break;
@@ -561,7 +617,6 @@ struct Gen {
           }
         }
       } else {
-        const bool ca = o.a.k == O_C, cb = o.b.k == O_C;
         switch (o.op) {
           case SRHIP_BOP_ADD:
           case SRHIP_BOP_MUL: {
@@ -655,9 +710,19 @@ struct Gen {
       for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGT + e, K(root.c));
       rreg = VGT;
     }
-    for (int e = 0; e < R; ++e) {
-      const Src r = V(rreg + e), z = K(0), c = V(VCHK);
-      as.vop3(VOP3_FMA_F32, "v_fma_f32", VCHK, r, z, &c, 0, 0);
+    if (packed && rreg != VGT) {
+      // (r0, r1)·0 + (r2, r3) is finite iff the four rows are: one packed fma, two into chk
+      const Src r01 = V(rreg), r23 = V(rreg + 2), z = K(0);
+      as.vop3p(VOP3P_FMA_F32, "v_pk_fma_f32", VGT, r01, z, &r23, 0, 5, 0, 0);
+      for (int e = 0; e < 2; ++e) {
+        const Src r = V(VGT + e), c = V(VCHK);
+        as.vop3(VOP3_FMA_F32, "v_fma_f32", VCHK, r, z, &c, 0, 0);
+      }
+    } else {
+      for (int e = 0; e < R; ++e) {
+        const Src r = V(rreg + e), z = K(0), c = V(VCHK);
+        as.vop3(VOP3_FMA_F32, "v_fma_f32", VCHK, r, z, &c, 0, 0);
+      }
     }
     wait_all();
     // ---- FAST-mode verdict: a failure or a guard redoes the tile precisely
@@ -682,7 +747,13 @@ struct Gen {
       as.bind(L_skip);
     }
     // ---- L2 loss of the tile: the residuals here, their squares in emit_tail
-    for (int e = 0; e < R; ++e) as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", VY + e, V(rreg + e), VY + e);
+    if (packed) {
+      Src r[R], y[R];
+      for (int e = 0; e < R; ++e) { r[e] = V(rreg + e); y[e] = V(VY + e); }
+      pk_block(VOP3P_ADD_F32, "v_pk_add_f32", VY, r, y, true);
+    } else {
+      for (int e = 0; e < R; ++e) as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", VY + e, V(rreg + e), VY + e);
+    }
     return true;
   }
 
@@ -713,9 +784,13 @@ struct Gen {
       // weighted: w * r^2 per row (eval_kernel.h tile_loss), masked, then summed
       as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VGT, S(S_WOFF), VLANE);
       as.ds_read_b128(VGT, VGT, 0);
-      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VY + e), VY + e);
+      Src y[R], w[R];
+      for (int e = 0; e < R; ++e) { y[e] = V(VY + e); w[e] = V(VGT + e); }
+      if (packed) pk_block(VOP3P_MUL_F32, "v_pk_mul_f32", VY, y, y, false);
+      else for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VY + e), VY + e);
       as.waitcnt_lgkm(0);
-      for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VGT + e), VY + e);
+      if (packed) pk_block(VOP3P_MUL_F32, "v_pk_mul_f32", VY, w, y, false);
+      else for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VGT + e), VY + e);
       emit_mask(VY);
       as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 2);
       as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY + 1, V(VY + 1), VY + 3);

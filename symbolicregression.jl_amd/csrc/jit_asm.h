@@ -38,6 +38,9 @@ constexpr int S_FASTOK = SR_JIT_S_FASTOK, S_EPS = SR_JIT_S_EPS;
 constexpr int S_K = SR_JIT_S_K, S_PE = SR_JIT_S_PE, S_MODE = SR_JIT_S_MODE, S_X0 = SR_JIT_S_X0;
 constexpr int S_BASE = SR_JIT_S_X2;
 constexpr int S_RECIP = SR_JIT_S_X1;  // RN(1/c) of a constant divisor (routine b_div_rk)  // s[86:87]: base of the routine region in use (FAST or PRECISE)
+// a routine temporary, free between calls: the constant operand of a packed
+// tree-code instruction (low half of s[20:21]; VOP3P takes no literal)
+constexpr int S_PKC = 20;
 constexpr int TILE = 64 * R;
 constexpr int kNumRoutines = SR_JIT_NUM_ROUTINES;
 const int kUopRoutine[SRHIP_NUM_UOPS] = SR_JIT_UOP_ROUTINE;
@@ -288,6 +291,45 @@ struct Asm {
     };
     t(std::string(nm) + " v" + std::to_string(vdst) + ", " + f(s0, 0) + ", " + f(s1, 1) + (s2 ? ", " + f(*s2, 2) : ""));
   }
+  // VOP3P (two f32 per lane in a register pair; no literals on gfx9): bit i of
+  // opsel / opsel_hi / neg_lo / neg_hi applies to source i. A constant source
+  // (an inline constant, or an SGPR pair whose low half holds it) feeds both
+  // halves with opsel_hi bit 0.
+  void vop3p(int op, const char* nm, int vdst, const Src& s0, const Src& s1, const Src* s2, int opsel, int opsel_hi,
+             int neg_lo, int neg_hi) {
+    if (s0.lit || s1.lit || (s2 && s2->lit)) throw Error(SRHIP_ERR_INVALID, "jit: literal in a VOP3P operand");
+    put(0xd3800000u | ((uint32_t)op << 16) | ((uint32_t)((opsel_hi >> 2) & 1) << 14) | ((uint32_t)(opsel & 7) << 11) |
+        ((uint32_t)(neg_hi & 7) << 8) | (uint32_t)vdst);
+    put(((uint32_t)(neg_lo & 7) << 29) | ((uint32_t)(opsel_hi & 3) << 27) | ((uint32_t)(s2 ? s2->enc : 0) << 18) |
+        ((uint32_t)s1.enc << 9) | (uint32_t)s0.enc);
+    if (!want_text) return;
+    const int n = s2 ? 3 : 2;
+    auto pair = [](const Src& s) -> std::string {
+      if (s.enc >= 256) return "v[" + std::to_string(s.enc - 256) + ":" + std::to_string(s.enc - 255) + "]";
+      if (s.enc < 102) return "s[" + std::to_string(s.enc) + ":" + std::to_string(s.enc + 1) + "]";
+      switch (s.val) {  // inline constants by value (llvm-mc reads hex as a literal here)
+        case 0x3f000000u: return "0.5";
+        case 0xbf000000u: return "-0.5";
+        case 0x3f800000u: return "1.0";
+        case 0xbf800000u: return "-1.0";
+        case 0x40000000u: return "2.0";
+        case 0xc0000000u: return "-2.0";
+        case 0x40800000u: return "4.0";
+        case 0xc0800000u: return "-4.0";
+        default: return std::to_string((int32_t)s.val);
+      }
+    };
+    auto arr = [&](const char* key, int bits, int dflt) -> std::string {
+      if (bits == dflt) return "";
+      std::string r = std::string(" ") + key + ":[";
+      for (int i = 0; i < n; ++i) r += std::string(i ? "," : "") + ((bits >> i) & 1 ? "1" : "0");
+      return r + "]";
+    };
+    const int full = (1 << n) - 1;
+    t(std::string(nm) + " v[" + std::to_string(vdst) + ":" + std::to_string(vdst + 1) + "], " + pair(s0) + ", " + pair(s1) +
+      (s2 ? ", " + pair(*s2) : "") + arr("op_sel", opsel & full, 0) + arr("op_sel_hi", opsel_hi & full, full) +
+      arr("neg_lo", neg_lo & full, 0) + arr("neg_hi", neg_hi & full, 0));
+  }
   void ds_read_b128(int vdst, int vaddr, int offset) {
     put(0xd8000000u | (0xffu << 17) | (uint32_t)(offset & 0xffff));
     put(((uint32_t)vdst << 24) | (uint32_t)vaddr);
@@ -318,6 +360,7 @@ enum : int {
   VOP1_MOV = 0x01,
   VOP3_ADD_F32 = 0x101, VOP3_MIN_F32 = 0x10a, VOP3_MAX_F32 = 0x10b, VOP3_FMA_F32 = 0x1cb,
   VOP3_MIN3_F32 = 0x1d0, VOP3_MAX3_F32 = 0x1d3,
+  VOP3P_FMA_F32 = 0x30, VOP3P_MUL_F32 = 0x31, VOP3P_ADD_F32 = 0x32, VOP3P_MOV_B32 = 0x33,
   VOPC_LT_F32 = 0x41, VOPC_LE_F32 = 0x43, VOPC_GT_F32 = 0x44, VOPC_U_F32 = 0x48, VOPC_GT_I32 = 0xc4,
   SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
   SOP2_ADD_U32 = 0x00, SOP2_SUB_U32 = 0x01, SOP2_SUB_I32 = 0x03, SOP2_SUBB_U32 = 0x05, SOP2_ADDC_U32 = 0x04, SOP2_CSELECT = 0x0a,

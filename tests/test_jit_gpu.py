@@ -221,3 +221,91 @@ def test_constant_divisor_is_ieee_exact(gpu_ctx, fast):
         assert info["ntrees"] == len(trees) and ok.all()
         bad = np.flatnonzero(s != 0)
         assert bad.size == 0, (c[bad[:5]], s[bad[:5]])
+
+
+def test_packed_and_hand_scheduled_code_equals_scalar_compiled(gpu_ctx):
+    """Packed tree code (+ - * square cube, residuals, block moves on
+    v_pk_*_f32) and the hand-scheduled packed exp / division bodies
+    (gen_jit.py manual_exp, manual_div) compute bit for bit what the scalar
+    tree code with hipcc's compiled routines computes (SRHIP_JIT_PACKED=0,
+    SRHIP_JIT_PKMOV=0, SRHIP_JIT_MANUAL=0): same did_succeed, same sums."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"],
+                      unary_operators=["sin", "cos", "exp", "square", "cube", "neg"])
+    trees = srhip.random_population(1500, o, 5, np.float32, seed=41)
+    rng = np.random.default_rng(42)
+    X = (rng.standard_normal((5, 60_000)) * rng.choice([1e-3, 1.0, 30.0, 1e4], (5, 60_000))).astype(np.float32)
+    X[:, :256] = rng.uniform(0.5, 2.0, (5, 256)).astype(np.float32)  # one tile with every division in range
+    y = (np.float32(2) * np.cos(X[3]) + X[0] * X[0] - np.float32(2)).astype(np.float32)
+    for fast in ("1", "0"):
+        s_m, w_m, ok_m, info_m, _ = run(trees, o, X, y, jit="1", fast=fast)
+        with env(SRHIP_JIT_MANUAL="0", SRHIP_JIT_PACKED="0", SRHIP_JIT_PKMOV="0"):
+            s_f, w_f, ok_f, info_f, _ = run(trees, o, X, y, jit="1", fast=fast)
+        assert info_m["ntrees"] == info_f["ntrees"] > 1000
+        assert np.array_equal(ok_m, ok_f)
+        assert np.array_equal(s_m[ok_m], s_f[ok_f])
+
+
+@pytest.mark.parametrize("fast", ["0", "1"])
+def test_variable_divisor_is_ieee_exact(gpu_ctx, fast):
+    """x0 / x1 through the packed division (every |a|, |b| of a tile in
+    [2^-45, 2^45]) or the compiled IEEE sequence (any row outside: zeros,
+    extreme exponents, the range edges): every row equals numpy's Float32
+    quotient bit for bit — the tree (x0 / x1) - x2, x2 = x0 / x1
+    precomputed, has loss exactly 0."""
+    rng = np.random.default_rng(51)
+    T = 256  # rows of a tile (one wave, 4 rows per lane)
+
+    def mag(lo, hi, n):
+        v = rng.uniform(1, 2, n) * np.exp2(rng.integers(lo, hi + 1, n).astype(np.float64))
+        return (v * rng.choice([-1, 1], n)).astype(np.float32)
+
+    blocks = []
+    for k in range(400):
+        kind = k % 4
+        if kind == 0:    # in range: the packed path
+            a, b = mag(-44, 44, T), mag(-44, 44, T)
+        elif kind == 1:  # the range edges
+            a, b = mag(-46, 45, T), mag(-46, 45, T)
+        elif kind == 2:  # large exponents: the compiled path
+            a, b = mag(-60, 60, T), mag(-60, 60, T)
+        else:            # in range but one zero numerator in the tile
+            a, b = mag(-20, 20, T), mag(-20, 20, T)
+            a[rng.integers(0, T)] = 0
+        blocks.append((a, b))
+    a = np.concatenate([p[0] for p in blocks])
+    b = np.concatenate([p[1] for p in blocks])
+    q = a / b
+    assert np.isfinite(q).all() and a.size == 400 * T  # tiles stay aligned with the blocks
+    X = np.stack([a, b, q]).astype(np.float32)
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    tree = o.make_binary("-", o.make_binary("/", srhip.Node(feature=1), srhip.Node(feature=2)), srhip.Node(feature=3))
+    y = np.zeros(X.shape[1], np.float32)
+    s, w, ok, info, _ = run([tree] * 8, o, X, y, jit="1", fast=fast)
+    assert info["ntrees"] == 8 and ok.all()
+    assert np.all(s == 0), s
+
+
+@pytest.mark.parametrize("fast", ["0", "1"])
+def test_constant_numerator_is_ieee_exact(gpu_ctx, fast):
+    """c / x0 (gen_jit.py manual_div_lc, compiled fallback outside
+    [2^-45, 2^45]): bit for bit numpy's Float32 quotient, loss exactly 0."""
+    rng = np.random.default_rng(61)
+    T, nb = 256, 200
+    b = []
+    for k in range(nb):
+        lo, hi = [(-44, 44), (-46, 45), (-60, 60), (-20, 20)][k % 4]
+        v = rng.uniform(1, 2, T) * np.exp2(rng.integers(lo, hi + 1, T).astype(np.float64))
+        b.append((v * rng.choice([-1, 1], T)).astype(np.float32))
+    b = np.concatenate(b)
+    c = np.float32([3.0, -0.1, 7.5e12, 2.0 ** 45, 2.0 ** -45, 3e-14, float.fromhex("0x1.fffffep44"), 1e-30])
+    X = np.empty((1 + len(c), b.size), np.float32)
+    X[0] = b
+    X[1:] = c[:, None] / b[None, :]
+    assert np.isfinite(X).all()
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = [o.make_binary("-", o.make_binary("/", srhip.Node(val=cj), srhip.Node(feature=1)),
+                           srhip.Node(feature=j + 2)) for j, cj in enumerate(c)]
+    y = np.zeros(b.size, np.float32)
+    s, w, ok, info, _ = run(trees, o, X, y, jit="1", fast=fast)
+    assert info["ntrees"] == len(trees) and ok.all()
+    assert np.all(s == 0), (c[s != 0], s[s != 0])
