@@ -732,21 +732,22 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   c->sums.ensure(std::max<size_t>(p->ntrees, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(p->ntrees, 1));
   const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
-  if (mode == MODE_LOSS) {
-    c->fail.ensure(std::max<size_t>(nslots, 1) * sizeof(uint32_t));
-    HIP_CHECK(hipMemsetAsync(c->fail.p, 0, std::max<size_t>(nslots, 1) * sizeof(uint32_t), s));
-  }
   // slot ranges: [0, nj) tree code, [nj, nlist_a) shallow interpreter, then deep
   const bool use_jit = std::is_same<T, float>::value && p->jit && p->nlist_j > 0 && mode == MODE_LOSS &&
                        loss == SRHIP_LOSS_L2;
   const int nj = use_jit ? p->nlist_j : 0;
+  // failure flags (and the tree code's bail flags): cleared in one launch
+  if (mode == MODE_LOSS) {
+    c->fail.ensure(std::max<size_t>(nslots, 1) * sizeof(uint32_t));
+    HIP_CHECK(launch_zero_words(static_cast<uint32_t*>(c->fail.p), (int64_t)std::max<size_t>(nslots, 1),
+                                use_jit ? jit::bail_flags(p->jit) : nullptr, use_jit ? jit::flag_words(p->jit) : 0, s));
+  }
   // launches: the tree-code parts (pass -1, one per code object), the shallow
   // interpreter (0), the deep interpreter (1)
   struct Launch { int pass, s0, nlist, part; };
   std::vector<Launch> launches;
   if (nj > 0) {
     if constexpr (std::is_same<T, float>::value) {
-      HIP_CHECK(jit::reset_flags(p->jit, s));
       for (int k = 0; k < jit::nparts(p->jit); ++k) {
         int s0, nsl;
         jit::part(p->jit, k, &s0, &nsl);

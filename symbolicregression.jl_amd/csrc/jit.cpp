@@ -1063,6 +1063,8 @@ struct JitArgs {
   int part_lds;
 };
 
+int64_t flag_words(Module* m) { return (int64_t)m->nslots + 2; }
+
 hipError_t reset_flags(Module* m, hipStream_t stream) {
   return hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t), stream);
 }

@@ -55,6 +55,8 @@ int nslots(const Module* m);
 int nparts(const Module* m);
 void part(const Module* m, int k, int* slot0, int* nslots);
 hipError_t reset_flags(Module* m, hipStream_t stream);
+// words at bail_flags(m) that reset_flags clears (per-slot flags + 2 counters)
+int64_t flag_words(Module* m);
 
 // Launch part k's driver over its slots (EvalArgs as for eval_kernel: list /
 // list_off / fail / partial of the part's slots).

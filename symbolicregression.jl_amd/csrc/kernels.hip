@@ -13,18 +13,22 @@
 namespace srhip {
 namespace {
 
+// One workgroup per 64 slots; its 16 waves split the row groups (a fixed
+// order: the sums do not depend on timing), then wave 0 adds the 16 parts.
+constexpr int kFinWaves = 16;
 template <typename T>
-__global__ void __launch_bounds__(256) finalize_kernel(EvalArgs<T> a, double* __restrict__ out_sum,
-                                                       uint8_t* __restrict__ out_ok) {
-  __shared__ double ss[4][64];
-  __shared__ double sc[4][64];
+__global__ void __launch_bounds__(64 * kFinWaves) finalize_kernel(EvalArgs<T> a, double* __restrict__ out_sum,
+                                                                  uint8_t* __restrict__ out_ok) {
+  __shared__ double ss[kFinWaves][64];
+  __shared__ double sc[kFinWaves][64];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
   const int npos = a.ntg * a.tpb;
   const int pos = blockIdx.x * 64 + lane;
   double s = 0.0, c = 0.0;
   if (pos < npos) {
-    for (int rg = w; rg < a.nrg; rg += 4) {
+#pragma unroll 4
+    for (int rg = w; rg < a.nrg; rg += kFinWaves) {
       const Part<T> q = a.partial[(size_t)rg * npos + pos];
       s += (double)q.sum;
       c += (double)q.chk;
@@ -34,8 +38,13 @@ __global__ void __launch_bounds__(256) finalize_kernel(EvalArgs<T> a, double* __
   sc[w][lane] = c;
   __syncthreads();
   if (w == 0 && pos < npos) {
-    s = (ss[0][lane] + ss[1][lane]) + (ss[2][lane] + ss[3][lane]);
-    c = (sc[0][lane] + sc[1][lane]) + (sc[2][lane] + sc[3][lane]);
+    for (int k = kFinWaves / 2; k >= 1; k /= 2)
+      for (int j = 0; j < k; ++j) {
+        ss[j][lane] += ss[j + k][lane];
+        sc[j][lane] += sc[j + k][lane];
+      }
+    s = ss[0][lane];
+    c = sc[0][lane];
     const int g = pos / a.tpb;
     const int i = pos - g * a.tpb;
     const int sidx = a.contig ? g * a.tpb + i : i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
@@ -45,6 +54,17 @@ __global__ void __launch_bounds__(256) finalize_kernel(EvalArgs<T> a, double* __
       out_sum[t] = ok ? s : __builtin_nan("");
       out_ok[t] = ok ? 1 : 0;
     }
+  }
+}
+
+// zero two word ranges in one launch (the per-slot failure flags and the tree
+// code's bail flags and counters, before every evaluation)
+__global__ void __launch_bounds__(256) zero_words_kernel(uint32_t* __restrict__ a, int64_t na,
+                                                        uint32_t* __restrict__ b, int64_t nb) {
+  for (int64_t i = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; i < na + nb;
+       i += (int64_t)gridDim.x * blockDim.x) {
+    if (i < na) a[i] = 0u;
+    else b[i - na] = 0u;
   }
 }
 
@@ -221,7 +241,14 @@ hipError_t launch_finalize(const EvalArgs<T>& a, double* out_sum, uint8_t* out_o
                            hipStream_t stream) {
   const int npos = a.ntg * a.tpb;
   const unsigned grid = (unsigned)((npos + 63) / 64);
-  hipLaunchKernelGGL((finalize_kernel<T>), dim3(grid), dim3(256), 0, stream, a, out_sum, out_ok);
+  hipLaunchKernelGGL((finalize_kernel<T>), dim3(grid), dim3(64 * kFinWaves), 0, stream, a, out_sum, out_ok);
+  return hipGetLastError();
+}
+
+hipError_t launch_zero_words(uint32_t* a, int64_t na, uint32_t* b, int64_t nb, hipStream_t stream) {
+  if (na + nb <= 0) return hipSuccess;
+  const unsigned grid = (unsigned)std::min<int64_t>(1024, (na + nb + 255) / 256);
+  hipLaunchKernelGGL(zero_words_kernel, dim3(grid), dim3(256), 0, stream, a, na, b, nb);
   return hipGetLastError();
 }
 
