@@ -236,21 +236,19 @@ def manual_trig(kind):
           "s_mov_b32 s18, 0xbe2aaaa6",
           "v_pk_fma_f32 v[20:21], v[20:21], v[16:17], s[16:17] op_sel_hi:[1,1,0]",
           "v_pk_fma_f32 v[22:23], v[22:23], v[18:19], s[16:17] op_sel_hi:[1,1,0]",
-          "v_lshlrev_b32_e32 v24, 31, v4",                                     # (-1)^n
           "v_pk_fma_f32 v[20:21], v[20:21], v[16:17], s[18:19] op_sel_hi:[1,1,0]",
           "v_pk_fma_f32 v[22:23], v[22:23], v[18:19], s[18:19] op_sel_hi:[1,1,0]",
-          "v_lshlrev_b32_e32 v25, 31, v5",
           "v_pk_mul_f32 v[20:21], v[16:17], v[20:21]",
-          "v_pk_mul_f32 v[22:23], v[18:19], v[22:23]",
-          "v_lshlrev_b32_e32 v26, 31, v6"]
+          "v_pk_mul_f32 v[22:23], v[18:19], v[22:23]"]
     neg = " neg_lo:[0,1,1] neg_hi:[0,1,1]" if cos else ""
+    # the sign (-1)^n: n's parity (low bit of t + 1.5*2^23) shifted to bit 31
+    # and added, which flips the sign bit exactly as a xor would
     L += [f"v_pk_fma_f32 v[20:21], v[20:21], v[12:13], v[12:13]{neg}",
           f"v_pk_fma_f32 v[22:23], v[22:23], v[14:15], v[14:15]{neg}",
-          "v_lshlrev_b32_e32 v27, 31, v7",
-          "v_xor_b32_e32 v32, v24, v20",
-          "v_xor_b32_e32 v33, v25, v21",
-          "v_xor_b32_e32 v34, v26, v22",
-          "v_xor_b32_e32 v35, v27, v23"]
+          "v_lshl_add_u32 v32, v4, 31, v20",
+          "v_lshl_add_u32 v33, v5, 31, v21",
+          "v_lshl_add_u32 v34, v6, 31, v22",
+          "v_lshl_add_u32 v35, v7, 31, v23"]
     return L
 
 
