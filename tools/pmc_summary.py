@@ -37,11 +37,18 @@ if "GRBM_GUI_ACTIVE" in avg and "SQ_INSTS_VALU" in avg:
     cyc = avg["GRBM_GUI_ACTIVE"] / 8  # summed over the 8 XCDs
     res["gpu_cycles"] = cyc
     res["valu_busy_2cyc"] = avg["SQ_INSTS_VALU"] * 2 / (cyc * 1024)
+    if "SQ_ACTIVE_INST_VALU" in avg:
+        # quad-cycles the SIMDs' VALUs work (≈ 1.05 per wave64 instruction,
+        # packed or not): the share of the 1024 SIMDs' cycles the VALU is busy
+        res["valu_busy_4cyc"] = avg["SQ_ACTIVE_INST_VALU"] * 4 / (cyc * 1024)
+        res["quad_cycles_per_valu_inst"] = avg["SQ_ACTIVE_INST_VALU"] / avg["SQ_INSTS_VALU"]
 if "FETCH_SIZE" in avg:
     # KB; FETCH_SIZE counts half the bytes of wide streaming reads on gfx950
     # (MI355X_MICROARCH.md, HBM): doubled
     res["hbm_bytes_per_launch"] = (2 * avg.get("FETCH_SIZE", 0) + avg.get("WRITE_SIZE", 0)) * 1024
-if "valu_busy_2cyc" in res:
+if "valu_busy_4cyc" in res:
+    res["valu_busy"] = res["valu_busy_4cyc"]
+elif "valu_busy_2cyc" in res:
     res["valu_busy"] = res["valu_busy_2cyc"]
 res["workload"] = os.environ.get("WORKLOAD", "config#2")
 print(json.dumps(res, indent=1))
