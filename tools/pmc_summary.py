@@ -27,6 +27,15 @@ if kt:
         if want in r["Name"]:
             dur = float(r["AverageNs"]) / 1e6
 res = {"kernel": want, "avg_ms_kernel_trace": dur, "counters_per_dispatch": avg}
+# the same average over the bench's timed steps only (the last STEPS dispatches;
+# the first warmup calls run on a cold instruction cache)
+ktr = glob.glob(os.path.join(out, "kt", "*kernel_trace.csv"))
+if ktr:
+    d = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"])) for r in csv.DictReader(open(ktr[0]))
+               if want in r["Kernel_Name"])
+    steps = int(os.environ.get("STEPS", "20"))
+    if len(d) >= steps:
+        res["avg_ms_timed_steps"] = sum(e - b for b, e in d[-steps:]) / steps / 1e6
 if "SQ_WAVE_CYCLES" in avg:
     wc = avg["SQ_WAVE_CYCLES"]
     for k in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_LDS", "SQ_ACTIVE_INST_LDS",
