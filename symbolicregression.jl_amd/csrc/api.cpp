@@ -773,7 +773,10 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     if (pass == -1) {
       const int narr = 1 + nfeat + (w ? 1 : 0);
       // partials go to global memory: LDS holds the tiles (1 byte per slot keeps the slot bound away)
-      if (!plan_geometry(4, 4, kShallowSlots, narr, 1, rows, nlist, &plan, jit_tile_budget(), 52 * 1024))
+      // 16384 workgroups, >= 64 trees per group (16 per wave): config #2 kernel
+      // 2.997 -> 2.867 ms at 4096 trees, 0.865 -> 0.828 at 1024, 512 unchanged
+      // (tools/gpu_targetwg.sh, profiles/r02n_targetwg.txt)
+      if (!plan_geometry(4, 4, kShallowSlots, narr, 1, rows, nlist, &plan, jit_tile_budget(), 52 * 1024, 16384, 64))
         throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
     } else if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan)) {
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");

@@ -71,8 +71,11 @@ hipError_t launch_ti_records(const Ins<float>* prog, const int32_t* list_off, in
 bool plan_eval(int dtype, bool deep, int opset, int mode, bool weighted, int nfeat,
                int64_t n, int nlist, EvalPlan* plan);
 // Same, for explicit R / D / LDS arrays / partial bytes per tree slot.
+// target_wg: workgroups the tree groups aim at; min_per_group: trees a group
+// keeps at least (the loss tree code: 16384 / 64, measured on config #2)
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n,
-                   int nlist, EvalPlan* plan, size_t tile_budget = 40 * 1024, size_t two_tile_cap = 0);
+                   int nlist, EvalPlan* plan, size_t tile_budget = 40 * 1024, size_t two_tile_cap = 0,
+                   int target_wg = 8192, int min_per_group = 4);
 
 // ---- constant gradients (grad_kernels.hip) -----------------------------------
 constexpr int kGradG = 4;  // tangents per pass (constants per "tangent group")

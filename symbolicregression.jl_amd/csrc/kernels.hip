@@ -161,7 +161,7 @@ hipError_t launch_ti_records(const Ins<float>* prog, const int32_t* list_off, in
 }
 
 bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_t n, int nlist,
-                   EvalPlan* p, size_t tile_budget, size_t two_tile_cap) {
+                   EvalPlan* p, size_t tile_budget, size_t two_tile_cap, int target_wg_in, int min_per_group) {
   p->R = R;
   p->D = D;
   p->opset = OPSET_FULL;
@@ -188,9 +188,18 @@ bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_
   p->rows_wg = nt * p->tile;
   p->nrg = (int)((n + p->rows_wg - 1) / p->rows_wg);
   if (p->nrg < 1) p->nrg = 1;
-  const int target_wg = 8192;
+  // SRHIP_TARGET_WG (experiments) overrides the caller's target
+  static const int target_env = [] {
+    const char* e = std::getenv("SRHIP_TARGET_WG");
+    return e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  const int target_wg = target_env ? target_env : target_wg_in;
   int ntg = (target_wg + p->nrg - 1) / p->nrg;
-  const int max_groups = (nlist + 3) / 4;  // at least ~4 trees (one per wave) per group
+  // at least min_per_group trees per group, unless that leaves fewer than 2048
+  // workgroups (few rows); never fewer than ~4 trees (one per wave)
+  const int max4 = std::max(1, (nlist + 3) / 4);
+  const int floor_groups = (2048 + p->nrg - 1) / p->nrg;
+  const int max_groups = std::min(max4, std::max((nlist + min_per_group - 1) / min_per_group, floor_groups));
   if (ntg > max_groups) ntg = max_groups;
   // XCD affinity: workgroups are dealt round-robin to the 8 XCDs, and block b
   // runs tree group b % ntg, so with ntg a divisor or multiple of 8 every XCD
