@@ -107,6 +107,11 @@ struct srhip_ctx {
   double* pin_sum = nullptr;
   uint8_t* pin_ok = nullptr;
   size_t pin_cap = 0;
+  // where the finalize of the current evaluation writes the per-tree results:
+  // the pinned host buffers themselves (zero copy) or sums / oks on the device
+  double* res_sum = nullptr;
+  uint8_t* res_ok = nullptr;
+  bool res_host = false;
   uint32_t* pin_cnt = nullptr;  // [2]
   double last_ms = 0.0;
   int last_launches = 0;
@@ -473,6 +478,12 @@ bool rg_xcd() {
   return !(e && e[0] == '0');
 }
 
+bool zero_copy_enabled() {
+  const char* e = std::getenv("SRHIP_ZERO_COPY");  // read per call: A/B measurements
+  return !(e && e[0] == '0');
+}
+void ensure_pinned(srhip_ctx* c, size_t nt);
+
 // LDS for the row tiles of a tree-code workgroup (SRHIP_EVAL_LDS, KiB)
 size_t jit_tile_budget() {
   static const size_t b = [] {
@@ -718,7 +729,7 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
     const int tk = timed_begin(c, s);
     HIP_CHECK(launch_eval<T>(plan, a, MODE_LOSS, s));
     timed_end(c, s, tk);
-    HIP_CHECK(launch_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
+    HIP_CHECK(launch_finalize<T>(a, c->res_sum, c->res_ok, s));
     c->last_bailed = nb;
     if (std::getenv("SRHIP_DEBUG_PASSES")) std::fprintf(stderr, "srhip pass bail-rerun: %d trees\n", nb);
   }
@@ -734,6 +745,17 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   timing_reset(c);
   c->sums.ensure(std::max<size_t>(p->ntrees, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(p->ntrees, 1));
+  // the finalize writes the per-tree results straight into the pinned host
+  // buffers (no copy launches; SRHIP_ZERO_COPY=0: device buffers + copies)
+  c->res_host = zero_copy_enabled();
+  if (c->res_host) {
+    ensure_pinned(c, std::max<size_t>(p->ntrees, 1));
+    c->res_sum = c->pin_sum;
+    c->res_ok = c->pin_ok;
+  } else {
+    c->res_sum = static_cast<double*>(c->sums.p);
+    c->res_ok = static_cast<uint8_t*>(c->oks.p);
+  }
   const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
   // slot ranges: [0, nj) tree code, [nj, nlist_a) shallow interpreter, then deep
   const bool use_jit = std::is_same<T, float>::value && p->jit && p->nlist_j > 0 && mode == MODE_LOSS &&
@@ -823,7 +845,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
     timed_end(c, s, tk);
-    HIP_CHECK(launch_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
+    HIP_CHECK(launch_finalize<T>(a, c->res_sum, c->res_ok, s));
     static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
     if (dbg) {  // debugging only: wait for the launch to report its time
       HIP_CHECK(hipStreamSynchronize(s));
@@ -845,15 +867,18 @@ void ensure_pinned(srhip_ctx* c, size_t nt) {
   c->pin_sum = nullptr;
   c->pin_ok = nullptr;
   c->pin_cap = 0;
-  HIP_CHECK(hipHostMalloc((void**)&c->pin_sum, nt * sizeof(double), hipHostMallocDefault));
-  HIP_CHECK(hipHostMalloc((void**)&c->pin_ok, nt, hipHostMallocDefault));
+  // coherent: the finalize kernel may write them directly (zero copy)
+  HIP_CHECK(hipHostMalloc((void**)&c->pin_sum, nt * sizeof(double), hipHostMallocCoherent));
+  HIP_CHECK(hipHostMalloc((void**)&c->pin_ok, nt, hipHostMallocCoherent));
   c->pin_cap = nt;
 }
 
-// the per-tree results to pinned host memory (asynchronous)
+// the per-tree results to pinned host memory (asynchronous; nothing to copy
+// when the finalize wrote them there)
 bool enqueue_result_copies(srhip_ctx* c, const srhip_program* p, int64_t rows) {
   const int nt = p->ntrees;
   if (!(rows > 0 && nt > 0 && (p->nlist_a + p->nlist_b) > 0)) return false;
+  if (c->res_host) return true;
   HIP_CHECK(hipMemcpyAsync(c->pin_sum, c->sums.p, nt * sizeof(double), hipMemcpyDeviceToHost, c->stream));
   HIP_CHECK(hipMemcpyAsync(c->pin_ok, c->oks.p, nt, hipMemcpyDeviceToHost, c->stream));
   return true;
