@@ -80,22 +80,56 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
     ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--stub", action="store_true",
+                    help="launcher test only (tests/test_bench_launcher.py): gloo, no GPU, no evaluation")
     return ap.parse_args()
+
+
+def free_port() -> int:
+    import socket
+
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def launch_ranks(nproc: int) -> int:
+    """`python bench.py --gpus N` without a launcher around it: start N ranks
+    through torch.distributed.run (one process per GPU, RCCL) and pass their
+    output through. This parent never touches the GPU (no HIP call before the
+    children start); rank 0 prints the JSON line."""
+    import subprocess
+
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", str(Path(__file__).resolve())] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    env.setdefault("OMP_NUM_THREADS", "1")
+    return subprocess.run(cmd, env=env).returncode
 
 
 def main():
     args = parse()
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but WORLD_SIZE {world}")
     dist = None
     if world > 1:
         import torch
         import torch.distributed as tdist
 
-        torch.cuda.set_device(local_rank)
-        tdist.init_process_group("nccl")
+        if args.stub:
+            tdist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local_rank)
+            tdist.init_process_group("nccl")
         dist = (torch, tdist)
+    if args.stub:
+        return stub_main(args, world, rank, dist)
 
     import srhip
     from srhip import constants as K
@@ -261,6 +295,22 @@ def main():
         "setup_s": {"tree_gen": round(t_gen, 2), "compile_upload": round(t_compile, 3)},
     }
     print(json.dumps(out))
+    if dist:
+        dist[1].destroy_process_group()
+
+
+def stub_main(args, world, rank, dist):
+    """Launcher test (no GPU): every rank reports its world and rank through
+    the same barrier / max-over-ranks path; no evaluation, no metric."""
+    import torch
+
+    t = torch.tensor([float(rank + 1)], dtype=torch.float64)
+    if dist:
+        dist[1].barrier()
+        dist[1].all_reduce(t, op=dist[1].ReduceOp.SUM)
+    if rank == 0:
+        print(json.dumps({"stub": True, "n_gpus": world, "rank_sum": float(t.item()), "steps": args.steps,
+                          "warmup": args.warmup}))
     if dist:
         dist[1].destroy_process_group()
 
