@@ -547,8 +547,8 @@ def _optimize_nelder_mead(dataset, trees, options, rng, device, evaluator_factor
     f_calls += 1
     xmin, fmin = [], np.zeros(nc)
     for k in range(nc):
-        i = int(np.argmin(np.where(np.isnan(fsx[k]), np.inf, fsx[k])))
-        if fcen[k] < fsx[k][i]:
+        i = julia_findmin(fsx[k])
+        if fcen[k] < fsx[k][i]:  # False for a NaN minimum: the NaN vertex is kept, as in Optim
             xmin.append(xcen[k])
             fmin[k] = fcen[k]
         else:
@@ -569,6 +569,15 @@ def _optimize_nelder_mead(dataset, trees, options, rng, device, evaluator_factor
             num_evals[i] += 1
     return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat), converged_out,
                           num_evals)
+
+
+def julia_findmin(f) -> int:
+    """Index Julia's `findmin` picks (Optim's NelderMead after_while!): the
+    first NaN if there is one (findmin propagates NaN), else the first
+    minimum."""
+    f = np.asarray(f)
+    nan = np.flatnonzero(np.isnan(f))
+    return int(nan[0]) if nan.size else int(np.argmin(f))
 
 
 def _final_losses(trees, dataset, options, device, factory, flat=None) -> np.ndarray:

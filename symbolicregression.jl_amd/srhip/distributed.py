@@ -187,11 +187,29 @@ def eval_loss_row_sharded(trees, dataset, options, device: Optional[int] = None,
     return out, tok
 
 
+def shared_rng(rng=None, group=None) -> np.random.Generator:
+    """One generator state on every rank: with rng None, rank 0 draws a seed
+    and broadcasts it; a given rng must already be seeded identically on every
+    rank (the caller's contract). The row-sharded optimiser needs this: each
+    rank builds the perturbed restarts (ConstantOptimization.jl:46-54) itself,
+    and partials all-reduced at different constants would describe no
+    candidate."""
+    import torch.distributed as dist
+
+    if rng is not None:
+        return rng
+    seed = [int(np.random.SeedSequence().entropy % (1 << 63))] if dist.get_rank(group) == 0 else [None]
+    dist.broadcast_object_list(seed, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+    return np.random.default_rng(seed[0])
+
+
 def optimize_constants_row_sharded(trees, dataset, options, rng=None, device: Optional[int] = None, group=None):
     """optimize_constants_batch with the dataset's rows sharded over the ranks
     of the process group: every rank uploads its shard, compiles the
     candidates on it, and all-reduces loss and gradient partials per step
-    (RowShardedEvaluator). All ranks return the same result."""
+    (RowShardedEvaluator). All ranks return the same result: with rng None
+    the ranks share one broadcast seed (`shared_rng`); a given rng must be
+    seeded identically on every rank."""
     import torch.distributed as dist
 
     from .constant_optimization import optimize_constants_batch
@@ -209,4 +227,4 @@ def optimize_constants_row_sharded(trees, dataset, options, rng=None, device: Op
         return RowShardedEvaluator(compile_trees(cands, options, dataset.T, dev.ctx.device), dev,
                                    options.elementwise_loss, red, dataset.T)
 
-    return optimize_constants_batch(dataset, trees, options, rng=rng, evaluator_factory=factory)
+    return optimize_constants_batch(dataset, trees, options, rng=shared_rng(rng, group), evaluator_factory=factory)

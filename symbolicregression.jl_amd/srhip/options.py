@@ -70,10 +70,26 @@ def LogitDistLoss():
 REFERENCE_ONLY_KWARGS = frozenset("""
 constraints tournament_selection_p fast_cycle migration hof_migration output_file mutation_weights
 crossover_probability warmup_maxsize_by use_frequency use_frequency_in_tournament adaptive_parsimony_scaling
-verbosity save_to_file seed bin_constraints una_constraints progress terminal_width optimizer_options
+verbosity save_to_file seed bin_constraints una_constraints progress terminal_width
 recorder recorder_file early_stop_condition return_state timeout_in_seconds max_evals skip_mutation_failures
 enable_autodiff nested_constraints deterministic define_helper_functions
 """.split())
+
+
+# Deprecated keyword aliases (src/Options.jl:122-143): accepted with a
+# DeprecationWarning (Base.depwarn, :380-399) and applied under the new name.
+DEPRECATED_KWARGS = {
+    "mutationWeights": "mutation_weights", "hofMigration": "hof_migration",
+    "shouldOptimizeConstants": "should_optimize_constants", "hofFile": "output_file",
+    "perturbationFactor": "perturbation_factor", "batchSize": "batch_size",
+    "crossoverProbability": "crossover_probability", "warmupMaxsizeBy": "warmup_maxsize_by",
+    "useFrequency": "use_frequency", "useFrequencyInTournament": "use_frequency_in_tournament",
+    "ncyclesperiteration": "ncycles_per_iteration", "fractionReplaced": "fraction_replaced",
+    "fractionReplacedHof": "fraction_replaced_hof", "probNegate": "probability_negate_constant",
+    "optimize_probability": "optimizer_probability", "probPickFirst": "tournament_selection_p",
+    "earlyStopCondition": "early_stop_condition", "stateReturn": "return_state", "ns": "tournament_selection_n",
+    "loss": "elementwise_loss",
+}
 
 
 def _opname(op) -> str:
@@ -111,6 +127,7 @@ class Options:
         optimizer_nrestarts: int = 2,
         optimizer_probability: float = 0.14,
         optimizer_iterations: Optional[int] = None,
+        optimizer_options=None,
         should_optimize_constants: bool = True,
         # search (src/Options.jl:315-370 defaults), read by srhip.equation_search
         npop: int = 33,
@@ -130,9 +147,40 @@ class Options:
         # keywords of the reference that only steer its control plane (which
         # this engine does not rebuild) are accepted and kept in
         # `self.ignored`, with one warning.
+        renamed = {}
+        for k in [k for k in kws if k in DEPRECATED_KWARGS]:
+            new = DEPRECATED_KWARGS[k]
+            warnings.warn(f"The keyword argument `{k}` is deprecated. Use `{new}` instead.", DeprecationWarning,
+                          stacklevel=2)
+            v = kws.pop(k)
+            if new in REFERENCE_ONLY_KWARGS:
+                kws[new] = v
+            else:
+                renamed[new] = v
         unknown = sorted(k for k in kws if k not in REFERENCE_ONLY_KWARGS)
         if unknown:
             raise TypeError(f"Unknown keyword argument(s): {', '.join(unknown)}")
+        loc = dict(locals())
+        for new, v in renamed.items():  # the deprecated alias wins, as in the reference
+            loc[new] = v
+        elementwise_loss, parsimony, batch_size = loc["elementwise_loss"], loc["parsimony"], loc["batch_size"]
+        should_optimize_constants, perturbation_factor = loc["should_optimize_constants"], loc["perturbation_factor"]
+        ncycles_per_iteration, fraction_replaced = loc["ncycles_per_iteration"], loc["fraction_replaced"]
+        fraction_replaced_hof = loc["fraction_replaced_hof"]
+        probability_negate_constant = loc["probability_negate_constant"]
+        optimizer_probability, tournament_selection_n = loc["optimizer_probability"], loc["tournament_selection_n"]
+        # optimizer_options (src/Options.jl:606-621): its `iterations` overrides
+        # optimizer_iterations; the batched optimiser implements no other
+        # Optim.Options field, so any other key is refused rather than dropped
+        if optimizer_options is not None:
+            oo = dict(optimizer_options) if not isinstance(optimizer_options, dict) else optimizer_options
+            other = sorted(str(k) for k in oo if str(k) != "iterations")
+            if other:
+                raise Unsupported(-2, "optimizer_options: only `iterations` is implemented by the batched "
+                                      f"constant optimiser (got {', '.join(other)})")
+            if "iterations" in oo:
+                optimizer_iterations = int(oo["iterations"])
+        self.optimizer_options = optimizer_options
         self.ignored = dict(kws)
         if kws:
             warnings.warn("Options: keyword(s) " + ", ".join(sorted(kws)) + " only affect the reference's "

@@ -20,7 +20,8 @@ not change what the engine evaluates): simplify/combine_operators (treated as
 do_nothing), crossover (fast_cycle forbids it, :41), `use_frequency`
 adaptive parsimony, the recorder, progress output, early stopping. One
 deviation: with `batching=true` the babies of one launch share one minibatch
-row sample (the reference draws one per `score_func_batch` call).
+row sample, and the parents' re-scores (Mutate.jl:41-47) another (the
+reference draws one per `score_func_batch` call).
 
 Islands are independent between migrations, so with `world > 1` each rank
 runs its own islands (no data-path collective) and the best members are
@@ -88,7 +89,8 @@ def _acceptance(after: float, before: float, temperature: float, options: Option
     """probChange of next_generation (src/Mutate.jl:229-233) with Julia's IEEE
     semantics: exp(-delta / (T * alpha)) where T = 0 on the last annealing cycle
     gives exp(±Inf) (0 or Inf) and an overflowing exponent gives Inf, not an
-    exception; NaN (e.g. Inf - Inf) never passes `probChange < rand()` as false."""
+    exception. A NaN (Inf - Inf, or 0/0 at T = 0) makes `probChange < rand()`
+    false, so the reference keeps such a baby; the caller compares the same way."""
     if not _opt(options, "annealing"):
         return 1.0
     with np.errstate(all="ignore"):
@@ -258,20 +260,29 @@ def equation_search(X: np.ndarray, y: np.ndarray, options: Options, niterations:
                     parents.append((k, allstar, choice, baby))
                     if baby is not None and choice not in ("do_nothing", "simplify", "optimize"):
                         babies.append(baby)
+            # with options.batching every next_generation first re-scores its
+            # parent on a fresh minibatch (Mutate.jl:41-47): one launch for all
+            # parents of the cycle, on a row sample of its own
+            if options.batching and parents:
+                psc, plo = score_babies([allstar.tree for _, allstar, _, _ in parents])
+            else:
+                psc = [allstar.score for _, allstar, _, _ in parents]
+                plo = [allstar.loss for _, allstar, _, _ in parents]
             sc, lo = score_babies(babies)  # ONE launch for every island's babies
             b = 0
-            for k, allstar, choice, baby in parents:
+            for q, (k, allstar, choice, baby) in enumerate(parents):
+                before_score, before_loss = psc[q], plo[q]
                 if baby is None:
                     continue  # failed mutation: skip_mutation_failures (default true)
                 if choice in ("do_nothing", "simplify", "optimize"):
-                    new = PopMember(baby, allstar.score, allstar.loss, born())
+                    new = PopMember(baby, before_score, before_loss, born())
                 else:
                     s, l = sc[b], lo[b]
                     b += 1
                     if np.isnan(s):  # Mutate.jl:207: only a NaN score is rejected outright
                         continue
-                    prob = _acceptance(s, allstar.score, temperature, options)
-                    if not (prob >= rng.random()):  # `probChange < rand()` rejects; NaN never accepts
+                    prob = _acceptance(s, before_score, temperature, options)
+                    if prob < rng.random():  # Mutate.jl:247 `probChange < rand()`: a NaN prob is kept
                         continue
                     new = PopMember(baby, s, l, born())
                 pop = pops[k]

@@ -294,3 +294,14 @@ def test_flat_take_matches_flatten():
         np.testing.assert_array_equal(getattr(got, k), getattr(ref, k))
     c = np.arange(ref.const_off[-1], dtype=np.float32)
     np.testing.assert_array_equal(flat.take(idx, c).consts, c)
+
+
+def test_nelder_mead_minimiser_follows_julia_findmin():
+    """Optim's after_while! takes findmin of the simplex losses: a NaN vertex is
+    the minimum (findmin propagates NaN), and `f_centroid < NaN` is false, so
+    that vertex is the result."""
+    from srhip.constant_optimization import julia_findmin
+    assert julia_findmin([3.0, 1.0, 2.0]) == 1
+    assert julia_findmin([3.0, np.nan, 1.0, np.nan]) == 1
+    assert julia_findmin([1.0, 1.0]) == 0
+    assert not (0.5 < np.nan)  # the centroid never replaces a NaN minimum

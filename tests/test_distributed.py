@@ -169,7 +169,7 @@ def _copt_problem():
     return o, X, y, trees
 
 
-def _copt_worker(rank, world, port, q):
+def _copt_worker(rank, world, port, q, shared=False):
     import sys
     from pathlib import Path
 
@@ -177,7 +177,7 @@ def _copt_worker(rank, world, port, q):
     sys.path[:0] = [str(root / "symbolicregression.jl_amd"), str(root / "oracle"), str(root / "tests")]
     import torch.distributed as dist
 
-    from srhip.distributed import RowShardedEvaluator, torch_all_reduce_sum
+    from srhip.distributed import RowShardedEvaluator, shared_rng, torch_all_reduce_sum
     from test_distributed import OracleShardProgram, _copt_problem
 
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
@@ -191,7 +191,9 @@ def _copt_worker(rank, world, port, q):
         return RowShardedEvaluator(OracleShardProgram(cands, o, X[:, b:e], y[b:e]), None, o.elementwise_loss, red,
                                    np.float64)
 
-    res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(5), evaluator_factory=factory)
+    # shared: no rng given, the ranks agree on rank 0's broadcast seed
+    rng = shared_rng(None) if shared else np.random.default_rng(5)
+    res = srhip.optimize_constants_batch(ds, trees, o, rng=rng, evaluator_factory=factory)
     q.put((rank, res.losses, res.converged))
     dist.destroy_process_group()
 
@@ -220,3 +222,23 @@ def test_constant_optimization_row_sharded_gloo_world2():
     np.testing.assert_array_equal(l0, l1)  # both ranks agree exactly
     assert np.array_equal(c0, ref.converged)
     np.testing.assert_allclose(l0, ref.losses, rtol=1e-7)
+
+
+@pytest.mark.timeout(120)
+def test_constant_optimization_row_sharded_unseeded_ranks_agree():
+    """With no rng given, every rank must still build the same perturbed
+    restarts: rank 0's seed is broadcast (srhip.distributed.shared_rng)."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_copt_worker, args=(r, world, port, q, True)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=100) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    (_, l0, c0), (_, l1, c1) = res
+    np.testing.assert_array_equal(l0, l1)
+    np.testing.assert_array_equal(c0, c1)

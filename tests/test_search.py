@@ -83,7 +83,8 @@ def test_annealing_acceptance_uses_ieee_semantics():
     assert _acceptance(1.0, 2.0, 0.0, o) == np.inf      # improvement at T = 0: exp(+Inf)
     assert _acceptance(2.0, 1.0, 0.0, o) == 0.0         # worse at T = 0: exp(-Inf)
     assert _acceptance(-100.0, 0.0, 1.0, o) == np.inf   # exponent 1000 overflows to Inf, no exception
-    assert np.isnan(_acceptance(np.inf, np.inf, 1.0, o))  # NaN: `NaN < rand()` is false -> never accepted
+    nan = _acceptance(np.inf, np.inf, 1.0, o)
+    assert np.isnan(nan) and not (nan < 0.5)  # `NaN < rand()` is false in Julia: the baby is KEPT (Mutate.jl:247)
     assert _acceptance(1.0, 2.0, 1.0, srhip.Options()) == 1.0
 
 
@@ -103,8 +104,11 @@ def test_search_with_annealing_and_batching_on_oracle():
                                        evaluator_factory=lambda c: OracleEvaluator(c, o, X, y))
     front = hof.dominating()
     assert front
-    # every baby launch went through the minibatch scorer with batch_size rows
-    assert len(sizes) >= 2 * 40 - 2 and set(sizes) == {30}
+    # every cycle: one minibatch launch re-scoring the parents (Mutate.jl:41-47)
+    # and one for the babies, each with batch_size rows
+    assert len(sizes) >= 2 * (2 * 40 - 2) and set(sizes) == {30}
+    # num_evals counts both minibatch evaluations per next_generation (Mutate.jl:44,200)
+    assert stats["evals"] > 0
 
 
 @pytest.mark.gpu
@@ -165,3 +169,22 @@ def test_islands_sharded_gloo_world2():
         assert p.exitcode == 0
     assert res[0][1] == res[1][1]
     assert res[0][2] > 0 and res[1][2] > 0
+
+
+def test_options_deprecated_aliases_and_optimizer_options():
+    """Deprecated keyword aliases (src/Options.jl:122-143) apply under their new
+    names with a DeprecationWarning; optimizer_options' `iterations` overrides
+    optimizer_iterations (:606-621); other Optim.Options fields are refused,
+    not dropped."""
+    import warnings
+    with warnings.catch_warnings(record=True) as w:
+        warnings.simplefilter("always")
+        o = srhip.Options(batchSize=77, ncyclesperiteration=9, ns=5, hofMigration=False,
+                          optimizer_options={"iterations": 3})
+    assert (o.batch_size, o.ncycles_per_iteration, o.tournament_selection_n, o.optimizer_iterations) == (77, 9, 5, 3)
+    assert o.ignored == {"hof_migration": False}
+    assert sum(issubclass(x.category, DeprecationWarning) for x in w) == 4
+    with pytest.raises(srhip.Unsupported):
+        srhip.Options(optimizer_options={"g_abstol": 1e-3})
+    with pytest.raises(TypeError):
+        srhip.Options(notAnOption=1)
