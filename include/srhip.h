@@ -16,8 +16,13 @@
  *  - All host buffers are owned by the caller. Calls are synchronous: the
  *    results are in the caller's buffers when the call returns.
  *  - A context serialises the calls made through it (one mutex, one stream).
- *    Use one context per host thread for concurrency; datasets and
- *    programs belong to the context that created them.
+ *    Use one context per host thread for concurrency. A program belongs to
+ *    the context that created it, and an evaluation call runs on the
+ *    PROGRAM's context: a dataset (read-only device memory once created) is
+ *    shared by every context of its device, so threads create their programs
+ *    in their own contexts and evaluate them concurrently on one dataset.
+ *    A program and a dataset on different devices give SRHIP_ERR_INVALID.
+ *    Destroy a dataset only when no call on it is in progress.
  *  - Trees cross the boundary as post-order (postfix) node streams: for a
  *    node, its left subtree, then its right subtree, then the node itself.
  *    Constants are listed separately, in the order of the constant leaves in
@@ -193,12 +198,22 @@ int32_t srhip_eval_loss(srhip_dataset* ds, const srhip_program* prog,
                         const int64_t* row_idx, int64_t nidx,
                         double* out_loss_sum, double* out_weight_sum,
                         uint8_t* out_ok);
-/* Convenience: srhip_program_create + srhip_eval_loss + destroy. */
+/* Convenience: srhip_program_create + srhip_eval_loss + destroy (the program
+ * in the dataset's context). */
 int32_t srhip_eval_loss_batch(srhip_dataset* ds, const srhip_trees* trees,
                               int32_t loss_kind, const double* loss_params,
                               const int64_t* row_idx, int64_t nidx,
                               double* out_loss_sum, double* out_weight_sum,
                               uint8_t* out_ok);
+/* The same with the program in `ctx` (a context of the dataset's device):
+ * one context per host thread scores that thread's candidates concurrently
+ * with the others on one shared dataset (SearchUtils.jl:33-45, one
+ * Threads.@spawn per island). */
+int32_t srhip_eval_loss_batch_ctx(srhip_ctx* ctx, srhip_dataset* ds, const srhip_trees* trees,
+                                  int32_t loss_kind, const double* loss_params,
+                                  const int64_t* row_idx, int64_t nidx,
+                                  double* out_loss_sum, double* out_weight_sum,
+                                  uint8_t* out_ok);
 
 /* ---- per-row outputs: eval_tree_array src/InterfaceDynamicExpressions.jl:50-52
  * out is [ntrees][rows] of the dataset dtype (row-major per tree); rows of a

@@ -637,7 +637,12 @@ void update_constants(srhip_program* p) {
 
 void check_program_vs_dataset(const srhip_dataset* ds, const srhip_program* p) {
   if (!ds || !p) throw Error(SRHIP_ERR_INVALID, "null dataset or program");
-  if (ds->ctx != p->ctx) throw Error(SRHIP_ERR_INVALID, "dataset and program belong to different contexts");
+  // a dataset is read-only device memory once created: any context of its
+  // device may evaluate a program on it (the program's context runs the call)
+  if (ds->ctx->device != p->ctx->device)
+    throw Error(SRHIP_ERR_INVALID, "dataset is on device " + std::to_string(ds->ctx->device) + " but the program on device " +
+                                       std::to_string(p->ctx->device) +
+                                       ": create the program with a context of the dataset's device");
   if (ds->dtype != p->dtype) throw Error(SRHIP_ERR_INVALID, "dataset and program dtypes differ");
   if (p->max_feature >= ds->nfeat)
     throw Error(SRHIP_ERR_INVALID, "tree references feature " + std::to_string(p->max_feature + 1) +
@@ -914,7 +919,7 @@ template <typename T>
 int eval_loss_impl(srhip_dataset* ds, const srhip_program* p, int loss, const double* params,
                    const int64_t* row_idx, int64_t nidx, double* out_sum, double* out_wsum,
                    uint8_t* out_ok) {
-  srhip_ctx* c = ds->ctx;
+  srhip_ctx* c = p->ctx;  // the program's context runs the call (stream, workspace, results)
   const T* X = static_cast<const T*>(ds->X);
   const T* y = static_cast<const T*>(ds->y);
   const T* w = static_cast<const T*>(ds->w);
@@ -957,7 +962,7 @@ int eval_loss_impl(srhip_dataset* ds, const srhip_program* p, int loss, const do
 
 template <typename T>
 int eval_tree_array_impl(srhip_dataset* ds, const srhip_program* p, void* out, uint8_t* out_ok) {
-  srhip_ctx* c = ds->ctx;
+  srhip_ctx* c = p->ctx;
   const int nt = p->ntrees;
   const int64_t rows = ds->rows, n_pad = ds->n_pad;
   const size_t es = sizeof(T);
@@ -1136,8 +1141,8 @@ void collect_grad_results(srhip_ctx* c, const srhip_program* p, int64_t rows, do
 template <typename T>
 int eval_loss_grad_impl(srhip_dataset* ds, srhip_program* p, int loss, const double* params,
                         double* out_sum, double* out_dloss, double* out_wsum, uint8_t* out_ok) {
-  run_grad<T>(ds->ctx, p, GRAD_LOSS, ds, loss, params ? params[0] : 0.0, nullptr, nullptr, 0);
-  collect_grad_results(ds->ctx, p, ds->rows, out_sum, out_dloss, out_ok);
+  run_grad<T>(p->ctx, p, GRAD_LOSS, ds, loss, params ? params[0] : 0.0, nullptr, nullptr, 0);
+  collect_grad_results(p->ctx, p, ds->rows, out_sum, out_dloss, out_ok);
   if (out_wsum) *out_wsum = ds->w ? ds->sum_w : (double)ds->rows;
   return SRHIP_OK;
 }
@@ -1145,7 +1150,7 @@ int eval_loss_grad_impl(srhip_dataset* ds, srhip_program* p, int loss, const dou
 template <typename T>
 int eval_grad_tree_array_impl(srhip_dataset* ds, srhip_program* p, void* out_value, void* out_grad,
                               uint8_t* out_ok) {
-  srhip_ctx* c = ds->ctx;
+  srhip_ctx* c = p->ctx;
   const int nt = p->ntrees;
   const int nconst = p->const_off.back();
   const int64_t rows = ds->rows, n_pad = ds->n_pad;
@@ -1514,8 +1519,8 @@ int32_t srhip_eval_loss(srhip_dataset* ds, const srhip_program* prog, int32_t lo
                              loss_kind == SRHIP_LOSS_L1EPSINS || loss_kind == SRHIP_LOSS_L2EPSINS ||
                              loss_kind == SRHIP_LOSS_QUANTILE || loss_kind == SRHIP_LOSS_PERIODIC;
     if (needs_param && !loss_params) throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
-    std::lock_guard<std::mutex> lk(ds->ctx->mu);
-    HIP_CHECK(hipSetDevice(ds->ctx->device));
+    std::lock_guard<std::mutex> lk(prog->ctx->mu);
+    HIP_CHECK(hipSetDevice(prog->ctx->device));
     if (ds->dtype == SRHIP_F32)
       return eval_loss_impl<float>(ds, prog, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
     return eval_loss_impl<double>(ds, prog, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
@@ -1526,8 +1531,17 @@ int32_t srhip_eval_loss_batch(srhip_dataset* ds, const srhip_trees* trees, int32
                               const double* loss_params, const int64_t* row_idx, int64_t nidx,
                               double* out_loss_sum, double* out_weight_sum, uint8_t* out_ok) {
   if (!ds) return set_error(SRHIP_ERR_INVALID, "null dataset");
+  return srhip_eval_loss_batch_ctx(ds->ctx, ds, trees, loss_kind, loss_params, row_idx, nidx, out_loss_sum,
+                                   out_weight_sum, out_ok);
+}
+
+int32_t srhip_eval_loss_batch_ctx(srhip_ctx* ctx, srhip_dataset* ds, const srhip_trees* trees, int32_t loss_kind,
+                                  const double* loss_params, const int64_t* row_idx, int64_t nidx,
+                                  double* out_loss_sum, double* out_weight_sum, uint8_t* out_ok) {
+  if (!ds) return set_error(SRHIP_ERR_INVALID, "null dataset");
+  if (!ctx) return set_error(SRHIP_ERR_INVALID, "null ctx");
   srhip_program* p = nullptr;
-  int32_t rc = srhip_program_create(ds->ctx, ds->dtype, trees, &p);
+  int32_t rc = srhip_program_create(ctx, ds->dtype, trees, &p);
   if (rc != SRHIP_OK) return rc;
   rc = srhip_eval_loss(ds, p, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
   std::string err = g_last_error;
@@ -1539,8 +1553,8 @@ int32_t srhip_eval_loss_batch(srhip_dataset* ds, const srhip_trees* trees, int32
 int32_t srhip_eval_tree_array(srhip_dataset* ds, const srhip_program* prog, void* out, uint8_t* out_ok) {
   return guarded([&] {
     check_program_vs_dataset(ds, prog);
-    std::lock_guard<std::mutex> lk(ds->ctx->mu);
-    HIP_CHECK(hipSetDevice(ds->ctx->device));
+    std::lock_guard<std::mutex> lk(prog->ctx->mu);
+    HIP_CHECK(hipSetDevice(prog->ctx->device));
     if (ds->dtype == SRHIP_F32) return eval_tree_array_impl<float>(ds, prog, out, out_ok);
     return eval_tree_array_impl<double>(ds, prog, out, out_ok);
   });
@@ -1555,8 +1569,8 @@ int32_t srhip_eval_loss_grad(srhip_dataset* ds, const srhip_program* prog, int32
     if (loss_kind != SRHIP_LOSS_L2 && loss_kind != SRHIP_LOSS_L1 && loss_kind != SRHIP_LOSS_LOGCOSH &&
         loss_kind != SRHIP_LOSS_LOGITDIST && !loss_params)
       throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
-    std::lock_guard<std::mutex> lk(ds->ctx->mu);
-    HIP_CHECK(hipSetDevice(ds->ctx->device));
+    std::lock_guard<std::mutex> lk(prog->ctx->mu);
+    HIP_CHECK(hipSetDevice(prog->ctx->device));
     auto* p = const_cast<srhip_program*>(prog);  // gradient programs are built lazily
     if (ds->dtype == SRHIP_F32)
       return eval_loss_grad_impl<float>(ds, p, loss_kind, loss_params, out_loss_sum, out_dloss, out_weight_sum, out_ok);
@@ -1568,8 +1582,8 @@ int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog,
                                    void* out_grad, uint8_t* out_ok) {
   return guarded([&] {
     check_program_vs_dataset(ds, prog);
-    std::lock_guard<std::mutex> lk(ds->ctx->mu);
-    HIP_CHECK(hipSetDevice(ds->ctx->device));
+    std::lock_guard<std::mutex> lk(prog->ctx->mu);
+    HIP_CHECK(hipSetDevice(prog->ctx->device));
     auto* p = const_cast<srhip_program*>(prog);
     if (ds->dtype == SRHIP_F32) return eval_grad_tree_array_impl<float>(ds, p, out_value, out_grad, out_ok);
     return eval_grad_tree_array_impl<double>(ds, p, out_value, out_grad, out_ok);

@@ -42,9 +42,12 @@ struct Unsupported <: Exception
 end
 
 last_error() = unsafe_string(ccall((:srhip_last_error, libsrhip), Cstring, ()))
+const SRHIP_ERR_INVALID = Int32(-1)
 function check(rc::Int32)
     rc == SRHIP_OK && return nothing
     rc == SRHIP_ERR_UNSUPPORTED && throw(Unsupported(last_error()))
+    # malformed input, e.g. a program and a dataset on different devices
+    rc == SRHIP_ERR_INVALID && throw(ArgumentError("srhip: $(last_error())"))
     error("srhip: $(last_error())")
 end
 
@@ -67,7 +70,13 @@ loss_code(l::PeriodicLoss) = (LOSS_PERIODIC, 2π / Float64(l.k))
 loss_code(::LogitDistLoss) = (LOSS_LOGITDIST, 0.0)
 loss_code(l) = throw(Unsupported("elementwise loss $(typeof(l)) is not in the engine's table"))
 
-# ---- contexts: one per (thread, device); calls through a context are serialised
+# ---- contexts: one per (thread, device); calls through a context are serialised.
+# An evaluation runs on its PROGRAM's context (srhip.h): programs are created
+# in the calling thread's context, datasets are uploaded once per device and
+# shared by every thread's context, so threads (one island each,
+# src/SearchUtils.jl:33-45) score concurrently. A task that migrates between
+# threads keeps using the context its program was created in, which is safe
+# (the context's mutex serialises it with that thread's calls).
 const CTX = Dict{Tuple{Int,Int},Ptr{Cvoid}}()
 const CTX_LOCK = ReentrantLock()
 function context(device::Int=0)
@@ -158,6 +167,7 @@ mutable struct Program
     h::Ptr{Cvoid}
     ntrees::Int
     const_off::Vector{Int32}
+    device::Int   # its datasets are this device's (srhip.h: a call runs on the program's context)
 end
 function destroy(p::Program)
     p.h == C_NULL && return nothing
@@ -175,7 +185,7 @@ function Program(trees::AbstractVector{Node{T}}, options::Options, device::Int=0
                     (Ptr{Cvoid}, Int32, Ref{SrhipTrees}, Ptr{Ptr{Cvoid}}),
                     context(device), dtype_code(T), tr, h))
     end
-    p = Program(h[], length(trees), const_off)
+    p = Program(h[], length(trees), const_off, device)
     finalizer(destroy, p)
     return p
 end
@@ -204,14 +214,17 @@ function upload(X::AbstractMatrix{T}, y::AbstractVector{T}, w, device::Int) wher
 end
 destroy_dataset(h::Ptr{Cvoid}) = ccall((:srhip_dataset_destroy, libsrhip), Int32, (Ptr{Cvoid},), h)
 
-# one device copy per Dataset (src/Dataset.jl:24-64), uploaded once; the table
-# is shared by all threads, so it is guarded by CTX_LOCK
-const DEVICE_DATASETS = IdDict{Any,Ptr{Cvoid}}()
+# one device copy per (Dataset, device) (src/Dataset.jl:24-64), uploaded once
+# and shared by the contexts of all threads; the table is guarded by CTX_LOCK
+const DEVICE_DATASETS = Dict{Tuple{UInt,Int},Tuple{Any,Ptr{Cvoid}}}()
 function device_dataset(dataset::Dataset{T}, device::Int=0) where {T}
     lock(CTX_LOCK) do
-        get!(DEVICE_DATASETS, dataset) do
-            upload(dataset.X, dataset.y, dataset.weighted ? dataset.weights : nothing, device)
-        end
+        key = (objectid(dataset), device)
+        entry = get(DEVICE_DATASETS, key, nothing)
+        (entry !== nothing && entry[1] === dataset) && return entry[2]
+        h = upload(dataset.X, dataset.y, dataset.weighted ? dataset.weights : nothing, device)
+        DEVICE_DATASETS[key] = (dataset, h)
+        return h
     end
 end
 
@@ -224,7 +237,7 @@ trees; T(Inf) where evaluation fails. `idx` (1-based, with repetition) is
 score_func_batch's row sample (src/LossFunctions.jl:95-115).
 """
 function eval_loss_batch(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, options::Options;
-                         idx=nothing) where {T}
+                         idx=nothing, device::Int=0) where {T}
     node_off, kind, arg, const_off, consts = flatten(trees, options)
     nt = length(trees)
     sums = Vector{Float64}(undef, nt); ok = Vector{UInt8}(undef, nt); wsum = Ref{Float64}(0)
@@ -234,10 +247,11 @@ function eval_loss_batch(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, op
     GC.@preserve node_off kind arg const_off consts sums ok params rows begin
         tr = Ref(SrhipTrees(Int32(nt), pointer(node_off), pointer(kind), pointer(arg), pointer(const_off),
                             Ptr{Cvoid}(pointer(consts))))
-        check(ccall((:srhip_eval_loss_batch, libsrhip), Int32,
-                    (Ptr{Cvoid}, Ref{SrhipTrees}, Int32, Ptr{Float64}, Ptr{Int64}, Int64, Ptr{Float64},
+        # the program lives in this thread's context, the dataset is shared
+        check(ccall((:srhip_eval_loss_batch_ctx, libsrhip), Int32,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{SrhipTrees}, Int32, Ptr{Float64}, Ptr{Int64}, Int64, Ptr{Float64},
                      Ref{Float64}, Ptr{UInt8}),
-                    device_dataset(dataset), tr, kindcode, params,
+                    context(device), device_dataset(dataset, device), tr, kindcode, params,
                     idx === nothing ? Ptr{Int64}(C_NULL) : pointer(rows), length(rows), sums, wsum, ok))
     end
     return [ok[i] == 1 ? T(sums[i] / wsum[]) : T(Inf) for i in 1:nt]
@@ -261,7 +275,7 @@ function eval_loss_grad_batch(p::Program, dataset::Dataset{T}, options::Options)
         check(ccall((:srhip_eval_loss_grad, libsrhip), Int32,
                     (Ptr{Cvoid}, Ptr{Cvoid}, Int32, Ptr{Float64}, Ptr{Float64}, Ptr{Float64}, Ref{Float64},
                      Ptr{UInt8}),
-                    device_dataset(dataset), p.h, kindcode, params, sums, dloss, wsum, ok))
+                    device_dataset(dataset, p.device), p.h, kindcode, params, sums, dloss, wsum, ok))
     end
     losses = [ok[i] == 1 ? T(sums[i] / wsum[]) : T(Inf) for i in 1:nt]
     grads = [dloss[(p.const_off[i] + 1):p.const_off[i + 1]] ./ wsum[] for i in 1:nt]

@@ -111,7 +111,7 @@ def test_every_ccall_matches_the_header():
         else:
             assert ret == "Int32" and cret == "int32_t", f"{name}: returns {ret} / {cret}"
     # the entry points the shim of INTEGRATION.md §3 needs are all bound
-    for need in ("srhip_eval_loss_batch", "srhip_eval_tree_array", "srhip_eval_grad_tree_array",
+    for need in ("srhip_eval_loss_batch_ctx", "srhip_eval_tree_array", "srhip_eval_grad_tree_array",
                  "srhip_eval_loss_grad", "srhip_program_create", "srhip_program_set_constants",
                  "srhip_dataset_create", "srhip_op_lookup", "srhip_open", "srhip_device_count"):
         assert need in seen, need
@@ -155,8 +155,17 @@ def test_binding_exposes_the_shim_api():
     for fn in ("enabled", "eval_loss_batch", "eval_tree_array", "eval_grad_tree_array", "eval_loss_grad_batch",
                "set_constants!", "flatten"):
         assert re.search(rf"^function {re.escape(fn)}\(|^{re.escape(fn)}\(.*\) =", src, re.M), fn
-    # the shared device-dataset table is only touched under the lock
-    assert re.search(r"lock\(CTX_LOCK\) do\s+get!\(DEVICE_DATASETS", src)
+    # the shared device-dataset table is only touched under the lock, keyed by
+    # (dataset, device); batch scoring creates its program in the calling
+    # thread's context (srhip_eval_loss_batch_ctx), so threads run concurrently
+    # on one shared dataset
+    body = re.search(r"function device_dataset\(.*?\nend", src, re.S).group(0)
+    assert re.search(r"lock\(CTX_LOCK\) do", body) and "DEVICE_DATASETS[key]" in body and "device)" in body
+    ev = re.search(r"function eval_loss_batch\(.*?\nend", src, re.S).group(0)
+    assert "srhip_eval_loss_batch_ctx" in ev and "context(device)" in ev
+    grad = re.search(r"function eval_loss_grad_batch\(.*?\nend", src, re.S).group(0)
+    assert "device_dataset(dataset, p.device)" in grad
+    assert re.search(r"rc == SRHIP_ERR_INVALID && throw\(ArgumentError", src)
 
 
 BATCHED = ROOT / "symbolicregression.jl_amd" / "julia" / "BatchedCallers.jl"
