@@ -117,6 +117,10 @@ struct Proposal{T}
     member::Union{PopMember{T},Nothing}
     accepted::Bool
     num_evals::Float64
+    # beforeScore / beforeLoss (src/Mutate.jl:41-47): the parent's own, or with
+    # options.batching its re-score on a fresh minibatch
+    before_score::T
+    before_loss::T
 end
 
 # the tree-producing mutations of next_generation (src/Mutate.jl:79-115,132-139),
@@ -133,13 +137,16 @@ function mutate_tree(choice::Symbol, tree::Node{T}, temperature, curmaxsize::Int
     error("Unknown mutation choice: $choice")
 end
 
-"""Everything of next_generation before score_func (src/Mutate.jl:26-193)."""
-function propose(dataset::Dataset{T}, member::PopMember{T}, temperature, curmaxsize::Int,
-                 options::Options) where {T}
+"""Everything of next_generation before score_func (src/Mutate.jl:26-193);
+`before` = (beforeScore, beforeLoss), already re-scored on a minibatch by the
+caller when options.batching (:41-47)."""
+function propose(dataset::Dataset{T}, member::PopMember{T}, before::Tuple{T,T}, temperature,
+                 curmaxsize::Int, options::Options) where {T}
     prev = member.tree
+    bs, bl = before
     keep(tree, accepted, evals=0.0) = Proposal{T}(member, nothing,
-        PopMember(tree, member.score, member.loss; parent=member.ref, deterministic=options.deterministic),
-        accepted, evals)
+        PopMember(tree, bs, bl; parent=member.ref, deterministic=options.deterministic),
+        accepted, evals, bs, bl)
     weights = copy(options.mutation_weights)
     weights.mutate_constant *= min(8, count_constants(prev)) / 8.0
     if compute_complexity(prev, options) >= curmaxsize || count_depth(prev) >= options.maxdepth
@@ -152,14 +159,15 @@ function propose(dataset::Dataset{T}, member::PopMember{T}, temperature, curmaxs
         return keep(combine_operators(simplify_tree(copy_node(prev), options.operators), options.operators), true)
     end
     if choice == :optimize
-        m, evals = optimize_constants(dataset, PopMember(copy_node(prev), member.score, member.loss;
+        m, evals = optimize_constants(dataset, PopMember(copy_node(prev), bs, bl;
                                                          parent=member.ref, deterministic=options.deterministic),
                                       options)
-        return Proposal{T}(member, nothing, m, true, evals)
+        return Proposal{T}(member, nothing, m, true, evals, bs, bl)
     end
     for _ in 1:10  # max_attempts
         tree = mutate_tree(choice, copy_node(prev), temperature, curmaxsize, options, dataset.nfeatures)
-        check_constraints(tree, options, curmaxsize) && return Proposal{T}(member, tree, nothing, false, 0.0)
+        check_constraints(tree, options, curmaxsize) &&
+            return Proposal{T}(member, tree, nothing, false, 0.0, bs, bl)
     end
     return keep(copy_node(prev), false)  # failed constraint check: rejected
 end
@@ -168,12 +176,12 @@ end
 function accept(p::Proposal{T}, score::T, loss::T, temperature, stats::RunningSearchStatistics,
                 options::Options) where {T}
     member = p.parent
-    reject() = (PopMember(copy_node(member.tree), member.score, member.loss; parent=member.ref,
+    reject() = (PopMember(copy_node(member.tree), p.before_score, p.before_loss; parent=member.ref,
                           deterministic=options.deterministic), false)
     isnan(score) && return reject()
     prob = 1.0
     if options.annealing
-        prob *= exp(-(score - member.score) / (temperature * options.alpha))
+        prob *= exp(-(score - p.before_score) / (temperature * options.alpha))
     end
     if options.use_frequency
         freq(c) = 0 < c <= options.maxsize ? stats.normalized_frequencies[c] : 1e-6
@@ -198,22 +206,41 @@ function reg_evol_cycle_batched(dataset::Dataset{T}, pops::AbstractVector{<:Popu
                                 curmaxsize::Int, stats::AbstractVector{RunningSearchStatistics},
                                 options::Options) where {T}
     proposals = Vector{Vector{Proposal{T}}}(undef, length(pops))
+    allstars = Vector{Vector{PopMember{T}}}(undef, length(pops))
     for (k, pop) in enumerate(pops)
         shuffle!(pop.members)
         ncyc = round(Int, pop.n / options.tournament_selection_n)
-        props = Vector{Proposal{T}}(undef, ncyc)
-        Threads.@threads for i in 1:ncyc
-            sub = (1 + (i - 1) * options.tournament_selection_n):(i * options.tournament_selection_n)
-            allstar = pop.members[sub[argmin([pop.members[j].score for j in sub])]]
-            props[i] = propose(dataset, allstar, temperature, curmaxsize, options)
+        allstars[k] = [begin
+                           sub = (1 + (i - 1) * options.tournament_selection_n):(i * options.tournament_selection_n)
+                           pop.members[sub[argmin([pop.members[j].score for j in sub])]]
+                       end for i in 1:ncyc]
+    end
+    # with options.batching, every next_generation first re-scores its parent
+    # on a minibatch (src/Mutate.jl:41-47): one launch for all islands' parents
+    parents = PopMember{T}[m for as in allstars for m in as]
+    num_evals = 0.0
+    before = if options.batching
+        ps, pl = score_batch_minibatch(dataset, Node{T}[m.tree for m in parents], options)
+        num_evals += length(parents) * (options.batch_size / dataset.n)
+        collect(zip(ps, pl))
+    else
+        [(m.score, m.loss) for m in parents]
+    end
+    q = 0
+    for (k, as) in enumerate(allstars)
+        props = Vector{Proposal{T}}(undef, length(as))
+        off = q
+        Threads.@threads for i in eachindex(as)
+            props[i] = propose(dataset, as[i], before[off + i], temperature, curmaxsize, options)
         end
+        q += length(as)
         proposals[k] = props
     end
     # one launch for every island's babies
     trees = Node{T}[p.tree for props in proposals for p in props if p.member === nothing]
     scores, losses = options.batching ? score_batch_minibatch(dataset, trees, options) :
                      score_batch(dataset, trees, options)
-    num_evals = length(trees) * (options.batching ? options.batch_size / dataset.n : 1.0)
+    num_evals += length(trees) * (options.batching ? options.batch_size / dataset.n : 1.0)
     j = 0
     for (k, pop) in enumerate(pops)
         for p in proposals[k]
