@@ -248,9 +248,11 @@ int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog,
 int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nfast,
                                int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load);
 /* How srhip_program_set_constants applied new constants so far: in place
- * (the device programs' immediates overwritten, same buffers) or by a full
- * rebuild (folding or a static verdict changed, or the first new constant set
- * of a tree-code program, which runs interpreted from then on). */
+ * (the device programs' immediates overwritten, same buffers; tree code built
+ * with its constants in memory reads them from there) or by a full rebuild
+ * (folding or a static verdict changed, or the first new constant set of a
+ * tree-code program whose constants were compiled into its code: rebuilt once
+ * as memory-constant tree code). */
 int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inplace, int64_t* out_rebuilt);
 /* Gradient tree code of this program (reverse-mode ∂L/∂c for
  * srhip_eval_loss_grad with the L2 loss, built on the first gradient call):
@@ -265,7 +267,8 @@ int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntre
  * guard fired or the tile failed; out_redone may be NULL). */
 int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* out_redone);
 /* Testing hook (no device needed): compile Float32 trees with the tree
- * compiler. Returns the code bytes, their assembly text ('\n'-separated lines)
+ * compiler (fast: bit 0 the guarded FAST path, bit 1 memory-constant code).
+ * Returns the code bytes, their assembly text ('\n'-separated lines)
  * and, per compiled tree, (tree id, byte offset). Each inout_n* holds the
  * capacity on entry and the size on return; SRHIP_ERR_INVALID if too small. */
 int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_bytes, int64_t* inout_nbytes,

@@ -117,7 +117,7 @@ struct srhip_ctx {
   int last_launches = 0;
   int last_bailed = 0;  // trees re-evaluated after their tree code handed a tile back
   int64_t last_redone = 0;  // tiles tree code redid with the PRECISE routines
-  DevBuf partial, sums, oks, dloss, scratch_idx, gather;
+  DevBuf partial, sums, oks, dloss, scratch_idx, gather, derived;
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
   DevBuf ti_rec;  // threaded-interpreter records of the shallow f32 list
   DevBuf bail_list, bail_fail;  // trees whose tree code handed a tile back, and their flags
@@ -166,10 +166,14 @@ struct srhip_program {
   // tree code is compiled for one constant set: a program whose constants are
   // set again (srhip_program_set_constants) runs on the interpreter
   bool jit_allowed = true;
+  // tree code reads its constants from the device programs (jit::Options::memc):
+  // built at the first new constant set, after which set_constants only
+  // updates the programs in place
+  bool jit_memc = false;
   // host image of the uploaded programs: set_constants patches the device
   // copies in place when only instruction immediates change
   std::vector<unsigned char> h_code, h_gcode;
-  std::vector<int32_t> h_toff, h_gtoff;
+  std::vector<int32_t> h_toff, h_gtoff, h_len, h_glen;
   int64_t n_inplace = 0, n_rebuild = 0;
   int opset = OPSET_FULL;      // smallest operator set covering the compiled programs
   // gradient programs (compiled on first use)
@@ -320,6 +324,40 @@ void free_program_device(srhip_program* p) {
 template <typename T>
 bool same_shape(const std::vector<Ins<T>>& code, const std::vector<unsigned char>& old);
 
+// New constants that make a tree fail statically (a non-finite constant or
+// folded value) leave it without code of its own: it keeps its previous code
+// segment, so that the program layout stays the same and the update stays in
+// place (the static verdict decides the tree's result; the device evaluates
+// its stale code for nothing). Returns true when cb was rewritten.
+template <typename T>
+bool keep_layout(CompiledBatch<T>& cb, const std::vector<unsigned char>& h_code, const std::vector<int32_t>& h_toff,
+                 const std::vector<int32_t>& h_len) {
+  const int nt = cb.ntrees;
+  if ((int)h_toff.size() != nt || (int)h_len.size() != nt) return false;
+  bool kept = false;
+  for (int t = 0; t < nt; ++t)
+    if (cb.tree_off[t] < 0 && h_toff[t] >= 0) kept = true;
+  if (!kept) return false;
+  const Ins<T>* old = reinterpret_cast<const Ins<T>*>(h_code.data());
+  std::vector<Ins<T>> code;
+  code.reserve(h_code.size() / sizeof(Ins<T>));
+  std::vector<int32_t> toff(nt, -1), len(nt, 0);
+  for (int t = 0; t < nt; ++t) {
+    const Ins<T>* src = cb.tree_off[t] >= 0 ? &cb.code[cb.tree_off[t]] : h_toff[t] >= 0 ? old + h_toff[t] : nullptr;
+    if (!src) continue;
+    const int n = cb.tree_off[t] >= 0 ? cb.len[t] : h_len[t];
+    toff[t] = (int32_t)code.size();
+    len[t] = n;
+    code.insert(code.end(), src, src + n);
+  }
+  // the trailing OP_ENDs of compile_batch
+  code.insert(code.end(), cb.code.end() - (kVProgMax + 1), cb.code.end());
+  cb.code.swap(code);
+  cb.tree_off.swap(toff);
+  cb.len.swap(len);
+  return true;
+}
+
 // New constants for built gradient programs: immediates patched in place when
 // the programs keep their shape, else a rebuild. Deferred from set_constants
 // to the next gradient call (a line search sets constants many times between
@@ -335,7 +373,13 @@ void patch_grad_constants(srhip_program* p) {
   tr.const_off = p->const_off.data();
   tr.consts = p->consts.data();
   CompiledBatch<T> gb = compile_batch<T>(tr, /*grad=*/true);
-  if (same_shape(gb.code, p->h_gcode) && gb.tree_off == p->h_gtoff && gb.static_fail == p->g_static_fail) {
+  keep_layout(gb, p->h_gcode, p->h_gtoff, p->h_glen);
+  // static verdicts may change in place: a newly failing tree keeps its old code (keep_layout)
+  bool verdicts_ok = true;
+  for (int t = 0; t < p->ntrees && verdicts_ok; ++t)
+    if (!gb.static_fail[t] && p->g_static_fail[t]) verdicts_ok = false;  // a tree without code needs some now
+  if (same_shape(gb.code, p->h_gcode) && gb.tree_off == p->h_gtoff && verdicts_ok) {
+    p->g_static_fail = gb.static_fail;
     hipStream_t s = p->ctx->stream;
     HIP_CHECK(hipStreamSynchronize(s));
     p->h_gcode.assign(reinterpret_cast<const unsigned char*>(gb.code.data()),
@@ -445,6 +489,7 @@ void build_grad_program(srhip_program* p) {
   p->h_gcode.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
                     reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   p->h_gtoff = cb.tree_off;
+  p->h_glen = cb.len;
   p->grad_built = true;
   p->grad_stale = false;
 }
@@ -542,6 +587,8 @@ void build_program(srhip_program* p) {
       std::vector<int32_t> jl, rest;
       jit::Options jo;
       jo.fast = jit_fast_enabled();
+      const char* me = std::getenv("SRHIP_JIT_MEMC");  // read per build: tests
+      jo.memc = p->jit_memc || (me && me[0] == '1');
       p->jit = jit::build(cb, a, jl, rest, jo, &p->jit_stats);
       if (p->jit) {
         p->nlist_j = (int)jl.size();
@@ -581,6 +628,7 @@ void build_program(srhip_program* p) {
   p->h_code.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
                    reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   p->h_toff = cb.tree_off;
+  p->h_len = cb.len;
 }
 
 // Same instruction streams (opcodes, operands, offsets, static verdicts) up to
@@ -599,8 +647,11 @@ bool same_shape(const std::vector<Ins<T>>& code, const std::vector<unsigned char
 // no list rebuild, gradient programs patched too); else rebuild.
 template <typename T>
 void update_constants(srhip_program* p) {
-  if (p->jit) {  // first new constant set of a tree-code program: interpreter from now on
-    p->jit_allowed = false;
+  if (p->jit && !p->jit_memc && !jit::memc(p->jit)) {
+    // first new constant set of a tree-code program with constants in its
+    // code: rebuilt once as memory-constant tree code (jit.cpp Gen::memc),
+    // which later constant sets reach through the in-place program update
+    p->jit_memc = true;
     ++p->n_rebuild;
     const bool had_grad = p->grad_built;
     build_program<T>(p);
@@ -610,7 +661,7 @@ void update_constants(srhip_program* p) {
     }
     return;
   }
-  p->jit_allowed = false;
+  if (!p->jit) p->jit_allowed = false;
   srhip_trees tr;
   tr.ntrees = p->ntrees;
   tr.node_off = p->node_off.data();
@@ -619,12 +670,15 @@ void update_constants(srhip_program* p) {
   tr.const_off = p->const_off.data();
   tr.consts = p->consts.data();
   CompiledBatch<T> cb = compile_batch<T>(tr);
-  if (!same_shape(cb.code, p->h_code) || cb.tree_off != p->h_toff || cb.static_fail != p->static_fail ||
-      cb.fail_if_rows != p->fail_if_rows) {
+  keep_layout(cb, p->h_code, p->h_toff, p->h_len);
+  if (!same_shape(cb.code, p->h_code) || cb.tree_off != p->h_toff) {
     ++p->n_rebuild;
     build_program<T>(p);
     return;
   }
+  // same layout: the static verdicts (host side) may change with it
+  p->static_fail = cb.static_fail;
+  p->fail_if_rows = cb.fail_if_rows;
   hipStream_t s = p->ctx->stream;
   HIP_CHECK(hipStreamSynchronize(s));  // no launch may still read the old programs / host images
   p->h_code.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
@@ -798,13 +852,21 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     }
     EvalPlan plan;
     if (pass == -1) {
-      const int narr = 1 + nfeat + (w ? 1 : 0);
+      // LDS columns: y, the raw features the tree code reads, its derived columns, w
+      const jit::Columns& jc = jit::columns(p->jit);
+      if (jc.nraw > nfeat) throw Error(SRHIP_ERR_INVALID, "dataset has fewer features than the program reads");
+      const int narr = 1 + jc.nraw + jc.nder + (w ? 1 : 0);
       // partials go to global memory: LDS holds the tiles (1 byte per slot keeps the slot bound away)
-      // 16384 workgroups, >= 64 trees per group (16 per wave): config #2 kernel
+      // 16384 workgroups of 4 waves, >= 64 trees per group (16 per wave): config #2 kernel
       // 2.997 -> 2.867 ms at 4096 trees, 0.865 -> 0.828 at 1024, 512 unchanged
-      // (tools/gpu_targetwg.sh, profiles/r02n_targetwg.txt)
-      if (!plan_geometry(4, 4, kShallowSlots, narr, 1, rows, nlist, &plan, jit_tile_budget(), 52 * 1024, 16384, 64))
+      // (profiles/r02n_targetwg.txt); scaled by the waves per workgroup
+      const int jw = jit::waves();
+      const size_t budget = std::max(jit_tile_budget() * jw / 4, jit::lds_per_workgroup() -
+                                     (jit::part_global() ? 0 : std::min<size_t>(jit::lds_per_workgroup() / 4, 8192)));
+      if (!plan_geometry(4, 4, kShallowSlots, narr, 1, rows, nlist, &plan, budget, 52 * 1024 * jw / 4,
+                         16384 * 4 / jw, 64 * jw / 4))
         throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
+      plan.threads = 64 * jw;
     } else if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan)) {
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
     }
@@ -844,8 +906,18 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.out_stride = out_stride;
     const int tk = timed_begin(c, s);
     if (pass == -1) {
-      if constexpr (std::is_same<T, float>::value)
-        HIP_CHECK(jit::launch(p->jit, launches[li].part, plan, a, jit_fast_enabled(), s));
+      if constexpr (std::is_same<T, float>::value) {
+        // the derived columns of this call, once per row, before the first part
+        const jit::Columns& jc = jit::columns(p->jit);
+        static const bool precompute = [] { const char* e = std::getenv("SRHIP_JIT_DERIVE_PRE"); return !(e && e[0] == '0'); }();
+        const float* dcols = nullptr;
+        if (jc.nder > 0 && precompute) {
+          c->derived.ensure((size_t)jc.nder * (size_t)n_pad * sizeof(float));
+          if (launches[li].part == 0) HIP_CHECK(jit::launch_derive(p->jit, X, n_pad, static_cast<float*>(c->derived.p), s));
+          dcols = static_cast<const float*>(c->derived.p);
+        }
+        HIP_CHECK(jit::launch(p->jit, launches[li].part, plan, a, jit_fast_enabled(), dcols, s));
+      }
     } else {
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
@@ -1691,7 +1763,8 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
       for (int t = 0; t < cb.ntrees; ++t)
         if (cb.tree_off[t] >= 0 && cb.need[t] <= kShallowSlots) cand.push_back(t);
       jit::Options jo;
-      jo.fast = mode != 0;
+      jo.fast = mode == 1 || mode == 4;
+      jo.memc = mode == 3 || mode == 4;
       jo.text = true;
       jit::compile_only(cb, cand, jo, &bytes, &text, &offs, nullptr);
     }
@@ -1716,7 +1789,9 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
 int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_bytes, int64_t* inout_nbytes,
                           char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
                           int64_t* inout_noffsets) {
-  return jit_compile_hook(trees, fast ? 1 : 0, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets,
+  // fast: bit 0 the FAST path, bit 1 memory-constant code (mode 3 / 4 below)
+  return jit_compile_hook(trees, (fast & 2) ? ((fast & 1) ? 4 : 3) : ((fast & 1) ? 1 : 0), out_bytes, inout_nbytes,
+                          out_text, inout_ntext, out_offsets,
                           inout_noffsets);
 }
 

@@ -300,8 +300,10 @@ def manual_exp():
     (round to nearest even, |t| < 2^22), and 2^f * 2^n is a normal number,
     i.e. its bits are those of 2^f plus n << 23 — the low bits of
     t + 1.5*2^23 shifted left by 23. Two rows per v_pk_*_f32 instruction.
-    The input is marked (chk) as in the compiled body: (x0, x1)*0 + (x2, x3)
-    is finite iff the four rows are."""
+    The input is not marked: an infinite x fires the exp guard (the tile is
+    redone with the PRECISE body, which marks it) and a NaN x gives a NaN
+    result (canonical NaNs: n << 23 adds nothing), which the marks downstream
+    see."""
     return ["s_mov_b32 s2, 0x3fb8aa3b",            # log2(e)
             "s_mov_b32 s4, 0x4b400000",            # 1.5 * 2^23
             "v_pk_mul_f32 v[0:1], v[32:33], s[2:3] op_sel_hi:[1,0]",   # t = x*log2e
@@ -319,9 +321,9 @@ def manual_exp():
             "v_exp_f32_e32 v9, v9",
             "v_exp_f32_e32 v10, v10",
             "v_exp_f32_e32 v11, v11",
-            "v_pk_fma_f32 v[12:13], v[32:33], 0, v[34:35] op_sel_hi:[1,0,1]",
-            "v_fmac_f32_e32 v40, 0, v12",
-            "v_fmac_f32_e32 v40, 0, v13",
+            # measured: the v_exp_f32 results are read too early with fewer
+            # than 3 independent instructions between (wrong rows on MI355X)
+            "s_nop 2",
             "v_lshl_add_u32 v32, v4, 23, v8",
             "v_lshl_add_u32 v33, v5, 23, v9",
             "v_lshl_add_u32 v34, v6, 23, v10",
@@ -335,9 +337,10 @@ def manual_div(rg):
     plain fma and v_div_fixup_f32 returns its input, so hipcc's IEEE sequence
     reduces to rcp, e = 1 - b*r, r += e*r, q = a*r, e = a - b*q, q += e*r,
     e = a - b*q, q += e*r — the same roundings, here two rows per v_pk_*_f32
-    instruction. b is marked as in the compiled body. Rows out of the range
-    (0, Inf, NaN, extreme exponents) send all four to the compiled routine
-    (b_div_full)."""
+    instruction. Rows out of the range (0, Inf, extreme exponents) send all
+    four to the compiled routine (b_div_full), which marks b; so b needs no
+    mark here: an infinite b (whose quotient would lose it) never takes
+    this path, and a NaN b gives a NaN quotient."""
     neg0 = " neg_lo:[1,0,0] neg_hi:[1,0,0]"
     return ["v_max3_f32 v0, |v32|, |v33|, |v34|",
             "v_min3_f32 v1, |v32|, |v33|, |v34|",
@@ -368,11 +371,8 @@ def manual_div(rg):
             "v_pk_fma_f32 v[8:9], v[38:39], v[12:13], v[34:35]" + neg0,
             "v_pk_fma_f32 v[10:11], v[6:7], v[2:3], v[10:11]",
             "v_pk_fma_f32 v[12:13], v[8:9], v[4:5], v[12:13]",
-            "v_pk_fma_f32 v[14:15], v[36:37], 0, v[38:39] op_sel_hi:[1,0,1]",
             "v_pk_fma_f32 v[6:7], v[36:37], v[10:11], v[32:33]" + neg0,
             "v_pk_fma_f32 v[8:9], v[38:39], v[12:13], v[34:35]" + neg0,
-            "v_fmac_f32_e32 v40, 0, v14",
-            "v_fmac_f32_e32 v40, 0, v15",
             "v_pk_fma_f32 v[32:33], v[6:7], v[2:3], v[10:11]",
             "v_pk_fma_f32 v[34:35], v[8:9], v[4:5], v[12:13]"]
 
@@ -381,7 +381,8 @@ def manual_div_lc(rg):
     """c / a for the constant c in s_k (the odd half of an SGPR pair, so the
     packed instructions pick it with op_sel) and the 4 rows of A: manual_div's
     sequence with c as the numerator, under the same range condition on c and
-    every |a|; otherwise the compiled routine (b_div_lc_full)."""
+    every |a|; otherwise the compiled routine (b_div_lc_full), which marks
+    a (here unmarked, as b in manual_div)."""
     k = rg.S["k"]
     assert k % 2 == 1
     cp = f"s[{k - 1}:{k}]"
@@ -411,11 +412,8 @@ def manual_div_lc(rg):
             f"v_pk_fma_f32 v[8:9], v[34:35], v[12:13], {cp} op_sel:[0,0,1]" + neg0,
             "v_pk_fma_f32 v[10:11], v[6:7], v[2:3], v[10:11]",
             "v_pk_fma_f32 v[12:13], v[8:9], v[4:5], v[12:13]",
-            "v_pk_fma_f32 v[14:15], v[32:33], 0, v[34:35] op_sel_hi:[1,0,1]",
             f"v_pk_fma_f32 v[6:7], v[32:33], v[10:11], {cp} op_sel:[0,0,1]" + neg0,
             f"v_pk_fma_f32 v[8:9], v[34:35], v[12:13], {cp} op_sel:[0,0,1]" + neg0,
-            "v_fmac_f32_e32 v40, 0, v14",
-            "v_fmac_f32_e32 v40, 0, v15",
             "v_pk_fma_f32 v[32:33], v[6:7], v[2:3], v[10:11]",
             "v_pk_fma_f32 v[34:35], v[8:9], v[4:5], v[12:13]"]
 
@@ -579,6 +577,8 @@ def build(hipcc, outdir, R):
         f.write("#define SR_JIT_ROUTINE_BODY_BYTES {" + ", ".join(str(fs[n] - 4) for n in names) + "}\n")
         f.write("#define SR_JIT_CLOBBERS " + ", ".join([f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s]
                                                           + ['"vcc"', '"scc"', '"m0"']) + "\n")
+        # memory-constant tree code (jit.cpp Gen::memc): its constants in s24..s39
+        f.write("#define SR_JIT_CLOBBERS_MEMC SR_JIT_CLOBBERS, " + ", ".join(f'"s{r}"' for r in range(24, 40)) + "\n")
         # gradient tree code (jit_grad.cpp): the same routines, a larger value
         # pool, per-constant accumulators, constants in SGPRs
         g = dict(GPOOL0=56, GNPOOL=20, GACC=136, NGACC=16, SC0=24, SCPTR=78, SGPTR=84)

@@ -60,6 +60,8 @@ struct Opnd {
   int k = O_VAL;
   int v = -1;        // value id (O_VAL) or feature (O_X)
   uint32_t c = 0;    // constant bits (O_C)
+  int pc = -1;       // O_C: the program instruction whose immediate holds it (memory-constant code)
+  bool der = false;  // O_X: a derived column (v is its column, not a dataset feature)
 };
 struct IrOp {
   bool un = false;
@@ -88,8 +90,27 @@ uint32_t fbits(float f) {
   return u;
 }
 
-// Program (compile.cpp) → IR: the accumulator machine with register renaming.
-bool build_ir(const Ins<float>* p, std::vector<IrOp>& ops, Opnd& root) {
+// Derived columns of a build (jit.h Columns): the column of u(x_f), -1 when
+// u(x_f) is not derived
+struct DerivedMap {
+  const Columns* cols = nullptr;
+  int col(int op, int f) const {
+    if (!cols) return -1;
+    const uint32_t key = ((uint32_t)op << 16) | (uint32_t)f;
+    for (int k = 0; k < cols->nder; ++k)
+      if (cols->der[k] == key) return cols->nraw + k;
+    return -1;
+  }
+};
+
+// operators that tree code runs as routines (the derivable ones)
+bool is_routine_uop(int op) {
+  return !(op == SRHIP_UOP_NEG || op == SRHIP_UOP_ABS || op == SRHIP_UOP_SQUARE || op == SRHIP_UOP_CUBE);
+}
+
+// Program (compile.cpp) → IR: the accumulator machine with register renaming;
+// u(x_f) of a derived column becomes a read of that column.
+bool build_ir(const Ins<float>* p, std::vector<IrOp>& ops, Opnd& root, const DerivedMap* dm = nullptr) {
   ops.clear();
   Opnd acc, tmp, slot[kMaxSlots];
   for (int pc = 0;; ++pc) {
@@ -99,7 +120,7 @@ bool build_ir(const Ins<float>* p, std::vector<IrOp>& ops, Opnd& root) {
     const int f = (int)(code >> 16);
     const float imm = p[pc].imm;
     auto X = [&](int ff) { Opnd o; o.k = O_X; o.v = ff; return o; };
-    auto C = [&](float c) { Opnd o; o.k = O_C; o.c = fbits(c); return o; };
+    auto C = [&](float c) { Opnd o; o.k = O_C; o.c = fbits(c); o.pc = pc; return o; };
     auto val = [&](IrOp o) {
       ops.push_back(o);
       Opnd r; r.k = O_VAL; r.v = (int)ops.size() - 1;
@@ -111,6 +132,10 @@ bool build_ir(const Ins<float>* p, std::vector<IrOp>& ops, Opnd& root) {
     if (opc >= OP_PUSH0 && opc < OP_PUSH0 + kMaxSlots) { slot[opc - OP_PUSH0] = acc; continue; }
     if (opc >= OP_POP0 && opc < OP_POP0 + kMaxSlots) { tmp = slot[opc - OP_POP0]; continue; }
     if (opc >= OP_UN0 && opc < OP_BIN0) {
+      if (dm && acc.k == O_X && !acc.der) {
+        const int c = dm->col(opc - OP_UN0, acc.v);
+        if (c >= 0) { acc = X(c); acc.der = true; continue; }
+      }
       IrOp o; o.un = true; o.op = opc - OP_UN0; o.a = acc;
       if (acc.k != O_VAL && !(o.un && is_inline(o) && acc.k == O_X)) {
         // a unary operator on a leaf (only with constant folding off): keep it simple
@@ -191,6 +216,25 @@ struct Gen {
   // + - * (and square / cube, residuals, the root check) two rows per
   // instruction on v_pk_*_f32; block moves on v_pk_mov_b32
   bool packed = true, pkmov = true;
+  // memory-constant code (Options::memc): every constant operand is an SGPR
+  // s[SC0 + k], loaded in the prologue from the immediate of its program
+  // instruction (s[SPROG:SPROG+1] = the tree's program in device memory), so
+  // srhip_program_set_constants' in-place program update is all a new
+  // constant set needs
+  static constexpr int SC0 = 24, NSC = 16, SPROG = 56;
+  bool memc = false;
+  std::vector<int> cpcs;          // program instruction of constant slot k
+  int cslot(const Opnd& q) {
+    for (size_t k = 0; k < cpcs.size(); ++k)
+      if (cpcs[k] == q.pc) return (int)k;
+    cpcs.push_back(q.pc);
+    return (int)cpcs.size() - 1;
+  }
+  int creg(const Opnd& q) const {
+    for (size_t k = 0; k < cpcs.size(); ++k)
+      if (cpcs[k] == q.pc) return SC0 + (int)k;
+    throw Error(SRHIP_ERR_INVALID, "jit: constant without a slot");
+  }
   Gen(Asm& a, const Tmpl& t, uint64_t va, bool f) : as(a), T(t), base_va(va), fast_opt(f) {
     const char* e = std::getenv("SRHIP_JIT_INLINE");  // measured no faster: off by default
     inline_ok = e && e[0] == '1';
@@ -233,6 +277,17 @@ struct Gen {
         if (s && o.un) break;
         if (q.k == O_VAL) { ops[q.v].consumer = i; ops[q.v].cpos = s; }
       }
+    }
+    if (memc) {
+      cpcs.clear();
+      for (const IrOp& o : ops) {
+        if (o.a.k == O_C) cslot(o.a);
+        if (!o.un && o.b.k == O_C) cslot(o.b);
+      }
+      if (root.k == O_C) cslot(root);
+      for (const IrOp& o : ops)
+        if ((o.a.k == O_C && o.a.pc < 0) || (!o.un && o.b.k == O_C && o.b.pc < 0)) { why = "constant without a program slot"; return false; }
+      if ((int)cpcs.size() > NSC) { why = "more constants than memory-constant SGPRs"; return false; }
     }
     // FAST eligibility, taint, zero sensitivity
     bool elig = fast_opt, trans = false;
@@ -312,7 +367,7 @@ struct Gen {
 
   // ---- emission helpers ----
   Src opsrc(const Opnd& q, int e) const {
-    if (q.k == O_C) return K(q.c);
+    if (q.k == O_C) return memc ? S(creg(q)) : K(q.c);
     if (q.k == O_X) return V(VPOOL0 + R * xblk[q.v] + e);
     return V(reg_of_loc(loc[q.v]) + e);
   }
@@ -361,9 +416,16 @@ struct Gen {
   void pk_block(int opc, const char* nm, int d, const Src (&a)[R], const Src (&b)[R], bool negb) {
     pk_const(a[0]);
     pk_const(b[0]);
-    const int hi = 4 | (a[0].enc >= 256 ? 1 : 0) | (b[0].enc >= 256 ? 2 : 0);
-    for (int e = 0; e < R; e += 2)
-      as.vop3p(opc, nm, d + e, pks(a[e]), pks(b[e]), nullptr, 0, hi, negb ? 2 : 0, negb ? 2 : 0);
+    int hi = 4 | (a[0].enc >= 256 ? 1 : 0) | (b[0].enc >= 256 ? 2 : 0), lo = 0;
+    // a constant in an odd SGPR (memory-constant code): the aligned pair below it, high half to both lanes
+    auto odd = [&](const Src& x, int bit) {
+      if (x.enc < 102 && !x.lit && (x.enc & 1)) { lo |= bit; hi |= bit; return S(x.enc - 1); }
+      return pks(x);
+    };
+    for (int e = 0; e < R; e += 2) {
+      const Src pa = odd(a[e], 1), pb = odd(b[e], 2);
+      as.vop3p(opc, nm, d + e, pa, pb, nullptr, lo, hi, negb ? 2 : 0, negb ? 2 : 0);
+    }
   }
   // a call operand into block `dst` (A or B): features not preloaded (or all
   // of them with xdirect) are read from the LDS tile, other operands moved
@@ -511,12 +573,14 @@ struct Gen {
     if (vq >= 0 && lq == L_B) b_owner = -1;
     a_owner = -1;
     const uint32_t cb = kr ? o.b.c : o.a.c;
-    as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(cb), "s" + std::to_string(S_K));
+    if (memc) as.sop1(SOP1_MOV, "s_mov_b32", S_K, S(creg(kr ? o.b : o.a)), "s" + std::to_string(S_K));
+    else as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(cb), "s" + std::to_string(S_K));
     int rid = o.krid;
     float cf;
     std::memcpy(&cf, &cb, 4);
     const float ac = std::fabs(cf);
-    if (kr && o.op == SRHIP_BOP_DIV && div_rk() >= 0 && ac >= 0x1p-60f && ac <= 0x1p60f) {
+    // (memory-constant code: the constant may change, so no host reciprocal)
+    if (!memc && kr && o.op == SRHIP_BOP_DIV && div_rk() >= 0 && ac >= 0x1p-60f && ac <= 0x1p60f) {
       // the reciprocal-and-correction routine (IEEE exact for admitted a; gen_jit.py manual_div_rk)
       const volatile float one = 1.0f;
       const float y = one / cf;  // correctly rounded (SSE division, no contraction)
@@ -548,8 +612,11 @@ struct Gen {
                       ((!o.un && o.op == SRHIP_BOP_MUL) || (o.un && (o.op == SRHIP_UOP_SQUARE || o.op == SRHIP_UOP_CUBE)));
     if (gcan) {  // t = |a| + |b| before the operands are overwritten
       Src ka, kb;
-      if (o.a.k == O_C) { as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(o.a.c & 0x7fffffffu), "s" + std::to_string(S_K)); }
-      if (o.b.k == O_C) { as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(o.b.c & 0x7fffffffu), "s" + std::to_string(S_K)); }
+      for (const Opnd* q : {&o.a, &o.b}) {
+        if (q->k != O_C) continue;
+        if (memc) as.sop2(SOP2_AND_B32, "s_and_b32", S_K, S(creg(*q)), K(0x7fffffffu));
+        else as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(q->c & 0x7fffffffu), "s" + std::to_string(S_K));
+      }
       for (int e = 0; e < R; ++e) {
         ka = o.a.k == O_C ? S(S_K) : opsrc(o.a, e);
         kb = o.b.k == O_C ? S(S_K) : opsrc(o.b, e);
@@ -664,6 +731,15 @@ struct Gen {
     const uint32_t D = (uint32_t)T.delta;
     // ---- prologue
     as.sop1(SOP1_MOV, "s_mov_b32", S_STATUS, K(0), "s" + std::to_string(S_STATUS));
+    for (size_t k = 0; k < cpcs.size(); ++k) {  // memory-constant code: s_load_dword s[SC0+k], the immediate
+      const uint32_t off = (uint32_t)cpcs[k] * 8u + 4u;
+      as.put(0xc0020000u | ((uint32_t)(SC0 + k) << 6) | (uint32_t)(SPROG >> 1));
+      as.put(off);
+      if (as.want_text)
+        as.lines.push_back("s_load_dword s" + std::to_string(SC0 + k) + ", s[" + std::to_string(SPROG) + ":" +
+                           std::to_string(SPROG + 1) + "], " + hex32(off));
+    }
+    if (!cpcs.empty()) as.waitcnt_lgkm(0);
     if (g_can) as.sop1(SOP1_MOV, "s_mov_b32", S_EPS, K(0x38800000u), "s" + std::to_string(S_EPS));  // 2^-14
     if (has_call) set_base();
     if (fast) {
@@ -707,7 +783,7 @@ struct Gen {
     if (root.k == O_VAL) rreg = reg_of_loc(loc[root.v]);
     else if (root.k == O_X) { wait_for(root); rreg = VPOOL0 + R * xblk[root.v]; }
     else {
-      for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGT + e, K(root.c));
+      for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGT + e, memc ? S(creg(root)) : K(root.c));
       rreg = VGT;
     }
     if (packed && rreg != VGT) {
@@ -850,14 +926,15 @@ struct Gen {
 // One tree: returns false (nothing appended) when it cannot be compiled.
 static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool text, std::vector<uint32_t>& out,
                      std::vector<std::string>* lines, uint64_t area_va, int32_t* off, bool* is_fast,
-                     std::string* why) {
+                     std::string* why, const DerivedMap& dm, bool memc) {
   std::vector<IrOp> ir;
   Opnd root;
-  if (!build_ir(prog, ir, root)) { *why = "program not translatable"; return false; }
+  if (!build_ir(prog, ir, root, &dm)) { *why = "program not translatable"; return false; }
   const size_t start = (out.size() + 15) / 16 * 16;  // 64-byte aligned entries
   Asm as;
   as.want_text = text;
   Gen g(as, T, area_va + start * 4, fast_opt);
+  g.memc = memc;
   if (!g.emit_tree(ir, root)) { *why = g.why; return false; }
   g.emit_tail();
   as.finish();
@@ -879,11 +956,13 @@ static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool 
 // (8 MiB) is split into consecutive slot ranges, one launch each.
 struct ModulePart {
   hipModule_t mod = nullptr;
-  hipFunction_t fn = nullptr, fn_w = nullptr;
+  hipFunction_t fn = nullptr, fn_w = nullptr, fn_derive = nullptr;
   int32_t* d_off = nullptr;  // [nslots] code offsets
   int slot0 = 0, nslots = 0;
 };
 struct Module {
+  Columns cols;
+  bool memc = false;
   std::vector<ModulePart> parts;
   uint32_t* d_bail = nullptr;  // [nslots + 2]: bail flags of all slots, bail count, PRECISE redo count
   int nslots = 0;
@@ -903,7 +982,9 @@ const char* unavailable_reason() { return templates().why.c_str(); }
 static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, size_t from,
                       const Options& opt, std::vector<uint32_t>& words, std::vector<std::string>* lines,
                       std::vector<int32_t>& offs, std::vector<int32_t>& ok_trees, std::vector<int32_t>& rest,
-                      Stats* st, const Tmpl& T) {
+                      Stats* st, const Tmpl& T, const Columns& cols) {
+  DerivedMap dm;
+  dm.cols = &cols;
   for (size_t k = from; k < cand.size(); ++k) {
     const int32_t t = cand[k];
     int32_t off = -1;
@@ -912,7 +993,7 @@ static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>
     const size_t before = words.size();
     const size_t lbefore = lines ? lines->size() : 0;
     const bool okc = cb.tree_off[t] >= 0 &&
-                     gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, opt.text, words, lines, T.area_va, &off, &f, &why);
+                     gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, opt.text, words, lines, T.area_va, &off, &f, &why, dm, opt.memc);
     if (okc && words.size() * 4 > T.area_bytes) {  // area full: the next part takes it
       words.resize(before);
       if (lines) lines->resize(lbefore);
@@ -934,6 +1015,90 @@ static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>
   return cand.size();
 }
 
+// SRHIP_JIT_PART_GLOBAL=1 (experiments): per-tree partials always straight to global memory
+bool part_global() {
+  static const bool g = [] { const char* e = std::getenv("SRHIP_JIT_PART_GLOBAL"); return e && e[0] == '1'; }();
+  return g;
+}
+int waves() {
+  static const int w = [] {
+    const char* e = std::getenv("SRHIP_JIT_WAVES");
+    const int v = e ? std::atoi(e) : 4;
+    return v >= 1 && v <= 16 ? v : 4;
+  }();
+  return w;
+}
+// 94 VGPRs: 5 waves per SIMD, 20 per CU; the CU's 160 KiB shared by its workgroups
+size_t lds_per_workgroup() {
+  const int per_cu = std::max(1, 20 / waves());
+  return (size_t)160 * 1024 / (size_t)per_cu;
+}
+
+// The derived columns of a batch: every u(x_f) (u a routine operator) used by
+// at least SRHIP_JIT_DERIVE_MIN (default 4) trees' code, most used first, as
+// many as leave room for four row tiles in the workgroup's LDS; nraw = the
+// raw features still read after the substitution.
+static Columns plan_columns(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt) {
+  Columns c;
+  std::vector<IrOp> ir;
+  Opnd root;
+  struct Cnt { uint32_t key; int n; };
+  std::vector<Cnt> cnt;
+  static const int min_uses = [] { const char* e = std::getenv("SRHIP_JIT_DERIVE_MIN"); return e ? std::max(1, std::atoi(e)) : 4; }();
+  static const bool env_on = [] { const char* e = std::getenv("SRHIP_JIT_DERIVE"); return !(e && e[0] == '0'); }();
+  const bool on = opt.derive && env_on;
+  for (int32_t t : cand) {
+    if (cb.tree_off[t] < 0 || !build_ir(&cb.code[cb.tree_off[t]], ir, root)) continue;
+    for (const IrOp& o : ir) {
+      if (o.un && o.a.k == O_X && !o.a.der && is_routine_uop(o.op) && on) {
+        const uint32_t key = ((uint32_t)o.op << 16) | (uint32_t)o.a.v;
+        auto it = std::find_if(cnt.begin(), cnt.end(), [&](const Cnt& q) { return q.key == key; });
+        if (it == cnt.end()) cnt.push_back({key, 1}); else ++it->n;
+      }
+    }
+  }
+  std::stable_sort(cnt.begin(), cnt.end(), [](const Cnt& a, const Cnt& b) { return a.n > b.n; });
+  std::vector<uint32_t> chosen;
+  for (const Cnt& q : cnt)
+    if (q.n >= min_uses && (int)chosen.size() < kMaxDerived) chosen.push_back(q.key);
+  // raw features read after the substitution
+  auto raw_max = [&](const std::vector<uint32_t>& ch) {
+    Columns tmp;
+    tmp.nraw = 1 << 14;  // out of the feature range: no clash with raw features while scanning
+    tmp.nder = (int)ch.size();
+    for (size_t k = 0; k < ch.size(); ++k) tmp.der[k] = ch[k];
+    DerivedMap dm;
+    dm.cols = &tmp;
+    int m = -1;
+    for (int32_t t : cand) {
+      if (cb.tree_off[t] < 0 || !build_ir(&cb.code[cb.tree_off[t]], ir, root, &dm)) continue;
+      for (const IrOp& o : ir) {
+        if (o.a.k == O_X && !o.a.der) m = std::max(m, o.a.v);
+        if (!o.un && o.b.k == O_X && !o.b.der) m = std::max(m, o.b.v);
+      }
+      if (root.k == O_X && !root.der) m = std::max(m, root.v);
+    }
+    return m + 1;
+  };
+  // room: four tiles (SRHIP_JIT_DERIVE_TILES) of (y, raw, derived) in the
+  // workgroup's LDS, less the partials' share
+  static const int dtiles = [] { const char* e = std::getenv("SRHIP_JIT_DERIVE_TILES"); return e ? std::max(1, std::atoi(e)) : 4; }();
+  const size_t tile_bytes = (size_t)dtiles * (size_t)(64 * SR_JIT_R) * sizeof(float);
+  const size_t budget = lds_per_workgroup() - (part_global() ? 0 : std::min<size_t>(lds_per_workgroup() / 8, 4096));
+  while (true) {
+    const int nraw = raw_max(chosen);
+    const size_t cols = 1 + (size_t)nraw + chosen.size();  // y, raw, derived (w, when weighted, may cost a tile)
+    if (chosen.empty() || (cols * tile_bytes <= budget && nraw + (int)chosen.size() <= 60)) {
+      c.nraw = nraw;
+      break;
+    }
+    chosen.pop_back();  // the least used one goes
+  }
+  c.nder = (int)chosen.size();
+  for (int k = 0; k < c.nder; ++k) c.der[k] = chosen[k];
+  return c;
+}
+
 bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt,
                   std::vector<uint8_t>* bytes, std::string* text, std::vector<int32_t>* offsets, Stats* st) {
   const Templates& TT = templates();
@@ -941,7 +1106,8 @@ bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& ca
   std::vector<uint32_t> words;
   std::vector<std::string> lines;
   std::vector<int32_t> offs, okt, rest;
-  codegen(cb, cand, 0, opt, words, opt.text ? &lines : nullptr, offs, okt, rest, st, TT.large);
+  const Columns cols = plan_columns(cb, cand, opt);
+  codegen(cb, cand, 0, opt, words, opt.text ? &lines : nullptr, offs, okt, rest, st, TT.large, cols);
   if (bytes) {
     bytes->resize(words.size() * 4);
     std::memcpy(bytes->data(), words.data(), bytes->size());
@@ -965,6 +1131,7 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
   const Templates& TT = templates();
   if (!TT.ok) { rest = cand; return nullptr; }
   auto t0 = std::chrono::steady_clock::now();
+  const Columns cols = plan_columns(cb, cand, opt);
   constexpr int kMaxParts = 8;
   struct Chunk { std::vector<uint32_t> words; std::vector<int32_t> offs, slots; const Tmpl* T; };
   std::vector<Chunk> chunks;
@@ -972,7 +1139,7 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
   while (pos < cand.size()) {
     Chunk ch;
     ch.T = &TT.large;
-    const size_t next = codegen(cb, cand, pos, opt, ch.words, nullptr, ch.offs, ch.slots, rest, st, TT.large);
+    const size_t next = codegen(cb, cand, pos, opt, ch.words, nullptr, ch.offs, ch.slots, rest, st, TT.large, cols);
     if (next == pos) {  // one tree larger than the area
       rest.push_back(cand[pos]);
       if (st) st->nrejected++;
@@ -991,7 +1158,7 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       Chunk sm;
       sm.T = &TT.small;
       std::vector<int32_t> rs;
-      codegen(cb, ch.slots, 0, opt, sm.words, nullptr, sm.offs, sm.slots, rs, nullptr, TT.small);
+      codegen(cb, ch.slots, 0, opt, sm.words, nullptr, sm.offs, sm.slots, rs, nullptr, TT.small, cols);
       if (sm.slots != ch.slots) throw Error(SRHIP_ERR_INVALID, "jit: small-template relayout differs");
       ch = std::move(sm);
     }
@@ -1001,6 +1168,8 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
   if (chunks.empty()) return nullptr;
   auto t1 = std::chrono::steady_clock::now();
   Module* m = new Module();
+  m->cols = cols;
+  m->memc = opt.memc;
   try {
     for (Chunk& ch : chunks) {
       ModulePart pt;
@@ -1011,8 +1180,9 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       std::vector<uint8_t> img(ch.T->img, ch.T->img + ch.T->size);
       std::memcpy(img.data() + ch.T->area_off, ch.words.data(), ch.words.size() * 4);
       HIP_CHECK(hipModuleLoadData(&q.mod, img.data()));
-      HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, "sr_jit_eval"));
-      HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, "sr_jit_eval_w"));
+      HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, opt.memc ? "sr_jit_eval_m" : "sr_jit_eval"));
+      HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, opt.memc ? "sr_jit_eval_mw" : "sr_jit_eval_w"));
+      HIP_CHECK(hipModuleGetFunction(&q.fn_derive, q.mod, "sr_jit_derive"));
       for (hipFunction_t f : {q.fn, q.fn_w})
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
@@ -1047,6 +1217,8 @@ void destroy(Module* m) {
 }
 
 uint32_t* bail_flags(Module* m) { return m->d_bail; }
+const Columns& columns(const Module* m) { return m->cols; }
+bool memc(const Module* m) { return m && m->memc; }
 int nslots(const Module* m) { return m->nslots; }
 int nparts(const Module* m) { return m ? (int)m->parts.size() : 0; }
 void part(const Module* m, int k, int* slot0, int* nslots) {
@@ -1061,7 +1233,32 @@ struct JitArgs {
   uint32_t* counters;
   int fast;
   int part_lds;
+  int nraw, nder;
+  uint32_t der[kMaxDerived];
+  const float* dcols;
 };
+struct DeriveArgs {
+  const float* X;
+  int64_t n_pad;
+  int nder;
+  uint32_t der[kMaxDerived];
+  float* out;
+};
+
+hipError_t launch_derive(Module* m, const float* X, int64_t n_pad, float* out, hipStream_t stream) {
+  if (m->cols.nder == 0) return hipSuccess;
+  DeriveArgs da;
+  da.X = X;
+  da.n_pad = n_pad;
+  da.nder = m->cols.nder;
+  std::memcpy(da.der, m->cols.der, sizeof(da.der));
+  da.out = out;
+  size_t sz = sizeof(da);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &da, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  const unsigned gx = (unsigned)std::min<int64_t>(1024, (n_pad / 4 + 255) / 256);
+  return hipModuleLaunchKernel(m->parts[0].fn_derive, std::max(gx, 1u), (unsigned)m->cols.nder, 1, 256, 1, 1, 0,
+                               stream, nullptr, cfg);
+}
 
 int64_t flag_words(Module* m) { return (int64_t)m->nslots + 2; }
 
@@ -1069,7 +1266,8 @@ hipError_t reset_flags(Module* m, hipStream_t stream) {
   return hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t), stream);
 }
 
-hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream) {
+hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, const float* dcols,
+                  hipStream_t stream) {
   const ModulePart& q = m->parts[k];
   if (a.nlist != q.nslots) return hipErrorInvalidValue;
   JitArgs ja;
@@ -1078,10 +1276,15 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   ja.bail = m->d_bail + q.slot0;
   ja.counters = m->d_bail + m->nslots;
   ja.fast = fast ? 1 : 0;
+  ja.nraw = m->cols.nraw;
+  ja.nder = m->cols.nder;
+  std::memcpy(ja.der, m->cols.der, sizeof(ja.der));
+  ja.dcols = dcols;
+  if (ja.nraw > a.nfeat) return hipErrorInvalidValue;
   // partials in LDS when they take little room next to the tiles (measured
   // faster on config #2: one coalesced write-out instead of a store per tree)
   const size_t part_bytes = (size_t)a.tpb * sizeof(Part<float>);
-  ja.part_lds = part_bytes <= 8192 ? 1 : 0;
+  ja.part_lds = part_bytes <= 8192 && !part_global() ? 1 : 0;
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned grid = a.rotate == 2 ? (unsigned)((a.nrg + 7) / 8 * 8) * (unsigned)a.ntg
@@ -1089,7 +1292,7 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   // SRHIP_JIT_LDS_PAD (experiments): extra LDS per workgroup, i.e. fewer resident waves
   static const unsigned pad = [] { const char* e = std::getenv("SRHIP_JIT_LDS_PAD"); return e ? (unsigned)std::atoi(e) : 0u; }();
   // LDS: the row tiles (+ the partials when part_lds)
-  const size_t narr = 1 + (size_t)a.nfeat + (a.w ? 1 : 0);
+  const size_t narr = 1 + (size_t)(ja.nraw + ja.nder) + (a.w ? 1 : 0);
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + (ja.part_lds ? part_bytes : 0) + 16;
   return hipModuleLaunchKernel(a.w ? q.fn_w : q.fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds + pad,
                                stream, nullptr, cfg);

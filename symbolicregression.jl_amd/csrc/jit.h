@@ -19,7 +19,30 @@ struct Module;
 struct Options {
   bool fast = true;       // emit the FAST-routine path + guards in eligible trees
   bool text = false;      // also produce the assembly text (tests: checked against llvm-mc)
+  bool derive = true;     // derived columns (below); SRHIP_JIT_DERIVE=0 turns them off
+  bool memc = false;      // constants read from the program's immediates (set_constants needs no new code)
 };
+
+// Derived columns: a routine unary operator applied to a dataset feature,
+// u(x_f), that several trees of the batch share is evaluated once per row by
+// the driver while it stages the row tiles (the PRECISE routine, the value
+// the Float64-evaluating reference gives) and read by tree code like a
+// feature, instead of once per tree. LDS columns of a tile: y, the raw
+// features 0 .. nraw-1, the derived columns, w.
+constexpr int kMaxDerived = 48;
+struct Columns {
+  int nraw = 0;                  // raw feature columns staged (max feature used + 1)
+  int nder = 0;                  // derived columns (column nraw + k)
+  uint32_t der[kMaxDerived] = {};  // (operator << 16) | feature
+};
+const Columns& columns(const Module* m);
+// the module's tree code reads its constants from the device programs
+bool memc(const Module* m);
+// waves per workgroup of the loss tree code (SRHIP_JIT_WAVES) and the LDS a
+// workgroup may take while the CU still holds 5 waves per SIMD
+int waves();
+size_t lds_per_workgroup();
+bool part_global();
 
 // Statistics of one build.
 struct Stats {
@@ -60,7 +83,12 @@ int64_t flag_words(Module* m);
 
 // Launch part k's driver over its slots (EvalArgs as for eval_kernel: list /
 // list_off / fail / partial of the part's slots).
-hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, hipStream_t stream);
+// dcols: the derived columns of this call ([nder][n_pad], launch_derive), or
+// null: the driver computes the staged ones itself
+hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, const float* dcols,
+                  hipStream_t stream);
+// out[k][r] = u_k(x_{f_k}[r]) for the module's derived columns (nothing to do when there are none)
+hipError_t launch_derive(Module* m, const float* X, int64_t n_pad, float* out, hipStream_t stream);
 
 // Test hook: compile without loading; returns bytes and (opt.text) the
 // assembly text of the whole area image.

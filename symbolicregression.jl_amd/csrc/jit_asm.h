@@ -364,6 +364,7 @@ enum : int {
   VOPC_LT_F32 = 0x41, VOPC_LE_F32 = 0x43, VOPC_GT_F32 = 0x44, VOPC_U_F32 = 0x48, VOPC_GT_I32 = 0xc4,
   SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
   SOP2_ADD_U32 = 0x00, SOP2_SUB_U32 = 0x01, SOP2_SUB_I32 = 0x03, SOP2_SUBB_U32 = 0x05, SOP2_ADDC_U32 = 0x04, SOP2_CSELECT = 0x0a,
+  SOP2_AND_B32 = 0x0c,
   SOPC_EQ_U32 = 0x06, SOPC_LG_U32 = 0x07, SOPC_GE_U32 = 0x09, SOPC_LT_U32 = 0x0a, SOPC_LG_U64 = 0x13,
   SOPP_BRANCH = 0x02, SOPP_SCC0 = 0x04, SOPP_SCC1 = 0x05, SOPP_VCCNZ = 0x07,
 };

@@ -68,34 +68,75 @@ struct JitArgs {
   int fast;                 // 1: trees may run their FAST-routine path (guarded)
   int part_lds;             // 1: per-tree partials gathered in LDS (after the tiles) and
                             //    written out together at the end; 0: straight to global memory
+  int nraw, nder;           // raw feature columns and derived columns (jit.h Columns)
+  uint32_t der[48];         // derived column k: (operator << 16) | feature
+  const float* dcols;       // [nder][n_pad] the derived columns (sr_jit_derive), or null: staged ones computed here
 };
 
-template <bool W>
+// A derived column's value: the PRECISE routine of the operator (the same
+// device_ops.h code as the tree code's PRECISE region and the interpreters).
+__device__ __forceinline__ float derive_uop(int op, float x) {
+  switch (op) {
+#define SR_DERIVE_CASE(U) case U: return dev::uop<U>(x);
+    SR_DERIVE_CASE(SRHIP_UOP_EXP) SR_DERIVE_CASE(SRHIP_UOP_LOG) SR_DERIVE_CASE(SRHIP_UOP_LOG2)
+    SR_DERIVE_CASE(SRHIP_UOP_LOG10) SR_DERIVE_CASE(SRHIP_UOP_LOG1P) SR_DERIVE_CASE(SRHIP_UOP_SQRT)
+    SR_DERIVE_CASE(SRHIP_UOP_SIN) SR_DERIVE_CASE(SRHIP_UOP_COS) SR_DERIVE_CASE(SRHIP_UOP_TAN)
+    SR_DERIVE_CASE(SRHIP_UOP_SINH) SR_DERIVE_CASE(SRHIP_UOP_COSH) SR_DERIVE_CASE(SRHIP_UOP_TANH)
+    SR_DERIVE_CASE(SRHIP_UOP_ATAN) SR_DERIVE_CASE(SRHIP_UOP_ASINH) SR_DERIVE_CASE(SRHIP_UOP_ACOSH)
+    SR_DERIVE_CASE(SRHIP_UOP_ATANH_CLIP) SR_DERIVE_CASE(SRHIP_UOP_ERF) SR_DERIVE_CASE(SRHIP_UOP_ERFC)
+    SR_DERIVE_CASE(SRHIP_UOP_GAMMA) SR_DERIVE_CASE(SRHIP_UOP_RELU) SR_DERIVE_CASE(SRHIP_UOP_ROUND)
+    SR_DERIVE_CASE(SRHIP_UOP_FLOOR) SR_DERIVE_CASE(SRHIP_UOP_CEIL) SR_DERIVE_CASE(SRHIP_UOP_SIGN)
+    SR_DERIVE_CASE(SRHIP_UOP_INV)
+#undef SR_DERIVE_CASE
+    default: return __builtin_nanf("");  // not derivable: jit.cpp never asks
+  }
+}
+
+template <bool W, bool MEMC>
 __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const EvalArgs<float>& a = ja.e;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   float* sX = reinterpret_cast<float*>(smem);
-  const int narr = 1 + a.nfeat + (W ? 1 : 0);
+  const int ncol = ja.nraw + ja.nder;
+  const int narr = 1 + ncol + (W ? 1 : 0);
   const int rows = a.ntiles * TILE;
   int rg, g;
   if (!block_of(a, rg, g)) return;
   const int64_t row0 = (int64_t)rg * rows;
+  const int nthreads = __builtin_amdgcn_readfirstlane((int)blockDim.x);
   // per-tree partials: gathered in LDS after the tiles when the host made room
   // for them (few trees per group), else stored straight to global memory
   Part<float>* gdst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
   Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
   Part<float>* dst = ja.part_lds ? sPart : gdst;
 
-  // 1. stage the row group tile-major: tile t, array k (0 = y, 1.. = x_{k-1}, last = w)
+  // 1. stage the row group tile-major: tile t, array k (0 = y, 1 .. nraw =
+  //    x_{k-1}, then the derived columns u(x_f), last = w); one wave per
+  //    (tile, array), so a derived column's operator is wave-uniform
   {
     constexpr int V = TILE / 4;  // float4 per array per tile
     const int total = a.ntiles * narr * V;
-    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+    for (int idx = threadIdx.x; idx < total; idx += nthreads) {
       const int v = idx % V;
       const int tk = idx / V;
       const int k = tk % narr;
       const int t = tk / narr;
-      const float* src = k == 0 ? a.y : (k <= a.nfeat ? a.X + (size_t)(k - 1) * a.n_pad : a.w);
+      if (k > ja.nraw && k <= ncol && ja.dcols) {
+        const float* src = ja.dcols + (size_t)(k - 1 - ja.nraw) * a.n_pad;
+        reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
+            reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
+        continue;
+      }
+      if (k > ja.nraw && k <= ncol) {
+        const uint32_t d = ja.der[k - 1 - ja.nraw];
+        const int op = __builtin_amdgcn_readfirstlane((int)(d >> 16));
+        const float4 x = reinterpret_cast<const float4*>(a.X + (size_t)(d & 0xffffu) * a.n_pad + row0 +
+                                                         (int64_t)t * TILE)[v];
+        reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
+            make_float4(derive_uop(op, x.x), derive_uop(op, x.y), derive_uop(op, x.z), derive_uop(op, x.w));
+        continue;
+      }
+      const float* src = k == 0 ? a.y : (k <= ja.nraw ? a.X + (size_t)(k - 1) * a.n_pad : a.w);
       reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
           reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
     }
@@ -107,10 +148,15 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE - 1) / TILE);
   const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-  const int nwaves = (int)(blockDim.x >> 6);
+  const int nwaves = nthreads >> 6;
   auto slot_of = [&](int i) { return a.contig ? g * a.tpb + i : i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
   auto code_of = [&](int s) {
     return __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(ja.code_off))[s]);
+  };
+  // the slot's program (memory-constant tree code loads its constants from it)
+  auto prog_of = [&](int s) {
+    return reinterpret_cast<uint64_t>(
+        a.prog + __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(a.list_off))[s]));
   };
   auto ld_flag = [&](int slot) { return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
 
@@ -124,7 +170,7 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)sX) +
                             (uint32_t)lane * 16u;
   const uint32_t tilebytes = (uint32_t)(narr * TILE * 4);
-  const uint32_t woff = W ? (uint32_t)((1 + a.nfeat) * TILE * 4) : 0u;  // 0: unweighted
+  const uint32_t woff = W ? (uint32_t)((1 + ncol) * TILE * 4) : 0u;  // 0: unweighted
   const uint32_t lane4 = (uint32_t)lane * R;
   const uint32_t partial = (uint32_t)last_valid;
   const uint32_t nt_u = (uint32_t)nt_valid;
@@ -152,12 +198,22 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
       const uint64_t target = area + (uint32_t)coff;
       uint32_t la = lds_lane;
       uint32_t tile = 0, status;
-      asm volatile("s_swappc_b64 s[76:77], %[tgt]"
-                   : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
-                     "+{s84}"(redos)
-                   : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial),
-                     "{s67}"(tilebytes), "{s68}"(woff), "{s79}"(fastok)
-                   : SR_JIT_CLOBBERS, "memory");
+      if constexpr (MEMC) {  // memory-constant tree code: its program in s[56:57], constants in s24..s39
+        uint64_t pptr = prog_of(s);
+        asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                     : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
+                       "+{s84}"(redos), "+{s[56:57]}"(pptr)
+                     : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial),
+                       "{s67}"(tilebytes), "{s68}"(woff), "{s79}"(fastok)
+                     : SR_JIT_CLOBBERS_MEMC, "memory");
+      } else {
+        asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                     : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
+                       "+{s84}"(redos)
+                     : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial),
+                       "{s67}"(tilebytes), "{s68}"(woff), "{s79}"(fastok)
+                     : SR_JIT_CLOBBERS, "memory");
+      }
       if (__builtin_amdgcn_readfirstlane((int)status) != 0) {
         // a tile the routines cannot do (sin/cos argument beyond the fast
         // reduction): the host re-evaluates this tree with the interpreter;
@@ -181,12 +237,36 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (ja.part_lds) {  // slots no wave ran keep whatever: finalize ignores them
     __syncthreads();
-    for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) gdst[i] = sPart[i];
+    for (int i = threadIdx.x; i < a.tpb; i += nthreads) gdst[i] = sPart[i];
   }
 }
 
-extern "C" __global__ void __launch_bounds__(256) sr_jit_eval(JitArgs ja) { jit_eval_body<false>(ja); }
-extern "C" __global__ void __launch_bounds__(256) sr_jit_eval_w(JitArgs ja) { jit_eval_body<true>(ja); }
+// The derived columns of a call, once per row: out[k][r] = u_k(x_{f_k}[r]) for
+// r < n_pad (padding rows replicate the last row, as X does).
+struct DeriveArgs {
+  const float* X;
+  int64_t n_pad;
+  int nder;
+  uint32_t der[48];
+  float* out;
+};
+extern "C" __global__ void __launch_bounds__(256) sr_jit_derive(DeriveArgs da) {
+  const int k = blockIdx.y;
+  const uint32_t d = da.der[k];
+  const int op = (int)(d >> 16);
+  const float* x = da.X + (size_t)(d & 0xffffu) * da.n_pad;
+  float* o = da.out + (size_t)k * da.n_pad;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < da.n_pad / 4; i += (int64_t)gridDim.x * blockDim.x) {
+    const float4 v = reinterpret_cast<const float4*>(x)[i];
+    reinterpret_cast<float4*>(o)[i] = make_float4(derive_uop(op, v.x), derive_uop(op, v.y), derive_uop(op, v.z),
+                                                  derive_uop(op, v.w));
+  }
+}
+
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval(JitArgs ja) { jit_eval_body<false, false>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_w(JitArgs ja) { jit_eval_body<true, false>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_m(JitArgs ja) { jit_eval_body<false, true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_mw(JitArgs ja) { jit_eval_body<true, true>(ja); }
 
 // ---- gradient tree code (jit_grad.cpp) ---------------------------------------------
 // One workgroup = (row group, tree group) as above; each tree's code runs the

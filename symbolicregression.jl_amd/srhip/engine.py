@@ -262,10 +262,11 @@ def _trees_struct(flat: FlatTrees, consts: np.ndarray) -> Trees:
     )
 
 
-def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False):
+def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bool = False):
     """Tree compiler without a device (srhip_jit_compile, or with grad=True
-    srhip_jit_compile_grad: the reverse-mode gradient tree code): (code
-    bytes, assembly text, {tree id: byte offset})."""
+    srhip_jit_compile_grad: the reverse-mode gradient tree code; memc: the
+    memory-constant loss tree code): (code bytes, assembly text, {tree id:
+    byte offset})."""
     consts = np.ascontiguousarray(flat.consts, dtype=np.float32)
     tr = _trees_struct(flat, consts)
     nb, nt, no = C.c_int64(0), C.c_int64(0), C.c_int64(0)
@@ -274,8 +275,8 @@ def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False):
         if grad:
             return lib().srhip_jit_compile_grad(C.byref(tr), bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
                                                 C.byref(no))
-        return lib().srhip_jit_compile(C.byref(tr), int(fast), bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
-                                       C.byref(no))
+        return lib().srhip_jit_compile(C.byref(tr), int(fast) | (2 if memc else 0), bufs[0], C.byref(nb), bufs[1],
+                                       C.byref(nt), bufs[2], C.byref(no))
 
     rc = call(None, None, None)
     if rc != -1:

@@ -92,8 +92,12 @@ def loss_spread_flat(flat, X, y, w, T, loss, nperturb=3, seed=0):
     return spread
 
 
-def assert_close_conditioned(actual, desired, spread, rtol, atol=0.0, factor=64.0, msg="", max_bad_frac=0.0):
+def assert_close_conditioned(actual, desired, spread, rtol, atol=0.0, factor=4.0, msg="", max_bad_frac=0.0):
     """|actual - desired| <= atol + rtol |desired| + factor * spread, elementwise
+    (factor 4: an evaluation within the per-operator bar lands within the
+    spread of the oracle's own perturbed evaluations, up to sampling: the
+    FAST path's outliers at full size measure <= 0.85 x spread,
+    profiles/r03_fast_parity.json)
     (a fraction max_bad_frac of the elements may exceed it: the input
     perturbation does not model rounding inside the tree, which matters for
     f32 derivatives near cancellations)."""

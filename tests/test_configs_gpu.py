@@ -49,7 +49,7 @@ def test_config5_20feat_10M_rows_16k_trees(gpu_ctx):
     _, ref_l, ref_ok = oracle.eval_loss_batch(srhip.flatten(st, o, dtype=np.float32), X, y, dtype=np.float32,
                                               nthreads=16)
     losses = (s[sub] / n).astype(np.float32)
-    nchk, _ = _check_losses(st, o, X, y, np.float32, losses, ok[sub], ref_l, ref_ok, 1e-5)
+    nchk, _ = _check_losses(st, o, X, y, np.float32, losses, ok[sub], ref_l, ref_ok, 1e-5, name="config5_sample")
     assert nchk > 150
 
     # (2) config #5's partition: 8 row shards of 1.25M rows

@@ -206,14 +206,77 @@ def test_engine_optimizer_random_population(gpu_ctx):
     assert res.converged.any()
 
 
+
+class _env:
+    """Environment variables set for a block (knobs read when a program is built)."""
+
+    def __init__(self, **kw):
+        self.kw, self.old = kw, {}
+
+    def __enter__(self):
+        import os
+        for k, v in self.kw.items():
+            self.old[k] = os.environ.get(k)
+            os.environ[k] = v
+
+    def __exit__(self, *a):
+        import os
+        for k, v in self.old.items():
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = v
+
+
+@pytest.mark.gpu
+def test_set_constants_static_failure_in_place(gpu_ctx):
+    """A constant set that makes some trees fail statically (a non-finite
+    constant) keeps the program layout: the update is in place (no rebuild of
+    the tree code), those trees fail, every other tree equals a fresh
+    program's result; restoring finite constants is in place too."""
+    from srhip import constants as K
+
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(700, o, 5, np.float32, seed=13)
+    rng = np.random.default_rng(14)
+    X = rng.standard_normal((5, 5001)).astype(np.float32)
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(np.float32)
+    ds = srhip.DeviceDataset(gpu_ctx, X, y)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    c0 = np.asarray(flat.consts, dtype=np.float32)
+    with _env(SRHIP_JIT="1", SRHIP_JIT_MEMC="1"):
+        prog = srhip.Program(gpu_ctx, flat, np.float32)
+    assert prog.jit_info()["ntrees"] > 500
+    # one constant of every 7th tree with constants becomes Inf
+    c1 = c0 * np.float32(1.01)
+    hit = [t for t in range(len(trees)) if flat.const_off[t + 1] > flat.const_off[t]][::7]
+    for t in hit:
+        c1[flat.const_off[t]] = np.inf
+    for k, c in enumerate((c1, c0 * np.float32(0.99))):
+        prog.set_constants(c)
+        fresh = srhip.Program(gpu_ctx, srhip.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off, c,
+                                                       flat.nodes), np.float32)
+        s1, _, ok1 = prog.eval_loss(ds, K.LOSS["L2"])
+        s2, _, ok2 = fresh.eval_loss(ds, K.LOSS["L2"])
+        assert np.array_equal(ok1, ok2)
+        np.testing.assert_array_equal(s1[ok1], s2[ok2])
+        if k == 0:
+            assert not ok1[hit].any()  # an Inf constant fails its tree
+    st = prog.update_stats()
+    assert st["rebuilt"] == 0 and st["inplace"] == 2, st
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("T,n", [(np.float32, 600), (np.float64, 200)])
 def test_set_constants_in_place(gpu_ctx, T, n):
     """srhip_program_set_constants overwrites the device programs' immediates
     in place (same folding / static verdicts) and the losses, gradients and
     did_succeed equal those of a program built from the new constants. A
-    tree-code program (600 Float32 trees, SRHIP_JIT=1) is rebuilt once and
-    runs interpreted from then on."""
+    tree-code program (600 Float32 trees, SRHIP_JIT=1) is rebuilt once, as
+    memory-constant tree code that reads its constants from the updated
+    programs (bit for bit the literal tree code of a fresh program); a
+    program built that way from the start (SRHIP_JIT_MEMC=1) is never
+    rebuilt."""
     import os
     from srhip import constants as K
 
@@ -228,31 +291,33 @@ def test_set_constants_in_place(gpu_ctx, T, n):
     old = os.environ.get("SRHIP_JIT")
     os.environ["SRHIP_JIT"] = "1"
     try:
-        prog = srhip.Program(ctx, flat, T)
-        jit0 = prog.jit_info()["ntrees"]
-        prog.eval_loss_grad(ds, K.LOSS["L2"])  # gradient programs built
-        c0 = np.asarray(flat.consts, dtype=T)
-        for k in range(3):
-            c = (c0 * T(1 + 0.01 * (k + 1)) + T(0.001 * k)).astype(T)
-            prog.set_constants(c)
-            fresh_flat = srhip.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off, c, flat.nodes)
-            os.environ["SRHIP_JIT"] = "0"
-            fresh_i = srhip.Program(ctx, fresh_flat, T)
-            os.environ["SRHIP_JIT"] = "1"
-            s1, w1, ok1 = prog.eval_loss(ds, K.LOSS["L2"])
-            s2, w2, ok2 = fresh_i.eval_loss(ds, K.LOSS["L2"])
-            assert np.array_equal(ok1, ok2)
-            np.testing.assert_array_equal(s1[ok1], s2[ok2])
-            g1 = prog.eval_loss_grad(ds, K.LOSS["L2"])
-            g2 = fresh_i.eval_loss_grad(ds, K.LOSS["L2"])
-            for a, b in zip(g1, g2):
-                np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
-        st = prog.update_stats()
-        assert prog.jit_info()["ntrees"] == 0
-        if jit0:
-            assert st["rebuilt"] == 1 and st["inplace"] == 2
-        else:
-            assert st["rebuilt"] == 0 and st["inplace"] == 3
+        for memc_env in ("0", "1"):
+            if memc_env == "1" and T != np.float32:
+                continue
+            with _env(SRHIP_JIT_MEMC=memc_env):
+                prog = srhip.Program(ctx, flat, T)
+            jit0 = prog.jit_info()["ntrees"]
+            prog.eval_loss_grad(ds, K.LOSS["L2"])  # gradient programs built
+            c0 = np.asarray(flat.consts, dtype=T)
+            for k in range(3):
+                c = (c0 * T(1 + 0.01 * (k + 1)) + T(0.001 * k)).astype(T)
+                prog.set_constants(c)
+                fresh_flat = srhip.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off, c, flat.nodes)
+                fresh = srhip.Program(ctx, fresh_flat, T)  # tree code with the constants compiled in
+                s1, w1, ok1 = prog.eval_loss(ds, K.LOSS["L2"])
+                s2, w2, ok2 = fresh.eval_loss(ds, K.LOSS["L2"])
+                assert np.array_equal(ok1, ok2)
+                np.testing.assert_array_equal(s1[ok1], s2[ok2])
+                g1 = prog.eval_loss_grad(ds, K.LOSS["L2"])
+                g2 = fresh.eval_loss_grad(ds, K.LOSS["L2"])
+                for a, b in zip(g1, g2):
+                    np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
+            st = prog.update_stats()
+            assert prog.jit_info()["ntrees"] == jit0  # still tree code
+            if jit0 and memc_env == "0":
+                assert st["rebuilt"] == 1 and st["inplace"] == 2
+            else:
+                assert st["rebuilt"] == 0 and st["inplace"] == 3
     finally:
         if old is None:
             os.environ.pop("SRHIP_JIT", None)

@@ -17,6 +17,7 @@ import torch.multiprocessing as mp
 
 import oracle
 import srhip
+from numerics import assert_close_conditioned, loss_spread
 
 pytestmark = pytest.mark.gpu
 
@@ -96,11 +97,13 @@ def test_row_sharded_engine_world2_on_one_gpu(gpu_ctx):
         # the shards regroup the Float32 per-tile partial sums: within the
         # north_star's 1e-5 of the single-process engine and of the oracle
         np.testing.assert_allclose(l[m], ref_l[m], rtol=1e-5)
-        # against the oracle's Float64-evaluated transcendentals the FAST
-        # path moves ill-conditioned trees more (tests/test_full_size.py
-        # checks those against the conditioning); the bulk agrees
+        # against the oracle: the north_star's 1e-5, or (a tree outside it)
+        # within 4x the oracle's own spread under ulp-scale perturbations
         rel = np.abs(l[m] - or_l[m]) / np.abs(or_l[m])
-        assert np.median(rel) < 1e-6 and np.mean(rel < 1e-5) > 0.9
+        out = np.flatnonzero(m)[~(rel <= 1e-5)]
+        if out.size:
+            sp = loss_spread([trees[i] for i in out], o, X, y, None, np.float32, nperturb=3) / X.shape[1]
+            assert_close_conditioned(l[out], or_l[out], sp, rtol=1e-5, factor=4.0, msg="row-sharded vs oracle")
     np.testing.assert_array_equal(res[0][1], res[1][1])
     # constant optimisation with all-reduced gradients
     o2, X2, y2, trees2 = _copt_problem()

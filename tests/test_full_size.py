@@ -23,7 +23,19 @@ from numerics import assert_close_conditioned, loss_spread
 pytestmark = pytest.mark.gpu
 
 
-def _check_losses(trees, o, X, y, T, losses, ok, ref_l, ref_ok, rtol):
+def _record(name, rec):
+    """Append the parity counts of a full-size check to gpurun_out/parity_counts.jsonl
+    (copied to profiles/ after a GPU run)."""
+    import json
+    from pathlib import Path
+
+    out = Path(__file__).resolve().parent.parent / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    with open(out / "parity_counts.jsonl", "a") as f:
+        f.write(json.dumps(dict(test=name, **rec)) + "\n")
+
+
+def _check_losses(trees, o, X, y, T, losses, ok, ref_l, ref_ok, rtol, name=""):
     bad = np.flatnonzero(ok != ref_ok)
     print(f"did_succeed mismatches: {bad.size} of {len(trees)}: {bad[:20]}")
     assert bad.size == 0, f"did_succeed differs on {bad[:20]}"
@@ -34,10 +46,19 @@ def _check_losses(trees, o, X, y, T, losses, ok, ref_l, ref_ok, rtol):
     # outliers must be ill-conditioned: check them against the perturbation spread
     print(f"{out.size} of {int(m.sum())} succeeding trees outside rtol {rtol}; "
           f"median rel {np.median(rel[m]):.2e}; max rel {np.max(rel[m]) if m.any() else 0:.2e}")
+    rec = dict(ntrees=len(trees), did_succeed_mismatch=int(bad.size), succeeding=int(m.sum()),
+               outside_rtol=int(out.size), rtol=rtol, max_rel=float(np.max(rel[m])) if m.any() else 0.0,
+               median_rel=float(np.median(rel[m])) if m.any() else 0.0)
     if out.size:
         sub = [trees[i] for i in out]
-        sp = loss_spread(sub, o, X, y, None, T, nperturb=2) / X.shape[1]
-        assert_close_conditioned(losses[out], ref_l[out], sp, rtol=rtol, msg="ill-conditioned outliers")
+        sp = loss_spread(sub, o, X, y, None, T, nperturb=3) / X.shape[1]
+        err = np.abs(losses[out].astype(np.float64) - ref_l[out].astype(np.float64))
+        rec["max_err_over_spread"] = float(np.max(err / np.maximum(sp, 1e-300)))
+        _record(name, rec)
+        print(f"worst outlier: {rec['max_err_over_spread']:.3f} x the oracle's perturbation spread")
+        assert_close_conditioned(losses[out], ref_l[out], sp, rtol=rtol, factor=4.0, msg="ill-conditioned outliers")
+    else:
+        _record(name, rec)
     return int(m.sum()), int(out.size)
 
 
@@ -56,7 +77,7 @@ def test_config2_full_4096_trees_1M_rows(gpu_ctx):
     losses, ok = srhip.eval_loss_batch_ok(trees, ds, o, program=prog)
     flat = srhip.flatten(trees, o, dtype=np.float32)
     _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, dtype=np.float32, nthreads=16)
-    n, nout = _check_losses(trees, o, X, y, np.float32, losses, ok, ref_l, ref_ok, 1e-5)
+    n, nout = _check_losses(trees, o, X, y, np.float32, losses, ok, ref_l, ref_ok, 1e-5, name="config2")
     assert n > 3000 and 0.05 < 1 - ok.mean() < 0.5
 
 
@@ -71,5 +92,5 @@ def test_config3_full_nan_heavy_f64(gpu_ctx):
     losses, ok = srhip.eval_loss_batch_ok(trees, ds, o)
     flat = srhip.flatten(trees, o, dtype=np.float64)
     _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, dtype=np.float64, nthreads=16)
-    n, _ = _check_losses(trees, o, X, y, np.float64, losses, ok, ref_l, ref_ok, 1e-10)
+    n, _ = _check_losses(trees, o, X, y, np.float64, losses, ok, ref_l, ref_ok, 1e-10, name="config3")
     assert 0.05 < ok.mean() < 0.95 and n > 200

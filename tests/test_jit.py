@@ -42,8 +42,8 @@ def test_machine_code_equals_llvm_mc(k):
     o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
     trees = srhip.random_population(300, o, 7, np.float32, seed=11 + k)
     flat = srhip.flatten(trees, o, dtype=np.float32)
-    for fast in (True, False):
-        code, text, offs = jit_compile(flat, fast=fast)
+    for fast, memc in ((True, False), (False, False), (True, True)):
+        code, text, offs = jit_compile(flat, fast=fast, memc=memc)
         assert len(offs) >= 0.7 * len(trees), f"only {len(offs)} of {len(trees)} trees compiled"
         ref = assemble(text)
         assert len(ref) == len(code)
@@ -63,6 +63,28 @@ def test_every_tree_of_config2_compiles():
     assert len(offs) >= 990
     assert all(v % 64 == 0 for v in offs.values())
     print(f"{len(offs)} trees, {len(code) / len(offs):.0f} bytes per tree")
+
+
+def test_memory_constant_code_loads_every_constant():
+    """Memory-constant tree code (set_constants without new code): no
+    literal of the tree's constants remains in its code, and every constant
+    is loaded from its program instruction (s_load_dword ..., 8 pc + 4)."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    x1, x2 = srhip.Node("x1"), srhip.Node("x2")
+    c = [np.float32(v) for v in (1.2345678, -0.7654321, 3.3333333)]
+    t = o.make_binary("+", o.make_binary("*", srhip.Node(val=c[0]), o.make_unary("cos", x1)),
+                      o.make_binary("/", x2, srhip.Node(val=c[1])))
+    t = o.make_binary("-", t, o.make_unary("exp", o.make_binary("*", x2, srhip.Node(val=c[2]))))
+    flat = srhip.flatten([t], o, dtype=np.float32)
+    for fast in (True, False):
+        _, lit_text, _ = jit_compile(flat, fast=fast)
+        _, text, offs = jit_compile(flat, fast=fast, memc=True)
+        assert offs
+        hexes = {hex(int(np.float32(v).view(np.uint32))) for v in c}
+        assert any(h in lit_text for h in hexes)
+        assert not any(h in text for h in hexes), "a constant compiled in as a literal"
+        loads = [ln for ln in text.splitlines() if ln.startswith("s_load_dword s")]
+        assert len(loads) == 3, loads
 
 
 GRAD_OPSETS = [

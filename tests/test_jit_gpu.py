@@ -20,6 +20,7 @@ import pytest
 import oracle
 import srhip
 from srhip import constants as K
+from numerics import assert_close_conditioned, loss_spread
 
 pytestmark = pytest.mark.gpu
 
@@ -117,8 +118,14 @@ def test_fast_path_did_succeed_matches_oracle(gpu_ctx):
     bad = np.flatnonzero(ok_j != ref_ok)
     assert bad.size == 0, f"did_succeed differs from the oracle on {bad[:10]}"
     m = ok_j & np.isfinite(ref_l)
-    rel = np.abs(s_j[m] / w_j - ref_l[m]) / np.abs(ref_l[m])
+    got = s_j / w_j
+    rel = np.abs(got[m] - ref_l[m]) / np.abs(ref_l[m])
     assert np.median(rel) < 1e-6
+    # every tree within the north_star's 1e-5, or within 4x its conditioning
+    out = np.flatnonzero(m)[~(rel <= 1e-5)]
+    if out.size:
+        sp = loss_spread([trees[i] for i in out], o, X, y, None, np.float32, nperturb=3) / X.shape[1]
+        assert_close_conditioned(got[out], ref_l[out], sp, rtol=1e-5, factor=4.0, msg="FAST path vs oracle")
 
 
 def test_big_trig_arguments_in_tree_code(gpu_ctx):
@@ -141,7 +148,11 @@ def test_big_trig_arguments_in_tree_code(gpu_ctx):
             m = ok_i & np.isfinite(s_i)
             assert np.array_equal(np.isfinite(s_j[ok_i]), np.isfinite(s_i[ok_i]))
             rel = np.abs(s_j[m] - s_i[m]) / np.abs(s_i[m])
-            assert np.median(rel) < 1e-6 and np.mean(rel < 1e-4) > 0.98
+            assert np.median(rel) < 1e-6
+            out = np.flatnonzero(m)[~(rel <= 1e-5)]
+            if out.size:  # each outlier within 4x the tree's conditioning
+                sp = loss_spread([trees[i] for i in out], o, X, y, None, np.float32, nperturb=3)
+                assert_close_conditioned(s_j[out], s_i[out], sp, rtol=1e-5, factor=4.0, msg="FAST path vs PRECISE")
 
 
 def _huge_floats(n, seed):

@@ -91,6 +91,9 @@ def disassemble(path):
     return ins
 
 
+BYPLACE = collections.Counter()
+
+
 def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000):
     """One interior tile of one tree: (prologue counts, tile counts).
     attrib (Counter) collects SIMD cycles per routine name / 'tree'."""
@@ -114,6 +117,7 @@ def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000):
             cur[m] += 1
             if attrib is not None and cur is tile and m.startswith("v_"):
                 attrib[where[-1]] += COST[vclass(m)]
+                BYPLACE[(where[-1], m)] += 1
         else:
             cur["S:" + m] += 1
         if m == "s_mov_b32" and ops[0].startswith("s") and ops[0][1:].isdigit():
@@ -196,6 +200,7 @@ def main():
     ap.add_argument("--nfeat", type=int, default=5)
     ap.add_argument("--fclk", type=float, default=2.4e9)
     ap.add_argument("--json", default="")
+    ap.add_argument("--by-place", action="store_true", help="per routine / tree-code opcode counts")
     args = ap.parse_args()
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     trees = srhip.random_population(args.ntrees, o, args.nfeat, np.float32, seed=args.seed, maxsize=30)
@@ -239,6 +244,9 @@ def main():
     print(f"{'instruction':34s} {'class':6s} {'count':>9s} {'SIMD-cyc':>10s} {'share':>7s}")
     for k, cl, v, c in rows_budget:
         print(f"{k:34s} {cl:6s} {v:9d} {c:10.0f} {100 * c / tot_cyc:6.1f}%")
+    if args.by_place:
+        for (pl, m), v in sorted(BYPLACE.items(), key=lambda z: (z[0][0], -z[1])):
+            print(f"  {pl:12s} {m:28s} {v:8d} {COST[vclass(m)] * v:10.0f}")
     nval = sum(v for k, v in tot_tile.items() if k.startswith("v_"))
     nsalu = sum(v for k, v in tot_tile.items() if k.startswith("S:"))
     nds = sum(v for k, v in tot_tile.items() if k.startswith("ds_"))

@@ -32,7 +32,7 @@
 
 enum Op { ADD, FMA, PK_ADD, PK_FMA, PK_MUL, EXP, RCP, FMA64, LSHLADD, MAX3, CNDMASK, MIX_PK_EXP, NOP,
           MOV, MUL, MAXF, CMP, XOR, ADDU, CVT64, RNDNE, LDEXP, PKMOV, MED3, CND2, LSHL, BFI, CVTI, MULF64, ADD_ABS,
-          MIX_F32_EXP, MIX_PK_MAX3 };
+          MIX_F32_EXP, MIX_PK_MAX3, MAX_ABS, FMAC, CMP64 };
 static const char* kName[] = {"v_add_f32", "v_fma_f32", "v_pk_add_f32", "v_pk_fma_f32", "v_pk_mul_f32",
                               "v_exp_f32", "v_rcp_f32", "v_fma_f64", "v_lshl_add_u32", "v_max3_f32",
                               "v_cndmask_b32", "4 v_pk_fma_f32 + 1 v_exp_f32 (ILP1: pk_fma)", "s_nop 0",
@@ -40,7 +40,8 @@ static const char* kName[] = {"v_add_f32", "v_fma_f32", "v_pk_add_f32", "v_pk_fm
                               "v_xor_b32", "v_add_u32", "v_cvt_f32_f64", "v_rndne_f32", "v_ldexp_f32",
                               "v_pk_mov_b32", "v_med3_f32", "v_cndmask_b32 (VOP2)", "v_lshlrev_b32", "v_bfi_b32",
                               "v_cvt_i32_f32", "v_mul_f64", "v_add_f32 |a|+|b| (VOP3)",
-                              "4 v_fma_f32 + 1 v_exp_f32", "2 v_pk_fma_f32 + 1 v_max3_f32"};
+                              "4 v_fma_f32 + 1 v_exp_f32", "2 v_pk_fma_f32 + 1 v_max3_f32",
+                              "v_max_f32 |a|,|b| (VOP3)", "v_fmac_f32 (VOP2)", "v_cmp_gt_f32 |a| -> sgpr (VOP3)"};
 
 // The loop body: 64 instructions of one kind in ONE asm statement (no
 // compiler-inserted s_nop between them), over 8 independent chains (ILP 8:
@@ -83,6 +84,9 @@ __device__ __forceinline__ void body(float (&v)[8], double (&pv)[8], double (&d)
 #define I_CVTI(r) "v_cvt_i32_f32 " r ", " r "\n"
 #define I_ADDABS(r) "v_add_f32_e64 " r ", |" r "|, |" r "|\n"
 #define I_MULF64(r) "v_mul_f64 " r ", " r ", " r "\n"
+#define I_MAXABS(r) "v_max_f32_e64 " r ", |" r "|, |" r "|\n"
+#define I_FMAC(r) "v_fmac_f32 " r ", " r ", " r "\n"
+#define I_CMP64(r) "v_cmp_gt_f32_e64 s[2:3], |" r "|, " r "\n"
 #define I_PKMOV(r) "v_pk_mov_b32 " r ", " r ", " r " op_sel:[0,1]\n"
   if constexpr (ILP == 8) {
     if constexpr (OP == ADD) V8(I_ADD);
@@ -121,6 +125,9 @@ __device__ __forceinline__ void body(float (&v)[8], double (&pv)[8], double (&d)
     else if constexpr (OP == CVTI) V8(I_CVTI);
     else if constexpr (OP == MULF64) P8(I_MULF64, d);
     else if constexpr (OP == ADD_ABS) V8(I_ADDABS);
+    else if constexpr (OP == MAX_ABS) V8(I_MAXABS);
+    else if constexpr (OP == FMAC) V8(I_FMAC);
+    else if constexpr (OP == CMP64) { asm volatile(R8(B8(I_CMP64("%0"), I_CMP64("%1"), I_CMP64("%2"), I_CMP64("%3"), I_CMP64("%4"), I_CMP64("%5"), I_CMP64("%6"), I_CMP64("%7"))) :: "v"(v[0]), "v"(v[1]), "v"(v[2]), "v"(v[3]), "v"(v[4]), "v"(v[5]), "v"(v[6]), "v"(v[7]) : "s2", "s3"); }
     else if constexpr (OP == MIX_F32_EXP) {  // 4 scalar fmas then 1 exp
       asm volatile(R8("v_fma_f32 %0, %0, %0, %0\n v_fma_f32 %1, %1, %1, %1\n v_fma_f32 %2, %2, %2, %2\n"
                       " v_fma_f32 %3, %3, %3, %3\n v_exp_f32 %4, %4\n")
@@ -211,6 +218,9 @@ static KFn kernel_for(int op, int ilp) {
     case ADD_ABS: return pick<ADD_ABS>(ilp);
     case MIX_F32_EXP: return pick<MIX_F32_EXP>(ilp);
     case MIX_PK_MAX3: return pick<MIX_PK_MAX3>(ilp);
+    case MAX_ABS: return pick<MAX_ABS>(ilp);
+    case FMAC: return pick<FMAC>(ilp);
+    case CMP64: return pick<CMP64>(ilp);
     default: return pick<NOP>(ilp);
   }
 }
@@ -240,7 +250,7 @@ int main(int argc, char** argv) {
   const bool ext = argc > 2 && std::strcmp(argv[2], "ext") == 0;
   std::vector<int> ops = {NOP, ADD, FMA, PK_ADD, PK_FMA, PK_MUL, EXP, RCP, FMA64, LSHLADD, MAX3, CNDMASK, MIX_PK_EXP};
   if (ext) ops = {MOV, MUL, MAXF, CMP, XOR, ADDU, CVT64, RNDNE, LDEXP, PKMOV, MED3, CND2, LSHL, BFI, CVTI, MULF64,
-                  ADD_ABS, MIX_F32_EXP, MIX_PK_MAX3};
+                  ADD_ABS, MIX_F32_EXP, MIX_PK_MAX3, MAX_ABS, FMAC, CMP64};
   const int ws[] = {1, 2, 4, 5, 8};
   for (int op : ops) {
     for (int ilp : {8, 1}) {
