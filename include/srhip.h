@@ -198,6 +198,19 @@ int32_t srhip_eval_loss(srhip_dataset* ds, const srhip_program* prog,
                         const int64_t* row_idx, int64_t nidx,
                         double* out_loss_sum, double* out_weight_sum,
                         uint8_t* out_ok);
+/* Row shards (config #5, src/ConstantOptimization.jl:43 with the rows split
+ * over GPUs): srhip_eval_loss's per-tree partials written to DEVICE memory
+ * for a device-side all-reduce (RCCL), no host round trip:
+ *   d_out[2t]      = Σ_i w_i ℓ(ŷ_t,i, y_i) over the shard (0 if t failed)
+ *   d_out[2t + 1]  = 1 if t failed on the shard (did_succeed false), else 0
+ *   d_out[2·ntrees] = Σ_i w_i (the row count when unweighted)
+ * d_out holds 2·ntrees + 1 doubles on the context's device. Asynchronous:
+ * enqueued on the context's stream; srhip_sync(ctx) before another stream
+ * or the host reads d_out. Summed over shards: loss = ΣΣ/ΣΣw, did_succeed =
+ * (Σ failed == 0). */
+int32_t srhip_eval_loss_packed(srhip_dataset* ds, srhip_program* prog, int32_t loss_kind,
+                               const double* loss_params, double* d_out);
+
 /* Convenience: srhip_program_create + srhip_eval_loss + destroy (the program
  * in the dataset's context). */
 int32_t srhip_eval_loss_batch(srhip_dataset* ds, const srhip_trees* trees,

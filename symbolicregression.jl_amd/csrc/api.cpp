@@ -14,6 +14,7 @@
 #include <mutex>
 #include <type_traits>
 #include <numeric>
+#include <thread>
 #include <string>
 #include <vector>
 
@@ -112,7 +113,13 @@ struct srhip_ctx {
   double* res_sum = nullptr;
   uint8_t* res_ok = nullptr;
   bool res_host = false;
+  bool want_device_results = false;  // srhip_eval_loss_packed: per-tree results stay in device buffers
   uint32_t* pin_cnt = nullptr;  // [2]
+  // pinned staging of large per-row outputs (srhip_eval_tree_array): two
+  // halves, DMA into one while the other is copied to the caller's memory
+  unsigned char* pin_stage = nullptr;
+  size_t stage_cap = 0;
+  hipEvent_t stage_ev[2] = {nullptr, nullptr};
   double last_ms = 0.0;
   int last_launches = 0;
   int last_bailed = 0;  // trees re-evaluated after their tree code handed a tile back
@@ -152,6 +159,9 @@ struct srhip_program {
   // compiled metadata
   std::vector<int32_t> nodes;
   std::vector<uint8_t> static_fail, fail_if_rows;
+  // the static verdicts on the device (srhip_eval_loss_packed), uploaded when stale
+  uint8_t* d_verdict = nullptr;
+  bool verdict_stale = true;
   int max_feature = -1;
   int64_t total_nodes = 0;
   // device
@@ -310,6 +320,9 @@ void free_program_device(srhip_program* p) {
   p->jit = nullptr;
   p->nlist_j = 0;
   if (p->d_code) (void)hipFree(p->d_code);
+  if (p->d_verdict) (void)hipFree(p->d_verdict);
+  p->d_verdict = nullptr;
+  p->verdict_stale = true;
   if (p->d_tree_off) (void)hipFree(p->d_tree_off);
   if (p->d_list) (void)hipFree(p->d_list);
   p->d_code = nullptr;
@@ -555,6 +568,7 @@ void build_program(srhip_program* p) {
   p->nodes = cb.nodes;
   p->static_fail = cb.static_fail;
   p->fail_if_rows = cb.fail_if_rows;
+  p->verdict_stale = true;
   p->max_feature = cb.max_feature;
   p->total_nodes = cb.total_nodes;
   // operator set: every opcode left after folding must be in it
@@ -677,6 +691,7 @@ void update_constants(srhip_program* p) {
     return;
   }
   // same layout: the static verdicts (host side) may change with it
+  if (cb.static_fail != p->static_fail || cb.fail_if_rows != p->fail_if_rows) p->verdict_stale = true;
   p->static_fail = cb.static_fail;
   p->fail_if_rows = cb.fail_if_rows;
   hipStream_t s = p->ctx->stream;
@@ -806,7 +821,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   c->oks.ensure(std::max<size_t>(p->ntrees, 1));
   // the finalize writes the per-tree results straight into the pinned host
   // buffers (no copy launches; SRHIP_ZERO_COPY=0: device buffers + copies)
-  c->res_host = zero_copy_enabled();
+  c->res_host = zero_copy_enabled() && !c->want_device_results;
   if (c->res_host) {
     ensure_pinned(c, std::max<size_t>(p->ntrees, 1));
     c->res_sum = c->pin_sum;
@@ -1033,6 +1048,82 @@ int eval_loss_impl(srhip_dataset* ds, const srhip_program* p, int loss, const do
 }
 
 template <typename T>
+int eval_loss_packed_impl(srhip_dataset* ds, srhip_program* p, int loss, const double* params, double* d_out) {
+  srhip_ctx* c = p->ctx;
+  const int nt = p->ntrees;
+  const double wsum = ds->w ? ds->sum_w : (double)ds->rows;
+  c->want_device_results = true;
+  try {
+    run_eval<T>(c, p, MODE_LOSS, static_cast<const T*>(ds->X), static_cast<const T*>(ds->y),
+                static_cast<const T*>(ds->w), ds->rows, ds->n_pad, ds->nfeat, loss, params ? params[0] : 0.0, nullptr, 0);
+  } catch (...) {
+    c->want_device_results = false;
+    throw;
+  }
+  c->want_device_results = false;
+  if (p->verdict_stale || !p->d_verdict) {
+    std::vector<uint8_t> v((size_t)std::max(nt, 1), 0);
+    for (int t = 0; t < nt; ++t) v[t] = p->static_fail[t] ? 1 : p->fail_if_rows[t] ? 2 : 0;
+    if (!p->d_verdict) HIP_CHECK(hipMalloc((void**)&p->d_verdict, v.size()));
+    HIP_CHECK(hipMemcpyAsync(p->d_verdict, v.data(), v.size(), hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(hipStreamSynchronize(c->stream));  // v leaves scope
+    p->verdict_stale = false;
+  }
+  c->sums.ensure(std::max<size_t>(nt, 1) * sizeof(double));
+  c->oks.ensure(std::max<size_t>(nt, 1));
+  HIP_CHECK(launch_pack_partials(static_cast<const double*>(c->sums.p), static_cast<const uint8_t*>(c->oks.p),
+                                 p->d_verdict, nt, ds->rows, wsum, d_out, c->stream));
+  return SRHIP_OK;  // timing_finish once the stream is synchronised (srhip_sync / srhip_last_kernel_time)
+}
+
+// Device rows (pitch bytes apart) to the caller's contiguous host rows,
+// through the pinned staging halves: the DMA of chunk i overlaps the host
+// copy of chunk i-1 (spread over threads). A pageable destination otherwise
+// goes through the runtime's own staging, one chunk at a time (config #3's
+// 0.82 GB output: 94 ms, profiles/r02j_configs.jsonl).
+void copy_rows_to_host(srhip_ctx* c, unsigned char* dst, const unsigned char* src, size_t pitch, size_t row_bytes,
+                       int64_t nrows) {
+  hipStream_t s = c->stream;
+  const int64_t k = std::max<int64_t>(1, (int64_t)((48u << 20) / row_bytes));  // rows per chunk
+  const size_t half = (size_t)k * row_bytes;
+  if (c->stage_cap < 2 * half) {
+    if (c->pin_stage) (void)hipHostFree(c->pin_stage);
+    c->pin_stage = nullptr;
+    c->stage_cap = 0;
+    HIP_CHECK(hipHostMalloc((void**)&c->pin_stage, 2 * half, hipHostMallocDefault));
+    c->stage_cap = 2 * half;
+  }
+  for (auto& e : c->stage_ev)
+    if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  static const unsigned nthr = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+  auto host_copy = [&](unsigned char* d, const unsigned char* a, size_t n) {
+    if (n < (4u << 20) || nthr == 1) { std::memcpy(d, a, n); return; }
+    std::vector<std::thread> th;
+    const size_t per = (n + nthr - 1) / nthr;
+    for (unsigned j = 0; j < nthr; ++j) {
+      const size_t b = (size_t)j * per, e = std::min(n, b + per);
+      if (b < e) th.emplace_back([=] { std::memcpy(d + b, a + b, e - b); });
+    }
+    for (auto& t : th) t.join();
+  };
+  const int64_t nch = (nrows + k - 1) / k;
+  for (int64_t i = 0; i <= nch; ++i) {
+    if (i < nch) {
+      const int64_t r0 = i * k, nr = std::min(k, nrows - r0);
+      unsigned char* buf = c->pin_stage + (size_t)(i & 1) * half;
+      HIP_CHECK(hipMemcpy2DAsync(buf, row_bytes, src + (size_t)r0 * pitch, pitch, row_bytes, (size_t)nr,
+                                 hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipEventRecord(c->stage_ev[i & 1], s));
+    }
+    if (i > 0) {  // the previous chunk: landed in its half, then to the caller
+      const int64_t j = i - 1, r0 = j * k, nr = std::min(k, nrows - r0);
+      HIP_CHECK(hipEventSynchronize(c->stage_ev[j & 1]));
+      host_copy(dst + (size_t)r0 * row_bytes, c->pin_stage + (size_t)(j & 1) * half, (size_t)nr * row_bytes);
+    }
+  }
+}
+
+template <typename T>
 int eval_tree_array_impl(srhip_dataset* ds, const srhip_program* p, void* out, uint8_t* out_ok) {
   srhip_ctx* c = p->ctx;
   const int nt = p->ntrees;
@@ -1042,8 +1133,13 @@ int eval_tree_array_impl(srhip_dataset* ds, const srhip_program* p, void* out, u
   T* d_out = static_cast<T*>(c->gather.p);
   run_eval<T>(c, p, MODE_OUT, static_cast<const T*>(ds->X), nullptr, nullptr, rows, n_pad,
               ds->nfeat, SRHIP_LOSS_L2, 0.0, d_out, n_pad);
-  if (out && rows > 0 && nt > 0)
-    HIP_CHECK(hipMemcpy2DAsync(out, rows * es, d_out, n_pad * es, rows * es, nt, hipMemcpyDeviceToHost, c->stream));
+  if (out && rows > 0 && nt > 0) {
+    if ((size_t)rows * es * nt < (32u << 20))
+      HIP_CHECK(hipMemcpy2DAsync(out, rows * es, d_out, n_pad * es, rows * es, nt, hipMemcpyDeviceToHost, c->stream));
+    else
+      copy_rows_to_host(c, static_cast<unsigned char*>(out), reinterpret_cast<const unsigned char*>(d_out),
+                        (size_t)n_pad * es, (size_t)rows * es, nt);
+  }
   collect_results(c, p, rows, nullptr, out_ok);
   if (out) {  // rows of trees that were never run: NaN (reference: undefined)
     T* o = static_cast<T*>(out);
@@ -1349,9 +1445,12 @@ int32_t srhip_close(srhip_ctx* ctx) {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->tev)
       if (e) (void)hipEventDestroy(e);
-    for (void* h : {(void*)ctx->pin_sum, (void*)ctx->pin_ok, (void*)ctx->pin_cnt})
+    for (auto& e : ctx->stage_ev)
+      if (e) (void)hipEventDestroy(e);
+    for (void* h : {(void*)ctx->pin_sum, (void*)ctx->pin_ok, (void*)ctx->pin_cnt, (void*)ctx->pin_stage})
       if (h) (void)hipHostFree(h);
     ctx->gpart.release();
+    ctx->derived.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return SRHIP_OK;
@@ -1596,6 +1695,26 @@ int32_t srhip_eval_loss(srhip_dataset* ds, const srhip_program* prog, int32_t lo
     if (ds->dtype == SRHIP_F32)
       return eval_loss_impl<float>(ds, prog, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
     return eval_loss_impl<double>(ds, prog, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
+  });
+}
+
+int32_t srhip_eval_loss_packed(srhip_dataset* ds, srhip_program* prog, int32_t loss_kind, const double* loss_params,
+                               double* d_out) {
+  return guarded([&] {
+    check_program_vs_dataset(ds, prog);
+    if (!d_out) throw Error(SRHIP_ERR_INVALID, "null output");
+    if (loss_kind < 0 || loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
+    const bool needs_param = loss_kind == SRHIP_LOSS_LP || loss_kind == SRHIP_LOSS_HUBER ||
+                             loss_kind == SRHIP_LOSS_L1EPSINS || loss_kind == SRHIP_LOSS_L2EPSINS ||
+                             loss_kind == SRHIP_LOSS_QUANTILE || loss_kind == SRHIP_LOSS_PERIODIC;
+    if (needs_param && !loss_params) throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
+    hipPointerAttribute_t at;
+    if (hipPointerGetAttributes(&at, d_out) != hipSuccess || at.type != hipMemoryTypeDevice)
+      throw Error(SRHIP_ERR_INVALID, "d_out is not device memory");
+    std::lock_guard<std::mutex> lk(prog->ctx->mu);
+    HIP_CHECK(hipSetDevice(prog->ctx->device));
+    if (ds->dtype == SRHIP_F32) return eval_loss_packed_impl<float>(ds, prog, loss_kind, loss_params, d_out);
+    return eval_loss_packed_impl<double>(ds, prog, loss_kind, loss_params, d_out);
   });
 }
 

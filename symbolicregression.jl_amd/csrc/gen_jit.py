@@ -51,7 +51,8 @@ class JitRegs:
         self.GCAN, self.GMIN, self.GEXP = 45, 46, 47
         self.GT, self.Y = 48, 52  # guard temp block, y / loss block
         self.POOL0, self.NPOOL = 56, 8  # value blocks v56..v87
-        self.VEND = self.POOL0 + self.NPOOL * R  # first register above tree-code state
+        self.GTRIG = self.POOL0 + self.NPOOL * R  # guard: max |x| of sin / cos of a FAST-derived value
+        self.VEND = self.GTRIG + 1  # first register above tree-code state
         # SGPR state of tree code (pinned in the routine snippets so that no
         # routine uses them as temporaries)
         self.S = dict(tile=64, nt=65, partial=66, tilebytes=67, woff=68, status=69, flag=70, rr=72, tgt=74,
@@ -300,10 +301,13 @@ def manual_exp():
     (round to nearest even, |t| < 2^22), and 2^f * 2^n is a normal number,
     i.e. its bits are those of 2^f plus n << 23 — the low bits of
     t + 1.5*2^23 shifted left by 23. Two rows per v_pk_*_f32 instruction.
-    The input is not marked: an infinite x fires the exp guard (the tile is
-    redone with the PRECISE body, which marks it) and a NaN x gives a NaN
-    result (canonical NaNs: n << 23 adds nothing), which the marks downstream
-    see."""
+    The input is marked (chk) as in the compiled body: (x0, x1)*0 + (x2, x3)
+    is finite iff the four rows are. The mark is load-bearing: for an x the
+    exp guard rejects this body returns garbage, possibly a signalling NaN;
+    a later FAST exp would turn that NaN finite (its payload added by the
+    n << 23 step), and v_max3 of an sNaN drops the guard accumulators'
+    earlier values (measured: config #2 trees 1000 and 2800 kept such a
+    tile), so a non-finite exp input must redo the tile itself."""
     return ["s_mov_b32 s2, 0x3fb8aa3b",            # log2(e)
             "s_mov_b32 s4, 0x4b400000",            # 1.5 * 2^23
             "v_pk_mul_f32 v[0:1], v[32:33], s[2:3] op_sel_hi:[1,0]",   # t = x*log2e
@@ -321,9 +325,9 @@ def manual_exp():
             "v_exp_f32_e32 v9, v9",
             "v_exp_f32_e32 v10, v10",
             "v_exp_f32_e32 v11, v11",
-            # measured: the v_exp_f32 results are read too early with fewer
-            # than 3 independent instructions between (wrong rows on MI355X)
-            "s_nop 2",
+            "v_pk_fma_f32 v[12:13], v[32:33], 0, v[34:35] op_sel_hi:[1,0,1]",
+            "v_fmac_f32_e32 v40, 0, v12",
+            "v_fmac_f32_e32 v40, 0, v13",
             "v_lshl_add_u32 v32, v4, 23, v8",
             "v_lshl_add_u32 v33, v5, 23, v9",
             "v_lshl_add_u32 v34, v6, 23, v10",
@@ -546,7 +550,8 @@ def build(hipcc, outdir, R):
         f.write(f"#define SR_JIT_R {R}\n")
         for k, v in (("A", rg.A), ("B", rg.B), ("CHK", rg.CHK), ("LANE", rg.LANE), ("LSUM", rg.LSUM),
                      ("LANE4", rg.LANE4), ("CHKSAVE", rg.CHKSAVE), ("GCAN", rg.GCAN), ("GMIN", rg.GMIN),
-                     ("GEXP", rg.GEXP), ("GT", rg.GT), ("Y", rg.Y), ("POOL0", rg.POOL0), ("NPOOL", rg.NPOOL),
+                     ("GEXP", rg.GEXP), ("GTRIG", rg.GTRIG), ("GT", rg.GT), ("Y", rg.Y), ("POOL0", rg.POOL0),
+                     ("NPOOL", rg.NPOOL),
                      ("VEND", rg.VEND)):
             f.write(f"#define SR_JIT_V_{k} {v}\n")
         for k, v in rg.S.items():

@@ -175,7 +175,7 @@ struct Gen {
   std::vector<IrOp> ops;
   Opnd root;
   bool fast = false;    // this tree has a guarded FAST path
-  bool g_can = false, g_min = false, g_exp = false, has_trig = false, has_call = false;
+  bool g_can = false, g_min = false, g_exp = false, g_trig = false, has_trig = false, has_call = false;
   // allocation state
   enum { L_NONE = -1, L_A = 100, L_B = 101 };
   std::vector<int> loc;          // per value
@@ -198,6 +198,7 @@ struct Gen {
   // SRHIP_JIT_MANUAL=0 (tests): sin, cos, exp and / through the compiled
   // routines instead of the hand-scheduled packed bodies (gen_jit.py manual_*)
   bool manual_off = false;
+  bool off_exp = false, off_trig = false, off_div = false;
   static int div_rk() {
     static const int r = [] {
       for (int k = 0; k < kNumRoutines; ++k)
@@ -248,9 +249,28 @@ struct Gen {
     trig_full = tf && tf[0] == '1';
     const char* mo = std::getenv("SRHIP_JIT_MANUAL");
     manual_off = mo && mo[0] == '0';
+    // SRHIP_JIT_MANUAL_OFF=exp,trig,div (debugging): only these through the compiled routines
+    if (const char* mf = std::getenv("SRHIP_JIT_MANUAL_OFF")) {
+      const std::string l(mf);
+      off_exp = l.find("exp") != std::string::npos;
+      off_trig = l.find("trig") != std::string::npos;
+      off_div = l.find("div") != std::string::npos;
+    }
   }
 
   uint64_t cur_va() const { return base_va + as.bytes(); }
+  // sin / cos of a value that carries FAST rounding: the result's phase error
+  // grows with |x| (a 1-ulp change of x = 2^14 moves it by 2^-9), so such
+  // arguments are guarded like a cancellation
+  static bool trig_guard_on() {  // SRHIP_JIT_TRIG_GUARD=0 (experiments): no such guard
+    static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_TRIG_GUARD"); return !(e && e[0] == '0'); }();
+    return on;
+  }
+  bool trig_of_tainted(const IrOp& o) const {
+    static const bool zs_only = [] { const char* e = std::getenv("SRHIP_JIT_TRIG_GUARD_ZS"); return !(e && e[0] == '0'); }();
+    return o.un && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS) && o.a.k == O_VAL && ops[o.a.v].taint &&
+           (o.zs || !zs_only);
+  }
   int reg_of_loc(int l) const { return l == L_A ? VA : l == L_B ? VB : VPOOL0 + R * l; }
 
   bool analyze() {
@@ -265,11 +285,14 @@ struct Gen {
         if (manual_off && ((o.un && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS || o.op == SRHIP_UOP_EXP)) ||
                            (!o.un && o.op == SRHIP_BOP_DIV)))
           o.rid = full_routine(o.rid);
+        if ((off_exp && o.un && o.op == SRHIP_UOP_EXP) || (off_trig && o.un && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS)) ||
+            (off_div && !o.un && o.op == SRHIP_BOP_DIV))
+          o.rid = full_routine(o.rid);
         has_call = true;
         // a constant operand rides in s_k: the routine variant takes the other one in A
         if (!o.un && o.b.k == O_C && o.a.k != O_C && kBopRoutineRC[o.op] >= 0) o.krid = kBopRoutineRC[o.op];
         if (!o.un && o.a.k == O_C && o.b.k != O_C && kBopRoutineLC[o.op] >= 0) o.krid = kBopRoutineLC[o.op];
-        if (manual_off && o.krid >= 0 && !o.un && o.op == SRHIP_BOP_DIV) o.krid = full_routine(o.krid);
+        if ((manual_off || off_div) && o.krid >= 0 && !o.un && o.op == SRHIP_BOP_DIV) o.krid = full_routine(o.krid);
         if (kRoutineTrig[o.rid]) has_trig = true;
       }
       for (int s = 0; s < 2; ++s) {
@@ -323,6 +346,7 @@ struct Gen {
     if (fast) {
       for (auto& o : ops) {
         if (o.un && o.op == SRHIP_UOP_EXP) g_exp = true;
+        if (trig_of_tainted(o) && trig_guard_on()) g_trig = true;
         if (o.taint && o.zs) {
           if (!o.un && (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB)) g_can = true;
           if ((!o.un && (o.op == SRHIP_BOP_MUL || o.op == SRHIP_BOP_DIV)) ||
@@ -546,6 +570,11 @@ struct Gen {
         const Src g = V(VGEXP), x0 = V(VA + e), x1 = V(VA + e + 1);
         as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGEXP, g, x0, &x1, 6, 0);
       }
+    if (fast && g_trig && trig_of_tainted(o))
+      for (int e = 0; e < R; e += 2) {
+        const Src g = V(VGTRIG), x0 = V(VA + e), x1 = V(VA + e + 1);
+        as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGTRIG, g, x0, &x1, 6, 0);
+      }
     call_routine(o.rid);
     loc[i] = L_A;
     a_owner = i;
@@ -760,6 +789,7 @@ struct Gen {
     if (g_can) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGCAN, K(0xbf800000u));   // -1
     if (g_min) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGMIN, K(0x3f800000u));   // 1
     if (g_exp) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGEXP, K(0));
+    if (g_trig) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGTRIG, K(0));
     a_owner = b_owner = -1;
     for (int k = 0; k < NPOOL; ++k) pool_owner[k] = -1;
     nloads = 0;
@@ -808,16 +838,28 @@ struct Gen {
       as.branch(SOPP_SCC1, "s_cbranch_scc1", L_skip);
       as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
       as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      // the guards fire on NaN too: a FAST exp of an argument the exp guard
+      // rejects returns garbage, possibly a signalling NaN, which poisons the
+      // max3 / min3 accumulators of later guards (v_max3 of an sNaN is NaN)
       if (g_can) {
-        as.vopc(VOPC_LE_F32, "v_cmp_le_f32_e32", K(0), VGCAN);
+        as.vopc(VOPC_NGT_F32, "v_cmp_ngt_f32_e32", K(0), VGCAN);  // !(0 > max): a cancellation or NaN
         as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
       }
       if (g_min) {
-        as.vopc(VOPC_GT_F32, "v_cmp_gt_f32_e32", K(0x03800000u), VGMIN);  // 2^-120 > min|v|
+        as.vopc(VOPC_NLE_F32, "v_cmp_nle_f32_e32", K(0x03800000u), VGMIN);  // !(2^-120 <= min|v|)
         as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
       }
       if (g_exp) {
-        as.vopc(VOPC_LT_F32, "v_cmp_lt_f32_e32", K(0x42ae0000u), VGEXP);  // 87 < max|x|
+        as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(0x42ae0000u), VGEXP);  // !(87 >= max|x|)
+        as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      }
+      if (g_trig) {
+        static const uint32_t lim = [] {  // 2^k, k = SRHIP_JIT_TRIG_GUARD_LOG2 (default 20)
+          const char* e = std::getenv("SRHIP_JIT_TRIG_GUARD_LOG2");
+          const int k = e ? std::max(1, std::min(100, std::atoi(e))) : 20;
+          return (uint32_t)(127 + k) << 23;
+        }();
+        as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(lim), VGTRIG);  // !(2^k >= max|x|)
         as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
       }
       as.bind(L_skip);

@@ -29,7 +29,7 @@ constexpr int R = SR_JIT_R;
 static_assert(R == 4, "tree code is laid out for 4 rows per lane");
 constexpr int VA = SR_JIT_V_A, VB = SR_JIT_V_B, VCHK = SR_JIT_V_CHK, VLANE = SR_JIT_V_LANE;
 constexpr int VLSUM = SR_JIT_V_LSUM, VLANE4 = SR_JIT_V_LANE4, VCHKSAVE = SR_JIT_V_CHKSAVE;
-constexpr int VGCAN = SR_JIT_V_GCAN, VGMIN = SR_JIT_V_GMIN, VGEXP = SR_JIT_V_GEXP;
+constexpr int VGCAN = SR_JIT_V_GCAN, VGMIN = SR_JIT_V_GMIN, VGEXP = SR_JIT_V_GEXP, VGTRIG = SR_JIT_V_GTRIG;
 constexpr int VGT = SR_JIT_V_GT, VY = SR_JIT_V_Y, VPOOL0 = SR_JIT_V_POOL0, NPOOL = SR_JIT_V_NPOOL;
 constexpr int S_TILE = SR_JIT_S_TILE, S_NT = SR_JIT_S_NT, S_PARTIAL = SR_JIT_S_PARTIAL;
 constexpr int S_TILEBYTES = SR_JIT_S_TILEBYTES, S_WOFF = SR_JIT_S_WOFF, S_STATUS = SR_JIT_S_STATUS;
@@ -362,6 +362,7 @@ enum : int {
   VOP3_MIN3_F32 = 0x1d0, VOP3_MAX3_F32 = 0x1d3,
   VOP3P_FMA_F32 = 0x30, VOP3P_MUL_F32 = 0x31, VOP3P_ADD_F32 = 0x32, VOP3P_MOV_B32 = 0x33,
   VOPC_LT_F32 = 0x41, VOPC_LE_F32 = 0x43, VOPC_GT_F32 = 0x44, VOPC_U_F32 = 0x48, VOPC_GT_I32 = 0xc4,
+  VOPC_NGE_F32 = 0x49, VOPC_NGT_F32 = 0x4b, VOPC_NLE_F32 = 0x4c,
   SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
   SOP2_ADD_U32 = 0x00, SOP2_SUB_U32 = 0x01, SOP2_SUB_I32 = 0x03, SOP2_SUBB_U32 = 0x05, SOP2_ADDC_U32 = 0x04, SOP2_CSELECT = 0x0a,
   SOP2_AND_B32 = 0x0c,

@@ -116,6 +116,9 @@ hipError_t launch_grad_finalize(const GradArgs<T>& a, double* out_sum, uint8_t* 
 // out[cidx[k]] = Σ_rg gpart[rg][cidx[k]] in fp64 (jit_grad.cpp).
 // zero a[0..na) and b[0..nb) (uint32 words) in one launch
 hipError_t launch_zero_words(uint32_t* a, int64_t na, uint32_t* b, int64_t nb, hipStream_t stream);
+// [Σ w·ℓ, failed] per tree + Σ w into device memory (srhip_eval_loss_packed)
+hipError_t launch_pack_partials(const double* sum, const uint8_t* ok, const uint8_t* verdict, int nt, int64_t rows,
+                                double wsum, double* out, hipStream_t stream);
 hipError_t launch_gconst_finalize(const float* gpart, int nrg, int nconst, const int32_t* cidx, int ncidx,
                                   double* out, hipStream_t stream);
 

@@ -254,6 +254,37 @@ hipError_t launch_finalize(const EvalArgs<T>& a, double* out_sum, uint8_t* out_o
   return hipGetLastError();
 }
 
+namespace {
+// Row-shard partials in device memory (srhip_eval_loss_packed): per tree
+// [Σ w·ℓ (0 when failed), failed (1/0)], then Σ w — the layout the host side
+// packs for the all-reduce (srhip/distributed.py pack_partials). verdict:
+// 1 = fails statically, 2 = fails iff there are rows, 0 = the kernels decide.
+__global__ void pack_partials_kernel(const double* __restrict__ sum, const uint8_t* __restrict__ ok,
+                                     const uint8_t* __restrict__ verdict, int nt, int64_t rows, double wsum,
+                                     double* __restrict__ out) {
+  const int t = blockIdx.x * blockDim.x + threadIdx.x;
+  if (t < nt) {
+    const uint8_t v = verdict[t];
+    bool good;
+    double s = 0.0;
+    if (v == 1) good = false;
+    else if (v == 2) good = rows == 0;
+    else if (rows == 0) good = true;
+    else { good = ok[t] != 0; s = good ? sum[t] : 0.0; }
+    out[2 * (size_t)t] = s;
+    out[2 * (size_t)t + 1] = good ? 0.0 : 1.0;
+  }
+  if (t == 0) out[2 * (size_t)nt] = wsum;
+}
+}  // namespace
+
+hipError_t launch_pack_partials(const double* sum, const uint8_t* ok, const uint8_t* verdict, int nt, int64_t rows,
+                                double wsum, double* out, hipStream_t stream) {
+  const unsigned grid = (unsigned)std::max(1, (nt + 255) / 256);
+  hipLaunchKernelGGL(pack_partials_kernel, dim3(grid), dim3(256), 0, stream, sum, ok, verdict, nt, rows, wsum, out);
+  return hipGetLastError();
+}
+
 hipError_t launch_zero_words(uint32_t* a, int64_t na, uint32_t* b, int64_t nb, hipStream_t stream) {
   if (na + nb <= 0) return hipSuccess;
   const unsigned grid = (unsigned)std::min<int64_t>(1024, (na + nb + 255) / 256);

@@ -64,6 +64,7 @@ SIGNATURES = {
     "srhip_program_set_constants": [C.c_void_p, C.c_void_p],
     "srhip_eval_loss": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int64,
                         C.c_void_p, C.POINTER(C.c_double), C.c_void_p],
+    "srhip_eval_loss_packed": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p],
     "srhip_eval_loss_batch": [C.c_void_p, C.POINTER(Trees), C.c_int32, C.c_void_p, C.c_void_p,
                               C.c_int64, C.c_void_p, C.POINTER(C.c_double), C.c_void_p],
     "srhip_eval_loss_batch_ctx": [C.c_void_p, C.c_void_p, C.POINTER(Trees), C.c_int32, C.c_void_p, C.c_void_p,

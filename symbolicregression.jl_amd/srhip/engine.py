@@ -212,6 +212,14 @@ class Program:
                                     C.byref(wsum), _p(ok)))
         return sums[:nt], wsum.value, ok[:nt].astype(bool)
 
+    def eval_loss_packed(self, ds: DeviceDataset, loss_kind: int, d_out: int, params=None):
+        """srhip_eval_loss_packed: [Σw·ℓ, failed] per tree + Σw written to the
+        device buffer at address d_out (2·ntrees + 1 float64, e.g. a torch
+        tensor's data_ptr()), enqueued on the context's stream (ctx.sync()
+        before another stream reads it)."""
+        par = None if params is None else np.asarray(params, dtype=np.float64)
+        check(lib().srhip_eval_loss_packed(ds.handle, self.handle, int(loss_kind), _p(par), C.c_void_p(int(d_out))))
+
     def eval_loss_grad(self, ds: DeviceDataset, loss_kind: int, params=None):
         """(Σ w·ℓ per tree, Σ w·∂ℓ/∂c per constant [const_off order], Σw, ok)."""
         nt = self.ntrees

@@ -114,3 +114,25 @@ def test_row_sharded_engine_world2_on_one_gpu(gpu_ctx):
     assert np.mean(c0 == ref.converged) >= 0.95
     both = c0 & ref.converged
     np.testing.assert_allclose(l0[both], ref.losses[both], rtol=1e-6)
+
+
+def test_packed_partials_equal_host_packing(gpu_ctx):
+    """srhip_eval_loss_packed (device buffer for the RCCL all-reduce) writes
+    exactly pack_partials(srhip_eval_loss(...)): per-tree sums and failure
+    flags (static failures included) and Σw."""
+    import torch
+
+    from srhip import constants as K
+    from srhip.distributed import pack_partials
+
+    o, X, y, trees = _problem()
+    trees = trees[:600] + [srhip.Node(val=np.float32(np.inf)), srhip.Node(val=np.float32(1.5))]
+    ctx = gpu_ctx
+    ds = srhip.DeviceDataset(ctx, X[:, :50_001], y[:50_001])
+    prog = srhip.Program(ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32)
+    buf = torch.full((2 * len(trees) + 1,), -7.0, dtype=torch.float64, device=f"cuda:{ctx.device}")
+    prog.eval_loss_packed(ds, K.LOSS["L2"], buf.data_ptr())
+    ctx.sync()
+    s, w, ok = prog.eval_loss(ds, K.LOSS["L2"])
+    np.testing.assert_array_equal(buf.cpu().numpy(), pack_partials(s, w, ok))
+    assert not ok[600] and ok[601]

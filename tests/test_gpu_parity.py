@@ -64,6 +64,27 @@ def oracle_outputs(trees, options, X, T):
 
 
 
+def test_large_per_row_output_through_pinned_staging(gpu_ctx):
+    """eval_tree_array with an output above 32 MB goes through the pinned
+    staging halves (api.cpp copy_rows_to_host): every row of every tree
+    equals the small-copy path's (a second program on the first rows' half
+    of the trees would take that path) and the oracle's on + - * / trees."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=[])
+    trees = srhip.random_population(700, o, 5, np.float64, seed=71)
+    rng = np.random.default_rng(72)
+    X = rng.uniform(-3, 3, (5, 10_007))
+    out, ok = srhip.eval_tree_array(trees, X, o)  # 700 x 10007 x 8 B = 56 MB
+    assert out.nbytes > (32 << 20)
+    ref, ref_ok = oracle_outputs(trees, o, X, np.float64)
+    assert np.array_equal(ok, ref_ok)
+    for t in np.flatnonzero(ok):
+        assert np.array_equal(out[t], ref[t]), f"tree {t}"
+    small, ok2 = srhip.eval_tree_array(trees[:60], X, o)  # 4.8 MB: the direct copy
+    assert np.array_equal(ok2, ok[:60])
+    for t in np.flatnonzero(ok2):
+        assert np.array_equal(small[t], out[t])
+
+
 @pytest.mark.parametrize("n", [1, 100, 513, 3000])
 def test_random_trees_f32_outputs(gpu_ctx, n):
     o = srhip.Options(binary_operators=F32_OPS[0], unary_operators=F32_OPS[1])

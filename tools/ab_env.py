@@ -43,8 +43,9 @@ def child(ntrees, steps):
     for _ in range(steps):
         s, w, ok = prog.eval_loss(ds, K.LOSS["L2"])
         ks.append(ctx.last_kernel_time()[0])
+    redone = ctx.last_jit_events()[1]
     wall = (time.perf_counter() - t0) / steps * 1e3
-    print(json.dumps(dict(kernel_ms=float(np.mean(ks)), wall_ms=wall, sums=[float(v) for v in s],
+    print(json.dumps(dict(kernel_ms=float(np.mean(ks)), wall_ms=wall, redone=int(redone), sums=[float(v) for v in s],
                           ok=[int(v) for v in ok], info=prog.jit_info())))
 
 
@@ -81,7 +82,8 @@ def main():
                 bit = np.array_equal(s0[m], s1[m])
                 rel = float(np.nanmax(np.abs(s1[m] - s0[m]) / np.maximum(np.abs(s0[m]), 1e-300))) if m.any() else 0.0
                 same = f" ok_equal={okeq} bit_equal={bit} max_rel={rel:.2e}"
-            print(f"{nt:5d} trees [{var or 'default'}] kernel {d['kernel_ms']:.3f} ms, call {d['wall_ms']:.3f} ms"
+            print(f"{nt:5d} trees [{var or 'default'}] kernel {d['kernel_ms']:.3f} ms, call {d['wall_ms']:.3f} ms, "
+                  f"tiles redone {d['redone']}"
                   f"{same}", flush=True)
     return 0
 
