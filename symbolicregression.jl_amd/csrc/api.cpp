@@ -385,7 +385,7 @@ void patch_grad_constants(srhip_program* p) {
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
   tr.consts = p->consts.data();
-  CompiledBatch<T> gb = compile_batch<T>(tr, /*grad=*/true);
+  CompiledBatch<T> gb = compile_batch_par<T>(tr, /*grad=*/true);
   keep_layout(gb, p->h_gcode, p->h_gtoff, p->h_glen);
   // static verdicts may change in place: a newly failing tree keeps its old code (keep_layout)
   bool verdicts_ok = true;
@@ -416,7 +416,7 @@ void build_grad_program(srhip_program* p) {
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
   tr.consts = p->consts.data();
-  CompiledBatch<T> cb = compile_batch<T>(tr, /*grad=*/true);
+  CompiledBatch<T> cb = compile_batch_par<T>(tr, /*grad=*/true);
   if (p->ntrees >= (1 << 24)) throw Error(SRHIP_ERR_UNSUPPORTED, "too many trees for gradient work items");
   p->g_static_fail = cb.static_fail;
   p->g_opset = OPSET_BASIC;
@@ -564,7 +564,7 @@ void build_program(srhip_program* p) {
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
   tr.consts = p->consts.data();
-  CompiledBatch<T> cb = compile_batch<T>(tr);
+  CompiledBatch<T> cb = compile_batch_par<T>(tr);
   p->nodes = cb.nodes;
   p->static_fail = cb.static_fail;
   p->fail_if_rows = cb.fail_if_rows;
@@ -683,7 +683,7 @@ void update_constants(srhip_program* p) {
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
   tr.consts = p->consts.data();
-  CompiledBatch<T> cb = compile_batch<T>(tr);
+  CompiledBatch<T> cb = compile_batch_par<T>(tr);
   keep_layout(cb, p->h_code, p->h_toff, p->h_len);
   if (!same_shape(cb.code, p->h_code) || cb.tree_off != p->h_toff) {
     ++p->n_rebuild;

@@ -18,6 +18,9 @@
 #include "compile.h"
 
 #include <algorithm>
+#include <exception>
+#include <thread>
+
 #include <cmath>
 #include <cstring>
 
@@ -302,7 +305,57 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
   return cb;
 }
 
+template <typename T>
+CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad) {
+  const int nt = trees.ntrees;
+  const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
+  const int nthr = (int)std::min<unsigned>(8u, hw);
+  if (nt < 2048 || nthr < 2) return compile_batch<T>(trees, grad);
+  const int nchunk = nthr;
+  std::vector<CompiledBatch<T>> part(nchunk);
+  std::vector<std::exception_ptr> err(nchunk);
+  std::vector<std::thread> th;
+  for (int k = 0; k < nchunk; ++k) {
+    th.emplace_back([&, k] {
+      try {
+        const int t0 = (int)((int64_t)nt * k / nchunk), t1 = (int)((int64_t)nt * (k + 1) / nchunk);
+        srhip_trees v = trees;  // a view of trees [t0, t1): the offsets index the shared arrays
+        v.ntrees = t1 - t0;
+        v.node_off = trees.node_off + t0;
+        v.const_off = trees.const_off + t0;
+        part[k] = compile_batch<T>(v, grad);
+      } catch (...) {
+        err[k] = std::current_exception();
+      }
+    });
+  }
+  for (auto& t : th) t.join();
+  for (auto& e : err)
+    if (e) std::rethrow_exception(e);
+  // merge: each part ends in the kVProgMax + 1 trailing OP_ENDs, kept once at the end
+  CompiledBatch<T> cb;
+  cb.ntrees = nt;
+  const size_t tail = (size_t)kVProgMax + 1;
+  for (int k = 0; k < nchunk; ++k) {
+    CompiledBatch<T>& p = part[k];
+    const int32_t base = (int32_t)cb.code.size();
+    cb.code.insert(cb.code.end(), p.code.begin(), p.code.end() - (k + 1 < nchunk ? (std::ptrdiff_t)tail : 0));
+    for (int32_t o : p.tree_off) cb.tree_off.push_back(o < 0 ? o : o + base);
+    cb.nodes.insert(cb.nodes.end(), p.nodes.begin(), p.nodes.end());
+    cb.static_fail.insert(cb.static_fail.end(), p.static_fail.begin(), p.static_fail.end());
+    cb.fail_if_rows.insert(cb.fail_if_rows.end(), p.fail_if_rows.begin(), p.fail_if_rows.end());
+    cb.need.insert(cb.need.end(), p.need.begin(), p.need.end());
+    cb.len.insert(cb.len.end(), p.len.begin(), p.len.end());
+    cb.cost.insert(cb.cost.end(), p.cost.begin(), p.cost.end());
+    cb.max_feature = std::max(cb.max_feature, p.max_feature);
+    cb.total_nodes += p.total_nodes;
+  }
+  return cb;
+}
+
 template CompiledBatch<float> compile_batch<float>(const srhip_trees&, bool);
 template CompiledBatch<double> compile_batch<double>(const srhip_trees&, bool);
+template CompiledBatch<float> compile_batch_par<float>(const srhip_trees&, bool);
+template CompiledBatch<double> compile_batch_par<double>(const srhip_trees&, bool);
 
 }  // namespace srhip

@@ -37,4 +37,10 @@ struct CompiledBatch {
 template <typename T>
 CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad = false);
 
+// compile_batch over contiguous slices of the batch on several host threads
+// (large batches: srhip_program_set_constants recompiles every call); the
+// result is identical to compile_batch's.
+template <typename T>
+CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad = false);
+
 }  // namespace srhip

@@ -592,7 +592,8 @@ def build(hipcc, outdir, R):
         for k, v in g.items():
             f.write(f"#define SR_JIT_G_{k} {v}\n")
         gin_v = {rg.CHK, rg.LANE, rg.LSUM, rg.LANE4}
-        gclob_v = sorted((vtemp | set(range(rg.A, g["GACC"] + g["NGACC"]))) - gin_v)
+        # + one above the accumulators: the FAST forward's sin / cos argument guard (jit_grad.cpp VGTRIG_G)
+        gclob_v = sorted((vtemp | set(range(rg.A, g["GACC"] + g["NGACC"] + 1))) - gin_v)
         gin_s = {rg.S[k] for k in ("tile", "nt", "partial", "tilebytes", "woff", "status")} | \
             {g["SCPTR"], g["SCPTR"] + 1, g["SGPTR"], g["SGPTR"] + 1}
         gclob_s = sorted((stemp | sstate | set(range(g["SC0"], g["SC0"] + g["NGACC"]))) - gin_s)

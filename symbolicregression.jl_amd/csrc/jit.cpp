@@ -854,9 +854,9 @@ struct Gen {
         as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
       }
       if (g_trig) {
-        static const uint32_t lim = [] {  // 2^k, k = SRHIP_JIT_TRIG_GUARD_LOG2 (default 20)
+        static const uint32_t lim = [] {  // 2^k, k = SRHIP_JIT_TRIG_GUARD_LOG2 (default 14)
           const char* e = std::getenv("SRHIP_JIT_TRIG_GUARD_LOG2");
-          const int k = e ? std::max(1, std::min(100, std::atoi(e))) : 20;
+          const int k = e ? std::max(1, std::min(100, std::atoi(e))) : 14;
           return (uint32_t)(127 + k) << 23;
         }();
         as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(lim), VGTRIG);  // !(2^k >= max|x|)

@@ -56,6 +56,8 @@ constexpr int SGPTR = SR_JIT_G_SGPTR;  // s[84:85]: this row group's ∂L/∂c p
 constexpr int XS0 = 0, XS1 = 4;   // feature values read in the reverse pass
 constexpr int TS = 8;             // 2 registers: row sums
 constexpr int TP = 12, TR = 16, TQ = 20;  // product / reciprocal / quotient-adjoint blocks
+// guard of sin / cos arguments (FAST forward), above the accumulators
+constexpr int VGTRIG_G = GACC + NGACC;
 enum : int { VOP1_RCP_F32 = 0x22, VOPC_NEQ_F32 = 0x4d, VOP3_MUL_F32 = 0x105 };
 
 // ---- IR: the accumulator machine of a gradient program, renamed ----------------
@@ -172,9 +174,21 @@ struct GradGen {
   std::vector<int> feats;
   int nloads = 0, waited = 0;
   bool has_call = false;
-  int L_tile = -1, L_done = -1;
+  int L_tile = -1, L_done = -1, L_redo = -1;
+  // guarded FAST forward (as the loss tree code, jit.cpp): exp / sin / cos by
+  // their FAST routines; a tile whose guards fire (or that fails) runs its
+  // forward again with the PRECISE routines before the loss and the reverse
+  // pass, so did_succeed and the values the gradients see stay those of the
+  // Float64-evaluated routines wherever the FAST ones could change them
+  bool fast = false;
+  bool g_can = false, g_min = false, g_exp = false, g_trig = false;
+  std::vector<uint8_t> taint, zs;
 
   GradGen(Asm& a, const Tmpl& t, uint64_t va) : as(a), T(t), base_va(va) {}
+  bool trig_tainted_zs(const GOp& o) const {
+    return o.kind == K_UN && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS) && o.a.k == G_VAL && taint[o.a.v] &&
+           zs[&o - ops.data()];
+  }
   uint64_t cur_va() const { return base_va + as.bytes(); }
   static int blk_reg(int k) { return GPOOL0 + R * k; }
   int bstep(int i) const { return 2 * n - i; }  // reverse steps n+1 .. 2n (n: the loss)
@@ -206,6 +220,43 @@ struct GradGen {
       }
     }
     if (root.k == G_C && root.ci >= nc) { why = "constant index out of range"; return false; }
+    // FAST forward: taint (a FAST-routine value flows in), zero sensitivity
+    // (a divisor depends on it), the guards they need (jit.cpp Gen::analyze)
+    taint.assign(n, 0);
+    zs.assign(n, 0);
+    bool trans = false;
+    for (int i = 0; i < n; ++i) {
+      const GOp& o = ops[i];
+      const bool t = o.kind == K_UN && (o.op == SRHIP_UOP_EXP || o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS);
+      trans = trans || t;
+      taint[i] = t || (o.a.k == G_VAL && taint[o.a.v]) || (o.kind == K_BIN && o.b.k == G_VAL && taint[o.b.v]);
+    }
+    for (int i = n - 1; i >= 0; --i) {
+      const GOp& o = ops[i];
+      auto mark = [&](const GOpnd& q) { if (q.k == G_VAL) zs[q.v] = 1; };
+      if (o.kind == K_BIN) {
+        if (o.op == SRHIP_BOP_DIV) { mark(o.b); if (zs[i]) mark(o.a); }
+        else if (zs[i]) { mark(o.a); mark(o.b); }
+      } else if (o.kind == K_UN && zs[i] && (o.op == SRHIP_UOP_NEG || o.op == SRHIP_UOP_ABS || o.op == SRHIP_UOP_SQUARE ||
+                                               o.op == SRHIP_UOP_CUBE || o.op == SRHIP_UOP_SIN)) {
+        mark(o.a);
+      }
+    }
+    static const bool fast_env = [] { const char* e = std::getenv("SRHIP_GJIT_FAST"); return !(e && e[0] == '0'); }();
+    fast = fast_env && trans;
+    if (fast) {
+      for (int i = 0; i < n; ++i) {
+        const GOp& o = ops[i];
+        if (o.kind == K_UN && o.op == SRHIP_UOP_EXP) g_exp = true;
+        if (trig_tainted_zs(o)) g_trig = true;
+        if (taint[i] && zs[i]) {
+          if (o.kind == K_BIN && (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB)) g_can = true;
+          if ((o.kind == K_BIN && (o.op == SRHIP_BOP_MUL || o.op == SRHIP_BOP_DIV)) ||
+              (o.kind == K_UN && (o.op == SRHIP_UOP_SQUARE || o.op == SRHIP_UOP_CUBE)))
+            g_min = true;
+        }
+      }
+    }
     // reverse-pass reads of saved values (operands and own results)
     for (int i = 0; i < n; ++i) {
       const GOp& o = ops[i];
@@ -339,6 +390,20 @@ struct GradGen {
     else as.vop2(VOP2_ADD_F32, "v_add_f32_e32", GACC + ci, V(GACC + ci), TS);
   }
 
+  // ---- FAST-forward guards
+  void guard_max(int g, int reg) {  // g = max(g, |reg_e|) over the block, two rows per instruction
+    for (int e = 0; e < R; e += 2) {
+      const Src gg = V(g), x0 = V(reg + e), x1 = V(reg + e + 1);
+      as.vop3(VOP3_MAX3_F32, "v_max3_f32", g, gg, x0, &x1, 6, 0);
+    }
+  }
+  void guard_min(int reg) {
+    for (int e = 0; e < R; e += 2) {
+      const Src gg = V(VGMIN), x0 = V(reg + e), x1 = V(reg + e + 1);
+      as.vop3(VOP3_MIN3_F32, "v_min3_f32", VGMIN, gg, x0, &x1, 6, 0);
+    }
+  }
+
   // ---- forward
   bool emit_mat(int i) {
     const GOp& o = ops[i];
@@ -358,6 +423,12 @@ struct GradGen {
       a[e] = fsrc(o.a, e);
       if (o.kind == K_BIN) b[e] = fsrc(o.b, e);
     }
+    const bool gcan = fast && taint[i] && zs[i] && o.kind == K_BIN && (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB);
+    const bool gmin = fast && taint[i] && zs[i] &&
+                      ((o.kind == K_BIN && o.op == SRHIP_BOP_MUL) ||
+                       (o.kind == K_UN && (o.op == SRHIP_UOP_SQUARE || o.op == SRHIP_UOP_CUBE)));
+    if (gcan)  // t = |a| + |b| before the operands' blocks may be reused
+      for (int e = 0; e < R; ++e) as.vop3(VOP3_ADD_F32, "v_add_f32_e64", VGT + e, a[e], b[e], nullptr, 3, 0);
     // blocks dying here may hold the result (rows are independent)
     free_values_at(i);
     free_feats_at(i);
@@ -394,6 +465,17 @@ struct GradGen {
         }
       }
     }
+    if (gcan) {  // t·2^-14 - |r| <= 0 unless a cancellation: max into GCAN
+      for (int e = 0; e < R; ++e) {
+        const Src t_ = V(VGT + e), eps = S(S_EPS), r = V(d + e);
+        as.vop3(VOP3_FMA_F32, "v_fma_f32", VGT + e, t_, eps, &r, 4, 4);
+      }
+      for (int e = 0; e < R; e += 2) {
+        const Src g = V(VGCAN), t0 = V(VGT + e), t1 = V(VGT + e + 1);
+        as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGCAN, g, t0, &t1, 0, 0);
+      }
+    }
+    if (gmin) guard_min(d);
     owner[k] = i;
     loc[i] = k;
     return true;
@@ -404,22 +486,28 @@ struct GradGen {
   }
   bool emit_call(int i) {
     const GOp& o = ops[i];
+    // FAST forward: routines relative to the region base in s[S_BASE] (FAST,
+    // or PRECISE while a tile is redone); else always the PRECISE region
+    const bool prec = !fast;
     if (o.krid >= 0) {
       const bool kr = o.b.k == G_C;
       operand_to(VA, kr ? o.a : o.b);
       as.sop1(SOP1_MOV, "s_mov_b32", S_K, S(SC0 + (kr ? o.b.ci : o.a.ci)), "s" + std::to_string(S_K));
       free_values_at(i);
-      routine(o.krid, true);
+      routine(o.krid, prec);
     } else {
       operand_to(VA, o.a);
       if (o.kind == K_BIN) operand_to(VB, o.b);
       free_values_at(i);
-      routine(o.rid, true);
+      if (fast && o.kind == K_UN && o.op == SRHIP_UOP_EXP) guard_max(VGEXP, VA);
+      if (fast && g_trig && trig_tainted_zs(o)) guard_max(VGTRIG_G, VA);
+      routine(o.rid, prec);
     }
     free_feats_at(i);
     const int k = free_block();
     if (k < 0) { why = "register pool exhausted"; return false; }
     mov4(blk_reg(k), VA);
+    if (fast && taint[i] && zs[i] && o.kind == K_BIN && o.op == SRHIP_BOP_DIV) guard_min(blk_reg(k));
     owner[k] = i;
     loc[i] = k;
     return true;
@@ -614,12 +702,24 @@ struct GradGen {
     for (const GOp& o : ops)
       if (o.kind == K_UN && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS)) trig = true;
     if (has_call || trig) set_base();
+    L_redo = as.label();
+    if (fast) {
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(0), "s" + std::to_string(S_MODE));  // FAST
+      if (g_can) as.sop1(SOP1_MOV, "s_mov_b32", S_EPS, K(0x38800000u), "s" + std::to_string(S_EPS));  // 2^-14
+    }
     for (int j = 0; j < nc; ++j) as.vop1(VOP1_MOV, "v_mov_b32_e32", GACC + j, K(0));
     if (nc > 0) as.waitcnt_lgkm(0);
     as.sopc(SOPC_GE_U32, "s_cmp_ge_u32", S(S_TILE), S(S_NT));
     as.branch(SOPP_SCC1, "s_cbranch_scc1", L_done);
     // ---- tile: forward
     as.bind(L_tile);
+    if (fast) {
+      as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHKSAVE, V(VCHK));  // for a redo
+      if (g_can) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGCAN, K(0xbf800000u));   // -1
+      if (g_min) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGMIN, K(0x3f800000u));   // 1
+      if (g_exp) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGEXP, K(0));
+      if (g_trig) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGTRIG_G, K(0));
+    }
     nloads = 0;
     waited = 0;
     as.ds_read_b128(VY, VLANE, 0);
@@ -652,9 +752,41 @@ struct GradGen {
       as.vop3(VOP3_FMA_F32, "v_fma_f32", VCHK, r, z, &c, 0, 0);
     }
     wait_all();
+    if (fast) {  // FAST verdict (NaN-true checks, as jit.cpp): a failure or a guard redoes the forward
+      const int L_skip = as.label();
+      as.sopc(SOPC_LG_U32, "s_cmp_lg_u32", S(S_MODE), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_skip);
+      as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
+      as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      if (g_can) {
+        as.vopc(VOPC_NGT_F32, "v_cmp_ngt_f32_e32", K(0), VGCAN);
+        as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      }
+      if (g_min) {
+        as.vopc(VOPC_NLE_F32, "v_cmp_nle_f32_e32", K(0x03800000u), VGMIN);
+        as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      }
+      if (g_exp) {
+        as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(0x42ae0000u), VGEXP);
+        as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      }
+      if (g_trig) {
+        as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(0x46800000u), VGTRIG_G);  // 2^14
+        as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
+      }
+      as.bind(L_skip);
+    }
     // a failed tile ends the tree (no reverse pass)
     as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
     as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
+    if (fast) {  // after a redone forward: the FAST base again (the reverse pass's sin / cos), next tile FAST
+      const int L_keep = as.label();
+      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_MODE), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_keep);
+      shift_base(false);
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(0), "s" + std::to_string(S_MODE));
+      as.bind(L_keep);
+    }
     // ---- loss of the tile and the seed 2·w·r (masked rows: r = 0)
     for (int e = 0; e < R; ++e) as.vop2(VOP2_SUB_F32, "v_sub_f32_e32", VY + e, V(rreg + e), VY + e);
     free_values_at(n);
@@ -746,7 +878,18 @@ struct GradGen {
     }
     as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(S_RT), "");
     if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(S_RT) + ":" + std::to_string(S_RT + 1) + "]";
+    as.bind(L_redo);
+    if (fast) {  // the forward again with the PRECISE routines
+      as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHK, V(VCHKSAVE));
+      as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(1), "s" + std::to_string(S_MODE));
+      shift_base(true);
+      as.branch(SOPP_BRANCH, "s_branch", L_tile);
+    }
     return true;
+  }
+  void shift_base(bool up) {
+    as.sop2(up ? SOP2_ADD_U32 : SOP2_SUB_U32, up ? "s_add_u32" : "s_sub_u32", S_BASE, S(S_BASE), K((uint32_t)T.delta));
+    as.sop2(up ? SOP2_ADDC_U32 : SOP2_SUBB_U32, up ? "s_addc_u32" : "s_subb_u32", S_BASE + 1, S(S_BASE + 1), K(0));
   }
 };
 

@@ -20,6 +20,7 @@ import oracle
 import srhip
 from srhip import Node
 from srhip import constants as K
+from numerics import assert_close_conditioned, loss_spread
 
 pytestmark = pytest.mark.gpu
 
@@ -92,7 +93,7 @@ def check_grads(g, ref, S, ok_c, rtol, max_bad_frac, msg, noise=None):
     a, b = g[sel], ref[sel]
     with np.errstate(invalid="ignore"):
         err = np.abs(a - b)
-    bound = rtol * S[sel] + 1e-30 + (0 if noise is None else 64 * noise[sel])
+    bound = rtol * S[sel] + 1e-30 + (0 if noise is None else 4 * noise[sel])
     same = (a == b) | (np.isnan(a) & np.isnan(b))
     bad = ~same & ~(err <= bound)
     frac = bad.mean() if bad.size else 0.0
@@ -119,7 +120,13 @@ def test_grad_tree_code_matches_interpreter_and_oracle(gpu_ctx, opset, weighted)
     assert info0["ntrees"] == 0
     assert np.array_equal(ok1, ok0)
     assert w1 == w0
-    np.testing.assert_allclose(s1[ok1], s0[ok0], rtol=2e-5)
+    # the tree code's forward runs the guarded FAST routines (the interpreter
+    # the PRECISE ones): within 2e-5, or within 4x the tree's conditioning
+    rel = np.abs(s1 - s0) / np.abs(s0)
+    out = np.flatnonzero(ok1 & ~(rel <= 2e-5))
+    if out.size:
+        sp = loss_spread([trees[i] for i in out], o, X, y, w, np.float32, nperturb=3)
+        assert_close_conditioned(s1[out], s0[out], sp, rtol=2e-5, factor=4.0, msg="tree code vs interpreter losses")
     ok_c = np.repeat(ok1, np.diff(prog.flat.const_off))
     assert np.all(np.isnan(g1[~ok_c])) and np.all(np.isnan(g0[~ok_c]))
     S, ref, N = scales(trees, o, X, y, w, with_noise=True)
