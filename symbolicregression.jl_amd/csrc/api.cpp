@@ -126,6 +126,7 @@ struct srhip_ctx {
   int64_t last_redone = 0;  // tiles tree code redid with the PRECISE routines
   DevBuf partial, sums, oks, dloss, scratch_idx, gather, derived;
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
+  bool fail_clean = false;  // all of `fail` is zero: the finalize kernels clear the flags they read
   DevBuf ti_rec;  // threaded-interpreter records of the shallow f32 list
   DevBuf bail_list, bail_fail;  // trees whose tree code handed a tile back, and their flags
   DevBuf gpart;  // [nrg][nconst] per-row-group ∂L/∂c of the gradient tree code
@@ -745,11 +746,7 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
   if constexpr (std::is_same<T, float>::value) {
     hipStream_t s = c->stream;
     const int nj = p->nlist_j;
-    if (!jit::can_bail()) {  // no routine hands a tile back: only the counters, read with the results
-      HIP_CHECK(hipMemcpyAsync(c->pin_cnt, jit::bail_flags(p->jit) + nj, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-      c->cnt_pending = true;
-      return;
-    }
+    if (!jit::can_bail()) return;  // no routine hands a tile back: the finalize copied the counters
     std::vector<uint32_t> flags((size_t)nj + 2);
     HIP_CHECK(hipMemcpyAsync(flags.data(), jit::bail_flags(p->jit), flags.size() * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, s));
@@ -835,11 +832,22 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   const bool use_jit = std::is_same<T, float>::value && p->jit && p->nlist_j > 0 && mode == MODE_LOSS &&
                        loss == SRHIP_LOSS_L2;
   const int nj = use_jit ? p->nlist_j : 0;
-  // failure flags (and the tree code's bail flags): cleared in one launch
+  // failure flags (and the tree code's bail flags): the finalize kernels of
+  // the previous call left them clean; one clearing launch only after a new
+  // buffer, an interrupted call or a path that leaves them set (gradients,
+  // tree code that can hand tiles back)
+  const bool jit_bail = use_jit && jit::can_bail();
   if (mode == MODE_LOSS) {
-    c->fail.ensure(std::max<size_t>(nslots, 1) * sizeof(uint32_t));
-    HIP_CHECK(launch_zero_words(static_cast<uint32_t*>(c->fail.p), (int64_t)std::max<size_t>(nslots, 1),
-                                use_jit ? jit::bail_flags(p->jit) : nullptr, use_jit ? jit::flag_words(p->jit) : 0, s));
+    const size_t need = std::max<size_t>(nslots, 1) * sizeof(uint32_t);
+    if (c->fail.bytes < need) {
+      c->fail.ensure(need);
+      c->fail_clean = false;
+    }
+    if (!c->fail_clean || jit_bail)
+      HIP_CHECK(launch_zero_words(static_cast<uint32_t*>(c->fail.p), (int64_t)(c->fail.bytes / sizeof(uint32_t)),
+                                  jit_bail ? jit::bail_flags(p->jit) : nullptr, jit_bail ? jit::flag_words(p->jit) : 0,
+                                  s));
+    c->fail_clean = false;  // until every finalize of this call is enqueued
   }
   // launches: the tree-code parts (pass -1, one per code object), the shallow
   // interpreter (0), the deep interpreter (1)
@@ -937,7 +945,10 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
     timed_end(c, s, tk);
-    HIP_CHECK(launch_finalize<T>(a, c->res_sum, c->res_ok, s));
+    // the last tree-code part's finalize hands over and clears the tree code's counters
+    uint32_t* cnt = (last_jit && !jit_bail) ? jit::bail_flags(p->jit) + nj : nullptr;
+    HIP_CHECK(launch_finalize<T>(a, c->res_sum, c->res_ok, s, cnt, cnt ? c->pin_cnt : nullptr));
+    if (cnt) c->cnt_pending = true;
     static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
     if (dbg) {  // debugging only: wait for the launch to report its time
       HIP_CHECK(hipStreamSynchronize(s));
@@ -949,6 +960,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     }
     if (last_jit) rerun_bailed<T>(c, p, a, plan, nfeat, rows, loss, lparam);
   }
+  if (mode == MODE_LOSS) c->fail_clean = true;
 }
 
 // Copy per-tree results to the caller, applying the static verdicts.
@@ -1181,6 +1193,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
       if (use_gjit) {
         const int nsl_all = jit::grad_nslots(p->gjit);
         c->fail.ensure((size_t)nsl_all * sizeof(uint32_t));
+        c->fail_clean = false;  // the gradient kernels leave their flags set
         HIP_CHECK(hipMemsetAsync(c->fail.p, 0, (size_t)nsl_all * sizeof(uint32_t), s));
         c->gpart.ensure(std::max<size_t>((size_t)plans[0].nrg * nconst, 1) * sizeof(float));
         for (int k = 0; k < nparts; ++k) {
@@ -1416,7 +1429,7 @@ int32_t srhip_open(int32_t device, srhip_ctx** out_ctx) {
     c->device = device;
     hipError_t e = hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking);
     for (int i = 0; i < 4 && e == hipSuccess; ++i) e = hipEventCreate(&c->ev[i]);
-    if (e == hipSuccess) e = hipHostMalloc((void**)&c->pin_cnt, 2 * sizeof(uint32_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc((void**)&c->pin_cnt, 2 * sizeof(uint32_t), hipHostMallocCoherent);
     if (e != hipSuccess) {
       delete c;
       throw Error(SRHIP_ERR_DEVICE, std::string("stream/event creation: ") + hipGetErrorString(e));

@@ -1234,6 +1234,8 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       jit_list.insert(jit_list.end(), ch.slots.begin(), ch.slots.end());
     }
     HIP_CHECK(hipMalloc((void**)&m->d_bail, (size_t)(m->nslots + 2) * sizeof(uint32_t)));
+    // clean from the start: each call's finalize leaves the counters clean again
+    HIP_CHECK(hipMemset(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t)));
   } catch (...) {
     destroy(m);
     throw;

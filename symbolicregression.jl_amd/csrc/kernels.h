@@ -126,10 +126,13 @@ template <typename T>
 hipError_t launch_eval(const EvalPlan& plan, const EvalArgs<T>& a, int mode,
                        hipStream_t stream);
 
-// Σ over row groups of the partials → per-tree fp64 sum and ok flag.
+// Σ over row groups of the partials → per-tree fp64 sum and ok flag; clears
+// the failure flags it read (a.fail) and, given cnt, copies the two tree-code
+// counters to cnt_host and clears them.
 template <typename T>
 hipError_t launch_finalize(const EvalArgs<T>& a, double* out_sum,
-                           uint8_t* out_ok, hipStream_t stream);
+                           uint8_t* out_ok, hipStream_t stream, uint32_t* cnt = nullptr,
+                           uint32_t* cnt_host = nullptr);
 
 // Dataset packing: src rows [0, rows) in Julia (nfeat, n) column-major layout
 // (layout 0) or feature-major with row stride src_stride (layout 1) →

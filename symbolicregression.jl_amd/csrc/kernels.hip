@@ -15,10 +15,21 @@ namespace {
 
 // One workgroup per 64 slots; its 16 waves split the row groups (a fixed
 // order: the sums do not depend on timing), then wave 0 adds the 16 parts.
+// It also leaves the launch's flags clean for the next call (no clearing
+// launch per call): each slot's failure flag, and (cnt != nullptr) the tree
+// code's counters, copied to cnt_host first.
 constexpr int kFinWaves = 16;
 template <typename T>
 __global__ void __launch_bounds__(64 * kFinWaves) finalize_kernel(EvalArgs<T> a, double* __restrict__ out_sum,
-                                                                  uint8_t* __restrict__ out_ok) {
+                                                                  uint8_t* __restrict__ out_ok,
+                                                                  uint32_t* __restrict__ cnt,
+                                                                  uint32_t* __restrict__ cnt_host) {
+  if (cnt && blockIdx.x == 0 && threadIdx.x == 0) {
+    cnt_host[0] = cnt[0];
+    cnt_host[1] = cnt[1];
+    cnt[0] = 0u;
+    cnt[1] = 0u;
+  }
   __shared__ double ss[kFinWaves][64];
   __shared__ double sc[kFinWaves][64];
   const int lane = threadIdx.x & 63;
@@ -53,6 +64,7 @@ __global__ void __launch_bounds__(64 * kFinWaves) finalize_kernel(EvalArgs<T> a,
       const bool ok = !__builtin_isnan(c);
       out_sum[t] = ok ? s : __builtin_nan("");
       out_ok[t] = ok ? 1 : 0;
+      if (a.fail) a.fail[sidx] = 0u;
     }
   }
 }
@@ -247,10 +259,11 @@ bool plan_eval(int dtype, bool deep, int opset, int mode, bool weighted, int nfe
 
 template <typename T>
 hipError_t launch_finalize(const EvalArgs<T>& a, double* out_sum, uint8_t* out_ok,
-                           hipStream_t stream) {
+                           hipStream_t stream, uint32_t* cnt, uint32_t* cnt_host) {
   const int npos = a.ntg * a.tpb;
   const unsigned grid = (unsigned)((npos + 63) / 64);
-  hipLaunchKernelGGL((finalize_kernel<T>), dim3(grid), dim3(64 * kFinWaves), 0, stream, a, out_sum, out_ok);
+  hipLaunchKernelGGL((finalize_kernel<T>), dim3(grid), dim3(64 * kFinWaves), 0, stream, a, out_sum, out_ok, cnt,
+                     cnt_host);
   return hipGetLastError();
 }
 
@@ -351,7 +364,7 @@ hipError_t launch_gather_rows(const T* X, const T* y, const T* w, int nfeat, int
 }
 
 #define SR_INST(T)                                                                             \
-  template hipError_t launch_finalize<T>(const EvalArgs<T>&, double*, uint8_t*, hipStream_t); \
+  template hipError_t launch_finalize<T>(const EvalArgs<T>&, double*, uint8_t*, hipStream_t, uint32_t*, uint32_t*); \
   template hipError_t launch_pack_x<T>(const T*, int, int64_t, int64_t, int, int64_t, T*,     \
                                        int*, hipStream_t);                                    \
   template hipError_t launch_pack_vec<T>(const T*, int64_t, int64_t, T*, hipStream_t);         \

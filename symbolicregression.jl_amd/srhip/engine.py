@@ -19,7 +19,7 @@ _contexts: dict = {}
 
 
 def _p(a: Optional[np.ndarray]):
-    return None if a is None else a.ctypes.data_as(C.c_void_p)
+    return None if a is None else a.ctypes.data  # an int: ctypes passes it as void*, cheaper than data_as
 
 
 def dtype_code(dtype) -> int:
@@ -202,15 +202,15 @@ class Program:
 
     def eval_loss(self, ds: DeviceDataset, loss_kind: int, params=None, row_idx=None):
         nt = self.ntrees
-        sums = np.zeros(max(nt, 1), dtype=np.float64)
-        ok = np.zeros(max(nt, 1), dtype=np.uint8)
+        sums = np.empty(max(nt, 1), dtype=np.float64)  # the library writes every tree's entry
+        ok = np.empty(max(nt, 1), dtype=np.uint8)
         wsum = C.c_double(0)
         par = None if params is None else np.asarray(params, dtype=np.float64)
         idx = None if row_idx is None else np.ascontiguousarray(row_idx, dtype=np.int64)
         nidx = 0 if idx is None else len(idx)
         check(lib().srhip_eval_loss(ds.handle, self.handle, int(loss_kind), _p(par), _p(idx), nidx, _p(sums),
                                     C.byref(wsum), _p(ok)))
-        return sums[:nt], wsum.value, ok[:nt].astype(bool)
+        return sums[:nt], wsum.value, ok[:nt].view(bool)  # 0/1 bytes: a view, no copy
 
     def eval_loss_packed(self, ds: DeviceDataset, loss_kind: int, d_out: int, params=None):
         """srhip_eval_loss_packed: [Σw·ℓ, failed] per tree + Σw written to the

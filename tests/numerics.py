@@ -106,7 +106,7 @@ def assert_close_conditioned(actual, desired, spread, rtol, atol=0.0, factor=4.0
     tol = atol + rtol * np.abs(desired) + factor * spread
     with np.errstate(invalid="ignore"):
         bad = ~(np.abs(actual - desired) <= tol)
-    bad &= ~(np.isnan(actual) & np.isnan(desired))
+    bad &= ~(np.isnan(actual) & np.isnan(desired)) & ~(actual == desired)  # equal infinities agree
     if bad.sum() > max_bad_frac * bad.size:
         i = np.flatnonzero(bad.ravel())[:5]
         raise AssertionError(f"{msg}: {bad.sum()} of {bad.size} beyond the conditioned bound; "
