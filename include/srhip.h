@@ -173,6 +173,14 @@ int32_t srhip_dataset_info(const srhip_dataset* ds, int64_t* out_rows,
  * times afterwards. */
 int32_t srhip_program_create(srhip_ctx* ctx, int32_t dtype,
                              const srhip_trees* trees, srhip_program** out_prog);
+/* srhip_program_create with flags. SRHIP_PROGRAM_VARYING_CONSTANTS: the
+ * caller will set new constants (srhip_program_set_constants, the candidates
+ * of `optimize_constants`, src/ConstantOptimization.jl:12-19): Float32 tree
+ * code is built reading its constants from memory from the start, so no
+ * constant set ever recompiles it (without the flag the first set does). */
+#define SRHIP_PROGRAM_VARYING_CONSTANTS 1u
+int32_t srhip_program_create_ex(srhip_ctx* ctx, int32_t dtype, const srhip_trees* trees, uint32_t flags,
+                                srhip_program** out_prog);
 int32_t srhip_program_destroy(srhip_program* prog);
 /* per-tree node counts (count_nodes, = compute_complexity without a custom
  * complexity mapping, src/Complexity.jl:13-19) */

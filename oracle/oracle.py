@@ -46,8 +46,10 @@ def load(variant: str = "simd"):
         g.restype = None
     L.oracle_elem_loss_f64.argtypes = [C.c_int, vp, C.c_double, C.c_double]
     L.oracle_elem_loss_f64.restype = C.c_double
-    L.oracle_eval_grad_consts_f64.argtypes = [vp, vp, vp, i32, vp, i64, i32, vp, vp]
-    L.oracle_eval_grad_consts_f64.restype = C.c_int
+    for sfx in ("f32", "f64"):
+        f = getattr(L, f"oracle_eval_grad_consts_{sfx}")
+        f.argtypes = [vp, vp, vp, i32, vp, i64, i32, vp, vp]
+        f.restype = C.c_int
     L.oracle_max_threads.restype = C.c_int
     L.oracle_set_noise.argtypes = [C.c_double, C.c_uint64]
     L.oracle_set_noise.restype = None
@@ -124,16 +126,21 @@ def eval_loss_batch(flat, X, y, w=None, loss=0, params=(0.0,), row_idx=None, nth
     return sums[:nt], losses[:nt], ok[:nt].astype(bool)
 
 
-def eval_grad_consts(kind, arg, consts, X, nconst):
+def eval_grad_consts(kind, arg, consts, X, nconst, dtype=np.float64):
+    """Forward-mode ∂ŷ/∂c of one tree at every row: (ŷ, grad [nconst][n], ok),
+    computed in dtype (float32: every intermediate rounded as the reference's
+    Float32 evaluation rounds it)."""
     L = load()
-    Xj = julia_X(X, np.float64)
+    dt = np.dtype(dtype)
+    Xj = julia_X(X, dt)
     nfeat, n = Xj.shape
     kind = np.ascontiguousarray(kind, dtype=np.uint8)
     arg = np.ascontiguousarray(arg, dtype=np.uint16)
-    c = np.ascontiguousarray(consts, dtype=np.float64)
-    out = np.empty(n)
-    grad = np.empty((max(nconst, 1), n))
-    ok = L.oracle_eval_grad_consts_f64(_p(kind), _p(arg), _p(c), len(kind), _p(Xj), n, nfeat, _p(out), _p(grad))
+    c = np.ascontiguousarray(consts, dtype=dt)
+    out = np.empty(n, dtype=dt)
+    grad = np.empty((max(nconst, 1), n), dtype=dt)
+    ok = getattr(L, f"oracle_eval_grad_consts_{_sfx(dt)}")(_p(kind), _p(arg), _p(c), len(kind), _p(Xj), n, nfeat,
+                                                           _p(out), _p(grad))
     return out, grad[:nconst], bool(ok)
 
 

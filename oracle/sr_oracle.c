@@ -117,23 +117,35 @@ float oracle_elem_loss_f32(int loss, const double* params, float yhat, float y) 
   return elem_loss_f32(loss, params, yhat, y);
 }
 
+/* one body for both precisions: the Float32 gradient is what the reference
+ * computes for Float32 trees (every intermediate rounded to Float32) */
+#define GRAD_CONSTS_BODY(T, SFX_)                                                                  \
+  if (nnodes <= 0) return 0;                                                                       \
+  CAT(onode, SFX_)* nd = (CAT(onode, SFX_)*)malloc(sizeof(CAT(onode, SFX_)) * nnodes);            \
+  int root = CAT(parse, SFX_)(kind, arg, consts, nnodes, nd);                                      \
+  if (root < 0) { free(nd); return 0; }                                                            \
+  int nc = 0;                                                                                      \
+  for (int i = 0; i < nnodes; ++i) nc += (kind[i] == SRHIP_NODE_CONST);                            \
+  CAT(ectx, SFX_) c = {nd, X, n, nfeat};                                                           \
+  int cidx = 0;                                                                                    \
+  T* val = (T*)malloc(sizeof(T) * (size_t)(n > 0 ? n : 1));                                        \
+  T* tan = (T*)malloc(sizeof(T) * (size_t)(nc > 0 ? nc : 1) * (size_t)(n > 0 ? n : 1));            \
+  int ok = CAT(grad_rec, SFX_)(&c, root, nc, &cidx, val, tan);                                     \
+  if (out) memcpy(out, val, sizeof(T) * (size_t)n);                                                \
+  if (grad) memcpy(grad, tan, sizeof(T) * (size_t)nc * (size_t)n);                                 \
+  free(val); free(tan); free(nd);                                                                  \
+  return ok;
+
 int oracle_eval_grad_consts_f64(const uint8_t* kind, const uint16_t* arg,
                                 const double* consts, int32_t nnodes,
                                 const double* X, int64_t n, int32_t nfeat,
                                 double* out, double* grad) {
-  if (nnodes <= 0) return 0;
-  onode_f64* nd = (onode_f64*)malloc(sizeof(onode_f64) * nnodes);
-  int root = parse_f64(kind, arg, consts, nnodes, nd);
-  if (root < 0) { free(nd); return 0; }
-  int nc = 0;
-  for (int i = 0; i < nnodes; ++i) nc += (kind[i] == SRHIP_NODE_CONST);
-  ectx_f64 c = {nd, X, n, nfeat};
-  int cidx = 0;
-  double* val = (double*)malloc(sizeof(double) * (size_t)(n > 0 ? n : 1));
-  double* tan = (double*)malloc(sizeof(double) * (size_t)(nc > 0 ? nc : 1) * (size_t)(n > 0 ? n : 1));
-  int ok = grad_rec_f64(&c, root, nc, &cidx, val, tan);
-  if (out) memcpy(out, val, sizeof(double) * (size_t)n);
-  if (grad) memcpy(grad, tan, sizeof(double) * (size_t)nc * (size_t)n);
-  free(val); free(tan); free(nd);
-  return ok;
+  GRAD_CONSTS_BODY(double, _f64)
+}
+
+int oracle_eval_grad_consts_f32(const uint8_t* kind, const uint16_t* arg,
+                                const float* consts, int32_t nnodes,
+                                const float* X, int64_t n, int32_t nfeat,
+                                float* out, float* grad) {
+  GRAD_CONSTS_BODY(float, _f32)
 }

@@ -75,6 +75,12 @@ int oracle_eval_grad_consts_f64(const uint8_t* kind, const uint16_t* arg,
                                 const double* consts, int32_t nnodes,
                                 const double* X, int64_t n, int32_t nfeat,
                                 double* out, double* grad);
+/* the same in Float32 arithmetic (the reference's own precision for Float32
+ * trees; the tests measure how far it strays from the Float64 gradient) */
+int oracle_eval_grad_consts_f32(const uint8_t* kind, const uint16_t* arg,
+                                const float* consts, int32_t nnodes,
+                                const float* X, int64_t n, int32_t nfeat,
+                                float* out, float* grad);
 
 int oracle_max_threads(void);
 /* test-only rounding-noise model of the float64 evaluator (sr_oracle.c) */

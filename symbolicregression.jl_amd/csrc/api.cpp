@@ -7,6 +7,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cstdio>
 #include <cmath>
 #include <cstring>
@@ -185,6 +186,11 @@ struct srhip_program {
   // copies in place when only instruction immediates change
   std::vector<unsigned char> h_code, h_gcode;
   std::vector<int32_t> h_toff, h_gtoff, h_len, h_glen;
+  // their constant maps (CompiledBatch::cmap / direct): new constants of a
+  // tree whose immediates are its constants are written without a recompile
+  std::vector<int32_t> h_cmap, h_gcmap;
+  std::vector<uint8_t> h_direct, h_gdirect;
+  std::vector<FoldRec> h_folds, h_gfolds;
   int64_t n_inplace = 0, n_rebuild = 0;
   int opset = OPSET_FULL;      // smallest operator set covering the compiled programs
   // gradient programs (compiled on first use)
@@ -333,42 +339,108 @@ void free_program_device(srhip_program* p) {
   free_grad_device(p);
 }
 
-// Gradient programs: compiled without folding, one work item per (tree,
-// tangent group of kGradG constants), cost-sorted.
+// New constants (p->consts) into a built program image, compiling only the
+// trees that need it: a tree whose constant-derived immediates are all in the
+// constant map (direct) gets the new values written through it — a constant
+// as given, a folded subtree evaluated again (eval_fold) — as long as every
+// new constant and folded value is finite (the static verdicts then stay
+// clear); the others (static failures, non-finite values) are compiled again
+// as one small batch and must keep their instruction stream (a tree that
+// newly fails statically keeps its old code; its verdict decides its result).
+// Returns false when the layout must change (the caller rebuilds: the image
+// may then be half patched). *verdicts_changed is set when a static verdict
+// moved.
 template <typename T>
-bool same_shape(const std::vector<Ins<T>>& code, const std::vector<unsigned char>& old);
-
-// New constants that make a tree fail statically (a non-finite constant or
-// folded value) leave it without code of its own: it keeps its previous code
-// segment, so that the program layout stays the same and the update stays in
-// place (the static verdict decides the tree's result; the device evaluates
-// its stale code for nothing). Returns true when cb was rewritten.
-template <typename T>
-bool keep_layout(CompiledBatch<T>& cb, const std::vector<unsigned char>& h_code, const std::vector<int32_t>& h_toff,
-                 const std::vector<int32_t>& h_len) {
-  const int nt = cb.ntrees;
-  if ((int)h_toff.size() != nt || (int)h_len.size() != nt) return false;
-  bool kept = false;
-  for (int t = 0; t < nt; ++t)
-    if (cb.tree_off[t] < 0 && h_toff[t] >= 0) kept = true;
-  if (!kept) return false;
-  const Ins<T>* old = reinterpret_cast<const Ins<T>*>(h_code.data());
-  std::vector<Ins<T>> code;
-  code.reserve(h_code.size() / sizeof(Ins<T>));
-  std::vector<int32_t> toff(nt, -1), len(nt, 0);
+bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::vector<int32_t>& toff,
+                 const std::vector<int32_t>& len, std::vector<int32_t>& cmap, std::vector<uint8_t>& direct,
+                 std::vector<FoldRec>& folds, std::vector<uint8_t>& sfail, std::vector<uint8_t>* fir, bool grad,
+                 bool* verdicts_changed) {
+  const int nt = p->ntrees;
+  if (cmap.size() * sizeof(Ins<T>) != code.size() || (int)direct.size() != nt || (int)toff.size() != nt ||
+      (int)len.size() != nt || (int)sfail.size() != nt)
+    return false;
+  Ins<T>* ins = reinterpret_cast<Ins<T>*>(code.data());
+  const T* c = reinterpret_cast<const T*>(p->consts.data());
+  const int32_t* co = p->const_off.data();
+  srhip_trees tr;  // the program's own trees with the new constants (eval_fold)
+  tr.ntrees = nt;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = co;
+  tr.consts = c;
+  std::vector<int32_t> redo;
   for (int t = 0; t < nt; ++t) {
-    const Ins<T>* src = cb.tree_off[t] >= 0 ? &cb.code[cb.tree_off[t]] : h_toff[t] >= 0 ? old + h_toff[t] : nullptr;
-    if (!src) continue;
-    const int n = cb.tree_off[t] >= 0 ? cb.len[t] : h_len[t];
-    toff[t] = (int32_t)code.size();
-    len[t] = n;
-    code.insert(code.end(), src, src + n);
+    if (direct[t]) {
+      bool finite = true;
+      for (int k = co[t]; k < co[t + 1]; ++k) finite &= std::isfinite(c[k]);
+      for (int i = toff[t], e = toff[t] + len[t]; i < e && finite; ++i) {
+        const int32_t m = cmap[i];
+        if (m >= 0) ins[i].imm = c[m];
+        else if (m <= -2) finite = eval_fold<T>(folds[-2 - m], tr, &ins[i].imm);
+      }
+      if (finite) continue;
+    }
+    redo.push_back(t);
   }
-  // the trailing OP_ENDs of compile_batch
-  code.insert(code.end(), cb.code.end() - (kVProgMax + 1), cb.code.end());
-  cb.code.swap(code);
-  cb.tree_off.swap(toff);
-  cb.len.swap(len);
+  if (std::getenv("SRHIP_DEBUG_SETC")) std::fprintf(stderr, "srhip set_constants: %d of %d trees recompiled\n", (int)redo.size(), nt);
+  if (redo.empty()) return true;
+  const int nr = (int)redo.size();
+  std::vector<int32_t> s_noff(1, 0), s_coff(1, 0);
+  std::vector<uint8_t> s_kind;
+  std::vector<uint16_t> s_arg;
+  std::vector<T> s_c;
+  for (int32_t t : redo) {
+    const int b = p->node_off[t], e = p->node_off[t + 1];
+    s_kind.insert(s_kind.end(), p->kind.begin() + b, p->kind.begin() + e);
+    s_arg.insert(s_arg.end(), p->arg.begin() + b, p->arg.begin() + e);
+    s_c.insert(s_c.end(), c + co[t], c + co[t + 1]);
+    s_noff.push_back((int32_t)s_kind.size());
+    s_coff.push_back((int32_t)s_c.size());
+  }
+  srhip_trees sub;
+  sub.ntrees = nr;
+  sub.node_off = s_noff.data();
+  sub.kind = s_kind.data();
+  sub.arg = s_arg.data();
+  sub.const_off = s_coff.data();
+  sub.consts = s_c.data();
+  CompiledBatch<T> rb = compile_batch_par<T>(sub, grad);
+  for (int r = 0; r < nr; ++r) {
+    const int t = redo[r];
+    if (rb.tree_off[r] >= 0) {
+      if (toff[t] < 0 || rb.len[r] != len[t]) return false;
+      const Ins<T>* src = &rb.code[rb.tree_off[r]];
+      for (int j = 0; j < len[t]; ++j)
+        if (src[j].code != ins[toff[t] + j].code) return false;
+      for (int j = 0; j < len[t]; ++j) {
+        ins[toff[t] + j] = src[j];
+        const int32_t m = rb.cmap[rb.tree_off[r] + j];
+        int32_t& dst = cmap[toff[t] + j];
+        if (m >= 0) {
+          dst = co[t] + (m - s_coff[r]);
+        } else if (m <= -2) {  // the fold, in the program's numbering (reusing the slot it had)
+          const FoldRec& f = rb.folds[-2 - m];
+          const FoldRec g{p->node_off[t] + (f.node_b - s_noff[r]), p->node_off[t] + (f.node_e - s_noff[r]),
+                          co[t] + (f.const_b - s_coff[r])};
+          if (dst <= -2) {
+            folds[-2 - dst] = g;
+          } else {
+            folds.push_back(g);
+            dst = -2 - ((int32_t)folds.size() - 1);
+          }
+        } else {
+          dst = -1;
+        }
+      }
+      direct[t] = rb.direct[r];
+    } else {
+      direct[t] = 0;  // keeps its old code: the static verdict decides its result
+    }
+    if (sfail[t] != rb.static_fail[r] || (fir && (*fir)[t] != rb.fail_if_rows[r])) *verdicts_changed = true;
+    sfail[t] = rb.static_fail[r];
+    if (fir) (*fir)[t] = rb.fail_if_rows[r];
+  }
   return true;
 }
 
@@ -379,25 +451,10 @@ bool keep_layout(CompiledBatch<T>& cb, const std::vector<unsigned char>& h_code,
 template <typename T>
 void patch_grad_constants(srhip_program* p) {
   p->grad_stale = false;
-  srhip_trees tr;
-  tr.ntrees = p->ntrees;
-  tr.node_off = p->node_off.data();
-  tr.kind = p->kind.data();
-  tr.arg = p->arg.data();
-  tr.const_off = p->const_off.data();
-  tr.consts = p->consts.data();
-  CompiledBatch<T> gb = compile_batch_par<T>(tr, /*grad=*/true);
-  keep_layout(gb, p->h_gcode, p->h_gtoff, p->h_glen);
-  // static verdicts may change in place: a newly failing tree keeps its old code (keep_layout)
-  bool verdicts_ok = true;
-  for (int t = 0; t < p->ntrees && verdicts_ok; ++t)
-    if (!gb.static_fail[t] && p->g_static_fail[t]) verdicts_ok = false;  // a tree without code needs some now
-  if (same_shape(gb.code, p->h_gcode) && gb.tree_off == p->h_gtoff && verdicts_ok) {
-    p->g_static_fail = gb.static_fail;
+  bool vchg = false;  // the gradient kernels read the verdicts from the programs themselves
+  if (patch_image<T>(p, p->h_gcode, p->h_gtoff, p->h_glen, p->h_gcmap, p->h_gdirect, p->h_gfolds, p->g_static_fail,
+                     nullptr, /*grad=*/true, &vchg)) {
     hipStream_t s = p->ctx->stream;
-    HIP_CHECK(hipStreamSynchronize(s));
-    p->h_gcode.assign(reinterpret_cast<const unsigned char*>(gb.code.data()),
-                      reinterpret_cast<const unsigned char*>(gb.code.data() + gb.code.size()));
     HIP_CHECK(hipMemcpyAsync(p->d_gcode, p->h_gcode.data(), p->h_gcode.size(), hipMemcpyHostToDevice, s));
     HIP_CHECK(hipStreamSynchronize(s));
     if (p->gjit) upload_gconsts(p);
@@ -406,6 +463,8 @@ void patch_grad_constants(srhip_program* p) {
   }
 }
 
+// Gradient programs: compiled without folding, one work item per (tree,
+// tangent group of kGradG constants), cost-sorted.
 template <typename T>
 void build_grad_program(srhip_program* p) {
   if (p->grad_built && p->grad_stale) patch_grad_constants<T>(p);
@@ -504,6 +563,9 @@ void build_grad_program(srhip_program* p) {
                     reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   p->h_gtoff = cb.tree_off;
   p->h_glen = cb.len;
+  p->h_gcmap = cb.cmap;
+  p->h_gdirect = cb.direct;
+  p->h_gfolds = cb.folds;
   p->grad_built = true;
   p->grad_stale = false;
 }
@@ -644,22 +706,15 @@ void build_program(srhip_program* p) {
                    reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   p->h_toff = cb.tree_off;
   p->h_len = cb.len;
+  p->h_cmap = cb.cmap;
+  p->h_direct = cb.direct;
+  p->h_folds = cb.folds;
 }
 
-// Same instruction streams (opcodes, operands, offsets, static verdicts) up to
-// the immediates of the instructions?
-template <typename T>
-bool same_shape(const std::vector<Ins<T>>& code, const std::vector<unsigned char>& old) {
-  if (code.size() * sizeof(Ins<T>) != old.size()) return false;
-  const Ins<T>* o = reinterpret_cast<const Ins<T>*>(old.data());
-  for (size_t k = 0; k < code.size(); ++k)
-    if (code[k].code != o[k].code) return false;
-  return true;
-}
-
-// srhip_program_set_constants: recompile on the host; when only the
-// immediates moved, overwrite the device programs in place (no reallocation,
-// no list rebuild, gradient programs patched too); else rebuild.
+// srhip_program_set_constants: new immediates written into the host image
+// through its constant map (patch_image) and the device programs overwritten
+// in place (no reallocation, no list rebuild; the gradient programs are
+// patched at the next gradient call); a changed layout rebuilds.
 template <typename T>
 void update_constants(srhip_program* p) {
   if (p->jit && !p->jit_memc && !jit::memc(p->jit)) {
@@ -677,31 +732,27 @@ void update_constants(srhip_program* p) {
     return;
   }
   if (!p->jit) p->jit_allowed = false;
-  srhip_trees tr;
-  tr.ntrees = p->ntrees;
-  tr.node_off = p->node_off.data();
-  tr.kind = p->kind.data();
-  tr.arg = p->arg.data();
-  tr.const_off = p->const_off.data();
-  tr.consts = p->consts.data();
-  CompiledBatch<T> cb = compile_batch_par<T>(tr);
-  keep_layout(cb, p->h_code, p->h_toff, p->h_len);
-  if (!same_shape(cb.code, p->h_code) || cb.tree_off != p->h_toff) {
+  // same layout: the immediates and the host-side static verdicts change in
+  // place (the host image is idle: every upload of it ends in a synchronisation,
+  // and the copy is ordered after the launches that read the old programs)
+  bool vchg = false;
+  const auto t0 = std::chrono::steady_clock::now();
+  if (!patch_image<T>(p, p->h_code, p->h_toff, p->h_len, p->h_cmap, p->h_direct, p->h_folds, p->static_fail,
+                      &p->fail_if_rows, /*grad=*/false, &vchg)) {
     ++p->n_rebuild;
     build_program<T>(p);
     return;
   }
-  // same layout: the static verdicts (host side) may change with it
-  if (cb.static_fail != p->static_fail || cb.fail_if_rows != p->fail_if_rows) p->verdict_stale = true;
-  p->static_fail = cb.static_fail;
-  p->fail_if_rows = cb.fail_if_rows;
+  if (vchg) p->verdict_stale = true;
+  const auto t1 = std::chrono::steady_clock::now();
   hipStream_t s = p->ctx->stream;
-  HIP_CHECK(hipStreamSynchronize(s));  // no launch may still read the old programs / host images
-  p->h_code.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
-                   reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   HIP_CHECK(hipMemcpyAsync(p->d_code, p->h_code.data(), p->h_code.size(), hipMemcpyHostToDevice, s));
   if (p->grad_built) p->grad_stale = true;  // patched by the next gradient call (patch_grad_constants)
   HIP_CHECK(hipStreamSynchronize(s));
+  if (std::getenv("SRHIP_DEBUG_SETC"))
+    std::fprintf(stderr, "srhip set_constants: patch %.1f us, upload of %zu bytes %.1f us\n",
+                 std::chrono::duration<double, std::micro>(t1 - t0).count(), p->h_code.size(),
+                 std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t1).count());
   ++p->n_inplace;
 }
 
@@ -1608,16 +1659,23 @@ int32_t srhip_dataset_info(const srhip_dataset* ds, int64_t* out_rows, int32_t* 
 
 int32_t srhip_program_create(srhip_ctx* ctx, int32_t dtype, const srhip_trees* trees,
                              srhip_program** out_prog) {
+  return srhip_program_create_ex(ctx, dtype, trees, 0u, out_prog);
+}
+
+int32_t srhip_program_create_ex(srhip_ctx* ctx, int32_t dtype, const srhip_trees* trees, uint32_t flags,
+                                srhip_program** out_prog) {
   return guarded([&] {
     if (!ctx || !trees || !out_prog) throw Error(SRHIP_ERR_INVALID, "null argument");
     *out_prog = nullptr;
     if (dtype != SRHIP_F32 && dtype != SRHIP_F64) throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
     if (trees->ntrees < 0) throw Error(SRHIP_ERR_INVALID, "negative tree count");
+    if (flags & ~SRHIP_PROGRAM_VARYING_CONSTANTS) throw Error(SRHIP_ERR_INVALID, "unknown program flags");
     const int nt = trees->ntrees;
     auto* p = new srhip_program();
     p->ctx = ctx;
     p->dtype = dtype;
     p->ntrees = nt;
+    p->jit_memc = (flags & SRHIP_PROGRAM_VARYING_CONSTANTS) != 0;
     try {
       if (nt > 0) {
         if (!trees->node_off || !trees->const_off) throw Error(SRHIP_ERR_INVALID, "null offsets");

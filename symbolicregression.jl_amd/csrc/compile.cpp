@@ -29,13 +29,17 @@
 namespace srhip {
 namespace {
 
+constexpr int kMaxFoldDepth = 64;  // operand stack of eval_fold (deeper folds recompile)
+
 struct HNode {
   int deg;       // 0, 1, 2
   int op;        // operator id (deg >= 1)
   int feat;      // feature index (deg 0, -1 for a constant)
   int l, r;      // children
   double val;    // constant value (deg 0 const), held in T precision
-  int cidx;      // constant index in get_constants order (deg 0 const)
+  int cidx;      // constant index in get_constants order (deg 0 const); <= -2: folded (cmap fold ref)
+  int size;      // nodes in the subtree (postfix: it spans [i - size + 1, i])
+  int cpre;      // constants before the subtree's first node (tree-local)
   bool has_feature;
   int need;      // stack slots needed (Sethi–Ullman number for this machine)
 };
@@ -44,6 +48,10 @@ template <typename T>
 struct TreeCompiler {
   std::vector<HNode> nd;
   std::vector<Ins<T>>* out;
+  std::vector<int32_t>* cmap;  // parallel to out: batch-wide constant index of each immediate
+  std::vector<FoldRec>* folds;
+  int cbase = 0;               // batch-wide index of this tree's first constant
+  int nbase = 0;               // batch-wide index of this tree's first node
   bool grad = false;  // slot field carries constant indices
   bool fold_fail = false;
   int max_feat = -1;
@@ -72,7 +80,10 @@ struct TreeCompiler {
     if (!x.has_feature) {
       T v;
       if (!eval_const(i, &v)) fold_fail = true;
+      const int first = i - x.size + 1;
+      folds->push_back({nbase + first, nbase + i + 1, cbase + nd[first].cpre});
       x.deg = 0; x.feat = -1; x.val = (double)v; x.l = x.r = -1;
+      x.cidx = -2 - ((int)folds->size() - 1);  // a folded value: its cmap reference
       return;
     }
     fold(x.l);
@@ -103,12 +114,17 @@ struct TreeCompiler {
     const bool nx = opc == OP_LDX || (opc >= OP_BIN0 && variant_needs_x((opc - OP_BIN0) / SRHIP_NUM_BOPS));
     return nx ? kNeedX : 0;
   }
-  void put(int opc, int slot, int feat, T imm) {
+  void put(int opc, int slot, int feat, T imm, int32_t gidx = -1) {
     Ins<T> ins;
     std::memset(&ins, 0, sizeof(ins));
     ins.code = make_code(opc, slot, feat) | need_x(opc);
     ins.imm = imm;
     out->push_back(ins);
+    cmap->push_back(gidx);
+  }
+  // the constant operand x: its immediate and batch-wide index
+  void putc(int opc, const HNode& x, int feat) {
+    put(opc, ci(x), feat, (T)x.val, x.cidx >= 0 ? cbase + x.cidx : x.cidx <= -2 ? x.cidx : -1);
   }
   void put_feat2(int opc, int f, int g) {
     Ins<T> ins;
@@ -122,6 +138,7 @@ struct TreeCompiler {
       std::memcpy(&ins.imm, &gg, 8);
     }
     out->push_back(ins);
+    cmap->push_back(-1);
   }
 
   // Emit code leaving node i's value in acc; slots [base, ...) are free.
@@ -129,7 +146,7 @@ struct TreeCompiler {
     const HNode& x = nd[i];
     if (x.deg == 0) {
       if (x.feat >= 0) put(OP_LDX, 0, x.feat, T(0));
-      else put(OP_LDC, ci(x), 0, (T)x.val);
+      else putc(OP_LDC, x, 0);
       return;
     }
     if (x.deg == 1) {
@@ -142,24 +159,24 @@ struct TreeCompiler {
     const int op = x.op;
     if (is_leaf(L) && is_leaf(R)) {
       if (L.feat >= 0 && R.feat >= 0) put_feat2(bin_opcode(V_XX, op), L.feat, R.feat);
-      else if (L.feat >= 0) put(bin_opcode(V_XC, op), ci(R), L.feat, (T)R.val);
-      else if (R.feat >= 0) put(bin_opcode(V_CX, op), ci(L), R.feat, (T)L.val);
+      else if (L.feat >= 0) putc(bin_opcode(V_XC, op), R, L.feat);
+      else if (R.feat >= 0) putc(bin_opcode(V_CX, op), L, R.feat);
       else {  // two constants: only without folding (gradient programs)
-        put(OP_LDC, ci(L), 0, (T)L.val);
-        put(bin_opcode(V_AC, op), ci(R), 0, (T)R.val);
+        putc(OP_LDC, L, 0);
+        putc(bin_opcode(V_AC, op), R, 0);
       }
       return;
     }
     if (is_leaf(R)) {
       emit(x.l, base);
       if (R.feat >= 0) put(bin_opcode(V_AX, op), 0, R.feat, T(0));
-      else put(bin_opcode(V_AC, op), ci(R), 0, (T)R.val);
+      else putc(bin_opcode(V_AC, op), R, 0);
       return;
     }
     if (is_leaf(L)) {
       emit(x.r, base);
       if (L.feat >= 0) put(bin_opcode(V_XA, op), 0, L.feat, T(0));
-      else put(bin_opcode(V_CA, op), ci(L), 0, (T)L.val);
+      else putc(bin_opcode(V_CA, op), L, 0);
       return;
     }
     if (base >= kMaxSlots) throw Error(SRHIP_ERR_UNSUPPORTED, "tree needs more than 16 stack slots");
@@ -213,9 +230,12 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
   cb.need.assign(nt, 0);
   cb.len.assign(nt, 0);
   cb.cost.assign(nt, 0);
+  cb.direct.assign(nt, 0);
   const T* consts = static_cast<const T*>(trees.consts);
   TreeCompiler<T> tc;
   tc.out = &cb.code;
+  tc.cmap = &cb.cmap;
+  tc.folds = &cb.folds;
   tc.grad = grad;
   std::vector<int> stk;
   for (int t = 0; t < nt; ++t) {
@@ -225,21 +245,24 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
     if (ce < cb0) throw Error(SRHIP_ERR_INVALID, "bad const_off");
     tc.nd.assign(e - b, HNode{});
     tc.fold_fail = false;
+    tc.cbase = cb0;
+    tc.nbase = b;
     stk.clear();
     int ci = cb0;
     for (int i = 0; i < e - b; ++i) {
       HNode& x = tc.nd[i];
-      x.l = x.r = -1; x.op = 0; x.feat = -1; x.val = 0; x.need = 0;
+      x.l = x.r = -1; x.op = 0; x.feat = -1; x.val = 0; x.need = 0; x.cidx = -1;
+      x.cpre = ci - cb0;  // constants before this node (a subtree's first node is a leaf)
       const int kind = trees.kind[b + i];
       const int arg = trees.arg[b + i];
       switch (kind) {
         case SRHIP_NODE_CONST:
           if (ci >= ce) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": more constant leaves than constants");
           x.cidx = ci - cb0;
-          x.deg = 0; x.val = (double)consts[ci++]; x.has_feature = false;
+          x.deg = 0; x.val = (double)consts[ci++]; x.has_feature = false; x.size = 1;
           break;
         case SRHIP_NODE_FEATURE:
-          x.deg = 0; x.feat = arg; x.has_feature = true;
+          x.deg = 0; x.feat = arg; x.has_feature = true; x.size = 1;
           tc.max_feat = std::max(tc.max_feat, arg);
           break;
         case SRHIP_NODE_UNARY:
@@ -247,6 +270,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
           if (stk.empty()) throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": stack underflow");
           x.deg = 1; x.op = arg; x.l = stk.back(); stk.pop_back();
           x.has_feature = tc.nd[x.l].has_feature;
+          x.size = 1 + tc.nd[x.l].size;
           break;
         case SRHIP_NODE_BINARY:
           if (arg >= SRHIP_NUM_BOPS) throw Error(SRHIP_ERR_UNSUPPORTED, "unknown binary operator id " + std::to_string(arg));
@@ -255,6 +279,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
           x.r = stk.back(); stk.pop_back();
           x.l = stk.back(); stk.pop_back();
           x.has_feature = tc.nd[x.l].has_feature || tc.nd[x.r].has_feature;
+          x.size = 1 + tc.nd[x.l].size + tc.nd[x.r].size;
           break;
         default:
           throw Error(SRHIP_ERR_INVALID, "tree " + std::to_string(t) + ": bad node kind " + std::to_string(kind));
@@ -278,6 +303,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
       tc.emit(root, 0);
       tc.put(OP_END, 0, 0, T(0));
       cb.len[t] = (int32_t)cb.code.size() - cb.tree_off[t];
+      cb.direct[t] = 1;
       continue;
     }
     const bool root_is_leaf = tc.nd[root].deg == 0;
@@ -297,6 +323,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
     tc.emit(root, 0);
     tc.put(OP_END, 0, 0, T(0));
     cb.len[t] = (int32_t)cb.code.size() - cb.tree_off[t];
+    cb.direct[t] = 1;  // folded values are in the map too (folds)
   }
   cb.max_feature = tc.max_feat;
   // trailing OP_ENDs: the kernels prefetch one instruction past each END and
@@ -340,6 +367,11 @@ CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad) {
     CompiledBatch<T>& p = part[k];
     const int32_t base = (int32_t)cb.code.size();
     cb.code.insert(cb.code.end(), p.code.begin(), p.code.end() - (k + 1 < nchunk ? (std::ptrdiff_t)tail : 0));
+    const int32_t fbase = (int32_t)cb.folds.size();  // this part's fold references move up by fbase
+    for (auto it = p.cmap.begin(); it != p.cmap.end() - (k + 1 < nchunk ? (std::ptrdiff_t)tail : 0); ++it)
+      cb.cmap.push_back(*it <= -2 ? *it - fbase : *it);
+    cb.folds.insert(cb.folds.end(), p.folds.begin(), p.folds.end());
+    cb.direct.insert(cb.direct.end(), p.direct.begin(), p.direct.end());
     for (int32_t o : p.tree_off) cb.tree_off.push_back(o < 0 ? o : o + base);
     cb.nodes.insert(cb.nodes.end(), p.nodes.begin(), p.nodes.end());
     cb.static_fail.insert(cb.static_fail.end(), p.static_fail.begin(), p.static_fail.end());
@@ -353,9 +385,43 @@ CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad) {
   return cb;
 }
 
+template <typename T>
+bool eval_fold(const FoldRec& f, const srhip_trees& trees, T* out) {
+  T stk[kMaxFoldDepth];
+  int sp = 0;
+  const T* c = static_cast<const T*>(trees.consts) + f.const_b;
+  for (int i = f.node_b; i < f.node_e; ++i) {
+    const int arg = trees.arg[i];
+    switch (trees.kind[i]) {
+      case SRHIP_NODE_CONST:
+        if (sp == kMaxFoldDepth) return false;
+        stk[sp++] = *c++;
+        break;
+      case SRHIP_NODE_UNARY:
+        if (sp < 1) return false;
+        stk[sp - 1] = host::unop<T>(arg, stk[sp - 1]);
+        if (!std::isfinite(stk[sp - 1])) return false;
+        break;
+      case SRHIP_NODE_BINARY:
+        if (sp < 2) return false;
+        stk[sp - 2] = host::binop<T>(arg, stk[sp - 2], stk[sp - 1]);
+        --sp;
+        if (!std::isfinite(stk[sp - 1])) return false;
+        break;
+      default:
+        return false;  // a feature: not a folded subtree
+    }
+  }
+  if (sp != 1) return false;
+  *out = stk[0];
+  return true;
+}
+
 template CompiledBatch<float> compile_batch<float>(const srhip_trees&, bool);
 template CompiledBatch<double> compile_batch<double>(const srhip_trees&, bool);
 template CompiledBatch<float> compile_batch_par<float>(const srhip_trees&, bool);
 template CompiledBatch<double> compile_batch_par<double>(const srhip_trees&, bool);
+template bool eval_fold<float>(const FoldRec&, const srhip_trees&, float*);
+template bool eval_fold<double>(const FoldRec&, const srhip_trees&, double*);
 
 }  // namespace srhip

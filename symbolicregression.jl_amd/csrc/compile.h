@@ -14,6 +14,12 @@ struct Error : std::runtime_error {
   Error(int c, const std::string& m) : std::runtime_error(m), code(c) {}
 };
 
+// a folded feature-free subtree (CompiledBatch::folds)
+struct FoldRec {
+  int32_t node_b, node_e;  // postfix nodes [node_b, node_e) of the batch
+  int32_t const_b;         // batch-wide index of its first constant
+};
+
 template <typename T>
 struct CompiledBatch {
   int ntrees = 0;
@@ -27,7 +33,22 @@ struct CompiledBatch {
   std::vector<int32_t> cost;         // VALU cost estimate per row
   int max_feature = -1;              // largest feature index referenced
   int64_t total_nodes = 0;
+  // constant map (srhip_program_set_constants without a recompile): per
+  // instruction, what its immediate holds: >= 0 the batch-wide index of a
+  // constant, <= -2 the folded value of folds[-2 - m], -1 nothing; per tree,
+  // 1 when its program has code and every constant-derived immediate is in
+  // the map, so new finite constants only rewrite those immediates
+  using Fold = FoldRec;
+  std::vector<int32_t> cmap;
+  std::vector<uint8_t> direct;
+  std::vector<Fold> folds;
 };
+
+// The value of a folded subtree for the constants `consts` (batch-wide, as in
+// trees): `_eval_constant_tree`'s arithmetic, false when an operator output is
+// not finite (the tree then fails statically and needs a recompile).
+template <typename T>
+bool eval_fold(const FoldRec& f, const srhip_trees& trees, T* out);
 
 // Compile every tree of the batch. Throws srhip::Error on malformed input
 // (SRHIP_ERR_INVALID) or on operators outside the table (SRHIP_ERR_UNSUPPORTED).

@@ -206,6 +206,12 @@ bool plan_geometry(size_t esz, int R, int D, int narr, size_t part_bytes, int64_
     return e ? std::max(1, std::atoi(e)) : 0;
   }();
   const int target_wg = target_env ? target_env : target_wg_in;
+  // SRHIP_MIN_PER_GROUP (experiments) overrides the caller's minimum trees per group
+  static const int mpg_env = [] {
+    const char* e = std::getenv("SRHIP_MIN_PER_GROUP");
+    return e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  if (mpg_env) min_per_group = mpg_env;
   int ntg = (target_wg + p->nrg - 1) / p->nrg;
   // at least min_per_group trees per group, unless that leaves fewer than 2048
   // workgroups (few rows); never fewer than ~4 trees (one per wave)

@@ -175,15 +175,21 @@ function destroy(p::Program)
     p.h = C_NULL
     return nothing
 end
-function Program(trees::AbstractVector{Node{T}}, options::Options, device::Int=0) where {T}
+# varying_constants: the caller will set_constants! (the candidates of
+# optimize_constants), so Float32 tree code reads its constants from memory
+# from the start (SRHIP_PROGRAM_VARYING_CONSTANTS: no recompile on a new set)
+const PROGRAM_VARYING_CONSTANTS = UInt32(1)
+function Program(trees::AbstractVector{Node{T}}, options::Options, device::Int=0;
+                 varying_constants::Bool=false) where {T}
     node_off, kind, arg, const_off, consts = flatten(trees, options)
     h = Ref{Ptr{Cvoid}}(C_NULL)
+    flags = varying_constants ? PROGRAM_VARYING_CONSTANTS : UInt32(0)
     GC.@preserve node_off kind arg const_off consts begin
         tr = Ref(SrhipTrees(Int32(length(trees)), pointer(node_off), pointer(kind), pointer(arg),
                             pointer(const_off), Ptr{Cvoid}(pointer(consts))))
-        check(ccall((:srhip_program_create, libsrhip), Int32,
-                    (Ptr{Cvoid}, Int32, Ref{SrhipTrees}, Ptr{Ptr{Cvoid}}),
-                    context(device), dtype_code(T), tr, h))
+        check(ccall((:srhip_program_create_ex, libsrhip), Int32,
+                    (Ptr{Cvoid}, Int32, Ref{SrhipTrees}, UInt32, Ptr{Ptr{Cvoid}}),
+                    context(device), dtype_code(T), tr, flags, h))
     end
     p = Program(h[], length(trees), const_off, device)
     finalizer(destroy, p)

@@ -59,6 +59,7 @@ SIGNATURES = {
     "srhip_dataset_info": [C.c_void_p, C.POINTER(C.c_int64), C.POINTER(C.c_int32),
                            C.POINTER(C.c_double), C.POINTER(C.c_double), C.POINTER(C.c_int32)],
     "srhip_program_create": [C.c_void_p, C.c_int32, C.POINTER(Trees), C.POINTER(C.c_void_p)],
+    "srhip_program_create_ex": [C.c_void_p, C.c_int32, C.POINTER(Trees), C.c_uint32, C.POINTER(C.c_void_p)],
     "srhip_program_destroy": [C.c_void_p],
     "srhip_program_info": [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64), C.c_void_p],
     "srhip_program_set_constants": [C.c_void_p, C.c_void_p],

@@ -66,13 +66,11 @@ class EngineEvaluator:
     def __init__(self, candidates, dataset: Dataset, options: Options, device: Optional[int] = None):
         """candidates: a list of Node, or a FlatTrees batch (no Python trees)."""
         from .engine import Program
-        from .interface import compile_trees
 
         self.dev = dataset.device(device)
-        if isinstance(candidates, FlatTrees):
-            self.prog = Program(self.dev.ctx, candidates, dataset.T)
-        else:
-            self.prog = compile_trees(candidates, options, dataset.T, self.dev.ctx.device)
+        flat = candidates if isinstance(candidates, FlatTrees) else flatten(candidates, options, dtype=dataset.T)
+        # the optimiser sets new constants on every step: memory-constant tree code from the start
+        self.prog = Program(self.dev.ctx, flat, dataset.T, varying_constants=True)
         self.loss = options.elementwise_loss
         self.T = dataset.T
 
@@ -86,7 +84,7 @@ class EngineEvaluator:
         from .engine import Program
 
         sub.dev, sub.loss, sub.T = self.dev, self.loss, self.T
-        sub.prog = Program(self.dev.ctx, self.prog.flat.take(idx), self.T)
+        sub.prog = Program(self.dev.ctx, self.prog.flat.take(idx), self.T, varying_constants=True)
         return sub
 
     def loss_grad(self, consts: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:

@@ -141,9 +141,11 @@ class DeviceDataset:
 
 
 class Program:
-    """srhip_program: a compiled, device-resident batch of trees."""
+    """srhip_program: a compiled, device-resident batch of trees.
+    varying_constants (SRHIP_PROGRAM_VARYING_CONSTANTS): the caller will set
+    new constants, so Float32 tree code reads them from memory from the start."""
 
-    def __init__(self, ctx: Context, flat: FlatTrees, dtype):
+    def __init__(self, ctx: Context, flat: FlatTrees, dtype, varying_constants: bool = False):
         self.ctx = ctx
         self.dtype = np.dtype(dtype)
         self.flat = flat
@@ -158,7 +160,8 @@ class Program:
             consts.ctypes.data_as(C.c_void_p),
         )
         h = C.c_void_p()
-        check(lib().srhip_program_create(ctx.handle, dtype_code(self.dtype), C.byref(tr), C.byref(h)))
+        check(lib().srhip_program_create_ex(ctx.handle, dtype_code(self.dtype), C.byref(tr),
+                                            K.PROGRAM_VARYING_CONSTANTS if varying_constants else 0, C.byref(h)))
         self.handle = h
         self.ntrees = flat.ntrees
 

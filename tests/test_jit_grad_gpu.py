@@ -44,12 +44,15 @@ def run(trees, o, X, y, w, gjit, T=np.float32):
 
 def scales(trees, o, X, y, w, with_noise=False):
     """S_j = Σ_rows |w·2r·∂ŷ/∂c_j| and the Float64 ∂L/∂c from the oracle;
-    with_noise also returns N_j, the oracle's perturbation spread of the
-    gradient: Σ_rows of the largest move of the row's term w·2r·∂ŷ/∂c_j under
-    three 4-ulp Float32 perturbations of X and the constants, plus
-    |w·2·∂ŷ/∂c_j|·4 ulp of |ŷ|+|y| (the residual's own rounding) — how far
-    a correct Float32 evaluation may move the sum, through the residual or
-    through an ill-conditioned local partial of ∂ŷ/∂c_j."""
+    with_noise also returns N_j, the oracle's spread of the gradient: Σ_rows
+    of the largest move of the row's term w·2r·∂ŷ/∂c_j under three 4-ulp
+    Float32 perturbations of X and the constants and under the oracle's own
+    Float32 evaluation (the reference's precision: every intermediate
+    rounded, which input perturbations cannot show inside a cancellation
+    such as x5 + (x1 - x5)), plus |w·2·∂ŷ/∂c_j|·4 ulp of |ŷ|+|y| (the
+    residual's own rounding) — how far a correct Float32 evaluation may move
+    the sum, through the residual or through an ill-conditioned local
+    partial of ∂ŷ/∂c_j."""
     flat = srhip.flatten(trees, o, dtype=np.float64)
     X64, y64 = X.astype(np.float64), y.astype(np.float64)
     w64 = np.ones_like(y64) if w is None else w.astype(np.float64)
@@ -78,6 +81,12 @@ def scales(trees, o, X, y, w, with_noise=False):
                         mv = np.maximum(mv, np.abs(w64 * 2.0 * (o2 - y64) * g2 - term))
                     else:
                         mv[:] = np.inf
+                o3, g3, ok3 = oracle.eval_grad_consts(k, a, c.astype(np.float32), X, len(c), dtype=np.float32)
+                if ok3:
+                    t3 = w64 * 2.0 * (o3.astype(np.float64) - y64) * g3.astype(np.float64)
+                    mv = np.maximum(mv, np.where(np.isfinite(t3), np.abs(t3 - term), np.inf))
+                else:
+                    mv[:] = np.inf
                 N.append((dv + mv).sum(axis=1))
         S.append(np.abs(term).sum(axis=1))
         G.append(term.sum(axis=1))

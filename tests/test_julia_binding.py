@@ -83,14 +83,14 @@ def _c_kind(param):
     if "*" in p:
         return "ptr"
     ty = p.split()[0]
-    return {"int32_t": "i32", "int64_t": "i64", "double": "f64", "uint8_t": "u8"}[ty]
+    return {"int32_t": "i32", "int64_t": "i64", "double": "f64", "uint8_t": "u8", "uint32_t": "u32"}[ty]
 
 
 def _jl_kind(t):
     t = t.strip()
     if t.startswith(("Ptr{", "Ref{")) or t == "Cstring":
         return "ptr"
-    return {"Int32": "i32", "Int64": "i64", "Float64": "f64", "UInt8": "u8", "Cint": "i32"}[t]
+    return {"Int32": "i32", "Int64": "i64", "Float64": "f64", "UInt8": "u8", "UInt32": "u32", "Cint": "i32"}[t]
 
 
 def test_every_ccall_matches_the_header():
@@ -112,7 +112,7 @@ def test_every_ccall_matches_the_header():
             assert ret == "Int32" and cret == "int32_t", f"{name}: returns {ret} / {cret}"
     # the entry points the shim of INTEGRATION.md §3 needs are all bound
     for need in ("srhip_eval_loss_batch_ctx", "srhip_eval_tree_array", "srhip_eval_grad_tree_array",
-                 "srhip_eval_loss_grad", "srhip_program_create", "srhip_program_set_constants",
+                 "srhip_eval_loss_grad", "srhip_program_create_ex", "srhip_program_set_constants",
                  "srhip_dataset_create", "srhip_op_lookup", "srhip_open", "srhip_device_count"):
         assert need in seen, need
 

@@ -14,7 +14,12 @@ summed over the batch) and a predicted kernel time:
   cycles per launch = sum over trees of cycles(tree) x tiles per row group
                       x row groups, / (1024 SIMDs x f_clk)
 
-Usage: python tools/census.py [--ntrees 4096] [--ops cfg2] [--json out.json]
+With --grad the gradient tree code (jit_grad.cpp) of config #5's shard is
+walked instead (forward, loss, reverse pass of one interior tile; defaults
+16384 trees x 20 features x 1.25M rows), routines by name, the tree's own
+code split into forward ("tree") and everything after the loss ("reverse").
+
+Usage: python tools/census.py [--ntrees 4096] [--grad] [--json out.json]
 """
 import argparse
 import collections
@@ -94,7 +99,7 @@ def disassemble(path):
 BYPLACE = collections.Counter()
 
 
-def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000):
+def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000, grad_split=False):
     """One interior tile of one tree: (prologue counts, tile counts).
     attrib (Counter) collects SIMD cycles per routine name / 'tree'."""
     pro, tile = collections.Counter(), collections.Counter()
@@ -182,6 +187,8 @@ def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000):
             continue
         if m == "s_add_u32" and ops[0] == "s74" and ops[1] == "s86":
             call_target = fast0 + int(ops[2], 0)
+        if grad_split and m == "s_cmp_eq_u32" and ops[0] == "s68" and where == ["tree"]:
+            where[0] = "reverse"  # the loss tail: everything after it is loss + reverse pass
         if m == "s_setpc_b64":
             if ret_stack:
                 pc = ret_stack.pop()
@@ -194,18 +201,27 @@ def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--ntrees", type=int, default=4096)
-    ap.add_argument("--seed", type=int, default=1000)
-    ap.add_argument("--rows", type=int, default=1_000_000)
-    ap.add_argument("--nfeat", type=int, default=5)
+    ap.add_argument("--ntrees", type=int, default=0)
+    ap.add_argument("--seed", type=int, default=-1)
+    ap.add_argument("--rows", type=int, default=0)
+    ap.add_argument("--nfeat", type=int, default=0)
+    ap.add_argument("--grad", action="store_true", help="the gradient tree code of config #5's shard")
     ap.add_argument("--fclk", type=float, default=2.4e9)
     ap.add_argument("--json", default="")
     ap.add_argument("--by-place", action="store_true", help="per routine / tree-code opcode counts")
     args = ap.parse_args()
+    dflt = dict(ntrees=16384, seed=5, rows=1_250_000, nfeat=20) if args.grad else \
+        dict(ntrees=4096, seed=1000, rows=1_000_000, nfeat=5)
+    for k, v in dflt.items():
+        if getattr(args, k) in (0, -1):
+            setattr(args, k, v)
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
-    trees = srhip.random_population(args.ntrees, o, args.nfeat, np.float32, seed=args.seed, maxsize=30)
+    if args.grad:  # tools/prof_grad.py's batch
+        trees = srhip.random_population(args.ntrees, o, args.nfeat, np.float32, seed=args.seed)
+    else:
+        trees = srhip.random_population(args.ntrees, o, args.nfeat, np.float32, seed=args.seed, maxsize=30)
     flat = srhip.flatten(trees, o, dtype=np.float32)
-    code, _, offs = srhip.engine.jit_compile(flat, fast=True)
+    code, _, offs = srhip.engine.jit_compile(flat, fast=True, grad=args.grad)
     tmpl = GEN / "jit_tmpl_l.hsaco"
     syms = readelf_syms(tmpl)
     taddr, toff = text_section(tmpl)
@@ -225,7 +241,7 @@ def main():
     per_tree = []
     for t, off in sorted(offs.items()):
         before = dict(attrib)
-        pro, tile = walk(ins, area + off, fast0, names, attrib)
+        pro, tile = walk(ins, area + off, fast0, names, attrib, grad_split=args.grad)
         tot_tile.update(tile)
         tot_pro.update(pro)
         cyc = sum(COST[vclass(k)] * v for k, v in tile.items() if k.startswith("v_"))
