@@ -42,12 +42,12 @@ GEN = ROOT / "symbolicregression.jl_amd" / "csrc" / "gen"
 # SIMD cycles per wave64 instruction, >= 2 waves per SIMD (profiles/r03a_issue_rate.txt)
 COST = {
     "pk": 4.25,      # v_pk_{add,mul,fma}_f32, v_pk_mov_b32
-    "f32": 2.2,      # v_{add,sub,subrev,mul,fma,fmac}_f32 (VOP2 / VOP3)
+    "f32": 2.2,      # v_{add,sub,subrev,mul,fma,fmac}_f32 (VOP2 / VOP3), v_mov_b32, v_xor_b32, v_add_u32
     "trans": 8.1,    # v_exp/rcp/log/sqrt/rsq/sin/cos_f32: 8 cycles, NOT hidden behind other VALU
     "f64": 4.2,      # v_fma_f64, v_mul_f64, v_add_f64
     "other": 4.2,    # integer, v_max3/min3, v_cmp, v_cndmask, conversions
 }
-F32 = re.compile(r"^v_(add|sub|subrev|mul|fma|fmac|mac)_f32")
+F32 = re.compile(r"^v_(add|sub|subrev|mul|fma|fmac|mac)_f32|^v_mov_b32|^v_xor_b32|^v_add_u32")
 TRANS = re.compile(r"^v_(exp|rcp|log|sqrt|rsq|sin|cos)_f32")
 
 
@@ -99,9 +99,11 @@ def disassemble(path):
 BYPLACE = collections.Counter()
 
 
-def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000, grad_split=False):
+def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000, grad_split=False, epi=None):
     """One interior tile of one tree: (prologue counts, tile counts).
-    attrib (Counter) collects SIMD cycles per routine name / 'tree'."""
+    attrib (Counter) collects SIMD cycles per routine name / 'tree'. With epi
+    (a Counter) the walk goes on after the tile loop and counts the tree's
+    epilogue there."""
     pro, tile = collections.Counter(), collections.Counter()
     where = ["tree"]
     cur = pro
@@ -146,9 +148,11 @@ def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000, grad_spli
                 scc = False  # tiles remain
                 prev_cmp_tile = True
             elif m == "s_cmp_lt_u32" and a == "s64":
-                scc = True   # loop back: the tile ends here
-                cur["S:" + m] += 0
-                return pro, tile
+                if epi is None:
+                    scc = True   # loop back: the tile ends here
+                    return pro, tile
+                scc = False  # the last tile: walk on through the tree's epilogue
+                cur = epi
             elif m == "s_cmp_eq_u32" and a == "s82":
                 scc = False  # not the last tile
             elif m == "s_cmp_lg_u64":
@@ -195,6 +199,8 @@ def walk(ins, entry, fast0, names=None, attrib=None, max_steps=100000, grad_spli
                 where.pop()
                 continue
             return pro, tile  # the tree returned (failed or done)
+        if m == "s_endpgm":
+            return pro, tile
         pc = nxt
     raise RuntimeError("walk did not finish")
 
@@ -237,11 +243,11 @@ def main():
     names = {v: k[len("sr_rt_fast_"):] for k, v in syms.items() if k.startswith("sr_rt_fast_")}
     attrib = collections.Counter()
     calls = collections.Counter()
-    tot_tile, tot_pro = collections.Counter(), collections.Counter()
+    tot_tile, tot_pro, tot_epi = collections.Counter(), collections.Counter(), collections.Counter()
     per_tree = []
     for t, off in sorted(offs.items()):
         before = dict(attrib)
-        pro, tile = walk(ins, area + off, fast0, names, attrib, grad_split=args.grad)
+        pro, tile = walk(ins, area + off, fast0, names, attrib, grad_split=args.grad, epi=tot_epi)
         tot_tile.update(tile)
         tot_pro.update(pro)
         cyc = sum(COST[vclass(k)] * v for k, v in tile.items() if k.startswith("v_"))
@@ -277,6 +283,14 @@ def main():
                                                for k, v in attrib.most_common()))
     print(f"VALU per tile of all trees: {nval} (ds {nds - nval if False else nds}, salu+branch {nsalu})")
     print("SIMD cycles by class: " + ", ".join(f"{k} {v:.0f} ({100 * v / tot_cyc:.1f}%)" for k, v in by_class.most_common()))
+    def cyc(cn):
+        return sum(COST[vclass(k)] * v for k, v in cn.items() if k.startswith("v_"))
+    print(f"per call of every tree (once per row group): prologue {cyc(tot_pro):.0f} SIMD-cycles "
+          f"({sum(v for k, v in tot_pro.items() if k.startswith('v_'))} VALU, "
+          f"{sum(v for k, v in tot_pro.items() if k.startswith('S:'))} SALU/branch), epilogue {cyc(tot_epi):.0f} "
+          f"({sum(v for k, v in tot_epi.items() if k.startswith('v_'))} VALU, "
+          f"{sum(v for k, v in tot_epi.items() if k.startswith('S:'))} SALU/branch, "
+          f"{tot_epi.get('S:s_nop', 0)} s_nop); per tile {tot_cyc:.0f}")
     print(f"predicted VALU-issue time for {args.rows} rows: {pred_ms:.3f} ms at f_clk {args.fclk / 1e9:.2f} GHz; "
           f"{pred_valu / 1e9:.3f}e9 VALU wave-instructions per launch (tile bodies only)")
     if args.json:

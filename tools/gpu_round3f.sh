@@ -21,3 +21,5 @@ print("recompiled median", st.median(r for r, _ in rc), "max", max(r for r, _ in
 PY
 timeout -k 10 300 python -u tools/prof_constopt.py > gpurun_out/constopt_profile.txt 2>&1 || exit 1
 head -25 gpurun_out/constopt_profile.txt
+SRHIP_DEBUG_PASSES=1 timeout -k 10 300 python -u tools/prof_grad.py 3 > gpurun_out/prof_grad_dbg.json 2> gpurun_out/prof_grad_dbg.err || exit 1
+cat gpurun_out/prof_grad_dbg.json; grep "grad tree code" gpurun_out/prof_grad_dbg.err | tail -4

@@ -31,6 +31,6 @@ for _ in range(steps):
     prog.eval_loss_grad(ds, K.LOSS["L2"])
     ks.append(ctx.last_kernel_time())
 k_ms = float(np.median([k[0] for k in ks]))
-print(json.dumps({"tool": "prof_grad", "trees": nt, "rows": rows, "nodes": int(nodes),
+print(json.dumps({"tool": "prof_grad", "trees": nt, "rows": rows, "nodes": int(nodes), "grad_jit": prog.grad_jit_info(),
                   "constants": int(prog.flat.const_off[-1]), "kernel_ms": k_ms, "launches": ks[-1][1],
                   "node_rows_per_s": nodes * rows / (k_ms * 1e-3)}))
