@@ -7,11 +7,13 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <chrono>
 #include <cstdio>
 #include <cmath>
 #include <cstring>
 #include <cstdlib>
+#include <memory>
 #include <mutex>
 #include <type_traits>
 #include <numeric>
@@ -120,7 +122,7 @@ struct srhip_ctx {
   // halves, DMA into one while the other is copied to the caller's memory
   unsigned char* pin_stage = nullptr;
   size_t stage_cap = 0;
-  hipEvent_t stage_ev[2] = {nullptr, nullptr};
+  std::vector<hipEvent_t> stage_evs;  // one per chunk of a staged copy
   double last_ms = 0.0;
   int last_launches = 0;
   int last_bailed = 0;  // trees re-evaluated after their tree code handed a tile back
@@ -857,6 +859,47 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
   }
 }
 
+// Compute units of the context's device (queried once).
+int device_cus(const srhip_ctx* c) {
+  static int cus[64] = {0};
+  const int d = c->device;
+  if (d < 0 || d >= 64) return 256;
+  if (!cus[d]) {
+    int v = 0;
+    if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) v = 256;
+    cus[d] = v;
+  }
+  return cus[d];
+}
+
+// Tree-code grids whose workgroups fill a whole number of rounds of the
+// device's resident workgroups plus a fraction f of one: the last round
+// would run with most of the device idle. The row groups past the whole
+// rounds are cut into single tiles instead (a quarter of the work each),
+// when their rounds, ceil(f·ntiles)/ntiles, come to less than a full one.
+// Rounds are counted at 5 waves per SIMD (the tree code's 94 VGPRs, LDS per
+// workgroup sized to match: jit::lds_per_workgroup). SRHIP_JIT_TAIL=0 keeps
+// every row group whole.
+void tail_split(const srhip_ctx* c, EvalPlan* plan, int64_t rows, int jw) {
+  static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_TAIL"); return !(e && e[0] == '0'); }();
+  if (!on || plan->ntiles < 2 || rows <= 0) return;
+  const int64_t conc = (int64_t)device_cus(c) * std::max(1, 20 / jw);
+  const int64_t W = (int64_t)plan->nrg * plan->ntg;
+  const int64_t full = W / conc;
+  const int64_t rest = W - full * conc;  // workgroups of the last, partial round
+  if (full < 1 || rest == 0) return;
+  // row groups in the whole rounds (the remaining ones become single tiles)
+  const int64_t nbig = full * conc / plan->ntg;
+  const int64_t left_rows = rows - nbig * (int64_t)plan->rows_wg;
+  if (nbig < 1 || left_rows <= 0) return;
+  const int64_t nsmall = (left_rows + plan->tile - 1) / plan->tile;
+  const int64_t small_rounds_x = (nsmall * plan->ntg + conc - 1) / conc;  // rounds of single-tile groups
+  if (small_rounds_x >= plan->ntiles) return;  // no shorter than one more round of whole groups
+  plan->nbig = (int)nbig;
+  plan->ts = 1;
+  plan->nrg = (int)(nbig + nsmall);
+}
+
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
 // n_pad) may be the dataset itself or a gathered row subset.
 template <typename T>
@@ -941,6 +984,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
                          16384 * 4 / jw, 64 * jw / 4))
         throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
       plan.threads = 64 * jw;
+      tail_split(c, &plan, rows, jw);
     } else if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan)) {
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
     }
@@ -1141,9 +1185,9 @@ int eval_loss_packed_impl(srhip_dataset* ds, srhip_program* p, int loss, const d
 
 // Device rows (pitch bytes apart) to the caller's contiguous host rows,
 // through the pinned staging halves: the DMA of chunk i overlaps the host
-// copy of chunk i-1 (spread over threads). A pageable destination otherwise
-// goes through the runtime's own staging, one chunk at a time (config #3's
-// 0.82 GB output: 94 ms, profiles/r02j_configs.jsonl).
+// copy of chunk i-1 (spread over persistent threads). A pageable destination
+// otherwise goes through the runtime's own staging, one chunk at a time
+// (config #3's 0.82 GB output: 94 ms, profiles/r02j_configs.jsonl).
 void copy_rows_to_host(srhip_ctx* c, unsigned char* dst, const unsigned char* src, size_t pitch, size_t row_bytes,
                        int64_t nrows) {
   hipStream_t s = c->stream;
@@ -1156,34 +1200,65 @@ void copy_rows_to_host(srhip_ctx* c, unsigned char* dst, const unsigned char* sr
     HIP_CHECK(hipHostMalloc((void**)&c->pin_stage, 2 * half, hipHostMallocDefault));
     c->stage_cap = 2 * half;
   }
-  for (auto& e : c->stage_ev)
-    if (!e) HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-  static const unsigned nthr = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
-  auto host_copy = [&](unsigned char* d, const unsigned char* a, size_t n) {
-    if (n < (4u << 20) || nthr == 1) { std::memcpy(d, a, n); return; }
-    std::vector<std::thread> th;
-    const size_t per = (n + nthr - 1) / nthr;
-    for (unsigned j = 0; j < nthr; ++j) {
-      const size_t b = (size_t)j * per, e = std::min(n, b + per);
-      if (b < e) th.emplace_back([=] { std::memcpy(d + b, a + b, e - b); });
-    }
-    for (auto& t : th) t.join();
-  };
   const int64_t nch = (nrows + k - 1) / k;
-  for (int64_t i = 0; i <= nch; ++i) {
-    if (i < nch) {
-      const int64_t r0 = i * k, nr = std::min(k, nrows - r0);
-      unsigned char* buf = c->pin_stage + (size_t)(i & 1) * half;
-      HIP_CHECK(hipMemcpy2DAsync(buf, row_bytes, src + (size_t)r0 * pitch, pitch, row_bytes, (size_t)nr,
-                                 hipMemcpyDeviceToHost, s));
-      HIP_CHECK(hipEventRecord(c->stage_ev[i & 1], s));
-    }
-    if (i > 0) {  // the previous chunk: landed in its half, then to the caller
-      const int64_t j = i - 1, r0 = j * k, nr = std::min(k, nrows - r0);
-      HIP_CHECK(hipEventSynchronize(c->stage_ev[j & 1]));
-      host_copy(dst + (size_t)r0 * row_bytes, c->pin_stage + (size_t)(j & 1) * half, (size_t)nr * row_bytes);
-    }
+  while ((int64_t)c->stage_evs.size() < nch) {
+    hipEvent_t e;
+    HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    c->stage_evs.push_back(e);
   }
+  // host copy threads: SRHIP_COPY_THREADS, default 16 (the CPU share of one
+  // GPU on the target hosts; first-touch page faults of the caller's fresh
+  // buffer are most of the cost: 0.82 GB in 43 ms on 16 threads, 63 ms on 8,
+  // profiles/r03_hostcopy.txt)
+  static const unsigned nthr = [] {
+    const char* e = std::getenv("SRHIP_COPY_THREADS");
+    const unsigned want = e ? (unsigned)std::max(1, std::atoi(e)) : 16u;
+    return std::max(1u, std::min(want, std::max(1u, std::thread::hardware_concurrency())));
+  }();
+  // workers copy their stripe of each chunk once its DMA has landed; the DMA of
+  // chunk i reuses the half of chunk i-2 after every worker is done with it
+  std::atomic<int64_t> recorded{-1};
+  std::atomic<bool> failed{false};
+  std::unique_ptr<std::atomic<unsigned>[]> done(new std::atomic<unsigned>[(size_t)nch]);
+  for (int64_t i = 0; i < nch; ++i) done[i].store(0);
+  auto worker = [&](unsigned j) {
+    if (hipSetDevice(c->device) != hipSuccess) { failed = true; return; }
+    for (int64_t i = 0; i < nch; ++i) {
+      while (recorded.load(std::memory_order_acquire) < i) {
+        if (failed.load()) return;
+        std::this_thread::yield();
+      }
+      if (hipEventSynchronize(c->stage_evs[i]) != hipSuccess) { failed = true; return; }
+      const int64_t r0 = i * k, nr = std::min(k, nrows - r0);
+      const size_t n = (size_t)nr * row_bytes;
+      const size_t per = ((n + nthr - 1) / nthr + 63) / 64 * 64;
+      const size_t b0 = std::min(n, (size_t)j * per), e0 = std::min(n, b0 + per);
+      if (b0 < e0) std::memcpy(dst + (size_t)r0 * row_bytes + b0, c->pin_stage + (size_t)(i & 1) * half + b0, e0 - b0);
+      done[i].fetch_add(1, std::memory_order_release);
+    }
+  };
+  std::vector<std::thread> th;
+  try {
+    for (unsigned j = 0; j < nthr; ++j) th.emplace_back(worker, j);
+    for (int64_t i = 0; i < nch; ++i) {
+      if (i >= 2)
+        while (done[i - 2].load(std::memory_order_acquire) < nthr) {
+          if (failed.load()) throw Error(SRHIP_ERR_DEVICE, "host copy of the per-row outputs failed");
+          std::this_thread::yield();
+        }
+      const int64_t r0 = i * k, nr = std::min(k, nrows - r0);
+      HIP_CHECK(hipMemcpy2DAsync(c->pin_stage + (size_t)(i & 1) * half, row_bytes, src + (size_t)r0 * pitch, pitch,
+                                 row_bytes, (size_t)nr, hipMemcpyDeviceToHost, s));
+      HIP_CHECK(hipEventRecord(c->stage_evs[i], s));
+      recorded.store(i, std::memory_order_release);
+    }
+  } catch (...) {
+    failed = true;
+    for (auto& t : th) t.join();
+    throw;
+  }
+  for (auto& t : th) t.join();
+  if (failed.load()) throw Error(SRHIP_ERR_DEVICE, "host copy of the per-row outputs failed");
 }
 
 template <typename T>
@@ -1509,7 +1584,7 @@ int32_t srhip_close(srhip_ctx* ctx) {
       if (e) (void)hipEventDestroy(e);
     for (auto& e : ctx->tev)
       if (e) (void)hipEventDestroy(e);
-    for (auto& e : ctx->stage_ev)
+    for (auto& e : ctx->stage_evs)
       if (e) (void)hipEventDestroy(e);
     for (void* h : {(void*)ctx->pin_sum, (void*)ctx->pin_ok, (void*)ctx->pin_cnt, (void*)ctx->pin_stage})
       if (h) (void)hipHostFree(h);

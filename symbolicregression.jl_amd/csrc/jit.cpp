@@ -1280,6 +1280,7 @@ struct JitArgs {
   int nraw, nder;
   uint32_t der[kMaxDerived];
   const float* dcols;
+  int nbig, ts;
 };
 struct DeriveArgs {
   const float* X;
@@ -1324,7 +1325,10 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   ja.nder = m->cols.nder;
   std::memcpy(ja.der, m->cols.der, sizeof(ja.der));
   ja.dcols = dcols;
+  ja.nbig = plan.nbig >= 0 ? plan.nbig : a.nrg;
+  ja.ts = plan.nbig >= 0 ? plan.ts : plan.ntiles;
   if (ja.nraw > a.nfeat) return hipErrorInvalidValue;
+  if (ja.nbig > a.nrg || ja.ts < 1 || ja.ts > plan.ntiles) return hipErrorInvalidValue;
   // partials in LDS when they take little room next to the tiles (measured
   // faster on config #2: one coalesced write-out instead of a store per tree)
   const size_t part_bytes = (size_t)a.tpb * sizeof(Part<float>);

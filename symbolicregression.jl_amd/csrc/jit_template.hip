@@ -71,6 +71,8 @@ struct JitArgs {
   int nraw, nder;           // raw feature columns and derived columns (jit.h Columns)
   uint32_t der[48];         // derived column k: (operator << 16) | feature
   const float* dcols;       // [nder][n_pad] the derived columns (sr_jit_derive), or null: staged ones computed here
+  int nbig;                 // row groups [0, nbig) hold e.ntiles tiles; the tail row groups after them
+  int ts;                   // hold ts tiles each (the last round of workgroups in smaller pieces)
 };
 
 // A derived column's value: the PRECISE routine of the operator (the same
@@ -99,10 +101,12 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   float* sX = reinterpret_cast<float*>(smem);
   const int ncol = ja.nraw + ja.nder;
   const int narr = 1 + ncol + (W ? 1 : 0);
-  const int rows = a.ntiles * TILE;
+  const int rows = a.ntiles * TILE;  // LDS layout: room for a full row group
   int rg, g;
   if (!block_of(a, rg, g)) return;
-  const int64_t row0 = (int64_t)rg * rows;
+  const bool tail = rg >= ja.nbig;
+  const int ntl = tail ? ja.ts : a.ntiles;  // tiles of this row group
+  const int64_t row0 = tail ? (int64_t)ja.nbig * rows + (int64_t)(rg - ja.nbig) * ja.ts * TILE : (int64_t)rg * rows;
   const int nthreads = __builtin_amdgcn_readfirstlane((int)blockDim.x);
   // per-tree partials: gathered in LDS after the tiles when the host made room
   // for them (few trees per group), else stored straight to global memory
@@ -115,7 +119,7 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   //    (tile, array), so a derived column's operator is wave-uniform
   {
     constexpr int V = TILE / 4;  // float4 per array per tile
-    const int total = a.ntiles * narr * V;
+    const int total = ntl * narr * V;
     for (int idx = threadIdx.x; idx < total; idx += nthreads) {
       const int v = idx % V;
       const int tk = idx / V;
@@ -145,7 +149,7 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
 
   const int lane = threadIdx.x & 63;
   const int64_t rem = a.n - row0;
-  const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE - 1) / TILE);
+  const int nt_valid = (int)min((int64_t)ntl, (rem + TILE - 1) / TILE);
   const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nwaves = nthreads >> 6;

@@ -58,6 +58,9 @@ struct EvalPlan {
   int nrg, ntg, tpb;
   size_t lds_bytes;
   int threads;    // workgroup size
+  // tree code only: row groups [0, nbig) of ntiles tiles, then row groups of
+  // ts tiles (the last round of workgroups in smaller pieces); nbig < 0: all full
+  int nbig = -1, ts = 0;
 };
 
 // Choose the geometry for `nlist` trees over `n` rows; returns false when the

@@ -5,6 +5,7 @@
 #   tools/gpu_run.sh smoke    __graft_entry__.smoke()   -> gpurun_out/smoke.log
 #   tools/gpu_run.sh bench    bench.py (BENCH_ARGS)     -> gpurun_out/bench.json
 #   tools/gpu_run.sh profile  bench under rocprofv3: kernel trace + PMC passes (tools/gpu_bench_profile.sh)
+#   tools/gpu_run.sh configs  tools/bench_configs.py   -> gpurun_out/configs.jsonl
 #   tools/gpu_run.sh final    suite, smoke, bench, profile
 # Several modes may be given: tools/gpu_run.sh suite bench
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
@@ -25,6 +26,10 @@ run_bench() {
   timeout -k 10 400 python -u bench.py ${BENCH_ARGS:-} > gpurun_out/bench.json 2> gpurun_out/bench.err || exit $?
   tail -c 600 gpurun_out/bench.json
 }
+run_configs() {
+  timeout -k 10 400 python -u tools/bench_configs.py > gpurun_out/configs.jsonl 2> gpurun_out/configs.err || exit $?
+  cat gpurun_out/configs.jsonl
+}
 run_profile() {
   bash tools/gpu_bench_profile.sh > gpurun_out/benchprof.log 2>&1 || exit $?
   tail -30 gpurun_out/benchprof.log
@@ -35,6 +40,7 @@ for mode in "$@"; do
     smoke) run_smoke ;;
     bench) run_bench ;;
     profile) run_profile ;;
+    configs) run_configs ;;
     final) run_suite; run_smoke; run_bench; run_profile ;;
     *) echo "unknown mode $mode"; exit 2 ;;
   esac
