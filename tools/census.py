@@ -227,31 +227,41 @@ def main():
     else:
         trees = srhip.random_population(args.ntrees, o, args.nfeat, np.float32, seed=args.seed, maxsize=30)
     flat = srhip.flatten(trees, o, dtype=np.float32)
-    code, _, offs = srhip.engine.jit_compile(flat, fast=True, grad=args.grad)
     tmpl = GEN / "jit_tmpl_l.hsaco"
     syms = readelf_syms(tmpl)
     taddr, toff = text_section(tmpl)
-    img = bytearray(tmpl.read_bytes())
     area = syms["sr_jit_code"]
     fo = toff + (area - taddr)
-    img[fo:fo + len(code)] = code
-    with tempfile.NamedTemporaryFile(suffix=".hsaco", delete=False) as f:
-        f.write(img)
-        path = f.name
-    ins = disassemble(path)
     fast0 = syms["sr_rt_fast"]
     names = {v: k[len("sr_rt_fast_"):] for k, v in syms.items() if k.startswith("sr_rt_fast_")}
     attrib = collections.Counter()
-    calls = collections.Counter()
     tot_tile, tot_pro, tot_epi = collections.Counter(), collections.Counter(), collections.Counter()
     per_tree = []
-    for t, off in sorted(offs.items()):
-        before = dict(attrib)
-        pro, tile = walk(ins, area + off, fast0, names, attrib, grad_split=args.grad, epi=tot_epi)
-        tot_tile.update(tile)
-        tot_pro.update(pro)
-        cyc = sum(COST[vclass(k)] * v for k, v in tile.items() if k.startswith("v_"))
-        per_tree.append(cyc)
+    # one code area at a time (a large batch fills several, as at run time)
+    left = list(range(len(trees)))
+    ncomp = 0
+    while left:
+        sub = srhip.flatten([trees[t] for t in left], o, dtype=np.float32)
+        code, _, offs = srhip.engine.jit_compile(sub, fast=True, grad=args.grad)
+        if not offs:
+            break
+        img = bytearray(tmpl.read_bytes())
+        img[fo:fo + len(code)] = code
+        with tempfile.NamedTemporaryFile(suffix=".hsaco", delete=False) as f:
+            f.write(img)
+            path = f.name
+        ins = disassemble(path)
+        for t, off in sorted(offs.items()):
+            pro, tile = walk(ins, area + off, fast0, names, attrib, grad_split=args.grad, epi=tot_epi)
+            tot_tile.update(tile)
+            tot_pro.update(pro)
+            per_tree.append(sum(COST[vclass(k)] * v for k, v in tile.items() if k.startswith("v_")))
+        ncomp += len(offs)
+        done = set(offs)
+        left = [t for k, t in enumerate(left) if k not in done]
+        if args.grad is False:
+            break  # the loss code of config #2 fits one area
+    offs = range(ncomp)
     nodes = int(flat.nodes.sum())
     # budget
     rows_budget = []
