@@ -164,7 +164,8 @@ struct GradGen {
   int n = 0;
   std::vector<uint8_t> hasc;      // value's subtree holds a constant: it needs an adjoint
   std::vector<int> last;          // last step (forward i, loss n, reverse 2n-i) that reads the value
-  std::vector<int> loc;           // pool block of each value, -1 none
+  std::vector<int> loc;           // pool block of each value, -1 none, LOC_VA: in the routine registers VA
+  static constexpr int LOC_VA = -7, LOC_VB = -8;
   int owner[GNPOOL];              // pool block: -1 free, value id, 1000 + feature (forward), 2000 + k adjoint
   int refs[GNPOOL];               // adjoint references of a block
   struct Adj { int reg = -1; int blk = -2; bool neg = false; };  // blk -1: the seed block Y
@@ -349,7 +350,30 @@ struct GradGen {
   Src fsrc(const GOpnd& q, int e) const {  // forward operand source
     if (q.k == G_C) return S(SC0 + q.ci);
     if (q.k == G_X) return V(blk_reg(xblk[q.v]) + e);
-    return V(blk_reg(loc[q.v]) + e);
+    return V(vreg(q.v) + e);
+  }
+  int vreg(int v) const { return loc[v] == LOC_VA ? VA : loc[v] == LOC_VB ? VB : blk_reg(loc[v]); }
+  bool in_va(const GOpnd& q) const { return q.k == G_VAL && loc[q.v] == LOC_VA; }
+  // a routine's result may stay in VA when its one use is the next forward
+  // operation (no reverse use, not the root): that operation reads VA before
+  // anything writes it (SRHIP_GJIT_KEEP_VA=0: always moved to a pool block)
+  // an inline result whose one use is the next operation, a routine call,
+  // is written straight into the call's argument registers: VA or VB (0: no)
+  int arg_reg_for(int i) const {
+    static const bool on = [] { const char* e = std::getenv("SRHIP_GJIT_KEEP_VA"); return !(e && e[0] == '0'); }();
+    if (!on || i + 1 >= n || last[i] != i + 1 || (root.k == G_VAL && root.v == i)) return 0;
+    const GOp& c = ops[i + 1];
+    if (c.kind == K_MAT || g_inline(c)) return 0;
+    const bool a = c.a.k == G_VAL && c.a.v == i, b = c.kind == K_BIN && c.b.k == G_VAL && c.b.v == i;
+    if (c.krid >= 0) return (a || b) ? VA : 0;  // the value operand goes to VA
+    return a ? VA : b ? VB : 0;
+  }
+  bool keep_in_va(int i) const {
+    static const bool on = [] { const char* e = std::getenv("SRHIP_GJIT_KEEP_VA"); return !(e && e[0] == '0'); }();
+    if (!on || i + 1 >= n || last[i] != i + 1 || (root.k == G_VAL && root.v == i)) return false;
+    const GOp& c = ops[i + 1];
+    if (c.kind == K_MAT) return false;
+    return (c.a.k == G_VAL && c.a.v == i) || (c.kind == K_BIN && c.b.k == G_VAL && c.b.v == i);
   }
   void read_feat(int dst, int f) {  // a feature block straight from the LDS tile
     as.ds_read_b128(dst, VLANE, (1 + f) * TILE * 4);
@@ -432,9 +456,10 @@ struct GradGen {
     // blocks dying here may hold the result (rows are independent)
     free_values_at(i);
     free_feats_at(i);
-    const int k = free_block();
-    if (k < 0) { why = "register pool exhausted"; return false; }
-    const int d = blk_reg(k);
+    const int areg = arg_reg_for(i);
+    const int k = areg ? -1 : free_block();
+    if (!areg && k < 0) { why = "register pool exhausted"; return false; }
+    const int d = areg ? areg : blk_reg(k);
     for (int e = 0; e < R; ++e) {
       if (o.kind == K_UN) {
         const int ar = a[e].enc - 256;
@@ -476,13 +501,18 @@ struct GradGen {
       }
     }
     if (gmin) guard_min(d);
+    if (areg) {
+      loc[i] = areg == VA ? LOC_VA : LOC_VB;
+      return true;
+    }
     owner[k] = i;
     loc[i] = k;
     return true;
   }
   void operand_to(int dst, const GOpnd& q) {
     if (q.k == G_X) { read_feat(dst, q.v); return; }
-    mov4(dst, blk_reg(loc[q.v]));
+    if (vreg(q.v) == dst) return;  // already there (a result kept in VA)
+    mov4(dst, vreg(q.v));
   }
   bool emit_call(int i) {
     const GOp& o = ops[i];
@@ -496,14 +526,24 @@ struct GradGen {
       free_values_at(i);
       routine(o.krid, prec);
     } else {
-      operand_to(VA, o.a);
-      if (o.kind == K_BIN) operand_to(VB, o.b);
+      if (o.kind == K_BIN && in_va(o.b)) {  // VB first: VA still holds it
+        operand_to(VB, o.b);
+        operand_to(VA, o.a);
+      } else {
+        operand_to(VA, o.a);
+        if (o.kind == K_BIN) operand_to(VB, o.b);
+      }
       free_values_at(i);
       if (fast && o.kind == K_UN && o.op == SRHIP_UOP_EXP) guard_max(VGEXP, VA);
       if (fast && g_trig && trig_tainted_zs(o)) guard_max(VGTRIG_G, VA);
       routine(o.rid, prec);
     }
     free_feats_at(i);
+    if (keep_in_va(i)) {
+      if (fast && taint[i] && zs[i] && o.kind == K_BIN && o.op == SRHIP_BOP_DIV) guard_min(VA);
+      loc[i] = LOC_VA;
+      return true;
+    }
     const int k = free_block();
     if (k < 0) { why = "register pool exhausted"; return false; }
     mov4(blk_reg(k), VA);
