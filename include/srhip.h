@@ -300,6 +300,15 @@ int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_b
 int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int64_t* inout_nbytes,
                                char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
                                int64_t* inout_noffsets);
+/* Testing hook (no device needed): the host side of
+ * srhip_program_set_constants. Compiles the trees (dtype F32/F64), writes
+ * new_consts through the programs' constant map (loss programs, grad = 0, or
+ * gradient programs, grad = 1) and compares every tree with a fresh compile
+ * of the new constants: out_mismatch = trees whose instruction stream or
+ * static verdict differs (0 is correct), out_recompiled = trees the update
+ * compiled again, out_relayout = 1 when it needed a rebuild instead. */
+int32_t srhip_debug_constant_map(const srhip_trees* trees, int32_t dtype, int32_t grad, const void* new_consts,
+                                 int64_t* out_mismatch, int64_t* out_recompiled, int32_t* out_relayout);
 
 /* ---- instrumentation ----------------------------------------------------
  * Device time (ms, HIP events on the context's stream) of the evaluation

@@ -356,7 +356,7 @@ template <typename T>
 bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::vector<int32_t>& toff,
                  const std::vector<int32_t>& len, std::vector<int32_t>& cmap, std::vector<uint8_t>& direct,
                  std::vector<FoldRec>& folds, std::vector<uint8_t>& sfail, std::vector<uint8_t>* fir, bool grad,
-                 bool* verdicts_changed) {
+                 bool* verdicts_changed, int64_t* n_recompiled = nullptr) {
   const int nt = p->ntrees;
   if (cmap.size() * sizeof(Ins<T>) != code.size() || (int)direct.size() != nt || (int)toff.size() != nt ||
       (int)len.size() != nt || (int)sfail.size() != nt)
@@ -385,6 +385,7 @@ bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::
     }
     redo.push_back(t);
   }
+  if (n_recompiled) *n_recompiled = (int64_t)redo.size();
   if (std::getenv("SRHIP_DEBUG_SETC")) std::fprintf(stderr, "srhip set_constants: %d of %d trees recompiled\n", (int)redo.size(), nt);
   if (redo.empty()) return true;
   const int nr = (int)redo.size();
@@ -2064,4 +2065,60 @@ int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int
                                char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
                                int64_t* inout_noffsets) {
   return jit_compile_hook(trees, 2, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets, inout_noffsets);
+}
+
+namespace {
+template <typename T>
+void constant_map_check(const srhip_trees* trees, bool grad, const void* new_consts, int64_t* mismatch,
+                        int64_t* recompiled, int32_t* relayout) {
+  srhip_program p;  // host state only: patch_image reads the trees and writes the images
+  p.ntrees = trees->ntrees;
+  const int nt = trees->ntrees;
+  p.node_off.assign(trees->node_off, trees->node_off + nt + 1);
+  p.const_off.assign(trees->const_off, trees->const_off + nt + 1);
+  p.kind.assign(trees->kind, trees->kind + p.node_off[nt]);
+  p.arg.assign(trees->arg, trees->arg + p.node_off[nt]);
+  const size_t cbytes = (size_t)p.const_off[nt] * sizeof(T);
+  p.consts.resize(std::max<size_t>(cbytes, 1));
+  if (cbytes) std::memcpy(p.consts.data(), trees->consts, cbytes);
+  CompiledBatch<T> cb = compile_batch_par<T>(*trees, grad);
+  std::vector<unsigned char> code(reinterpret_cast<const unsigned char*>(cb.code.data()),
+                                  reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
+  std::vector<uint8_t> sfail = cb.static_fail, fir = cb.fail_if_rows;
+  if (cbytes) std::memcpy(p.consts.data(), new_consts, cbytes);
+  bool vchg = false;
+  *relayout = patch_image<T>(&p, code, cb.tree_off, cb.len, cb.cmap, cb.direct, cb.folds, sfail, grad ? nullptr : &fir,
+                             grad, &vchg, recompiled) ? 0 : 1;
+  if (*relayout) return;
+  srhip_trees fresh_trees = *trees;
+  fresh_trees.consts = new_consts;
+  const CompiledBatch<T> fresh = compile_batch_par<T>(fresh_trees, grad);
+  const Ins<T>* ins = reinterpret_cast<const Ins<T>*>(code.data());
+  *mismatch = 0;
+  for (int t = 0; t < nt; ++t) {
+    bool bad = sfail[t] != fresh.static_fail[t] || (!grad && fir[t] != fresh.fail_if_rows[t]);
+    if (!bad && fresh.tree_off[t] >= 0) {
+      bad = cb.tree_off[t] < 0 || cb.len[t] != fresh.len[t] ||
+            std::memcmp(ins + cb.tree_off[t], &fresh.code[fresh.tree_off[t]], sizeof(Ins<T>) * fresh.len[t]) != 0;
+    }
+    *mismatch += bad ? 1 : 0;
+  }
+}
+}  // namespace
+
+int32_t srhip_debug_constant_map(const srhip_trees* trees, int32_t dtype, int32_t grad, const void* new_consts,
+                                 int64_t* out_mismatch, int64_t* out_recompiled, int32_t* out_relayout) {
+  return guarded([&] {
+    if (!trees || !out_mismatch || !out_recompiled || !out_relayout) throw Error(SRHIP_ERR_INVALID, "null argument");
+    if (trees->ntrees < 0 || (trees->ntrees > 0 && (!trees->node_off || !trees->const_off)))
+      throw Error(SRHIP_ERR_INVALID, "bad trees");
+    if (trees->ntrees > 0 && trees->const_off[trees->ntrees] > 0 && !new_consts) throw Error(SRHIP_ERR_INVALID, "null constants");
+    *out_mismatch = 0;
+    *out_recompiled = 0;
+    *out_relayout = 0;
+    if (dtype == SRHIP_F32) constant_map_check<float>(trees, grad != 0, new_consts, out_mismatch, out_recompiled, out_relayout);
+    else if (dtype == SRHIP_F64) constant_map_check<double>(trees, grad != 0, new_consts, out_mismatch, out_recompiled, out_relayout);
+    else throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
+    return SRHIP_OK;
+  });
 }

@@ -86,6 +86,8 @@ SIGNATURES = {
                           C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)],
     "srhip_jit_compile_grad": [C.POINTER(Trees), C.c_void_p, C.POINTER(C.c_int64), C.c_char_p,
                                C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)],
+    "srhip_debug_constant_map": [C.POINTER(Trees), C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_int64),
+                                 C.POINTER(C.c_int64), C.POINTER(C.c_int32)],
 }
 
 

@@ -1,0 +1,82 @@
+"""The host side of srhip_program_set_constants (api.cpp patch_image), no
+device needed: new constants written through the constant map must give
+every tree the instruction stream and static verdict a fresh compile of the
+new constants gives (compile.cpp, the reference's `_eval_constant_tree`
+folding, src/InterfaceDynamicExpressions.jl eval_tree_array). Trees whose
+immediates are their constants or folded subtrees of them are patched with no
+recompile; non-finite values recompile just their trees."""
+import numpy as np
+import pytest
+
+import srhip
+from srhip.engine import debug_constant_map
+
+OPS = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+
+
+def _flat(n, T, seed):
+    """n random trees, without those that fail statically for their own
+    constants (they have no code: new constants that make them compile need
+    a new layout, which set_constants handles by a rebuild)"""
+    trees = srhip.random_population(n, OPS, 5, T, seed=seed)
+    keep = []
+    for t in trees:
+        f = srhip.flatten([t], OPS, dtype=T)
+        if debug_constant_map(f, np.asarray(f.consts, dtype=T), T)[1] == 0:  # patched in place: it has code
+            keep.append(t)
+    assert len(keep) > 0.8 * n
+    return srhip.flatten(keep, OPS, dtype=T)
+
+
+@pytest.mark.parametrize("T", [np.float32, np.float64])
+@pytest.mark.parametrize("grad", [False, True])
+def test_scaled_constants_patch_without_recompile(T, grad):
+    flat = _flat(3000, T, 21)
+    c = np.asarray(flat.consts, dtype=T)
+    for k, new in enumerate((c * T(1.01), c + T(0.25), -c)):
+        mismatch, recompiled, relayout = debug_constant_map(flat, new, T, grad)
+        assert relayout == 0 and mismatch == 0, (k, mismatch, relayout)
+        assert recompiled <= 0.02 * flat.ntrees, (k, recompiled)  # only folds that newly overflow
+
+
+@pytest.mark.parametrize("grad", [False, True])
+def test_folded_subtrees_are_re_evaluated(grad):
+    """exp(c1 * c2)-style folds: new values move the folded immediate; a fold
+    that overflows makes its tree fail statically (recompiled, old code kept)."""
+    B, U = OPS.make_binary, OPS.make_unary
+
+    def x():
+        return srhip.Node(feature=1)
+
+    def c(v):
+        return srhip.Node(val=v)
+
+    trees = [B("+", B("*", x(), U("exp", B("*", c(0.5), c(2.0)))), c(3.0)),
+             B("/", U("cos", B("-", c(0.5), c(2.0))), x()),
+             B("+", x(), c(0.5))]
+    T = np.float32
+    flat = srhip.flatten(trees, OPS, dtype=T)
+    c0 = np.asarray(flat.consts, dtype=T)
+    assert debug_constant_map(flat, c0 * T(1.5), T, grad)[:2] == (0, 0)
+    big = c0.copy()
+    big[0] = T(1e30)  # exp(1e30 * 2) overflows: tree 0 fails statically
+    mismatch, recompiled, relayout = debug_constant_map(flat, big, T, grad)
+    # gradient programs fold nothing: a large finite constant is just written
+    assert mismatch == 0 and relayout == 0 and recompiled == (0 if grad else 1)
+
+
+@pytest.mark.parametrize("T", [np.float32, np.float64])
+def test_non_finite_constants(T):
+    flat = _flat(2000, T, 22)
+    c = np.asarray(flat.consts, dtype=T)
+    rng = np.random.default_rng(3)
+    new = c.copy()
+    hit = rng.choice(len(c), size=len(c) // 10, replace=False)
+    new[hit[: len(hit) // 2]] = np.inf
+    new[hit[len(hit) // 2:]] = np.nan
+    for grad in (False, True):
+        mismatch, recompiled, relayout = debug_constant_map(flat, new, T, grad)
+        assert relayout == 0 and mismatch == 0 and recompiled > 0
+    # and back to finite values: the failing trees' kept code is patched again
+    mismatch, recompiled, relayout = debug_constant_map(flat, c * T(0.9), T, False)
+    assert relayout == 0 and mismatch == 0
