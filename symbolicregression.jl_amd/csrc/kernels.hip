@@ -13,12 +13,18 @@
 namespace srhip {
 namespace {
 
-// One workgroup per 64 slots; its 16 waves split the row groups (a fixed
-// order: the sums do not depend on timing), then wave 0 adds the 16 parts.
-// It also leaves the launch's flags clean for the next call (no clearing
-// launch per call): each slot's failure flag, and (cnt != nullptr) the tree
-// code's counters, copied to cnt_host first.
+// One workgroup per 16 slots; lane l of wave w sums slot l % 16 over the row
+// groups rg ≡ 4w + l / 16 (mod 64) — a fixed order: the sums do not depend
+// on timing — and the workgroup adds the 64 parts of each slot in a fixed tree.
+// (16 slots per workgroup spread a batch's sums over 4x the CUs of one slot
+// per lane: the loop per lane is a quarter as long.) It also leaves the
+// launch's flags clean for the next call (no clearing launch per call): each
+// slot's failure flag, and (cnt != nullptr) the tree code's counters, copied
+// to cnt_host first.
 constexpr int kFinWaves = 16;
+constexpr int kFinPos = 16;                      // slots per workgroup
+constexpr int kFinSub = 64 / kFinPos;            // row-group lanes per slot and wave
+constexpr int kFinStride = kFinWaves * kFinSub;  // row groups per round of the workgroup
 template <typename T>
 __global__ void __launch_bounds__(64 * kFinWaves) finalize_kernel(EvalArgs<T> a, double* __restrict__ out_sum,
                                                                   uint8_t* __restrict__ out_ok,
@@ -30,32 +36,36 @@ __global__ void __launch_bounds__(64 * kFinWaves) finalize_kernel(EvalArgs<T> a,
     cnt[0] = 0u;
     cnt[1] = 0u;
   }
-  __shared__ double ss[kFinWaves][64];
-  __shared__ double sc[kFinWaves][64];
+  __shared__ double ss[kFinWaves * kFinSub][kFinPos];
+  __shared__ double sc[kFinWaves * kFinSub][kFinPos];
   const int lane = threadIdx.x & 63;
   const int w = threadIdx.x >> 6;
+  const int p = lane % kFinPos, r = lane / kFinPos;
   const int npos = a.ntg * a.tpb;
-  const int pos = blockIdx.x * 64 + lane;
+  const int pos = blockIdx.x * kFinPos + p;
   double s = 0.0, c = 0.0;
   if (pos < npos) {
 #pragma unroll 4
-    for (int rg = w; rg < a.nrg; rg += kFinWaves) {
+    for (int rg = w * kFinSub + r; rg < a.nrg; rg += kFinStride) {
       const Part<T> q = a.partial[(size_t)rg * npos + pos];
       s += (double)q.sum;
       c += (double)q.chk;
     }
   }
-  ss[w][lane] = s;
-  sc[w][lane] = c;
+  const int row = w * kFinSub + r;  // = threadIdx.x / kFinPos
+  ss[row][p] = s;
+  sc[row][p] = c;
   __syncthreads();
-  if (w == 0 && pos < npos) {
-    for (int k = kFinWaves / 2; k >= 1; k /= 2)
-      for (int j = 0; j < k; ++j) {
-        ss[j][lane] += ss[j + k][lane];
-        sc[j][lane] += sc[j + k][lane];
-      }
-    s = ss[0][lane];
-    c = sc[0][lane];
+  for (int k = kFinWaves * kFinSub / 2; k >= 1; k /= 2) {  // a fixed tree over the 64 parts
+    if (row < k) {
+      ss[row][p] += ss[row + k][p];
+      sc[row][p] += sc[row + k][p];
+    }
+    __syncthreads();
+  }
+  if (row == 0 && pos < npos) {
+    s = ss[0][p];
+    c = sc[0][p];
     const int g = pos / a.tpb;
     const int i = pos - g * a.tpb;
     const int sidx = a.contig ? g * a.tpb + i : i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
@@ -267,7 +277,7 @@ template <typename T>
 hipError_t launch_finalize(const EvalArgs<T>& a, double* out_sum, uint8_t* out_ok,
                            hipStream_t stream, uint32_t* cnt, uint32_t* cnt_host) {
   const int npos = a.ntg * a.tpb;
-  const unsigned grid = (unsigned)((npos + 63) / 64);
+  const unsigned grid = (unsigned)((npos + kFinPos - 1) / kFinPos);
   hipLaunchKernelGGL((finalize_kernel<T>), dim3(grid), dim3(64 * kFinWaves), 0, stream, a, out_sum, out_ok, cnt,
                      cnt_host);
   return hipGetLastError();
