@@ -405,6 +405,16 @@ struct GradGen {
     if (y.enc >= 256) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d, x, y.enc - 256);
     else as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d, y, x.enc - 256);
   }
+  // acc_ci ±= x·y for one row (the product and the sum in one rounding);
+  // SRHIP_GJIT_ACC_FMA=0: products to a block, then acc_add
+  static bool acc_fma_on() {
+    static const bool on = [] { const char* e = std::getenv("SRHIP_GJIT_ACC_FMA"); return !(e && e[0] == '0'); }();
+    return on;
+  }
+  void acc_fma(int ci, const Src& x, const Src& y, bool neg) {
+    const Src a = V(GACC + ci);
+    as.vop3(VOP3_FMA_F32, "v_fma_f32", GACC + ci, x, y, &a, 0, neg ? 1 : 0);
+  }
   // acc_ci ±= Σ_e blk_e
   void acc_add(int ci, int reg, bool neg) {
     as.vop2(VOP2_ADD_F32, "v_add_f32_e32", TS, V(reg), reg + 1);
@@ -606,14 +616,18 @@ struct GradGen {
         case SRHIP_BOP_MUL: {
           fetch(o.a, XS0);
           fetch(o.b, XS1);
-          if (aa) {
+          if (aa && o.a.k == G_C && acc_fma_on()) {  // ∂c = g·b, summed straight into c's accumulator
+            for (int e = 0; e < R; ++e) acc_fma(o.a.ci, gv(e), rsrc(o.b, XS1, e), g.neg);
+          } else if (aa) {
             int blk;
             const int d = dest(o.a, TP, &blk);
             if (d < 0) return false;
             for (int e = 0; e < R; ++e) vmul(d + e, rsrc(o.b, XS1, e), gv(e));
             give(o.a, d, g.neg, blk);
           }
-          if (ab) {
+          if (ab && o.b.k == G_C && acc_fma_on()) {
+            for (int e = 0; e < R; ++e) acc_fma(o.b.ci, gv(e), rsrc(o.a, XS0, e), g.neg);
+          } else if (ab) {
             int blk;
             const int d = dest(o.b, TP, &blk);
             if (d < 0) return false;
@@ -630,7 +644,10 @@ struct GradGen {
           if (ra < 0) return false;
           for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", ra + e, gv(e), TR + e);
           if (aa) give(o.a, ra, g.neg, blk_a);
-          if (ab) {
+          if (ab && o.b.k == G_C && acc_fma_on()) {  // ∂c = -(g/c)·q into c's accumulator
+            const int qreg = blk_reg(loc[i]);
+            for (int e = 0; e < R; ++e) acc_fma(o.b.ci, V(ra + e), V(qreg + e), !g.neg);
+          } else if (ab) {
             int blk;
             const int d = dest(o.b, TP, &blk);
             if (d < 0) return false;

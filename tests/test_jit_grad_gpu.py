@@ -9,8 +9,9 @@ against Float64 oracle gradients. Tolerance: per constant, relative to
 S_j = Σ_rows |w·ℓ'·∂ŷ/∂c_j| (from the Float64 oracle): in a tree each
 constant has one path to the root, so ∂ŷ/∂c_j is a product of local
 partials that both modes compute from the same forward values; 1e-4·S_j
-bounds their Float32 differences, a tiny fraction may exceed it where a
-local partial is itself ill-conditioned (max_bad_frac)."""
+bounds their Float32 differences, plus 4x the oracle's own spread of the
+gradient N_j (perturbed inputs and its Float32 evaluation, `scales`), which
+covers ill-conditioned local partials: no constant may exceed it."""
 import os
 
 import numpy as np
@@ -148,9 +149,11 @@ def test_grad_tree_code_matches_interpreter_and_oracle(gpu_ctx, opset, weighted)
     S, ref, N = scales(trees, o, X, y, w, with_noise=True)
     # the tree code's forward is the guarded FAST one: the residuals may move
     # by what a correct Float32 evaluation may (N)
-    n1 = check_grads(g1, g0, S, ok_c, 1e-4, 2e-3, "tree code vs interpreter", noise=N)
-    check_grads(g1, ref, S, ok_c, 1e-4, 1e-2, "tree code vs Float64 oracle", noise=N)
-    check_grads(g0, ref, S, ok_c, 1e-4, 1e-2, "interpreter vs Float64 oracle", noise=N)
+    # every constant within the bound (none allowed beyond it: tools/debug_grads.py
+    # reports 0 of 1041-1554 in each case, profiles/r03_debug_grads.txt)
+    n1 = check_grads(g1, g0, S, ok_c, 1e-4, 0.0, "tree code vs interpreter", noise=N)
+    check_grads(g1, ref, S, ok_c, 1e-4, 0.0, "tree code vs Float64 oracle", noise=N)
+    check_grads(g0, ref, S, ok_c, 1e-4, 0.0, "interpreter vs Float64 oracle", noise=N)
     assert n1 > 500
 
 
