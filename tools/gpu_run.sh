@@ -8,6 +8,12 @@
 #   tools/gpu_run.sh configs  tools/bench_configs.py   -> gpurun_out/configs.jsonl
 #   tools/gpu_run.sh final    suite, smoke, bench, profile
 # Several modes may be given: tools/gpu_run.sh suite bench
+# The round-3 measurements in profiles/ came from these tools, each step under
+# its own `timeout -k 10 ...` on the box: ab_env.py (env-knob A/Bs: tail split,
+# tree groups, waves), step_overhead.py, out_copy.py + hostcopy.cpp (per-row
+# outputs), prof_grad.py / pmc_grad.sh / debug_grads.py (gradient tree code),
+# pmc_shard.sh (512 vs 4096 trees), bench_constopt.py / prof_constopt.py,
+# census.py (no GPU: the VALU-issue budget).
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
 run_suite() {
