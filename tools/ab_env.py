@@ -8,6 +8,7 @@ per-call wall time, and checks that every variant returns the same losses
 and did_succeed as the first one (bit for bit).
 
 Usage: python tools/ab_env.py [--ntrees 4096,512] [--steps 20] 'A=1 B=2' 'A=0' ...
+(AB_CFG=5: config #5's 1.25M-row shard with 20 features, the first NTREES of its 16384 trees)
 """
 import argparse
 import json
@@ -28,11 +29,17 @@ def child(ntrees, steps):
     from srhip import constants as K
 
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
-    rng = np.random.default_rng(1)
-    X = rng.standard_normal((5, 1_000_000)).astype(np.float32)
-    y = (np.float32(2) * np.cos(X[3]) + X[0] * X[0] - np.float32(2)).astype(np.float32)
-    trees = srhip.random_population(4096, o, 5, np.float32, seed=1000)
-    trees = trees[::4096 // ntrees]
+    if os.environ.get("AB_CFG") == "5":  # config #5's shard: 20 features x 1.25M rows, 16384 trees
+        rng = np.random.default_rng(5)
+        X = rng.standard_normal((20, 1_250_000), dtype=np.float32)
+        y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(np.float32)
+        trees = srhip.random_population(16384, o, 20, np.float32, seed=5)[: ntrees]
+    else:
+        rng = np.random.default_rng(1)
+        X = rng.standard_normal((5, 1_000_000)).astype(np.float32)
+        y = (np.float32(2) * np.cos(X[3]) + X[0] * X[0] - np.float32(2)).astype(np.float32)
+        trees = srhip.random_population(4096, o, 5, np.float32, seed=1000)
+        trees = trees[::4096 // ntrees]
     ctx = srhip.get_context(0)
     ds = srhip.DeviceDataset(ctx, X, y)
     prog = srhip.Program(ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32)
