@@ -168,15 +168,22 @@ def main():
             torch.cuda.synchronize()
             tdist.barrier()
 
-    def timed(p, steps, warmup):
+    step_ms = []  # per-step wall time of the headline loop (each call returns synchronised)
+
+    def timed(p, steps, warmup, record=None):
         for _ in range(warmup):
             p.eval_loss(ds, K.LOSS["L2"])
         barrier()
         kms = []
         t_ = time.perf_counter()
+        t_prev = t_
         for _ in range(steps):
             p.eval_loss(ds, K.LOSS["L2"])
             kms.append(ctx.last_kernel_time()[0])
+            if record is not None:
+                t_now = time.perf_counter()
+                record.append((t_now - t_prev) * 1e3)
+                t_prev = t_now
         barrier()
         return time.perf_counter() - t_, kms
 
@@ -190,7 +197,7 @@ def main():
         tdist.all_reduce(nr, op=tdist.ReduceOp.SUM)
         return float(t.item()), float(nr.item())
 
-    elapsed, kernel_ms = timed(prog, args.steps, args.warmup)
+    elapsed, kernel_ms = timed(prog, args.steps, args.warmup, step_ms)
     elapsed, total_node_rows = reduce_max_sum(elapsed, node_rows * args.steps)
     tree_code = prog.jit_info()
 
@@ -302,10 +309,26 @@ def main():
         "roofline": roof,
         "cpu_baseline": cpu,
         "setup_s": {"tree_gen": round(t_gen, 2), "compile_upload": round(t_compile, 3)},
+        "steps_detail": step_stats(step_ms, kernel_ms),
     }
     print(json.dumps(out))
     if dist:
         dist[1].destroy_process_group()
+
+
+def step_stats(wall_ms, kern_ms):
+    """Rank 0's per-step wall time (host clock between the returns of
+    consecutive synchronous calls) and kernel time (HIP events on the
+    context's stream): min / median / max and the first three steps, so a
+    single stall and a uniform per-call cost can be told apart."""
+    def s(v):
+        a = np.asarray(v, dtype=np.float64)
+        if a.size == 0:
+            return None
+        return {"min": round(float(a.min()), 4), "median": round(float(np.median(a)), 4),
+                "max": round(float(a.max()), 4), "first3": [round(float(x), 4) for x in a[:3]]}
+    gap = [w - k for w, k in zip(wall_ms, kern_ms)]
+    return {"wall_ms": s(wall_ms), "kernel_ms": s(kern_ms), "non_kernel_ms": s(gap)}
 
 
 def row_shard_leg(args, world, rank, ctx, dist, barrier):

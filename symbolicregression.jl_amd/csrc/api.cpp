@@ -9,6 +9,8 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <condition_variable>
+#include <functional>
 #include <cstdio>
 #include <cmath>
 #include <cstring>
@@ -94,6 +96,64 @@ int64_t pad_rows(int64_t rows) { return ((std::max<int64_t>(rows, 1) + kRowPad -
 
 size_t dtype_size(int dtype) { return dtype == SRHIP_F32 ? 4 : 8; }
 
+// Persistent host-copy workers of one context (copy_rows_to_host): created
+// at the first large per-row output, joined when the context closes. A job is
+// one function run by every worker with its index; the caller keeps issuing
+// the DMA chunks meanwhile and waits for the job at the end.
+class CopyPool {
+ public:
+  ~CopyPool() {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      stop_ = true;
+    }
+    cv_.notify_all();
+    for (auto& t : th_) t.join();
+  }
+  unsigned size() const { return (unsigned)th_.size(); }
+  void start(unsigned n, int device) {
+    if (!th_.empty()) return;
+    for (unsigned j = 0; j < n; ++j)
+      th_.emplace_back([this, j, device] {
+        const bool dev_ok = hipSetDevice(device) == hipSuccess;
+        uint64_t seen = 0;
+        std::unique_lock<std::mutex> lk(m_);
+        for (;;) {
+          cv_.wait(lk, [&] { return stop_ || gen_ != seen; });
+          if (stop_) return;
+          seen = gen_;
+          std::function<void(unsigned, bool)> f = job_;
+          lk.unlock();
+          f(j, dev_ok);
+          lk.lock();
+          if (--busy_ == 0) cv_done_.notify_all();
+        }
+      });
+  }
+  void submit(std::function<void(unsigned, bool)> f) {
+    {
+      std::lock_guard<std::mutex> lk(m_);
+      job_ = std::move(f);
+      busy_ = (unsigned)th_.size();
+      ++gen_;
+    }
+    cv_.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(m_);
+    cv_done_.wait(lk, [&] { return busy_ == 0; });
+  }
+
+ private:
+  std::vector<std::thread> th_;
+  std::mutex m_;
+  std::condition_variable cv_, cv_done_;
+  std::function<void(unsigned, bool)> job_;
+  uint64_t gen_ = 0;
+  unsigned busy_ = 0;
+  bool stop_ = false;
+};
+
 }  // namespace
 
 struct srhip_ctx {
@@ -123,6 +183,7 @@ struct srhip_ctx {
   unsigned char* pin_stage = nullptr;
   size_t stage_cap = 0;
   std::vector<hipEvent_t> stage_evs;  // one per chunk of a staged copy
+  std::unique_ptr<CopyPool> copy_pool;  // its host-copy workers (persistent)
   double last_ms = 0.0;
   int last_launches = 0;
   int last_bailed = 0;  // trees re-evaluated after their tree code handed a tile back
@@ -608,6 +669,22 @@ bool zero_copy_enabled() {
 }
 void ensure_pinned(srhip_ctx* c, size_t nt);
 
+// Wait for a call's last launch by polling the stream instead of the runtime's
+// blocking wait: hipStreamSynchronize sleeps on a completion interrupt, whose
+// wake-up costs tens of microseconds per call on an idle host (more when the
+// cores sit in deep C-states), on every synchronous eval_loss. SRHIP_SPIN=0:
+// the blocking wait (A/B measurements).
+void wait_stream(hipStream_t s) {
+  const char* e = std::getenv("SRHIP_SPIN");  // read per call: A/B measurements
+  if (e && e[0] == '0') {
+    HIP_CHECK(hipStreamSynchronize(s));
+    return;
+  }
+  hipError_t r;
+  while ((r = hipStreamQuery(s)) == hipErrorNotReady) __builtin_ia32_pause();
+  HIP_CHECK(r);
+}
+
 // LDS for the row tiles of a tree-code workgroup (SRHIP_EVAL_LDS, KiB)
 size_t jit_tile_budget() {
   static const size_t b = [] {
@@ -862,15 +939,17 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, c
 
 // Compute units of the context's device (queried once).
 int device_cus(const srhip_ctx* c) {
-  static int cus[64] = {0};
+  // contexts on several threads may ask at once: each entry is written with
+  // the same value by whichever thread gets there first
+  static std::atomic<int> cus[64];
   const int d = c->device;
   if (d < 0 || d >= 64) return 256;
-  if (!cus[d]) {
-    int v = 0;
+  int v = cus[d].load(std::memory_order_relaxed);
+  if (!v) {
     if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, d) != hipSuccess || v <= 0) v = 256;
-    cus[d] = v;
+    cus[d].store(v, std::memory_order_relaxed);
   }
-  return cus[d];
+  return v;
 }
 
 // Tree-code grids whose workgroups fill a whole number of rounds of the
@@ -964,7 +1043,10 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     const int s0 = launches[li].s0;
     const int nlist = launches[li].nlist;
     const bool last_jit = pass == -1 && (li + 1 == launches.size() || launches[li + 1].pass != -1);
-    if (nlist == 0 || rows == 0) {
+    // no rows (an empty row shard): nothing to launch; every tree's result is
+    // its static verdict (finish_results, pack_partials_kernel)
+    if (rows == 0) continue;
+    if (nlist == 0) {
       if (last_jit) throw Error(SRHIP_ERR_INVALID, "empty tree-code part");
       continue;
     }
@@ -1087,7 +1169,7 @@ bool enqueue_result_copies(srhip_ctx* c, const srhip_program* p, int64_t rows) {
 // wait for the call, then the per-tree results with the static verdicts applied
 void finish_results(srhip_ctx* c, const srhip_program* p, int64_t rows, bool copied, double* out_sum,
                     uint8_t* out_ok) {
-  HIP_CHECK(hipStreamSynchronize(c->stream));
+  wait_stream(c->stream);
   timing_finish(c);
   const int nt = p->ntrees;
   for (int t = 0; t < nt; ++t) {
@@ -1216,20 +1298,22 @@ void copy_rows_to_host(srhip_ctx* c, unsigned char* dst, const unsigned char* sr
     const unsigned want = e ? (unsigned)std::max(1, std::atoi(e)) : 16u;
     return std::max(1u, std::min(want, std::max(1u, std::thread::hardware_concurrency())));
   }();
+  if (!c->copy_pool) c->copy_pool.reset(new CopyPool());
+  c->copy_pool->start(nthr, c->device);
   // workers copy their stripe of each chunk once its DMA has landed; the DMA of
   // chunk i reuses the half of chunk i-2 after every worker is done with it
   std::atomic<int64_t> recorded{-1};
   std::atomic<bool> failed{false};
   std::unique_ptr<std::atomic<unsigned>[]> done(new std::atomic<unsigned>[(size_t)nch]);
   for (int64_t i = 0; i < nch; ++i) done[i].store(0);
-  auto worker = [&](unsigned j) {
-    if (hipSetDevice(c->device) != hipSuccess) { failed = true; return; }
+  c->copy_pool->submit([&](unsigned j, bool dev_ok) {
+    if (!dev_ok) failed = true;
     for (int64_t i = 0; i < nch; ++i) {
       while (recorded.load(std::memory_order_acquire) < i) {
         if (failed.load()) return;
         std::this_thread::yield();
       }
-      if (hipEventSynchronize(c->stage_evs[i]) != hipSuccess) { failed = true; return; }
+      if (failed.load() || hipEventSynchronize(c->stage_evs[i]) != hipSuccess) { failed = true; return; }
       const int64_t r0 = i * k, nr = std::min(k, nrows - r0);
       const size_t n = (size_t)nr * row_bytes;
       const size_t per = ((n + nthr - 1) / nthr + 63) / 64 * 64;
@@ -1237,10 +1321,8 @@ void copy_rows_to_host(srhip_ctx* c, unsigned char* dst, const unsigned char* sr
       if (b0 < e0) std::memcpy(dst + (size_t)r0 * row_bytes + b0, c->pin_stage + (size_t)(i & 1) * half + b0, e0 - b0);
       done[i].fetch_add(1, std::memory_order_release);
     }
-  };
-  std::vector<std::thread> th;
+  });
   try {
-    for (unsigned j = 0; j < nthr; ++j) th.emplace_back(worker, j);
     for (int64_t i = 0; i < nch; ++i) {
       if (i >= 2)
         while (done[i - 2].load(std::memory_order_acquire) < nthr) {
@@ -1255,10 +1337,10 @@ void copy_rows_to_host(srhip_ctx* c, unsigned char* dst, const unsigned char* sr
     }
   } catch (...) {
     failed = true;
-    for (auto& t : th) t.join();
+    c->copy_pool->wait();
     throw;
   }
-  for (auto& t : th) t.join();
+  c->copy_pool->wait();
   if (failed.load()) throw Error(SRHIP_ERR_DEVICE, "host copy of the per-row outputs failed");
 }
 
@@ -1571,6 +1653,7 @@ int32_t srhip_close(srhip_ctx* ctx) {
     if (!ctx) return SRHIP_OK;
     (void)hipSetDevice(ctx->device);
     (void)hipStreamSynchronize(ctx->stream);
+    ctx->copy_pool.reset();  // joins the host-copy workers
     ctx->partial.release();
     ctx->sums.release();
     ctx->oks.release();
@@ -1858,6 +1941,9 @@ int32_t srhip_eval_loss_packed(srhip_dataset* ds, srhip_program* prog, int32_t l
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, d_out) != hipSuccess || at.type != hipMemoryTypeDevice)
       throw Error(SRHIP_ERR_INVALID, "d_out is not device memory");
+    if (at.device != prog->ctx->device)
+      throw Error(SRHIP_ERR_INVALID, "d_out is on device " + std::to_string(at.device) + ", the program on device " +
+                                         std::to_string(prog->ctx->device));
     std::lock_guard<std::mutex> lk(prog->ctx->mu);
     HIP_CHECK(hipSetDevice(prog->ctx->device));
     if (ds->dtype == SRHIP_F32) return eval_loss_packed_impl<float>(ds, prog, loss_kind, loss_params, d_out);

@@ -162,31 +162,32 @@ def torch_all_reduce_sum(device: Optional[str] = None, group=None):
 
 
 class DeviceRowShard:
-    """Row-sharded eval_loss with the partials kept on the device (config #5
-    at N GPUs): srhip_eval_loss_packed writes [Σw·ℓ, failed] per tree + Σw
-    into a torch tensor on this rank's GPU and one all_reduce(SUM) combines
-    the shards — RCCL over xGMI with the nccl backend, on the tensor itself;
-    the gloo backend (tests, ranks sharing one GPU) reduces a host copy.
-    step() returns the reduced buffer (device tensor) and records the
-    evaluation and all-reduce times of the call (host clock around a
-    synchronised stream / collective)."""
+    """Row-sharded eval_loss (config #5 at N GPUs). With the nccl backend
+    (RCCL over xGMI) srhip_eval_loss_packed writes [Σw·ℓ, failed] per tree +
+    Σw into a torch tensor on this rank's GPU and one all_reduce(SUM)
+    combines the shards on the tensor itself, no host round trip. Any other
+    backend (gloo: CPU tests, ranks sharing one GPU) takes the host path: the
+    per-tree results of srhip_eval_loss, packed on the host (pack_partials)
+    and all-reduced as a CPU tensor, so no torch GPU support is needed.
+    step() returns the reduced buffer (device tensor or numpy array) and
+    records the evaluation and all-reduce times of the call (host clock
+    around a synchronised stream / collective)."""
 
     def __init__(self, prog, dev, loss, group=None):
         self.prog, self.dev, self.loss, self.group = prog, dev, loss, group
         self.nt = prog.ntrees
         self.eval_ms = self.reduce_ms = 0.0
+        self.buf = self.host = None
         import torch.distributed as dist
 
         # no process group (one GPU): the shard is the whole dataset, nothing
         # to reduce, and no torch device state (torch's HIP runtime must be
         # loaded before libsrhip's when both are used: bench.py, tests)
         self.backend = dist.get_backend(group) if dist.is_available() and dist.is_initialized() else None
-        if self.backend is None:
-            self.buf = None
-            return
-        import torch
+        if self.backend == "nccl":
+            import torch
 
-        self.buf = torch.zeros(2 * self.nt + 1, dtype=torch.float64, device=f"cuda:{dev.ctx.device}")
+            self.buf = torch.zeros(2 * self.nt + 1, dtype=torch.float64, device=f"cuda:{dev.ctx.device}")
 
     def step(self):
         import time
@@ -195,21 +196,22 @@ class DeviceRowShard:
         import torch.distributed as dist
 
         t0 = time.perf_counter()
-        if self.backend is None:
+        if self.backend != "nccl":
             sums, wsum, ok = self.prog.eval_loss(self.dev, self.loss.kind, self.loss.params)
-            self.host = pack_partials(sums, wsum, ok)
-            self.eval_ms, self.reduce_ms = (time.perf_counter() - t0) * 1e3, 0.0
+            packed = pack_partials(sums, wsum, ok)
+            t1 = time.perf_counter()
+            if self.backend is not None:
+                t = torch.from_numpy(packed)
+                dist.all_reduce(t, op=dist.ReduceOp.SUM, group=self.group)
+                packed = t.numpy()
+            self.host = packed
+            self.eval_ms, self.reduce_ms = (t1 - t0) * 1e3, (time.perf_counter() - t1) * 1e3
             return self.host
         self.prog.eval_loss_packed(self.dev, self.loss.kind, self.buf.data_ptr(), self.loss.params)
         self.dev.ctx.sync()
         t1 = time.perf_counter()
-        if self.backend == "nccl":
-            dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group)
-            torch.cuda.synchronize(self.buf.device)
-        else:
-            h = self.buf.cpu()
-            dist.all_reduce(h, op=dist.ReduceOp.SUM, group=self.group)
-            self.buf.copy_(h)
+        dist.all_reduce(self.buf, op=dist.ReduceOp.SUM, group=self.group)
+        torch.cuda.synchronize(self.buf.device)
         t2 = time.perf_counter()
         self.eval_ms, self.reduce_ms = (t1 - t0) * 1e3, (t2 - t1) * 1e3
         return self.buf
@@ -235,7 +237,8 @@ def eval_loss_row_sharded(trees, dataset, options, device: Optional[int] = None,
     shard = Dataset(dataset.X, dataset.y, dataset.weights, row_range=(rb, re))
     dev = shard.device(device)
     prog = compile_trees(trees, options, dataset.T, dev.ctx.device)
-    # partials packed on the device and all-reduced there (DeviceRowShard)
+    # nccl: partials packed on the device and all-reduced there; other
+    # backends: packed on the host and all-reduced as a CPU tensor (DeviceRowShard)
     rs = DeviceRowShard(prog, dev, options.elementwise_loss, group)
     rs.step()
     loss, tok = rs.result()

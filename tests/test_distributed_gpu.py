@@ -136,3 +136,92 @@ def test_packed_partials_equal_host_packing(gpu_ctx):
     s, w, ok = prog.eval_loss(ds, K.LOSS["L2"])
     np.testing.assert_array_equal(buf.cpu().numpy(), pack_partials(s, w, ok))
     assert not ok[600] and ok[601]
+
+
+def _empty_shard_worker(rank, world, port, q):
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(root / "symbolicregression.jl_amd"), str(root / "oracle"), str(root / "tests")]
+    os.environ["SRHIP_DEVICE"] = "0"
+    import torch.distributed as dist
+
+    from srhip.distributed import eval_loss_row_sharded
+    from test_distributed_gpu import _problem
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        o, X, y, trees = _problem()
+        # one row over two ranks: rank 1's shard is empty (shard_range)
+        losses, ok = eval_loss_row_sharded(trees[:600], srhip.Dataset(X[:, :1], y[:1]), o, device=0)
+        q.put((rank, losses, ok))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(200)
+def test_row_sharded_world2_with_an_empty_shard(gpu_ctx):
+    """A rank whose row shard is empty evaluates nothing (every tree's result
+    is its static verdict) and still joins the all-reduce: the combined
+    result equals the single-process engine's on the one row."""
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_empty_shard_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=150) for _ in range(world)], key=lambda t: t[0])
+    for p in procs:
+        p.join(timeout=60)
+        assert p.exitcode == 0
+    o, X, y, trees = _problem()
+    ref_l, ref_ok = srhip.eval_loss_batch_ok(trees[:600], srhip.Dataset(X[:, :1], y[:1]), o)
+    for _, l, k in res:
+        np.testing.assert_array_equal(k, ref_ok)
+        np.testing.assert_allclose(l[k], ref_l[k], rtol=1e-6)
+
+
+def test_empty_dataset_tree_code_batch(gpu_ctx):
+    """Zero rows with a batch large enough for tree code: no launch, every
+    tree succeeds with a zero sum unless it fails statically (eval_loss and
+    the packed device buffer agree)."""
+    import torch
+
+    from srhip import constants as K
+    from srhip.distributed import pack_partials
+
+    o, X, y, trees = _problem()
+    trees = trees[:600] + [srhip.Node(val=np.float32(np.inf))]
+    ds = srhip.DeviceDataset(gpu_ctx, X[:, :0], y[:0])
+    prog = srhip.Program(gpu_ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32)
+    s, w, ok = prog.eval_loss(ds, K.LOSS["L2"])
+    assert ok[:600].all() and not ok[600] and w == 0.0
+    assert np.all(s[:600] == 0.0)
+    buf = torch.full((2 * len(trees) + 1,), -7.0, dtype=torch.float64, device=f"cuda:{gpu_ctx.device}")
+    prog.eval_loss_packed(ds, K.LOSS["L2"], buf.data_ptr())
+    gpu_ctx.sync()
+    np.testing.assert_array_equal(buf.cpu().numpy(), pack_partials(s, w, ok))
+
+
+def test_packed_rejects_a_buffer_on_another_device(gpu_ctx):
+    """srhip_eval_loss_packed refuses host memory (and, on a multi-GPU box,
+    a buffer of another device) with SRHIP_ERR_INVALID instead of writing it
+    from the wrong device's stream."""
+    import torch
+
+    from srhip import constants as K
+
+    o, X, y, trees = _problem()
+    ds = srhip.DeviceDataset(gpu_ctx, X[:, :1000], y[:1000])
+    prog = srhip.Program(gpu_ctx, srhip.flatten(trees[:8], o, dtype=np.float32), np.float32)
+    host = torch.zeros(2 * 8 + 1, dtype=torch.float64)
+    with pytest.raises(Exception):
+        prog.eval_loss_packed(ds, K.LOSS["L2"], host.data_ptr())
+    if torch.cuda.device_count() > 1:
+        other = (gpu_ctx.device + 1) % torch.cuda.device_count()
+        buf = torch.zeros(2 * 8 + 1, dtype=torch.float64, device=f"cuda:{other}")
+        with pytest.raises(Exception):
+            prog.eval_loss_packed(ds, K.LOSS["L2"], buf.data_ptr())
