@@ -258,6 +258,57 @@ int32_t srhip_eval_grad_tree_array(srhip_dataset* ds, const srhip_program* prog,
                                    void* out_value, void* out_grad,
                                    uint8_t* out_ok);
 
+/* ---- batched constant optimisation ----------------------------------------
+ * optimize_constants (src/ConstantOptimization.jl:22-65) for every tree of a
+ * batch at once — the per-member loop of optimize_and_simplify_population
+ * (src/SingleIteration.jl:63-82) in one call: every start (x0 and
+ * `nrestarts` perturbed copies x0 .* (1 .+ randn/2), :46-54) of every tree
+ * is a candidate, all advance in lockstep, and each phase of an iteration is
+ * ONE evaluation of all candidates. BFGS (Newton for one constant, :32-33)
+ * with LineSearches.BackTracking, or Nelder-Mead for trees of two or more
+ * constants (:35-36); `iterations` = optimizer_iterations (Options.jl,
+ * default 8). The best start of a tree is kept if it converged, else the
+ * tree keeps x0 (:56-63). Gradients are analytic (srhip_eval_loss_grad), not
+ * Optim's finite differences. */
+#define SRHIP_OPT_BFGS 0
+#define SRHIP_OPT_NELDERMEAD 1
+typedef struct srhip_constopt_options {
+  int32_t algorithm;          /* SRHIP_OPT_*                                              */
+  int32_t iterations;         /* optimizer_iterations                                     */
+  int32_t nrestarts;          /* optimizer_nrestarts                                      */
+  int32_t loss_kind;          /* SRHIP_LOSS_* (srhip_optimize_constants_batch)            */
+  const double* loss_params;  /* the loss parameter, or NULL                              */
+  /* [nrestarts * const_off[ntrees]]: the standard normal draws of the
+   * perturbed starts (Julia: randn(T, size(x0)) per restart), tree by tree,
+   * restart by restart; NULL: drawn from an internal generator seeded with
+   * `seed` */
+  const double* start_noise;
+  uint64_t seed;
+} srhip_constopt_options;
+
+/* On the engine: loss and ∂L/∂c of all candidates per launch on `ds` (the
+ * programs in `ctx`, a context of the dataset's device; NULL = the dataset's
+ * own context). Outputs (caller-owned): out_consts [const_off[ntrees]] of
+ * the dtype — the constants to set_constants! (x0 where the run did not
+ * converge); out_loss [ntrees] the loss at those constants in T (+Inf on
+ * failure); out_converged [ntrees]; out_num_evals [ntrees] loss evaluations
+ * (a member's num_evals increment). */
+int32_t srhip_optimize_constants_batch(srhip_ctx* ctx, srhip_dataset* ds, const srhip_trees* trees,
+                                       const srhip_constopt_options* opts, void* out_consts, double* out_loss,
+                                       uint8_t* out_converged, double* out_num_evals);
+/* The same optimiser over any evaluator (row-sharded datasets whose partials
+ * the caller all-reduces, custom losses on the CPU, tests): fn scores
+ * ntasks candidates — tree_idx[k] is the input tree of candidate k, consts
+ * their constants concatenated in that order (values of the dtype) —
+ * writing out_f[ntasks] (the loss, +Inf on failure) and, when grad != 0,
+ * out_g[constants] (∂L/∂c, NaN for failed candidates). A nonzero return
+ * aborts the optimisation with SRHIP_ERR_INVALID. No device is used. */
+typedef int32_t (*srhip_constopt_eval_fn)(void* user, int64_t ntasks, const int32_t* tree_idx, const double* consts,
+                                          int32_t grad, double* out_f, double* out_g);
+int32_t srhip_optimize_constants_cb(const srhip_trees* trees, int32_t dtype, const srhip_constopt_options* opts,
+                                    srhip_constopt_eval_fn fn, void* user, void* out_consts, double* out_loss,
+                                    uint8_t* out_converged, double* out_num_evals);
+
 /* ---- tree compiler ---------------------------------------------------------
  * Large Float32 programs are compiled to machine code, one block per tree
  * (symbolicregression.jl_amd/csrc/jit.cpp; SRHIP_JIT=0 turns it off, =1 on

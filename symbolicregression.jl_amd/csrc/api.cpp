@@ -25,6 +25,7 @@
 
 #include "../../include/srhip.h"
 #include "compile.h"
+#include "constopt.h"
 #include "jit.h"
 #include "kernels.h"
 
@@ -2205,6 +2206,216 @@ int32_t srhip_debug_constant_map(const srhip_trees* trees, int32_t dtype, int32_
     if (dtype == SRHIP_F32) constant_map_check<float>(trees, grad != 0, new_consts, out_mismatch, out_recompiled, out_relayout);
     else if (dtype == SRHIP_F64) constant_map_check<double>(trees, grad != 0, new_consts, out_mismatch, out_recompiled, out_relayout);
     else throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
+    return SRHIP_OK;
+  });
+}
+
+// ---- batched constant optimisation (constopt.cpp) ------------------------------
+namespace {
+
+void check_rc(int32_t rc) {
+  if (rc != SRHIP_OK) throw Error(rc, g_last_error);
+}
+
+copt::Problem make_problem(const srhip_trees* trees, int dtype) {
+  if (!trees || trees->ntrees < 0 || !trees->const_off || (trees->ntrees > 0 && !trees->node_off))
+    throw Error(SRHIP_ERR_INVALID, "null or malformed trees");
+  if (dtype != SRHIP_F32 && dtype != SRHIP_F64) throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
+  copt::Problem pb;
+  pb.dtype = dtype;
+  pb.const_off.assign(trees->const_off, trees->const_off + trees->ntrees + 1);
+  if (pb.const_off[0] != 0) throw Error(SRHIP_ERR_INVALID, "const_off[0] must be 0");
+  for (int t = 0; t < trees->ntrees; ++t)
+    if (pb.const_off[t + 1] < pb.const_off[t]) throw Error(SRHIP_ERR_INVALID, "const_off must be non-decreasing");
+  const size_t nc = (size_t)pb.const_off.back();
+  if (nc && !trees->consts) throw Error(SRHIP_ERR_INVALID, "null consts");
+  pb.consts.resize(nc);
+  for (size_t j = 0; j < nc; ++j)
+    pb.consts[j] = dtype == SRHIP_F32 ? (double)static_cast<const float*>(trees->consts)[j]
+                                      : static_cast<const double*>(trees->consts)[j];
+  return pb;
+}
+
+copt::Options make_copt_options(const srhip_constopt_options* o) {
+  if (!o) throw Error(SRHIP_ERR_INVALID, "null options");
+  copt::Options r;
+  r.algorithm = o->algorithm;
+  r.iterations = o->iterations;
+  r.nrestarts = o->nrestarts;
+  r.noise = o->start_noise;
+  r.seed = o->seed;
+  return r;
+}
+
+void write_result(const copt::Result& r, int dtype, void* out_consts, double* out_loss, uint8_t* out_conv,
+                  double* out_nev, bool loss_in_t) {
+  const size_t nc = r.consts.size(), nt = r.loss.size();
+  if (out_consts)
+    for (size_t j = 0; j < nc; ++j) {
+      if (dtype == SRHIP_F32) static_cast<float*>(out_consts)[j] = (float)r.consts[j];
+      else static_cast<double*>(out_consts)[j] = r.consts[j];
+    }
+  for (size_t t = 0; t < nt; ++t) {
+    if (out_loss) {
+      double v = r.loss[t];
+      if (loss_in_t && dtype == SRHIP_F32) v = (double)(float)v;
+      out_loss[t] = v;
+    }
+    if (out_conv) out_conv[t] = r.converged[t];
+    if (out_nev) out_nev[t] = r.num_evals[t];
+  }
+}
+
+// The candidates of one evaluation set as a program on the engine (memory-
+// constant tree code: constant updates never recompile); loss and ∂L/∂c of
+// every member in one call each, finished as the reference's loss (:12-19).
+struct EngineSet : copt::Set {
+  srhip_ctx* ctx;
+  srhip_dataset* ds;
+  int dtype, loss;
+  const double* params;
+  srhip_program* prog = nullptr;
+  std::vector<int32_t> coff;  // members' constant offsets
+  EngineSet(srhip_ctx* c, srhip_dataset* d, const srhip_trees* trees, int dt, int ls, const double* pr,
+            const std::vector<int32_t>& members)
+      : ctx(c), ds(d), dtype(dt), loss(ls), params(pr) {
+    const size_t es = dt == SRHIP_F32 ? 4 : 8;
+    std::vector<int32_t> noff{0};
+    std::vector<uint8_t> kind;
+    std::vector<uint16_t> arg;
+    std::vector<unsigned char> cst;
+    coff.push_back(0);
+    for (int32_t t : members) {
+      if (t < 0 || t >= trees->ntrees) throw Error(SRHIP_ERR_INVALID, "member out of range");
+      const int32_t a = trees->node_off[t], b = trees->node_off[t + 1];
+      kind.insert(kind.end(), trees->kind + a, trees->kind + b);
+      arg.insert(arg.end(), trees->arg + a, trees->arg + b);
+      noff.push_back((int32_t)kind.size());
+      const int32_t ca = trees->const_off[t], cb = trees->const_off[t + 1];
+      const unsigned char* src = static_cast<const unsigned char*>(trees->consts);
+      cst.insert(cst.end(), src + (size_t)ca * es, src + (size_t)cb * es);
+      coff.push_back(coff.back() + (cb - ca));
+    }
+    srhip_trees tr;
+    tr.ntrees = (int32_t)members.size();
+    tr.node_off = noff.data();
+    tr.kind = kind.data();
+    tr.arg = arg.data();
+    tr.const_off = coff.data();
+    tr.consts = cst.data();
+    check_rc(srhip_program_create_ex(ctx, dtype, &tr, SRHIP_PROGRAM_VARYING_CONSTANTS, &prog));
+  }
+  ~EngineSet() override {
+    if (prog) (void)srhip_program_destroy(prog);
+  }
+  void eval(const std::vector<double>& X, bool grad, std::vector<double>& f, std::vector<double>& g) override {
+    const int n = (int)coff.size() - 1;
+    const size_t nc = (size_t)coff.back();
+    if (X.size() != nc) throw Error(SRHIP_ERR_INVALID, "constant count mismatch");
+    if (dtype == SRHIP_F32) {
+      std::vector<float> c(nc);
+      for (size_t j = 0; j < nc; ++j) c[j] = (float)X[j];
+      check_rc(srhip_program_set_constants(prog, c.data()));
+    } else {
+      check_rc(srhip_program_set_constants(prog, X.data()));
+    }
+    std::vector<double> sums(std::max(n, 1)), dl(std::max<size_t>(nc, 1));
+    std::vector<uint8_t> ok(std::max(n, 1));
+    double wsum = 0.0;
+    if (grad) check_rc(srhip_eval_loss_grad(ds, prog, loss, params, sums.data(), dl.data(), &wsum, ok.data()));
+    else check_rc(srhip_eval_loss(ds, prog, loss, params, nullptr, 0, sums.data(), &wsum, ok.data()));
+    f.assign(n, 0.0);
+    for (int t = 0; t < n; ++t) {
+      const double v = sums[t] / wsum;
+      f[t] = (ok[t] && std::isfinite(v)) ? v : INFINITY;
+    }
+    if (grad) {
+      g.assign(nc, 0.0);
+      for (int t = 0; t < n; ++t)
+        for (int32_t j = coff[t]; j < coff[t + 1]; ++j) g[j] = ok[t] ? dl[j] / wsum : NAN;
+    }
+  }
+};
+struct EngineFactory : copt::Factory {
+  srhip_ctx* ctx;
+  srhip_dataset* ds;
+  const srhip_trees* trees;
+  int dtype, loss;
+  const double* params;
+  std::unique_ptr<copt::Set> make(const std::vector<int32_t>& members) override {
+    return std::unique_ptr<copt::Set>(new EngineSet(ctx, ds, trees, dtype, loss, params, members));
+  }
+};
+
+// the caller's evaluator
+struct CallbackSet : copt::Set {
+  srhip_constopt_eval_fn fn;
+  void* user;
+  std::vector<int32_t> members;
+  size_t nconst;
+  void eval(const std::vector<double>& X, bool grad, std::vector<double>& f, std::vector<double>& g) override {
+    if (X.size() != nconst) throw Error(SRHIP_ERR_INVALID, "constant count mismatch");
+    f.assign(members.size(), 0.0);
+    g.assign(grad ? nconst : 0, 0.0);
+    const int32_t rc = fn(user, (int64_t)members.size(), members.data(), X.data(), grad ? 1 : 0, f.data(),
+                          grad ? g.data() : nullptr);
+    if (rc != 0) throw Error(SRHIP_ERR_INVALID, "constant optimisation: the evaluator callback failed");
+  }
+};
+struct CallbackFactory : copt::Factory {
+  srhip_constopt_eval_fn fn;
+  void* user;
+  const std::vector<int32_t>* const_off;
+  std::unique_ptr<copt::Set> make(const std::vector<int32_t>& members) override {
+    std::unique_ptr<CallbackSet> s(new CallbackSet());
+    s->fn = fn;
+    s->user = user;
+    s->members = members;
+    s->nconst = 0;
+    const int nt = (int)const_off->size() - 1;
+    for (int32_t t : members) {
+      if (t < 0 || t >= nt) throw Error(SRHIP_ERR_INVALID, "member out of range");
+      s->nconst += (size_t)((*const_off)[t + 1] - (*const_off)[t]);
+    }
+    return s;
+  }
+};
+
+}  // namespace
+
+int32_t srhip_optimize_constants_batch(srhip_ctx* ctx, srhip_dataset* ds, const srhip_trees* trees,
+                                       const srhip_constopt_options* opts, void* out_consts, double* out_loss,
+                                       uint8_t* out_converged, double* out_num_evals) {
+  return guarded([&] {
+    if (!ds) throw Error(SRHIP_ERR_INVALID, "null dataset");
+    if (!opts) throw Error(SRHIP_ERR_INVALID, "null options");
+    if (opts->loss_kind < 0 || opts->loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
+    copt::Problem pb = make_problem(trees, ds->dtype);
+    EngineFactory fac;
+    fac.ctx = ctx ? ctx : ds->ctx;
+    fac.ds = ds;
+    fac.trees = trees;
+    fac.dtype = ds->dtype;
+    fac.loss = opts->loss_kind;
+    fac.params = opts->loss_params;
+    const copt::Result r = copt::optimize(pb, make_copt_options(opts), fac);
+    write_result(r, ds->dtype, out_consts, out_loss, out_converged, out_num_evals, true);
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_optimize_constants_cb(const srhip_trees* trees, int32_t dtype, const srhip_constopt_options* opts,
+                                    srhip_constopt_eval_fn fn, void* user, void* out_consts, double* out_loss,
+                                    uint8_t* out_converged, double* out_num_evals) {
+  return guarded([&] {
+    if (!fn) throw Error(SRHIP_ERR_INVALID, "null evaluator");
+    copt::Problem pb = make_problem(trees, dtype);
+    CallbackFactory fac;
+    fac.fn = fn;
+    fac.user = user;
+    fac.const_off = &pb.const_off;
+    const copt::Result r = copt::optimize(pb, make_copt_options(opts), fac);
+    write_result(r, dtype, out_consts, out_loss, out_converged, out_num_evals, false);
     return SRHIP_OK;
   });
 }

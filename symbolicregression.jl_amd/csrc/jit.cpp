@@ -267,9 +267,43 @@ struct Gen {
     return on;
   }
   bool trig_of_tainted(const IrOp& o) const {
-    static const bool zs_only = [] { const char* e = std::getenv("SRHIP_JIT_TRIG_GUARD_ZS"); return !(e && e[0] == '0'); }();
+    static const bool zs_only = [] { const char* e = std::getenv("SRHIP_JIT_TRIG_GUARD_ZS"); return e && e[0] == '1'; }();
     return o.un && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS) && o.a.k == O_VAL && ops[o.a.v].taint &&
            (o.zs || !zs_only);
+  }
+  // Loss-parity guards (round 4; thresholds from
+  // tools/fast_guard_sim.py): FAST rounding in a value that reaches a divisor
+  // is amplified without bound near the divisor's zeros, and those rows carry
+  // most of the loss (a 1/d pole: the relative loss error grows like ε/d_min).
+  // A sin / cos of a FAST-derived u on a divisor path redoes the tile when
+  // |result| < 2^-k·|u| (its relative condition |u·tan u| above 2^k), as a
+  // cancellation does (|a ± b| <= 2^-k (|a| + |b|)), k = SRHIP_JIT_CAN_LOG2
+  // (default 7); an exp of a FAST-derived u when |u| > 16 (relative error
+  // amplified |u|-fold); a sin / cos of a FAST-derived u when |u| > 2^10
+  // (absolute error |u|·ε).
+  static bool loss_guards_on() {  // SRHIP_JIT_LOSS_GUARDS=0 (experiments): the round-3 guards only
+    static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_LOSS_GUARDS"); return !(e && e[0] == '0'); }();
+    return on;
+  }
+  static uint32_t can_eps_bits() {  // 2^-k
+    static const uint32_t b = [] {
+      const char* e = std::getenv("SRHIP_JIT_CAN_LOG2");
+      const int k = e ? std::max(1, std::min(100, std::atoi(e))) : (loss_guards_on() ? 7 : 14);
+      return (uint32_t)(127 - k) << 23;
+    }();
+    return b;
+  }
+  static uint32_t exp_scale_bits() {  // 87 / 2^k, k = SRHIP_JIT_EXP_GUARD_LOG2 (default 4: |x| > 16)
+    static const uint32_t b = [] {
+      const char* e = std::getenv("SRHIP_JIT_EXP_GUARD_LOG2");
+      const int k = e ? std::max(0, std::min(6, std::atoi(e))) : 4;
+      return fbits(87.0f / (float)(1 << k));
+    }();
+    return b;
+  }
+  bool trig_small(const IrOp& o) const { return loss_guards_on() && trig_of_tainted(o) && o.zs; }
+  bool exp_tainted(const IrOp& o) const {
+    return loss_guards_on() && o.un && o.op == SRHIP_UOP_EXP && o.a.k == O_VAL && ops[o.a.v].taint;
   }
   int reg_of_loc(int l) const { return l == L_A ? VA : l == L_B ? VB : VPOOL0 + R * l; }
 
@@ -347,6 +381,7 @@ struct Gen {
       for (auto& o : ops) {
         if (o.un && o.op == SRHIP_UOP_EXP) g_exp = true;
         if (trig_of_tainted(o) && trig_guard_on()) g_trig = true;
+        if (trig_small(o)) g_can = true;  // its guard shares the cancellation accumulator
         if (o.taint && o.zs) {
           if (!o.un && (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB)) g_can = true;
           if ((!o.un && (o.op == SRHIP_BOP_MUL || o.op == SRHIP_BOP_DIV)) ||
@@ -565,19 +600,40 @@ struct Gen {
     if (!o.un && o.b.k == O_X) release_x(o.b.v, i);
     a_owner = -1;
     if (!o.un) b_owner = -1;
-    if (fast && o.un && o.op == SRHIP_UOP_EXP)  // max |x| over the rows, two per instruction
+    if (fast && o.un && o.op == SRHIP_UOP_EXP) {  // max |x| over the rows, two per instruction
+      // a FAST-derived x counts 87/16 times its size: |x| > 16 fires the 87 check
+      int src = VA;
+      if (exp_tainted(o)) {
+        Src a4[R], k4[R];
+        for (int e = 0; e < R; ++e) { a4[e] = V(VA + e); k4[e] = K(exp_scale_bits()); }  // 87/16 = 5.4375
+        pk_block(VOP3P_MUL_F32, "v_pk_mul_f32", VGT, a4, k4, false);
+        src = VGT;
+      }
       for (int e = 0; e < R; e += 2) {
-        const Src g = V(VGEXP), x0 = V(VA + e), x1 = V(VA + e + 1);
+        const Src g = V(VGEXP), x0 = V(src + e), x1 = V(src + e + 1);
         as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGEXP, g, x0, &x1, 6, 0);
       }
+    }
     if (fast && g_trig && trig_of_tainted(o))
       for (int e = 0; e < R; e += 2) {
         const Src g = V(VGTRIG), x0 = V(VA + e), x1 = V(VA + e + 1);
         as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGTRIG, g, x0, &x1, 6, 0);
       }
+    const bool tsmall = fast && trig_small(o);
+    if (tsmall) mov_block_reg(VGT, VA);  // u, for the condition check after the call
     call_routine(o.rid);
     loc[i] = L_A;
     a_owner = i;
+    if (tsmall) {  // fires when 2^-k·|u| - |sin/cos u| > 0 (or NaN)
+      for (int e = 0; e < R; ++e) {
+        const Src u = V(VGT + e), eps = S(S_EPS), r = V(VA + e);
+        as.vop3(VOP3_FMA_F32, "v_fma_f32", VGT + e, u, eps, &r, 5, 4);
+      }
+      for (int e = 0; e < R; e += 2) {
+        const Src g = V(VGCAN), t0 = V(VGT + e), t1 = V(VGT + e + 1);
+        as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGCAN, g, t0, &t1, 0, 0);
+      }
+    }
     if (fast && o.taint && o.zs && !o.un && o.op == SRHIP_BOP_DIV) guard_min(VA);
     return true;
   }
@@ -769,7 +825,7 @@ struct Gen {
                            std::to_string(SPROG + 1) + "], " + hex32(off));
     }
     if (!cpcs.empty()) as.waitcnt_lgkm(0);
-    if (g_can) as.sop1(SOP1_MOV, "s_mov_b32", S_EPS, K(0x38800000u), "s" + std::to_string(S_EPS));  // 2^-14
+    if (g_can) as.sop1(SOP1_MOV, "s_mov_b32", S_EPS, K(can_eps_bits()), "s" + std::to_string(S_EPS));  // 2^-k
     if (has_call) set_base();
     if (fast) {
       as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_FASTOK), K(0));
@@ -856,7 +912,7 @@ struct Gen {
       if (g_trig) {
         static const uint32_t lim = [] {  // 2^k, k = SRHIP_JIT_TRIG_GUARD_LOG2 (default 14)
           const char* e = std::getenv("SRHIP_JIT_TRIG_GUARD_LOG2");
-          const int k = e ? std::max(1, std::min(100, std::atoi(e))) : 14;
+          const int k = e ? std::max(1, std::min(100, std::atoi(e))) : (loss_guards_on() ? 10 : 14);
           return (uint32_t)(127 + k) << 23;
         }();
         as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(lim), VGTRIG);  // !(2^k >= max|x|)
@@ -927,7 +983,11 @@ struct Gen {
     // a failed tile ends the tree
     as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
     as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
-    if (fast) {  // after a redone tile, the next tile starts FAST again
+    // after a redone tile the call's remaining tiles run PRECISE directly
+    // (a tree whose guards fire on one tile mostly fires on the next: poles,
+    // large arguments); SRHIP_JIT_STICKY=0: the next tile starts FAST again
+    static const bool sticky = [] { const char* e = std::getenv("SRHIP_JIT_STICKY"); return !(e && e[0] == '0'); }();
+    if (fast && !sticky) {
       const int L_keep = as.label();
       as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_FASTOK), K(0));
       as.branch(SOPP_SCC1, "s_cbranch_scc1", L_keep);

@@ -32,6 +32,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdlib>
+#include <cstring>
 
 #include "jit.h"
 #include "jit_asm.h"
@@ -186,9 +187,29 @@ struct GradGen {
   std::vector<uint8_t> taint, zs;
 
   GradGen(Asm& a, const Tmpl& t, uint64_t va) : as(a), T(t), base_va(va) {}
-  bool trig_tainted_zs(const GOp& o) const {
+  // sin / cos of a FAST-derived value: its argument guard (|u| > 2^10, or
+  // 2^14 on a divisor path only with SRHIP_JIT_LOSS_GUARDS=0); on a divisor
+  // path also the condition guard |result| < 2^-7·|u| (jit.cpp Gen: the
+  // round-4 loss-parity guards, same thresholds)
+  static bool loss_guards_on() {
+    static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_LOSS_GUARDS"); return !(e && e[0] == '0'); }();
+    return on;
+  }
+  static uint32_t can_eps_bits() {  // 2^-k
+    static const uint32_t b = [] {
+      const char* e = std::getenv("SRHIP_JIT_CAN_LOG2");
+      const int k = e ? std::max(1, std::min(100, std::atoi(e))) : (loss_guards_on() ? 7 : 14);
+      return (uint32_t)(127 - k) << 23;
+    }();
+    return b;
+  }
+  bool trig_tainted(const GOp& o) const {
     return o.kind == K_UN && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS) && o.a.k == G_VAL && taint[o.a.v] &&
-           zs[&o - ops.data()];
+           (loss_guards_on() || zs[&o - ops.data()]);
+  }
+  bool trig_small(const GOp& o) const { return loss_guards_on() && trig_tainted(o) && zs[&o - ops.data()]; }
+  bool exp_tainted(const GOp& o) const {
+    return loss_guards_on() && o.kind == K_UN && o.op == SRHIP_UOP_EXP && o.a.k == G_VAL && taint[o.a.v];
   }
   uint64_t cur_va() const { return base_va + as.bytes(); }
   static int blk_reg(int k) { return GPOOL0 + R * k; }
@@ -249,7 +270,8 @@ struct GradGen {
       for (int i = 0; i < n; ++i) {
         const GOp& o = ops[i];
         if (o.kind == K_UN && o.op == SRHIP_UOP_EXP) g_exp = true;
-        if (trig_tainted_zs(o)) g_trig = true;
+        if (trig_tainted(o)) g_trig = true;
+        if (trig_small(o)) g_can = true;
         if (taint[i] && zs[i]) {
           if (o.kind == K_BIN && (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB)) g_can = true;
           if ((o.kind == K_BIN && (o.op == SRHIP_BOP_MUL || o.op == SRHIP_BOP_DIV)) ||
@@ -544,9 +566,36 @@ struct GradGen {
         if (o.kind == K_BIN) operand_to(VB, o.b);
       }
       free_values_at(i);
-      if (fast && o.kind == K_UN && o.op == SRHIP_UOP_EXP) guard_max(VGEXP, VA);
-      if (fast && g_trig && trig_tainted_zs(o)) guard_max(VGTRIG_G, VA);
+      if (fast && o.kind == K_UN && o.op == SRHIP_UOP_EXP) {
+        if (exp_tainted(o)) {  // |u| > 16 fires the 87 check: u counts 87/16 = 5.4375 times
+          static const uint32_t scale = [] {  // 87 / 2^k (jit.cpp Gen::exp_scale_bits)
+            const char* ev = std::getenv("SRHIP_JIT_EXP_GUARD_LOG2");
+            const int k = ev ? std::max(0, std::min(6, std::atoi(ev))) : 4;
+            const float v = 87.0f / (float)(1 << k);
+            uint32_t u;
+            std::memcpy(&u, &v, 4);
+            return u;
+          }();
+          for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VGT + e, K(scale), VA + e);
+          guard_max(VGEXP, VGT);
+        } else {
+          guard_max(VGEXP, VA);
+        }
+      }
+      if (fast && g_trig && trig_tainted(o)) guard_max(VGTRIG_G, VA);
+      const bool tsmall = fast && trig_small(o);
+      if (tsmall) mov4(VGT, VA);
       routine(o.rid, prec);
+      if (tsmall) {  // fires when 2^-k·|u| - |sin/cos u| >= 0 (or NaN): max into GCAN
+        for (int e = 0; e < R; ++e) {
+          const Src u = V(VGT + e), eps = S(S_EPS), r = V(VA + e);
+          as.vop3(VOP3_FMA_F32, "v_fma_f32", VGT + e, u, eps, &r, 5, 4);
+        }
+        for (int e = 0; e < R; e += 2) {
+          const Src g = V(VGCAN), t0 = V(VGT + e), t1 = V(VGT + e + 1);
+          as.vop3(VOP3_MAX3_F32, "v_max3_f32", VGCAN, g, t0, &t1, 0, 0);
+        }
+      }
     }
     free_feats_at(i);
     if (keep_in_va(i)) {
@@ -762,7 +811,7 @@ struct GradGen {
     L_redo = as.label();
     if (fast) {
       as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(0), "s" + std::to_string(S_MODE));  // FAST
-      if (g_can) as.sop1(SOP1_MOV, "s_mov_b32", S_EPS, K(0x38800000u), "s" + std::to_string(S_EPS));  // 2^-14
+      if (g_can) as.sop1(SOP1_MOV, "s_mov_b32", S_EPS, K(can_eps_bits()), "s" + std::to_string(S_EPS));  // 2^-k
     }
     for (int j = 0; j < nc; ++j) as.vop1(VOP1_MOV, "v_mov_b32_e32", GACC + j, K(0));
     if (nc > 0) as.waitcnt_lgkm(0);
@@ -828,7 +877,7 @@ struct GradGen {
         as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
       }
       if (g_trig) {
-        as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(0x46800000u), VGTRIG_G);  // 2^14
+        as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(loss_guards_on() ? 0x44800000u : 0x46800000u), VGTRIG_G);  // 2^10 (2^14)
         as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
       }
       as.bind(L_skip);

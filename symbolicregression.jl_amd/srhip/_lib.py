@@ -42,6 +42,23 @@ class Trees(C.Structure):
     ]
 
 
+class ConstOptOptions(C.Structure):
+    """srhip_constopt_options (include/srhip.h)."""
+    _fields_ = [
+        ("algorithm", C.c_int32),
+        ("iterations", C.c_int32),
+        ("nrestarts", C.c_int32),
+        ("loss_kind", C.c_int32),
+        ("loss_params", C.POINTER(C.c_double)),
+        ("start_noise", C.POINTER(C.c_double)),
+        ("seed", C.c_uint64),
+    ]
+
+
+# srhip_constopt_eval_fn
+CONSTOPT_EVAL_FN = C.CFUNCTYPE(C.c_int32, C.c_void_p, C.c_int64, C.POINTER(C.c_int32), C.POINTER(C.c_double),
+                               C.c_int32, C.POINTER(C.c_double), C.POINTER(C.c_double))
+
 _lib = None
 _load_error: Exception | None = None
 
@@ -86,6 +103,10 @@ SIGNATURES = {
                           C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)],
     "srhip_jit_compile_grad": [C.POINTER(Trees), C.c_void_p, C.POINTER(C.c_int64), C.c_char_p,
                                C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)],
+    "srhip_optimize_constants_batch": [C.c_void_p, C.c_void_p, C.POINTER(Trees), C.POINTER(ConstOptOptions),
+                                       C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
+    "srhip_optimize_constants_cb": [C.POINTER(Trees), C.c_int32, C.POINTER(ConstOptOptions), CONSTOPT_EVAL_FN,
+                                    C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
     "srhip_debug_constant_map": [C.POINTER(Trees), C.c_int32, C.c_int32, C.c_void_p, C.POINTER(C.c_int64),
                                  C.POINTER(C.c_int64), C.POINTER(C.c_int32)],
 }

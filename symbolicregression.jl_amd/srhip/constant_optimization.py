@@ -1,51 +1,44 @@
-"""Batched constant optimisation on the device.
+"""Batched constant optimisation: the Python mirror
+of `optimize_constants` (src/ConstantOptimization.jl:22-65) for a whole
+population, over libsrhip's lockstep optimiser (csrc/constopt.cpp).
 
-The reference optimises one PopMember at a time
-(`optimize_constants`, src/ConstantOptimization.jl:22-65): Optim.Newton
-(one constant) or Optim.BFGS, both with LineSearches.BackTracking,
-`optimizer_iterations` = 8 (src/Options.jl:607-621), from x0 and from
-`optimizer_nrestarts` = 2 perturbed starts x0 .* (1 + randn/2) (:46-54); the
-best run is kept if Optim reports convergence, else the constants go back to
-x0 (:56-63). Every loss value is a full `eval_loss` (:12-19) and the
-gradient comes from finite differences of it.
+The reference optimises one PopMember at a time: Optim.Newton (one
+constant) or Optim.BFGS — or NelderMead (:35-36) — with
+LineSearches.BackTracking, `optimizer_iterations` = 8 (src/Options.jl:607-621),
+from x0 and from `optimizer_nrestarts` = 2 perturbed starts x0 .* (1 + randn/2)
+(:46-54); the best run is kept if Optim reports convergence, else the
+constants go back to x0 (:56-63).
 
-Here every start of every tree is one *candidate*, all candidates advance in
-lockstep, and each phase of the iteration is ONE engine launch over all of
-them: the constant vector of the compiled program is replaced
-(`srhip_program_set_constants`) and `srhip_eval_loss_grad` returns loss and
-the analytic forward-mode ∂L/∂c (or `srhip_eval_loss` for line-search trials).
-The per-candidate algebra (BFGS inverse-Hessian update, backtracking
-interpolation) is a few flops per constant and stays on the host.
+Here every start of every tree is a candidate and all candidates advance in
+lockstep inside libsrhip (srhip_optimize_constants_batch): each phase of an
+iteration is ONE launch over all of them (srhip_program_set_constants +
+srhip_eval_loss_grad / srhip_eval_loss). The per-candidate algebra runs in
+C++ next to the engine; this module draws the start noise (from the caller's
+numpy Generator, tree by tree, restart by restart — where the reference
+calls randn) and writes the results back into the trees.
 
-Deviations from Optim, all deliberate:
-* gradients are analytic (the engine's tangents), not finite differences;
-* Newton's Hessian (one constant) is the central difference of the analytic
-  gradient, made positive as PositiveFactorizations does for a 1×1 matrix;
-* `f_calls` counts loss evaluations (a loss+gradient launch counts once).
+`evaluator_factory` plugs any other evaluator into the same C++ driver
+through srhip_optimize_constants_cb (a row-sharded dataset whose partials
+are all-reduced, the oracle in tests): factory(candidates) returns an object
+with loss_grad(consts) -> (f, g) and loss_only(consts) -> f. No part of the
+optimiser runs in Python; tests/constopt_reference.py restates it as the
+checker.
 """
 from __future__ import annotations
 
+import ctypes as C
 from dataclasses import dataclass
-from typing import Callable, List, Optional, Sequence, Tuple
+from typing import Callable, Optional, Sequence
 
 import numpy as np
 
+from ._lib import CONSTOPT_EVAL_FN, ConstOptOptions, check, lib
 from .dataset import Dataset
-from .interface import eval_loss_batch
-from .node import FlatTrees, Node, flatten, get_constants, set_constants
+from .engine import _trees_struct
+from .node import Node, flatten, set_constants
 from .options import Options
 
-# Optim.Options defaults the reference inherits (g_abstol = 1e-8; x/f tolerances 0).
-G_TOL = 1e-8
-# LineSearches.BackTracking defaults (c_1, ρ_hi, ρ_lo, order = 3, iterations = 1000).
-# Its iterations = 1000 is replaced by 60 shrinks: each shrink multiplies α by at
-# most ρ_hi, so after 60 the step is below 2⁻⁶⁰ of the search direction and no
-# longer changes x in Float64; a candidate still failing Armijo then is a failed
-# line search (LineSearchException → Optim stops, not converged).
-C1, RHO_HI, RHO_LO, LS_ITERATIONS = 1e-4, 0.5, 0.1, 60
-# a line-search round with fewer than 1/SUBSET_FRACTION of the candidates still
-# shrinking moves them to a program of their own
-SUBSET_FRACTION = 10
+ALGORITHMS = {"BFGS": 0, "NelderMead": 1}  # SRHIP_OPT_*
 
 
 @dataclass
@@ -59,536 +52,110 @@ class ConstOptResult:
     num_evals: np.ndarray
 
 
-class EngineEvaluator:
-    """Loss / loss+gradient of all candidates in one launch each, through the
-    C ABI (srhip_program_set_constants + srhip_eval_loss[_grad])."""
-
-    def __init__(self, candidates, dataset: Dataset, options: Options, device: Optional[int] = None):
-        """candidates: a list of Node, or a FlatTrees batch (no Python trees)."""
-        from .engine import Program
-
-        self.dev = dataset.device(device)
-        flat = candidates if isinstance(candidates, FlatTrees) else flatten(candidates, options, dtype=dataset.T)
-        # the optimiser sets new constants on every step: memory-constant tree code from the start
-        self.prog = Program(self.dev.ctx, flat, dataset.T, varying_constants=True)
-        self.loss = options.elementwise_loss
-        self.T = dataset.T
-
-    def _set(self, consts: np.ndarray) -> None:
-        self.prog.set_constants(consts.astype(self.T, copy=False))
-
-    def subset(self, idx) -> "EngineEvaluator":
-        """An evaluator of candidates idx only (a small program: its launches
-        and constant updates cost little when few candidates are left)."""
-        sub = EngineEvaluator.__new__(EngineEvaluator)
-        from .engine import Program
-
-        sub.dev, sub.loss, sub.T = self.dev, self.loss, self.T
-        sub.prog = Program(self.dev.ctx, self.prog.flat.take(idx), self.T, varying_constants=True)
-        return sub
-
-    def loss_grad(self, consts: np.ndarray) -> Tuple[np.ndarray, np.ndarray]:
-        self._set(consts)
-        sums, grads, wsum, ok = self.prog.eval_loss_grad(self.dev, self.loss.kind, self.loss.params)
-        return _finish(sums, wsum, ok), _grad_finish(grads, wsum, ok, self.prog.flat.const_off)
-
-    def loss_only(self, consts: np.ndarray) -> np.ndarray:
-        self._set(consts)
-        sums, wsum, ok = self.prog.eval_loss(self.dev, self.loss.kind, self.loss.params)
-        return _finish(sums, wsum, ok)
-
-
 def _finish(sums, wsum, ok) -> np.ndarray:
+    """Loss of each candidate from engine partials (:12-19): Σw·ℓ/Σw, +Inf on failure."""
     with np.errstate(invalid="ignore", divide="ignore"):
         f = sums / wsum
-    f = np.where(ok & np.isfinite(f), f, np.inf)
-    return f
+    return np.where(ok & np.isfinite(f), f, np.inf)
 
 
 def _grad_finish(grads, wsum, ok, const_off) -> np.ndarray:
+    """∂L/∂c of each constant from engine partials, NaN for failed candidates."""
     g = grads / wsum
-    bad = np.repeat(~ok, np.diff(const_off))
-    g[bad] = np.nan
+    g[np.repeat(~ok, np.diff(const_off))] = np.nan
     return g
 
 
-def _backtrack_step(a1, a2, phi0, dphi0, phix0, phix1, first: bool) -> float:
-    """One BackTracking shrink (LineSearches.jl, order 3): quadratic
-    interpolation on the first shrink, cubic after, safeguarded to
-    [ρ_lo·α, ρ_hi·α]. Published algorithm: Nocedal & Wright §3.5."""
-    if first:
-        den = 2.0 * (phix1 - phi0 - dphi0 * a2)
-        at = -(dphi0 * a2 * a2) / den if den != 0 else np.nan
-    else:
-        div = 1.0 / (a1 * a1 * a2 * a2 * (a2 - a1))
-        r1 = phix1 - phi0 - dphi0 * a2
-        r0 = phix0 - phi0 - dphi0 * a1
-        a = (a1 * a1 * r1 - a2 * a2 * r0) * div
-        b = (-a1 ** 3 * r1 + a2 ** 3 * r0) * div
-        if abs(a) <= 1e-12 * max(1.0, abs(b)):
-            at = dphi0 / (2.0 * b) if b != 0 else np.nan
-        else:
-            d = max(b * b - 3.0 * a * dphi0, 0.0)
-            at = (-b + np.sqrt(d)) / (3.0 * a)
-    hi, lo = a2 * RHO_HI, a2 * RHO_LO
-    at = hi if not np.isfinite(at) else min(at, hi)  # NaNMath.min
-    return max(at, lo)
-
-
-def _backtrack_steps(a1, a2, phi0, dphi0, phix0, phix1, first):
-    """_backtrack_step for arrays of candidates (NaN/Inf arithmetic as IEEE)."""
-    with np.errstate(all="ignore"):
-        den = 2.0 * (phix1 - phi0 - dphi0 * a2)
-        at_q = np.where(den != 0, -(dphi0 * a2 * a2) / den, np.nan)
-        div = 1.0 / (a1 * a1 * a2 * a2 * (a2 - a1))
-        r1 = phix1 - phi0 - dphi0 * a2
-        r0 = phix0 - phi0 - dphi0 * a1
-        a = (a1 * a1 * r1 - a2 * a2 * r0) * div
-        b = (-a1 ** 3 * r1 + a2 ** 3 * r0) * div
-        lin = np.abs(a) <= 1e-12 * np.maximum(1.0, np.abs(b))
-        at_l = np.where(b != 0, dphi0 / (2.0 * b), np.nan)
-        d = np.maximum(b * b - 3.0 * a * dphi0, 0.0)
-        at_c = (-b + np.sqrt(d)) / (3.0 * a)
-        at = np.where(first, at_q, np.where(lin, at_l, at_c))
-        hi, lo = a2 * RHO_HI, a2 * RHO_LO
-        at = np.where(np.isfinite(at), np.minimum(at, hi), hi)  # NaNMath.min
-        return np.maximum(at, lo)
+def start_noise(flat, nrestarts: int, rng: np.random.Generator) -> np.ndarray:
+    """The standard normal draws of the perturbed starts in the C ABI's order
+    (tree by tree, restart by restart, :46-54)."""
+    co = flat.const_off
+    parts = []
+    for i in range(flat.ntrees):
+        n = int(co[i + 1] - co[i])
+        for _ in range(nrestarts if n else 0):
+            parts.append(rng.standard_normal(n))
+    return np.concatenate(parts) if parts else np.zeros(0)
 
 
 def optimize_constants_batch(dataset: Dataset, trees: Sequence[Node], options: Options,
                              rng: Optional[np.random.Generator] = None, device: Optional[int] = None,
                              evaluator_factory: Optional[Callable] = None) -> ConstOptResult:
     """`optimize_constants` for many trees at once. Trees are updated in place
-    (constants of the best start when it converged, else left at x0).
-    `evaluator_factory(candidates)` replaces the engine evaluator (tests use
-    it to run the same driver over the CPU oracle)."""
-    with np.errstate(all="ignore"):  # NaN/Inf losses and gradients are data here
-        return _optimize(dataset, trees, options, rng or np.random.default_rng(), device, evaluator_factory)
-
-
-def _optimize(dataset, trees, options, rng, device, evaluator_factory) -> ConstOptResult:
+    (constants of the best start when it converged, else left at x0)."""
     algorithm = getattr(options, "optimizer_algorithm", "BFGS")
-    if algorithm == "NelderMead":
-        # one constant: Newton whatever the option says (:32-33); more: NelderMead (:35-36)
-        multi = np.array([len(get_constants(t)) > 1 for t in trees], dtype=bool)
-        out = ConstOptResult(np.full(len(trees), np.inf), np.zeros(len(trees), dtype=bool), np.zeros(len(trees)))
-        for sel, fn in ((~multi, _optimize_gradient), (multi, _optimize_nelder_mead)):
-            idx = np.nonzero(sel)[0]
-            if idx.size == 0:
-                continue
-            r = fn(dataset, [trees[i] for i in idx], options, rng, device, evaluator_factory)
-            out.losses[idx], out.converged[idx], out.num_evals[idx] = r.losses, r.converged, r.num_evals
-        return out
-    if algorithm != "BFGS":
+    if algorithm not in ALGORITHMS:
         raise ValueError("Optimization function not implemented.")  # :39-41
-    return _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory)
-
-
-def _starts(flat: FlatTrees, T, nrestarts, rng):
-    """Candidates: x0 and `nrestarts` perturbed copies x0 .* (1 + randn/2) per
-    tree with constants (:42-54)."""
-    cand_tree: List[int] = []
-    cand_x: List[np.ndarray] = []
+    T = np.dtype(dataset.T).type
+    flat = flatten(trees, options, dtype=T)
+    nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
+    noise = np.ascontiguousarray(start_noise(flat, nrestarts, rng or np.random.default_rng()), dtype=np.float64)
+    loss = options.elementwise_loss
+    par = None if loss.params is None else np.ascontiguousarray(loss.params, dtype=np.float64)
+    opts = ConstOptOptions(ALGORITHMS[algorithm], int(getattr(options, "optimizer_iterations", 8)), nrestarts,
+                           int(loss.kind), None if par is None else par.ctypes.data_as(C.POINTER(C.c_double)),
+                           noise.ctypes.data_as(C.POINTER(C.c_double)), 0)
+    consts = np.ascontiguousarray(flat.consts, dtype=T)
+    tr = _trees_struct(flat, consts)
+    nt = len(trees)
+    out_c = np.zeros(max(consts.size, 1), dtype=T)
+    out_l = np.zeros(max(nt, 1))
+    out_k = np.zeros(max(nt, 1), dtype=np.uint8)
+    out_n = np.zeros(max(nt, 1))
+    ptrs = [a.ctypes.data_as(C.c_void_p) for a in (out_c, out_l, out_k, out_n)]
+    if evaluator_factory is None:
+        dev = dataset.device(device)
+        check(lib().srhip_optimize_constants_batch(dev.ctx.handle, dev.handle, C.byref(tr), C.byref(opts), *ptrs))
+    else:
+        cb = _Callback(trees, evaluator_factory)
+        rc = lib().srhip_optimize_constants_cb(C.byref(tr), 0 if T == np.float32 else 1, C.byref(opts),
+                                               cb.fn, None, *ptrs)
+        if cb.error is not None:
+            raise cb.error
+        check(rc)
+    conv = out_k[:nt].astype(bool)
     co = flat.const_off
-    for i in range(flat.ntrees):
-        x0 = np.asarray(flat.consts[co[i]:co[i + 1]], dtype=T)
-        if x0.size == 0:
-            continue
-        cand_tree.append(i)
-        cand_x.append(x0.copy())
-        for _ in range(nrestarts):  # :47
-            cand_tree.append(i)
-            cand_x.append((x0 * (T(1) + T(0.5) * rng.standard_normal(x0.size).astype(T))).astype(T))
-    return cand_tree, cand_x
+    for i in np.flatnonzero(conv):
+        set_constants(trees[i], [T(v) for v in out_c[co[i]:co[i + 1]]])
+    return ConstOptResult(out_l[:nt].copy(), conv, out_n[:nt].copy())
 
 
-def _optimize_gradient(dataset, trees, options, rng, device, evaluator_factory) -> ConstOptResult:
-    """BFGS (Newton for one constant) with BackTracking, all starts in lockstep."""
-    T = np.dtype(dataset.T).type
-    iterations = int(getattr(options, "optimizer_iterations", 8))
-    nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
+class _Callback:
+    """srhip_constopt_eval_fn over evaluator_factory: one evaluator per member
+    list the driver asks for (candidates, simplex vertices, line-search
+    stragglers, the final trees), built from copies of the input trees."""
 
-    ntrees = len(trees)
-    flat = flatten(trees, options, dtype=T)
-    cand_tree, cand_x = _starts(flat, T, nrestarts, rng)
-    losses = np.full(ntrees, np.inf)
-    converged_out = np.zeros(ntrees, dtype=bool)
-    num_evals = np.zeros(ntrees)
-    if not cand_tree:
-        return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat)
-                              if ntrees else losses, converged_out, num_evals)
-    ev = _make_evaluator(trees, flat, cand_tree, cand_x, dataset, options, device, evaluator_factory)
+    def __init__(self, trees, factory):
+        self.trees, self.factory = trees, factory
+        self.cache = {}
+        self.error = None
+        self.fn = CONSTOPT_EVAL_FN(self._eval)
 
-    nc = len(cand_tree)
-    sizes = np.array([x.size for x in cand_x])
-    off = np.concatenate([[0], np.cumsum(sizes)])
-    starts = off[:-1]
-    X = np.concatenate(cand_x).astype(T)
-    newton = sizes == 1
-    f_calls = np.zeros(nc)
-    # candidates grouped by constant count: the BFGS algebra runs batched per group
-    groups = {int(sz): np.nonzero(sizes == sz)[0] for sz in np.unique(sizes) if sz > 1}
-    gidx = {sz: starts[ks][:, None] + np.arange(sz)[None, :] for sz, ks in groups.items()}  # flat positions
-    invH = {sz: np.repeat(np.eye(sz)[None], len(ks), axis=0) for sz, ks in groups.items()}
-
-    def segsum(v):
-        return np.add.reduceat(v, starts)
-
-    def segmax_abs(v):
-        return np.maximum.reduceat(np.abs(v), starts)
-
-    f, G = ev.loss_grad(X)
-    f_calls += 1
-    active = np.isfinite(f)
-    with np.errstate(invalid="ignore"):
-        conv = active & (segmax_abs(G) <= G_TOL)  # converged at x0
-    active &= ~conv
-
-    for _ in range(iterations):
-        if not active.any():
-            break
-        # search directions
-        S = np.zeros_like(X, dtype=np.float64)
-        nw = newton & active
-        if nw.any():
-            step = np.where(nw, np.cbrt(np.finfo(T).eps) * np.maximum(1.0, np.abs(X[starts].astype(np.float64))), 0)
-            Xp, Xm = X.astype(np.float64), X.astype(np.float64)
-            Xp[starts[nw]] += step[nw]
-            Xm[starts[nw]] -= step[nw]
-            _, Gp = ev.loss_grad(Xp.astype(T))
-            _, Gm = ev.loss_grad(Xm.astype(T))
-            h = (Gp[starts] - Gm[starts]) / np.where(nw, 2 * step, 1.0)
-            hk = np.where(np.isfinite(h) & (np.abs(h) > np.finfo(T).eps), np.abs(h), 1.0)
-            S[starts[nw]] = -G[starts[nw]] / hk[nw]
-        for sz, ks in groups.items():
-            act = active[ks]
-            if not act.any():
-                continue
-            g = G[gidx[sz]]
-            sd = -np.einsum("mij,mj->mi", invH[sz], g)
-            bad = ~(np.einsum("mi,mi->m", g, sd) < 0)  # not a descent direction: restart from I
-            if (bad & act).any():
-                invH[sz][bad & act] = np.eye(sz)
-                sd[bad] = -g[bad]
-            S[gidx[sz][act]] = sd[act]
-        with np.errstate(invalid="ignore", over="ignore"):
-            dphi0 = np.where(active, segsum(G * S), 0.0)
-        # a NaN gradient (or no descent at all) ends the run: Optim's x would turn NaN
-        active &= np.isfinite(dphi0) & (dphi0 < 0)
-
-        # BackTracking line search, all candidates in lockstep
-        a1 = np.ones(nc)
-        a2 = np.ones(nc)
-        phix0 = f.copy()
-        searching = active.copy()
-        Xbase = X.astype(np.float64)
-        trial = ev.loss_only((Xbase + S).astype(T))
-        f_calls += searching
-        phix1 = np.where(searching, trial, f)
-        finite_left = np.where(searching, int(-np.log2(np.finfo(T).eps)), 0)
-        first = np.ones(nc, dtype=bool)
-        ls_iter = np.zeros(nc, dtype=int)
-        sub = None  # (candidates, evaluator, flat positions) once few are left searching
-        while True:
-            fin = np.isfinite(phix1)
-            halve = searching & ~fin & (finite_left > 0)  # halve until the loss is finite
-            searching &= fin | halve
-            with np.errstate(invalid="ignore"):
-                armijo = searching & fin & (phix1 <= f + C1 * a2 * dphi0)
-            searching &= ~armijo
-            failed = searching & fin & (ls_iter >= LS_ITERATIONS)  # failed line search: stays at x
-            searching &= ~failed
-            phix1 = np.where(failed, np.inf, phix1)
-            step = searching & fin
-            finite_left = np.where(halve, finite_left - 1, finite_left)
-            ls_iter = np.where(step, ls_iter + 1, ls_iter)
-            at = _backtrack_steps(a1, a2, f, dphi0, phix0, phix1, first)
-            shrink = halve | step
-            a1 = np.where(shrink, a2, a1)
-            a2 = np.where(halve, a2 * 0.5, np.where(step, at, a2))
-            first = np.where(step, False, first)
-            if not shrink.any():
-                break
-            alpha_full = np.repeat(a2, sizes)
-            Xt = np.where(np.repeat(shrink, sizes), Xbase + alpha_full * S, Xbase).astype(T)
-            if sub is None and hasattr(ev, "subset") and shrink.sum() * SUBSET_FRACTION < nc:
-                # the stragglers (a line search that keeps shrinking) continue on their own
-                # program: the full batch's launches and constant updates cost the same for
-                # 10 or 10⁴ candidates
-                ks = np.nonzero(searching | halve)[0]
-                pos = np.concatenate([np.arange(off[k], off[k + 1]) for k in ks])
-                sub = (ks, ev.subset(ks), pos)
-            if sub is not None:
-                ks, sev, pos = sub
-                trial = np.full(nc, np.inf)
-                trial[ks] = sev.loss_only(Xt[pos])
+    def _eval(self, _user, n, idx, consts, grad, out_f, out_g):
+        try:
+            members = np.ctypeslib.as_array(idx, shape=(n,)).copy() if n else np.zeros(0, dtype=np.int32)
+            key = members.tobytes()
+            ev = self.cache.get(key)
+            if ev is None:
+                ev = self.factory([self.trees[int(i)].copy() for i in members])
+                self.cache[key] = ev
+            nconst = sum(len(_consts_of(self.trees[int(i)])) for i in members)
+            x = np.ctypeslib.as_array(consts, shape=(nconst,)).copy() if nconst else np.zeros(0)
+            if grad:
+                f, g = ev.loss_grad(x)
+                if nconst:
+                    np.ctypeslib.as_array(out_g, shape=(nconst,))[:] = np.asarray(g, dtype=np.float64)
             else:
-                trial = ev.loss_only(Xt)
-            f_calls += shrink
-            phix0 = np.where(shrink, phix1, phix0)
-            phix1 = np.where(shrink, trial, phix1)
-
-        # accept, new gradient (one launch), BFGS update, convergence (Optim.converged)
-        moved = active & np.isfinite(phix1)
-        Xn = np.where(np.repeat(moved, sizes), Xbase + np.repeat(a2, sizes) * S, Xbase).astype(T)
-        fn, Gn = ev.loss_grad(Xn)
-        f_calls += moved
-        upd = active & moved & np.isfinite(fn)
-        active &= upd
-        dx_all = Xn.astype(np.float64) - X.astype(np.float64)
-        dg_all = Gn - G
-        with np.errstate(invalid="ignore", over="ignore"):
-            x_conv = segmax_abs(dx_all) <= 0.0
-            f_conv = np.abs(fn - f) <= 0.0
-            g_conv = segmax_abs(Gn) <= G_TOL
-        with np.errstate(all="ignore"):  # IEEE arithmetic: overflow gives Inf, as in Julia
-            for sz, ks in groups.items():
-                u = upd[ks]
-                if not u.any():
-                    continue
-                dx, dg = dx_all[gidx[sz]], dg_all[gidx[sz]]
-                dxdg = np.einsum("mi,mi->m", dx, dg)
-                u &= dxdg > 0
-                if not u.any():
-                    continue
-                H = invH[sz][u]
-                dxu, dgu, d = dx[u], dg[u], dxdg[u]
-                Hdg = np.einsum("mij,mj->mi", H, dgu)
-                outer_dx = dxu[:, :, None] * dxu[:, None, :]
-                coef = (d + np.einsum("mi,mi->m", dgu, Hdg)) / (d * d)
-                invH[sz][u] = (H + coef[:, None, None] * outer_dx
-                               - (Hdg[:, :, None] * dxu[:, None, :] + dxu[:, :, None] * Hdg[:, None, :])
-                               / d[:, None, None])
-        done = upd & (x_conv | f_conv | g_conv)
-        conv |= done
-        active &= ~done
-        keep = np.repeat(moved, sizes)
-        X = np.where(keep, Xn, X).astype(T)
-        G = np.where(keep, Gn, G)
-        f = np.where(moved & np.isfinite(fn), fn, f)
-
-    def seg(v, k):
-        return v[off[k]:off[k + 1]]
-
-    # best start per tree (:51-53), then the converged check (:56-63)
-    best = {}
-    for k, i in enumerate(cand_tree):
-        num_evals[i] += f_calls[k]
-        if i not in best or f[k] < f[best[i]]:
-            best[i] = k
-    for i, k in best.items():
-        if conv[k]:
-            vals = seg(X, k).astype(T)
-            set_constants(trees[i], [T(v) for v in vals])
-            flat.consts[flat.const_off[i]:flat.const_off[i + 1]] = vals
-            converged_out[i] = True
-            num_evals[i] += 1
-    return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat), converged_out,
-                          num_evals)
+                f = ev.loss_only(x)
+            if n:
+                np.ctypeslib.as_array(out_f, shape=(n,))[:] = np.asarray(f, dtype=np.float64)
+            return 0
+        except BaseException as e:  # reported after the C call returns
+            self.error = e
+            return 1
 
 
-def _make_evaluator(trees, flat, cand_tree, cand_x, dataset, options, device, factory, repeat=None):
-    """The evaluator of the candidates (start k = tree cand_tree[k] with
-    constants cand_x[k]); `repeat[k]` copies of each when given. The engine
-    takes the flattened batch directly; a test factory gets Node copies."""
-    idx = np.asarray(cand_tree) if repeat is None else np.repeat(cand_tree, repeat)
-    xs = cand_x if repeat is None else [x for x, r in zip(cand_x, repeat) for _ in range(r)]
-    if factory is None:
-        return EngineEvaluator(flat.take(idx, np.concatenate(xs)), dataset, options, device)
-    cands = []
-    for i, x in zip(idx, xs):
-        c = trees[i].copy()
-        set_constants(c, list(x))
-        cands.append(c)
-    return factory(cands)
+def _consts_of(tree: Node):
+    from .node import get_constants
 
-
-NM_INITIAL_A, NM_INITIAL_B = 0.025, 0.5  # Optim.AffineSimplexer defaults
-
-
-def _optimize_nelder_mead(dataset, trees, options, rng, device, evaluator_factory) -> ConstOptResult:
-    """Optim.NelderMead for trees of two or more constants (:35-36), every
-    start of every tree in lockstep. Optim is not vendored in the reference;
-    this restates its published algorithm (Optim.jl, nelder_mead.jl): the
-    affine initial simplex x0 + (a + b·x0_j)·e_j (a = 0.025, b = 0.5), the
-    adaptive parameters of Gao & Han (α = 1, β = 1 + 2/n, γ = 0.75 - 1/(2n),
-    δ = 1 - 1/n), reflection / expansion / outside and inside contraction /
-    shrink, convergence when the population standard deviation of the simplex
-    losses is <= g_abstol (1e-8), and the final minimiser = the centroid of
-    the best n vertices if its loss beats the best vertex. Launches per
-    iteration: one for the reflections, one for the expansion / contraction
-    points, one for the shrinks (all vertices); vertices live in T."""
-    T = np.dtype(dataset.T).type
-    iterations = int(getattr(options, "optimizer_iterations", 8))
-    nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
-    ntrees = len(trees)
-    flat = flatten(trees, options, dtype=T)
-    cand_tree, cand_x = _starts(flat, T, nrestarts, rng)
-    converged_out = np.zeros(ntrees, dtype=bool)
-    num_evals = np.zeros(ntrees)
-    if not cand_tree:
-        return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat),
-                              converged_out, num_evals)
-    nc = len(cand_tree)
-    sizes = [x.size for x in cand_x]
-    point_ev = _make_evaluator(trees, flat, cand_tree, cand_x, dataset, options, device, evaluator_factory)
-    simplex_ev = _make_evaluator(trees, flat, cand_tree, cand_x, dataset, options, device, evaluator_factory,
-                                 repeat=[sz + 1 for sz in sizes])  # every vertex
-
-    # initial simplex (AffineSimplexer) and its losses: one launch
-    simplex = []
-    for x0 in cand_x:
-        v = np.repeat(x0[None, :], x0.size + 1, axis=0).astype(T)
-        for j in range(x0.size):
-            v[j + 1, j] = T((1.0 + NM_INITIAL_B) * float(v[j + 1, j]) + NM_INITIAL_A)
-        simplex.append(v)
-
-    def eval_simplices():
-        fl = simplex_ev.loss_only(np.concatenate([v.reshape(-1) for v in simplex]))
-        out, o = [], 0
-        for k in range(nc):
-            out.append(np.asarray(fl[o:o + sizes[k] + 1], dtype=np.float64))
-            o += sizes[k] + 1
-        return out
-
-    def eval_points(pts):
-        return np.asarray(point_ev.loss_only(np.concatenate(pts)), dtype=np.float64)
-
-    def nm_x(fs):  # sqrt(var(f) * n/m), var with m-1: the population standard deviation
-        with np.errstate(invalid="ignore"):
-            return float(np.sqrt(np.mean((fs - fs.mean()) ** 2)))
-
-    def centroid(v, h):
-        return np.delete(v, h, axis=0).astype(np.float64).mean(axis=0)
-
-    fsx = eval_simplices()
-    f_calls = np.array([s + 1.0 for s in sizes])
-    order = [np.argsort(f, kind="stable") for f in fsx]
-    conv = np.zeros(nc, dtype=bool)
-    active = np.ones(nc, dtype=bool)
-    params = []
-    for n in sizes:
-        params.append((1.0, 1.0 + 2.0 / n, 0.75 - 1.0 / (2.0 * n), 1.0 - 1.0 / n))
-
-    for _ in range(iterations):
-        if not active.any():
-            break
-        # 1. reflections
-        xc, xh, xr = [None] * nc, [None] * nc, [None] * nc
-        for k in range(nc):
-            m = sizes[k] + 1
-            xc[k] = centroid(simplex[k], order[k][m - 1])
-            xh[k] = simplex[k][order[k][m - 1]].astype(np.float64)
-            xr[k] = (xc[k] + params[k][0] * (xc[k] - xh[k])).astype(T) if active[k] else simplex[k][0]
-        fr = eval_points(xr)
-        f_calls += active
-        # 2. expansion / contraction points
-        second = np.zeros(nc, dtype=int)  # 0 none, 1 expand, 2 outside, 3 inside
-        xs = [simplex[k][0] for k in range(nc)]
-        shrink = np.zeros(nc, dtype=bool)
-        for k in np.nonzero(active)[0]:
-            m = sizes[k] + 1
-            f, o = fsx[k], order[k]
-            al, be, ga, de = params[k]
-            xrf = xr[k].astype(np.float64)
-            if fr[k] < f[o[0]]:
-                second[k], xs[k] = 1, (xc[k] + be * (xrf - xc[k])).astype(T)
-            elif fr[k] < f[o[m - 2]]:
-                simplex[k][o[m - 1]], f[o[m - 1]] = xr[k], fr[k]
-                order[k] = np.argsort(f, kind="stable")
-            elif fr[k] < f[o[m - 1]]:
-                second[k], xs[k] = 2, (xc[k] + ga * (xrf - xc[k])).astype(T)
-            else:
-                second[k], xs[k] = 3, (xc[k] - ga * (xrf - xc[k])).astype(T)
-        if second.any():
-            fs2 = eval_points(xs)
-            f_calls += second > 0
-            for k in np.nonzero(second)[0]:
-                m = sizes[k] + 1
-                f, o = fsx[k], order[k]
-                h = o[m - 1]
-                if second[k] == 1:
-                    if fs2[k] < fr[k]:
-                        simplex[k][h], f[h] = xs[k], fs2[k]
-                    else:
-                        simplex[k][h], f[h] = xr[k], fr[k]
-                    order[k] = np.concatenate([[h], o[:m - 1]])  # the new vertex is the lowest
-                elif (second[k] == 2 and fs2[k] < fr[k]) or (second[k] == 3 and fs2[k] < f[h]):
-                    simplex[k][h], f[h] = xs[k], fs2[k]
-                    order[k] = np.argsort(f, kind="stable")
-                else:
-                    shrink[k] = True
-        # 3. shrinks towards the lowest vertex: every other vertex re-evaluated
-        if shrink.any():
-            for k in np.nonzero(shrink)[0]:
-                lo = simplex[k][order[k][0]].astype(np.float64)
-                de = params[k][3]
-                for i in order[k][1:]:
-                    simplex[k][i] = (lo + de * (simplex[k][i].astype(np.float64) - lo)).astype(T)
-            fall = eval_simplices()
-            for k in np.nonzero(shrink)[0]:
-                f = fsx[k]
-                for i in order[k][1:]:
-                    f[i] = fall[k][i]
-                f_calls[k] += sizes[k]
-                order[k] = np.argsort(f, kind="stable")
-        for k in np.nonzero(active)[0]:
-            if nm_x(fsx[k]) <= G_TOL:
-                conv[k], active[k] = True, False
-
-    # after the loop: the centroid of the best n vertices against the best vertex
-    xcen = []
-    for k in range(nc):
-        order[k] = np.argsort(fsx[k], kind="stable")
-        xcen.append(centroid(simplex[k], order[k][-1]).astype(T))
-    fcen = eval_points(xcen)
-    f_calls += 1
-    xmin, fmin = [], np.zeros(nc)
-    for k in range(nc):
-        i = julia_findmin(fsx[k])
-        if fcen[k] < fsx[k][i]:  # False for a NaN minimum: the NaN vertex is kept, as in Optim
-            xmin.append(xcen[k])
-            fmin[k] = fcen[k]
-        else:
-            xmin.append(simplex[k][i].copy())
-            fmin[k] = fsx[k][i]
-
-    best = {}
-    for k, i in enumerate(cand_tree):
-        num_evals[i] += f_calls[k]
-        if i not in best or fmin[k] < fmin[best[i]]:  # tmpresult.minimum < result.minimum (:51)
-            best[i] = k
-    for i, k in best.items():
-        if conv[k]:
-            vals = np.asarray(xmin[k], dtype=T)
-            set_constants(trees[i], [T(v) for v in vals])
-            flat.consts[flat.const_off[i]:flat.const_off[i + 1]] = vals
-            converged_out[i] = True
-            num_evals[i] += 1
-    return ConstOptResult(_final_losses(trees, dataset, options, device, evaluator_factory, flat), converged_out,
-                          num_evals)
-
-
-def julia_findmin(f) -> int:
-    """Index Julia's `findmin` picks (Optim's NelderMead after_while!): the
-    first NaN if there is one (findmin propagates NaN), else the first
-    minimum."""
-    f = np.asarray(f)
-    nan = np.flatnonzero(np.isnan(f))
-    return int(nan[0]) if nan.size else int(np.argmin(f))
-
-
-def _final_losses(trees, dataset, options, device, factory, flat=None) -> np.ndarray:
-    """Losses of the trees as they stand (one launch; the reference's
-    score_func re-score of a converged member, :58)."""
-    if factory is None:
-        prog = None
-        if flat is not None:
-            from .engine import Program
-
-            prog = Program(dataset.device(device).ctx, flat, dataset.T)
-        return np.asarray(eval_loss_batch(trees, dataset, options, device=device, program=prog), dtype=np.float64)
-    ev = factory(list(trees))
-    consts = [np.asarray(get_constants(t), dtype=np.float64) for t in trees]
-    X = np.concatenate(consts) if consts else np.zeros(0)
-    return ev.loss_only(X)
+    return get_constants(tree)

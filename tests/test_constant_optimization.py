@@ -328,7 +328,7 @@ def test_set_constants_in_place(gpu_ctx, T, n):
 def test_vectorised_backtrack_step_matches_scalar():
     """_backtrack_steps (all candidates at once) equals _backtrack_step (the
     LineSearches BackTracking order-3 interpolation) element by element."""
-    from srhip.constant_optimization import _backtrack_step, _backtrack_steps
+    from constopt_reference import _backtrack_step, _backtrack_steps
 
     rng = np.random.default_rng(4)
     n = 2000
@@ -365,7 +365,7 @@ def test_nelder_mead_minimiser_follows_julia_findmin():
     """Optim's after_while! takes findmin of the simplex losses: a NaN vertex is
     the minimum (findmin propagates NaN), and `f_centroid < NaN` is false, so
     that vertex is the result."""
-    from srhip.constant_optimization import julia_findmin
+    from constopt_reference import julia_findmin
     assert julia_findmin([3.0, 1.0, 2.0]) == 1
     assert julia_findmin([3.0, np.nan, 1.0, np.nan]) == 1
     assert julia_findmin([1.0, 1.0]) == 0
