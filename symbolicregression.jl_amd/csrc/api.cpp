@@ -1061,9 +1061,10 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
       // 16384 workgroups of 4 waves, >= 64 trees per group (16 per wave): config #2 kernel
       // 2.997 -> 2.867 ms at 4096 trees, 0.865 -> 0.828 at 1024, 512 unchanged
       // (profiles/r02n_targetwg.txt); scaled by the waves per workgroup
-      const int jw = jit::waves();
-      const size_t budget = std::max(jit_tile_budget() * jw / 4, jit::lds_per_workgroup() -
-                                     (jit::part_global() ? 0 : std::min<size_t>(jit::lds_per_workgroup() / 4, 8192)));
+      const int jw = jc.waves;
+      const size_t lds_wg = jit::lds_per_workgroup(jw);
+      const size_t budget = std::max(jit_tile_budget() * jw / 4,
+                                     lds_wg - (jit::part_global() ? 0 : std::min<size_t>(lds_wg / 4, 8192)));
       if (!plan_geometry(4, 4, kShallowSlots, narr, 1, rows, nlist, &plan, budget, 52 * 1024 * jw / 4,
                          16384 * 4 / jw, 64 * jw / 4))
         throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");

@@ -1122,17 +1122,22 @@ bool part_global() {
   static const bool g = [] { const char* e = std::getenv("SRHIP_JIT_PART_GLOBAL"); return e && e[0] == '1'; }();
   return g;
 }
-int waves() {
-  static const int w = [] {
+int choose_waves(int nraw) {
+  static const int forced = [] {
     const char* e = std::getenv("SRHIP_JIT_WAVES");
-    const int v = e ? std::atoi(e) : 4;
-    return v >= 1 && v <= 16 ? v : 4;
+    const int v = e ? std::atoi(e) : 0;
+    return v >= 1 && v <= 16 ? v : 0;
   }();
-  return w;
+  if (forced) return forced;
+  static const int wide = [] {  // SRHIP_JIT_WIDE_FEATURES: the feature count from which 8 waves
+    const char* e = std::getenv("SRHIP_JIT_WIDE_FEATURES");
+    return e ? std::max(1, std::atoi(e)) : 10;
+  }();
+  return nraw >= wide ? 8 : 4;
 }
 // 94 VGPRs: 5 waves per SIMD, 20 per CU; the CU's 160 KiB shared by its workgroups
-size_t lds_per_workgroup() {
-  const int per_cu = std::max(1, 20 / waves());
+size_t lds_per_workgroup(int waves) {
+  const int per_cu = std::max(1, 20 / std::max(1, waves));
   return (size_t)160 * 1024 / (size_t)per_cu;
 }
 
@@ -1186,7 +1191,9 @@ static Columns plan_columns(const CompiledBatch<float>& cb, const std::vector<in
   // workgroup's LDS, less the partials' share
   static const int dtiles = [] { const char* e = std::getenv("SRHIP_JIT_DERIVE_TILES"); return e ? std::max(1, std::atoi(e)) : 4; }();
   const size_t tile_bytes = (size_t)dtiles * (size_t)(64 * SR_JIT_R) * sizeof(float);
-  const size_t budget = lds_per_workgroup() - (part_global() ? 0 : std::min<size_t>(lds_per_workgroup() / 8, 4096));
+  c.waves = choose_waves(raw_max({}));  // from the raw features before any substitution
+  const size_t lds_wg = lds_per_workgroup(c.waves);
+  const size_t budget = lds_wg - (part_global() ? 0 : std::min<size_t>(lds_wg / 8, 4096));
   while (true) {
     const int nraw = raw_max(chosen);
     const size_t cols = 1 + (size_t)nraw + chosen.size();  // y, raw, derived (w, when weighted, may cost a tile)

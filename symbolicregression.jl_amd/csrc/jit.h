@@ -34,14 +34,18 @@ struct Columns {
   int nraw = 0;                  // raw feature columns staged (max feature used + 1)
   int nder = 0;                  // derived columns (column nraw + k)
   uint32_t der[kMaxDerived] = {};  // (operator << 16) | feature
+  int waves = 4;                 // waves per workgroup of the loss tree code (choose_waves)
 };
 const Columns& columns(const Module* m);
 // the module's tree code reads its constants from the device programs
 bool memc(const Module* m);
-// waves per workgroup of the loss tree code (SRHIP_JIT_WAVES) and the LDS a
-// workgroup may take while the CU still holds 5 waves per SIMD
-int waves();
-size_t lds_per_workgroup();
+// waves per workgroup of the loss tree code for a batch whose code reads
+// `nraw` raw features: 8 from 10 features on (twice the LDS per workgroup, so
+// a wide row tile still fits four times; config #5's shard 20.26 -> 17.10 ms,
+// profiles/r03_ab_cfg5.txt), else 4; SRHIP_JIT_WAVES forces a width. And the
+// LDS a workgroup of that width may take while the CU holds 5 waves per SIMD.
+int choose_waves(int nraw);
+size_t lds_per_workgroup(int waves);
 bool part_global();
 
 // Statistics of one build.

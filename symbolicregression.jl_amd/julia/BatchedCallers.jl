@@ -12,7 +12,14 @@
 #   * `finalize_scores_batched` — finalize_scores(dataset, pop, options)
 #   * `reg_evol_cycle_batched`  — reg_evol_cycle with fast_cycle semantics
 #     (one baby per tournament_selection_n-member subsample, replace-oldest),
-#     for several islands in lockstep: every island's babies in one launch.
+#     for several islands in lockstep: every island's babies in one launch,
+#     and every `:optimize` mutation of the cycle in one batched optimiser call.
+#   * `optimize_constants_batched` — optimize_constants (src/ConstantOptimization.jl:22-65)
+#     for many members: SRHip.optimize_constants_batch! (srhip_optimize_constants_batch,
+#     all starts of all members in lockstep, one launch per phase).
+#   * `optimize_and_simplify_population_batched` — optimize_and_simplify_population
+#     (src/SingleIteration.jl:63-123): the members drawn for optimisation go
+#     through one batched optimiser call instead of one Optim run each.
 #
 # next_generation is split into `propose` (mutation choice, attempts,
 # check_constraints — everything before score_func, calling the reference's
@@ -39,6 +46,10 @@ import ..MutationFunctionsModule:
     gen_random_tree, gen_random_tree_fixed_size, mutate_constant, mutate_operator, append_random_op,
     prepend_random_op, insert_random_op, delete_random_op
 import ..ConstantOptimizationModule: optimize_constants
+import ..UtilsModule: get_birth_order
+import ..PopMemberModule: generate_reference
+import ..RecorderModule: @recorder
+import DynamicExpressions: string_tree
 import ..SRHip
 
 """
@@ -108,6 +119,85 @@ function finalize_scores_batched(dataset::Dataset{T}, pop::Population, options::
     return (pop, pop.n * (options.batch_size / dataset.n))
 end
 
+# ---- constant optimisation ---------------------------------------------------------------
+
+"""
+    optimize_constants_batched(dataset, members, options) -> num_evals::Vector{Float64}
+
+optimize_constants (src/ConstantOptimization.jl:22-65) for every member at once,
+updated in place: a converged member gets the optimised constants, its
+score_func re-score (:58) and a new birth (:60); the others keep x0 (:62).
+One SRHip call when the engine covers the options, else the reference member
+by member.
+"""
+function optimize_constants_batched(dataset::Dataset{T}, members::AbstractVector{<:PopMember{T}},
+                                    options::Options) where {T}
+    isempty(members) && return Float64[]
+    if SRHip.enabled(options)
+        try
+            trees = Node{T}[m.tree for m in members]
+            losses, converged, num_evals = SRHip.optimize_constants_batch!(trees, dataset, options)
+            for (m, l, c) in zip(members, losses, converged)
+                c || continue
+                m.score = loss_to_score(l, dataset.baseline_loss, m.tree, options)
+                m.loss = l
+                m.birth = get_birth_order(; deterministic=options.deterministic)
+            end
+            return num_evals
+        catch e
+            e isa SRHip.Unsupported || rethrow()
+        end
+    end
+    evals = zeros(Float64, length(members))
+    for (j, m) in enumerate(members)
+        _, evals[j] = optimize_constants(dataset, m, options)
+    end
+    return evals
+end
+
+"""
+    optimize_and_simplify_population_batched(dataset, pop, options, curmaxsize, record) -> (pop, num_evals)
+
+optimize_and_simplify_population (src/SingleIteration.jl:63-123) with the
+members drawn for optimisation (rand(pop.n) .< optimizer_probability)
+optimised in one batched call and finalize_scores as one launch; the
+simplification, the new references and the record are the reference's.
+"""
+function optimize_and_simplify_population_batched(dataset::Dataset{T}, pop::Population, options::Options,
+                                                  curmaxsize::Int, record::RecordType) where {T}
+    do_optimization = rand(pop.n) .< options.optimizer_probability
+    for j in 1:(pop.n)
+        pop.members[j].tree = simplify_tree(pop.members[j].tree, options.operators)
+        pop.members[j].tree = combine_operators(pop.members[j].tree, options.operators)
+    end
+    chosen = options.should_optimize_constants ? findall(do_optimization) : Int[]
+    num_evals = sum(optimize_constants_batched(dataset, pop.members[chosen], options); init=0.0)
+    pop, tmp_num_evals = finalize_scores_batched(dataset, pop, options)
+    num_evals += tmp_num_evals
+    for j in 1:(pop.n)
+        old_ref = pop.members[j].ref
+        new_ref = generate_reference()
+        pop.members[j].parent = old_ref
+        pop.members[j].ref = new_ref
+        @recorder begin
+            @assert haskey(record, "mutations")
+            member = pop.members[j]
+            if !haskey(record["mutations"], "$(member.ref)")
+                record["mutations"]["$(member.ref)"] = RecordType(
+                    "events" => Vector{RecordType}(), "tree" => string_tree(member.tree, options.operators),
+                    "score" => member.score, "loss" => member.loss, "parent" => member.parent)
+            end
+            kind = (do_optimization[j] && options.should_optimize_constants) ? "simplification_and_optimization" :
+                   "simplification"
+            push!(record["mutations"]["$(old_ref)"]["events"],
+                  RecordType("type" => "tuning", "time" => time(), "child" => new_ref,
+                             "mutation" => RecordType("type" => kind)))
+            push!(record["mutations"]["$(old_ref)"]["events"], RecordType("type" => "death", "time" => time()))
+        end
+    end
+    return (pop, num_evals)
+end
+
 # ---- next_generation, split around its score_func call ---------------------------------
 
 # A proposal: either decided (`member` set: no score needed) or a tree to score.
@@ -121,7 +211,12 @@ struct Proposal{T}
     # options.batching its re-score on a fresh minibatch
     before_score::T
     before_loss::T
+    # an `:optimize` mutation (src/Mutate.jl:147-152): `member` holds the copy to
+    # optimise; reg_evol_cycle_batched optimises all of them in one batched call
+    optimize::Bool
 end
+Proposal{T}(parent, tree, member, accepted, num_evals, bs, bl) where {T} =
+    Proposal{T}(parent, tree, member, accepted, num_evals, bs, bl, false)
 
 # the tree-producing mutations of next_generation (src/Mutate.jl:79-115,132-139),
 # through the reference's own mutation functions
@@ -158,11 +253,9 @@ function propose(dataset::Dataset{T}, member::PopMember{T}, before::Tuple{T,T}, 
     if choice == :simplify
         return keep(combine_operators(simplify_tree(copy_node(prev), options.operators), options.operators), true)
     end
-    if choice == :optimize
-        m, evals = optimize_constants(dataset, PopMember(copy_node(prev), bs, bl;
-                                                         parent=member.ref, deterministic=options.deterministic),
-                                      options)
-        return Proposal{T}(member, nothing, m, true, evals, bs, bl)
+    if choice == :optimize  # optimised with the cycle's other :optimize proposals (reg_evol_cycle_batched)
+        m = PopMember(copy_node(prev), bs, bl; parent=member.ref, deterministic=options.deterministic)
+        return Proposal{T}(member, nothing, m, true, 0.0, bs, bl, true)
     end
     for _ in 1:10  # max_attempts
         tree = mutate_tree(choice, copy_node(prev), temperature, curmaxsize, options, dataset.nfeatures)
@@ -236,6 +329,9 @@ function reg_evol_cycle_batched(dataset::Dataset{T}, pops::AbstractVector{<:Popu
         q += length(as)
         proposals[k] = props
     end
+    # every :optimize mutation of every island in one batched optimiser call
+    to_opt = PopMember{T}[p.member for props in proposals for p in props if p.optimize]
+    num_evals += sum(optimize_constants_batched(dataset, to_opt, options); init=0.0)
     # one launch for every island's babies
     trees = Node{T}[p.tree for props in proposals for p in props if p.member === nothing]
     scores, losses = options.batching ? score_batch_minibatch(dataset, trees, options) :

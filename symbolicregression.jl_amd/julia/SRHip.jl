@@ -10,7 +10,7 @@
 # same entry points (tests/test_abi.py, tests/test_gpu_parity.py, ...).
 module SRHip
 
-using DynamicExpressions: Node, count_nodes
+using DynamicExpressions: Node, count_nodes, set_constants
 using LossFunctions: L2DistLoss, L1DistLoss, LPDistLoss, HuberLoss, LogCoshLoss, L1EpsilonInsLoss,
     L2EpsilonInsLoss, QuantileLoss, PeriodicLoss, LogitDistLoss
 import ..CoreModule: Options, Dataset
@@ -221,16 +221,50 @@ end
 destroy_dataset(h::Ptr{Cvoid}) = ccall((:srhip_dataset_destroy, libsrhip), Int32, (Ptr{Cvoid},), h)
 
 # one device copy per (Dataset, device) (src/Dataset.jl:24-64), uploaded once
-# and shared by the contexts of all threads; the table is guarded by CTX_LOCK
-const DEVICE_DATASETS = Dict{Tuple{UInt,Int},Tuple{Any,Ptr{Cvoid}}}()
+# and shared by the contexts of all threads. The table holds its Datasets
+# weakly (Dataset is a mutable struct): when a Dataset is collected its entry
+# goes, and the DeviceCopy's finaliser frees the device memory. Guarded by
+# CTX_LOCK.
+mutable struct DeviceCopy
+    h::Ptr{Cvoid}
+end
+function free!(d::DeviceCopy)
+    d.h == C_NULL && return nothing
+    destroy_dataset(d.h)
+    d.h = C_NULL
+    return nothing
+end
+const DEVICE_DATASETS = WeakKeyDict{Dataset,Dict{Int,DeviceCopy}}()
 function device_dataset(dataset::Dataset{T}, device::Int=0) where {T}
     lock(CTX_LOCK) do
-        key = (objectid(dataset), device)
-        entry = get(DEVICE_DATASETS, key, nothing)
-        (entry !== nothing && entry[1] === dataset) && return entry[2]
-        h = upload(dataset.X, dataset.y, dataset.weighted ? dataset.weights : nothing, device)
-        DEVICE_DATASETS[key] = (dataset, h)
-        return h
+        copies = get!(() -> Dict{Int,DeviceCopy}(), DEVICE_DATASETS, dataset)
+        d = get(copies, device, nothing)
+        d !== nothing && d.h != C_NULL && return d.h
+        d = DeviceCopy(upload(dataset.X, dataset.y, dataset.weighted ? dataset.weights : nothing, device))
+        finalizer(free!, d)
+        copies[device] = d
+        return d.h
+    end
+end
+"""Free the device copies of `dataset` now (they are also freed when the
+Dataset is garbage-collected)."""
+function release_dataset!(dataset::Dataset)
+    lock(CTX_LOCK) do
+        copies = pop!(DEVICE_DATASETS, dataset, nothing)
+        copies === nothing || foreach(free!, values(copies))
+    end
+    return nothing
+end
+# the device copy of the Dataset whose X this is, if one is uploaded (an
+# eval_tree_array on a Dataset's own X reuses it instead of uploading X again)
+function uploaded_dataset_of(X::AbstractMatrix, device::Int)
+    lock(CTX_LOCK) do
+        for (ds, copies) in DEVICE_DATASETS
+            ds.X === X || continue
+            d = get(copies, device, nothing)
+            d !== nothing && d.h != C_NULL && return d.h
+        end
+        return nothing
     end
 end
 
@@ -288,6 +322,67 @@ function eval_loss_grad_batch(p::Program, dataset::Dataset{T}, options::Options)
     return losses, grads, ok .== 1
 end
 
+# ---- batched constant optimisation (src/ConstantOptimization.jl:22-65) ----------------
+struct ConstOptOptions         # include/srhip.h: srhip_constopt_options
+    algorithm::Int32
+    iterations::Int32
+    nrestarts::Int32
+    loss_kind::Int32
+    loss_params::Ptr{Float64}
+    start_noise::Ptr{Float64}
+    seed::UInt64
+end
+const OPT_BFGS, OPT_NELDERMEAD = Int32(0), Int32(1)
+
+"""
+    optimize_constants_batch!(trees, dataset, options) -> (losses, converged, num_evals)
+
+optimize_constants (src/ConstantOptimization.jl:22-65) for every tree at once
+(srhip_optimize_constants_batch): all starts of all trees in lockstep on the
+engine, one launch per phase. The perturbed starts draw `randn(T, nconst)`
+per restart, tree by tree, where the reference does (:47). Trees whose run
+converged get the best start's constants (set_constants); the others keep
+x0 (:56-63). losses[i] is the loss of trees[i] at its final constants;
+num_evals[i] counts its loss evaluations (+1 for the re-score of a converged
+member, :58-59).
+"""
+function optimize_constants_batch!(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, options::Options;
+                                   device::Int=0) where {T}
+    algo = options.optimizer_algorithm == "BFGS" ? OPT_BFGS :
+           options.optimizer_algorithm == "NelderMead" ? OPT_NELDERMEAD :
+           error("Optimization function not implemented.")
+    node_off, kind, arg, const_off, consts = flatten(trees, options)
+    nt = length(trees)
+    nr = options.optimizer_nrestarts
+    noise = Float64[]
+    for i in 1:nt
+        nc = Int(const_off[i + 1] - const_off[i])
+        nc == 0 && continue
+        for _ in 1:nr
+            append!(noise, Float64.(randn(T, nc)))
+        end
+    end
+    kindcode, param = loss_code(options.elementwise_loss)
+    params = Float64[param]
+    out_c = similar(consts); out_l = Vector{Float64}(undef, nt)
+    out_k = Vector{UInt8}(undef, nt); out_n = Vector{Float64}(undef, nt)
+    GC.@preserve node_off kind arg const_off consts noise params out_c out_l out_k out_n begin
+        tr = Ref(SrhipTrees(Int32(nt), pointer(node_off), pointer(kind), pointer(arg), pointer(const_off),
+                            Ptr{Cvoid}(pointer(consts))))
+        opts = Ref(ConstOptOptions(algo, Int32(options.optimizer_options.iterations), Int32(nr), kindcode,
+                                   pointer(params), pointer(noise), UInt64(0)))
+        check(ccall((:srhip_optimize_constants_batch, libsrhip), Int32,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{SrhipTrees}, Ref{ConstOptOptions}, Ptr{Cvoid}, Ptr{Float64},
+                     Ptr{UInt8}, Ptr{Float64}),
+                    context(device), device_dataset(dataset, device), tr, opts, out_c, out_l, out_k, out_n))
+    end
+    converged = out_k .== 1
+    for i in 1:nt
+        converged[i] && set_constants(trees[i], out_c[(const_off[i] + 1):const_off[i + 1]])
+    end
+    return T.(out_l), converged, out_n
+end
+
 # ---- eval_tree_array (src/InterfaceDynamicExpressions.jl:50-52) -------------------
 """
     eval_tree_array(tree, X, options) -> (output, did_succeed)
@@ -297,18 +392,33 @@ for this call. On failure the output contents are unspecified, as in the
 reference (an undef array).
 """
 function eval_tree_array(tree::Node{T}, X::AbstractMatrix{T}, options::Options; device::Int=0) where {T}
+    out, ok = eval_tree_array_batch([tree], X, options; device=device)
+    return out[:, 1], ok[1]
+end
+
+"""
+    eval_tree_array_batch(trees, X, options) -> (outputs::Matrix (n, ntrees), did_succeed::Vector{Bool})
+
+Per-row outputs of many trees in one launch. When X is the X of a Dataset
+already on the device (device_dataset), that copy is used; otherwise X is
+uploaded for this call.
+"""
+function eval_tree_array_batch(trees::AbstractVector{Node{T}}, X::AbstractMatrix{T}, options::Options;
+                               device::Int=0) where {T}
     n = size(X, 2)
-    ds = upload(X, zeros(T, n), nothing, device)
-    p = Program([tree], options, device)
-    out = Vector{T}(undef, n); ok = Ref{UInt8}(0)
+    nt = length(trees)
+    shared = uploaded_dataset_of(X, device)
+    ds = shared === nothing ? upload(X, zeros(T, n), nothing, device) : shared
+    p = Program(trees, options, device)
+    out = Matrix{T}(undef, n, nt); ok = Vector{UInt8}(undef, nt)
     try
-        GC.@preserve out check(ccall((:srhip_eval_tree_array, libsrhip), Int32,
-                                     (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ref{UInt8}), ds, p.h, out, ok))
+        GC.@preserve out ok check(ccall((:srhip_eval_tree_array, libsrhip), Int32,
+                                        (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{UInt8}), ds, p.h, out, ok))
     finally
         destroy(p)
-        destroy_dataset(ds)
+        shared === nothing && destroy_dataset(ds)
     end
-    return out, ok[] == 1
+    return out, ok .== 1
 end
 
 # ---- eval_grad_tree_array (src/InterfaceDynamicExpressions.jl:83-107) -------------

@@ -1,8 +1,10 @@
 """Parity at BASELINE.json's full sizes (configs #2 and #3), on every tree.
 
 north_star: did_succeed must match bit-exactly on every tree; losses within
-1e-5 relative (F32) — a tree outside that bar must be ill-conditioned, i.e.
-within the loss spread of the oracle under ulp-scale perturbations
+1e-5 relative — on every succeeding tree of configs #2 and #3 (and of the
+config #5 sample, tests/test_configs_gpu.py), with no allowance for
+conditioning; config #3 is also held to 1e-10, where an outlier must lie
+within the oracle's loss spread under ulp-scale perturbations
 (tests/numerics.py). Plus a size-independent property: results are bitwise
 reproducible run to run (the early-exit flags only decide which row groups
 skip a failed tree).
@@ -35,7 +37,11 @@ def _record(name, rec):
         f.write(json.dumps(dict(test=name, **rec)) + "\n")
 
 
-def _check_losses(trees, o, X, y, T, losses, ok, ref_l, ref_ok, rtol, name=""):
+def _check_losses(trees, o, X, y, T, losses, ok, ref_l, ref_ok, rtol, name="", strict=False):
+    """did_succeed identical on every tree; losses within rtol of the oracle.
+    strict: every succeeding tree within rtol (north_star's bar, no allowance
+    for conditioning); otherwise an outlier must lie within 4x the oracle's
+    own spread under ulp-scale perturbations."""
     bad = np.flatnonzero(ok != ref_ok)
     print(f"did_succeed mismatches: {bad.size} of {len(trees)}: {bad[:20]}")
     assert bad.size == 0, f"did_succeed differs on {bad[:20]}"
@@ -49,6 +55,10 @@ def _check_losses(trees, o, X, y, T, losses, ok, ref_l, ref_ok, rtol, name=""):
     rec = dict(ntrees=len(trees), did_succeed_mismatch=int(bad.size), succeeding=int(m.sum()),
                outside_rtol=int(out.size), rtol=rtol, max_rel=float(np.max(rel[m])) if m.any() else 0.0,
                median_rel=float(np.median(rel[m])) if m.any() else 0.0)
+    if strict:
+        _record(name, rec)
+        assert out.size == 0, f"{out.size} trees outside {rtol}: {out[:20]}, worst rel {rec['max_rel']:.3g}"
+        return int(m.sum()), 0
     if out.size:
         sub = [trees[i] for i in out]
         sp = loss_spread(sub, o, X, y, None, T, nperturb=3) / X.shape[1]
@@ -77,7 +87,10 @@ def test_config2_full_4096_trees_1M_rows(gpu_ctx):
     losses, ok = srhip.eval_loss_batch_ok(trees, ds, o, program=prog)
     flat = srhip.flatten(trees, o, dtype=np.float32)
     _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, dtype=np.float32, nthreads=16)
-    n, nout = _check_losses(trees, o, X, y, np.float32, losses, ok, ref_l, ref_ok, 1e-5, name="config2")
+    # the north_star's 1e-5 on every succeeding tree (FAST path with the
+    # round-4 loss-parity guards)
+    n, nout = _check_losses(trees, o, X, y, np.float32, losses, ok, ref_l, ref_ok, 1e-5, name="config2",
+                            strict=True)
     assert n > 3000 and 0.05 < 1 - ok.mean() < 0.5
 
 
@@ -92,5 +105,7 @@ def test_config3_full_nan_heavy_f64(gpu_ctx):
     losses, ok = srhip.eval_loss_batch_ok(trees, ds, o)
     flat = srhip.flatten(trees, o, dtype=np.float64)
     _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, dtype=np.float64, nthreads=16)
+    # the north_star's 1e-5 on every succeeding tree, and 1e-10 up to conditioning
+    _check_losses(trees, o, X, y, np.float64, losses, ok, ref_l, ref_ok, 1e-5, name="config3_1e-5", strict=True)
     n, _ = _check_losses(trees, o, X, y, np.float64, losses, ok, ref_l, ref_ok, 1e-10, name="config3")
     assert 0.05 < ok.mean() < 0.95 and n > 200

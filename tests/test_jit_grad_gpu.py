@@ -95,6 +95,34 @@ def scales(trees, o, X, y, w, with_noise=False):
     return out + (np.concatenate(N),) if with_noise else out
 
 
+def scales32(trees, o, X, y, w):
+    """The oracle's Float32 evaluation of ∂L/∂c (the reference's precision):
+    per constant Σ|terms|, Σ terms, and what a 4-ulp move of ŷ (or y) moves
+    the terms by — the tight bound of the direct comparison (no perturbation
+    allowance)."""
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    y64 = y.astype(np.float64)
+    w64 = np.ones_like(y64) if w is None else w.astype(np.float64)
+    eps = float(np.finfo(np.float32).eps)
+    S, G, DV = [], [], []
+    for t in range(len(trees)):
+        k, a, c = flat.tree(t)
+        if len(c) == 0:
+            continue
+        with np.errstate(all="ignore"):
+            out, g, ok = oracle.eval_grad_consts(k, a, c.astype(np.float32), X, len(c), dtype=np.float32)
+            if not ok:
+                for L in (S, G, DV):
+                    L.append(np.full(len(c), np.nan))
+                continue
+            out, g = out.astype(np.float64), g.astype(np.float64)
+            term = w64 * 2.0 * (out - y64) * g
+            DV.append((np.abs(w64 * 2.0 * g) * (4 * eps * (np.abs(out) + np.abs(y64)))).sum(axis=1))
+        S.append(np.abs(term).sum(axis=1))
+        G.append(term.sum(axis=1))
+    return np.concatenate(S), np.concatenate(G), np.concatenate(DV)
+
+
 # Beyond this scale a constant's Float32 gradient overflows depending on the
 # order of its products (reverse mode multiplies from the seed 2·w·r down the
 # path, forward mode from 1 up): such trees have losses near 1e30 or more
@@ -155,6 +183,11 @@ def test_grad_tree_code_matches_interpreter_and_oracle(gpu_ctx, opset, weighted)
     check_grads(g1, ref, S, ok_c, 1e-4, 0.0, "tree code vs Float64 oracle", noise=N)
     check_grads(g0, ref, S, ok_c, 1e-4, 0.0, "interpreter vs Float64 oracle", noise=N)
     assert n1 > 500
+    # directly against the oracle's Float32 gradients, tight: 1e-5 of Σ|terms|
+    # plus a 4-ulp move of ŷ (the sums' rounding and the FAST forward), none beyond
+    S32, G32, DV = scales32(trees, o, X, y, w)
+    check_grads(g1, G32, S32, ok_c, 1e-5, 0.0, "tree code vs Float32 oracle", noise=DV / 4)
+    check_grads(g0, G32, S32, ok_c, 1e-5, 0.0, "interpreter vs Float32 oracle", noise=DV / 4)
 
 
 def test_grad_tree_code_many_constants_fall_back(gpu_ctx):

@@ -160,7 +160,7 @@ def test_binding_exposes_the_shim_api():
     # thread's context (srhip_eval_loss_batch_ctx), so threads run concurrently
     # on one shared dataset
     body = re.search(r"function device_dataset\(.*?\nend", src, re.S).group(0)
-    assert re.search(r"lock\(CTX_LOCK\) do", body) and "DEVICE_DATASETS[key]" in body and "device)" in body
+    assert re.search(r"lock\(CTX_LOCK\) do", body) and "DEVICE_DATASETS" in body and "device)" in body
     ev = re.search(r"function eval_loss_batch\(.*?\nend", src, re.S).group(0)
     assert "srhip_eval_loss_batch_ctx" in ev and "context(device)" in ev
     grad = re.search(r"function eval_loss_grad_batch\(.*?\nend", src, re.S).group(0)
@@ -188,8 +188,9 @@ def test_batched_callers_use_existing_functions():
                  "delete_random_op", "check_constraints", "score_func", "loss_to_score", "optimize_constants"):
         assert need in imported, need
     srhip_jl = JL.read_text()
-    for call in set(re.findall(r"SRHip\.(\w+)", code)):
-        assert re.search(rf"(function {call}\(|struct {call}\b|^{call}\()", srhip_jl, re.M), f"SRHip.{call} missing"
+    for call in set(re.findall(r"SRHip\.([\w!]+)", code)):
+        c = re.escape(call)
+        assert re.search(rf"(function {c}\(|struct {c}\b|^{c}\()", srhip_jl, re.M), f"SRHip.{call} missing"
     for fn in ("population_batched", "finalize_scores_batched", "reg_evol_cycle_batched", "propose", "accept"):
         assert re.search(rf"^function {fn}\(", code, re.M), fn
     if REFERENCE_SRC.exists():
@@ -199,4 +200,64 @@ def test_batched_callers_use_existing_functions():
             if name in dyn or name in ("Options", "Dataset", "RecordType", "RunningSearchStatistics", "PopMember",
                                        "Population"):
                 continue  # DynamicExpressions (not vendored) or types
-            assert re.search(rf"function {re.escape(name)}\(", defs), f"{name} is not defined in the reference"
+            assert re.search(rf"(function {re.escape(name)}\(|^{re.escape(name)}\(.*\) =)", defs, re.M), \
+                f"{name} is not defined in the reference"
+
+
+def test_device_datasets_are_weak_and_freed():
+    """the device copies of a Dataset are held weakly
+    (WeakKeyDict keyed by the mutable Dataset) and freed by a finaliser that
+    calls srhip_dataset_destroy, or at once by release_dataset!."""
+    src = JL.read_text()
+    assert re.search(r"const DEVICE_DATASETS = WeakKeyDict\{Dataset,", src)
+    assert re.search(r"mutable struct DeviceCopy", src)
+    body = re.search(r"function device_dataset\(.*?\nend", src, re.S).group(0)
+    assert "finalizer(free!, d)" in body
+    free = re.search(r"function free!\(d::DeviceCopy\).*?\nend", src, re.S).group(0)
+    assert "destroy_dataset(d.h)" in free and "d.h = C_NULL" in free
+    assert re.search(r"^function release_dataset!\(", src, re.M)
+    # the reference's Dataset is a mutable struct (a WeakKeyDict needs one)
+    if REFERENCE_SRC.exists():
+        assert re.search(r"mutable struct Dataset\{", (REFERENCE_SRC / "Dataset.jl").read_text())
+
+
+def test_eval_tree_array_reuses_an_uploaded_dataset():
+    """eval_tree_array on a Dataset's own X uses that dataset's device copy
+    (no per-call upload of X); other X are uploaded for the call and freed."""
+    src = JL.read_text()
+    body = re.search(r"function eval_tree_array_batch\(.*?\nend", src, re.S).group(0)
+    assert "uploaded_dataset_of(X, device)" in body
+    assert "shared === nothing && destroy_dataset(ds)" in body
+    one = re.search(r"function eval_tree_array\(.*?\nend", src, re.S).group(0)
+    assert "eval_tree_array_batch(" in one and "upload(" not in one
+
+
+def test_constopt_struct_matches_the_header():
+    """SRHip.ConstOptOptions mirrors srhip_constopt_options field by field."""
+    hdr = re.sub(r"/\*.*?\*/", "", HDR.read_text(), flags=re.S)
+    cstruct = re.search(r"typedef struct srhip_constopt_options \{(.*?)\}", hdr, re.S).group(1)
+    cfields = [re.match(r"\s*(.*?)\s*(\w+)$", f.strip()).groups() for f in cstruct.split(";") if f.strip()]
+    jl = re.search(r"struct ConstOptOptions.*?\n(.*?)\nend", JL.read_text(), re.S).group(1)
+    jfields = [ln.split("#")[0].strip().split("::") for ln in jl.splitlines() if "::" in ln]
+    assert [n for _, n in cfields] == [n for n, _ in jfields]
+    kinds = {"int32_t": "Int32", "const double*": "Ptr{Float64}", "uint64_t": "UInt64"}
+    assert [kinds[t] for t, _ in cfields] == [t for _, t in jfields]
+
+
+def test_batched_optimiser_is_used_by_the_callers():
+    """optimize_and_simplify_population (SingleIteration.jl:63-82)
+    and the :optimize mutation go through SRHip.optimize_constants_batch!
+    (srhip_optimize_constants_batch), not the per-member CPU optimiser."""
+    src = JL.read_text()
+    body = re.search(r"function optimize_constants_batch!\(.*?\nend", src, re.S).group(0)
+    assert "srhip_optimize_constants_batch" in body and "randn(T, nc)" in body
+    assert "options.optimizer_options.iterations" in body and "set_constants(trees[i]" in body
+    code = "\n".join(ln.split("#")[0] for ln in BATCHED.read_text().splitlines())
+    oc = re.search(r"function optimize_constants_batched\(.*?\nend", code, re.S).group(0)
+    assert "SRHip.optimize_constants_batch!(" in oc
+    pop = re.search(r"function optimize_and_simplify_population_batched\(.*?\nend", code, re.S).group(0)
+    assert "optimize_constants_batched(" in pop and "finalize_scores_batched(" in pop
+    prop = re.search(r"function propose\(.*?\nend", code, re.S).group(0)
+    assert "optimize_constants(" not in prop  # deferred to one batched call per cycle
+    cyc = re.search(r"function reg_evol_cycle_batched\(.*?\nend", code, re.S).group(0)
+    assert "optimize_constants_batched(dataset, to_opt, options)" in cyc
