@@ -195,11 +195,25 @@ struct GradGen {
     static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_LOSS_GUARDS"); return !(e && e[0] == '0'); }();
     return on;
   }
+  // The gradient's thresholds (SRHIP_GJIT_*_LOG2, own defaults): a term
+  // w·2r·∂ŷ/∂c near a pole weighs the row's FAST rounding more than the loss
+  // does (the derivative factor 1/b, or the reverse pass's sin / cos at the
+  // forward argument), so the gradient code guards tighter than the loss code
+  static int env_log2(const char* name, int dflt, int lo, int hi) {
+    const char* e = std::getenv(name);
+    return e ? std::max(lo, std::min(hi, std::atoi(e))) : dflt;
+  }
   static uint32_t can_eps_bits() {  // 2^-k
     static const uint32_t b = [] {
-      const char* e = std::getenv("SRHIP_JIT_CAN_LOG2");
-      const int k = e ? std::max(1, std::min(100, std::atoi(e))) : (loss_guards_on() ? 7 : 14);
+      const int k = env_log2("SRHIP_GJIT_CAN_LOG2", loss_guards_on() ? 7 : 14, 1, 100);
       return (uint32_t)(127 - k) << 23;
+    }();
+    return b;
+  }
+  static uint32_t trig_lim_bits() {  // 2^k
+    static const uint32_t b = [] {
+      const int k = env_log2("SRHIP_GJIT_TRIG_GUARD_LOG2", loss_guards_on() ? 10 : 14, 1, 100);
+      return (uint32_t)(127 + k) << 23;
     }();
     return b;
   }
@@ -264,7 +278,15 @@ struct GradGen {
         mark(o.a);
       }
     }
-    static const bool fast_env = [] { const char* e = std::getenv("SRHIP_GJIT_FAST"); return !(e && e[0] == '0'); }();
+    // The forward pass runs the PRECISE routines by default (round 4): with
+    // guards tight enough that every constant's ∂L/∂c stays within 1e-5 of
+    // Σ|terms| of the oracle's Float32 gradient (SRHIP_GJIT_TRIG_GUARD_LOG2=6),
+    // the guarded FAST forward redoes so many tiles that it costs what the
+    // PRECISE forward does (config #5 shard 48.5 vs 48.5 ms), and with the
+    // loss code's thresholds it leaves constants up to 1.8 % of Σ|terms| off
+    // (round 3's guards: 112 %; profiles/r04_grad_guards.txt).
+    // SRHIP_GJIT_FAST=1: the guarded FAST forward.
+    static const bool fast_env = [] { const char* e = std::getenv("SRHIP_GJIT_FAST"); return e && e[0] == '1'; }();
     fast = fast_env && trans;
     if (fast) {
       for (int i = 0; i < n; ++i) {
@@ -569,8 +591,7 @@ struct GradGen {
       if (fast && o.kind == K_UN && o.op == SRHIP_UOP_EXP) {
         if (exp_tainted(o)) {  // |u| > 16 fires the 87 check: u counts 87/16 = 5.4375 times
           static const uint32_t scale = [] {  // 87 / 2^k (jit.cpp Gen::exp_scale_bits)
-            const char* ev = std::getenv("SRHIP_JIT_EXP_GUARD_LOG2");
-            const int k = ev ? std::max(0, std::min(6, std::atoi(ev))) : 4;
+            const int k = env_log2("SRHIP_GJIT_EXP_GUARD_LOG2", 4, 0, 6);
             const float v = 87.0f / (float)(1 << k);
             uint32_t u;
             std::memcpy(&u, &v, 4);
@@ -877,7 +898,7 @@ struct GradGen {
         as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
       }
       if (g_trig) {
-        as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(loss_guards_on() ? 0x44800000u : 0x46800000u), VGTRIG_G);  // 2^10 (2^14)
+        as.vopc(VOPC_NGE_F32, "v_cmp_nge_f32_e32", K(trig_lim_bits()), VGTRIG_G);  // !(2^k >= max|x|)
         as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_redo);
       }
       as.bind(L_skip);
