@@ -338,6 +338,10 @@ int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntre
  * tiles that tree code redid with the Float64-evaluated routines (a FAST-path
  * guard fired or the tile failed; out_redone may be NULL). */
 int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* out_redone);
+/* Trees the last eval on this context ran as tree code (0: all interpreted;
+ * Float32 loss evaluations: L2 and, compiled at their first use, L1 / LP /
+ * Huber / the epsilon-insensitive losses / Quantile / Periodic). */
+int32_t srhip_last_tree_code(const srhip_ctx* ctx, int32_t* out_ntrees);
 /* Testing hook (no device needed): compile Float32 trees with the tree
  * compiler (fast: bit 0 the guarded FAST path, bit 1 memory-constant code).
  * Returns the code bytes, their assembly text ('\n'-separated lines)

@@ -188,6 +188,7 @@ struct srhip_ctx {
   double last_ms = 0.0;
   int last_launches = 0;
   int last_bailed = 0;  // trees re-evaluated after their tree code handed a tile back
+  int last_jit_trees = 0;  // trees the last evaluation ran as tree code
   int64_t last_redone = 0;  // tiles tree code redid with the PRECISE routines
   DevBuf partial, sums, oks, dloss, scratch_idx, gather, derived;
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
@@ -238,6 +239,11 @@ struct srhip_program {
   // tree code (jit.cpp) of the first nlist_j shallow slots, Float32 programs
   jit::Module* jit = nullptr;
   int nlist_j = 0;
+  std::vector<int32_t> h_jit_list;  // the trees of those slots, in slot order
+  // the same trees' tree code for other elementwise losses (jit::Options::loss),
+  // built at a loss's first evaluation; null m: that loss runs interpreted
+  struct LossJit { int kind; uint32_t bits; jit::Module* m; };
+  mutable std::vector<LossJit> jit_loss;
   jit::Stats jit_stats;
   // tree code is compiled for one constant set: a program whose constants are
   // set again (srhip_program_set_constants) runs on the interpreter
@@ -386,9 +392,15 @@ void upload_gconsts(srhip_program* p) {
   HIP_CHECK(hipStreamSynchronize(p->ctx->stream));
 }
 
+void free_loss_jits(const srhip_program* p) {
+  for (auto& l : p->jit_loss) jit::destroy(l.m);
+  p->jit_loss.clear();
+}
+
 void free_program_device(srhip_program* p) {
   jit::destroy(p->jit);
   p->jit = nullptr;
+  free_loss_jits(p);
   p->nlist_j = 0;
   if (p->d_code) (void)hipFree(p->d_code);
   if (p->d_verdict) (void)hipFree(p->d_verdict);
@@ -738,6 +750,8 @@ void build_program(srhip_program* p) {
   // trees lead the shallow list, the others follow (interpreter)
   jit::destroy(p->jit);
   p->jit = nullptr;
+  free_loss_jits(p);
+  p->h_jit_list.clear();
   p->nlist_j = 0;
   p->jit_stats = jit::Stats();
   if constexpr (std::is_same<T, float>::value) {
@@ -750,6 +764,7 @@ void build_program(srhip_program* p) {
       p->jit = jit::build(cb, a, jl, rest, jo, &p->jit_stats);
       if (p->jit) {
         p->nlist_j = (int)jl.size();
+        p->h_jit_list = jl;
         a = jl;
         a.insert(a.end(), rest.begin(), rest.end());
       }
@@ -872,15 +887,15 @@ static bool rotate_enabled() {
 // fast reduction, jit_template.hip) are evaluated again, whole, by the
 // shallow interpreter kernel; finalize overwrites their results.
 template <typename T>
-void rerun_bailed(srhip_ctx* c, const srhip_program* p, const EvalArgs<T>& ja, const EvalPlan& jplan, int nfeat,
-                  int64_t rows, int loss, double lparam) {
+void rerun_bailed(srhip_ctx* c, const srhip_program* p, jit::Module* jm, const EvalArgs<T>& ja, const EvalPlan& jplan,
+                  int nfeat, int64_t rows, int loss, double lparam) {
   (void)jplan;
   if constexpr (std::is_same<T, float>::value) {
     hipStream_t s = c->stream;
     const int nj = p->nlist_j;
     if (!jit::can_bail()) return;  // no routine hands a tile back: the finalize copied the counters
     std::vector<uint32_t> flags((size_t)nj + 2);
-    HIP_CHECK(hipMemcpyAsync(flags.data(), jit::bail_flags(p->jit), flags.size() * sizeof(uint32_t),
+    HIP_CHECK(hipMemcpyAsync(flags.data(), jit::bail_flags(jm), flags.size() * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, s));
     HIP_CHECK(hipStreamSynchronize(s));
     c->last_redone = flags[nj + 1];
@@ -981,6 +996,44 @@ void tail_split(const srhip_ctx* c, EvalPlan* plan, int64_t rows, int jw) {
   plan->nrg = (int)(nbig + nsmall);
 }
 
+// The tree code of a Float32 program for an elementwise loss: the L2 build
+// itself, or (other losses) the same trees compiled with that loss's tile
+// tail, built at the loss's first evaluation and kept with the program
+// (SRHIP_JIT_LOSSES=0: other losses interpreted). Null: no tree code.
+jit::Module* loss_module(const srhip_program* p, int loss, double lparam) {
+  if (!p->jit || p->nlist_j == 0) return nullptr;
+  if (loss == SRHIP_LOSS_L2) return p->jit;
+  static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_LOSSES"); return !(e && e[0] == '0'); }();
+  if (!on || loss < 0 || loss >= SRHIP_NUM_LOSSES || !jit::has_loss_routine(loss)) return nullptr;
+  const float pf = (float)lparam;
+  uint32_t bits;
+  std::memcpy(&bits, &pf, 4);
+  for (const auto& l : p->jit_loss)
+    if (l.kind == loss && l.bits == bits) return l.m;
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->consts.data();
+  CompiledBatch<float> cb = compile_batch_par<float>(tr);
+  jit::Options jo;
+  jo.fast = jit_fast_enabled();
+  jo.memc = jit::memc(p->jit);
+  jo.loss = loss;
+  jo.lparam = bits;
+  std::vector<int32_t> jl, rest;
+  jit::Stats st;
+  jit::Module* m = jit::build(cb, p->h_jit_list, jl, rest, jo, &st);
+  if (m && (jl != p->h_jit_list || !rest.empty())) {
+    jit::destroy(m);  // a different slot layout: this loss runs interpreted
+    m = nullptr;
+  }
+  p->jit_loss.push_back({loss, bits, m});
+  return m;
+}
+
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
 // n_pad) may be the dataset itself or a gathered row subset.
 template <typename T>
@@ -1004,8 +1057,9 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   }
   const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
   // slot ranges: [0, nj) tree code, [nj, nlist_a) shallow interpreter, then deep
-  const bool use_jit = std::is_same<T, float>::value && p->jit && p->nlist_j > 0 && mode == MODE_LOSS &&
-                       loss == SRHIP_LOSS_L2;
+  jit::Module* jm = (std::is_same<T, float>::value && mode == MODE_LOSS) ? loss_module(p, loss, lparam) : nullptr;
+  const bool use_jit = jm != nullptr;
+  c->last_jit_trees = (use_jit && rows > 0) ? p->nlist_j : 0;
   const int nj = use_jit ? p->nlist_j : 0;
   // failure flags (and the tree code's bail flags): the finalize kernels of
   // the previous call left them clean; one clearing launch only after a new
@@ -1020,7 +1074,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     }
     if (!c->fail_clean || jit_bail)
       HIP_CHECK(launch_zero_words(static_cast<uint32_t*>(c->fail.p), (int64_t)(c->fail.bytes / sizeof(uint32_t)),
-                                  jit_bail ? jit::bail_flags(p->jit) : nullptr, jit_bail ? jit::flag_words(p->jit) : 0,
+                                  jit_bail ? jit::bail_flags(jm) : nullptr, jit_bail ? jit::flag_words(jm) : 0,
                                   s));
     c->fail_clean = false;  // until every finalize of this call is enqueued
   }
@@ -1030,9 +1084,9 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   std::vector<Launch> launches;
   if (nj > 0) {
     if constexpr (std::is_same<T, float>::value) {
-      for (int k = 0; k < jit::nparts(p->jit); ++k) {
+      for (int k = 0; k < jit::nparts(jm); ++k) {
         int s0, nsl;
-        jit::part(p->jit, k, &s0, &nsl);
+        jit::part(jm, k, &s0, &nsl);
         launches.push_back({-1, s0, nsl, k});
       }
     }
@@ -1054,7 +1108,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     EvalPlan plan;
     if (pass == -1) {
       // LDS columns: y, the raw features the tree code reads, its derived columns, w
-      const jit::Columns& jc = jit::columns(p->jit);
+      const jit::Columns& jc = jit::columns(jm);
       if (jc.nraw > nfeat) throw Error(SRHIP_ERR_INVALID, "dataset has fewer features than the program reads");
       const int narr = 1 + jc.nraw + jc.nder + (w ? 1 : 0);
       // partials go to global memory: LDS holds the tiles (1 byte per slot keeps the slot bound away)
@@ -1111,22 +1165,22 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     if (pass == -1) {
       if constexpr (std::is_same<T, float>::value) {
         // the derived columns of this call, once per row, before the first part
-        const jit::Columns& jc = jit::columns(p->jit);
+        const jit::Columns& jc = jit::columns(jm);
         static const bool precompute = [] { const char* e = std::getenv("SRHIP_JIT_DERIVE_PRE"); return !(e && e[0] == '0'); }();
         const float* dcols = nullptr;
         if (jc.nder > 0 && precompute) {
           c->derived.ensure((size_t)jc.nder * (size_t)n_pad * sizeof(float));
-          if (launches[li].part == 0) HIP_CHECK(jit::launch_derive(p->jit, X, n_pad, static_cast<float*>(c->derived.p), s));
+          if (launches[li].part == 0) HIP_CHECK(jit::launch_derive(jm, X, n_pad, static_cast<float*>(c->derived.p), s));
           dcols = static_cast<const float*>(c->derived.p);
         }
-        HIP_CHECK(jit::launch(p->jit, launches[li].part, plan, a, jit_fast_enabled(), dcols, s));
+        HIP_CHECK(jit::launch(jm, launches[li].part, plan, a, jit_fast_enabled(), dcols, s));
       }
     } else {
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
     timed_end(c, s, tk);
     // the last tree-code part's finalize hands over and clears the tree code's counters
-    uint32_t* cnt = (last_jit && !jit_bail) ? jit::bail_flags(p->jit) + nj : nullptr;
+    uint32_t* cnt = (last_jit && !jit_bail) ? jit::bail_flags(jm) + nj : nullptr;
     HIP_CHECK(launch_finalize<T>(a, c->res_sum, c->res_ok, s, cnt, cnt ? c->pin_cnt : nullptr));
     if (cnt) c->cnt_pending = true;
     static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
@@ -1138,7 +1192,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
                    pass == -1 ? "tree-code" : pass == 0 ? "shallow" : "deep", nlist, ms, plan.nrg, plan.ntg,
                    plan.ntiles);
     }
-    if (last_jit) rerun_bailed<T>(c, p, a, plan, nfeat, rows, loss, lparam);
+    if (last_jit) rerun_bailed<T>(c, p, jm, a, plan, nfeat, rows, loss, lparam);
   }
   if (mode == MODE_LOSS) c->fail_clean = true;
 }
@@ -2076,6 +2130,14 @@ int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, i
     if (out_code_bytes) *out_code_bytes = on ? (int64_t)prog->jit_stats.code_bytes : 0;
     if (out_ms_codegen) *out_ms_codegen = on ? prog->jit_stats.ms_codegen : 0.0;
     if (out_ms_load) *out_ms_load = on ? prog->jit_stats.ms_load : 0.0;
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_last_tree_code(const srhip_ctx* ctx, int32_t* out_ntrees) {
+  return guarded([&] {
+    if (!ctx || !out_ntrees) throw Error(SRHIP_ERR_INVALID, "null argument");
+    *out_ntrees = ctx->last_jit_trees;
     return SRHIP_OK;
   });
 }

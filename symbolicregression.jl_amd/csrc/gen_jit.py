@@ -129,8 +129,19 @@ INLINE_BOPS = {"ADD", "SUB", "MUL"}
 INLINE_UOPS = {"NEG", "ABS", "SQUARE", "CUBE"}
 
 
+def losses():
+    """SRHIP_LOSS_* of include/srhip.h: {name: id}."""
+    txt = open(G.INCLUDE).read()
+    return {m.group(1): int(m.group(2)) for m in re.finditer(r"#define SRHIP_LOSS_(\w+)\s+(\d+)", txt)}
+
+
+LOSSES = losses()
+
+
 def routine_list():
-    """(name, body, trig) of every routine: one per operator not emitted inline."""
+    """(name, body, trig) of every routine: one per operator not emitted inline,
+    and one per elementwise loss but L2 (r in A -> ℓ(r) in A, the parameter in
+    s_k: device_ops.h elem_loss with ŷ = r, y = 0, so r - 0 = r exactly)."""
     rs = []
     for u in sorted(UOPS, key=lambda k: UOPS[k]):
         if u in INLINE_UOPS:
@@ -182,6 +193,12 @@ def routine_list():
         rs.append((f"b_{b.lower()}_lc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
         if b == "DIV":
             rs.append(("b_div_lc_full", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
+    for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
+        if name == "L2":
+            continue
+        imm = "const float imm = __int_as_float((int)s.s_k); "
+        rs.append((f"l_{name.lower()}",
+                   imm + rows(f"s.a[r] = dev::elem_loss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"), False))
     return rs
 
 
@@ -483,6 +500,17 @@ def build(hipcc, outdir, R):
     trig = {n for n, _, t in routines if t}
     vstate = set(range(rg.A, rg.VEND))
     sstate = {r for _, r in rg.sregs()}
+    # a loss routine runs between the tiles of memory-constant tree code, whose
+    # constants live in s24..s39 (jit.cpp Gen::SC0): one whose SGPR temporaries
+    # reach them (logcosh, logitdist: Float64 constants) is left out, and that
+    # loss runs interpreted (SR_JIT_LOSS_ROUTINE -1)
+    for n in [n for n in names if n.startswith("l_")]:
+        used = set()
+        for d in (fast, prec):
+            used |= G.regs_used(d[n], G.REG_S) - sstate
+        if any(24 <= r < 64 for r in used):
+            sys.stderr.write(f"gen_jit: loss routine {n} left out (SGPR temps {sorted(r for r in used if r >= 24)})\n")
+            names.remove(n)
     vtemp, stemp = set(), set()
     for d in (fast, prec):
         for n in names:
@@ -569,6 +597,9 @@ def build(hipcc, outdir, R):
             f.write(f"#define SR_JIT_BOP_ROUTINE_{suf.upper()} {{" + ", ".join(
                 str(-1 if b_name.upper()[2:] in INLINE_BOPS else rid(f"{b_name}_{suf}"))
                 for _, b_name in sorted(bop_rt.items())) + "}\n")
+        f.write("// routine of each elementwise loss, by SRHIP_LOSS_* (-1: L2, inline)\n")
+        f.write("#define SR_JIT_LOSS_ROUTINE {" + ", ".join(
+            str(-1 if n == "L2" else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write(f"#define SR_JIT_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT_ROUTINE_TRIG {" + ", ".join("1" if n in trig else "0" for n in names) + "}\n")

@@ -224,6 +224,8 @@ struct Gen {
   // constant set needs
   static constexpr int SC0 = 24, NSC = 16, SPROG = 56;
   bool memc = false;
+  int loss = SRHIP_LOSS_L2;       // the tile tail's elementwise loss (Options::loss)
+  uint32_t lparam = 0;
   std::vector<int> cpcs;          // program instruction of constant slot k
   int cslot(const Opnd& q) {
     for (size_t k = 0; k < cpcs.size(); ++k)
@@ -949,9 +951,55 @@ struct Gen {
     as.bind(L_nomask);
   }
 
+  // call a routine of the PRECISE region whatever the mode (the loss: the
+  // interpreter's elem_loss in Float64-evaluated form, bit for bit)
+  void call_precise(int rid) {
+    as.sop1(SOP1_GETPC, "s_getpc_b64", S_TGT, Src{0, false, 0}, "");
+    if (as.want_text) as.lines.back() = "s_getpc_b64 s[" + std::to_string(S_TGT) + ":" + std::to_string(S_TGT + 1) + "]";
+    const uint64_t pc_next = cur_va();
+    const int64_t rel = (int64_t)(T.rt_va[rid] + T.delta - pc_next);
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_TGT, S(S_TGT), K((uint32_t)(uint64_t)rel));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_TGT + 1, S(S_TGT + 1), K((uint32_t)((uint64_t)rel >> 32)));
+    as.sop1(SOP1_SWAPPC, "s_swappc_b64", S_RR, S(S_TGT), "s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "]");
+    if (as.want_text)
+      as.lines.back() = "s_swappc_b64 s[" + std::to_string(S_RR) + ":" + std::to_string(S_RR + 1) + "], s[" +
+                        std::to_string(S_TGT) + ":" + std::to_string(S_TGT + 1) + "]";
+  }
+
+  // the tile tail of a loss other than L2: ℓ(r) of the residual block VY by
+  // the loss routine, weighted, masked and summed as eval_kernel.h's
+  // tile_loss does ((ℓ0 + ℓ2) + (ℓ1 + ℓ3)), then the loop
+  void emit_tail_loss() {
+    mov_block_reg(VA, VY);
+    as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(lparam), "s" + std::to_string(S_K));
+    call_precise(kLossRoutine[loss]);
+    mov_block_reg(VY, VA);
+    const int L_unw = as.label(), L_sum = as.label();
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
+    as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VGT, S(S_WOFF), VLANE);
+    as.ds_read_b128(VGT, VGT, 0);
+    as.waitcnt_lgkm(0);
+    {
+      Src y[R], w[R];
+      for (int e = 0; e < R; ++e) { y[e] = V(VY + e); w[e] = V(VGT + e); }
+      if (packed) pk_block(VOP3P_MUL_F32, "v_pk_mul_f32", VY, w, y, false);
+      else for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VGT + e), VY + e);
+    }
+    as.bind(L_unw);
+    emit_mask(VY);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 2);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY + 1, V(VY + 1), VY + 3);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 1);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VLSUM, V(VLSUM), VY);
+    as.bind(L_sum);
+  }
+
   // second half of the tile: squares (weighted when s_woff != 0), mask, sums, loop
   void emit_tail() {
-    {
+    if (loss != SRHIP_LOSS_L2) {
+      emit_tail_loss();
+    } else {
       const int L_unw = as.label(), L_sum = as.label();
       as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
       as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
@@ -1028,15 +1076,18 @@ struct Gen {
 // One tree: returns false (nothing appended) when it cannot be compiled.
 static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool text, std::vector<uint32_t>& out,
                      std::vector<std::string>* lines, uint64_t area_va, int32_t* off, bool* is_fast,
-                     std::string* why, const DerivedMap& dm, bool memc) {
+                     std::string* why, const DerivedMap& dm, bool memc, int loss = SRHIP_LOSS_L2,
+                     uint32_t lparam = 0) {
   std::vector<IrOp> ir;
   Opnd root;
   if (!build_ir(prog, ir, root, &dm)) { *why = "program not translatable"; return false; }
   const size_t start = (out.size() + 15) / 16 * 16;  // 64-byte aligned entries
   Asm as;
   as.want_text = text;
-  Gen g(as, T, area_va + start * 4, fast_opt);
+  Gen g(as, T, area_va + start * 4, fast_opt && loss != SRHIP_LOSS_PERIODIC);
   g.memc = memc;
+  g.loss = loss;
+  g.lparam = lparam;
   if (!g.emit_tree(ir, root)) { *why = g.why; return false; }
   g.emit_tail();
   as.finish();
@@ -1095,7 +1146,8 @@ static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>
     const size_t before = words.size();
     const size_t lbefore = lines ? lines->size() : 0;
     const bool okc = cb.tree_off[t] >= 0 &&
-                     gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, opt.text, words, lines, T.area_va, &off, &f, &why, dm, opt.memc);
+                     gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, opt.text, words, lines, T.area_va, &off, &f, &why, dm, opt.memc,
+                              opt.loss, opt.lparam);
     if (okc && words.size() * 4 > T.area_bytes) {  // area full: the next part takes it
       words.resize(before);
       if (lines) lines->resize(lbefore);
@@ -1121,6 +1173,9 @@ static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>
 bool part_global() {
   static const bool g = [] { const char* e = std::getenv("SRHIP_JIT_PART_GLOBAL"); return e && e[0] == '1'; }();
   return g;
+}
+bool has_loss_routine(int loss) {
+  return loss == SRHIP_LOSS_L2 || (loss >= 0 && loss < SRHIP_NUM_LOSSES && kLossRoutine[loss] >= 0);
 }
 int choose_waves(int nraw) {
   static const int forced = [] {

@@ -21,6 +21,12 @@ struct Options {
   bool text = false;      // also produce the assembly text (tests: checked against llvm-mc)
   bool derive = true;     // derived columns (below); SRHIP_JIT_DERIVE=0 turns them off
   bool memc = false;      // constants read from the program's immediates (set_constants needs no new code)
+  // the elementwise loss of the tile tail (SRHIP_LOSS_*) and its parameter
+  // (Float32 bits, a literal of the code): L2 inline, the others through the
+  // loss routine of the PRECISE region (device_ops.h elem_loss, bit for bit
+  // the interpreter's); PERIODIC keeps every tree off the FAST path
+  int loss = SRHIP_LOSS_L2;
+  uint32_t lparam = 0;
 };
 
 // Derived columns: a routine unary operator applied to a dataset feature,
@@ -45,6 +51,10 @@ bool memc(const Module* m);
 // profiles/r03_ab_cfg5.txt), else 4; SRHIP_JIT_WAVES forces a width. And the
 // LDS a workgroup of that width may take while the CU holds 5 waves per SIMD.
 int choose_waves(int nraw);
+// tree code can end its tiles with this elementwise loss (L2 inline, the
+// others through a loss routine; gen_jit.py leaves out the ones whose
+// registers clash with memory-constant tree code)
+bool has_loss_routine(int loss);
 size_t lds_per_workgroup(int waves);
 bool part_global();
 

@@ -99,6 +99,7 @@ SIGNATURES = {
     "srhip_program_grad_jit_info": [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32), C.POINTER(C.c_int64),
                                     C.POINTER(C.c_double), C.POINTER(C.c_double)],
     "srhip_last_bailed": [C.c_void_p, C.POINTER(C.c_int32), C.POINTER(C.c_int64)],
+    "srhip_last_tree_code": [C.c_void_p, C.POINTER(C.c_int32)],
     "srhip_jit_compile": [C.POINTER(Trees), C.c_int32, C.c_void_p, C.POINTER(C.c_int64), C.c_char_p,
                           C.POINTER(C.c_int64), C.c_void_p, C.POINTER(C.c_int64)],
     "srhip_jit_compile_grad": [C.POINTER(Trees), C.c_void_p, C.POINTER(C.c_int64), C.c_char_p,

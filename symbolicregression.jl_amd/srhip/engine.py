@@ -67,6 +67,12 @@ class Context:
         """Trees of the last eval whose tree code handed a tile back."""
         return self.last_jit_events()[0]
 
+    def last_tree_code(self) -> int:
+        """Trees the last eval ran as tree code (srhip_last_tree_code)."""
+        n = C.c_int32(0)
+        check(lib().srhip_last_tree_code(self.handle, C.byref(n)))
+        return n.value
+
     def last_jit_events(self):
         """(trees handed back to the interpreter, tiles redone with the
         PRECISE routines) of the last eval."""
