@@ -242,7 +242,7 @@ struct srhip_program {
   std::vector<int32_t> h_jit_list;  // the trees of those slots, in slot order
   // the same trees' tree code for other elementwise losses (jit::Options::loss),
   // built at a loss's first evaluation; null m: that loss runs interpreted
-  struct LossJit { int kind; uint32_t bits; jit::Module* m; };
+  struct LossJit { int kind; uint64_t bits; jit::Module* m; };
   mutable std::vector<LossJit> jit_loss;
   jit::Stats jit_stats;
   // tree code is compiled for one constant set: a program whose constants are
@@ -941,7 +941,7 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, jit::Module* jm, const E
     a.tpb = plan.tpb;
     a.nrg = plan.nrg;
     a.loss = loss;
-    a.lparam = (T)lparam;
+    a.lparam = lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);
     const int tk = timed_begin(c, s);
@@ -1005,9 +1005,8 @@ jit::Module* loss_module(const srhip_program* p, int loss, double lparam) {
   if (loss == SRHIP_LOSS_L2) return p->jit;
   static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_LOSSES"); return !(e && e[0] == '0'); }();
   if (!on || loss < 0 || loss >= SRHIP_NUM_LOSSES || !jit::has_loss_routine(loss)) return nullptr;
-  const float pf = (float)lparam;
-  uint32_t bits;
-  std::memcpy(&bits, &pf, 4);
+  uint64_t bits;
+  std::memcpy(&bits, &lparam, 8);
   for (const auto& l : p->jit_loss)
     if (l.kind == loss && l.bits == bits) return l.m;
   srhip_trees tr;
@@ -1156,7 +1155,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.rotate = rotate_enabled() ? 1 : 0;
     a.contig = (pass == -1 && jit_contig()) ? 1 : 0;
     if (pass == -1 && rg_xcd()) a.rotate = 2;  // tree code: row groups per XCD
-    a.lparam = (T)lparam;
+    a.lparam = lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);
     a.out = out;
@@ -1535,7 +1534,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
     a.tpb = plan.tpb;
     a.nrg = plan.nrg;
     a.loss = loss;
-    a.lparam = (T)lparam;
+    a.lparam = lparam;
     a.G = G;
     a.opset = deep ? OPSET_FULL : p->g_opset;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * (2 + G) * sizeof(T));

@@ -409,27 +409,38 @@ __device__ __forceinline__ T uop(T x) {
 }
 
 // ---- elementwise losses, r = ŷ - y -------------------------------------------------
-// L2 and L1 are formed in T like LossFunctions (abs2 / abs of the T residual);
-// the parametric losses evaluate in T with the parameter rounded to T.
+// r = ŷ - y in T (LossFunctions' DistanceLoss: value(L, output - target)).
+// L2, L1, LogCosh and LogitDist have no parameter and stay in T (abs2 / abs of
+// the T residual). The parametric losses hold a Float64 field (LPDistLoss's P,
+// HuberLoss's d, the ε / τ / k of the others; src/Options.jl:429-435 builds them
+// from Float64 literals), so Julia promotes a Float32 residual to Float64 and
+// evaluates them in Float64: so do these, with the parameter as given (never
+// rounded to T), and the value rounded to T once.
 template <typename T>
-__device__ __forceinline__ T elem_loss(int kind, T p, T yhat, T y) {
+__device__ __forceinline__ double elem_loss_param(int kind, double p, double r) {
+  const double ar = __builtin_fabs(r);
+  switch (kind) {
+    case SRHIP_LOSS_LP: return m_pow(ar, p);
+    case SRHIP_LOSS_HUBER: return ar <= p ? 0.5 * r * r : p * (ar - 0.5 * p);
+    case SRHIP_LOSS_L1EPSINS: return ar > p ? ar - p : 0.0;
+    case SRHIP_LOSS_L2EPSINS: { double e = ar > p ? ar - p : 0.0; return e * e; }
+    case SRHIP_LOSS_QUANTILE: return r >= 0.0 ? p * r : (p - 1.0) * r;
+    case SRHIP_LOSS_PERIODIC: return 1.0 - m_cos(6.28318530717958647692 * r / p);
+  }
+  return qnan<double>();
+}
+template <typename T>
+__device__ __forceinline__ T elem_loss(int kind, double p, T yhat, T y) {
   const T r = yhat - y;
   const T ar = m_fabs(r);
   switch (kind) {
     case SRHIP_LOSS_L2: return r * r;
     case SRHIP_LOSS_L1: return ar;
-    case SRHIP_LOSS_LP: return m_pow(ar, p);
-    case SRHIP_LOSS_HUBER: return ar <= p ? T(0.5) * r * r : p * (ar - T(0.5) * p);
     case SRHIP_LOSS_LOGCOSH: return ar + m_log1p(m_exp(T(-2) * ar)) - T(0.69314718055994530942);
-    case SRHIP_LOSS_L1EPSINS: return ar > p ? ar - p : T(0);
-    case SRHIP_LOSS_L2EPSINS: { T e = ar > p ? ar - p : T(0); return e * e; }
-    case SRHIP_LOSS_QUANTILE: return r >= T(0) ? p * r : (p - T(1)) * r;
-    case SRHIP_LOSS_PERIODIC: return T(1) - m_cos(T(6.28318530717958647692) * r / p);
     case SRHIP_LOSS_LOGITDIST: return ar + T(2) * m_log1p(m_exp(-ar)) - T(1.38629436111989061883);
   }
-  return qnan<T>();
+  return (T)elem_loss_param<T>(kind, p, (double)r);
 }
-
 
 // ---- forward-mode partial derivatives (constant gradients) -----------------------
 // f = op(x, y) exactly as bop/uop compute it, plus ∂f/∂x, ∂f/∂y. The rules are
@@ -495,23 +506,26 @@ __device__ __forceinline__ void uop_d(T x, T& f, T& fx) {
   else fx = T(0);
 }
 
-// dℓ/dŷ of the elementwise losses (r = ŷ - y)
+// dℓ/dŷ of the elementwise losses (r = ŷ - y); the parametric ones in
+// Float64 like their values (elem_loss)
 template <typename T>
-__device__ __forceinline__ T elem_dloss(int kind, T p, T yhat, T y) {
+__device__ __forceinline__ T elem_dloss(int kind, double p, T yhat, T y) {
   const T r = yhat - y;
-  const T ar = m_fabs(r);
   const T sg = r > T(0) ? T(1) : (r < T(0) ? T(-1) : T(0));
   switch (kind) {
     case SRHIP_LOSS_L2: return T(2) * r;
     case SRHIP_LOSS_L1: return sg;
-    case SRHIP_LOSS_LP: return p * m_pow(ar, p - T(1)) * sg;
-    case SRHIP_LOSS_HUBER: return ar <= p ? r : p * sg;
     case SRHIP_LOSS_LOGCOSH: return m_tanh(r);
-    case SRHIP_LOSS_L1EPSINS: return ar > p ? sg : T(0);
-    case SRHIP_LOSS_L2EPSINS: return ar > p ? T(2) * (ar - p) * sg : T(0);
-    case SRHIP_LOSS_QUANTILE: return r >= T(0) ? p : p - T(1);
-    case SRHIP_LOSS_PERIODIC: { T k = T(6.28318530717958647692) / p; return k * m_sin(k * r); }
     case SRHIP_LOSS_LOGITDIST: return m_tanh(T(0.5) * r);
+  }
+  const double rd = (double)r, ar = __builtin_fabs(rd), sd = (double)sg;
+  switch (kind) {
+    case SRHIP_LOSS_LP: return (T)(p * m_pow(ar, p - 1.0) * sd);
+    case SRHIP_LOSS_HUBER: return (T)(ar <= p ? rd : p * sd);
+    case SRHIP_LOSS_L1EPSINS: return (T)(ar > p ? sd : 0.0);
+    case SRHIP_LOSS_L2EPSINS: return (T)(ar > p ? 2.0 * (ar - p) * sd : 0.0);
+    case SRHIP_LOSS_QUANTILE: return (T)(rd >= 0.0 ? p : p - 1.0);
+    case SRHIP_LOSS_PERIODIC: { const double k = 6.28318530717958647692 / p; return (T)(k * m_sin(k * rd)); }
   }
   return qnan<T>();
 }

@@ -51,7 +51,7 @@ using namespace interp;
 // Σ over this lane's rows of the tile of w·ℓ(ŷ, y); masked rows (past n) add 0.
 template <int LK, bool W, bool MASK, typename T, int R>
 __device__ __forceinline__ T tile_loss(const T (&acc)[R], const T (&yv)[R], const T (&wv)[R],
-                                       T lp, int lane, int valid) {
+                                       double lp, int lane, int valid) {
   T s0 = T(0), s1 = T(0);
 #pragma unroll
   for (int e = 0; e < R; ++e) {
@@ -100,7 +100,7 @@ __device__ __forceinline__ bool run_program_ti(const uint4* recs, uint32_t lane_
 
 template <bool W, bool MASK, typename T, int R>
 __device__ __forceinline__ T tile_loss_any(int lk, const T (&acc)[R], const T (&yv)[R],
-                                           const T (&wv)[R], T lp, int lane, int valid) {
+                                           const T (&wv)[R], double lp, int lane, int valid) {
   switch (lk) {
     case SRHIP_LOSS_L2: return tile_loss<SRHIP_LOSS_L2, W, MASK>(acc, yv, wv, lp, lane, valid);
     case SRHIP_LOSS_L1: return tile_loss<SRHIP_LOSS_L1, W, MASK>(acc, yv, wv, lp, lane, valid);
@@ -157,7 +157,7 @@ eval_kernel(EvalArgs<T> a) {
   const int64_t rem = a.n - row0;
   const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE - 1) / TILE);
   const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
-  const T lp = a.lparam;
+  const double lp = a.lparam;
 
   // 2. trees of this group, taken dynamically by the waves
   // Waves take the group's (cost-sorted) trees round-robin: a static,

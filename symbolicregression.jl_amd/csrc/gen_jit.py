@@ -56,7 +56,8 @@ class JitRegs:
         # SGPR state of tree code (pinned in the routine snippets so that no
         # routine uses them as temporaries)
         self.S = dict(tile=64, nt=65, partial=66, tilebytes=67, woff=68, status=69, flag=70, rr=72, tgt=74,
-                      rt=76, mdelta=78, fastok=79, eps=80, k=81, pe=82, mode=83, x0=84, x1=85, x2=86, x3=87)
+                      rt=76, mdelta=78, fastok=79, eps=80, k=81, pe=82, mode=83, x0=84, x1=85, x2=86, x3=87,
+                      kh=90)  # kh: high word of a loss routine's Float64 parameter (low word in k)
         self.SPAIRS = {"flag", "rr", "tgt", "rt"}
 
     def vstate(self):
@@ -196,7 +197,8 @@ def routine_list():
     for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
         if name == "L2":
             continue
-        imm = "const float imm = __int_as_float((int)s.s_k); "
+        imm = ("const double imm = __builtin_bit_cast(double, ((unsigned long long)s.s_kh << 32) | "
+               "(unsigned long long)s.s_k); ")
         rs.append((f"l_{name.lower()}",
                    imm + rows(f"s.a[r] = dev::elem_loss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"), False))
     return rs
@@ -504,12 +506,15 @@ def build(hipcc, outdir, R):
     # constants live in s24..s39 (jit.cpp Gen::SC0): one whose SGPR temporaries
     # reach them (logcosh, logitdist: Float64 constants) is left out, and that
     # loss runs interpreted (SR_JIT_LOSS_ROUTINE -1)
+    # (and one whose VGPR temporaries run into the state block: LP's Float64 pow)
     for n in [n for n in names if n.startswith("l_")]:
-        used = set()
+        used, vused = set(), set()
         for d in (fast, prec):
             used |= G.regs_used(d[n], G.REG_S) - sstate
-        if any(24 <= r < 64 for r in used):
-            sys.stderr.write(f"gen_jit: loss routine {n} left out (SGPR temps {sorted(r for r in used if r >= 24)})\n")
+            vused |= G.regs_used(d[n], G.REG_V) - vstate
+        if any(24 <= r < 64 for r in used) or any(r >= rg.A for r in vused):
+            sys.stderr.write(f"gen_jit: loss routine {n} left out (SGPR temps {sorted(r for r in used if r >= 24)}, "
+                             f"VGPR temps up to v{max(vused, default=0)})\n")
             names.remove(n)
     vtemp, stemp = set(), set()
     for d in (fast, prec):

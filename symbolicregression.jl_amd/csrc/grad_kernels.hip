@@ -52,7 +52,7 @@ __global__ void __launch_bounds__(256) grad_kernel(GradArgs<T> a) {
   const int64_t rem = a.n - row0;
   const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE - 1) / TILE);
   const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
-  const T lp = a.lparam;
+  const double lp = a.lparam;
 
   // Waves take the group's (cost-sorted) trees round-robin: a static,
   // wave-uniform schedule (no atomics, no divergent loop exit).

@@ -225,7 +225,7 @@ struct Gen {
   static constexpr int SC0 = 24, NSC = 16, SPROG = 56;
   bool memc = false;
   int loss = SRHIP_LOSS_L2;       // the tile tail's elementwise loss (Options::loss)
-  uint32_t lparam = 0;
+  uint64_t lparam = 0;            // its Float64 parameter's bits
   std::vector<int> cpcs;          // program instruction of constant slot k
   int cslot(const Opnd& q) {
     for (size_t k = 0; k < cpcs.size(); ++k)
@@ -971,7 +971,8 @@ struct Gen {
   // tile_loss does ((ℓ0 + ℓ2) + (ℓ1 + ℓ3)), then the loop
   void emit_tail_loss() {
     mov_block_reg(VA, VY);
-    as.sop1(SOP1_MOV, "s_mov_b32", S_K, K(lparam), "s" + std::to_string(S_K));
+    as.sop1(SOP1_MOV, "s_mov_b32", S_K, K((uint32_t)lparam), "s" + std::to_string(S_K));
+    as.sop1(SOP1_MOV, "s_mov_b32", S_KH, K((uint32_t)(lparam >> 32)), "s" + std::to_string(S_KH));
     call_precise(kLossRoutine[loss]);
     mov_block_reg(VY, VA);
     const int L_unw = as.label(), L_sum = as.label();
@@ -1077,7 +1078,7 @@ struct Gen {
 static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool text, std::vector<uint32_t>& out,
                      std::vector<std::string>* lines, uint64_t area_va, int32_t* off, bool* is_fast,
                      std::string* why, const DerivedMap& dm, bool memc, int loss = SRHIP_LOSS_L2,
-                     uint32_t lparam = 0) {
+                     uint64_t lparam = 0) {
   std::vector<IrOp> ir;
   Opnd root;
   if (!build_ir(prog, ir, root, &dm)) { *why = "program not translatable"; return false; }

@@ -22,11 +22,11 @@ struct Options {
   bool derive = true;     // derived columns (below); SRHIP_JIT_DERIVE=0 turns them off
   bool memc = false;      // constants read from the program's immediates (set_constants needs no new code)
   // the elementwise loss of the tile tail (SRHIP_LOSS_*) and its parameter
-  // (Float32 bits, a literal of the code): L2 inline, the others through the
+  // (Float64 bits, literals of the code): L2 inline, the others through the
   // loss routine of the PRECISE region (device_ops.h elem_loss, bit for bit
   // the interpreter's); PERIODIC keeps every tree off the FAST path
   int loss = SRHIP_LOSS_L2;
-  uint32_t lparam = 0;
+  uint64_t lparam = 0;     // Float64 bits (LossFunctions' field, never rounded to Float32)
 };
 
 // Derived columns: a routine unary operator applied to a dataset feature,

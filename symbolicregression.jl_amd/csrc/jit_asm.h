@@ -35,6 +35,7 @@ constexpr int S_TILE = SR_JIT_S_TILE, S_NT = SR_JIT_S_NT, S_PARTIAL = SR_JIT_S_P
 constexpr int S_TILEBYTES = SR_JIT_S_TILEBYTES, S_WOFF = SR_JIT_S_WOFF, S_STATUS = SR_JIT_S_STATUS;
 constexpr int S_FLAG = SR_JIT_S_FLAG, S_RR = SR_JIT_S_RR, S_TGT = SR_JIT_S_TGT, S_RT = SR_JIT_S_RT;
 constexpr int S_FASTOK = SR_JIT_S_FASTOK, S_EPS = SR_JIT_S_EPS;
+constexpr int S_KH = SR_JIT_S_KH;  // high word of a loss routine's Float64 parameter
 constexpr int S_K = SR_JIT_S_K, S_PE = SR_JIT_S_PE, S_MODE = SR_JIT_S_MODE, S_X0 = SR_JIT_S_X0;
 constexpr int S_BASE = SR_JIT_S_X2;
 constexpr int S_RECIP = SR_JIT_S_X1;  // RN(1/c) of a constant divisor (routine b_div_rk)  // s[86:87]: base of the routine region in use (FAST or PRECISE)

@@ -41,7 +41,7 @@ struct EvalArgs {
   int rotate;              // MODE_LOSS: start each wave's tree sequence at row-group-dependent offsets
   int contig;              // tree group g holds list slots [g*tpb, (g+1)*tpb) (tree code: a group's
                            // code is one contiguous range); 0: slots dealt in snake order
-  T lparam;
+  double lparam;           // the loss parameter (LossFunctions' Float64 field, not rounded to T)
   Part<T>* partial;        // [nrg][ntg*tpb]
   T* out;                  // MODE_OUT: [ntrees][out_stride]
   int64_t out_stride;
@@ -98,7 +98,7 @@ struct GradArgs {
   int nfeat;
   int ntiles, ntg, tpb, nrg;
   int loss;
-  T lparam;
+  double lparam;
   int G;                    // tangents carried by this launch (1, 2 or kGradG)
   int opset;                // OPSET_BASIC: the programs use only the basic operators
   T* partial;               // [nrg][ntg*tpb][2 + G]

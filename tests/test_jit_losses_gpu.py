@@ -4,12 +4,18 @@ LossFunctions.jl's distance losses (src/LossFunctions.jl:11-31, the
 Options.elementwise_loss of src/Options.jl:429-435) at the end of every tile
 of Float32 tree code, weighted and unweighted.
 
-Per loss: the tree code ran (srhip_last_tree_code), did_succeed equals the
-interpreter's and the oracle's on every tree, and losses agree with the
-oracle within the north_star's 1e-5 on every succeeding tree (Periodic runs
-without the FAST path: its cos(2πr/c) amplifies a residual's rounding by
-2π|r|/c). LogCosh and LogitDist keep the interpreter (their loss routines'
-registers clash with memory-constant tree code), which this checks too."""
+The parametric losses hold Float64 fields, so Julia evaluates them in
+Float64 for a Float32 residual (device_ops.h elem_loss, the oracle likewise):
+PeriodicLoss's cos(2πr/c) of a large residual made the Float32 evaluation
+0.6 % off before (round 4). L1, Huber, the epsilon-insensitive losses and
+Quantile run as tree code; LP (Float64 pow), Periodic (Float64 cos), LogCosh
+and LogitDist keep the interpreter (their loss routines' registers exceed
+what tree code leaves them), which this checks too.
+
+Per loss: the tree code ran or not (srhip_last_tree_code), did_succeed equals
+the interpreter's and the oracle's on every tree, and losses agree with the
+interpreter and with the oracle within the north_star's 1e-5 on every
+succeeding tree."""
 import os
 
 import numpy as np
@@ -17,13 +23,14 @@ import pytest
 
 import oracle
 import srhip
+from srhip import constants as K
 
 pytestmark = pytest.mark.gpu
 
 LOSSES = [
-    (srhip.L1DistLoss(), True), (srhip.LPDistLoss(1.7), True), (srhip.LPDistLoss(3.0), True),
+    (srhip.L1DistLoss(), True), (srhip.LPDistLoss(1.7), False), (srhip.LPDistLoss(3.0), False),
     (srhip.HuberLoss(0.8), True), (srhip.L1EpsilonInsLoss(0.3), True), (srhip.L2EpsilonInsLoss(0.3), True),
-    (srhip.QuantileLoss(0.3), True), (srhip.PeriodicLoss(2.0), True),
+    (srhip.QuantileLoss(0.3), True), (srhip.PeriodicLoss(2.0), False),
     (srhip.LogCoshLoss(), False), (srhip.LogitDistLoss(), False),
 ]
 
@@ -39,30 +46,37 @@ def _problem():
     return o, X, y, w, trees
 
 
-@pytest.mark.parametrize("loss,jit", LOSSES, ids=lambda v: type(v).__name__ if not isinstance(v, bool) else str(v))
+@pytest.mark.parametrize("loss,jit", LOSSES, ids=[f"{l.kind}-{l.params}" for l, _ in LOSSES])
 def test_tree_code_losses_match_oracle(gpu_ctx, loss, jit):
     o, X, y, w, trees = _problem()
     ctx = gpu_ctx
     flat = srhip.flatten(trees, o, dtype=np.float32)
-    os.environ["SRHIP_JIT"] = "1"
-    try:
-        prog = srhip.Program(ctx, flat, np.float32)
-    finally:
-        del os.environ["SRHIP_JIT"]
-    assert prog.jit_info()["ntrees"] > 900
+    progs = {}
+    for mode in ("1", "0"):
+        os.environ["SRHIP_JIT"] = mode
+        try:
+            progs[mode] = srhip.Program(ctx, flat, np.float32)
+        finally:
+            del os.environ["SRHIP_JIT"]
+    assert progs["1"].jit_info()["ntrees"] > 900 and progs["0"].jit_info()["ntrees"] == 0
     par = None if loss.params is None else loss.params
     for weights in (None, w):
         ds = srhip.DeviceDataset(ctx, X, y, weights)
-        s, wsum, ok = prog.eval_loss(ds, loss.kind, par)
+        s, wsum, ok = progs["1"].eval_loss(ds, loss.kind, par)
         ran = ctx.last_tree_code()
-        assert (ran > 900) if jit else (ran == 0), (type(loss).__name__, ran)
+        assert (ran > 900) if jit else (ran == 0), (loss.kind, ran)
+        si, wi, oki = progs["0"].eval_loss(ds, loss.kind, par)
+        assert ctx.last_tree_code() == 0 and wi == wsum
         _, rl, rok = oracle.eval_loss_batch(flat, X, y, weights, loss.kind, par if par is not None else (0.0,),
                                             dtype=np.float32, nthreads=16)
-        assert np.array_equal(ok, rok), type(loss).__name__
+        assert np.array_equal(ok, rok) and np.array_equal(oki, rok), loss.kind
         m = ok & np.isfinite(rl)
-        got = s / wsum
+        got, interp = s / wsum, si / wsum
         with np.errstate(invalid="ignore", divide="ignore"):
             rel = np.abs(got - rl) / np.abs(rl)
+            rel_i = np.abs(got - interp) / np.abs(interp)
+        name = (loss.kind, loss.params, weights is not None)
+        assert np.all(rel_i[m] <= 1e-5), (name, float(np.nanmax(rel_i[m])))
         bad = np.flatnonzero(m & ~(rel <= 1e-5))
-        assert bad.size == 0, (type(loss).__name__, weights is not None, bad[:10], float(np.nanmax(rel[m])))
+        assert bad.size == 0, (name, bad[:10], float(np.nanmax(rel[m])))
         assert m.sum() > 300
