@@ -45,6 +45,47 @@ def shard_trees(ntrees: int, rank: int, world: int) -> np.ndarray:
     return np.arange(rank, ntrees, world, dtype=np.int64)
 
 
+# Estimated device cost of an operator per row (SIMD cycles of its tree code,
+# tools/census.py on config #2: a packed + - * about 1, exp 5, sin / cos 7,
+# IEEE division 8; leaves are register reads). Other operators count as a
+# transcendental.
+OP_COST = {"+": 1.0, "-": 1.0, "*": 1.0, "/": 8.0, "cos": 7.0, "sin": 7.0, "exp": 5.0, "neg": 0.5,
+           "abs": 0.5, "square": 1.0, "cube": 2.0}
+
+
+def tree_cost(tree, options) -> float:
+    """The tree's estimated evaluation cost per row (OP_COST over its nodes)."""
+    stack, c = [tree], 0.0
+    while stack:
+        t = stack.pop()
+        if t.degree == 1:
+            c += OP_COST.get(options.unary_operators[t.op - 1], 7.0)
+            stack.append(t.l)
+        elif t.degree == 2:
+            c += OP_COST.get(options.binary_operators[t.op - 1], 7.0)
+            stack += [t.l, t.r]
+        else:
+            c += 0.1
+    return c
+
+
+def shard_trees_balanced(trees, options, rank: int, world: int) -> np.ndarray:
+    """Indices of the trees rank evaluates, partitioned by estimated cost:
+    most expensive first, each to the rank with the least cost so far (LPT;
+    ties to the lower rank), so the slowest rank — which sets the step time of
+    a strong-scaling run — carries about 1/world of the work. Deterministic:
+    every rank computes the same partition."""
+    costs = np.array([tree_cost(t, options) for t in trees])
+    order = np.argsort(-costs, kind="stable")
+    load = np.zeros(world)
+    owner = np.empty(len(trees), dtype=np.int64)
+    for i in order:
+        r = int(np.argmin(load))
+        owner[i] = r
+        load[r] += costs[i]
+    return np.flatnonzero(owner == rank)
+
+
 def merge_tree_shards(parts, ntrees: int) -> np.ndarray:
     """Per-rank result arrays (in shard_trees order, rank 0 first) back into
     tree order."""
