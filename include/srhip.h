@@ -338,9 +338,10 @@ int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntre
  * tiles that tree code redid with the Float64-evaluated routines (a FAST-path
  * guard fired or the tile failed; out_redone may be NULL). */
 int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* out_redone);
-/* Trees the last eval on this context ran as tree code (0: all interpreted;
- * Float32 loss evaluations: L2 and, compiled at their first use, L1 / LP /
- * Huber / the epsilon-insensitive losses / Quantile / Periodic). */
+/* Trees the last eval or gradient on this context ran as tree code (0: all
+ * interpreted; Float32 loss evaluations and srhip_eval_loss_grad: L2 and,
+ * compiled at their first use, L1 / Huber / the epsilon-insensitive losses /
+ * Quantile). */
 int32_t srhip_last_tree_code(const srhip_ctx* ctx, int32_t* out_ntrees);
 /* Testing hook (no device needed): compile Float32 trees with the tree
  * compiler (fast: bit 0 the guarded FAST path, bit 1 memory-constant code).
@@ -355,6 +356,13 @@ int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_b
 int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int64_t* inout_nbytes,
                                char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
                                int64_t* inout_noffsets);
+/* Testing hook, same contract: the loss tree code (grad = 0; fast: its
+ * guarded FAST path) or the gradient tree code (grad = 1) of Float32 trees
+ * for the elementwise loss `loss` (SRHIP_LOSS_*) with its parameter.
+ * SRHIP_ERR_UNSUPPORTED when tree code has no routine for that loss. */
+int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t fast, int32_t loss, double loss_param,
+                               uint8_t* out_bytes, int64_t* inout_nbytes, char* out_text, int64_t* inout_ntext,
+                               int32_t* out_offsets, int64_t* inout_noffsets);
 /* Testing hook (no device needed): the host side of
  * srhip_program_set_constants. Compiles the trees (dtype F32/F64), writes
  * new_consts through the programs' constant map (loss programs, grad = 0, or

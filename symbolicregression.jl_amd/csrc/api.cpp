@@ -279,6 +279,13 @@ struct srhip_program {
   // stored after the ngitems[] items in d_gitems)
   jit::GradModule* gjit = nullptr;
   jit::GradStats gjit_stats;
+  // its candidate trees (cost order) and compiled slot list: the gradient tree
+  // code of another elementwise loss is built from the same candidates at that
+  // loss's first gradient and used only with the same slots (null m: that
+  // loss's gradients run interpreted)
+  std::vector<int32_t> h_gcand, h_gjl;
+  struct GradLossJit { int kind; uint64_t bits; jit::GradModule* m; };
+  std::vector<GradLossJit> gjit_loss;
   int ngitems_rest[4] = {0, 0, 0, 0};
   int32_t* d_gjit_list = nullptr;   // [nslots] tree of each gradient-code slot
   int32_t* d_gjit_cidx = nullptr;   // constants of those trees
@@ -358,6 +365,8 @@ void free_grad_device(srhip_program* p) {
   p->gjl_cap = p->gjc_cap = p->gcs_cap = 0;
   jit::destroy_grad(p->gjit);
   p->gjit = nullptr;
+  for (auto& l : p->gjit_loss) jit::destroy_grad(l.m);
+  p->gjit_loss.clear();
   p->grad_built = false;
 }
 
@@ -566,6 +575,10 @@ void build_grad_program(srhip_program* p) {
   // gradient tree code for the Float32 trees it can compile (cost-sorted slots)
   jit::destroy_grad(p->gjit);
   p->gjit = nullptr;
+  for (auto& l : p->gjit_loss) jit::destroy_grad(l.m);
+  p->gjit_loss.clear();
+  p->h_gcand.clear();
+  p->h_gjl.clear();
   p->gjit_stats = jit::GradStats();
   std::vector<uint8_t> in_jit(p->ntrees, 0);
   std::vector<int32_t> gjl, gcidx;
@@ -579,6 +592,10 @@ void build_grad_program(srhip_program* p) {
       });
       std::vector<int32_t> rest;
       p->gjit = jit::build_grad(cb, p->const_off, cand, gjl, rest, &p->gjit_stats);
+      if (p->gjit) {
+        p->h_gcand = cand;
+        p->h_gjl = gjl;
+      }
       if (p->gjit)
         for (int32_t t : gjl) {
           in_jit[t] = 1;
@@ -1033,6 +1050,39 @@ jit::Module* loss_module(const srhip_program* p, int loss, double lparam) {
   return m;
 }
 
+// The gradient tree code of a Float32 program for an elementwise loss: the
+// L2 build, or the same candidates compiled with that loss's seed (jit_grad.cpp
+// emit_loss_seed), built at the loss's first gradient and kept with the
+// program; null: that loss's gradients run interpreted (SRHIP_JIT_LOSSES=0,
+// no dℓ/dr routine, or a different slot layout).
+jit::GradModule* grad_module(srhip_program* p, int loss, double lparam) {
+  if (!p->gjit) return nullptr;
+  if (loss == SRHIP_LOSS_L2) return p->gjit;
+  static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_LOSSES"); return !(e && e[0] == '0'); }();
+  if (!on || loss < 0 || loss >= SRHIP_NUM_LOSSES || !jit::has_dloss_routine(loss)) return nullptr;
+  uint64_t bits;
+  std::memcpy(&bits, &lparam, 8);
+  for (const auto& l : p->gjit_loss)
+    if (l.kind == loss && l.bits == bits) return l.m;
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->consts.data();
+  CompiledBatch<float> cb = compile_batch_par<float>(tr, /*grad=*/true);
+  std::vector<int32_t> gjl, rest;
+  jit::GradStats st;
+  jit::GradModule* m = jit::build_grad(cb, p->const_off, p->h_gcand, gjl, rest, &st, loss, bits);
+  if (m && gjl != p->h_gjl) {
+    jit::destroy_grad(m);
+    m = nullptr;
+  }
+  p->gjit_loss.push_back({loss, bits, m});
+  return m;
+}
+
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
 // n_pad) may be the dataset itself or a gathered row subset.
 template <typename T>
@@ -1437,32 +1487,33 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
   c->sums.ensure(std::max<size_t>(nt, 1) * sizeof(double));
   c->oks.ensure(std::max<size_t>(nt, 1));
   c->dloss.ensure(std::max<size_t>(nconst, 1) * sizeof(double));
-  // gradient tree code (L2 loss, ∂L/∂c) for the trees it holds; the
+  // gradient tree code (∂L/∂c of the loss) for the trees it holds; the
   // interpreter items of the other trees follow
   bool use_gjit = false;
   if constexpr (std::is_same<T, float>::value) {
-    if (p->gjit && mode == GRAD_LOSS && loss == SRHIP_LOSS_L2 && ds->rows > 0) {
-      const int nparts = jit::grad_nparts(p->gjit);
+    jit::GradModule* gm = (p->gjit && mode == GRAD_LOSS && ds->rows > 0) ? grad_module(p, loss, lparam) : nullptr;
+    if (gm) {
+      const int nparts = jit::grad_nparts(gm);
       const int narr = 1 + ds->nfeat + (ds->w ? 1 : 0);
       std::vector<EvalPlan> plans(nparts);
       use_gjit = true;
       for (int k = 0; k < nparts && use_gjit; ++k) {
         int s0, nsl;
-        jit::grad_part(p->gjit, k, &s0, &nsl);
+        jit::grad_part(gm, k, &s0, &nsl);
         // partials go straight to global memory: LDS holds the row tiles only (1 byte per slot below
         // keeps plan_geometry's slot bound out of the way)
         use_gjit = plan_geometry(4, 4, kShallowSlots, narr, 1, ds->rows, nsl, &plans[k], gjit_tile_budget()) &&
                    plans[k].nrg == plans[0].nrg;
       }
       if (use_gjit) {
-        const int nsl_all = jit::grad_nslots(p->gjit);
+        const int nsl_all = jit::grad_nslots(gm);
         c->fail.ensure((size_t)nsl_all * sizeof(uint32_t));
         c->fail_clean = false;  // the gradient kernels leave their flags set
         HIP_CHECK(hipMemsetAsync(c->fail.p, 0, (size_t)nsl_all * sizeof(uint32_t), s));
         c->gpart.ensure(std::max<size_t>((size_t)plans[0].nrg * nconst, 1) * sizeof(float));
         for (int k = 0; k < nparts; ++k) {
           int s0, nsl;
-          jit::grad_part(p->gjit, k, &s0, &nsl);
+          jit::grad_part(gm, k, &s0, &nsl);
           const EvalPlan& plan = plans[k];
           EvalArgs<float> a;
           std::memset(&a, 0, sizeof(a));
@@ -1485,7 +1536,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
           c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<float>));
           a.partial = static_cast<Part<float>*>(c->partial.p);
           const int tk = timed_begin(c, s);
-          HIP_CHECK(jit::launch_grad_code(p->gjit, k, plan, a, p->d_gconsts, static_cast<float*>(c->gpart.p), nconst,
+          HIP_CHECK(jit::launch_grad_code(gm, k, plan, a, p->d_gconsts, static_cast<float*>(c->gpart.p), nconst,
                                           s));
           timed_end(c, s, tk);
           HIP_CHECK(launch_finalize<float>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
@@ -1503,6 +1554,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
       }
     }
   }
+  c->last_jit_trees = use_gjit ? (int)p->h_gjl.size() : 0;
   const int* ngi = use_gjit ? p->ngitems_rest : p->ngitems;
   int first = 0;
   if (use_gjit)
@@ -2159,19 +2211,26 @@ int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* ou
 
 namespace {
 int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes, int64_t* inout_nbytes,
-                         char* out_text, int64_t* inout_ntext, int32_t* out_offsets, int64_t* inout_noffsets) {
+                         char* out_text, int64_t* inout_ntext, int32_t* out_offsets, int64_t* inout_noffsets,
+                         int loss = SRHIP_LOSS_L2, double lparam = 0.0) {
   return guarded([&] {
     if (!trees || !inout_nbytes || !inout_ntext || !inout_noffsets) throw Error(SRHIP_ERR_INVALID, "null argument");
     if (!jit::available()) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("tree compiler: ") + jit::unavailable_reason());
     std::vector<uint8_t> bytes;
     std::string text;
     std::vector<int32_t> offs;
+    if (loss < 0 || loss >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_INVALID, "unknown loss");
+    uint64_t lbits;
+    std::memcpy(&lbits, &lparam, 8);
+    if (mode == 2 && !jit::has_dloss_routine(loss))
+      throw Error(SRHIP_ERR_UNSUPPORTED, "no gradient tree code for this loss");
+    if (mode != 2 && !jit::has_loss_routine(loss)) throw Error(SRHIP_ERR_UNSUPPORTED, "no tree code for this loss");
     if (mode == 2) {  // gradient tree code
       CompiledBatch<float> cb = compile_batch<float>(*trees, /*grad=*/true);
       std::vector<int32_t> cand, coff(trees->const_off, trees->const_off + trees->ntrees + 1);
       for (int t = 0; t < cb.ntrees; ++t)
         if (cb.tree_off[t] >= 0) cand.push_back(t);
-      jit::compile_grad_only(cb, coff, cand, &bytes, &text, &offs, nullptr);
+      jit::compile_grad_only(cb, coff, cand, &bytes, &text, &offs, nullptr, loss, lbits);
     } else {
       CompiledBatch<float> cb = compile_batch<float>(*trees);
       std::vector<int32_t> cand;
@@ -2181,6 +2240,8 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
       jo.fast = mode == 1 || mode == 4;
       jo.memc = mode == 3 || mode == 4;
       jo.text = true;
+      jo.loss = loss;
+      jo.lparam = lbits;
       jit::compile_only(cb, cand, jo, &bytes, &text, &offs, nullptr);
     }
     if ((int64_t)bytes.size() > *inout_nbytes || (int64_t)text.size() + 1 > *inout_ntext ||
@@ -2214,6 +2275,13 @@ int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int
                                char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
                                int64_t* inout_noffsets) {
   return jit_compile_hook(trees, 2, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets, inout_noffsets);
+}
+
+int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t fast, int32_t loss, double loss_param,
+                               uint8_t* out_bytes, int64_t* inout_nbytes, char* out_text, int64_t* inout_ntext,
+                               int32_t* out_offsets, int64_t* inout_noffsets) {
+  return jit_compile_hook(trees, grad ? 2 : (fast ? 1 : 0), out_bytes, inout_nbytes, out_text, inout_ntext,
+                          out_offsets, inout_noffsets, loss, loss_param);
 }
 
 namespace {

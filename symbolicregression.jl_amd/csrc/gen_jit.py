@@ -201,6 +201,14 @@ def routine_list():
                "(unsigned long long)s.s_k); ")
         rs.append((f"l_{name.lower()}",
                    imm + rows(f"s.a[r] = dev::elem_loss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"), False))
+    # dℓ/dr of the same losses (the gradient tree code's seed, jit_grad.cpp)
+    for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
+        if name == "L2":
+            continue
+        imm = ("const double imm = __builtin_bit_cast(double, ((unsigned long long)s.s_kh << 32) | "
+               "(unsigned long long)s.s_k); ")
+        rs.append((f"d_{name.lower()}",
+                   imm + rows(f"s.a[r] = dev::elem_dloss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"), False))
     return rs
 
 
@@ -507,7 +515,7 @@ def build(hipcc, outdir, R):
     # reach them (logcosh, logitdist: Float64 constants) is left out, and that
     # loss runs interpreted (SR_JIT_LOSS_ROUTINE -1)
     # (and one whose VGPR temporaries run into the state block: LP's Float64 pow)
-    for n in [n for n in names if n.startswith("l_")]:
+    for n in [n for n in names if n.startswith(("l_", "d_"))]:
         used, vused = set(), set()
         for d in (fast, prec):
             used |= G.regs_used(d[n], G.REG_S) - sstate
@@ -605,6 +613,9 @@ def build(hipcc, outdir, R):
         f.write("// routine of each elementwise loss, by SRHIP_LOSS_* (-1: L2, inline)\n")
         f.write("#define SR_JIT_LOSS_ROUTINE {" + ", ".join(
             str(-1 if n == "L2" else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
+        f.write("// dℓ/dr routine of each elementwise loss (-1: L2, inline, or left out)\n")
+        f.write("#define SR_JIT_DLOSS_ROUTINE {" + ", ".join(
+            str(-1 if n == "L2" else rid(f"d_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write(f"#define SR_JIT_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT_ROUTINE_TRIG {" + ", ".join("1" if n in trig else "0" for n in names) + "}\n")

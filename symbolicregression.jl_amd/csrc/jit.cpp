@@ -1404,6 +1404,7 @@ struct JitArgs {
   uint32_t der[kMaxDerived];
   const float* dcols;
   int nbig, ts;
+  int dyn;
 };
 struct DeriveArgs {
   const float* X;
@@ -1434,6 +1435,13 @@ hipError_t reset_flags(Module* m, hipStream_t stream) {
   return hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t), stream);
 }
 
+// waves take their trees from an LDS counter (jit_template.hip next_tree);
+// SRHIP_JIT_DYNAMIC=0: the static deal
+bool dynamic_trees() {
+  static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_DYNAMIC"); return !(e && e[0] == '0'); }();
+  return on;
+}
+
 hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, const float* dcols,
                   hipStream_t stream) {
   const ModulePart& q = m->parts[k];
@@ -1450,6 +1458,7 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   ja.dcols = dcols;
   ja.nbig = plan.nbig >= 0 ? plan.nbig : a.nrg;
   ja.ts = plan.nbig >= 0 ? plan.ts : plan.ntiles;
+  ja.dyn = dynamic_trees() ? 1 : 0;
   if (ja.nraw > a.nfeat) return hipErrorInvalidValue;
   if (ja.nbig > a.nrg || ja.ts < 1 || ja.ts > plan.ntiles) return hipErrorInvalidValue;
   // partials in LDS when they take little room next to the tiles (measured

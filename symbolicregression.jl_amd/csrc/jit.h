@@ -55,8 +55,12 @@ int choose_waves(int nraw);
 // others through a loss routine; gen_jit.py leaves out the ones whose
 // registers clash with memory-constant tree code)
 bool has_loss_routine(int loss);
+// the gradient tree code can seed its reverse pass with this loss (L2 inline,
+// the others through their loss and dℓ/dr routines)
+bool has_dloss_routine(int loss);
 size_t lds_per_workgroup(int waves);
 bool part_global();
+bool dynamic_trees();
 
 // Statistics of one build.
 struct Stats {
@@ -110,7 +114,8 @@ bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& ca
                   std::vector<uint8_t>* bytes, std::string* text, std::vector<int32_t>* offsets, Stats* st);
 
 // ---- gradient tree code (jit_grad.cpp) ----------------------------------------------
-// Reverse-mode ∂L/∂c of every constant of a tree in one pass (L2 loss), for
+// Reverse-mode ∂L/∂c of every constant of a tree in one pass (any elementwise
+// loss has_dloss_routine accepts; lparam: its Float64 parameter's bits), for
 // gradient programs (compile_batch(..., grad = true)) of Float32 trees whose
 // operators are + - * / neg abs square cube exp sin cos and that have at
 // most SR_JIT_G_NGACC constants. Constants are read from a device array at
@@ -125,7 +130,7 @@ struct GradStats {
 };
 GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
                        const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list, std::vector<int32_t>& rest,
-                       GradStats* st);
+                       GradStats* st, int loss = SRHIP_LOSS_L2, uint64_t lparam = 0);
 void destroy_grad(GradModule* m);
 int grad_nslots(const GradModule* m);
 // the module's code objects: consecutive slot ranges, one launch each
@@ -138,7 +143,7 @@ hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const
                             const float* consts, float* gpart, int nconst, hipStream_t stream);
 bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
                        const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
-                       std::vector<int32_t>* offsets, GradStats* st);
+                       std::vector<int32_t>* offsets, GradStats* st, int loss = SRHIP_LOSS_L2, uint64_t lparam = 0);
 
 }  // namespace jit
 }  // namespace srhip

@@ -49,6 +49,7 @@ const int kBopRoutine[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE;
 const int kBopRoutineRC[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE_RC;  // rhs constant in s_k
 const int kBopRoutineLC[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE_LC;  // lhs constant in s_k
 const int kLossRoutine[SRHIP_NUM_LOSSES] = SR_JIT_LOSS_ROUTINE;     // -1: L2 (inline)
+const int kDLossRoutine[SRHIP_NUM_LOSSES] = SR_JIT_DLOSS_ROUTINE;   // dℓ/dr; -1: L2 (inline)
 const char* const kRoutineName[kNumRoutines] = SR_JIT_ROUTINE_NAMES;
 const int kRoutineTrig[kNumRoutines] = SR_JIT_ROUTINE_TRIG;
 const int kRoutineInline[kNumRoutines] = SR_JIT_ROUTINE_INLINE;        // same FAST / PRECISE code, small

@@ -1,8 +1,9 @@
 // jit_grad.cpp — gradient tree code: every tree of a Float32 gradient program
 // becomes straight-line gfx950 machine code that computes, per tile of 256
-// rows, the forward values, the L2 loss and the REVERSE-mode adjoints of its
+// rows, the forward values, the loss and the REVERSE-mode adjoints of its
 // constants: Σ_rows w·ℓ'(r)·∂ŷ/∂c_j for every constant c_j of the tree in one
-// pass, whatever the constant count.
+// pass, whatever the constant count. L2 inline; the other elementwise losses
+// (round 4) through their PRECISE-region loss and dℓ/dr routines.
 //
 // It replaces, for the batched constant optimiser (srhip_eval_loss_grad), the
 // forward-mode interpreter of grad_kernels.hip, which carries 1-4 tangents per
@@ -21,7 +22,8 @@
 //              code and the interpreters: did_succeed and values identical);
 //              every value the reverse pass needs stays in its block;
 //              root mark, a failed tile ends the tree;
-//              loss: r = ŷ - y masked past the last row, Σ w·r², seed 2·w·r;
+//              loss: r = ŷ - y masked past the last row, Σ w·r², seed 2·w·r
+//              (other losses: Σ w·ℓ(r), seed w·ℓ'(r), both by routine);
 //              reverse: adjoints in pool blocks, one per value, sign carried
 //              as a flag (neg / sub cost nothing); a constant's adjoint is
 //              summed over the lane's rows into its accumulator VGPR; sin /
@@ -161,6 +163,8 @@ struct GradGen {
   std::vector<GOp> ops;
   GOpnd root;
   int nc = 0;              // constants of the tree
+  int loss = SRHIP_LOSS_L2;
+  uint64_t lparam = 0;     // bits of the loss's Float64 parameter
   std::string why;
   int n = 0;
   std::vector<uint8_t> hasc;      // value's subtree holds a constant: it needs an adjoint
@@ -828,7 +832,7 @@ struct GradGen {
     bool trig = false;
     for (const GOp& o : ops)
       if (o.kind == K_UN && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS)) trig = true;
-    if (has_call || trig) set_base();
+    if (has_call || trig || loss != SRHIP_LOSS_L2) set_base();
     L_redo = as.label();
     if (fast) {
       as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(0), "s" + std::to_string(S_MODE));  // FAST
@@ -919,7 +923,9 @@ struct GradGen {
     free_values_at(n);
     free_feats_at(n);
     emit_mask(VY);
-    {
+    if (loss != SRHIP_LOSS_L2) {
+      if (!emit_loss_seed()) return false;
+    } else {
       const int L_unw = as.label(), L_seed = as.label();
       as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
       as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
@@ -1014,6 +1020,40 @@ struct GradGen {
     }
     return true;
   }
+  // Σ w·ℓ(r) into the lane's loss sum and the seed w·ℓ'(r) into VY (r in VY,
+  // 0 past the last row), ℓ and ℓ' by the PRECISE-region loss routines of
+  // gen_jit.py (device_ops.h elem_loss / elem_dloss, parameter in s_k:s_kh),
+  // both masked after the call (ℓ'(0) need not be 0: Quantile's is τ)
+  bool emit_loss_seed() {
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted (loss)"; return false; }
+    const int rb = blk_reg(k);
+    mov4(rb, VY);
+    mov4(VA, VY);
+    as.sop1(SOP1_MOV, "s_mov_b32", S_K, K((uint32_t)lparam), "s" + std::to_string(S_K));
+    as.sop1(SOP1_MOV, "s_mov_b32", S_KH, K((uint32_t)(lparam >> 32)), "s" + std::to_string(S_KH));
+    routine(kLossRoutine[loss], true);
+    mov4(VY, VA);
+    mov4(VA, rb);
+    routine(kDLossRoutine[loss], true);
+    const int L_unw = as.label();
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
+    as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VGT, S(S_WOFF), VLANE);
+    as.ds_read_b128(VGT, VGT, 0);
+    as.waitcnt_lgkm(0);
+    for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VY + e, V(VGT + e), VY + e);
+    for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", VA + e, V(VGT + e), VA + e);
+    as.bind(L_unw);
+    emit_mask(VY);
+    emit_mask(VA);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 2);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY + 1, V(VY + 1), VY + 3);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 1);
+    as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VLSUM, V(VLSUM), VY);
+    mov4(VY, VA);
+    return true;
+  }
   void shift_base(bool up) {
     as.sop2(up ? SOP2_ADD_U32 : SOP2_SUB_U32, up ? "s_add_u32" : "s_sub_u32", S_BASE, S(S_BASE), K((uint32_t)T.delta));
     as.sop2(up ? SOP2_ADDC_U32 : SOP2_SUBB_U32, up ? "s_addc_u32" : "s_subb_u32", S_BASE + 1, S(S_BASE + 1), K(0));
@@ -1021,8 +1061,9 @@ struct GradGen {
 };
 
 bool gen_grad_tree(const Ins<float>* prog, int nc, const Tmpl& T, bool text, std::vector<uint32_t>& out,
-                   std::vector<std::string>* lines, int32_t* off, std::string* why) {
+                   std::vector<std::string>* lines, int32_t* off, std::string* why, int loss, uint64_t lparam) {
   if (nc > NGACC) { *why = "more constants than accumulators"; return false; }
+  if (!has_dloss_routine(loss)) { *why = "loss without gradient routines"; return false; }
   std::vector<GOp> ir;
   GOpnd root;
   if (!build_gir(prog, ir, root, why)) return false;
@@ -1033,6 +1074,8 @@ bool gen_grad_tree(const Ins<float>* prog, int nc, const Tmpl& T, bool text, std
   g.ops = ir;
   g.root = root;
   g.nc = nc;
+  g.loss = loss;
+  g.lparam = lparam;
   if (!g.emit_tree()) { *why = g.why; return false; }
   as.finish();
   while (out.size() < start) {
@@ -1054,7 +1097,7 @@ bool gen_grad_tree(const Ins<float>* prog, int nc, const Tmpl& T, bool text, std
 size_t grad_codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
                     const std::vector<int32_t>& cand, size_t from, bool text, std::vector<uint32_t>& words,
                     std::vector<std::string>* lines, std::vector<int32_t>& offs, std::vector<int32_t>& ok_trees,
-                    std::vector<int32_t>& rest, GradStats* st, const Tmpl& T) {
+                    std::vector<int32_t>& rest, GradStats* st, const Tmpl& T, int loss, uint64_t lparam) {
   for (size_t k = from; k < cand.size(); ++k) {
     const int32_t t = cand[k];
     int32_t off = -1;
@@ -1062,7 +1105,8 @@ size_t grad_codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& 
     const size_t before = words.size();
     const size_t lbefore = lines ? lines->size() : 0;
     const int nc = const_off[t + 1] - const_off[t];
-    const bool okc = cb.tree_off[t] >= 0 && gen_grad_tree(&cb.code[cb.tree_off[t]], nc, T, text, words, lines, &off, &why);
+    const bool okc = cb.tree_off[t] >= 0 && gen_grad_tree(&cb.code[cb.tree_off[t]], nc, T, text, words, lines, &off, &why,
+                                                                  loss, lparam);
     if (okc && words.size() * 4 > T.area_bytes) {  // area full: the next part takes it
       words.resize(before);
       if (lines) lines->resize(lbefore);
@@ -1130,7 +1174,7 @@ void load_part(GradPart& pt, const Tmpl& T, const std::vector<uint32_t>& words, 
 
 GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
                        const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list, std::vector<int32_t>& rest,
-                       GradStats* st) {
+                       GradStats* st, int loss, uint64_t lparam) {
   const Templates& TT = templates();
   if (!TT.ok) { rest = cand; return nullptr; }
   auto t0 = std::chrono::steady_clock::now();
@@ -1142,7 +1186,7 @@ GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t
     Chunk ch;
     ch.T = &TT.large;
     const size_t next = grad_codegen(cb, const_off, cand, pos, false, ch.words, nullptr, ch.offs, ch.slots, rest, st,
-                                     TT.large);
+                                     TT.large, loss, lparam);
     if (next == pos) { rest.push_back(cand[pos]); if (st) st->nrejected++; pos = next + 1; continue; }  // one tree > area
     if ((int)chunks.size() + 1 == kMaxGradParts && next < cand.size()) {  // the rest stays interpreted
       for (size_t k = next; k < cand.size(); ++k) rest.push_back(cand[k]);
@@ -1156,7 +1200,8 @@ GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t
       Chunk sm;
       sm.T = &TT.small;
       std::vector<int32_t> rs;
-      grad_codegen(cb, const_off, ch.slots, 0, false, sm.words, nullptr, sm.offs, sm.slots, rs, nullptr, TT.small);
+      grad_codegen(cb, const_off, ch.slots, 0, false, sm.words, nullptr, sm.offs, sm.slots, rs, nullptr, TT.small, loss,
+                   lparam);
       if (sm.slots != ch.slots) throw Error(SRHIP_ERR_INVALID, "jit-grad: small-template relayout differs");
       ch = std::move(sm);
     }
@@ -1200,6 +1245,11 @@ void destroy_grad(GradModule* m) {
   delete m;
 }
 
+bool has_dloss_routine(int loss) {
+  return loss == SRHIP_LOSS_L2 ||
+         (loss >= 0 && loss < SRHIP_NUM_LOSSES && kLossRoutine[loss] >= 0 && kDLossRoutine[loss] >= 0);
+}
+
 int grad_nslots(const GradModule* m) { return m ? m->nslots : 0; }
 int grad_nparts(const GradModule* m) { return m ? (int)m->parts.size() : 0; }
 void grad_part(const GradModule* m, int k, int* slot0, int* nslots) {
@@ -1216,6 +1266,7 @@ struct JitGradArgs {
   const int32_t* ncon;
   float* gpart;
   int nconst;
+  int dyn;
 };
 
 hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const EvalArgs<float>& a,
@@ -1231,6 +1282,7 @@ hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const
   ja.ncon = pt.d_ncon;
   ja.gpart = gpart;
   ja.nconst = nconst;
+  ja.dyn = dynamic_trees() ? 1 : 0;
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned grid = a.rotate == 2 ? (unsigned)((a.nrg + 7) / 8 * 8) * (unsigned)a.ntg
@@ -1244,13 +1296,14 @@ hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const
 
 bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
                        const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
-                       std::vector<int32_t>* offsets, GradStats* st) {
+                       std::vector<int32_t>* offsets, GradStats* st, int loss, uint64_t lparam) {
   const Templates& TT = templates();
   if (!TT.ok) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("jit templates unavailable: ") + TT.why);
   std::vector<uint32_t> words;
   std::vector<std::string> lines;
   std::vector<int32_t> offs, okt, rest;
-  grad_codegen(cb, const_off, cand, 0, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, st, TT.large);
+  grad_codegen(cb, const_off, cand, 0, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, st, TT.large, loss,
+               lparam);
   if (bytes) {
     bytes->resize(words.size() * 4);
     std::memcpy(bytes->data(), words.data(), bytes->size());

@@ -73,7 +73,21 @@ struct JitArgs {
   const float* dcols;       // [nder][n_pad] the derived columns (sr_jit_derive), or null: staged ones computed here
   int nbig;                 // row groups [0, nbig) hold e.ntiles tiles; the tail row groups after them
   int ts;                   // hold ts tiles each (the last round of workgroups in smaller pieces)
+  int dyn;                  // 1: waves take their trees from an LDS counter (next_tree)
 };
+
+// The workgroup's trees are dealt to its waves one at a time from a counter in
+// the 16 LDS bytes after the tiles (and partials): a wave that drew expensive
+// trees (tiles redone PRECISE, long trees) no longer holds the workgroup, and
+// with it the CU's LDS, while its other waves idle (dyn = 0: the static deal
+// i = wave + k·nwaves). The counter starts at nwaves (each wave's first tree
+// is its own index); lane 0 takes the next index, the wave reads it.
+__device__ __forceinline__ int next_tree(uint32_t* ctr, int lane, int dyn, int i, int nwaves) {
+  if (!dyn) return i + nwaves;
+  uint32_t v = 0;
+  if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+  return __builtin_amdgcn_readfirstlane((int)v);
+}
 
 // A derived column's value: the PRECISE routine of the operator (the same
 // device_ops.h code as the tree code's PRECISE region and the interpreters).
@@ -113,6 +127,9 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   Part<float>* gdst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
   Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
   Part<float>* dst = ja.part_lds ? sPart : gdst;
+  uint32_t* sCtr = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(sPart) +
+                                               (ja.part_lds ? (size_t)a.tpb * sizeof(Part<float>) : 0));
+  if (threadIdx.x == 0) *sCtr = (uint32_t)(nthreads >> 6);
 
   // 1. stage the row group tile-major: tile t, array k (0 = y, 1 .. nraw =
   //    x_{k-1}, then the derived columns u(x_f), last = w); one wave per
@@ -180,22 +197,23 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const uint32_t nt_u = (uint32_t)nt_valid;
   const uint32_t fastok = (uint32_t)ja.fast;
 
-  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
-  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
-  m = __builtin_amdgcn_readfirstlane(m);
-  uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
+  // slot_of grows with i: the group's trees are the i < tpb whose slot exists
+  auto valid = [&](int i) { return i < a.tpb && slot_of(i) < a.nlist; };
+  int i = wave;
+  bool have = valid(i);
+  uint32_t fnext = have ? ld_flag(slot_of(i)) : 0u;
   // the next slot's code offset is loaded one tree ahead, like its flag
-  int32_t cnext = m > 0 ? code_of(slot_of(wave)) : 0;
+  int32_t cnext = have ? code_of(slot_of(i)) : 0;
   uint32_t redos = 0;  // tiles redone with the PRECISE routines (counted by tree code)
-  for (int k = 0; k < m; ++k) {
-    const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
+  while (have) {
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
-    const bool more = k + 1 < m;
+    const int inext = next_tree(sCtr, lane, ja.dyn, i, nwaves);
+    const bool more = valid(inext);
     const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
     const int32_t coff = cnext;
     if (more) {
-      fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
-      cnext = code_of(slot_of(wave + (k + 1) * nwaves));
+      fnext = ld_flag(slot_of(inext));
+      cnext = code_of(slot_of(inext));
     }
     float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
     if (!skip) {
@@ -235,6 +253,8 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
     if (lane == 0) dst[i] = Part<float>{lsum, chk};
     if (!skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    i = inext;
+    have = more;
   }
   if (lane == 0 && __builtin_amdgcn_readfirstlane((int)redos) != 0)
     __hip_atomic_fetch_add(ja.counters + 1, (uint32_t)__builtin_amdgcn_readfirstlane((int)redos),
@@ -286,6 +306,7 @@ struct JitGradArgs {
   const int32_t* ncon;      // [nlist] its constant count (<= SR_JIT_G_NGACC)
   float* gpart;             // [nrg][nconst] per-row-group Σ w·ℓ'·∂ŷ/∂c
   int nconst;
+  int dyn;                  // as JitArgs::dyn
 };
 
 template <bool W>
@@ -298,6 +319,8 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   if (!block_of(a, rg, g)) return;
   const int rows = a.ntiles * TILE;
   const int64_t row0 = (int64_t)rg * rows;
+  uint32_t* sCtr = reinterpret_cast<uint32_t*>(sX + (size_t)narr * rows);  // the 16 bytes after the tiles
+  if (threadIdx.x == 0) *sCtr = (uint32_t)(blockDim.x >> 6);
   {
     constexpr int V = TILE / 4;
     const int total = a.ntiles * narr * V;
@@ -338,18 +361,18 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   const uint32_t partial = (uint32_t)last_valid;
   const uint32_t nt_u = (uint32_t)nt_valid;
 
-  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
-  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
-  m = __builtin_amdgcn_readfirstlane(m);
-  uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
+  auto valid = [&](int i) { return i < a.tpb && slot_of(i) < a.nlist; };
+  int i = wave;
+  bool have = valid(i);
+  uint32_t fnext = have ? ld_flag(slot_of(i)) : 0u;
   float* gdst = ja.gpart + (size_t)rg * (size_t)ja.nconst;
   Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
-  for (int k = 0; k < m; ++k) {
-    const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
+  while (have) {
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
-    const bool more = k + 1 < m;
+    const int inext = next_tree(sCtr, lane, ja.dyn, i, nwaves);
+    const bool more = valid(inext);
     const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
-    if (more) fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
+    if (more) fnext = ld_flag(slot_of(inext));
     float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
     if (!skip) {
       const int cb = sld(ja.cbase, s);
@@ -371,6 +394,8 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
     if (lane == 0) dst[i] = Part<float>{lsum, chk};
     if (!skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    i = inext;
+    have = more;
   }
 }
 

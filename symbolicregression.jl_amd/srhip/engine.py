@@ -279,16 +279,20 @@ def _trees_struct(flat: FlatTrees, consts: np.ndarray) -> Trees:
     )
 
 
-def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bool = False):
+def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bool = False, loss=None):
     """Tree compiler without a device (srhip_jit_compile, or with grad=True
     srhip_jit_compile_grad: the reverse-mode gradient tree code; memc: the
-    memory-constant loss tree code): (code bytes, assembly text, {tree id:
-    byte offset})."""
+    memory-constant loss tree code; loss: a Loss other than L2, through
+    srhip_jit_compile_loss): (code bytes, assembly text, {tree id: byte
+    offset})."""
     consts = np.ascontiguousarray(flat.consts, dtype=np.float32)
     tr = _trees_struct(flat, consts)
     nb, nt, no = C.c_int64(0), C.c_int64(0), C.c_int64(0)
 
     def call(*bufs):
+        if loss is not None:
+            return lib().srhip_jit_compile_loss(C.byref(tr), int(grad), int(fast), int(loss.kind), float(loss.param),
+                                                bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2], C.byref(no))
         if grad:
             return lib().srhip_jit_compile_grad(C.byref(tr), bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
                                                 C.byref(no))

@@ -119,3 +119,36 @@ def test_gradient_code_covers_config5_trees():
     code, _, offs = jit_compile(flat, grad=True)
     assert len(offs) >= 0.97 * len(trees), f"{len(offs)} of {len(trees)}"
     print(f"{len(offs)} of {len(trees)} trees, {len(code) / len(offs):.0f} bytes per tree")
+
+
+LOSS_CASES = [srhip.L1DistLoss(), srhip.HuberLoss(0.7), srhip.L1EpsilonInsLoss(0.3), srhip.L2EpsilonInsLoss(0.25),
+              srhip.QuantileLoss(0.8)]
+
+
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.parametrize("loss", LOSS_CASES, ids=lambda l: f"kind{l.kind}")
+def test_loss_tails_equal_llvm_mc(loss):
+    """Tree code of the non-L2 elementwise losses: the loss tree code's tile
+    tail (FAST and PRECISE) and the gradient tree code's seed w·ℓ'(r) call the
+    loss's routines with its Float64 parameter in s_k:s_kh; same byte check."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(120, o, 5, np.float32, seed=31 + loss.kind)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    bits = int(np.float64(loss.param).view(np.uint64))
+    for grad, fast in ((False, True), (False, False), (True, False)):
+        code, text, offs = jit_compile(flat, fast=fast, grad=grad, loss=loss)
+        assert len(offs) >= 0.9 * len(trees), f"grad={grad}: only {len(offs)} of {len(trees)} trees compiled"
+        assert f"s_mov_b32 s90, {hex(bits >> 32)}" in text or (bits >> 32) == 0
+        ref = assemble(text)
+        assert ref == code, f"grad={grad} fast={fast}: machine code differs from llvm-mc"
+        if grad:  # two routine calls per tile beyond the L2 code's: ℓ and ℓ'
+            _, l2text, _ = jit_compile(flat, fast=fast, grad=True)
+            assert text.count("s_swappc_b64") == l2text.count("s_swappc_b64") + 2 * len(offs)
+
+
+def test_losses_without_routines_are_unsupported():
+    o = srhip.Options(binary_operators=["+", "*"], unary_operators=["cos"])
+    flat = srhip.flatten(srhip.random_population(4, o, 3, np.float32, seed=1), o, dtype=np.float32)
+    for loss in (srhip.LPDistLoss(3.0), srhip.PeriodicLoss(2.0)):
+        with pytest.raises(srhip.Unsupported):
+            jit_compile(flat, grad=True, loss=loss)

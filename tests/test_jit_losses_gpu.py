@@ -80,3 +80,85 @@ def test_tree_code_losses_match_oracle(gpu_ctx, loss, jit):
         bad = np.flatnonzero(m & ~(rel <= 1e-5))
         assert bad.size == 0, (name, bad[:10], float(np.nanmax(rel[m])))
         assert m.sum() > 300
+
+
+def _dloss(loss, r):
+    """dℓ/dr of LossFunctions.jl's distance losses (Float64 of the Float32
+    residual, the parameter unrounded: device_ops.h elem_dloss)."""
+    p, ar, sg = float(loss.param), np.abs(r), np.sign(r)
+    kind = loss.kind
+    if kind == K.LOSS["L1"]:
+        return sg
+    if kind == K.LOSS["HUBER"]:
+        return np.where(ar <= p, r, p * sg)
+    if kind == K.LOSS["L1EPSINS"]:
+        return np.where(ar > p, sg, 0.0)
+    if kind == K.LOSS["L2EPSINS"]:
+        return np.where(ar > p, 2.0 * (ar - p) * sg, 0.0)
+    assert kind == K.LOSS["QUANTILE"]
+    return np.where(r >= 0, p, p - 1.0)
+
+
+GRAD_LOSSES = [srhip.L1DistLoss(), srhip.HuberLoss(0.8), srhip.L1EpsilonInsLoss(0.3), srhip.L2EpsilonInsLoss(0.3),
+               srhip.QuantileLoss(0.3)]
+
+
+@pytest.mark.parametrize("loss", GRAD_LOSSES, ids=[f"{l.kind}-{l.params}" for l in GRAD_LOSSES])
+def test_gradient_tree_code_losses_match_oracle(gpu_ctx, loss):
+    """The gradient tree code's seed w·ℓ'(r) for the non-L2 losses (jit_grad.cpp
+    emit_loss_seed): ran as tree code, did_succeed and the loss as the
+    interpreter's, and every constant's ∂L/∂c directly against the oracle's
+    Float32 gradient terms w·ℓ'(ŷ - y)·∂ŷ/∂c within 1e-5 of Σ|terms| plus what a
+    4-ulp move of ŷ does to them (which covers the losses' kinks)."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(81 + loss.kind)
+    n = 3001
+    X = rng.standard_normal((5, n)).astype(np.float32)
+    y = (np.float32(2) * np.cos(X[3]) + X[0] * X[0] - np.float32(2)).astype(np.float32)
+    w = np.abs(rng.standard_normal(n)).astype(np.float32)
+    trees = srhip.random_population(400, o, 5, np.float32, seed=82)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    ctx = gpu_ctx
+    for weights in (None, w):
+        ds = srhip.DeviceDataset(ctx, X, y, weights)
+        res = {}
+        for mode in ("1", "0"):
+            os.environ["SRHIP_GJIT"] = mode
+            try:
+                prog = srhip.Program(ctx, flat, np.float32)
+                res[mode] = prog.eval_loss_grad(ds, loss.kind, loss.params)
+                res[mode + "ran"] = ctx.last_tree_code()
+            finally:
+                del os.environ["SRHIP_GJIT"]
+        assert res["1ran"] >= 0.95 * len(trees) and res["0ran"] == 0, (res["1ran"], res["0ran"])
+        s1, g1, w1, ok1 = res["1"]
+        s0, g0, w0, ok0 = res["0"]
+        assert np.array_equal(ok1, ok0) and w1 == w0
+        with np.errstate(invalid="ignore", divide="ignore"):
+            rel = np.abs(s1 - s0) / np.abs(s0)
+        assert np.all(rel[ok1 & (s0 != 0)] <= 1e-5), float(np.nanmax(rel[ok1 & (s0 != 0)]))
+        w64 = np.ones(n) if weights is None else weights.astype(np.float64)
+        eps = float(np.finfo(np.float32).eps)
+        checked = 0
+        for t in range(len(trees)):
+            k, a, c = flat.tree(t)
+            lo, hi = flat.const_off[t], flat.const_off[t + 1]
+            if hi == lo or not ok1[t]:
+                continue
+            with np.errstate(all="ignore"):
+                out, g, ok = oracle.eval_grad_consts(k, a, c.astype(np.float32), X, len(c), dtype=np.float32)
+                assert ok
+                r = (out - y).astype(np.float64)  # the Float32 residual, promoted
+                g = g.astype(np.float64)
+                term = w64 * _dloss(loss, r) * g
+                d = 4 * eps * (np.abs(out.astype(np.float64)) + np.abs(y.astype(np.float64)))
+                dv = np.maximum(np.abs(_dloss(loss, r + d) - _dloss(loss, r)),
+                                np.abs(_dloss(loss, r - d) - _dloss(loss, r))) * np.abs(w64 * g)
+            S, G, DV = np.abs(term).sum(axis=1), term.sum(axis=1), dv.sum(axis=1)
+            sel = np.isfinite(S) & (S < 1e20)
+            for gg, name in ((g1, "tree code"), (g0, "interpreter")):
+                err = np.abs(gg[lo:hi] - G)
+                bound = 1e-5 * S + DV + 1e-30
+                assert np.all(err[sel] <= bound[sel]), (name, loss.kind, t, err[sel].tolist(), bound[sel].tolist())
+            checked += int(sel.sum())
+        assert checked > 300
