@@ -1050,6 +1050,39 @@ jit::Module* loss_module(const srhip_program* p, int loss, double lparam) {
   return m;
 }
 
+// The per-row output tree code of a Float32 program (srhip_eval_tree_array):
+// the same trees compiled with jit::Options::out, PRECISE routines only, built
+// at the first per-row evaluation and kept with the program (kind -2 in
+// jit_loss); null (SRHIP_JIT_OUT=0, a different slot layout): interpreted.
+jit::Module* out_module(const srhip_program* p) {
+  if (!p->jit || p->nlist_j == 0) return nullptr;
+  static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_OUT"); return !(e && e[0] == '0'); }();
+  if (!on) return nullptr;
+  for (const auto& l : p->jit_loss)
+    if (l.kind == -2) return l.m;
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->consts.data();
+  CompiledBatch<float> cb = compile_batch_par<float>(tr);
+  jit::Options jo;
+  jo.fast = false;
+  jo.memc = jit::memc(p->jit);
+  jo.out = true;
+  std::vector<int32_t> jl, rest;
+  jit::Stats st;
+  jit::Module* m = jit::build(cb, p->h_jit_list, jl, rest, jo, &st);
+  if (m && (jl != p->h_jit_list || !rest.empty())) {
+    jit::destroy(m);
+    m = nullptr;
+  }
+  p->jit_loss.push_back({-2, 0, m});
+  return m;
+}
+
 // The gradient tree code of a Float32 program for an elementwise loss: the
 // L2 build, or the same candidates compiled with that loss's seed (jit_grad.cpp
 // emit_loss_seed), built at the loss's first gradient and kept with the
@@ -1106,7 +1139,9 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   }
   const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
   // slot ranges: [0, nj) tree code, [nj, nlist_a) shallow interpreter, then deep
-  jit::Module* jm = (std::is_same<T, float>::value && mode == MODE_LOSS) ? loss_module(p, loss, lparam) : nullptr;
+  jit::Module* jm = !std::is_same<T, float>::value ? nullptr
+                    : mode == MODE_LOSS          ? loss_module(p, loss, lparam)
+                                                 : out_module(p);
   const bool use_jit = jm != nullptr;
   c->last_jit_trees = (use_jit && rows > 0) ? p->nlist_j : 0;
   const int nj = use_jit ? p->nlist_j : 0;
@@ -2212,7 +2247,7 @@ int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* ou
 namespace {
 int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes, int64_t* inout_nbytes,
                          char* out_text, int64_t* inout_ntext, int32_t* out_offsets, int64_t* inout_noffsets,
-                         int loss = SRHIP_LOSS_L2, double lparam = 0.0) {
+                         int loss = SRHIP_LOSS_L2, double lparam = 0.0, bool out_mode = false) {
   return guarded([&] {
     if (!trees || !inout_nbytes || !inout_ntext || !inout_noffsets) throw Error(SRHIP_ERR_INVALID, "null argument");
     if (!jit::available()) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("tree compiler: ") + jit::unavailable_reason());
@@ -2242,6 +2277,7 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
       jo.text = true;
       jo.loss = loss;
       jo.lparam = lbits;
+      jo.out = out_mode;
       jit::compile_only(cb, cand, jo, &bytes, &text, &offs, nullptr);
     }
     if ((int64_t)bytes.size() > *inout_nbytes || (int64_t)text.size() + 1 > *inout_ntext ||
@@ -2265,10 +2301,10 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
 int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_bytes, int64_t* inout_nbytes,
                           char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
                           int64_t* inout_noffsets) {
-  // fast: bit 0 the FAST path, bit 1 memory-constant code (mode 3 / 4 below)
+  // fast: bit 0 the FAST path, bit 1 memory-constant code (mode 3 / 4 below),
+  // bit 2 per-row output code
   return jit_compile_hook(trees, (fast & 2) ? ((fast & 1) ? 4 : 3) : ((fast & 1) ? 1 : 0), out_bytes, inout_nbytes,
-                          out_text, inout_ntext, out_offsets,
-                          inout_noffsets);
+                          out_text, inout_ntext, out_offsets, inout_noffsets, SRHIP_LOSS_L2, 0.0, (fast & 4) != 0);
 }
 
 int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int64_t* inout_nbytes,

@@ -191,6 +191,8 @@ struct Gen {
   std::vector<int> next_call;    // first call index > i
   int L_tile = -1, L_done = -1, L_redo = -1, L_bail = -1;
   std::string why;
+  bool out = false;              // per-row output code (Options::out)
+  int out_rreg = -1;             // the root block of the tile (out mode)
 
   // SRHIP_JIT_TRIG_FULL=1 (tests): sin / cos through the complete compiled
   // routines instead of the hand-scheduled FAST bodies
@@ -852,8 +854,10 @@ struct Gen {
     for (int k = 0; k < NPOOL; ++k) pool_owner[k] = -1;
     nloads = 0;
     waited = 0;
-    as.ds_read_b128(VY, VLANE, 0);
-    ++nloads;
+    if (!out) {  // y (no y column in out mode)
+      as.ds_read_b128(VY, VLANE, 0);
+      ++nloads;
+    }
     for (size_t j = 0; j < feats.size(); ++j) {
       const int f = feats[j];
       xblk[f] = (int)j;
@@ -889,6 +893,10 @@ struct Gen {
       }
     }
     wait_all();
+    if (out) {  // out mode: the root block is stored by emit_tail_out
+      out_rreg = rreg;
+      return true;
+    }
     // ---- FAST-mode verdict: a failure or a guard redoes the tile precisely
     if (fast) {
       const int L_skip = as.label();
@@ -996,9 +1004,28 @@ struct Gen {
     as.bind(L_sum);
   }
 
+  // out mode: the tile's root block to the tree's output rows (lane ℓ holds
+  // rows 4ℓ .. 4ℓ+3 of the tile: one coalesced 1 KiB global_store_dwordx4 per
+  // wave at s[S_OUT:S_OUT+1] + 16ℓ), then the next tile's rows. Rows past the
+  // last are written too: they lie in the output's padding (stride n_pad).
+  void emit_store_out() {
+    const int voff = VGCAN;  // free without the FAST path: 16ℓ
+    as.vop2(VOP2_LSHLREV_B32, "v_lshlrev_b32_e32", voff, K(2), VLANE4);
+    as.put(0xdc7c8000u);  // global_store_dwordx4 voff, v[rreg:rreg+3], s[S_OUT:S_OUT+1]
+    as.put((uint32_t)voff | ((uint32_t)out_rreg << 8) | ((uint32_t)S_OUT << 16));
+    if (as.want_text)
+      as.lines.push_back("global_store_dwordx4 v" + std::to_string(voff) + ", v[" + std::to_string(out_rreg) + ":" +
+                         std::to_string(out_rreg + 3) + "], s[" + std::to_string(S_OUT) + ":" +
+                         std::to_string(S_OUT + 1) + "]");
+    as.sop2(SOP2_ADD_U32, "s_add_u32", S_OUT, S(S_OUT), K((uint32_t)(TILE * 4)));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", S_OUT + 1, S(S_OUT + 1), K(0));
+  }
+
   // second half of the tile: squares (weighted when s_woff != 0), mask, sums, loop
   void emit_tail() {
-    if (loss != SRHIP_LOSS_L2) {
+    if (out) {
+      emit_store_out();
+    } else if (loss != SRHIP_LOSS_L2) {
       emit_tail_loss();
     } else {
       const int L_unw = as.label(), L_sum = as.label();
@@ -1029,9 +1056,11 @@ struct Gen {
       }
       as.bind(L_sum);
     }
-    // a failed tile ends the tree
-    as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
-    as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
+    // a failed tile ends the tree (out mode: every tile is stored)
+    if (!out) {
+      as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
+      as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
+    }
     // after a redone tile the call's remaining tiles run PRECISE directly
     // (a tree whose guards fire on one tile mostly fires on the next: poles,
     // large arguments); SRHIP_JIT_STICKY=0: the next tile starts FAST again
@@ -1078,14 +1107,15 @@ struct Gen {
 static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool text, std::vector<uint32_t>& out,
                      std::vector<std::string>* lines, uint64_t area_va, int32_t* off, bool* is_fast,
                      std::string* why, const DerivedMap& dm, bool memc, int loss = SRHIP_LOSS_L2,
-                     uint64_t lparam = 0) {
+                     uint64_t lparam = 0, bool out_mode = false) {
   std::vector<IrOp> ir;
   Opnd root;
   if (!build_ir(prog, ir, root, &dm)) { *why = "program not translatable"; return false; }
   const size_t start = (out.size() + 15) / 16 * 16;  // 64-byte aligned entries
   Asm as;
   as.want_text = text;
-  Gen g(as, T, area_va + start * 4, fast_opt && loss != SRHIP_LOSS_PERIODIC);
+  Gen g(as, T, area_va + start * 4, fast_opt && loss != SRHIP_LOSS_PERIODIC && !out_mode);
+  g.out = out_mode;
   g.memc = memc;
   g.loss = loss;
   g.lparam = lparam;
@@ -1117,6 +1147,7 @@ struct ModulePart {
 struct Module {
   Columns cols;
   bool memc = false;
+  bool out = false;  // per-row output code: fn runs sr_jit_out(_m)
   std::vector<ModulePart> parts;
   uint32_t* d_bail = nullptr;  // [nslots + 2]: bail flags of all slots, bail count, PRECISE redo count
   int nslots = 0;
@@ -1148,7 +1179,7 @@ static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>
     const size_t lbefore = lines ? lines->size() : 0;
     const bool okc = cb.tree_off[t] >= 0 &&
                      gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, opt.text, words, lines, T.area_va, &off, &f, &why, dm, opt.memc,
-                              opt.loss, opt.lparam);
+                              opt.loss, opt.lparam, opt.out);
     if (okc && words.size() * 4 > T.area_bytes) {  // area full: the next part takes it
       words.resize(before);
       if (lines) lines->resize(lbefore);
@@ -1335,6 +1366,7 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
   Module* m = new Module();
   m->cols = cols;
   m->memc = opt.memc;
+  m->out = opt.out;
   try {
     for (Chunk& ch : chunks) {
       ModulePart pt;
@@ -1345,8 +1377,13 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       std::vector<uint8_t> img(ch.T->img, ch.T->img + ch.T->size);
       std::memcpy(img.data() + ch.T->area_off, ch.words.data(), ch.words.size() * 4);
       HIP_CHECK(hipModuleLoadData(&q.mod, img.data()));
-      HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, opt.memc ? "sr_jit_eval_m" : "sr_jit_eval"));
-      HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, opt.memc ? "sr_jit_eval_mw" : "sr_jit_eval_w"));
+      if (opt.out) {  // no weighted variant: the output kernel reads no y / w
+        HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, opt.memc ? "sr_jit_out_m" : "sr_jit_out"));
+        q.fn_w = q.fn;
+      } else {
+        HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, opt.memc ? "sr_jit_eval_m" : "sr_jit_eval"));
+        HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, opt.memc ? "sr_jit_eval_mw" : "sr_jit_eval_w"));
+      }
       HIP_CHECK(hipModuleGetFunction(&q.fn_derive, q.mod, "sr_jit_derive"));
       for (hipFunction_t f : {q.fn, q.fn_w})
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
@@ -1446,12 +1483,13 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
                   hipStream_t stream) {
   const ModulePart& q = m->parts[k];
   if (a.nlist != q.nslots) return hipErrorInvalidValue;
+  if (m->out && (a.w != nullptr || a.out == nullptr || a.out_stride < a.n_pad)) return hipErrorInvalidValue;
   JitArgs ja;
   ja.e = a;
   ja.code_off = q.d_off;
   ja.bail = m->d_bail + q.slot0;
   ja.counters = m->d_bail + m->nslots;
-  ja.fast = fast ? 1 : 0;
+  ja.fast = (fast && !m->out) ? 1 : 0;
   ja.nraw = m->cols.nraw;
   ja.nder = m->cols.nder;
   std::memcpy(ja.der, m->cols.der, sizeof(ja.der));

@@ -27,6 +27,11 @@ struct Options {
   // the interpreter's); PERIODIC keeps every tree off the FAST path
   int loss = SRHIP_LOSS_L2;
   uint64_t lparam = 0;     // Float64 bits (LossFunctions' field, never rounded to Float32)
+  // per-row output tree code (srhip_eval_tree_array): every tile stores its
+  // root values to the tree's output rows instead of ending with a loss; the
+  // PRECISE routines only (the interpreter's values, bit for bit), every tile
+  // evaluated whatever fails (the interpreter's MODE_OUT writes them too)
+  bool out = false;
 };
 
 // Derived columns: a routine unary operator applied to a dataset feature,

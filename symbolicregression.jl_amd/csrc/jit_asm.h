@@ -38,6 +38,10 @@ constexpr int S_FASTOK = SR_JIT_S_FASTOK, S_EPS = SR_JIT_S_EPS;
 constexpr int S_KH = SR_JIT_S_KH;  // high word of a loss routine's Float64 parameter
 constexpr int S_K = SR_JIT_S_K, S_PE = SR_JIT_S_PE, S_MODE = SR_JIT_S_MODE, S_X0 = SR_JIT_S_X0;
 constexpr int S_BASE = SR_JIT_S_X2;
+// per-row output tree code (Options::out): s[92:93] = this tree's output rows
+// of the current tile (set by the driver, advanced a tile per tile); above
+// every register of tree-code state and of the routines
+constexpr int S_OUT = 92;
 constexpr int S_RECIP = SR_JIT_S_X1;  // RN(1/c) of a constant divisor (routine b_div_rk)  // s[86:87]: base of the routine region in use (FAST or PRECISE)
 // a routine temporary, free between calls: the constant operand of a packed
 // tree-code instruction (low half of s[20:21]; VOP3P takes no literal)
@@ -359,7 +363,8 @@ struct Asm {
 // VALU / SALU opcodes (gfx9 encodings, checked against llvm-mc by tests/test_jit.py)
 enum : int {
   VOP2_CNDMASK = 0x00, VOP2_ADD_F32 = 0x01, VOP2_SUB_F32 = 0x02, VOP2_SUBREV_F32 = 0x03, VOP2_MUL_F32 = 0x05,
-  VOP2_MIN_F32 = 0x0a, VOP2_MAX_F32 = 0x0b, VOP2_AND_B32 = 0x13, VOP2_XOR_B32 = 0x15, VOP2_ADD_U32 = 0x34,
+  VOP2_MIN_F32 = 0x0a, VOP2_MAX_F32 = 0x0b, VOP2_LSHLREV_B32 = 0x12, VOP2_AND_B32 = 0x13, VOP2_XOR_B32 = 0x15,
+  VOP2_ADD_U32 = 0x34,
   VOP1_MOV = 0x01,
   VOP3_ADD_F32 = 0x101, VOP3_MIN_F32 = 0x10a, VOP3_MAX_F32 = 0x10b, VOP3_FMA_F32 = 0x1cb,
   VOP3_MIN3_F32 = 0x1d0, VOP3_MAX3_F32 = 0x1d3,

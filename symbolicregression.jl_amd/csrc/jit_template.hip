@@ -73,21 +73,8 @@ struct JitArgs {
   const float* dcols;       // [nder][n_pad] the derived columns (sr_jit_derive), or null: staged ones computed here
   int nbig;                 // row groups [0, nbig) hold e.ntiles tiles; the tail row groups after them
   int ts;                   // hold ts tiles each (the last round of workgroups in smaller pieces)
-  int dyn;                  // 1: waves take their trees from an LDS counter (next_tree)
+  int dyn;                  // (reserved: dynamic tree dealing, not in this build)
 };
-
-// The workgroup's trees are dealt to its waves one at a time from a counter in
-// the 16 LDS bytes after the tiles (and partials): a wave that drew expensive
-// trees (tiles redone PRECISE, long trees) no longer holds the workgroup, and
-// with it the CU's LDS, while its other waves idle (dyn = 0: the static deal
-// i = wave + k·nwaves). The counter starts at nwaves (each wave's first tree
-// is its own index); lane 0 takes the next index, the wave reads it.
-__device__ __forceinline__ int next_tree(uint32_t* ctr, int lane, int dyn, int i, int nwaves) {
-  if (!dyn) return i + nwaves;
-  uint32_t v = 0;
-  if (lane == 0) v = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-  return __builtin_amdgcn_readfirstlane((int)v);
-}
 
 // A derived column's value: the PRECISE routine of the operator (the same
 // device_ops.h code as the tree code's PRECISE region and the interpreters).
@@ -108,7 +95,11 @@ __device__ __forceinline__ float derive_uop(int op, float x) {
   }
 }
 
-template <bool W, bool MEMC>
+// OUT: per-row output tree code (srhip_eval_tree_array): no y column is
+// staged, no failure flags are read or set (every tile of every tree is
+// evaluated, as the interpreter's MODE_OUT does), and each tree's code gets
+// its output rows of this row group in s[92:93] (jit.cpp S_OUT).
+template <bool W, bool MEMC, bool OUT = false>
 __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const EvalArgs<float>& a = ja.e;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -127,9 +118,6 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   Part<float>* gdst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
   Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
   Part<float>* dst = ja.part_lds ? sPart : gdst;
-  uint32_t* sCtr = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(sPart) +
-                                               (ja.part_lds ? (size_t)a.tpb * sizeof(Part<float>) : 0));
-  if (threadIdx.x == 0) *sCtr = (uint32_t)(nthreads >> 6);
 
   // 1. stage the row group tile-major: tile t, array k (0 = y, 1 .. nraw =
   //    x_{k-1}, then the derived columns u(x_f), last = w); one wave per
@@ -142,6 +130,7 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
       const int tk = idx / V;
       const int k = tk % narr;
       const int t = tk / narr;
+      if (OUT && k == 0) continue;  // no y
       if (k > ja.nraw && k <= ncol && ja.dcols) {
         const float* src = ja.dcols + (size_t)(k - 1 - ja.nraw) * a.n_pad;
         reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
@@ -179,7 +168,9 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
     return reinterpret_cast<uint64_t>(
         a.prog + __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(a.list_off))[s]));
   };
-  auto ld_flag = [&](int slot) { return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto ld_flag = [&](int slot) {
+    return OUT ? 0u : __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
 
   // address of the code area (PC-relative, resolved when the image is linked)
   uint64_t area;
@@ -197,30 +188,48 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const uint32_t nt_u = (uint32_t)nt_valid;
   const uint32_t fastok = (uint32_t)ja.fast;
 
-  // slot_of grows with i: the group's trees are the i < tpb whose slot exists
-  auto valid = [&](int i) { return i < a.tpb && slot_of(i) < a.nlist; };
-  int i = wave;
-  bool have = valid(i);
-  uint32_t fnext = have ? ld_flag(slot_of(i)) : 0u;
+  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
+  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
+  m = __builtin_amdgcn_readfirstlane(m);
+  uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
   // the next slot's code offset is loaded one tree ahead, like its flag
-  int32_t cnext = have ? code_of(slot_of(i)) : 0;
+  int32_t cnext = m > 0 ? code_of(slot_of(wave)) : 0;
   uint32_t redos = 0;  // tiles redone with the PRECISE routines (counted by tree code)
-  while (have) {
+  for (int k = 0; k < m; ++k) {
+    const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
-    const int inext = next_tree(sCtr, lane, ja.dyn, i, nwaves);
-    const bool more = valid(inext);
+    const bool more = k + 1 < m;
     const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
     const int32_t coff = cnext;
     if (more) {
-      fnext = ld_flag(slot_of(inext));
-      cnext = code_of(slot_of(inext));
+      fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
+      cnext = code_of(slot_of(wave + (k + 1) * nwaves));
     }
     float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
     if (!skip) {
       const uint64_t target = area + (uint32_t)coff;
       uint32_t la = lds_lane;
       uint32_t tile = 0, status;
-      if constexpr (MEMC) {  // memory-constant tree code: its program in s[56:57], constants in s24..s39
+      if constexpr (OUT) {  // the tree's output rows of this row group
+        const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
+        uint64_t optr = reinterpret_cast<uint64_t>(a.out + (size_t)t * (size_t)a.out_stride + row0);
+        if constexpr (MEMC) {
+          uint64_t pptr = prog_of(s);
+          asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                       : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
+                         "+{s84}"(redos), "+{s[56:57]}"(pptr), "+{s[92:93]}"(optr)
+                       : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial),
+                         "{s67}"(tilebytes), "{s68}"(woff), "{s79}"(fastok)
+                       : SR_JIT_CLOBBERS_MEMC, "memory");
+        } else {
+          asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                       : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
+                         "+{s84}"(redos), "+{s[92:93]}"(optr)
+                       : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial),
+                         "{s67}"(tilebytes), "{s68}"(woff), "{s79}"(fastok)
+                       : SR_JIT_CLOBBERS, "memory");
+        }
+      } else if constexpr (MEMC) {  // memory-constant tree code: its program in s[56:57], constants in s24..s39
         uint64_t pptr = prog_of(s);
         asm volatile("s_swappc_b64 s[76:77], %[tgt]"
                      : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
@@ -251,10 +260,8 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
     lsum = wave_sum(lsum);
     chk = __builtin_amdgcn_ballot_w64(chk != chk) != 0 ? __builtin_nanf("") : 0.0f;
     if (lane == 0) dst[i] = Part<float>{lsum, chk};
-    if (!skip && chk != chk && lane == 0)
+    if (!OUT && !skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    i = inext;
-    have = more;
   }
   if (lane == 0 && __builtin_amdgcn_readfirstlane((int)redos) != 0)
     __hip_atomic_fetch_add(ja.counters + 1, (uint32_t)__builtin_amdgcn_readfirstlane((int)redos),
@@ -291,6 +298,8 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval(JitArgs ja) { jit
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_w(JitArgs ja) { jit_eval_body<true, false>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_m(JitArgs ja) { jit_eval_body<false, true>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_mw(JitArgs ja) { jit_eval_body<true, true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_out(JitArgs ja) { jit_eval_body<false, false, true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { jit_eval_body<false, true, true>(ja); }
 
 // ---- gradient tree code (jit_grad.cpp) ---------------------------------------------
 // One workgroup = (row group, tree group) as above; each tree's code runs the
@@ -306,7 +315,7 @@ struct JitGradArgs {
   const int32_t* ncon;      // [nlist] its constant count (<= SR_JIT_G_NGACC)
   float* gpart;             // [nrg][nconst] per-row-group Σ w·ℓ'·∂ŷ/∂c
   int nconst;
-  int dyn;                  // as JitArgs::dyn
+  int dyn;                  // (reserved, as JitArgs::dyn)
 };
 
 template <bool W>
@@ -319,8 +328,6 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   if (!block_of(a, rg, g)) return;
   const int rows = a.ntiles * TILE;
   const int64_t row0 = (int64_t)rg * rows;
-  uint32_t* sCtr = reinterpret_cast<uint32_t*>(sX + (size_t)narr * rows);  // the 16 bytes after the tiles
-  if (threadIdx.x == 0) *sCtr = (uint32_t)(blockDim.x >> 6);
   {
     constexpr int V = TILE / 4;
     const int total = a.ntiles * narr * V;
@@ -361,18 +368,18 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   const uint32_t partial = (uint32_t)last_valid;
   const uint32_t nt_u = (uint32_t)nt_valid;
 
-  auto valid = [&](int i) { return i < a.tpb && slot_of(i) < a.nlist; };
-  int i = wave;
-  bool have = valid(i);
-  uint32_t fnext = have ? ld_flag(slot_of(i)) : 0u;
+  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
+  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
+  m = __builtin_amdgcn_readfirstlane(m);
+  uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
   float* gdst = ja.gpart + (size_t)rg * (size_t)ja.nconst;
   Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
-  while (have) {
+  for (int k = 0; k < m; ++k) {
+    const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
-    const int inext = next_tree(sCtr, lane, ja.dyn, i, nwaves);
-    const bool more = valid(inext);
+    const bool more = k + 1 < m;
     const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
-    if (more) fnext = ld_flag(slot_of(inext));
+    if (more) fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
     float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
     if (!skip) {
       const int cb = sld(ja.cbase, s);
@@ -394,8 +401,6 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
     if (lane == 0) dst[i] = Part<float>{lsum, chk};
     if (!skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    i = inext;
-    have = more;
   }
 }
 

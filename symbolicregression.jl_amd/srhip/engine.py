@@ -279,11 +279,13 @@ def _trees_struct(flat: FlatTrees, consts: np.ndarray) -> Trees:
     )
 
 
-def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bool = False, loss=None):
+def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bool = False, loss=None,
+                out: bool = False):
     """Tree compiler without a device (srhip_jit_compile, or with grad=True
     srhip_jit_compile_grad: the reverse-mode gradient tree code; memc: the
     memory-constant loss tree code; loss: a Loss other than L2, through
-    srhip_jit_compile_loss): (code bytes, assembly text, {tree id: byte
+    srhip_jit_compile_loss; out: the per-row output code of
+    srhip_eval_tree_array): (code bytes, assembly text, {tree id: byte
     offset})."""
     consts = np.ascontiguousarray(flat.consts, dtype=np.float32)
     tr = _trees_struct(flat, consts)
@@ -296,7 +298,8 @@ def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bo
         if grad:
             return lib().srhip_jit_compile_grad(C.byref(tr), bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
                                                 C.byref(no))
-        return lib().srhip_jit_compile(C.byref(tr), int(fast) | (2 if memc else 0), bufs[0], C.byref(nb), bufs[1],
+        return lib().srhip_jit_compile(C.byref(tr), int(fast) | (2 if memc else 0) | (4 if out else 0), bufs[0],
+                                       C.byref(nb), bufs[1],
                                        C.byref(nt), bufs[2], C.byref(no))
 
     rc = call(None, None, None)

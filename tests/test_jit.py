@@ -152,3 +152,20 @@ def test_losses_without_routines_are_unsupported():
     for loss in (srhip.LPDistLoss(3.0), srhip.PeriodicLoss(2.0)):
         with pytest.raises(srhip.Unsupported):
             jit_compile(flat, grad=True, loss=loss)
+
+
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.parametrize("memc", [False, True])
+def test_output_code_equals_llvm_mc(memc):
+    """The per-row output tree code of srhip_eval_tree_array (Options::out):
+    PRECISE only, no y load, one global_store_dwordx4 of the root block per
+    tile, no early exit; same byte check."""
+    b_ops, u_ops = OPSETS[1]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    trees = srhip.random_population(200, o, 6, np.float32, seed=41)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    code, text, offs = jit_compile(flat, fast=False, memc=memc, out=True)
+    assert len(offs) >= 0.7 * len(trees)
+    assert text.count("global_store_dwordx4") == len(offs)
+    assert "s_cmp_lg_u32 s83" not in text  # no FAST verdict
+    assert assemble(text) == code
