@@ -238,6 +238,7 @@ struct srhip_program {
   int nlist_a = 0, nlist_b = 0;
   // tree code (jit.cpp) of the first nlist_j shallow slots, Float32 programs
   jit::Module* jit = nullptr;
+  jit::Module64* jit64 = nullptr;  // Float64 programs: the same slots as Float64 tree code (jit64.cpp)
   int nlist_j = 0;
   std::vector<int32_t> h_jit_list;  // the trees of those slots, in slot order
   // the same trees' tree code for other elementwise losses (jit::Options::loss),
@@ -409,6 +410,8 @@ void free_loss_jits(const srhip_program* p) {
 void free_program_device(srhip_program* p) {
   jit::destroy(p->jit);
   p->jit = nullptr;
+  jit::destroy64(p->jit64);
+  p->jit64 = nullptr;
   free_loss_jits(p);
   p->nlist_j = 0;
   if (p->d_code) (void)hipFree(p->d_code);
@@ -767,6 +770,8 @@ void build_program(srhip_program* p) {
   // trees lead the shallow list, the others follow (interpreter)
   jit::destroy(p->jit);
   p->jit = nullptr;
+  jit::destroy64(p->jit64);
+  p->jit64 = nullptr;
   free_loss_jits(p);
   p->h_jit_list.clear();
   p->nlist_j = 0;
@@ -780,6 +785,20 @@ void build_program(srhip_program* p) {
       jo.memc = p->jit_memc || (me && me[0] == '1');
       p->jit = jit::build(cb, a, jl, rest, jo, &p->jit_stats);
       if (p->jit) {
+        p->nlist_j = (int)jl.size();
+        p->h_jit_list = jl;
+        a = jl;
+        a.insert(a.end(), rest.begin(), rest.end());
+      }
+    }
+  } else {
+    // Float64 tree code (jit64.cpp) for the shallow trees of large batches;
+    // SRHIP_JIT64=0: interpreted
+    static const bool on64 = [] { const char* e = std::getenv("SRHIP_JIT64"); return !(e && e[0] == '0'); }();
+    if (on64 && p->jit_allowed && jit_wanted((int)a.size()) && jit::available64()) {
+      std::vector<int32_t> jl, rest;
+      p->jit64 = jit::build64(cb, a, jl, rest, &p->jit_stats);
+      if (p->jit64) {
         p->nlist_j = (int)jl.size();
         p->h_jit_list = jl;
         a = jl;
@@ -830,6 +849,17 @@ void build_program(srhip_program* p) {
 // patched at the next gradient call); a changed layout rebuilds.
 template <typename T>
 void update_constants(srhip_program* p) {
+  if (p->jit64) {  // Float64 tree code holds its constants as literals: interpreted from now on
+    p->jit_allowed = false;
+    ++p->n_rebuild;
+    const bool had_grad = p->grad_built;
+    build_program<T>(p);
+    if (had_grad) {
+      p->grad_built = true;
+      p->grad_stale = true;
+    }
+    return;
+  }
   if (p->jit && !p->jit_memc && !jit::memc(p->jit)) {
     // first new constant set of a tree-code program with constants in its
     // code: rebuilt once as memory-constant tree code (jit.cpp Gen::memc),
@@ -1142,14 +1172,18 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   jit::Module* jm = !std::is_same<T, float>::value ? nullptr
                     : mode == MODE_LOSS          ? loss_module(p, loss, lparam)
                                                  : out_module(p);
-  const bool use_jit = jm != nullptr;
+  // Float64 programs: their tree code (L2 loss)
+  jit::Module64* jm64 = nullptr;
+  if constexpr (std::is_same<T, double>::value)
+    if (mode == MODE_LOSS && loss == SRHIP_LOSS_L2 && p->jit64 && p->nlist_j > 0) jm64 = p->jit64;
+  const bool use_jit = jm != nullptr || jm64 != nullptr;
   c->last_jit_trees = (use_jit && rows > 0) ? p->nlist_j : 0;
   const int nj = use_jit ? p->nlist_j : 0;
   // failure flags (and the tree code's bail flags): the finalize kernels of
   // the previous call left them clean; one clearing launch only after a new
   // buffer, an interrupted call or a path that leaves them set (gradients,
   // tree code that can hand tiles back)
-  const bool jit_bail = use_jit && jit::can_bail();
+  const bool jit_bail = jm != nullptr && jit::can_bail();
   if (mode == MODE_LOSS) {
     const size_t need = std::max<size_t>(nslots, 1) * sizeof(uint32_t);
     if (c->fail.bytes < need) {
@@ -1173,6 +1207,12 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
         jit::part(jm, k, &s0, &nsl);
         launches.push_back({-1, s0, nsl, k});
       }
+    } else {
+      for (int k = 0; k < jit::nparts64(jm64); ++k) {
+        int s0, nsl;
+        jit::part64(jm64, k, &s0, &nsl);
+        launches.push_back({-1, s0, nsl, k});
+      }
     }
   }
   launches.push_back({0, nj, p->nlist_a - nj, -1});
@@ -1190,7 +1230,14 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
       continue;
     }
     EvalPlan plan;
-    if (pass == -1) {
+    if (pass == -1 && jm64) {
+      // Float64 tree code: 128-row tiles of y, the features it reads, w; 4 waves
+      const int narr = 1 + jit::nraw64(jm64) + (w ? 1 : 0);
+      if (jit::nraw64(jm64) > nfeat) throw Error(SRHIP_ERR_INVALID, "dataset has fewer features than the program reads");
+      if (!plan_geometry(8, 2, kShallowSlots, narr, 1, rows, nlist, &plan, 52 * 1024, 52 * 1024, 16384, 64))
+        throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
+      plan.threads = 256;
+    } else if (pass == -1) {
       // LDS columns: y, the raw features the tree code reads, its derived columns, w
       const jit::Columns& jc = jit::columns(jm);
       if (jc.nraw > nfeat) throw Error(SRHIP_ERR_INVALID, "dataset has fewer features than the program reads");
@@ -1238,8 +1285,8 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.nrg = plan.nrg;
     a.loss = loss;
     a.rotate = rotate_enabled() ? 1 : 0;
-    a.contig = (pass == -1 && jit_contig()) ? 1 : 0;
-    if (pass == -1 && rg_xcd()) a.rotate = 2;  // tree code: row groups per XCD
+    a.contig = (pass == -1 && jm && jit_contig()) ? 1 : 0;
+    if (pass == -1 && jm && rg_xcd()) a.rotate = 2;  // tree code: row groups per XCD
     a.lparam = lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);
@@ -1258,13 +1305,15 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
           dcols = static_cast<const float*>(c->derived.p);
         }
         HIP_CHECK(jit::launch(jm, launches[li].part, plan, a, jit_fast_enabled(), dcols, s));
+      } else {
+        HIP_CHECK(jit::launch64(jm64, launches[li].part, plan, a, s));
       }
     } else {
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
     timed_end(c, s, tk);
     // the last tree-code part's finalize hands over and clears the tree code's counters
-    uint32_t* cnt = (last_jit && !jit_bail) ? jit::bail_flags(jm) + nj : nullptr;
+    uint32_t* cnt = (last_jit && jm && !jit_bail) ? jit::bail_flags(jm) + nj : nullptr;
     HIP_CHECK(launch_finalize<T>(a, c->res_sum, c->res_ok, s, cnt, cnt ? c->pin_cnt : nullptr));
     if (cnt) c->cnt_pending = true;
     static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
@@ -2260,7 +2309,13 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
     if (mode == 2 && !jit::has_dloss_routine(loss))
       throw Error(SRHIP_ERR_UNSUPPORTED, "no gradient tree code for this loss");
     if (mode != 2 && !jit::has_loss_routine(loss)) throw Error(SRHIP_ERR_UNSUPPORTED, "no tree code for this loss");
-    if (mode == 2) {  // gradient tree code
+    if (mode == 5) {  // Float64 tree code (jit64.cpp)
+      CompiledBatch<double> cb = compile_batch<double>(*trees);
+      std::vector<int32_t> cand;
+      for (int t = 0; t < cb.ntrees; ++t)
+        if (cb.tree_off[t] >= 0 && cb.need[t] <= kShallowSlots) cand.push_back(t);
+      jit::compile_only64(cb, cand, &bytes, &text, &offs);
+    } else if (mode == 2) {  // gradient tree code
       CompiledBatch<float> cb = compile_batch<float>(*trees, /*grad=*/true);
       std::vector<int32_t> cand, coff(trees->const_off, trees->const_off + trees->ntrees + 1);
       for (int t = 0; t < cb.ntrees; ++t)
@@ -2302,7 +2357,9 @@ int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_b
                           char* out_text, int64_t* inout_ntext, int32_t* out_offsets,
                           int64_t* inout_noffsets) {
   // fast: bit 0 the FAST path, bit 1 memory-constant code (mode 3 / 4 below),
-  // bit 2 per-row output code
+  // bit 2 per-row output code, bit 3 Float64 trees (jit64.cpp; the other bits ignored)
+  if (fast & 8)  // Float64 trees
+    return jit_compile_hook(trees, 5, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets, inout_noffsets);
   return jit_compile_hook(trees, (fast & 2) ? ((fast & 1) ? 4 : 3) : ((fast & 1) ? 1 : 0), out_bytes, inout_nbytes,
                           out_text, inout_ntext, out_offsets, inout_noffsets, SRHIP_LOSS_L2, 0.0, (fast & 4) != 0);
 }

@@ -150,5 +150,23 @@ bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t
                        const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
                        std::vector<int32_t>* offsets, GradStats* st, int loss = SRHIP_LOSS_L2, uint64_t lparam = 0);
 
+// ---- Float64 tree code (jit64.cpp) ---------------------------------------------------
+// The shallow trees of a Float64 program as straight-line code with the
+// Float64 interpreter's operator routines (no FAST path), L2 loss; 2 rows per
+// lane, 128-row tiles. Constants are literals: a program whose constants are
+// set again runs on the interpreter.
+struct Module64;
+bool available64();
+Module64* build64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list,
+                  std::vector<int32_t>& rest, Stats* st);
+void destroy64(Module64* m);
+int nparts64(const Module64* m);
+void part64(const Module64* m, int k, int* slot0, int* nslots);
+int nraw64(const Module64* m);  // feature columns the code reads (staged per tile)
+// plan: tile 128 rows, 256 threads; EvalArgs as for the interpreter (list / fail / partial of the part)
+hipError_t launch64(Module64* m, int k, const EvalPlan& plan, const EvalArgs<double>& a, hipStream_t stream);
+bool compile_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes,
+                    std::string* text, std::vector<int32_t>* offsets);
+
 }  // namespace jit
 }  // namespace srhip

@@ -1,0 +1,727 @@
+// jit64.cpp — the Float64 tree compiler: every shallow tree of a Float64
+// batch becomes straight-line gfx950 machine code, the counterpart of jit.cpp
+// for Dataset{Float64} (BASELINE config #3: NaN-heavy Float64 evaluation).
+//
+// Float64 has no FAST path: the routines are the Float64 interpreter's
+// operator code (gen_jit64.py), so losses and did_succeed are the
+// interpreter's. Layout (jit64_layout.h): R = 2 rows per lane, a 128-row tile
+// is 1 KiB per column (the byte layout of the Float32 tiles), a value block is
+// 4 VGPRs (two Float64), 8 pool blocks, the routine operands in A = v[32:35]
+// and B = v[36:39], the non-finite marker CHK = v[40:41] (Float64), the lane's
+// loss sum LSUM = v[44:45].
+//
+// Tree code of one tree:
+//   prologue  routine base (s_getpc), status 0
+//   tile      y and the features inline operators read, from the LDS tile
+//             (ds_read_b128: two rows); + - * neg abs square cube inline
+//             (v_add_f64 / v_mul_f64, sign bits on the high word), every other
+//             operator by routine; the root marked into CHK (fma(v, 0, chk):
+//             NaN for a non-finite value, as the interpreter's mark); the
+//             residual, masked past the last row, squared (weighted) into LSUM;
+//             a failed tile ends the tree (DynamicExpressions' early exit)
+//   epilogue  s_setpc_b64 back to the driver (jit64_template.hip)
+// Constants are literals of the code (an SGPR pair per use, or s_k : s_kh for
+// a routine's constant operand): a program whose constants are set again runs
+// on the interpreter (api.cpp update_constants).
+#include <algorithm>
+#include <chrono>
+#include <cstdlib>
+#include <cstring>
+
+#include "jit.h"
+#include "jit_asm.h"
+#include "gen/jit64_layout.h"
+
+#define HIP_CHECK(expr)                                                                  \
+  do {                                                                                   \
+    hipError_t _e = (expr);                                                              \
+    if (_e != hipSuccess)                                                                \
+      throw Error(SRHIP_ERR_DEVICE, std::string(#expr) + ": " + hipGetErrorString(_e));  \
+  } while (0)
+
+extern "C" const unsigned char srhip_jit64_tmpl[];
+extern "C" const unsigned char srhip_jit64_tmpl_end[];
+
+namespace srhip {
+namespace jit {
+namespace {
+
+using detail::Asm;
+using detail::K;
+using detail::S;
+using detail::Src;
+using detail::V;
+
+constexpr int R2 = 2, TILE2 = 64 * R2;
+constexpr int A2 = SR_JIT64_V_A, B2 = SR_JIT64_V_B, CHK2 = SR_JIT64_V_CHK, LANE2 = SR_JIT64_V_LANE;
+constexpr int LROW2 = SR_JIT64_V_LANE2, LSUM2 = SR_JIT64_V_LSUM, GT2 = SR_JIT64_V_GT, Y2 = SR_JIT64_V_Y;
+constexpr int POOL2 = SR_JIT64_V_POOL0, NPOOL2 = SR_JIT64_V_NPOOL;
+constexpr int T_TILE = SR_JIT64_S_TILE, T_NT = SR_JIT64_S_NT, T_PARTIAL = SR_JIT64_S_PARTIAL;
+constexpr int T_TILEBYTES = SR_JIT64_S_TILEBYTES, T_WOFF = SR_JIT64_S_WOFF, T_STATUS = SR_JIT64_S_STATUS;
+constexpr int T_RR = SR_JIT64_S_RR, T_TGT = SR_JIT64_S_TGT, T_RT = SR_JIT64_S_RT, T_K = SR_JIT64_S_K;
+constexpr int T_PE = SR_JIT64_S_PE, T_BASE = SR_JIT64_S_BASE, T_KH = SR_JIT64_S_KH;
+constexpr int T_C = 20;  // s[20:21]: the Float64 constant of an inline operator (a routine temporary)
+constexpr int kNum64 = SR_JIT64_NUM_ROUTINES;
+const int kUop64[SRHIP_NUM_UOPS] = SR_JIT64_UOP_ROUTINE;
+const int kBop64[SRHIP_NUM_BOPS] = SR_JIT64_BOP_ROUTINE;
+const int kBop64RC[SRHIP_NUM_BOPS] = SR_JIT64_BOP_ROUTINE_RC;
+const int kBop64LC[SRHIP_NUM_BOPS] = SR_JIT64_BOP_ROUTINE_LC;
+const char* const kName64[kNum64] = SR_JIT64_ROUTINE_NAMES;
+
+// gfx950 encodings used here and not by jit.cpp (checked against llvm-mc by tests/test_jit.py)
+enum : int {
+  VOP3_FMA_F64 = 0x1cc, VOP3_ADD_F64 = 0x280, VOP3_MUL_F64 = 0x281, VOPC_U_F64 = 0x68,
+  VOP1_MOV = 0x01, VOP2_CNDMASK = 0x00, VOP2_AND_B32 = 0x13, VOP2_XOR_B32 = 0x15, VOP2_ADD_U32 = 0x34,
+  VOP3P_MOV_B32 = 0x33, VOPC_GT_I32 = 0xc4,
+  SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
+  SOP2_ADD_U32 = 0x00, SOP2_SUB_I32 = 0x03, SOP2_ADDC_U32 = 0x04,
+  SOPC_EQ_U32 = 0x06, SOPC_GE_U32 = 0x09, SOPC_LT_U32 = 0x0a,
+  SOPP_BRANCH = 0x02, SOPP_SCC0 = 0x04, SOPP_SCC1 = 0x05, SOPP_VCCNZ = 0x07,
+};
+
+// ---- the template ------------------------------------------------------------------
+struct Tmpl64 {
+  const uint8_t* img = nullptr;
+  size_t size = 0, area_off = 0, area_bytes = 0;
+  uint64_t area_va = 0, rt0 = 0;
+  uint64_t rt_va[kNum64] = {};
+  bool ok = false;
+  std::string why;
+};
+
+bool parse_tmpl64(const uint8_t* img, size_t size, Tmpl64* t) {
+  t->img = img;
+  t->size = size;
+  if (size < sizeof(Elf64_Ehdr)) { t->why = "template too small"; return false; }
+  Elf64_Ehdr eh;
+  std::memcpy(&eh, img, sizeof(eh));
+  if (std::memcmp(eh.e_ident, ELFMAG, SELFMAG) != 0 || eh.e_shoff + (size_t)eh.e_shnum * sizeof(Elf64_Shdr) > size) {
+    t->why = "template is not an ELF64 image";
+    return false;
+  }
+  std::vector<Elf64_Shdr> sh(eh.e_shnum);
+  std::memcpy(sh.data(), img + eh.e_shoff, sh.size() * sizeof(Elf64_Shdr));
+  const Elf64_Shdr* symtab = nullptr;
+  for (auto& s : sh)
+    if (s.sh_type == SHT_SYMTAB) symtab = &s;
+  if (!symtab || symtab->sh_link >= sh.size()) { t->why = "template has no symbol table"; return false; }
+  const Elf64_Shdr& strtab = sh[symtab->sh_link];
+  uint64_t code_va = 0, area_fn_va = 0, area_fn_size = 0;
+  int found = 0;
+  for (size_t i = 0; i < symtab->sh_size / sizeof(Elf64_Sym); ++i) {
+    Elf64_Sym sym;
+    std::memcpy(&sym, img + symtab->sh_offset + i * sizeof(Elf64_Sym), sizeof(sym));
+    if (sym.st_name >= strtab.sh_size) continue;
+    const std::string n(reinterpret_cast<const char*>(img + strtab.sh_offset + sym.st_name));
+    if (n == "sr_jit64_code") { code_va = sym.st_value; found |= 1; }
+    else if (n == "sr_jit64_area") { area_fn_va = sym.st_value; area_fn_size = sym.st_size; found |= 2; }
+    else if (n == "sr_rt64") { t->rt0 = sym.st_value; found |= 4; }
+    else if (n.rfind("sr_rt64_", 0) == 0) {
+      for (int k = 0; k < kNum64; ++k)
+        if (n.compare(8, std::string::npos, kName64[k]) == 0) t->rt_va[k] = sym.st_value;
+    }
+  }
+  if (found != 7) { t->why = "template symbols missing"; return false; }
+  for (int k = 0; k < kNum64; ++k)
+    if (!t->rt_va[k]) { t->why = std::string("routine missing: ") + kName64[k]; return false; }
+  const Elf64_Shdr* text = nullptr;
+  for (auto& s : sh)
+    if (s.sh_type == SHT_PROGBITS && (s.sh_flags & SHF_EXECINSTR) && code_va >= s.sh_addr &&
+        code_va < s.sh_addr + s.sh_size)
+      text = &s;
+  if (!text) { t->why = "code area outside .text"; return false; }
+  t->area_va = code_va;
+  t->area_off = (size_t)(code_va - text->sh_addr + text->sh_offset);
+  const uint64_t end = area_fn_va + area_fn_size;
+  if (end <= code_va + 64 || end > text->sh_addr + text->sh_size) { t->why = "bad area size"; return false; }
+  t->area_bytes = (size_t)(end - code_va) - 64;
+  if (t->area_off + t->area_bytes > size) { t->why = "area beyond the image"; return false; }
+  t->ok = true;
+  return true;
+}
+
+const Tmpl64& tmpl64() {
+  static Tmpl64 T;
+  static std::once_flag once;
+  std::call_once(once, [] { parse_tmpl64(srhip_jit64_tmpl, (size_t)(srhip_jit64_tmpl_end - srhip_jit64_tmpl), &T); });
+  return T;
+}
+
+// ---- IR ------------------------------------------------------------------------------
+enum { Q_VAL = 0, Q_X = 1, Q_C = 2 };
+struct Q {
+  int k = Q_VAL;
+  int v = -1;      // value id or feature
+  uint64_t c = 0;  // constant bits
+};
+struct Op64 {
+  bool un = false;
+  int op = 0;
+  Q a, b;
+  int rid = -1, krid = -1;  // routine; constant-operand variant (constant in s_k : s_kh)
+};
+
+bool inline64(const Op64& o) {
+  return o.un ? (o.op == SRHIP_UOP_NEG || o.op == SRHIP_UOP_ABS || o.op == SRHIP_UOP_SQUARE || o.op == SRHIP_UOP_CUBE)
+              : (o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_SUB || o.op == SRHIP_BOP_MUL);
+}
+
+bool build_ir64(const Ins<double>* p, std::vector<Op64>& ops, Q& root) {
+  ops.clear();
+  Q acc, tmp, slot[kMaxSlots];
+  for (int pc = 0;; ++pc) {
+    if (pc > 4096) return false;
+    const uint32_t code = p[pc].code;
+    const int opc = (int)(code & 0xffu);
+    const int f = (int)(code >> 16);
+    uint64_t bits;
+    std::memcpy(&bits, &p[pc].imm, 8);
+    auto X = [&](int ff) { Q q; q.k = Q_X; q.v = ff; return q; };
+    auto C = [&]() { Q q; q.k = Q_C; q.c = bits; return q; };
+    auto val = [&](const Op64& o) { ops.push_back(o); Q q; q.k = Q_VAL; q.v = (int)ops.size() - 1; return q; };
+    if (opc == OP_END) { root = acc; return true; }
+    if (opc == OP_LDX) { acc = X(f); continue; }
+    if (opc == OP_LDC) { acc = C(); continue; }
+    if (opc >= OP_PUSH0 && opc < OP_PUSH0 + kMaxSlots) { slot[opc - OP_PUSH0] = acc; continue; }
+    if (opc >= OP_POP0 && opc < OP_POP0 + kMaxSlots) { tmp = slot[opc - OP_POP0]; continue; }
+    if (opc >= OP_UN0 && opc < OP_BIN0) {
+      if (acc.k == Q_C) return false;
+      Op64 o;
+      o.un = true;
+      o.op = opc - OP_UN0;
+      o.a = acc;
+      acc = val(o);
+      continue;
+    }
+    const int v = (opc - OP_BIN0) / SRHIP_NUM_BOPS;
+    Op64 o;
+    o.op = (opc - OP_BIN0) % SRHIP_NUM_BOPS;
+    switch (v) {
+      case V_AX: o.a = acc; o.b = X(f); break;
+      case V_XA: o.a = X(f); o.b = acc; break;
+      case V_AC: o.a = acc; o.b = C(); break;
+      case V_CA: o.a = C(); o.b = acc; break;
+      case V_AT: o.a = acc; o.b = tmp; break;
+      case V_TA: o.a = tmp; o.b = acc; break;
+      case V_XX: o.a = X(f); o.b = X((int)bits); break;
+      case V_XC: o.a = X(f); o.b = C(); break;
+      case V_CX: o.a = C(); o.b = X(f); break;
+      default: return false;
+    }
+    if (o.a.k == Q_C && o.b.k == Q_C) return false;
+    acc = val(o);
+  }
+}
+
+// ---- code generation of one tree -----------------------------------------------------
+struct Gen64 {
+  Asm& as;
+  const Tmpl64& T;
+  uint64_t base_va;
+  std::vector<Op64> ops;
+  Q root;
+  int n = 0;
+  std::vector<int> last, loc;  // last reader of a value (n: the root), its pool block (-1: none)
+  int owner[NPOOL2];           // -1 free, value id, 1000 + feature
+  int xblk[256], xlast[256], load_idx[256];
+  std::vector<int> feats;      // features inline operators read, in first-use order
+  int nloads = 0, waited = 0, max_feat = -1;
+  bool has_call = false;
+  int L_tile = -1, L_done = -1;
+  std::string why;
+
+  Gen64(Asm& a, const Tmpl64& t, uint64_t va) : as(a), T(t), base_va(va) {}
+  uint64_t cur_va() const { return base_va + as.bytes(); }
+  static int blk(int k) { return POOL2 + 4 * k; }
+
+  bool analyze() {
+    n = (int)ops.size();
+    last.assign(n, -1);
+    loc.assign(n, -1);
+    for (int f = 0; f < 256; ++f) { xblk[f] = -1; xlast[f] = -1; load_idx[f] = -1; }
+    auto usef = [&](const Q& q, int i, bool inl) {
+      if (q.k != Q_X) return true;
+      if (q.v < 0 || q.v > 62) { why = "feature offset beyond the DS immediate"; return false; }
+      max_feat = std::max(max_feat, q.v);
+      if (inl) {
+        if (xlast[q.v] < 0) feats.push_back(q.v);
+        xlast[q.v] = std::max(xlast[q.v], i);
+      }
+      return true;
+    };
+    for (int i = 0; i < n; ++i) {
+      Op64& o = ops[i];
+      const bool inl = inline64(o);
+      if (!inl) {
+        if (!o.un && o.b.k == Q_C) o.krid = kBop64RC[o.op];
+        if (!o.un && o.a.k == Q_C) o.krid = kBop64LC[o.op];
+        o.rid = o.un ? kUop64[o.op] : kBop64[o.op];
+        if (o.rid < 0 && o.krid < 0) { why = "operator without a Float64 routine"; return false; }
+        if (o.rid < 0 && !(o.a.k == Q_C || o.b.k == Q_C)) { why = "operator without a Float64 routine"; return false; }
+        has_call = true;
+      }
+      if (!usef(o.a, i, inl)) return false;
+      if (!o.un && !usef(o.b, i, inl)) return false;
+      if (o.a.k == Q_VAL) last[o.a.v] = i;
+      if (!o.un && o.b.k == Q_VAL) last[o.b.v] = i;
+    }
+    if (!usef(root, n, true)) return false;
+    if (root.k == Q_VAL) last[root.v] = n;
+    if ((int)feats.size() > NPOOL2) { why = "more features than register blocks"; return false; }
+    return true;
+  }
+
+  // ---- emission helpers
+  static std::string pr(int r) { return "v[" + std::to_string(r) + ":" + std::to_string(r + 1) + "]"; }
+  static std::string pname(const Src& s) {
+    if (s.enc >= 256) return pr(s.enc - 256);
+    if (s.enc < 102) return "s[" + std::to_string(s.enc) + ":" + std::to_string(s.enc + 1) + "]";
+    return s.enc == 128 ? "0" : s.name();
+  }
+  // VOP3 on Float64 register pairs (neg bit i negates source i)
+  void vop3d(int op, const char* nm, int vdst, const Src& s0, const Src& s1, const Src* s2, int neg) {
+    as.put(0xd0000000u | ((uint32_t)op << 16) | (uint32_t)vdst);
+    as.put(((uint32_t)(neg & 7) << 29) | ((uint32_t)(s2 ? s2->enc : 0) << 18) | ((uint32_t)s1.enc << 9) |
+           (uint32_t)s0.enc);
+    if (!as.want_text) return;
+    auto f = [&](const Src& s, int i) { return ((neg >> i) & 1 ? "-" : "") + pname(s); };
+    as.t(std::string(nm) + " " + pr(vdst) + ", " + f(s0, 0) + ", " + f(s1, 1) + (s2 ? ", " + f(*s2, 2) : ""));
+  }
+  void movd(int dst, int src) {  // one Float64 (a register pair)
+    as.vop3p(VOP3P_MOV_B32, "v_pk_mov_b32", dst, V(src), V(src), nullptr, 2, 7, 0, 0);
+  }
+  void mov_block(int dst, int src) {
+    if (dst == src) return;
+    movd(dst, src);
+    movd(dst + 2, src + 2);
+  }
+  void const_to_s(int sreg, uint64_t bits) {
+    as.sop1(SOP1_MOV, "s_mov_b32", sreg, K((uint32_t)bits), "s" + std::to_string(sreg));
+    as.sop1(SOP1_MOV, "s_mov_b32", sreg + 1, K((uint32_t)(bits >> 32)), "s" + std::to_string(sreg + 1));
+  }
+  void wait_for(int f) {
+    const int li = load_idx[f];
+    if (li >= waited) {
+      as.waitcnt_lgkm(nloads - 1 - li);
+      waited = li + 1;
+    }
+  }
+  void wait_all() {
+    if (waited < nloads) { as.waitcnt_lgkm(0); waited = nloads; }
+  }
+  int free_block() const {
+    for (int k = 0; k < NPOOL2; ++k)
+      if (owner[k] == -1) return k;
+    return -1;
+  }
+  void free_at(int i) {  // values and features whose last reader is step i
+    for (int k = 0; k < NPOOL2; ++k) {
+      const int w = owner[k];
+      if (w >= 0 && w < 1000 && last[w] == i) owner[k] = -1;
+      if (w >= 1000 && xlast[w - 1000] == i) owner[k] = -1;
+    }
+  }
+  // block register of an operand for inline use (-1: a constant, in s[T_C:T_C+1])
+  int opnd_reg(const Q& q) {
+    if (q.k == Q_VAL) return blk(loc[q.v]);
+    if (q.k == Q_X) { wait_for(q.v); return blk(xblk[q.v]); }
+    const_to_s(T_C, q.c);
+    return -1;
+  }
+  // a call operand into block A or B: a value block, a feature from the LDS
+  // tile, or a constant (both rows)
+  void operand_to(int dst, const Q& q) {
+    if (q.k == Q_VAL) { mov_block(dst, blk(loc[q.v])); return; }
+    if (q.k == Q_X) {
+      as.ds_read_b128(dst, LANE2, (1 + q.v) * TILE2 * 8);
+      as.waitcnt_lgkm(0);
+      waited = nloads;
+      return;
+    }
+    const_to_s(T_C, q.c);
+    for (int e = 0; e < 4; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", dst + e, S(T_C + (e & 1)));
+  }
+  void set_base() {
+    as.sop1(SOP1_GETPC, "s_getpc_b64", T_BASE, Src{0, false, 0}, "");
+    if (as.want_text) as.lines.back() = "s_getpc_b64 s[" + std::to_string(T_BASE) + ":" + std::to_string(T_BASE + 1) + "]";
+    const int64_t rel = (int64_t)(T.rt0 - cur_va());
+    as.sop2(SOP2_ADD_U32, "s_add_u32", T_BASE, S(T_BASE), K((uint32_t)(uint64_t)rel));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", T_BASE + 1, S(T_BASE + 1), K((uint32_t)((uint64_t)rel >> 32)));
+  }
+  void routine(int rid) {
+    const uint64_t off = T.rt_va[rid] - T.rt0;
+    as.sop2(SOP2_ADD_U32, "s_add_u32", T_TGT, S(T_BASE), K((uint32_t)off));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", T_TGT + 1, S(T_BASE + 1), K((uint32_t)(off >> 32)));
+    as.sop1(SOP1_SWAPPC, "s_swappc_b64", T_RR, S(T_TGT), "");
+    if (as.want_text)
+      as.lines.back() = "s_swappc_b64 s[" + std::to_string(T_RR) + ":" + std::to_string(T_RR + 1) + "], s[" +
+                        std::to_string(T_TGT) + ":" + std::to_string(T_TGT + 1) + "]";
+  }
+
+  bool emit_inline(int i) {
+    const Op64& o = ops[i];
+    const int ra = opnd_reg(o.a);
+    const int rb = o.un ? 0 : opnd_reg(o.b);
+    free_at(i);
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted"; return false; }
+    const int d = blk(k);
+    for (int e = 0; e < R2; ++e) {
+      const Src a = ra < 0 ? S(T_C) : V(ra + 2 * e);
+      if (o.un) {
+        switch (o.op) {
+          case SRHIP_UOP_NEG:
+          case SRHIP_UOP_ABS:
+            as.vop1(VOP1_MOV, "v_mov_b32_e32", d + 2 * e, V(ra + 2 * e));
+            if (o.op == SRHIP_UOP_NEG) as.vop2(VOP2_XOR_B32, "v_xor_b32_e32", d + 2 * e + 1, K(0x80000000u), ra + 2 * e + 1);
+            else as.vop2(VOP2_AND_B32, "v_and_b32_e32", d + 2 * e + 1, K(0x7fffffffu), ra + 2 * e + 1);
+            break;
+          case SRHIP_UOP_SQUARE: vop3d(VOP3_MUL_F64, "v_mul_f64", d + 2 * e, a, a, nullptr, 0); break;
+          default: {  // CUBE = (x*x)*x
+            const int t = (d == ra) ? GT2 + 2 * e : d + 2 * e;
+            vop3d(VOP3_MUL_F64, "v_mul_f64", t, a, a, nullptr, 0);
+            vop3d(VOP3_MUL_F64, "v_mul_f64", d + 2 * e, V(t), a, nullptr, 0);
+          }
+        }
+      } else {
+        const Src b = rb < 0 ? S(T_C) : V(rb + 2 * e);
+        switch (o.op) {
+          case SRHIP_BOP_ADD: vop3d(VOP3_ADD_F64, "v_add_f64", d + 2 * e, a, b, nullptr, 0); break;
+          case SRHIP_BOP_SUB: vop3d(VOP3_ADD_F64, "v_add_f64", d + 2 * e, a, b, nullptr, 2); break;
+          default: vop3d(VOP3_MUL_F64, "v_mul_f64", d + 2 * e, a, b, nullptr, 0);
+        }
+      }
+    }
+    owner[k] = i;
+    loc[i] = k;
+    return true;
+  }
+
+  bool emit_call(int i) {
+    const Op64& o = ops[i];
+    if (o.krid >= 0) {  // one constant operand: in s_k : s_kh
+      const bool rc = o.b.k == Q_C;
+      operand_to(A2, rc ? o.a : o.b);
+      const uint64_t c = rc ? o.b.c : o.a.c;
+      as.sop1(SOP1_MOV, "s_mov_b32", T_K, K((uint32_t)c), "s" + std::to_string(T_K));
+      as.sop1(SOP1_MOV, "s_mov_b32", T_KH, K((uint32_t)(c >> 32)), "s" + std::to_string(T_KH));
+      free_at(i);
+      routine(o.krid);
+    } else {
+      operand_to(A2, o.a);
+      if (!o.un) operand_to(B2, o.b);
+      free_at(i);
+      routine(o.rid);
+    }
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted"; return false; }
+    mov_block(blk(k), A2);
+    owner[k] = i;
+    loc[i] = k;
+    return true;
+  }
+
+  // rows past the last of the last tile: 0 in block `reg`
+  void emit_mask(int reg) {
+    const int L_nomask = as.label();
+    as.sop2(SOP2_ADD_U32, "s_add_u32", T_PE, S(T_TILE), K(1));
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(T_PE), S(T_NT));
+    as.branch(SOPP_SCC0, "s_cbranch_scc0", L_nomask);
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(T_PARTIAL), K((uint32_t)TILE2));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_nomask);
+    for (int e = 0; e < R2; ++e) {
+      as.sop2(SOP2_SUB_I32, "s_sub_i32", T_PE, S(T_PARTIAL), K((uint32_t)e));
+      as.vopc(VOPC_GT_I32, "v_cmp_gt_i32_e32", S(T_PE), LROW2);
+      as.sopp(0x00, "s_nop", 1);  // VALU-written VCC read as a VALU mask
+      as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", reg + 2 * e, K(0), reg + 2 * e, ", vcc");
+      as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", reg + 2 * e + 1, K(0), reg + 2 * e + 1, ", vcc");
+    }
+    as.bind(L_nomask);
+  }
+
+  bool emit_tree() {
+    if (!analyze()) return false;
+    L_tile = as.label();
+    L_done = as.label();
+    as.sop1(SOP1_MOV, "s_mov_b32", T_STATUS, K(0), "s" + std::to_string(T_STATUS));
+    if (has_call) set_base();
+    as.sopc(SOPC_GE_U32, "s_cmp_ge_u32", S(T_TILE), S(T_NT));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_done);
+    // ---- tile
+    as.bind(L_tile);
+    for (int k = 0; k < NPOOL2; ++k) owner[k] = -1;
+    nloads = 0;
+    waited = 0;
+    as.ds_read_b128(Y2, LANE2, 0);
+    ++nloads;
+    for (size_t j = 0; j < feats.size(); ++j) {
+      const int f = feats[j];
+      xblk[f] = (int)j;
+      owner[j] = 1000 + f;
+      load_idx[f] = nloads++;
+      as.ds_read_b128(blk((int)j), LANE2, (1 + f) * TILE2 * 8);
+    }
+    std::fill(loc.begin(), loc.end(), -1);
+    for (int i = 0; i < n; ++i) {
+      if (!(inline64(ops[i]) ? emit_inline(i) : emit_call(i))) return false;
+    }
+    // root value → rreg
+    int rreg;
+    if (root.k == Q_VAL) rreg = blk(loc[root.v]);
+    else if (root.k == Q_X) { wait_for(root.v); rreg = blk(xblk[root.v]); }
+    else {
+      const_to_s(T_C, root.c);
+      for (int e = 0; e < 4; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", GT2 + e, S(T_C + (e & 1)));
+      rreg = GT2;
+    }
+    for (int e = 0; e < R2; ++e) {  // chk = fma(v, 0, chk): NaN for a non-finite root value
+      const Src r = V(rreg + 2 * e), z = K(0), c = V(CHK2);
+      vop3d(VOP3_FMA_F64, "v_fma_f64", CHK2, r, z, &c, 0);
+    }
+    wait_all();
+    // residuals r = ŷ - y, masked, squared (weighted) into the lane's sum
+    for (int e = 0; e < R2; ++e) vop3d(VOP3_ADD_F64, "v_add_f64", Y2 + 2 * e, V(rreg + 2 * e), V(Y2 + 2 * e), nullptr, 2);
+    emit_mask(Y2);
+    {
+      const int L_unw = as.label(), L_sum = as.label();
+      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(T_WOFF), K(0));
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
+      as.vop2(VOP2_ADD_U32, "v_add_u32_e32", GT2, S(T_WOFF), LANE2);
+      as.ds_read_b128(GT2, GT2, 0);
+      as.waitcnt_lgkm(0);
+      for (int e = 0; e < R2; ++e) {  // Σ w·(r·r)
+        const Src r = V(Y2 + 2 * e);
+        vop3d(VOP3_MUL_F64, "v_mul_f64", Y2 + 2 * e, r, r, nullptr, 0);
+        const Src w = V(GT2 + 2 * e), t = V(Y2 + 2 * e), l = V(LSUM2);
+        vop3d(VOP3_FMA_F64, "v_fma_f64", LSUM2, w, t, &l, 0);
+      }
+      as.branch(SOPP_BRANCH, "s_branch", L_sum);
+      as.bind(L_unw);
+      for (int e = 0; e < R2; ++e) {
+        const Src r = V(Y2 + 2 * e), l = V(LSUM2);
+        vop3d(VOP3_FMA_F64, "v_fma_f64", LSUM2, r, r, &l, 0);
+      }
+      as.bind(L_sum);
+    }
+    // a failed tile ends the tree
+    as.put(0x7c000000u | ((uint32_t)VOPC_U_F64 << 17) | ((uint32_t)CHK2 << 9) | (uint32_t)(256 + CHK2));
+    if (as.want_text) as.t("v_cmp_u_f64_e32 vcc, " + pr(CHK2) + ", " + pr(CHK2));
+    as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
+    // ---- next tile
+    as.vop2(VOP2_ADD_U32, "v_add_u32_e32", LANE2, S(T_TILEBYTES), LANE2);
+    as.sop2(SOP2_ADD_U32, "s_add_u32", T_TILE, S(T_TILE), K(1));
+    as.sopc(SOPC_LT_U32, "s_cmp_lt_u32", S(T_TILE), S(T_NT));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_tile);
+    as.bind(L_done);
+    as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(T_RT), "");
+    if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(T_RT) + ":" + std::to_string(T_RT + 1) + "]";
+    return true;
+  }
+};
+
+bool gen_tree64(const Ins<double>* prog, const Tmpl64& T, bool text, std::vector<uint32_t>& out,
+                std::vector<std::string>* lines, int32_t* off, int* max_feat, std::string* why) {
+  std::vector<Op64> ir;
+  Q root;
+  if (!build_ir64(prog, ir, root)) { *why = "program not translatable"; return false; }
+  const size_t start = (out.size() + 15) / 16 * 16;  // 64-byte aligned entries
+  Asm as;
+  as.want_text = text;
+  Gen64 g(as, T, T.area_va + start * 4);
+  g.ops = ir;
+  g.root = root;
+  if (!g.emit_tree()) { *why = g.why; return false; }
+  as.finish();
+  while (out.size() < start) {
+    out.push_back(0xbf800000u);
+    if (lines) lines->push_back("s_nop 0");
+  }
+  out.insert(out.end(), as.w.begin(), as.w.end());
+  if (lines) {
+    lines->push_back("; tree code at " + std::to_string(start * 4));
+    lines->insert(lines->end(), as.lines.begin(), as.lines.end());
+  }
+  *off = (int32_t)(start * 4);
+  *max_feat = std::max(*max_feat, g.max_feat);
+  return true;
+}
+
+// Trees that compile are appended to ok_trees / offs, the others to `rest`; a
+// tree that no longer fits in the area ends the call (returns its position).
+size_t codegen64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, size_t from, bool text,
+                 std::vector<uint32_t>& words, std::vector<std::string>* lines, std::vector<int32_t>& offs,
+                 std::vector<int32_t>& ok_trees, std::vector<int32_t>& rest, int* max_feat, Stats* st) {
+  const Tmpl64& T = tmpl64();
+  for (size_t k = from; k < cand.size(); ++k) {
+    const int32_t t = cand[k];
+    int32_t off = -1;
+    std::string why;
+    const size_t before = words.size(), lbefore = lines ? lines->size() : 0;
+    int mf = *max_feat;
+    const bool okc = cb.tree_off[t] >= 0 && gen_tree64(&cb.code[cb.tree_off[t]], T, text, words, lines, &off, &mf, &why);
+    if (okc && words.size() * 4 > T.area_bytes) {
+      words.resize(before);
+      if (lines) lines->resize(lbefore);
+      return k;
+    }
+    if (okc) {
+      *max_feat = mf;
+      ok_trees.push_back(t);
+      offs.push_back(off);
+      if (st) st->ntrees++;
+    } else {
+      words.resize(before);
+      if (lines) lines->resize(lbefore);
+      rest.push_back(t);
+      if (st) st->nrejected++;
+      static const bool dbg = std::getenv("SRHIP_JIT_DEBUG") != nullptr;
+      if (dbg) std::fprintf(stderr, "jit64: tree %d not compiled: %s\n", t, why.c_str());
+    }
+  }
+  return cand.size();
+}
+
+struct Jit64Args {
+  EvalArgs<double> e;
+  const int32_t* code_off;
+  int nraw;
+};
+
+}  // namespace
+
+struct Part64 {
+  hipModule_t mod = nullptr;
+  hipFunction_t fn = nullptr, fn_w = nullptr;
+  int32_t* d_off = nullptr;
+  int slot0 = 0, nslots = 0;
+};
+struct Module64 {
+  std::vector<Part64> parts;
+  int nslots = 0;
+  int nraw = 0;
+};
+
+bool available64() { return tmpl64().ok; }
+
+Module64* build64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list,
+                  std::vector<int32_t>& rest, Stats* st) {
+  const Tmpl64& T = tmpl64();
+  if (!T.ok) { rest = cand; return nullptr; }
+  const auto t0 = std::chrono::steady_clock::now();
+  struct Chunk { std::vector<uint32_t> words; std::vector<int32_t> offs, slots; };
+  std::vector<Chunk> chunks;
+  int max_feat = -1;
+  size_t pos = 0, bytes = 0;
+  constexpr int kMaxParts64 = 8;
+  while (pos < cand.size()) {
+    Chunk ch;
+    const size_t next = codegen64(cb, cand, pos, false, ch.words, nullptr, ch.offs, ch.slots, rest, &max_feat, st);
+    if (next == pos) { rest.push_back(cand[pos]); if (st) st->nrejected++; pos = next + 1; continue; }
+    if ((int)chunks.size() + 1 == kMaxParts64 && next < cand.size()) {
+      for (size_t k = next; k < cand.size(); ++k) rest.push_back(cand[k]);
+      if (st) st->nrejected += (int)(cand.size() - next);
+      pos = cand.size();
+    } else {
+      pos = next;
+    }
+    if (ch.slots.empty()) continue;
+    bytes += ch.words.size() * 4;
+    chunks.push_back(std::move(ch));
+  }
+  if (chunks.empty()) return nullptr;
+  const auto t1 = std::chrono::steady_clock::now();
+  Module64* m = new Module64();
+  m->nraw = max_feat + 1;
+  try {
+    for (Chunk& ch : chunks) {
+      Part64 pt;
+      pt.slot0 = m->nslots;
+      pt.nslots = (int)ch.slots.size();
+      m->parts.push_back(pt);
+      Part64& q = m->parts.back();
+      std::vector<uint8_t> img(T.img, T.img + T.size);
+      std::memcpy(img.data() + T.area_off, ch.words.data(), ch.words.size() * 4);
+      HIP_CHECK(hipModuleLoadData(&q.mod, img.data()));
+      HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, "sr_jit64_eval"));
+      HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, "sr_jit64_eval_w"));
+      for (hipFunction_t f : {q.fn, q.fn_w})
+        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      160 * 1024));
+      HIP_CHECK(hipMalloc((void**)&q.d_off, ch.offs.size() * sizeof(int32_t)));
+      HIP_CHECK(hipMemcpy(q.d_off, ch.offs.data(), ch.offs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+      m->nslots += pt.nslots;
+      jit_list.insert(jit_list.end(), ch.slots.begin(), ch.slots.end());
+    }
+  } catch (...) {
+    destroy64(m);
+    throw;
+  }
+  if (st) {
+    st->ms_codegen = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    st->ms_load = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t1).count();
+    st->code_bytes = bytes;
+    st->nparts = (int)chunks.size();
+  }
+  return m;
+}
+
+void destroy64(Module64* m) {
+  if (!m) return;
+  for (Part64& q : m->parts) {
+    if (q.d_off) (void)hipFree(q.d_off);
+    if (q.mod) (void)hipModuleUnload(q.mod);
+  }
+  delete m;
+}
+
+int nparts64(const Module64* m) { return m ? (int)m->parts.size() : 0; }
+void part64(const Module64* m, int k, int* slot0, int* nslots) {
+  *slot0 = m->parts[k].slot0;
+  *nslots = m->parts[k].nslots;
+}
+int nraw64(const Module64* m) { return m ? m->nraw : 0; }
+
+hipError_t launch64(Module64* m, int k, const EvalPlan& plan, const EvalArgs<double>& a, hipStream_t stream) {
+  const Part64& q = m->parts[k];
+  if (a.nlist != q.nslots || m->nraw > a.nfeat || plan.tile != TILE2 || plan.threads != 256) return hipErrorInvalidValue;
+  Jit64Args ja;
+  ja.e = a;
+  ja.code_off = q.d_off;
+  ja.nraw = m->nraw;
+  size_t sz = sizeof(ja);
+  void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
+  const size_t narr = 1 + (size_t)m->nraw + (a.w ? 1 : 0);
+  const size_t lds = narr * (size_t)plan.ntiles * (size_t)TILE2 * sizeof(double) + 16;
+  return hipModuleLaunchKernel(a.w ? q.fn_w : q.fn, (unsigned)a.nrg * (unsigned)a.ntg, 1, 1, 256, 1, 1, (unsigned)lds,
+                               stream, nullptr, cfg);
+}
+
+bool compile_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes,
+                    std::string* text, std::vector<int32_t>* offsets) {
+  const Tmpl64& T = tmpl64();
+  if (!T.ok) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("Float64 jit template unavailable: ") + T.why);
+  std::vector<uint32_t> words;
+  std::vector<std::string> lines;
+  std::vector<int32_t> offs, okt, rest;
+  int mf = -1;
+  codegen64(cb, cand, 0, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, &mf, nullptr);
+  if (bytes) {
+    bytes->resize(words.size() * 4);
+    std::memcpy(bytes->data(), words.data(), bytes->size());
+  }
+  if (text) {
+    text->clear();
+    for (auto& l : lines) { *text += l; *text += '\n'; }
+  }
+  if (offsets) {
+    offsets->clear();
+    for (size_t k = 0; k < okt.size(); ++k) {
+      offsets->push_back(okt[k]);
+      offsets->push_back(offs[k]);
+    }
+  }
+  return !okt.empty();
+}
+
+}  // namespace jit
+}  // namespace srhip

@@ -287,11 +287,15 @@ def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bo
     srhip_jit_compile_loss; out: the per-row output code of
     srhip_eval_tree_array): (code bytes, assembly text, {tree id: byte
     offset})."""
-    consts = np.ascontiguousarray(flat.consts, dtype=np.float32)
+    f64 = np.dtype(flat.consts.dtype) == np.float64
+    consts = np.ascontiguousarray(flat.consts, dtype=np.float64 if f64 else np.float32)
     tr = _trees_struct(flat, consts)
     nb, nt, no = C.c_int64(0), C.c_int64(0), C.c_int64(0)
 
     def call(*bufs):
+        if f64:  # the Float64 tree compiler (jit64.cpp)
+            return lib().srhip_jit_compile(C.byref(tr), 8, bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
+                                           C.byref(no))
         if loss is not None:
             return lib().srhip_jit_compile_loss(C.byref(tr), int(grad), int(fast), int(loss.kind), float(loss.param),
                                                 bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2], C.byref(no))

@@ -169,3 +169,24 @@ def test_output_code_equals_llvm_mc(memc):
     assert text.count("global_store_dwordx4") == len(offs)
     assert "s_cmp_lg_u32 s83" not in text  # no FAST verdict
     assert assemble(text) == code
+
+
+F64_OPSETS = [
+    (["+", "-", "*", "/", "^"], ["safe_log", "safe_sqrt", "cos", "exp"]),  # config #3
+    (["+", "-", "*", "/", "max", "min"], ["neg", "abs", "square", "cube", "sin", "tanh", "relu"]),
+]
+
+
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.parametrize("k", range(len(F64_OPSETS)))
+def test_float64_tree_code_equals_llvm_mc(k):
+    """The Float64 tree compiler (csrc/jit64.cpp): same byte check; the
+    shallow trees of config #3's operator set compile."""
+    b_ops, u_ops = F64_OPSETS[k]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    trees = srhip.random_population(300, o, 5, np.float64, seed=51 + k)
+    flat = srhip.flatten(trees, o, dtype=np.float64)
+    code, text, offs = jit_compile(flat)
+    assert len(offs) >= 0.6 * len(trees), f"only {len(offs)} of {len(trees)} trees compiled"
+    assert "v_add_f64" in text or "v_mul_f64" in text
+    assert assemble(text) == code
