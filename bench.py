@@ -78,6 +78,9 @@ def parse():
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
+    ap.add_argument("--shard", default="trees", choices=["trees", "rows"],
+                    help="N > 1: trees split over the ranks (no collective) or rows split over the ranks "
+                         "(every rank all trees, partials all-reduced on the device per step)")
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
     ap.add_argument("--no-cpu", action="store_true")
     ap.add_argument("--no-row-shard", action="store_true",
@@ -139,7 +142,7 @@ def main():
 
     import srhip
     from srhip import constants as K
-    from srhip.distributed import shard_trees
+    from srhip.distributed import DeviceRowShard, shard_range, shard_trees
 
     T = np.float32 if args.dtype == "f32" else np.float64
     options = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
@@ -149,7 +152,13 @@ def main():
     t0 = time.time()
     # the same batch on every rank; rank r evaluates every world-th tree (strong scaling)
     all_trees = srhip.random_population(args.ntrees, options, args.nfeat, T, seed=1000, maxsize=args.maxsize)
-    trees = [all_trees[i] for i in shard_trees(len(all_trees), rank, world)]
+    rows_mode = world > 1 and args.shard == "rows"
+    if rows_mode:  # every tree on rows [rb, re)
+        trees = all_trees
+        rb, re = shard_range(args.rows, rank, world)
+        X, y = np.ascontiguousarray(X[:, rb:re]), np.ascontiguousarray(y[rb:re])
+    else:
+        trees = [all_trees[i] for i in shard_trees(len(all_trees), rank, world)]
     t_gen = time.time() - t0
 
     ctx = srhip.get_context(local_rank)
@@ -159,7 +168,8 @@ def main():
     prog = srhip.Program(ctx, flat, T)
     t_compile = time.time() - t0
     _, total_nodes, _ = prog.info()
-    node_rows = float(total_nodes) * args.rows
+    node_rows = float(total_nodes) * X.shape[1]
+    rshard = DeviceRowShard(prog, ds, options.elementwise_loss) if rows_mode else None
 
     def barrier():
         ctx.sync()
@@ -171,14 +181,17 @@ def main():
     step_ms = []  # per-step wall time of the headline loop (each call returns synchronised)
 
     def timed(p, steps, warmup, record=None):
+        # one step: the loss of every tree on this rank's rows (rows mode: + the
+        # all-reduce of the per-tree partials over the ranks)
+        step = rshard.step if (rshard is not None and p is prog) else (lambda: p.eval_loss(ds, K.LOSS["L2"]))
         for _ in range(warmup):
-            p.eval_loss(ds, K.LOSS["L2"])
+            step()
         barrier()
         kms = []
         t_ = time.perf_counter()
         t_prev = t_
         for _ in range(steps):
-            p.eval_loss(ds, K.LOSS["L2"])
+            step()
             kms.append(ctx.last_kernel_time()[0])
             if record is not None:
                 t_now = time.perf_counter()
@@ -203,7 +216,7 @@ def main():
 
     # secondary: weak scaling (the whole batch on every rank)
     weak = None
-    if world > 1 and not args.no_weak:
+    if world > 1 and not args.no_weak and not rows_mode:
         wprog = srhip.Program(ctx, srhip.flatten(all_trees, options, dtype=T), T)
         _, wnodes, _ = wprog.info()
         w_el, _ = timed(wprog, max(args.steps // 2, 3), 1)
@@ -235,7 +248,7 @@ def main():
         "kernel_ms": k_ms,
     }
     esz = np.dtype(T).itemsize
-    alg_bytes = args.rows * (args.nfeat + 1) * esz + prog.ntrees * 17
+    alg_bytes = X.shape[1] * (args.nfeat + 1) * esz + prog.ntrees * 17
     roof["hbm_algorithmic_GBs"] = alg_bytes / (k_ms * 1e-3) / 1e9
     prof = ROOT / "profiles" / "current_pmc_summary.json"
     if prof.exists():
@@ -250,7 +263,7 @@ def main():
 
     # ---- CPU baseline (oracle, host cores) ----------------------------------------------
     cpu = None
-    if not args.no_cpu:
+    if not args.no_cpu and world == 1:  # rank 0 at N = 1 only
         sys.path.insert(0, str(ROOT / "oracle"))
         import oracle
 
@@ -300,8 +313,11 @@ def main():
             "rows": args.rows,
             "nfeat": args.nfeat,
             "total_nodes_per_gpu": int(total_nodes),
-            "parallelism": f"the {args.ntrees} trees sharded over {world} GPU(s) (strong scaling), "
-                           "no data-path collective",
+            "parallelism": (f"the {args.rows} rows sharded over {world} GPU(s) (strong scaling): every tree on "
+                            "each shard, [Σw·ℓ, failed] per tree + Σw all-reduced on the device (RCCL) each step"
+                            if rows_mode else
+                            f"the {args.ntrees} trees sharded over {world} GPU(s) (strong scaling), "
+                            "no data-path collective"),
         },
         "weak": weak,
         "row_shard": row_shard,

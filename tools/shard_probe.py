@@ -8,7 +8,9 @@ shards, under two partitions:
            (nodes weighted by operator: srhip.distributed.tree_cost).
 Per shard: kernel time (HIP events, median of K calls) and node count. The
 N = 8 step is the slowest shard, so the projected speedup is
-t(4096) / max_r t(shard r). Prints one JSON line."""
+t(4096) / max_r t(shard r). Row shards (every tree on n/N rows, N = 2, 4,
+8; the N > 1 step adds an all-reduce of the per-tree partials) are timed too.
+Prints one JSON line."""
 import json
 import sys
 from pathlib import Path
@@ -33,7 +35,7 @@ def main():
     ctx = srhip.get_context(0)
     ds = srhip.DeviceDataset(ctx, X, y)
 
-    def timed(sub):
+    def timed(sub, ds=ds):
         prog = srhip.Program(ctx, srhip.flatten(sub, o, dtype=np.float32), np.float32)
         _, nodes, _ = prog.info()
         ks, walls = [], []
@@ -55,6 +57,22 @@ def main():
         mx = max(s["wall_ms"] for s in shards)
         out[name] = dict(shards=shards, max_wall_ms=mx, max_kernel_ms=max(s["kernel_ms"] for s in shards),
                          projected_speedup_wall=full["wall_ms"] / mx)
+    # row shards: every tree on rows [r n/N, (r+1) n/N) (the partials then
+    # all-reduced: one [Σ, failed] pair per tree + Σw, 64 KiB at 4096 trees)
+    n = X.shape[1]
+    rows_out = {}
+    for N in (2, 4, 8):
+        rs = range(N) if N == 8 else (0,)
+        sh = []
+        for r in rs:
+            rb, re = r * n // N, (r + 1) * n // N
+            dsr = srhip.DeviceDataset(ctx, np.ascontiguousarray(X[:, rb:re]), np.ascontiguousarray(y[rb:re]))
+            sh.append(timed(trees, dsr))
+            del dsr
+        mx = max(s["wall_ms"] for s in sh)
+        rows_out[str(N)] = dict(shards=sh, max_wall_ms=mx, max_kernel_ms=max(s["kernel_ms"] for s in sh),
+                                projected_speedup_wall_no_allreduce=full["wall_ms"] / mx)
+    out["rows"] = rows_out
     print(json.dumps(out), flush=True)
 
 
