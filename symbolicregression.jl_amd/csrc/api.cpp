@@ -245,6 +245,11 @@ struct srhip_program {
   // built at a loss's first evaluation; null m: that loss runs interpreted
   struct LossJit { int kind; uint64_t bits; jit::Module* m; };
   mutable std::vector<LossJit> jit_loss;
+  // the constants the tree code was built with: the trees of a later loss or
+  // output build are compiled with them, so that every tree folds and fails
+  // statically as in that build (the slot layouts match); memory-constant code
+  // reads the current constants from the programs either way
+  std::vector<unsigned char> jit_consts, gjit_consts;
   jit::Stats jit_stats;
   // tree code is compiled for one constant set: a program whose constants are
   // set again (srhip_program_set_constants) runs on the interpreter
@@ -598,6 +603,7 @@ void build_grad_program(srhip_program* p) {
       if (p->gjit) {
         p->h_gcand = cand;
         p->h_gjl = gjl;
+        p->gjit_consts = p->consts;
       }
       if (p->gjit)
         for (int32_t t : gjl) {
@@ -787,6 +793,7 @@ void build_program(srhip_program* p) {
       if (p->jit) {
         p->nlist_j = (int)jl.size();
         p->h_jit_list = jl;
+        p->jit_consts = p->consts;
         a = jl;
         a.insert(a.end(), rest.begin(), rest.end());
       }
@@ -1062,7 +1069,7 @@ jit::Module* loss_module(const srhip_program* p, int loss, double lparam) {
   tr.kind = p->kind.data();
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
-  tr.consts = p->consts.data();
+  tr.consts = p->jit_consts.data();
   CompiledBatch<float> cb = compile_batch_par<float>(tr);
   jit::Options jo;
   jo.fast = jit_fast_enabled();
@@ -1096,7 +1103,7 @@ jit::Module* out_module(const srhip_program* p) {
   tr.kind = p->kind.data();
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
-  tr.consts = p->consts.data();
+  tr.consts = p->jit_consts.data();
   CompiledBatch<float> cb = compile_batch_par<float>(tr);
   jit::Options jo;
   jo.fast = false;
@@ -1133,7 +1140,7 @@ jit::GradModule* grad_module(srhip_program* p, int loss, double lparam) {
   tr.kind = p->kind.data();
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
-  tr.consts = p->consts.data();
+  tr.consts = p->gjit_consts.data();
   CompiledBatch<float> cb = compile_batch_par<float>(tr, /*grad=*/true);
   std::vector<int32_t> gjl, rest;
   jit::GradStats st;
@@ -2259,7 +2266,7 @@ int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, i
                                int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load) {
   return guarded([&] {
     if (!prog) throw Error(SRHIP_ERR_INVALID, "null program");
-    const bool on = prog->jit != nullptr;
+    const bool on = prog->jit != nullptr || prog->jit64 != nullptr;
     if (out_ntrees) *out_ntrees = on ? prog->nlist_j : 0;
     if (out_nfast) *out_nfast = on ? prog->jit_stats.nfast : 0;
     if (out_code_bytes) *out_code_bytes = on ? (int64_t)prog->jit_stats.code_bytes : 0;

@@ -136,7 +136,9 @@ def test_gradient_tree_code_losses_match_oracle(gpu_ctx, loss):
         assert np.array_equal(ok1, ok0) and w1 == w0
         with np.errstate(invalid="ignore", divide="ignore"):
             rel = np.abs(s1 - s0) / np.abs(s0)
-        assert np.all(rel[ok1 & (s0 != 0)] <= 1e-5), float(np.nanmax(rel[ok1 & (s0 != 0)]))
+        fin = ok1 & np.isfinite(s0) & (s0 != 0)  # a loss can overflow Float32 on a succeeding tree
+        assert np.array_equal(s1[ok1 & ~np.isfinite(s0)], s0[ok1 & ~np.isfinite(s0)], equal_nan=True)
+        assert np.all(rel[fin] <= 1e-5), float(np.nanmax(rel[fin]))
         w64 = np.ones(n) if weights is None else weights.astype(np.float64)
         eps = float(np.finfo(np.float32).eps)
         checked = 0

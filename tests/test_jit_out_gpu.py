@@ -13,6 +13,7 @@ import pytest
 
 import oracle
 import srhip
+from numerics import assert_close_conditioned, output_spread_flat
 from srhip import constants as K
 
 pytestmark = pytest.mark.gpu
@@ -58,10 +59,11 @@ def test_output_tree_code_equals_interpreter(gpu_ctx, opset):
     # against the oracle's Float32 evaluation on the succeeding trees
     ref, rok = oracle.eval_trees(flat, X, np.float32)
     assert np.array_equal(ok1, rok.astype(bool))
-    m = ok1
-    with np.errstate(invalid="ignore"):
-        rel = np.abs(out1[m].astype(np.float64) - ref[m]) / np.maximum(np.abs(ref[m]), 1e-30)
-    assert np.nanmax(rel) < 1e-5 or np.mean(rel > 1e-5) < 1e-6, float(np.nanmax(rel))
+    # condition-aware (numerics.py): per row, cancellations amplify the
+    # per-operator rounding differences (tanh, ^, safe_log in f32) far past 1e-5
+    m = np.flatnonzero(ok1)
+    spread = output_spread_flat(flat, X, np.float32)
+    assert_close_conditioned(out1[m], ref[m], spread[m], rtol=1e-5, atol=1e-6, msg=f"{opset} outputs")
 
 
 def test_output_tree_code_after_new_constants(gpu_ctx):
