@@ -303,7 +303,11 @@ def test_set_constants_in_place(gpu_ctx, T, n):
                 c = (c0 * T(1 + 0.01 * (k + 1)) + T(0.001 * k)).astype(T)
                 prog.set_constants(c)
                 fresh_flat = srhip.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off, c, flat.nodes)
-                fresh = srhip.Program(ctx, fresh_flat, T)  # tree code with the constants compiled in
+                # tree code with the constants compiled in (Float64: a program
+                # with new constants runs interpreted, jit64.cpp literals, so the
+                # fresh one is interpreted too: the same summation order)
+                with _env(SRHIP_JIT="1" if T == np.float32 else "0"):
+                    fresh = srhip.Program(ctx, fresh_flat, T)
                 s1, w1, ok1 = prog.eval_loss(ds, K.LOSS["L2"])
                 s2, w2, ok2 = fresh.eval_loss(ds, K.LOSS["L2"])
                 assert np.array_equal(ok1, ok2)
@@ -313,6 +317,10 @@ def test_set_constants_in_place(gpu_ctx, T, n):
                 for a, b in zip(g1, g2):
                     np.testing.assert_array_equal(np.asarray(a), np.asarray(b))
             st = prog.update_stats()
+            if T == np.float64:  # Float64 tree code: rebuilt once, interpreted from then on
+                assert prog.jit_info()["ntrees"] == 0
+                assert st["rebuilt"] == (1 if jit0 else 0) and st["inplace"] == (2 if jit0 else 3)
+                continue
             assert prog.jit_info()["ntrees"] == jit0  # still tree code
             if jit0 and memc_env == "0":
                 assert st["rebuilt"] == 1 and st["inplace"] == 2
