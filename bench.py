@@ -11,13 +11,22 @@ compiles every tree to machine code (reported under setup_s / tree_code).
 Metric: node·row evals/sec = Σ_trees count_nodes × rows ÷ wall time
 (nominal count, no credit for early-failed trees).
 
-Multi-GPU (torchrun, one rank per GPU): strong scaling over trees — the same
-4096 trees are split over the N ranks (srhip.distributed.shard_trees, every
-N-th tree), each rank evaluates its share against its own copy of the
-dataset, no collective on the data path. Timing: barrier + sync on both
-sides of the K timed steps, max over ranks; value = the 4096 trees'
-node·rows ÷ that time. A weak-scaling figure (4096 trees on every rank) is
-reported beside it as `weak`.
+Multi-GPU (torchrun, one rank per GPU), strong scaling of the one batch:
+  --shard rows (default) the 1M rows split over the N ranks (contiguous
+      shards), every rank evaluates all 4096 trees on its shard and the
+      per-tree [Σw·ℓ, failed] partials + Σw are all-reduced on the device
+      (RCCL, 64 KiB) each step, so every rank holds every tree's loss — the
+      reference's Dataset split the other way round;
+  --shard trees  every N-th tree per rank (srhip.distributed.shard_trees), no
+      collective on the data path, plus a weak-scaling figure (4096 trees on
+      every rank) as `weak`.
+Rows are the default because every shard then holds the same mix of trees:
+tree shards of 512 differ by up to 1.6x in time at equal node counts (the
+trees whose tiles are redone PRECISE land unevenly; profiles/
+r04_shard_probe.json: max 0.90 ms against 0.58 for the fastest), so the
+slowest rank projects 3.9x at N = 8, against 5.3x for row shards before the
+all-reduce. Timing: barrier + sync on both sides of the K timed steps, max
+over ranks; value = the 4096 trees' node·rows ÷ that time.
 
 cpu_baseline: the oracle/ CPU restatement of the reference algorithm
 (recursive per-node arrays with early exit, fused leaf patterns, separate
@@ -46,6 +55,9 @@ sys.path.insert(0, str(ROOT / "symbolicregression.jl_amd"))
 PEAK_VALU_LANE_OPS = 256 * 4 * 32 * 2.4e9
 METRIC = "node\u00b7row evals/sec (Float32, 4096 trees\u00d71M rows) at 1/2/4/8 GPUs; % VALU peak"
 HBM_PEAK_GBS = 8000.0
+# SRHIP_BENCH_SHARED_GPU=1: every rank on GPU 0 over gloo (rehearsing the N > 1
+# code paths on a one-GPU box; the numbers are not a measurement)
+SHARED_GPU = os.environ.get("SRHIP_BENCH_SHARED_GPU") == "1"
 
 
 def available_cpus() -> int:
@@ -78,7 +90,7 @@ def parse():
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
-    ap.add_argument("--shard", default="trees", choices=["trees", "rows"],
+    ap.add_argument("--shard", default="rows", choices=["trees", "rows"],
                     help="N > 1: trees split over the ranks (no collective) or rows split over the ranks "
                          "(every rank all trees, partials all-reduced on the device per step)")
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
@@ -133,6 +145,11 @@ def main():
 
         if args.stub:
             tdist.init_process_group("gloo")
+        elif SHARED_GPU:
+            # rehearsal of the N > 1 paths on a one-GPU box (tools/gpu_bench_n2.sh):
+            # every rank on GPU 0, gloo, host-side reductions; not a measurement
+            torch.cuda.set_device(0)
+            tdist.init_process_group("gloo")
         else:
             torch.cuda.set_device(local_rank)
             tdist.init_process_group("nccl")
@@ -161,7 +178,7 @@ def main():
         trees = [all_trees[i] for i in shard_trees(len(all_trees), rank, world)]
     t_gen = time.time() - t0
 
-    ctx = srhip.get_context(local_rank)
+    ctx = srhip.get_context(0 if SHARED_GPU else local_rank)
     ds = srhip.DeviceDataset(ctx, X, y)
     flat = srhip.flatten(trees, options, dtype=T)
     t0 = time.time()
@@ -200,13 +217,15 @@ def main():
         barrier()
         return time.perf_counter() - t_, kms
 
+    dev = "cpu" if SHARED_GPU else "cuda"
+
     def reduce_max_sum(elapsed_, node_rows_):
         if not dist:
             return elapsed_, node_rows_
         torch, tdist = dist
-        t = torch.tensor([elapsed_], dtype=torch.float64, device="cuda")
+        t = torch.tensor([elapsed_], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        nr = torch.tensor([node_rows_], dtype=torch.float64, device="cuda")
+        nr = torch.tensor([node_rows_], dtype=torch.float64, device=dev)
         tdist.all_reduce(nr, op=tdist.ReduceOp.SUM)
         return float(t.item()), float(nr.item())
 
@@ -391,7 +410,7 @@ def row_shard_leg(args, world, rank, ctx, dist, barrier):
     vals = [el, float(np.mean(ev)), float(np.mean(red))]
     if dist:
         torch, tdist = dist
-        t = torch.tensor(vals, dtype=torch.float64, device="cuda")
+        t = torch.tensor(vals, dtype=torch.float64, device="cpu" if SHARED_GPU else "cuda")
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         vals = t.tolist()
     el, ev_ms, red_ms = vals
