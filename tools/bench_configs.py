@@ -77,7 +77,8 @@ def main():
         ok = p3.eval_loss(ds3, K.LOSS["L2"])[2]
         emit(config="#3 NaN-heavy F64", what="eval_loss 4096 trees x 100k rows", dtype="f64",
              node_rows_per_s=nodes3 * n3 / k, call_node_rows_per_s=nodes3 * n3 / w, kernel_ms=k * 1e3,
-             did_succeed_rate=float(np.mean(ok)))
+             did_succeed_rate=float(np.mean(ok)), tree_code_trees=p3.jit_info()["ntrees"],
+             ok_sum=int(np.sum(ok)))
         p3o = srhip.Program(ctx, srhip.flatten(t3[:1024], o3, np.float64), np.float64)
         _, nodes3o, _ = p3o.info()
         w, k = timed(ctx, lambda: p3o.eval_tree_array(ds3))

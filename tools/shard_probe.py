@@ -47,7 +47,9 @@ def main():
             if i >= 2:
                 ks.append(ctx.last_kernel_time()[0])
                 walls.append(w)
-        return dict(trees=len(sub), nodes=int(nodes), kernel_ms=float(np.median(ks)), wall_ms=float(np.median(walls)))
+        redone = ctx.last_jit_events()[1]
+        return dict(trees=len(sub), nodes=int(nodes), kernel_ms=float(np.median(ks)), wall_ms=float(np.median(walls)),
+                    redone_tiles=int(redone))
 
     full = timed(trees)
     out = dict(tool="shard_probe", full=full)
@@ -57,6 +59,19 @@ def main():
         mx = max(s["wall_ms"] for s in shards)
         out[name] = dict(shards=shards, max_wall_ms=mx, max_kernel_ms=max(s["kernel_ms"] for s in shards),
                          projected_speedup_wall=full["wall_ms"] / mx)
+    # the same strided shards with every tile PRECISE (SRHIP_JIT_FAST=0, read
+    # per call): if their spread goes, it came from the tiles redone PRECISE
+    import os
+    os.environ["SRHIP_JIT_FAST"] = "0"
+    try:
+        full_p = timed(trees)
+        shards = [timed([trees[i] for i in shard_trees(len(trees), r, world)]) for r in range(world)]
+    finally:
+        del os.environ["SRHIP_JIT_FAST"]
+    mx = max(s["wall_ms"] for s in shards)
+    out["strided_precise"] = dict(full=full_p, shards=shards, max_wall_ms=mx,
+                                  min_wall_ms=min(s["wall_ms"] for s in shards),
+                                  projected_speedup_wall=full_p["wall_ms"] / mx)
     # row shards: every tree on rows [r n/N, (r+1) n/N) (the partials then
     # all-reduced: one [Σ, failed] pair per tree + Σw, 64 KiB at 4096 trees)
     n = X.shape[1]
