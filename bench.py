@@ -12,21 +12,19 @@ Metric: node·row evals/sec = Σ_trees count_nodes × rows ÷ wall time
 (nominal count, no credit for early-failed trees).
 
 Multi-GPU (torchrun, one rank per GPU), strong scaling of the one batch:
-  --shard rows (default) the 1M rows split over the N ranks (contiguous
-      shards), every rank evaluates all 4096 trees on its shard and the
-      per-tree [Σw·ℓ, failed] partials + Σw are all-reduced on the device
-      (RCCL, 64 KiB) each step, so every rank holds every tree's loss — the
-      reference's Dataset split the other way round;
-  --shard trees  every N-th tree per rank (srhip.distributed.shard_trees), no
-      collective on the data path, plus a weak-scaling figure (4096 trees on
-      every rank) as `weak`.
-Rows are the default because every shard then holds the same mix of trees:
-tree shards of 512 differ by up to 1.6x in time at equal node counts (the
-trees whose tiles are redone PRECISE land unevenly; profiles/
-r04_shard_probe.json: max 0.90 ms against 0.58 for the fastest), so the
-slowest rank projects 3.9x at N = 8, against 5.3x for row shards before the
-all-reduce. Timing: barrier + sync on both sides of the K timed steps, max
-over ranks; value = the 4096 trees' node·rows ÷ that time.
+  --shard trees (default) each rank evaluates its share of the 4096 trees
+      against its own copy of the dataset, no collective on the data path;
+      the share is cost-balanced (srhip.distributed.shard_trees_balanced:
+      LPT on the estimated VALU cost; --partition strided: every N-th tree),
+      plus a weak-scaling figure (4096 trees on every rank) as `weak`;
+  --shard rows  the 1M rows split over the N ranks, every rank evaluates all
+      trees on its shard and the per-tree [Σw·ℓ, failed] partials + Σw are
+      all-reduced on the device (RCCL, 64 KiB) each step.
+Measured on one GPU at the N = 8 sizes (profiles/r04_shard_probe_c.json):
+slowest balanced tree shard 0.659 ms, strided 0.685, row shard 0.676 before
+its all-reduce, against 3.53 ms for the whole batch (5.35x / 5.15x / 5.2x).
+Timing: barrier + sync on both sides of the K timed steps, max over ranks;
+value = the 4096 trees' node·rows ÷ that time.
 
 cpu_baseline: the oracle/ CPU restatement of the reference algorithm
 (recursive per-node arrays with early exit, fused leaf patterns, separate
@@ -90,7 +88,9 @@ def parse():
     ap.add_argument("--dtype", default="f32", choices=["f32", "f64"])
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU baseline sample time")
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
-    ap.add_argument("--shard", default="rows", choices=["trees", "rows"],
+    ap.add_argument("--partition", default="balanced", choices=["balanced", "strided"],
+                    help="--shard trees: cost-balanced (LPT) or every N-th tree")
+    ap.add_argument("--shard", default="trees", choices=["trees", "rows"],
                     help="N > 1: trees split over the ranks (no collective) or rows split over the ranks "
                          "(every rank all trees, partials all-reduced on the device per step)")
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")
@@ -159,7 +159,7 @@ def main():
 
     import srhip
     from srhip import constants as K
-    from srhip.distributed import DeviceRowShard, shard_range, shard_trees
+    from srhip.distributed import DeviceRowShard, shard_range, shard_trees, shard_trees_balanced
 
     T = np.float32 if args.dtype == "f32" else np.float64
     options = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
@@ -167,7 +167,7 @@ def main():
     X = rng.standard_normal((args.nfeat, args.rows)).astype(T)
     y = (T(2) * np.cos(X[3 % args.nfeat]) + X[0] * X[0] - T(2)).astype(T)
     t0 = time.time()
-    # the same batch on every rank; rank r evaluates every world-th tree (strong scaling)
+    # the same batch on every rank; rank r evaluates its share of the trees (strong scaling)
     all_trees = srhip.random_population(args.ntrees, options, args.nfeat, T, seed=1000, maxsize=args.maxsize)
     rows_mode = world > 1 and args.shard == "rows"
     if rows_mode:  # every tree on rows [rb, re)
@@ -175,7 +175,9 @@ def main():
         rb, re = shard_range(args.rows, rank, world)
         X, y = np.ascontiguousarray(X[:, rb:re]), np.ascontiguousarray(y[rb:re])
     else:
-        trees = [all_trees[i] for i in shard_trees(len(all_trees), rank, world)]
+        part = (shard_trees_balanced(all_trees, options, rank, world) if args.partition == "balanced"
+                else shard_trees(len(all_trees), rank, world))
+        trees = [all_trees[i] for i in part]
     t_gen = time.time() - t0
 
     ctx = srhip.get_context(0 if SHARED_GPU else local_rank)
@@ -289,27 +291,32 @@ def main():
         threads = args.cpu_threads or available_cpus()
         fl = srhip.flatten(trees, options, dtype=T)
 
-        def run_cpu(nrows, variant="simd"):
+        def run_cpu(nrows, variant="simd", reps=1):
             t_ = time.perf_counter()
-            oracle.eval_loss_batch(fl, X[:, :nrows], y[:nrows], dtype=T, nthreads=threads, variant=variant)
-            return time.perf_counter() - t_, float(fl.nodes.sum()) * nrows
+            for _ in range(reps):
+                oracle.eval_loss_batch(fl, X[:, :nrows], y[:nrows], dtype=T, nthreads=threads, variant=variant)
+            return time.perf_counter() - t_, float(fl.nodes.sum()) * nrows * reps
 
         probe = min(args.rows, 10_000)
         dt, nr = run_cpu(probe)
         nrows = int(min(args.rows, max(probe, probe * args.cpu_seconds / max(dt, 1e-3))))
-        dt, nr = run_cpu(nrows)
+        # the whole workload in less than the target time: repeated, so the
+        # sample is about --cpu-seconds of CPU work
+        reps = max(1, int(round(args.cpu_seconds / max(dt * nrows / probe, 1e-3)))) if nrows == args.rows else 1
+        dt, nr = run_cpu(nrows, reps=reps)
         cpu = {
             "value": nr / dt,
             "unit": "node·row/s",
             "cores": threads,
             "kind": "port",
-            "sample": f"all {len(trees)} trees x first {nrows} rows; oracle simd build (turbo=true analogue), "
+            "sample": f"all {len(trees)} trees x first {nrows} rows" + (f", {reps} passes" if reps > 1 else "") +
+                      "; oracle simd build (turbo=true analogue), "
                       f"OpenMP over trees on {threads} threads (the CPUs this job may use: {cpu_note()}); "
                       f"{dt:.1f} s",
         }
         # turbo=false analogue (scalar build) on the same rows
-        dts, nrs = run_cpu(nrows, "scalar")
-        cpu["turbo_false"] = {"value": nrs / dts, "sample": f"same {nrows} rows; oracle scalar build; {dts:.1f} s"}
+        dts, nrs = run_cpu(nrows, "scalar", reps=reps)
+        cpu["turbo_false"] = {"value": nrs / dts, "sample": f"same {nrows} rows x {reps}; oracle scalar build; {dts:.1f} s"}
 
     out = {
         "metric": METRIC if T == np.float32 else "node·row evals/sec (Float64)",
@@ -335,8 +342,8 @@ def main():
             "parallelism": (f"the {args.rows} rows sharded over {world} GPU(s) (strong scaling): every tree on "
                             "each shard, [Σw·ℓ, failed] per tree + Σw all-reduced on the device (RCCL) each step"
                             if rows_mode else
-                            f"the {args.ntrees} trees sharded over {world} GPU(s) (strong scaling), "
-                            "no data-path collective"),
+                            f"the {args.ntrees} trees sharded over {world} GPU(s) ({args.partition}, strong "
+                            "scaling), no data-path collective"),
         },
         "weak": weak,
         "row_shard": row_shard,

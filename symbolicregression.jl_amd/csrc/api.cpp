@@ -673,15 +673,20 @@ void build_grad_program(srhip_program* p) {
   p->grad_stale = false;
 }
 
-// Tree code (jit.cpp) on/off: SRHIP_JIT=0 never, =1 for every Float32
-// program, default for programs of at least 512 shallow trees (loading a code
-// object costs about a millisecond). SRHIP_JIT_FAST=0 keeps the FAST path out.
+// Tree code (jit.cpp, jit64.cpp) on/off: SRHIP_JIT=0 never, =1 for every
+// program, default for programs of at least 256 shallow trees (code generation
+// ~5 µs per tree, loading a code object about a millisecond). The bar was 512
+// until round 4: a 512-tree shard of config #2 (bench.py --shard trees, N = 8)
+// has 509-512 shallow trees — a tree folds to a constant or fails statically —
+// so three of the eight shards ran interpreted at 0.84-0.89 ms against
+// 0.55-0.64 ms for the others (profiles/r04_shard_fast.jsonl).
+// SRHIP_JIT_FAST=0 keeps the FAST path out.
 bool jit_wanted(int nshallow) {
   if (!jit::available() || nshallow == 0) return false;
   const char* e = std::getenv("SRHIP_JIT");
   if (e && e[0] == '0') return false;
   if (e && e[0] == '1') return true;
-  return nshallow >= 512;
+  return nshallow >= 256;
 }
 // Tree code: SRHIP_JIT_CONTIG=1 gives tree group g the contiguous slots
 // [g*tpb, (g+1)*tpb) of the cost-sorted list (its code one contiguous range).
