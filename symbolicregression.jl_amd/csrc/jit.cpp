@@ -1141,6 +1141,7 @@ static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool 
 struct ModulePart {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr, fn_derive = nullptr;
+  hipFunction_t fn_dl = nullptr, fn_dlw = nullptr;  // the hand-written tree loop (sr_jit_eval_dl), L2 / literal code
   int32_t* d_off = nullptr;  // [nslots] code offsets
   int slot0 = 0, nslots = 0;
 };
@@ -1383,11 +1384,16 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       } else {
         HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, opt.memc ? "sr_jit_eval_m" : "sr_jit_eval"));
         HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, opt.memc ? "sr_jit_eval_mw" : "sr_jit_eval_w"));
+        if (!opt.memc) {
+          HIP_CHECK(hipModuleGetFunction(&q.fn_dl, q.mod, "sr_jit_eval_dl"));
+          HIP_CHECK(hipModuleGetFunction(&q.fn_dlw, q.mod, "sr_jit_eval_dlw"));
+        }
       }
       HIP_CHECK(hipModuleGetFunction(&q.fn_derive, q.mod, "sr_jit_derive"));
-      for (hipFunction_t f : {q.fn, q.fn_w})
-        HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
-                                      160 * 1024));
+      for (hipFunction_t f : {q.fn, q.fn_w, q.fn_dl, q.fn_dlw})
+        if (f)
+          HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
+                                        160 * 1024));
       HIP_CHECK(hipMalloc((void**)&q.d_off, ch.offs.size() * sizeof(int32_t)));
       HIP_CHECK(hipMemcpy(q.d_off, ch.offs.data(), ch.offs.size() * sizeof(int32_t), hipMemcpyHostToDevice));
       m->nslots += pt.nslots;
@@ -1472,11 +1478,20 @@ hipError_t reset_flags(Module* m, hipStream_t stream) {
   return hipMemsetAsync(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t), stream);
 }
 
-// waves take their trees from an LDS counter (jit_template.hip next_tree);
-// SRHIP_JIT_DYNAMIC=0: the static deal
-bool dynamic_trees() {
-  static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_DYNAMIC"); return !(e && e[0] == '0'); }();
-  return on;
+// (reserved: JitArgs::dyn)
+bool dynamic_trees() { return false; }
+
+// Loss tree code of literal-constant programs runs under sr_jit_eval_dl(w),
+// whose tree loop is hand-written (jit_template.hip SR_JIT_LOOP_TEXT): the
+// waves of a workgroup take their trees from an LDS counter, so the workgroup
+// is not held by the wave that drew the costly trees (or the trees whose tiles
+// are redone PRECISE). Same sums bit for bit (wave_sum's order); config #2
+// 3.597 → 3.244 ms, its 125k-row shard 0.640 → 0.568, a 512-tree shard
+// 0.557 → 0.529 (profiles/r04_dynloop.jsonl, tools/dynloop_check.py).
+// SRHIP_JIT_DYNLOOP=0 (read per launch): the compiled static loop.
+static bool dynloop() {
+  const char* e = std::getenv("SRHIP_JIT_DYNLOOP");
+  return !(e && e[0] == '0');
 }
 
 hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, const float* dcols,
@@ -1512,8 +1527,10 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   // LDS: the row tiles (+ the partials when part_lds)
   const size_t narr = 1 + (size_t)(ja.nraw + ja.nder) + (a.w ? 1 : 0);
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + (ja.part_lds ? part_bytes : 0) + 16;
-  return hipModuleLaunchKernel(a.w ? q.fn_w : q.fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds + pad,
-                               stream, nullptr, cfg);
+  // the hand-written loop keeps its tree counter in the last 16 bytes
+  hipFunction_t fn = a.w ? q.fn_w : q.fn;
+  if (q.fn_dl && !m->out && !m->memc && dynloop()) fn = a.w ? q.fn_dlw : q.fn_dl;
+  return hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds + pad, stream, nullptr, cfg);
 }
 
 }  // namespace jit

@@ -86,7 +86,9 @@ __device__ __forceinline__ void jit64_eval_body(const Jit64Args& ja) {
       "s_getpc_b64 s[88:89]\n"
       "s_add_u32 s88, s88, sr_jit64_code@rel32@lo+4\n"
       "s_addc_u32 s89, s89, sr_jit64_code@rel32@hi+12"
-      : "={s[88:89]}"(area));
+      : "={s[88:89]}"(area)
+      :
+      : "scc");  // s_add / s_addc: a carry chain of the compiler must not span this
   const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) double*)sX) +
                             (uint32_t)lane * 16u;
   const uint32_t tilebytes = (uint32_t)(narr * TILE64 * 8);

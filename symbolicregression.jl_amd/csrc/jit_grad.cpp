@@ -1135,6 +1135,7 @@ size_t grad_codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& 
 struct GradPart {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr;
+  hipFunction_t fn_dl = nullptr, fn_dlw = nullptr;  // the hand-written tree loop (sr_jit_grad_dl)
   int32_t* d_off = nullptr;    // [nslots] code offsets
   int32_t* d_cbase = nullptr;  // [nslots] first constant of the slot's tree
   int32_t* d_ncon = nullptr;   // [nslots] its constant count
@@ -1160,7 +1161,9 @@ void load_part(GradPart& pt, const Tmpl& T, const std::vector<uint32_t>& words, 
   HIP_CHECK(hipModuleLoadData(&pt.mod, img.data()));
   HIP_CHECK(hipModuleGetFunction(&pt.fn, pt.mod, "sr_jit_grad"));
   HIP_CHECK(hipModuleGetFunction(&pt.fn_w, pt.mod, "sr_jit_grad_w"));
-  for (hipFunction_t f : {pt.fn, pt.fn_w})
+  HIP_CHECK(hipModuleGetFunction(&pt.fn_dl, pt.mod, "sr_jit_grad_dl"));
+  HIP_CHECK(hipModuleGetFunction(&pt.fn_dlw, pt.mod, "sr_jit_grad_dlw"));
+  for (hipFunction_t f : {pt.fn, pt.fn_w, pt.fn_dl, pt.fn_dlw})
     HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                   160 * 1024));
   const std::pair<int32_t**, const std::vector<int32_t>*> arrays[] = {
@@ -1290,7 +1293,10 @@ hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const
   // LDS: the row tiles only (partials and ∂L/∂c go straight to global memory)
   const size_t narr = 1 + (size_t)a.nfeat + (a.w ? 1 : 0);
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + 16;
-  return hipModuleLaunchKernel(a.w ? pt.fn_w : pt.fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds,
+  // the hand-written tree loop (its counter in the last 16 bytes); SRHIP_JIT_DYNLOOP=0: the compiled one
+  const char* dl = std::getenv("SRHIP_JIT_DYNLOOP");
+  hipFunction_t fn = (dl && dl[0] == '0') ? (a.w ? pt.fn_w : pt.fn) : (a.w ? pt.fn_dlw : pt.fn_dl);
+  return hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds,
                                stream, nullptr, cfg);
 }
 

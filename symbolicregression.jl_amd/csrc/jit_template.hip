@@ -178,7 +178,9 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
       "s_getpc_b64 s[88:89]\n"
       "s_add_u32 s88, s88, sr_jit_code@rel32@lo+4\n"
       "s_addc_u32 s89, s89, sr_jit_code@rel32@hi+12"
-      : "={s[88:89]}"(area));
+      : "={s[88:89]}"(area)
+      :
+      : "scc");  // s_add / s_addc: a carry chain of the compiler must not span this
   const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)sX) +
                             (uint32_t)lane * 16u;
   const uint32_t tilebytes = (uint32_t)(narr * TILE * 4);
@@ -301,6 +303,241 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_mw(JitArgs ja) { 
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_out(JitArgs ja) { jit_eval_body<false, false, true>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { jit_eval_body<false, true, true>(ja); }
 
+// ---- the tree loop as hand-written code (sr_jit_eval_dl, SRHIP_JIT_DYNLOOP) -------
+// The waves of a workgroup take the group's trees from an LDS counter (one
+// ds_add_rtn per tree), so a wave that drew cheap trees takes more and the
+// workgroup ends with its waves together. The loop around the tree calls is
+// written here, not compiled: the compiler only sets up its fixed registers
+// once and never allocates around a tree call (compiled variants of such
+// loops broke the driver). Registers (none of them written by
+// tree code, gen_jit.py SR_JIT_CLOBBERS):
+//   v30 the lane's LDS tile address, v31 the counter's LDS address, v43 lane*R
+//   s40 tpb, s41 ntg, s42 g, s43 ntg-1-g, s44 nlist (slots of this part)
+//   s[46:47] failure flags, s[48:49] code offsets, s[50:51] this group's
+//   global partials, s52 partials in LDS (1) or global (0), s53 their LDS
+//   address, s[54:55] bail flags, s[56:57] counters, s[88:89] the code area,
+//   s65-s68 / s79 / s84 as for the compiled loop; return address s[94:95];
+//   temps s58-s63, s96-s97, v0-v2, v89-v91.
+// Per tree i (slot s = i*ntg + (i odd ? ntg-1-g : g)): a set failure flag
+// skips it (partial {0, NaN}); else its code runs; a bail (s69 != 0) sets the
+// slot's bail flag and counts it; the loss is summed over the wave in the
+// order of interp.h wave_sum; lane 0 stores the partial {Σ, NaN or 0} and, if
+// some row failed, the slot's failure flag (vector stores only).
+#define SR_JIT_LOOP_TEXT                                                              \
+  ".globl sr_jit_loop\n.hidden sr_jit_loop\n.p2align 6\nsr_jit_loop:\n"               \
+  "v_mov_b32_e32 v89, 1\n"                                                            \
+  ".Lsrl_next:\n"                                                                     \
+  "s_mov_b64 s[58:59], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "ds_add_rtn_u32 v90, v31, v89\n"                                                    \
+  "s_waitcnt lgkmcnt(0)\n"                                                            \
+  "s_mov_b64 exec, s[58:59]\n"                                                        \
+  "v_readlane_b32 s60, v90, 0\n"                                                      \
+  "s_cmp_ge_u32 s60, s40\n"                                                           \
+  "s_cbranch_scc1 .Lsrl_done\n"                                                       \
+  "s_mul_i32 s61, s60, s41\n"                                                         \
+  "s_bitcmp1_b32 s60, 0\n"                                                            \
+  "s_cselect_b32 s62, s43, s42\n"                                                     \
+  "s_add_u32 s61, s61, s62\n"                                                         \
+  "s_cmp_ge_u32 s61, s44\n"                                                           \
+  "s_cbranch_scc1 .Lsrl_done\n"                                                       \
+  "s_lshl_b32 s62, s61, 2\n"                                                          \
+  "v_mov_b32_e32 v90, s62\n"                                                          \
+  "global_load_dword v91, v90, s[46:47] sc1\n"                                        \
+  "s_load_dword s63, s[48:49], s62\n"                                                 \
+  "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                                   \
+  "v_readfirstlane_b32 s62, v91\n"                                                    \
+  "s_cmp_lg_u32 s62, 0\n"                                                             \
+  "s_cbranch_scc1 .Lsrl_skip\n"                                                       \
+  "s_add_u32 s96, s88, s63\n"                                                         \
+  "s_addc_u32 s97, s89, 0\n"                                                          \
+  "v_mov_b32_e32 v41, v30\n"                                                          \
+  "v_mov_b32_e32 v42, 0\n"                                                            \
+  "v_mov_b32_e32 v40, 0\n"                                                            \
+  "s_mov_b32 s64, 0\n"                                                                \
+  "s_swappc_b64 s[76:77], s[96:97]\n"                                                 \
+  "v_mov_b32_e32 v89, 1\n"                                                            \
+  "s_cmp_eq_u32 s69, 0\n"                                                             \
+  "s_cbranch_scc1 .Lsrl_sum\n"                                                        \
+  "v_mov_b32_e32 v40, 0x7fc00000\n"                                                   \
+  "s_mov_b64 s[58:59], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "s_lshl_b32 s62, s61, 2\n"                                                          \
+  "v_mov_b32_e32 v90, s62\n"                                                          \
+  "global_store_dword v90, v89, s[54:55] sc1\n"                                       \
+  "v_mov_b32_e32 v90, 0\n"                                                            \
+  "global_atomic_add v90, v89, s[56:57]\n"                                            \
+  "s_mov_b64 exec, s[58:59]\n"                                                        \
+  ".Lsrl_sum:\n"                                                                      \
+  "v_cmp_u_f32_e32 vcc, v40, v40\n"                                                   \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v42, v42 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n"     \
+  "v_mov_b32_e32 v2, 0\n"                                                             \
+  "s_nop 1\n"                                                                         \
+  "v_mov_b32_dpp v2, v1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"                    \
+  "v_add_f32_e32 v1, v1, v2\n"                                                        \
+  "v_mov_b32_e32 v2, 0\n"                                                             \
+  "s_nop 1\n"                                                                         \
+  "v_mov_b32_dpp v2, v1 row_bcast:31 row_mask:0xc bank_mask:0xf\n"                    \
+  "v_add_f32_e32 v1, v1, v2\n"                                                        \
+  "s_nop 1\n"                                                                         \
+  "v_readlane_b32 s62, v1, 63\n"                                                      \
+  "s_cmp_lg_u64 vcc, 0\n"                                                             \
+  "s_cselect_b32 s63, 0x7fc00000, 0\n"                                                \
+  "s_mov_b64 s[58:59], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "v_mov_b32_e32 v0, s62\n"                                                           \
+  "v_mov_b32_e32 v1, s63\n"                                                           \
+  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "s_cmp_eq_u32 s52, 0\n"                                                             \
+  "s_cbranch_scc1 .Lsrl_g1\n"                                                         \
+  "v_mov_b32_e32 v2, s53\n"                                                           \
+  "v_add_u32_e32 v2, s62, v2\n"                                                       \
+  "ds_write_b64 v2, v[0:1]\n"                                                         \
+  "s_branch .Lsrl_st1\n"                                                              \
+  ".Lsrl_g1:\n"                                                                       \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  ".Lsrl_st1:\n"                                                                      \
+  "s_cmp_eq_u32 s63, 0\n"                                                             \
+  "s_cbranch_scc1 .Lsrl_nf\n"                                                         \
+  "s_lshl_b32 s62, s61, 2\n"                                                          \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dword v2, v89, s[46:47] sc1\n"                                        \
+  ".Lsrl_nf:\n"                                                                       \
+  "s_mov_b64 exec, s[58:59]\n"                                                        \
+  "s_branch .Lsrl_next\n"                                                             \
+  ".Lsrl_skip:\n"                                                                     \
+  "s_mov_b64 s[58:59], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "v_mov_b32_e32 v0, 0\n"                                                             \
+  "v_mov_b32_e32 v1, 0x7fc00000\n"                                                    \
+  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "s_cmp_eq_u32 s52, 0\n"                                                             \
+  "s_cbranch_scc1 .Lsrl_g2\n"                                                         \
+  "v_mov_b32_e32 v2, s53\n"                                                           \
+  "v_add_u32_e32 v2, s62, v2\n"                                                       \
+  "ds_write_b64 v2, v[0:1]\n"                                                         \
+  "s_branch .Lsrl_st2\n"                                                              \
+  ".Lsrl_g2:\n"                                                                       \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  ".Lsrl_st2:\n"                                                                      \
+  "s_mov_b64 exec, s[58:59]\n"                                                        \
+  "s_branch .Lsrl_next\n"                                                             \
+  ".Lsrl_done:\n"                                                                     \
+  "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                                   \
+  "s_setpc_b64 s[94:95]\n"
+
+extern "C" __global__ void __launch_bounds__(64) sr_jit_loop_holder() { asm volatile("s_endpgm\n" SR_JIT_LOOP_TEXT); }
+
+template <bool W>
+__device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
+  const EvalArgs<float>& a = ja.e;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* sX = reinterpret_cast<float*>(smem);
+  const int ncol = ja.nraw + ja.nder;
+  const int narr = 1 + ncol + (W ? 1 : 0);
+  const int rows = a.ntiles * TILE;
+  int rg, g;
+  if (!block_of(a, rg, g)) return;
+  const bool tail = rg >= ja.nbig;
+  const int ntl = tail ? ja.ts : a.ntiles;
+  const int64_t row0 = tail ? (int64_t)ja.nbig * rows + (int64_t)(rg - ja.nbig) * ja.ts * TILE : (int64_t)rg * rows;
+  const int nthreads = __builtin_amdgcn_readfirstlane((int)blockDim.x);
+  Part<float>* gdst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
+  Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
+  // the tree counter after the tiles (and the partials): launch() adds 16 bytes
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(sPart) +
+                                              (ja.part_lds ? (size_t)a.tpb * sizeof(Part<float>) : 0));
+  {
+    constexpr int V = TILE / 4;
+    const int total = ntl * narr * V;
+    for (int idx = threadIdx.x; idx < total; idx += nthreads) {
+      const int v = idx % V;
+      const int tk = idx / V;
+      const int k = tk % narr;
+      const int t = tk / narr;
+      if (k > ja.nraw && k <= ncol && ja.dcols) {
+        const float* src = ja.dcols + (size_t)(k - 1 - ja.nraw) * a.n_pad;
+        reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
+            reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
+        continue;
+      }
+      if (k > ja.nraw && k <= ncol) {
+        const uint32_t d = ja.der[k - 1 - ja.nraw];
+        const int op = __builtin_amdgcn_readfirstlane((int)(d >> 16));
+        const float4 x = reinterpret_cast<const float4*>(a.X + (size_t)(d & 0xffffu) * a.n_pad + row0 +
+                                                         (int64_t)t * TILE)[v];
+        reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
+            make_float4(derive_uop(op, x.x), derive_uop(op, x.y), derive_uop(op, x.z), derive_uop(op, x.w));
+        continue;
+      }
+      const float* src = k == 0 ? a.y : (k <= ja.nraw ? a.X + (size_t)(k - 1) * a.n_pad : a.w);
+      reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
+          reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
+    }
+    if (threadIdx.x == 0) *cnt = 0u;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int64_t rem = a.n - row0;
+  const int nt_valid = (int)min((int64_t)ntl, (rem + TILE - 1) / TILE);
+  const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
+  uint64_t area;
+  asm volatile(
+      "s_getpc_b64 s[88:89]\n"
+      "s_add_u32 s88, s88, sr_jit_code@rel32@lo+4\n"
+      "s_addc_u32 s89, s89, sr_jit_code@rel32@hi+12"
+      : "={s[88:89]}"(area)
+      :
+      : "scc");  // s_add / s_addc: a carry chain of the compiler must not span this
+  const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)sX) +
+                            (uint32_t)lane * 16u;
+  const uint32_t cnt_addr = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) uint32_t*)cnt);
+  const uint32_t spart = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) Part<float>*)sPart);
+  const uint32_t tilebytes = (uint32_t)(narr * TILE * 4);
+  const uint32_t woff = W ? (uint32_t)((1 + ncol) * TILE * 4) : 0u;
+  const uint32_t lane4 = (uint32_t)lane * R;
+  const uint32_t partial = (uint32_t)last_valid;
+  const uint32_t nt_u = (uint32_t)nt_valid;
+  const uint32_t fastok = (uint32_t)ja.fast;
+  const uint32_t tpb = (uint32_t)a.tpb, ntg = (uint32_t)a.ntg, gg = (uint32_t)g, g1 = (uint32_t)(a.ntg - 1 - g);
+  const uint32_t nlist = (uint32_t)a.nlist, plds = (uint32_t)ja.part_lds;
+  const uint64_t failp = reinterpret_cast<uint64_t>(a.fail), codep = reinterpret_cast<uint64_t>(ja.code_off);
+  const uint64_t dstp = reinterpret_cast<uint64_t>(gdst), bailp = reinterpret_cast<uint64_t>(ja.bail);
+  const uint64_t cntp = reinterpret_cast<uint64_t>(ja.counters);
+  uint32_t redos = 0;
+  asm volatile(
+      "s_getpc_b64 s[96:97]\n"
+      "s_add_u32 s96, s96, sr_jit_loop@rel32@lo+4\n"
+      "s_addc_u32 s97, s97, sr_jit_loop@rel32@hi+12\n"
+      "s_swappc_b64 s[94:95], s[96:97]"
+      : "+{s84}"(redos)
+      : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+        "{s68}"(woff), "{s79}"(fastok), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
+        "{s[46:47]}"(failp), "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s52}"(plds), "{s53}"(spart),
+        "{s[54:55]}"(bailp), "{s[56:57]}"(cntp), "{s[88:89]}"(area)
+      : SR_JIT_CLOBBERS, "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94", "s95", "s96", "s97",
+        "v40", "v41", "v42", "v89", "v90", "v91", "memory");
+  if (lane == 0 && __builtin_amdgcn_readfirstlane((int)redos) != 0)
+    __hip_atomic_fetch_add(ja.counters + 1, (uint32_t)__builtin_amdgcn_readfirstlane((int)redos),
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (ja.part_lds) {  // slots no wave ran keep whatever: finalize ignores them
+    __syncthreads();
+    for (int i = threadIdx.x; i < a.tpb; i += nthreads) gdst[i] = sPart[i];
+  }
+}
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dl(JitArgs ja) { jit_eval_dl_body<false>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlw(JitArgs ja) { jit_eval_dl_body<true>(ja); }
+
 // ---- gradient tree code (jit_grad.cpp) ---------------------------------------------
 // One workgroup = (row group, tree group) as above; each tree's code runs the
 // forward pass and the reverse (adjoint) pass of every tile, leaves Σ w·ℓ in
@@ -359,7 +596,9 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
       "s_getpc_b64 s[88:89]\n"
       "s_add_u32 s88, s88, sr_jit_code@rel32@lo+4\n"
       "s_addc_u32 s89, s89, sr_jit_code@rel32@hi+12"
-      : "={s[88:89]}"(area));
+      : "={s[88:89]}"(area)
+      :
+      : "scc");  // s_add / s_addc: a carry chain of the compiler must not span this
   const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)sX) +
                             (uint32_t)lane * 16u;
   const uint32_t tilebytes = (uint32_t)(narr * TILE * 4);
@@ -406,3 +645,172 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
 
 extern "C" __global__ void __launch_bounds__(256) sr_jit_grad(JitGradArgs ja) { jit_grad_body<false>(ja); }
 extern "C" __global__ void __launch_bounds__(256) sr_jit_grad_w(JitGradArgs ja) { jit_grad_body<true>(ja); }
+
+// The gradient tree code's loop, hand-written as SR_JIT_LOOP_TEXT (the waves
+// of a workgroup take their trees from an LDS counter). Registers as there,
+// except: s[50:51] the group's partials (global), s[52:53] the slots' first
+// constants (cbase), s[54:55] the constants, s[56:57] this row group's ∂L/∂c
+// partials; per tree s[78:79] = constants + cbase, s[84:85] = partials +
+// cbase (the gradient code's inputs); temps s58-s63, s91, s96-s97, v0-v2,
+// v153-v155 (above the gradient code's registers, gen_jit.py
+// SR_JIT_GRAD_CLOBBERS). No bails and no redo count in gradient code.
+#define SR_JIT_GLOOP_TEXT                                                             \
+  ".globl sr_jit_gloop\n.hidden sr_jit_gloop\n.p2align 6\nsr_jit_gloop:\n"            \
+  "v_mov_b32_e32 v153, 1\n"                                                           \
+  ".Lsrg_next:\n"                                                                     \
+  "s_mov_b64 s[58:59], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "ds_add_rtn_u32 v154, v31, v153\n"                                                  \
+  "s_waitcnt lgkmcnt(0)\n"                                                            \
+  "s_mov_b64 exec, s[58:59]\n"                                                        \
+  "v_readlane_b32 s60, v154, 0\n"                                                     \
+  "s_cmp_ge_u32 s60, s40\n"                                                           \
+  "s_cbranch_scc1 .Lsrg_done\n"                                                       \
+  "s_mul_i32 s61, s60, s41\n"                                                         \
+  "s_bitcmp1_b32 s60, 0\n"                                                            \
+  "s_cselect_b32 s62, s43, s42\n"                                                     \
+  "s_add_u32 s61, s61, s62\n"                                                         \
+  "s_cmp_ge_u32 s61, s44\n"                                                           \
+  "s_cbranch_scc1 .Lsrg_done\n"                                                       \
+  "s_lshl_b32 s62, s61, 2\n"                                                          \
+  "v_mov_b32_e32 v154, s62\n"                                                         \
+  "global_load_dword v155, v154, s[46:47] sc1\n"                                      \
+  "s_load_dword s63, s[48:49], s62\n"                                                 \
+  "s_load_dword s91, s[52:53], s62\n"                                                 \
+  "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                                   \
+  "v_readfirstlane_b32 s62, v155\n"                                                   \
+  "s_cmp_lg_u32 s62, 0\n"                                                             \
+  "s_cbranch_scc1 .Lsrg_skip\n"                                                       \
+  "s_add_u32 s96, s88, s63\n"                                                         \
+  "s_addc_u32 s97, s89, 0\n"                                                          \
+  "s_lshl_b32 s62, s91, 2\n"                                                          \
+  "s_add_u32 s78, s54, s62\n"                                                         \
+  "s_addc_u32 s79, s55, 0\n"                                                          \
+  "s_add_u32 s84, s56, s62\n"                                                         \
+  "s_addc_u32 s85, s57, 0\n"                                                          \
+  "v_mov_b32_e32 v41, v30\n"                                                          \
+  "v_mov_b32_e32 v42, 0\n"                                                            \
+  "v_mov_b32_e32 v40, 0\n"                                                            \
+  "s_mov_b32 s64, 0\n"                                                                \
+  "s_swappc_b64 s[76:77], s[96:97]\n"                                                 \
+  "v_mov_b32_e32 v153, 1\n"                                                           \
+  "v_cmp_u_f32_e32 vcc, v40, v40\n"                                                   \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v42, v42 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n"     \
+  "v_mov_b32_e32 v2, 0\n"                                                             \
+  "s_nop 1\n"                                                                         \
+  "v_mov_b32_dpp v2, v1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"                    \
+  "v_add_f32_e32 v1, v1, v2\n"                                                        \
+  "v_mov_b32_e32 v2, 0\n"                                                             \
+  "s_nop 1\n"                                                                         \
+  "v_mov_b32_dpp v2, v1 row_bcast:31 row_mask:0xc bank_mask:0xf\n"                    \
+  "v_add_f32_e32 v1, v1, v2\n"                                                        \
+  "s_nop 1\n"                                                                         \
+  "v_readlane_b32 s62, v1, 63\n"                                                      \
+  "s_cmp_lg_u64 vcc, 0\n"                                                             \
+  "s_cselect_b32 s63, 0x7fc00000, 0\n"                                                \
+  "s_mov_b64 s[58:59], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "v_mov_b32_e32 v0, s62\n"                                                           \
+  "v_mov_b32_e32 v1, s63\n"                                                           \
+  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  "s_cmp_eq_u32 s63, 0\n"                                                             \
+  "s_cbranch_scc1 .Lsrg_nf\n"                                                         \
+  "s_lshl_b32 s62, s61, 2\n"                                                          \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dword v2, v153, s[46:47] sc1\n"                                       \
+  ".Lsrg_nf:\n"                                                                       \
+  "s_mov_b64 exec, s[58:59]\n"                                                        \
+  "s_branch .Lsrg_next\n"                                                             \
+  ".Lsrg_skip:\n"                                                                     \
+  "s_mov_b64 s[58:59], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "v_mov_b32_e32 v0, 0\n"                                                             \
+  "v_mov_b32_e32 v1, 0x7fc00000\n"                                                    \
+  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  "s_mov_b64 exec, s[58:59]\n"                                                        \
+  "s_branch .Lsrg_next\n"                                                             \
+  ".Lsrg_done:\n"                                                                     \
+  "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                                   \
+  "s_setpc_b64 s[94:95]\n"
+
+extern "C" __global__ void __launch_bounds__(64) sr_jit_gloop_holder() { asm volatile("s_endpgm\n" SR_JIT_GLOOP_TEXT); }
+
+template <bool W>
+__device__ __forceinline__ void jit_grad_dl_body(const JitGradArgs& ja) {
+  const EvalArgs<float>& a = ja.e;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  float* sX = reinterpret_cast<float*>(smem);
+  const int narr = 1 + a.nfeat + (W ? 1 : 0);
+  int rg, g;
+  if (!block_of(a, rg, g)) return;
+  const int rows = a.ntiles * TILE;
+  const int64_t row0 = (int64_t)rg * rows;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(sX + (size_t)narr * rows);  // launch_grad adds 16 bytes
+  {
+    constexpr int V = TILE / 4;
+    const int total = a.ntiles * narr * V;
+    for (int idx = threadIdx.x; idx < total; idx += blockDim.x) {
+      const int v = idx % V;
+      const int tk = idx / V;
+      const int k = tk % narr;
+      const int t = tk / narr;
+      const float* src = k == 0 ? a.y : (k <= a.nfeat ? a.X + (size_t)(k - 1) * a.n_pad : a.w);
+      reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
+          reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
+    }
+    if (threadIdx.x == 0) *cnt = 0u;
+  }
+  __syncthreads();
+
+  const int lane = threadIdx.x & 63;
+  const int64_t rem = a.n - row0;
+  const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE - 1) / TILE);
+  const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
+  uint64_t area;
+  asm volatile(
+      "s_getpc_b64 s[88:89]\n"
+      "s_add_u32 s88, s88, sr_jit_code@rel32@lo+4\n"
+      "s_addc_u32 s89, s89, sr_jit_code@rel32@hi+12"
+      : "={s[88:89]}"(area)
+      :
+      : "scc");  // s_add / s_addc: a carry chain of the compiler must not span this
+  const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) float*)sX) +
+                            (uint32_t)lane * 16u;
+  const uint32_t cnt_addr = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) uint32_t*)cnt);
+  const uint32_t tilebytes = (uint32_t)(narr * TILE * 4);
+  const uint32_t woff = W ? (uint32_t)((1 + a.nfeat) * TILE * 4) : 0u;
+  const uint32_t lane4 = (uint32_t)lane * R;
+  const uint32_t partial = (uint32_t)last_valid;
+  const uint32_t nt_u = (uint32_t)nt_valid;
+  const uint32_t tpb = (uint32_t)a.tpb, ntg = (uint32_t)a.ntg, gg = (uint32_t)g, g1 = (uint32_t)(a.ntg - 1 - g);
+  const uint32_t nlist = (uint32_t)a.nlist;
+  const uint64_t failp = reinterpret_cast<uint64_t>(a.fail), codep = reinterpret_cast<uint64_t>(ja.code_off);
+  const uint64_t dstp = reinterpret_cast<uint64_t>(a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb);
+  const uint64_t cbp = reinterpret_cast<uint64_t>(ja.cbase), constp = reinterpret_cast<uint64_t>(ja.consts);
+  const uint64_t gdstp = reinterpret_cast<uint64_t>(ja.gpart + (size_t)rg * (size_t)ja.nconst);
+  asm volatile(
+      "s_getpc_b64 s[96:97]\n"
+      "s_add_u32 s96, s96, sr_jit_gloop@rel32@lo+4\n"
+      "s_addc_u32 s97, s97, sr_jit_gloop@rel32@hi+12\n"
+      "s_swappc_b64 s[94:95], s[96:97]"
+      :
+      : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+        "{s68}"(woff), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist), "{s[46:47]}"(failp),
+        "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s[52:53]}"(cbp), "{s[54:55]}"(constp), "{s[56:57]}"(gdstp),
+        "{s[88:89]}"(area)
+      : SR_JIT_GRAD_CLOBBERS, "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s78", "s79", "s84", "s85",
+        "s91", "s94", "s95", "s96", "s97", "v40", "v41", "v42", "v153", "v154", "v155", "memory");
+}
+extern "C" __global__ void __launch_bounds__(256) sr_jit_grad_dl(JitGradArgs ja) { jit_grad_dl_body<false>(ja); }
+extern "C" __global__ void __launch_bounds__(256) sr_jit_grad_dlw(JitGradArgs ja) { jit_grad_dl_body<true>(ja); }

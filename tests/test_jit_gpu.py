@@ -1,7 +1,7 @@
 """Tree code (csrc/jit.cpp) on the MI355X against the interpreter and the oracle.
 
 Programs are compiled to machine code when SRHIP_JIT=1 at program creation
-(the default only for >= 512 shallow trees). Checks:
+(the default only for >= 256 shallow trees). Checks:
   * PRECISE routines only (SRHIP_JIT_FAST=0): did_succeed identical to the
     interpreter, losses equal up to the summation grouping (4 vs 8 rows per
     lane: a few ulp of the tree's fp32 partial sums);
@@ -320,3 +320,31 @@ def test_constant_numerator_is_ieee_exact(gpu_ctx, fast):
     s, w, ok, info, _ = run(trees, o, X, y, jit="1", fast=fast)
     assert info["ntrees"] == len(trees) and ok.all()
     assert np.all(s == 0), (c[s != 0], s[s != 0])
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_hand_written_tree_loop_equals_compiled(gpu_ctx, weighted):
+    """The waves' tree loop written by hand with an LDS work counter
+    (jit_template.hip SR_JIT_LOOP_TEXT / SR_JIT_GLOOP_TEXT, the default)
+    against the compiled static deal (SRHIP_JIT_DYNLOOP=0) on the same
+    programs: losses, did_succeed and ∂L/∂c bit for bit (each tree's wave is
+    summed in wave_sum's order either way), FAST path and bails included."""
+    o = srhip.Options(**CFG2)
+    trees = srhip.random_population(700, o, 5, np.float32, seed=41 + weighted)
+    X, y, w = data(5, 50_001, 42, weighted=weighted)
+    ctx = gpu_ctx
+    ds = srhip.DeviceDataset(ctx, X, y, w)
+    with env(SRHIP_JIT="1"):
+        prog = srhip.Program(ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32)
+    res = {}
+    for mode in ("0", "1"):
+        with env(SRHIP_JIT_DYNLOOP=mode):
+            res[mode] = (prog.eval_loss(ds, K.LOSS["L2"]), ctx.last_tree_code(),
+                         prog.eval_loss_grad(ds, K.LOSS["L2"]), ctx.last_tree_code())
+    (s0, w0, ok0), n0, g0, m0 = res["0"]
+    (s1, w1, ok1), n1, g1, m1 = res["1"]
+    assert n0 == n1 > 600 and m0 == m1 > 600
+    assert w0 == w1 and np.array_equal(ok0, ok1)
+    np.testing.assert_array_equal(s0[ok0], s1[ok1])
+    for a, b in zip(g0, g1):
+        assert np.array_equal(np.asarray(a), np.asarray(b), equal_nan=True)
