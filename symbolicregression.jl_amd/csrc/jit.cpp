@@ -1141,7 +1141,7 @@ static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool 
 struct ModulePart {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr, fn_derive = nullptr;
-  hipFunction_t fn_dl = nullptr, fn_dlw = nullptr;  // the hand-written tree loop (sr_jit_eval_dl), L2 / literal code
+  hipFunction_t fn_dl = nullptr, fn_dlw = nullptr;  // the hand-written tree loop (sr_jit_eval_dl / _dlm)
   int32_t* d_off = nullptr;  // [nslots] code offsets
   int slot0 = 0, nslots = 0;
 };
@@ -1384,10 +1384,8 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       } else {
         HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, opt.memc ? "sr_jit_eval_m" : "sr_jit_eval"));
         HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, opt.memc ? "sr_jit_eval_mw" : "sr_jit_eval_w"));
-        if (!opt.memc) {
-          HIP_CHECK(hipModuleGetFunction(&q.fn_dl, q.mod, "sr_jit_eval_dl"));
-          HIP_CHECK(hipModuleGetFunction(&q.fn_dlw, q.mod, "sr_jit_eval_dlw"));
-        }
+        HIP_CHECK(hipModuleGetFunction(&q.fn_dl, q.mod, opt.memc ? "sr_jit_eval_dlm" : "sr_jit_eval_dl"));
+        HIP_CHECK(hipModuleGetFunction(&q.fn_dlw, q.mod, opt.memc ? "sr_jit_eval_dlmw" : "sr_jit_eval_dlw"));
       }
       HIP_CHECK(hipModuleGetFunction(&q.fn_derive, q.mod, "sr_jit_derive"));
       for (hipFunction_t f : {q.fn, q.fn_w, q.fn_dl, q.fn_dlw})
@@ -1481,7 +1479,7 @@ hipError_t reset_flags(Module* m, hipStream_t stream) {
 // (reserved: JitArgs::dyn)
 bool dynamic_trees() { return false; }
 
-// Loss tree code of literal-constant programs runs under sr_jit_eval_dl(w),
+// Loss tree code runs under sr_jit_eval_dl(w) / _dlm(w) (memory constants),
 // whose tree loop is hand-written (jit_template.hip SR_JIT_LOOP_TEXT): the
 // waves of a workgroup take their trees from an LDS counter, so the workgroup
 // is not held by the wave that drew the costly trees (or the trees whose tiles
@@ -1529,7 +1527,7 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + (ja.part_lds ? part_bytes : 0) + 16;
   // the hand-written loop keeps its tree counter in the last 16 bytes
   hipFunction_t fn = a.w ? q.fn_w : q.fn;
-  if (q.fn_dl && !m->out && !m->memc && dynloop()) fn = a.w ? q.fn_dlw : q.fn_dl;
+  if (q.fn_dl && !m->out && dynloop()) fn = a.w ? q.fn_dlw : q.fn_dl;
   return hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds + pad, stream, nullptr, cfg);
 }
 

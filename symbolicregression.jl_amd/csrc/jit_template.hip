@@ -315,7 +315,9 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
 //   s40 tpb, s41 ntg, s42 g, s43 ntg-1-g, s44 nlist (slots of this part)
 //   s[46:47] failure flags, s[48:49] code offsets, s[50:51] this group's
 //   global partials, s52 partials in LDS (1) or global (0), s53 their LDS
-//   address, s[54:55] bail flags, s[56:57] counters, s[88:89] the code area,
+//   address, s[54:55] bail flags, s[92:93] counters, s[88:89] the code area,
+//   memory-constant code (sr_jit_loop_m): s[98:99] the programs, s[100:101]
+//   list_off, each tree's program address into s[56:57] (SR_JIT_LOOP_PROG),
 //   s65-s68 / s79 / s84 as for the compiled loop; return address s[94:95];
 //   temps s58-s63, s96-s97, v0-v2, v89-v91.
 // Per tree i (slot s = i*ntg + (i odd ? ntg-1-g : g)): a set failure flag
@@ -323,10 +325,10 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
 // slot's bail flag and counts it; the loss is summed over the wave in the
 // order of interp.h wave_sum; lane 0 stores the partial {Σ, NaN or 0} and, if
 // some row failed, the slot's failure flag (vector stores only).
-#define SR_JIT_LOOP_TEXT                                                              \
-  ".globl sr_jit_loop\n.hidden sr_jit_loop\n.p2align 6\nsr_jit_loop:\n"               \
+#define SR_JIT_LOOP_TEXT(NAME, PROG)                                                              \
+  ".globl " #NAME "\n.hidden " #NAME "\n.p2align 6\n" #NAME ":\n"               \
   "v_mov_b32_e32 v89, 1\n"                                                            \
-  ".Lsrl_next:\n"                                                                     \
+  ".L" #NAME "_next:\n"                                                                     \
   "s_mov_b64 s[58:59], exec\n"                                                        \
   "s_mov_b64 exec, 1\n"                                                               \
   "ds_add_rtn_u32 v90, v31, v89\n"                                                    \
@@ -334,13 +336,13 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_mov_b64 exec, s[58:59]\n"                                                        \
   "v_readlane_b32 s60, v90, 0\n"                                                      \
   "s_cmp_ge_u32 s60, s40\n"                                                           \
-  "s_cbranch_scc1 .Lsrl_done\n"                                                       \
+  "s_cbranch_scc1 .L" #NAME "_done\n"                                                       \
   "s_mul_i32 s61, s60, s41\n"                                                         \
   "s_bitcmp1_b32 s60, 0\n"                                                            \
   "s_cselect_b32 s62, s43, s42\n"                                                     \
   "s_add_u32 s61, s61, s62\n"                                                         \
   "s_cmp_ge_u32 s61, s44\n"                                                           \
-  "s_cbranch_scc1 .Lsrl_done\n"                                                       \
+  "s_cbranch_scc1 .L" #NAME "_done\n"                                                       \
   "s_lshl_b32 s62, s61, 2\n"                                                          \
   "v_mov_b32_e32 v90, s62\n"                                                          \
   "global_load_dword v91, v90, s[46:47] sc1\n"                                        \
@@ -348,9 +350,10 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                                   \
   "v_readfirstlane_b32 s62, v91\n"                                                    \
   "s_cmp_lg_u32 s62, 0\n"                                                             \
-  "s_cbranch_scc1 .Lsrl_skip\n"                                                       \
+  "s_cbranch_scc1 .L" #NAME "_skip\n"                                                       \
   "s_add_u32 s96, s88, s63\n"                                                         \
   "s_addc_u32 s97, s89, 0\n"                                                          \
+  PROG                                                                                \
   "v_mov_b32_e32 v41, v30\n"                                                          \
   "v_mov_b32_e32 v42, 0\n"                                                            \
   "v_mov_b32_e32 v40, 0\n"                                                            \
@@ -358,7 +361,7 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_swappc_b64 s[76:77], s[96:97]\n"                                                 \
   "v_mov_b32_e32 v89, 1\n"                                                            \
   "s_cmp_eq_u32 s69, 0\n"                                                             \
-  "s_cbranch_scc1 .Lsrl_sum\n"                                                        \
+  "s_cbranch_scc1 .L" #NAME "_sum\n"                                                        \
   "v_mov_b32_e32 v40, 0x7fc00000\n"                                                   \
   "s_mov_b64 s[58:59], exec\n"                                                        \
   "s_mov_b64 exec, 1\n"                                                               \
@@ -366,9 +369,9 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "v_mov_b32_e32 v90, s62\n"                                                          \
   "global_store_dword v90, v89, s[54:55] sc1\n"                                       \
   "v_mov_b32_e32 v90, 0\n"                                                            \
-  "global_atomic_add v90, v89, s[56:57]\n"                                            \
+  "global_atomic_add v90, v89, s[92:93]\n"                                            \
   "s_mov_b64 exec, s[58:59]\n"                                                        \
-  ".Lsrl_sum:\n"                                                                      \
+  ".L" #NAME "_sum:\n"                                                                      \
   "v_cmp_u_f32_e32 vcc, v40, v40\n"                                                   \
   "s_nop 1\n"                                                                         \
   "v_add_f32_dpp v1, v42, v42 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
@@ -396,48 +399,59 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "v_mov_b32_e32 v1, s63\n"                                                           \
   "s_lshl_b32 s62, s60, 3\n"                                                          \
   "s_cmp_eq_u32 s52, 0\n"                                                             \
-  "s_cbranch_scc1 .Lsrl_g1\n"                                                         \
+  "s_cbranch_scc1 .L" #NAME "_g1\n"                                                         \
   "v_mov_b32_e32 v2, s53\n"                                                           \
   "v_add_u32_e32 v2, s62, v2\n"                                                       \
   "ds_write_b64 v2, v[0:1]\n"                                                         \
-  "s_branch .Lsrl_st1\n"                                                              \
-  ".Lsrl_g1:\n"                                                                       \
+  "s_branch .L" #NAME "_st1\n"                                                              \
+  ".L" #NAME "_g1:\n"                                                                       \
   "v_mov_b32_e32 v2, s62\n"                                                           \
   "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
-  ".Lsrl_st1:\n"                                                                      \
+  ".L" #NAME "_st1:\n"                                                                      \
   "s_cmp_eq_u32 s63, 0\n"                                                             \
-  "s_cbranch_scc1 .Lsrl_nf\n"                                                         \
+  "s_cbranch_scc1 .L" #NAME "_nf\n"                                                         \
   "s_lshl_b32 s62, s61, 2\n"                                                          \
   "v_mov_b32_e32 v2, s62\n"                                                           \
   "global_store_dword v2, v89, s[46:47] sc1\n"                                        \
-  ".Lsrl_nf:\n"                                                                       \
+  ".L" #NAME "_nf:\n"                                                                       \
   "s_mov_b64 exec, s[58:59]\n"                                                        \
-  "s_branch .Lsrl_next\n"                                                             \
-  ".Lsrl_skip:\n"                                                                     \
+  "s_branch .L" #NAME "_next\n"                                                             \
+  ".L" #NAME "_skip:\n"                                                                     \
   "s_mov_b64 s[58:59], exec\n"                                                        \
   "s_mov_b64 exec, 1\n"                                                               \
   "v_mov_b32_e32 v0, 0\n"                                                             \
   "v_mov_b32_e32 v1, 0x7fc00000\n"                                                    \
   "s_lshl_b32 s62, s60, 3\n"                                                          \
   "s_cmp_eq_u32 s52, 0\n"                                                             \
-  "s_cbranch_scc1 .Lsrl_g2\n"                                                         \
+  "s_cbranch_scc1 .L" #NAME "_g2\n"                                                         \
   "v_mov_b32_e32 v2, s53\n"                                                           \
   "v_add_u32_e32 v2, s62, v2\n"                                                       \
   "ds_write_b64 v2, v[0:1]\n"                                                         \
-  "s_branch .Lsrl_st2\n"                                                              \
-  ".Lsrl_g2:\n"                                                                       \
+  "s_branch .L" #NAME "_st2\n"                                                              \
+  ".L" #NAME "_g2:\n"                                                                       \
   "v_mov_b32_e32 v2, s62\n"                                                           \
   "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
-  ".Lsrl_st2:\n"                                                                      \
+  ".L" #NAME "_st2:\n"                                                                      \
   "s_mov_b64 exec, s[58:59]\n"                                                        \
-  "s_branch .Lsrl_next\n"                                                             \
-  ".Lsrl_done:\n"                                                                     \
+  "s_branch .L" #NAME "_next\n"                                                             \
+  ".L" #NAME "_done:\n"                                                                     \
   "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                                   \
   "s_setpc_b64 s[94:95]\n"
 
-extern "C" __global__ void __launch_bounds__(64) sr_jit_loop_holder() { asm volatile("s_endpgm\n" SR_JIT_LOOP_TEXT); }
+// the slot's program (memory-constant tree code loads its constants from it):
+// s[56:57] = program base s[98:99] + 8 * list_off[slot] (list_off at s[100:101])
+#define SR_JIT_LOOP_PROG                                                              \
+  "s_lshl_b32 s62, s61, 2\n"                                                          \
+  "s_load_dword s91, s[100:101], s62\n"                                               \
+  "s_waitcnt lgkmcnt(0)\n"                                                            \
+  "s_lshl_b32 s91, s91, 3\n"                                                          \
+  "s_add_u32 s56, s98, s91\n"                                                         \
+  "s_addc_u32 s57, s99, 0\n"
+extern "C" __global__ void __launch_bounds__(64) sr_jit_loop_holder() {
+  asm volatile("s_endpgm\n" SR_JIT_LOOP_TEXT(sr_jit_loop, "") SR_JIT_LOOP_TEXT(sr_jit_loop_m, SR_JIT_LOOP_PROG));
+}
 
-template <bool W>
+template <bool W, bool MEMC>
 __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
   const EvalArgs<float>& a = ja.e;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -515,18 +529,34 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
   const uint64_t dstp = reinterpret_cast<uint64_t>(gdst), bailp = reinterpret_cast<uint64_t>(ja.bail);
   const uint64_t cntp = reinterpret_cast<uint64_t>(ja.counters);
   uint32_t redos = 0;
-  asm volatile(
-      "s_getpc_b64 s[96:97]\n"
-      "s_add_u32 s96, s96, sr_jit_loop@rel32@lo+4\n"
-      "s_addc_u32 s97, s97, sr_jit_loop@rel32@hi+12\n"
-      "s_swappc_b64 s[94:95], s[96:97]"
-      : "+{s84}"(redos)
-      : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
-        "{s68}"(woff), "{s79}"(fastok), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
-        "{s[46:47]}"(failp), "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s52}"(plds), "{s53}"(spart),
-        "{s[54:55]}"(bailp), "{s[56:57]}"(cntp), "{s[88:89]}"(area)
-      : SR_JIT_CLOBBERS, "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94", "s95", "s96", "s97",
-        "v40", "v41", "v42", "v89", "v90", "v91", "memory");
+  if constexpr (MEMC) {
+    const uint64_t progp = reinterpret_cast<uint64_t>(a.prog), lop = reinterpret_cast<uint64_t>(a.list_off);
+    asm volatile(
+        "s_getpc_b64 s[96:97]\n"
+        "s_add_u32 s96, s96, sr_jit_loop_m@rel32@lo+4\n"
+        "s_addc_u32 s97, s97, sr_jit_loop_m@rel32@hi+12\n"
+        "s_swappc_b64 s[94:95], s[96:97]"
+        : "+{s84}"(redos)
+        : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+          "{s68}"(woff), "{s79}"(fastok), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
+          "{s[46:47]}"(failp), "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s52}"(plds), "{s53}"(spart),
+          "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area), "{s[98:99]}"(progp), "{s[100:101]}"(lop)
+        : SR_JIT_CLOBBERS_MEMC, "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94",
+          "s95", "s96", "s97", "v40", "v41", "v42", "v89", "v90", "v91", "memory");
+  } else {
+    asm volatile(
+        "s_getpc_b64 s[96:97]\n"
+        "s_add_u32 s96, s96, sr_jit_loop@rel32@lo+4\n"
+        "s_addc_u32 s97, s97, sr_jit_loop@rel32@hi+12\n"
+        "s_swappc_b64 s[94:95], s[96:97]"
+        : "+{s84}"(redos)
+        : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+          "{s68}"(woff), "{s79}"(fastok), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
+          "{s[46:47]}"(failp), "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s52}"(plds), "{s53}"(spart),
+          "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area)
+        : SR_JIT_CLOBBERS, "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94", "s95", "s96", "s97",
+          "v40", "v41", "v42", "v89", "v90", "v91", "memory");
+  }
   if (lane == 0 && __builtin_amdgcn_readfirstlane((int)redos) != 0)
     __hip_atomic_fetch_add(ja.counters + 1, (uint32_t)__builtin_amdgcn_readfirstlane((int)redos),
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -535,8 +565,10 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
     for (int i = threadIdx.x; i < a.tpb; i += nthreads) gdst[i] = sPart[i];
   }
 }
-extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dl(JitArgs ja) { jit_eval_dl_body<false>(ja); }
-extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlw(JitArgs ja) { jit_eval_dl_body<true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dl(JitArgs ja) { jit_eval_dl_body<false, false>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlw(JitArgs ja) { jit_eval_dl_body<true, false>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlm(JitArgs ja) { jit_eval_dl_body<false, true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlmw(JitArgs ja) { jit_eval_dl_body<true, true>(ja); }
 
 // ---- gradient tree code (jit_grad.cpp) ---------------------------------------------
 // One workgroup = (row group, tree group) as above; each tree's code runs the

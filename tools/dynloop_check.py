@@ -42,6 +42,8 @@ def main():
     small = srhip.random_population(600, o, 5, np.float32, seed=4)
     cases.append(("small", small, X, y, None, 3))
     cases.append(("small_w", small, X, y, w, 3))
+    cases.append(("small_memc", small, X, y, None, 3))
+    cases.append(("small_memc_w", small, X, y, w, 3))
     if len(sys.argv) > 1 and sys.argv[1] == "full":
         rng = np.random.default_rng(1)
         Xf = rng.standard_normal((5, 1_000_000)).astype(np.float32)
@@ -53,8 +55,12 @@ def main():
     for name, trees, Xc, yc, wc, reps in cases:
         ds = srhip.DeviceDataset(ctx, Xc, yc, wc)
         os.environ["SRHIP_JIT"] = "1"
-        try:
-            prog = srhip.Program(ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32)
+        try:  # *_memc: memory-constant tree code (sr_jit_eval_dlm), new constants set in place
+            memc = "memc" in name
+            prog = srhip.Program(ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32, varying_constants=memc)
+            if memc:
+                c = prog.flat.consts.astype(np.float32)
+                prog.set_constants((c * np.float32(1.01) + np.float32(0.002)).astype(np.float32))
         finally:
             del os.environ["SRHIP_JIT"]
         s0, w0, ok0, k0, e0 = run(ctx, prog, ds, "0", reps)
