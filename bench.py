@@ -20,9 +20,9 @@ Multi-GPU (torchrun, one rank per GPU), strong scaling of the one batch:
   --shard rows  the 1M rows split over the N ranks, every rank evaluates all
       trees on its shard and the per-tree [Σw·ℓ, failed] partials + Σw are
       all-reduced on the device (RCCL, 64 KiB) each step.
-Measured on one GPU at the N = 8 sizes (profiles/r04_shard_probe_c.json):
-slowest balanced tree shard 0.659 ms, strided 0.685, row shard 0.676 before
-its all-reduce, against 3.53 ms for the whole batch (5.35x / 5.15x / 5.2x).
+Measured on one GPU at the N = 8 sizes (profiles/r04_shard_probe_d.json):
+slowest balanced tree shard 0.661 ms, strided 0.663, row shard 0.644 before
+its all-reduce, against 3.48 ms for the whole batch (5.27x / 5.25x / 5.41x).
 Timing: barrier + sync on both sides of the K timed steps, max over ranks;
 value = the 4096 trees' node·rows ÷ that time.
 
