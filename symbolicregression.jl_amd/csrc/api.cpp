@@ -706,6 +706,14 @@ bool rg_xcd() {
   const char* e = std::getenv("SRHIP_RG_XCD");  // read per launch: A/B measurements
   return !(e && e[0] == '0');
 }
+// SRHIP_TG_MAJOR=1 (experiment, read per launch): within an XCD the blocks
+// run tree group by tree group (jit_template.hip block_of, rotate 3), so the
+// workgroups resident on a CU share their tree code in the instruction cache
+int rotate_mode() {
+  if (!rg_xcd()) return 0;
+  const char* e = std::getenv("SRHIP_TG_MAJOR");
+  return (e && e[0] == '1') ? 3 : 2;
+}
 
 bool zero_copy_enabled() {
   const char* e = std::getenv("SRHIP_ZERO_COPY");  // read per call: A/B measurements
@@ -1298,7 +1306,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.loss = loss;
     a.rotate = rotate_enabled() ? 1 : 0;
     a.contig = (pass == -1 && jm && jit_contig()) ? 1 : 0;
-    if (pass == -1 && jm && rg_xcd()) a.rotate = 2;  // tree code: row groups per XCD
+    if (pass == -1 && jm && rg_xcd()) a.rotate = rotate_mode();  // tree code: row groups per XCD
     a.lparam = lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);
@@ -1628,7 +1636,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
           a.nrg = plan.nrg;
           a.loss = loss;
           a.contig = jit_contig() ? 1 : 0;
-          a.rotate = rg_xcd() ? 2 : 0;
+          a.rotate = rotate_mode();
           c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<float>));
           a.partial = static_cast<Part<float>*>(c->partial.p);
           const int tk = timed_begin(c, s);

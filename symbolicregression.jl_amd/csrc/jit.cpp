@@ -1518,7 +1518,7 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   ja.part_lds = part_bytes <= 8192 && !part_global() ? 1 : 0;
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  const unsigned grid = a.rotate == 2 ? (unsigned)((a.nrg + 7) / 8 * 8) * (unsigned)a.ntg
+  const unsigned grid = a.rotate >= 2 ? (unsigned)((a.nrg + 7) / 8 * 8) * (unsigned)a.ntg
                                       : (unsigned)a.nrg * (unsigned)a.ntg;
   // SRHIP_JIT_LDS_PAD (experiments): extra LDS per workgroup, i.e. fewer resident waves
   static const unsigned pad = [] { const char* e = std::getenv("SRHIP_JIT_LDS_PAD"); return e ? (unsigned)std::atoi(e) : 0u; }();

@@ -1288,7 +1288,7 @@ hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const
   ja.dyn = dynamic_trees() ? 1 : 0;
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
-  const unsigned grid = a.rotate == 2 ? (unsigned)((a.nrg + 7) / 8 * 8) * (unsigned)a.ntg
+  const unsigned grid = a.rotate >= 2 ? (unsigned)((a.nrg + 7) / 8 * 8) * (unsigned)a.ntg
                                       : (unsigned)a.nrg * (unsigned)a.ntg;
   // LDS: the row tiles only (partials and ∂L/∂c go straight to global memory)
   const size_t narr = 1 + (size_t)a.nfeat + (a.w ? 1 : 0);

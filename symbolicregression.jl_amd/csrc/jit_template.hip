@@ -47,8 +47,19 @@ constexpr int TILE = 64 * R;
 // g = (b/8) % ntg put every tree group of a row group on the same XCD (its X
 // tile is read from HBM once per XCD); the grid is padded to whole octets of
 // row groups and the padding blocks return at once.
+// a.rotate == 3 (SRHIP_TG_MAJOR=1, experiment): the same XCD deal, but an
+// XCD's blocks run tree group by tree group, g = (b/8) / nrg8, rg =
+// ((b/8) % nrg8)·8 + b % 8, so the workgroups resident on its CUs share their
+// tree code in the instruction cache.
 __device__ __forceinline__ bool block_of(const EvalArgs<float>& a, int& rg, int& g) {
   const int b = blockIdx.x;
+  if (a.rotate == 3) {
+    const int k = b >> 3;
+    const int nrg8 = (a.nrg + 7) >> 3;
+    g = k / nrg8;
+    rg = (k - g * nrg8) * 8 + (b & 7);
+    return rg < a.nrg && g < a.ntg;
+  }
   if (a.rotate == 2) {
     const int k = b >> 3;
     rg = (k / a.ntg) * 8 + (b & 7);
