@@ -1142,6 +1142,7 @@ struct ModulePart {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr, fn_derive = nullptr;
   hipFunction_t fn_dl = nullptr, fn_dlw = nullptr;  // the hand-written tree loop (sr_jit_eval_dl / _dlm)
+  hipFunction_t fn_dlp = nullptr, fn_dlpw = nullptr;  // its prefetching variant (literal code)
   int32_t* d_off = nullptr;  // [nslots] code offsets
   int slot0 = 0, nslots = 0;
 };
@@ -1386,9 +1387,13 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
         HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, opt.memc ? "sr_jit_eval_mw" : "sr_jit_eval_w"));
         HIP_CHECK(hipModuleGetFunction(&q.fn_dl, q.mod, opt.memc ? "sr_jit_eval_dlm" : "sr_jit_eval_dl"));
         HIP_CHECK(hipModuleGetFunction(&q.fn_dlw, q.mod, opt.memc ? "sr_jit_eval_dlmw" : "sr_jit_eval_dlw"));
+        if (!opt.memc) {
+          HIP_CHECK(hipModuleGetFunction(&q.fn_dlp, q.mod, "sr_jit_eval_dlp"));
+          HIP_CHECK(hipModuleGetFunction(&q.fn_dlpw, q.mod, "sr_jit_eval_dlpw"));
+        }
       }
       HIP_CHECK(hipModuleGetFunction(&q.fn_derive, q.mod, "sr_jit_derive"));
-      for (hipFunction_t f : {q.fn, q.fn_w, q.fn_dl, q.fn_dlw})
+      for (hipFunction_t f : {q.fn, q.fn_w, q.fn_dl, q.fn_dlw, q.fn_dlp, q.fn_dlpw})
         if (f)
           HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                         160 * 1024));
@@ -1483,9 +1488,9 @@ bool dynamic_trees() { return false; }
 // whose tree loop is hand-written (jit_template.hip SR_JIT_LOOP_TEXT): the
 // waves of a workgroup take their trees from an LDS counter, so the workgroup
 // is not held by the wave that drew the costly trees (or the trees whose tiles
-// are redone PRECISE). Same sums bit for bit (wave_sum's order); config #2
-// 3.597 → 3.244 ms, its 125k-row shard 0.640 → 0.568, a 512-tree shard
-// 0.557 → 0.529 (profiles/r04_dynloop.jsonl, tools/dynloop_check.py).
+// are redone PRECISE). Same sums bit for bit (wave_sum's order); interleaved
+// A/B (tools/loop_ab.py, profiles/r04_loop_ab.jsonl): config #2 3.380 →
+// 3.247 ms, its 125k-row shard 0.546 → 0.506, a 512-tree shard 0.515 → 0.503.
 // SRHIP_JIT_DYNLOOP=0 (read per launch): the compiled static loop.
 static bool dynloop() {
   const char* e = std::getenv("SRHIP_JIT_DYNLOOP");
@@ -1528,6 +1533,12 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   // the hand-written loop keeps its tree counter in the last 16 bytes
   hipFunction_t fn = a.w ? q.fn_w : q.fn;
   if (q.fn_dl && !m->out && dynloop()) fn = a.w ? q.fn_dlw : q.fn_dl;
+  // literal code: the loop that claims the next tree and loads its flag and
+  // code offset before running this one (interleaved A/B, profiles/
+  // r04_loop_ab.jsonl: config #2 3.247 → 3.231 ms, a 512-tree shard 0.503 →
+  // 0.483); SRHIP_JIT_PREFETCH=0 (read per launch): without
+  static const auto prefetch = [] { const char* e = std::getenv("SRHIP_JIT_PREFETCH"); return !(e && e[0] == '0'); };
+  if (q.fn_dlp && !m->out && dynloop() && prefetch()) fn = a.w ? q.fn_dlpw : q.fn_dlp;
   return hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds + pad, stream, nullptr, cfg);
 }
 

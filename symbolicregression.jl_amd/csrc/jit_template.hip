@@ -448,6 +448,153 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   ".L" #NAME "_done:\n"                                                                     \
   "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                                   \
   "s_setpc_b64 s[94:95]\n"
+// The same loop with the next tree claimed and its failure flag / code offset
+// loaded before the current tree runs (their latency under its work):
+// next i s58, slot s59, flag v92, code offset s23; exec saved in s[96:97].
+#define SR_JIT_LOOP_PF_TEXT(NAME)                                                      \
+  ".globl " #NAME "\n.hidden " #NAME "\n.p2align 6\n" #NAME ":\n"               \
+  "v_mov_b32_e32 v89, 1\n"                                                       \
+  "s_mov_b64 s[96:97], exec\n"                                                   \
+  "s_mov_b64 exec, 1\n"                                                          \
+  "ds_add_rtn_u32 v90, v31, v89\n"                                               \
+  "s_waitcnt lgkmcnt(0)\n"                                                       \
+  "s_mov_b64 exec, s[96:97]\n"                                                   \
+  "v_readlane_b32 s58, v90, 0\n"                                                 \
+  "s_cmp_ge_u32 s58, s40\n"                                                      \
+  "s_cbranch_scc1 .L" #NAME "_inv0\n"                                        \
+  "s_mul_i32 s59, s58, s41\n"                                                    \
+  "s_bitcmp1_b32 s58, 0\n"                                                       \
+  "s_cselect_b32 s62, s43, s42\n"                                                \
+  "s_add_u32 s59, s59, s62\n"                                                    \
+  "s_cmp_ge_u32 s59, s44\n"                                                      \
+  "s_cbranch_scc1 .L" #NAME "_inv0\n"                                        \
+  "s_lshl_b32 s62, s59, 2\n"                                                     \
+  "v_mov_b32_e32 v90, s62\n"                                                     \
+  "global_load_dword v92, v90, s[46:47] sc1\n"                                   \
+  "s_load_dword s23, s[48:49], s62\n"                                            \
+  "s_branch .L" #NAME "_ok0\n"                                        \
+  ".L" #NAME "_inv0:\n"                                        \
+  "s_mov_b32 s58, -1\n"                                                          \
+  ".L" #NAME "_ok0:\n"                                        \
+  ".L" #NAME "_next:\n"                                        \
+  "s_cmp_ge_u32 s58, s40\n"                                                      \
+  "s_cbranch_scc1 .L" #NAME "_done\n"                                        \
+  "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                              \
+  "v_readfirstlane_b32 s62, v92\n"                                               \
+  "s_mov_b32 s60, s58\n"                                                         \
+  "s_mov_b32 s61, s59\n"                                                         \
+  "s_mov_b32 s63, s23\n"                                                         \
+  "s_mov_b32 s91, s62\n"                                                         \
+  "s_mov_b64 s[96:97], exec\n"                                                   \
+  "s_mov_b64 exec, 1\n"                                                          \
+  "ds_add_rtn_u32 v90, v31, v89\n"                                               \
+  "s_waitcnt lgkmcnt(0)\n"                                                       \
+  "s_mov_b64 exec, s[96:97]\n"                                                   \
+  "v_readlane_b32 s58, v90, 0\n"                                                 \
+  "s_cmp_ge_u32 s58, s40\n"                                                      \
+  "s_cbranch_scc1 .L" #NAME "_inv1\n"                                        \
+  "s_mul_i32 s59, s58, s41\n"                                                    \
+  "s_bitcmp1_b32 s58, 0\n"                                                       \
+  "s_cselect_b32 s62, s43, s42\n"                                                \
+  "s_add_u32 s59, s59, s62\n"                                                    \
+  "s_cmp_ge_u32 s59, s44\n"                                                      \
+  "s_cbranch_scc1 .L" #NAME "_inv1\n"                                        \
+  "s_lshl_b32 s62, s59, 2\n"                                                     \
+  "v_mov_b32_e32 v90, s62\n"                                                     \
+  "global_load_dword v92, v90, s[46:47] sc1\n"                                   \
+  "s_load_dword s23, s[48:49], s62\n"                                            \
+  "s_branch .L" #NAME "_ok1\n"                                        \
+  ".L" #NAME "_inv1:\n"                                        \
+  "s_mov_b32 s58, -1\n"                                                          \
+  ".L" #NAME "_ok1:\n"                                        \
+  "s_cmp_lg_u32 s91, 0\n"                                                        \
+  "s_cbranch_scc1 .L" #NAME "_skip\n"                                        \
+  "s_add_u32 s96, s88, s63\n"                                                         \
+  "s_addc_u32 s97, s89, 0\n"                                                          \
+  "v_mov_b32_e32 v41, v30\n"                                                          \
+  "v_mov_b32_e32 v42, 0\n"                                                            \
+  "v_mov_b32_e32 v40, 0\n"                                                            \
+  "s_mov_b32 s64, 0\n"                                                                \
+  "s_swappc_b64 s[76:77], s[96:97]\n"                                                 \
+  "v_mov_b32_e32 v89, 1\n"                                                            \
+  "s_cmp_eq_u32 s69, 0\n"                                                             \
+  "s_cbranch_scc1 .L" #NAME "_sum\n"                                                        \
+  "v_mov_b32_e32 v40, 0x7fc00000\n"                                                   \
+  "s_mov_b64 s[96:97], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "s_lshl_b32 s62, s61, 2\n"                                                          \
+  "v_mov_b32_e32 v90, s62\n"                                                          \
+  "global_store_dword v90, v89, s[54:55] sc1\n"                                       \
+  "v_mov_b32_e32 v90, 0\n"                                                            \
+  "global_atomic_add v90, v89, s[92:93]\n"                                            \
+  "s_mov_b64 exec, s[96:97]\n"                                                        \
+  ".L" #NAME "_sum:\n"                                                                      \
+  "v_cmp_u_f32_e32 vcc, v40, v40\n"                                                   \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v42, v42 quad_perm:[1,0,3,2] row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 quad_perm:[2,3,0,1] row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 row_half_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n" \
+  "s_nop 1\n"                                                                         \
+  "v_add_f32_dpp v1, v1, v1 row_mirror row_mask:0xf bank_mask:0xf bound_ctrl:1\n"     \
+  "v_mov_b32_e32 v2, 0\n"                                                             \
+  "s_nop 1\n"                                                                         \
+  "v_mov_b32_dpp v2, v1 row_bcast:15 row_mask:0xa bank_mask:0xf\n"                    \
+  "v_add_f32_e32 v1, v1, v2\n"                                                        \
+  "v_mov_b32_e32 v2, 0\n"                                                             \
+  "s_nop 1\n"                                                                         \
+  "v_mov_b32_dpp v2, v1 row_bcast:31 row_mask:0xc bank_mask:0xf\n"                    \
+  "v_add_f32_e32 v1, v1, v2\n"                                                        \
+  "s_nop 1\n"                                                                         \
+  "v_readlane_b32 s62, v1, 63\n"                                                      \
+  "s_cmp_lg_u64 vcc, 0\n"                                                             \
+  "s_cselect_b32 s63, 0x7fc00000, 0\n"                                                \
+  "s_mov_b64 s[96:97], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "v_mov_b32_e32 v0, s62\n"                                                           \
+  "v_mov_b32_e32 v1, s63\n"                                                           \
+  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "s_cmp_eq_u32 s52, 0\n"                                                             \
+  "s_cbranch_scc1 .L" #NAME "_g1\n"                                                         \
+  "v_mov_b32_e32 v2, s53\n"                                                           \
+  "v_add_u32_e32 v2, s62, v2\n"                                                       \
+  "ds_write_b64 v2, v[0:1]\n"                                                         \
+  "s_branch .L" #NAME "_st1\n"                                                              \
+  ".L" #NAME "_g1:\n"                                                                       \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  ".L" #NAME "_st1:\n"                                                                      \
+  "s_cmp_eq_u32 s63, 0\n"                                                             \
+  "s_cbranch_scc1 .L" #NAME "_nf\n"                                                         \
+  "s_lshl_b32 s62, s61, 2\n"                                                          \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dword v2, v89, s[46:47] sc1\n"                                        \
+  ".L" #NAME "_nf:\n"                                                                       \
+  "s_mov_b64 exec, s[96:97]\n"                                                        \
+  "s_branch .L" #NAME "_next\n"                                                             \
+  ".L" #NAME "_skip:\n"                                                                     \
+  "s_mov_b64 s[96:97], exec\n"                                                        \
+  "s_mov_b64 exec, 1\n"                                                               \
+  "v_mov_b32_e32 v0, 0\n"                                                             \
+  "v_mov_b32_e32 v1, 0x7fc00000\n"                                                    \
+  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "s_cmp_eq_u32 s52, 0\n"                                                             \
+  "s_cbranch_scc1 .L" #NAME "_g2\n"                                                         \
+  "v_mov_b32_e32 v2, s53\n"                                                           \
+  "v_add_u32_e32 v2, s62, v2\n"                                                       \
+  "ds_write_b64 v2, v[0:1]\n"                                                         \
+  "s_branch .L" #NAME "_st2\n"                                                              \
+  ".L" #NAME "_g2:\n"                                                                       \
+  "v_mov_b32_e32 v2, s62\n"                                                           \
+  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  ".L" #NAME "_st2:\n"                                                                      \
+  "s_mov_b64 exec, s[96:97]\n"                                                        \
+  "s_branch .L" #NAME "_next\n"                                                             \
+  ".L" #NAME "_done:\n"                                                                     \
+  "s_waitcnt vmcnt(0) lgkmcnt(0)\n"                                                   \
+  "s_setpc_b64 s[94:95]\n"
+
 
 // the slot's program (memory-constant tree code loads its constants from it):
 // s[56:57] = program base s[98:99] + 8 * list_off[slot] (list_off at s[100:101])
@@ -459,10 +606,11 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_add_u32 s56, s98, s91\n"                                                         \
   "s_addc_u32 s57, s99, 0\n"
 extern "C" __global__ void __launch_bounds__(64) sr_jit_loop_holder() {
-  asm volatile("s_endpgm\n" SR_JIT_LOOP_TEXT(sr_jit_loop, "") SR_JIT_LOOP_TEXT(sr_jit_loop_m, SR_JIT_LOOP_PROG));
+  asm volatile("s_endpgm\n" SR_JIT_LOOP_TEXT(sr_jit_loop, "") SR_JIT_LOOP_TEXT(sr_jit_loop_m, SR_JIT_LOOP_PROG)
+                   SR_JIT_LOOP_PF_TEXT(sr_jit_loop_p));
 }
 
-template <bool W, bool MEMC>
+template <bool W, bool MEMC, bool PF = false>
 __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
   const EvalArgs<float>& a = ja.e;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -554,6 +702,19 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
           "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area), "{s[98:99]}"(progp), "{s[100:101]}"(lop)
         : SR_JIT_CLOBBERS_MEMC, "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94",
           "s95", "s96", "s97", "v40", "v41", "v42", "v89", "v90", "v91", "memory");
+  } else if constexpr (PF) {
+    asm volatile(
+        "s_getpc_b64 s[96:97]\n"
+        "s_add_u32 s96, s96, sr_jit_loop_p@rel32@lo+4\n"
+        "s_addc_u32 s97, s97, sr_jit_loop_p@rel32@hi+12\n"
+        "s_swappc_b64 s[94:95], s[96:97]"
+        : "+{s84}"(redos)
+        : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+          "{s68}"(woff), "{s79}"(fastok), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
+          "{s[46:47]}"(failp), "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s52}"(plds), "{s53}"(spart),
+          "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area)
+        : SR_JIT_CLOBBERS, "s23", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94", "s95", "s96",
+          "s97", "v40", "v41", "v42", "v89", "v90", "v91", "v92", "memory");
   } else {
     asm volatile(
         "s_getpc_b64 s[96:97]\n"
@@ -578,6 +739,8 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
 }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dl(JitArgs ja) { jit_eval_dl_body<false, false>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlw(JitArgs ja) { jit_eval_dl_body<true, false>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlp(JitArgs ja) { jit_eval_dl_body<false, false, true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlpw(JitArgs ja) { jit_eval_dl_body<true, false, true>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlm(JitArgs ja) { jit_eval_dl_body<false, true>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dlmw(JitArgs ja) { jit_eval_dl_body<true, true>(ja); }
 
