@@ -242,3 +242,21 @@ def test_constant_optimization_row_sharded_unseeded_ranks_agree():
     (_, l0, c0), (_, l1, c1) = res
     np.testing.assert_array_equal(l0, l1)
     np.testing.assert_array_equal(c0, c1)
+
+
+def test_balanced_tree_shards_cover_and_balance():
+    """bench.py's default N > 1 partition (shard_trees_balanced, LPT on the
+    estimated cost): every tree on exactly one rank, the ranks' estimated
+    costs within one costliest tree of each other, the same on every rank."""
+    import srhip
+    from srhip.distributed import shard_trees_balanced, tree_cost
+
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(1000, o, 5, np.float32, seed=3, maxsize=30)
+    costs = np.array([tree_cost(t, o) for t in trees])
+    for world in (1, 2, 3, 8):
+        parts = [shard_trees_balanced(trees, o, r, world) for r in range(world)]
+        assert np.array_equal(np.sort(np.concatenate(parts)), np.arange(len(trees)))
+        loads = [costs[p].sum() for p in parts]
+        assert max(loads) - min(loads) <= costs.max() + 1e-9
+        assert all(np.array_equal(p, shard_trees_balanced(trees, o, r, world)) for r, p in enumerate(parts))
