@@ -592,6 +592,7 @@ struct Jit64Args {
 struct Part64 {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr;
+  hipFunction_t fn_dl = nullptr, fn_dlw = nullptr;  // the hand-written tree loop (sr_jit64_eval_dl)
   int32_t* d_off = nullptr;
   int slot0 = 0, nslots = 0;
 };
@@ -644,7 +645,9 @@ Module64* build64(const CompiledBatch<double>& cb, const std::vector<int32_t>& c
       HIP_CHECK(hipModuleLoadData(&q.mod, img.data()));
       HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, "sr_jit64_eval"));
       HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, "sr_jit64_eval_w"));
-      for (hipFunction_t f : {q.fn, q.fn_w})
+      HIP_CHECK(hipModuleGetFunction(&q.fn_dl, q.mod, "sr_jit64_eval_dl"));
+      HIP_CHECK(hipModuleGetFunction(&q.fn_dlw, q.mod, "sr_jit64_eval_dlw"));
+      for (hipFunction_t f : {q.fn, q.fn_w, q.fn_dl, q.fn_dlw})
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
       HIP_CHECK(hipMalloc((void**)&q.d_off, ch.offs.size() * sizeof(int32_t)));
@@ -692,8 +695,11 @@ hipError_t launch64(Module64* m, int k, const EvalPlan& plan, const EvalArgs<dou
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const size_t narr = 1 + (size_t)m->nraw + (a.w ? 1 : 0);
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)TILE2 * sizeof(double) + 16;
-  return hipModuleLaunchKernel(a.w ? q.fn_w : q.fn, (unsigned)a.nrg * (unsigned)a.ntg, 1, 1, 256, 1, 1, (unsigned)lds,
-                               stream, nullptr, cfg);
+  // the hand-written tree loop (its counter in the last 16 bytes); SRHIP_JIT_DYNLOOP=0: the compiled one
+  const char* dl = std::getenv("SRHIP_JIT_DYNLOOP");
+  hipFunction_t fn = (dl && dl[0] == '0') ? (a.w ? q.fn_w : q.fn) : (a.w ? q.fn_dlw : q.fn_dl);
+  return hipModuleLaunchKernel(fn, (unsigned)a.nrg * (unsigned)a.ntg, 1, 1, 256, 1, 1, (unsigned)lds, stream, nullptr,
+                               cfg);
 }
 
 bool compile_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes,
