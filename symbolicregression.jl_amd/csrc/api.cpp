@@ -945,6 +945,15 @@ static bool ti_enabled() {
 
 // Row-group rotation of the tree order, off by default (SRHIP_ROT=1 enables
 // it): measured 4.09 -> 4.15 ms on config #2.
+// The interpreter kernels' waves take their trees from an LDS counter
+// (eval_kernel.h, a.rotate & 4): interleaved A/B (tools/interp_dyn_ab.py,
+// profiles/r04_interp_dyn_ab.jsonl) config #3 interpreted 0.511 → 0.469 ms,
+// a 300-tree batch 0.117 → 0.112, config #2 interpreted 5.95 → 5.90; sums bit
+// for bit. SRHIP_INTERP_DYN=0 (read per launch): round-robin.
+static bool interp_dyn() {
+  const char* e = std::getenv("SRHIP_INTERP_DYN");
+  return !(e && e[0] == '0');
+}
 static bool rotate_enabled() {
   const char* e = std::getenv("SRHIP_ROT");  // read per launch: A/B measurements
   return e && e[0] == '1';
@@ -1307,6 +1316,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.rotate = rotate_enabled() ? 1 : 0;
     a.contig = (pass == -1 && jm && jit_contig()) ? 1 : 0;
     if (pass == -1 && jm && rg_xcd()) a.rotate = rotate_mode();  // tree code: row groups per XCD
+    if (pass >= 0 && interp_dyn()) a.rotate |= 4;  // interpreter: trees from an LDS counter
     a.lparam = lparam;
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);

@@ -121,6 +121,66 @@ __device__ __forceinline__ T tile_loss_any(int lk, const T (&acc)[R], const T (&
 // (R = 16 pins 130 VGPRs of threaded-interpreter state: 3 waves.)
 template <typename T, int R, int D>
 constexpr int kWavesPerEU = (sizeof(T) == 4 && D == kShallowSlots) ? (R > 8 ? 3 : 5) : 1;
+// One tree of a workgroup's group on its row tiles: the loss (or the per-row
+// outputs) of tree slot s into sPart[i], its failure flag set when a row fails
+// (the body of the interpreter's tree loop, static or dynamic deal).
+template <typename T, int R, int D, int SET, int MODE, bool W, bool VP, bool TI>
+__device__ __forceinline__ void eval_tree_in_group(const EvalArgs<T>& a, int i, int s, bool skip, const VProg<T>& vp,
+                                                   const Ins<T>* prog, const T* sX, const T* sY, const T* sW,
+                                                   Part<T>* sPart, int rows, int lane, int64_t row0, int nt_valid,
+                                                   int last_valid, double lp) {
+  constexpr int TILE = 64 * R;
+  constexpr bool EE = MODE != MODE_OUT;
+  CIns<T>* p = const_prog(prog);
+  T lsum = T(0), chk = skip ? qnan_v<T>() : T(0);
+  for (int tl = 0; tl < (skip ? 0 : nt_valid); ++tl) {
+    const T* sXt = sX + tl * TILE;
+    T acc[R];
+    bool done = false;
+    if constexpr (TI) {
+      if (a.ti_rec) {
+        const T chk0 = chk;
+        const uint32_t lds = (uint32_t)reinterpret_cast<uintptr_t>(
+            (const __attribute__((address_space(3))) T*)(sXt)) + (uint32_t)lane * 16u;
+        done = run_program_ti<R>(a.ti_rec + (size_t)s * 64, lds, acc, chk);
+        if (!done) chk = chk0;
+      }
+    }
+    if (done) {
+    } else if constexpr (VP && SR_VP == 2) run_program_v2<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
+    else if constexpr (VP) run_program_v<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
+    else run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
+#pragma unroll
+    for (int r = 0; r < R; ++r) chk = mark(acc[r], chk);  // root value
+    if constexpr (MODE == MODE_OUT) {
+      const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
+      store_rows<T, R>(a.out + (size_t)t * a.out_stride + row0 + tl * TILE, lane, acc);
+    } else {
+      T yv[R], wv[R];
+      lds_rows<T, R>(sY + tl * TILE, lane, yv);
+      if constexpr (W) lds_rows<T, R>(sW + tl * TILE, lane, wv);
+      if constexpr (MODE == kModeLossL2) {  // L2 known at compile time: no loss switch
+        if (tl < nt_valid - 1 || last_valid == TILE)
+          lsum += tile_loss<SRHIP_LOSS_L2, W, false>(acc, yv, wv, lp, lane, TILE);
+        else
+          lsum += tile_loss<SRHIP_LOSS_L2, W, true>(acc, yv, wv, lp, lane, last_valid);
+      } else if (tl < nt_valid - 1 || last_valid == TILE) {
+        lsum += tile_loss_any<W, false, T, R>(a.loss, acc, yv, wv, lp, lane, TILE);
+      } else {
+        lsum += tile_loss_any<W, true, T, R>(a.loss, acc, yv, wv, lp, lane, last_valid);
+      }
+      if (__builtin_amdgcn_ballot_w64(chk != chk) != 0) break;  // failed: the rest is moot
+    }
+  }
+  lsum = wave_sum(lsum);
+  chk = wave_sum(chk);
+  if (lane == 0) sPart[i] = Part<T>{lsum, chk};
+  if constexpr (EE) {
+    if (!skip && chk != chk && lane == 0)
+      __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 template <typename T, int R, int D, int SET, int MODE, bool W>
 __global__ void __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kWavesPerEU<T, R, D>)))
 eval_kernel(EvalArgs<T> a) {
@@ -150,6 +210,7 @@ eval_kernel(EvalArgs<T> a) {
       reinterpret_cast<V*>(sX + (size_t)arr * rows)[v] = reinterpret_cast<const V*>(src + row0)[v];
     }
     for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) sPart[i] = Part<T>{T(0), T(0)};
+    if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(sPart + a.tpb) = 0u;  // tree counter (a.rotate & 4)
   }
   __syncthreads();
 
@@ -195,6 +256,49 @@ eval_kernel(EvalArgs<T> a) {
   // row group is skipped by the others that get there later (a tree that
   // overflows on a few rows is otherwise evaluated by every row group at
   // once). Each wave keeps its own set of trees: load balance is unchanged.
+  if (a.rotate & 4) {
+    // Dynamic dealing (round 4): the waves take the group's trees from an LDS
+    // counter, one tree claimed ahead (its flag and program loaded while the
+    // current one runs); claim c runs tree (c + rot) mod tpb, rot = the row
+    // group's share of tpb (a.rotate & 1), so row groups still reach a tree
+    // at different times.
+    uint32_t* cnt = reinterpret_cast<uint32_t*>(sPart + a.tpb);
+    const int drot = (EE && (a.rotate & 1)) ? __builtin_amdgcn_readfirstlane((int)(((int64_t)rg * a.tpb) / a.nrg)) : 0;
+    auto claim = [&]() {
+      int c = a.tpb;
+      for (;;) {
+        uint32_t v = 0;
+        if (lane == 0) v = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        c = __builtin_amdgcn_readfirstlane((int)v);
+        if (c >= a.tpb) return a.tpb;
+        const int i = c + drot < a.tpb ? c + drot : c + drot - a.tpb;
+        if (slot_of(i) < a.nlist) return i;
+      }
+    };
+    int inext = claim();
+    if (inext < a.tpb) {
+      if constexpr (EE) fnext = ld_flag(slot_of(inext));
+      if constexpr (VP) vnext.load(prog_of(slot_of(inext)), lane);
+    }
+    while (inext < a.tpb) {
+      const int i = __builtin_amdgcn_readfirstlane(inext);
+      const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
+      inext = claim();
+      const bool more = inext < a.tpb;
+      const int s2 = __builtin_amdgcn_readfirstlane(more ? slot_of(inext) : s);
+      VProg<T> vp;
+      if constexpr (VP) {
+        vp = vnext;
+        if (more) vnext.load(prog_of(s2), lane);
+      }
+      const bool skip = EE && __builtin_amdgcn_readfirstlane((int)fnext) != 0;
+      if constexpr (EE) {
+        if (more) fnext = ld_flag(s2);
+      }
+      eval_tree_in_group<T, R, D, SET, MODE, W, VP, TI>(a, i, s, skip, vp, prog_of(s), sX, sY, sW, sPart, rows, lane,
+                                                        row0, nt_valid, last_valid, lp);
+    }
+  } else {
   int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
   while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
   m = __builtin_amdgcn_readfirstlane(m);
@@ -224,55 +328,10 @@ eval_kernel(EvalArgs<T> a) {
     if constexpr (EE) {
       if (more) fnext = ld_flag(s2);
     }
-    CIns<T>* p = const_prog(prog_of(s));
-    T lsum = T(0), chk = skip ? qnan_v<T>() : T(0);
-    for (int tl = 0; tl < (skip ? 0 : nt_valid); ++tl) {
-      const T* sXt = sX + tl * TILE;
-      T acc[R];
-      bool done = false;
-      if constexpr (TI) {
-        if (a.ti_rec) {
-          const T chk0 = chk;
-          const uint32_t lds = (uint32_t)reinterpret_cast<uintptr_t>(
-              (const __attribute__((address_space(3))) T*)(sXt)) + (uint32_t)lane * 16u;
-          done = run_program_ti<R>(a.ti_rec + (size_t)s * 64, lds, acc, chk);
-          if (!done) chk = chk0;
-        }
-      }
-      if (done) {
-      } else if constexpr (VP && SR_VP == 2) run_program_v2<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
-      else if constexpr (VP) run_program_v<T, R, D, SET>(vp, sXt, rows, lane, acc, chk);
-      else run_program<T, R, D, SET>(p, sXt, rows, lane, acc, chk);
-#pragma unroll
-      for (int r = 0; r < R; ++r) chk = mark(acc[r], chk);  // root value
-      if constexpr (MODE == MODE_OUT) {
-        const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
-        store_rows<T, R>(a.out + (size_t)t * a.out_stride + row0 + tl * TILE, lane, acc);
-      } else {
-        T yv[R], wv[R];
-        lds_rows<T, R>(sY + tl * TILE, lane, yv);
-        if constexpr (W) lds_rows<T, R>(sW + tl * TILE, lane, wv);
-        if constexpr (MODE == kModeLossL2) {  // L2 known at compile time: no loss switch
-          if (tl < nt_valid - 1 || last_valid == TILE)
-            lsum += tile_loss<SRHIP_LOSS_L2, W, false>(acc, yv, wv, lp, lane, TILE);
-          else
-            lsum += tile_loss<SRHIP_LOSS_L2, W, true>(acc, yv, wv, lp, lane, last_valid);
-        } else if (tl < nt_valid - 1 || last_valid == TILE) {
-          lsum += tile_loss_any<W, false, T, R>(a.loss, acc, yv, wv, lp, lane, TILE);
-        } else {
-          lsum += tile_loss_any<W, true, T, R>(a.loss, acc, yv, wv, lp, lane, last_valid);
-        }
-        if (__builtin_amdgcn_ballot_w64(chk != chk) != 0) break;  // failed: the rest is moot
-      }
-    }
-    lsum = wave_sum(lsum);
-    chk = wave_sum(chk);
-    if (lane == 0) sPart[i] = Part<T>{lsum, chk};
-    if constexpr (EE) {
-      if (!skip && chk != chk && lane == 0)
-        __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
+    eval_tree_in_group<T, R, D, SET, MODE, W, VP, TI>(a, i, s, skip, vp, prog_of(s), sX, sY, sW, sPart, rows, lane,
+                                                      row0, nt_valid, last_valid, lp);
   }
+  }  // static deal
   __syncthreads();
   // 3. one coalesced store of the group's partials
   Part<T>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
@@ -288,7 +347,7 @@ hipError_t launch_one(const EvalPlan& plan, const EvalArgs<T>& a, hipStream_t st
   if (attr_err != hipSuccess) return attr_err;
   const unsigned grid = (unsigned)a.nrg * (unsigned)a.ntg;
   hipLaunchKernelGGL((eval_kernel<T, R, D, SET, MODE, W>), dim3(grid), dim3(plan.threads),
-                     plan.lds_bytes, stream, a);
+                     plan.lds_bytes, stream, a);  // (plan_geometry: + 16 bytes after the partials, the tree counter)
   return hipGetLastError();
 }
 
