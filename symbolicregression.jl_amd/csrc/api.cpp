@@ -1688,6 +1688,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
     a.tree_off = p->d_gtree_off;
     a.items = p->d_gitems + item0;
     a.nitems = nitems;
+    a.dyn = interp_dyn() ? 1 : 0;
     a.const_off = p->d_const_off;
     a.X = static_cast<const T*>(ds->X);
     a.y = static_cast<const T*>(ds->y);

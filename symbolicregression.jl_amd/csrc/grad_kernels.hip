@@ -45,6 +45,7 @@ __global__ void __launch_bounds__(256) grad_kernel(GradArgs<T> a) {
       reinterpret_cast<V*>(sX + (size_t)arr * rows)[v] = reinterpret_cast<const V*>(src + row0)[v];
     }
     for (int i = threadIdx.x; i < a.tpb * S; i += blockDim.x) sPart[i] = T(0);
+    if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(sPart + a.tpb * S) = 0u;  // item counter (a.dyn)
   }
   __syncthreads();
 
@@ -54,11 +55,17 @@ __global__ void __launch_bounds__(256) grad_kernel(GradArgs<T> a) {
   const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE);
   const double lp = a.lparam;
 
-  // Waves take the group's (cost-sorted) trees round-robin: a static,
-  // wave-uniform schedule (no atomics, no divergent loop exit).
+  // Waves take the group's (cost-sorted) items round-robin, or (a.dyn, the
+  // default) from an LDS counter, so a wave that drew cheap items takes more.
   const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
   const int nwaves = (int)(blockDim.x >> 6);
-  for (int i = wave; i < a.tpb; i += nwaves) {
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(sPart + a.tpb * S);
+  auto claim = [&]() {
+    uint32_t v = 0;
+    if (lane == 0) v = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return __builtin_amdgcn_readfirstlane((int)v);
+  };
+  for (int i = a.dyn ? claim() : wave; i < a.tpb; i = a.dyn ? claim() : i + nwaves) {
     const int s = i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
     if (s >= a.nitems) continue;
     const int item = __builtin_amdgcn_readfirstlane(a.items[s]);

@@ -105,6 +105,7 @@ struct GradArgs {
   T* out_value;             // GRAD_OUT: [ntrees][out_stride]
   T* out_grad;              // GRAD_OUT: [total consts][out_stride]
   int64_t out_stride;
+  int dyn = 0;              // waves take their items from an LDS counter (SRHIP_INTERP_DYN)
 };
 
 bool plan_grad(int dtype, bool deep, int G, int mode, bool weighted, int nfeat, int64_t n,
