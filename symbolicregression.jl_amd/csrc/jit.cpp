@@ -1514,7 +1514,15 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   ja.dcols = dcols;
   ja.nbig = plan.nbig >= 0 ? plan.nbig : a.nrg;
   ja.ts = plan.nbig >= 0 ? plan.ts : plan.ntiles;
-  ja.dyn = dynamic_trees() ? 1 : 0;
+  // SRHIP_JIT_STICKY_TREE=1 (experiment, read per launch): sticky PRECISE per
+  // tree across row groups in the prefetching hand-written loop. Measured
+  // slower (profiles/r04_sticky_tree_ab.jsonl: config #2 3.28 → 3.39 ms, a
+  // 512-tree shard 0.486 → 0.528; redone tiles 452k → 21k, but the trees then
+  // run PRECISE on row groups where FAST would have held), so off.
+  {
+    const char* e = std::getenv("SRHIP_JIT_STICKY_TREE");
+    ja.dyn = (e && e[0] == '1') ? 1 : 0;
+  }
   if (ja.nraw > a.nfeat) return hipErrorInvalidValue;
   if (ja.nbig > a.nrg || ja.ts < 1 || ja.ts > plan.ntiles) return hipErrorInvalidValue;
   // partials in LDS when they take little room next to the tiles (measured

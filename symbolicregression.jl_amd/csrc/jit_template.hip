@@ -84,7 +84,7 @@ struct JitArgs {
   const float* dcols;       // [nder][n_pad] the derived columns (sr_jit_derive), or null: staged ones computed here
   int nbig;                 // row groups [0, nbig) hold e.ntiles tiles; the tail row groups after them
   int ts;                   // hold ts tiles each (the last round of workgroups in smaller pieces)
-  int dyn;                  // (reserved: dynamic tree dealing, not in this build)
+  int dyn;                  // hand-written prefetching loop: a tree redone PRECISE in one row group runs PRECISE in the later ones
 };
 
 // A derived column's value: the PRECISE routine of the operator (the same
@@ -507,8 +507,12 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   ".L" #NAME "_inv1:\n"                                        \
   "s_mov_b32 s58, -1\n"                                                          \
   ".L" #NAME "_ok1:\n"                                        \
-  "s_cmp_lg_u32 s91, 0\n"                                                        \
+  "s_bitcmp1_b32 s91, 0\n"                                                       \
   "s_cbranch_scc1 .L" #NAME "_skip\n"                                        \
+  "s_and_b32 s79, s45, 1\n"                                                          \
+  "s_bitcmp1_b32 s91, 1\n"                                                           \
+  "s_cselect_b32 s79, 0, s79\n"                                                      \
+  "s_mov_b32 s91, s84\n"                                                             \
   "s_add_u32 s96, s88, s63\n"                                                         \
   "s_addc_u32 s97, s89, 0\n"                                                          \
   "v_mov_b32_e32 v41, v30\n"                                                          \
@@ -517,6 +521,18 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_mov_b32 s64, 0\n"                                                                \
   "s_swappc_b64 s[76:77], s[96:97]\n"                                                 \
   "v_mov_b32_e32 v89, 1\n"                                                            \
+  "s_cmp_eq_u32 s84, s91\n"                                                          \
+  "s_cbranch_scc1 .L" #NAME "_nore\n"                                       \
+  "s_bitcmp1_b32 s45, 1\n"                                                           \
+  "s_cbranch_scc0 .L" #NAME "_nore\n"                                       \
+  "s_mov_b64 s[96:97], exec\n"                                                       \
+  "s_mov_b64 exec, 1\n"                                                              \
+  "s_lshl_b32 s62, s61, 2\n"                                                         \
+  "v_mov_b32_e32 v90, s62\n"                                                         \
+  "v_mov_b32_e32 v91, 2\n"                                                           \
+  "global_atomic_or v90, v91, s[46:47]\n"                                           \
+  "s_mov_b64 exec, s[96:97]\n"                                                       \
+  ".L" #NAME "_nore:\n"                                                   \
   "s_cmp_eq_u32 s69, 0\n"                                                             \
   "s_cbranch_scc1 .L" #NAME "_sum\n"                                                        \
   "v_mov_b32_e32 v40, 0x7fc00000\n"                                                   \
@@ -703,6 +719,7 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
         : SR_JIT_CLOBBERS_MEMC, "s56", "s57", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94",
           "s95", "s96", "s97", "v40", "v41", "v42", "v89", "v90", "v91", "memory");
   } else if constexpr (PF) {
+    const uint32_t fastflags = fastok | (ja.dyn ? 2u : 0u);  // JitArgs::dyn: sticky PRECISE per tree
     asm volatile(
         "s_getpc_b64 s[96:97]\n"
         "s_add_u32 s96, s96, sr_jit_loop_p@rel32@lo+4\n"
@@ -710,11 +727,11 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
         "s_swappc_b64 s[94:95], s[96:97]"
         : "+{s84}"(redos)
         : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
-          "{s68}"(woff), "{s79}"(fastok), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
+          "{s68}"(woff), "{s45}"(fastflags), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
           "{s[46:47]}"(failp), "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s52}"(plds), "{s53}"(spart),
           "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area)
-        : SR_JIT_CLOBBERS, "s23", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94", "s95", "s96",
-          "s97", "v40", "v41", "v42", "v89", "v90", "v91", "v92", "memory");
+        : SR_JIT_CLOBBERS, "s23", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s79", "s91", "s94", "s95",
+          "s96", "s97", "v40", "v41", "v42", "v89", "v90", "v91", "v92", "memory");
   } else {
     asm volatile(
         "s_getpc_b64 s[96:97]\n"

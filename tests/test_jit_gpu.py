@@ -337,8 +337,8 @@ def test_hand_written_tree_loop_equals_compiled(gpu_ctx, weighted):
     with env(SRHIP_JIT="1"):
         prog = srhip.Program(ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32)
     res = {}
-    for mode in ("0", "1"):
-        with env(SRHIP_JIT_DYNLOOP=mode):
+    for mode in ("0", "1"):  # sticky PRECISE per tree off: the same FAST / PRECISE choice per tile
+        with env(SRHIP_JIT_DYNLOOP=mode, SRHIP_JIT_STICKY_TREE="0"):
             res[mode] = (prog.eval_loss(ds, K.LOSS["L2"]), ctx.last_tree_code(),
                          prog.eval_loss_grad(ds, K.LOSS["L2"]), ctx.last_tree_code())
     (s0, w0, ok0), n0, g0, m0 = res["0"]

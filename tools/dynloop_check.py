@@ -32,6 +32,7 @@ def run(ctx, prog, ds, mode, reps):
 
 
 def main():
+    os.environ["SRHIP_JIT_STICKY_TREE"] = "0"  # bit-identity needs the same FAST / PRECISE choices per tile
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     ctx = srhip.get_context(0)
     rng = np.random.default_rng(5)
