@@ -1514,11 +1514,15 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   ja.dcols = dcols;
   ja.nbig = plan.nbig >= 0 ? plan.nbig : a.nrg;
   ja.ts = plan.nbig >= 0 ? plan.ts : plan.ntiles;
-  // SRHIP_JIT_STICKY_TREE=1 (experiment, read per launch): sticky PRECISE per
-  // tree across row groups in the prefetching hand-written loop. Measured
-  // slower (profiles/r04_sticky_tree_ab.jsonl: config #2 3.28 → 3.39 ms, a
-  // 512-tree shard 0.486 → 0.528; redone tiles 452k → 21k, but the trees then
-  // run PRECISE on row groups where FAST would have held), so off.
+  // Sticky PRECISE per tree across row groups (prefetching hand-written loop):
+  // a tree redone PRECISE in one row group runs PRECISE in the later ones.
+  // It pays with few row groups and costs with many (the trees then run
+  // PRECISE where FAST would have held): 4096 config #2 trees, interleaved
+  // A/B (profiles/r04_sticky_tree_sizes.jsonl, r04_sticky_tree_ab.jsonl):
+  // 30k rows 0.248 → 0.190 ms, 100k 0.449 → 0.449, 250k 0.956 → 0.951, 500k
+  // 1.734 → 1.762, 1M 3.28 → 3.39. A default of "on for at most 128 row
+  // groups" is the next step once it has run through the GPU suite; until then
+  // SRHIP_JIT_STICKY_TREE=1 (read per launch) turns it on.
   {
     const char* e = std::getenv("SRHIP_JIT_STICKY_TREE");
     ja.dyn = (e && e[0] == '1') ? 1 : 0;
