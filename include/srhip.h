@@ -152,6 +152,17 @@ int32_t srhip_close(srhip_ctx* ctx);
  * (src/Options.jl:86-120). Unknown → SRHIP_ERR_UNSUPPORTED. */
 int32_t srhip_op_lookup(const char* name, int32_t* out_arity, int32_t* out_id);
 
+/* One operator on scalars of the program dtype (SRHIP_F32 / SRHIP_F64), with
+ * the engine's semantics (the same host routines its compiler folds
+ * constant subtrees with: Operators.jl:8-111, Float32 transcendentals
+ * evaluated in double and rounded once). For the host callers that fold
+ * constants themselves — DynamicExpressions' `simplify_tree` /
+ * `combine_operators`, used by optimize_and_simplify_population
+ * (src/SingleIteration.jl:73-74) and the :simplify mutation
+ * (src/Mutate.jl:107-109). b is ignored for arity 1. No device work. */
+int32_t srhip_op_eval(int32_t dtype, int32_t arity, int32_t id, double a, double b,
+                      double* out);
+
 /* ---- dataset: Dataset(X, y; weights) src/Dataset.jl:43-64 ----------------
  * Uploads rows [row_begin, row_end) of X / y / w once (the row shard of this
  * device); X is transposed to feature-major on the device. w may be NULL

@@ -25,6 +25,7 @@
 
 #include "../../include/srhip.h"
 #include "compile.h"
+#include "host_ops.h"
 #include "constopt.h"
 #include "jit.h"
 #include "kernels.h"
@@ -1913,6 +1914,23 @@ int32_t srhip_op_lookup(const char* name, int32_t* out_arity, int32_t* out_id) {
       }
     }
     throw Error(SRHIP_ERR_UNSUPPORTED, std::string("operator not supported by the engine: ") + name);
+  });
+}
+
+int32_t srhip_op_eval(int32_t dtype, int32_t arity, int32_t id, double a, double b, double* out) {
+  return guarded([&] {
+    if (!out) throw Error(SRHIP_ERR_INVALID, "null out");
+    if (dtype != SRHIP_F32 && dtype != SRHIP_F64) throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
+    bool known = false;
+    for (const auto& o : kOpNames) known = known || (o.arity == arity && o.id == id);
+    if (!known) throw Error(SRHIP_ERR_UNSUPPORTED, "unknown operator id for this arity");
+    if (dtype == SRHIP_F32) {
+      const float x = (float)a, y = (float)b;
+      *out = arity == 1 ? (double)host::unop<float>(id, x) : (double)host::binop<float>(id, x, y);
+    } else {
+      *out = arity == 1 ? host::unop<double>(id, a) : host::binop<double>(id, a, b);
+    }
+    return SRHIP_OK;
   });
 }
 

@@ -80,16 +80,25 @@ def start_noise(flat, nrestarts: int, rng: np.random.Generator) -> np.ndarray:
 
 def optimize_constants_batch(dataset: Dataset, trees: Sequence[Node], options: Options,
                              rng: Optional[np.random.Generator] = None, device: Optional[int] = None,
-                             evaluator_factory: Optional[Callable] = None) -> ConstOptResult:
+                             evaluator_factory: Optional[Callable] = None,
+                             noise: Optional[np.ndarray] = None) -> ConstOptResult:
     """`optimize_constants` for many trees at once. Trees are updated in place
-    (constants of the best start when it converged, else left at x0)."""
+    (constants of the best start when it converged, else left at x0).
+    `noise` (default: drawn from `rng`) is the standard normal draws of the
+    perturbed starts in start_noise's order, for callers that draw them
+    where the reference does (srhip.evolution: from each island's stream)."""
     algorithm = getattr(options, "optimizer_algorithm", "BFGS")
     if algorithm not in ALGORITHMS:
         raise ValueError("Optimization function not implemented.")  # :39-41
     T = np.dtype(dataset.T).type
     flat = flatten(trees, options, dtype=T)
     nrestarts = int(getattr(options, "optimizer_nrestarts", 2))
-    noise = np.ascontiguousarray(start_noise(flat, nrestarts, rng or np.random.default_rng()), dtype=np.float64)
+    if noise is None:
+        noise = start_noise(flat, nrestarts, rng or np.random.default_rng())
+    noise = np.ascontiguousarray(noise, dtype=np.float64)
+    need = int(sum(nrestarts * int(flat.const_off[i + 1] - flat.const_off[i]) for i in range(flat.ntrees)))
+    if noise.shape != (need,):
+        raise ValueError(f"start noise has {noise.size} values, the trees' restarts need {need}")
     loss = options.elementwise_loss
     par = None if loss.params is None else np.ascontiguousarray(loss.params, dtype=np.float64)
     opts = ConstOptOptions(ALGORITHMS[algorithm], int(getattr(options, "optimizer_iterations", 8)), nrestarts,

@@ -210,6 +210,26 @@ def eval_loss_batch_ok(trees: Sequence[Node], dataset: Dataset, options: Options
     return out, ok
 
 
+def eval_loss_batch_rowsets(trees: Sequence[Node], dataset: Dataset, options: Options,
+                            rows: Sequence[np.ndarray], device: Optional[int] = None
+                            ) -> Tuple[np.ndarray, np.ndarray]:
+    """score_func_batch's evaluation for many trees, tree t on its OWN row
+    sample rows[t] (with replacement, LossFunctions.jl:95-115): (losses in T,
+    did_succeed). Trees that share a sample share a launch."""
+    T = dataset.T
+    losses = np.zeros(len(trees), dtype=T)
+    ok = np.zeros(len(trees), dtype=bool)
+    groups = {}
+    for t, r in enumerate(rows):
+        groups.setdefault(np.asarray(r, dtype=np.int64).tobytes(), []).append(t)
+    for key, idx in groups.items():
+        r = np.frombuffer(key, dtype=np.int64)
+        l, k = eval_loss_batch_ok([trees[t] for t in idx], dataset, options, row_idx=r, device=device)
+        losses[idx] = l
+        ok[idx] = k
+    return losses, ok
+
+
 def eval_loss(tree: Node, dataset: Dataset, options: Options) -> float:
     return eval_loss_batch([tree], dataset, options)[0]
 
@@ -229,9 +249,13 @@ def compute_complexity(tree: Node, options: Options) -> int:
 
 
 def loss_to_score(loss, baseline, tree: Node, options: Options):
+    """LossFunctions.jl:69-82 in T; the parsimony term is Int × Float32
+    (options.parsimony is a Float32 field, Options.jl:327)."""
     T = type(loss) if isinstance(loss, np.floating) else np.float64
     normalization = T(0.01) if baseline < T(0.01) else T(baseline)
-    return T(loss / normalization + T(compute_complexity(tree, options) * options.parsimony))
+    term = np.float32(compute_complexity(tree, options)) * np.float32(options.parsimony)
+    with np.errstate(all="ignore"):
+        return T(T(loss / normalization) + T(term))
 
 
 def score_func_batched(dataset: Dataset, trees: Sequence[Node], options: Options,

@@ -201,27 +201,35 @@ def flatten(trees: Iterable[Node], options, dtype=np.float32) -> FlatTrees:
     node_off = [0]
     const_off = [0]
     nodes = []
-    for tree in trees:
-        cnt = 0
-        for t in _postorder(tree):
-            cnt += 1
-            if t.degree == 0:
-                if t.constant:
-                    kinds.append(K.NODE_CONST)
-                    args.append(0)
-                    consts.append(t.val)
-                else:
-                    kinds.append(K.NODE_FEATURE)
-                    args.append(t.feature - 1)
-            elif t.degree == 1:
-                kinds.append(K.NODE_UNARY)
-                args.append(una_ids[t.op - 1])
+    kapp, aapp, capp = kinds.append, args.append, consts.append
+    NC, NF, NU, NB = K.NODE_CONST, K.NODE_FEATURE, K.NODE_UNARY, K.NODE_BINARY
+
+    def emit(t):  # post-order
+        d = t.degree
+        if d == 0:
+            if t.constant:
+                kapp(NC)
+                aapp(0)
+                capp(t.val)
             else:
-                kinds.append(K.NODE_BINARY)
-                args.append(bin_ids[t.op - 1])
+                kapp(NF)
+                aapp(t.feature - 1)
+        elif d == 1:
+            emit(t.l)
+            kapp(NU)
+            aapp(una_ids[t.op - 1])
+        else:
+            emit(t.l)
+            emit(t.r)
+            kapp(NB)
+            aapp(bin_ids[t.op - 1])
+
+    for tree in trees:
+        before = len(kinds)
+        emit(tree)
         node_off.append(len(kinds))
         const_off.append(len(consts))
-        nodes.append(cnt)
+        nodes.append(len(kinds) - before)
     return FlatTrees(
         np.asarray(node_off, dtype=np.int32),
         np.asarray(kinds, dtype=np.uint8),

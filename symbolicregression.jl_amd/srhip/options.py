@@ -68,11 +68,9 @@ def LogitDistLoss():
 # its search control plane (mutation/crossover schedule, constraints, output,
 # recorder, stopping rules): accepted, stored, not used by this engine.
 REFERENCE_ONLY_KWARGS = frozenset("""
-constraints tournament_selection_p fast_cycle migration hof_migration output_file mutation_weights
-crossover_probability warmup_maxsize_by use_frequency use_frequency_in_tournament adaptive_parsimony_scaling
-verbosity save_to_file seed bin_constraints una_constraints progress terminal_width
-recorder recorder_file early_stop_condition return_state timeout_in_seconds max_evals skip_mutation_failures
-enable_autodiff nested_constraints deterministic define_helper_functions
+output_file verbosity save_to_file seed progress terminal_width
+recorder recorder_file early_stop_condition return_state timeout_in_seconds max_evals
+enable_autodiff deterministic define_helper_functions
 """.split())
 
 
@@ -141,6 +139,23 @@ class Options:
         fraction_replaced: float = 0.00036,
         fraction_replaced_hof: float = 0.035,
         maxdepth: Optional[int] = None,
+        # the regularized-evolution schedule (src/Options.jl:315-379), read by
+        # srhip.evolution (the default path) and srhip.search (fast_cycle)
+        tournament_selection_p: float = 0.86,
+        fast_cycle: bool = False,
+        migration: bool = True,
+        hof_migration: bool = True,
+        mutation_weights=None,
+        crossover_probability: float = 0.066,
+        warmup_maxsize_by: float = 0.0,
+        use_frequency: bool = True,
+        use_frequency_in_tournament: bool = True,
+        adaptive_parsimony_scaling: float = 20.0,
+        skip_mutation_failures: bool = True,
+        constraints=None,
+        bin_constraints=None,
+        una_constraints=None,
+        nested_constraints=None,
         **kws,
     ):
         # Options(; kws...) raises on unknown keywords (src/Options.jl:388-390);
@@ -167,6 +182,10 @@ class Options:
         should_optimize_constants, perturbation_factor = loc["should_optimize_constants"], loc["perturbation_factor"]
         ncycles_per_iteration, fraction_replaced = loc["ncycles_per_iteration"], loc["fraction_replaced"]
         fraction_replaced_hof = loc["fraction_replaced_hof"]
+        tournament_selection_p, mutation_weights = loc["tournament_selection_p"], loc["mutation_weights"]
+        crossover_probability, warmup_maxsize_by = loc["crossover_probability"], loc["warmup_maxsize_by"]
+        use_frequency, use_frequency_in_tournament = loc["use_frequency"], loc["use_frequency_in_tournament"]
+        hof_migration = loc["hof_migration"]
         probability_negate_constant = loc["probability_negate_constant"]
         optimizer_probability, tournament_selection_n = loc["optimizer_probability"], loc["tournament_selection_n"]
         # optimizer_options (src/Options.jl:606-621): its `iterations` overrides
@@ -216,6 +235,24 @@ class Options:
         self.maxdepth = maxdepth
         self.nbin = len(self.binary_operators)
         self.nuna = len(self.unary_operators)
+        self.tournament_selection_p = float(tournament_selection_p)
+        self.fast_cycle = bool(fast_cycle)
+        self.migration = bool(migration)
+        self.hof_migration = bool(hof_migration)
+        self.mutation_weights = mutation_weights
+        self.crossover_probability = float(crossover_probability)
+        if warmup_maxsize_by < 0:
+            raise AssertionError("warmup_maxsize_by >= 0")  # Options.jl:444
+        self.warmup_maxsize_by = float(warmup_maxsize_by)
+        self.use_frequency = bool(use_frequency)
+        self.use_frequency_in_tournament = bool(use_frequency_in_tournament)
+        self.adaptive_parsimony_scaling = float(adaptive_parsimony_scaling)
+        self.skip_mutation_failures = bool(skip_mutation_failures)
+        self.una_constraints, self.bin_constraints = self._build_constraints(constraints, una_constraints,
+                                                                             bin_constraints)
+        self.nested_constraints = self._build_nested(nested_constraints)
+        self.has_constraints = bool(self.nested_constraints) or any(c != -1 for c in self.una_constraints) or any(
+            tuple(c) != (-1, -1) for c in self.bin_constraints)
         # ComplexityMapping (src/OptionsStruct.jl:55-104): use when any is given
         self.complexity_use = any(
             v is not None for v in (complexity_of_operators, complexity_of_constants, complexity_of_variables)
@@ -226,6 +263,42 @@ class Options:
         self.constant_complexity = float(1 if complexity_of_constants is None else complexity_of_constants)
         self.variable_complexity = float(1 if complexity_of_variables is None else complexity_of_variables)
         self._ids = None
+
+    def _build_constraints(self, constraints, una, bina):
+        """build_constraints (src/Options.jl:33-84; `constraints` sets both, :505-519):
+        per unary operator a max complexity of its argument (-1 = none), per
+        binary operator a (left, right) pair."""
+        if constraints is not None:
+            if una is not None or bina is not None:
+                raise AssertionError("give constraints or bin/una_constraints, not both")
+            una = bina = constraints
+        una = {} if una is None else dict(una)
+        bina = {} if bina is None else dict(bina)
+        una = {_opname(k): v for k, v in una.items()}
+        bina = {_opname(k): v for k, v in bina.items()}
+        una_c = [int(una[o]) if o in una else -1 for o in self.unary_operators]
+        bin_c = [tuple(int(v) for v in bina[o]) if o in bina else (-1, -1) for o in self.binary_operators]
+        return una_c, bin_c
+
+    def _build_nested(self, nested):
+        """nested_constraints (src/Options.jl:447-503) as [(degree, op, [(degree', op', max)])]."""
+        if nested is None:
+            return None
+        nested = dict(nested) if not isinstance(nested, dict) else nested
+
+        def locate(op):
+            if op in self.binary_operators:
+                return 2, self.binary_operators.index(op) + 1
+            if op in self.unary_operators:
+                return 1, self.unary_operators.index(op) + 1
+            raise ValueError(f"Operator {op} is not in the operator set.")
+
+        out = []
+        for op, inner in nested.items():
+            d, i = locate(_opname(op))
+            inner = dict(inner) if not isinstance(inner, dict) else inner
+            out.append((d, i, [(*locate(_opname(k)), int(v)) for k, v in inner.items()]))
+        return out
 
     def engine_operator_ids(self):
         """Engine ids of binary_operators / unary_operators (raises Unsupported

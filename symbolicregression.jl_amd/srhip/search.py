@@ -1,5 +1,9 @@
 """Lockstep search driver: the hot path's callers batched.
 
+`equation_search` dispatches: default Options (`fast_cycle=false`) run the
+reference's regularized evolution in srhip.evolution; this module keeps the
+`fast_cycle=true` variant described below.
+
 The reference scores one candidate at a time: `next_generation`
 (src/Mutate.jl:41-205) calls `score_func` per mutated tree, inside
 `reg_evol_cycle` (src/RegularizedEvolution.jl:13-155), inside `s_r_cycle`
@@ -167,15 +171,67 @@ def _new_op(left: Node, options: Options, nfeat: int, T, rng) -> Node:
     return Node(int(rng.integers(1, options.nuna + 1)), left)
 
 
+class _CallbackEvaluator:
+    """srhip.evolution's evaluator over the test hooks of equation_search."""
+
+    def __init__(self, dataset, options, scorer, batch_scorer, evaluator_factory):
+        self.dataset, self.options = dataset, options
+        self.scorer, self.batch_scorer, self.factory = scorer, batch_scorer, evaluator_factory
+
+    def losses(self, trees):
+        return np.asarray(self.scorer(trees), dtype=np.float64)
+
+    def losses_rows(self, trees, rows):
+        out = np.asarray([self.batch_scorer([t], r)[0] for t, r in zip(trees, rows)], dtype=np.float64)
+        return out, np.isfinite(out)
+
+    def optimize(self, trees, noise):
+        return optimize_constants_batch(self.dataset, trees, self.options, noise=noise,
+                                        evaluator_factory=self.factory)
+
+
 def equation_search(X: np.ndarray, y: np.ndarray, options: Options, niterations: int = 10,
                     weights: Optional[np.ndarray] = None, seed: int = 0, rank: int = 0, world: int = 1,
                     group=None, scorer: Optional[Callable[[Sequence[Node]], np.ndarray]] = None,
                     evaluator_factory: Optional[Callable] = None, verbose: bool = False,
-                    batch_scorer: Optional[Callable[[Sequence[Node], np.ndarray], np.ndarray]] = None):
-    """EquationSearch(X, y; niterations, options) with all islands in lockstep.
-    Returns (hall_of_fame, stats). `scorer(trees) -> losses` and
-    `batch_scorer(trees, row_idx) -> losses` replace the engine (tests run the
-    same driver over the CPU oracle)."""
+                    batch_scorer: Optional[Callable[[Sequence[Node], np.ndarray], np.ndarray]] = None,
+                    evaluator=None, lockstep: bool = True):
+    """EquationSearch(X, y; niterations, options). Returns (hall_of_fame, stats).
+
+    Default Options run the reference's regularized evolution
+    (`fast_cycle=false`: srhip.evolution, every island's candidates scored in
+    one launch); `options.fast_cycle=True` runs the fast_cycle variant below.
+    `evaluator` (losses / losses_rows / optimize), or the older hooks
+    `scorer(trees) -> losses`, `batch_scorer(trees, row_idx) -> losses` and
+    `evaluator_factory`, replace the engine (tests run the search over the CPU
+    oracle). `lockstep=False` answers every request alone, island after
+    island (the reference's one-tree-per-call schedule)."""
+    if not getattr(options, "fast_cycle", False):
+        from .evolution import EngineEvaluator, equation_search_default
+
+        dataset = Dataset(np.asarray(X), np.asarray(y), weights)
+        if evaluator is None and scorer is None:
+            evaluator = EngineEvaluator(dataset, options)
+        elif evaluator is None:
+            evaluator = _CallbackEvaluator(dataset, options, scorer, batch_scorer, evaluator_factory)
+        base = Node(val=dataset.avg_y)
+        dataset.baseline_loss = dataset.T(np.asarray(evaluator.losses([base]), dtype=np.float64)[0])
+        res = equation_search_default(dataset, options, niterations, evaluator, seed=seed, lockstep=lockstep,
+                                      rank=rank, world=world, group=group, verbose=verbose)
+        res.stats["result"] = res
+        return res.hall_of_fame, res.stats
+    return _equation_search_fast_cycle(X, y, options, niterations, weights, seed, rank, world, group, scorer,
+                                       evaluator_factory, verbose, batch_scorer)
+
+
+def _equation_search_fast_cycle(X, y, options, niterations, weights, seed, rank, world, group, scorer,
+                                evaluator_factory, verbose, batch_scorer):
+    """EquationSearch with `fast_cycle=true` (RegularizedEvolution.jl:32-79):
+    one baby per `tournament_selection_n`-member subsample, all islands in
+    lockstep."""
+    # RegularizedEvolution.jl:38-39
+    if options.tournament_selection_p != 1.0 or options.crossover_probability != 0.0:
+        raise AssertionError("fast_cycle needs tournament_selection_p == 1 and crossover_probability == 0")
     rng = np.random.default_rng(seed + 1000 * rank)
     dataset = Dataset(np.asarray(X), np.asarray(y), weights)
     T = np.dtype(dataset.T).type

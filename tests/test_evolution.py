@@ -1,0 +1,313 @@
+"""The reference's default regularized evolution (srhip.evolution), batched
+across islands: RegularizedEvolution.jl:81-155 (fast_cycle=false),
+Mutate.jl:25-341, Population.jl:79-148, SingleIteration.jl,
+SymbolicRegression.jl:539-866, MutationFunctions.jl, CheckConstraints.jl,
+AdaptiveParsimony.jl, Migration.jl, HallOfFame.jl.
+
+The central check: the lockstep driver (one evaluator call per round for
+every island's pending requests) reproduces the serial per-island schedule
+(one call per request, island after island — the reference's one tree per
+`score_func` call) EXACTLY, over the CPU oracle, with default Options
+(crossover, adaptive parsimony, tournament p = 0.86, constant optimisation),
+with batching, and sharded over two gloo ranks."""
+import numpy as np
+import pytest
+
+import oracle
+import srhip
+from srhip import Node, evolution as E
+from test_constant_optimization import OracleEvaluator
+
+
+class OracleSearchEvaluator:
+    """Test evaluator: every request on the CPU oracle, tree by tree independent."""
+
+    def __init__(self, o, X, y):
+        self.o, self.X, self.y = o, X, y
+        self.ds = srhip.Dataset(X, y)
+        self.calls = 0
+
+    def losses(self, trees):
+        self.calls += 1
+        flat = srhip.flatten(trees, self.o, dtype=self.X.dtype)
+        _, losses, ok = oracle.eval_loss_batch(flat, self.X, self.y, dtype=self.X.dtype)
+        return np.where(ok, losses.astype(np.float64), np.inf)
+
+    def losses_rows(self, trees, rows):
+        self.calls += 1
+        out, oks = [], []
+        for t, r in zip(trees, rows):
+            flat = srhip.flatten([t], self.o, dtype=self.X.dtype)
+            _, l, ok = oracle.eval_loss_batch(flat, self.X, self.y, row_idx=r, dtype=self.X.dtype)
+            out.append(float(l[0]) if ok[0] else np.inf)
+            oks.append(bool(ok[0]))
+        return np.asarray(out), np.asarray(oks)
+
+    def optimize(self, trees, noise):
+        self.calls += 1
+        return srhip.optimize_constants_batch(self.ds, trees, self.o, noise=noise,
+                                              evaluator_factory=lambda c: OracleEvaluator(c, self.o, self.X, self.y))
+
+
+def quickstart(n=100, T=np.float32, seed=0, **kw):
+    """README quickstart data (config #1): y = 2cos(x4) + x1² − 2, [+,*,/,-] / [cos,exp]."""
+    rng = np.random.default_rng(seed)
+    X = rng.standard_normal((5, n)).astype(T)
+    y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(T)
+    o = srhip.Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], **kw)
+    return X, y, o
+
+
+def _state(hof, stats):
+    res = stats["result"]
+    o = res.hall_of_fame.options
+    front = [(srhip.string_tree(m.tree, o), m.loss, m.score) for m in hof.pareto()]
+    pops = [[(srhip.string_tree(m.tree, o), m.loss, m.score, m.birth) for m in pop] for pop in res.populations]
+    return front, pops
+
+
+def _run(o, X, y, lockstep, niterations=2, seed=3):
+    ev = OracleSearchEvaluator(o, X, y)
+    hof, stats = srhip.equation_search(X, y, o, niterations=niterations, seed=seed, evaluator=ev, lockstep=lockstep)
+    return _state(hof, stats), stats, ev.calls
+
+
+def test_defaults_are_the_references():
+    o = srhip.Options()
+    assert not o.fast_cycle and o.crossover_probability == 0.066 and o.tournament_selection_p == 0.86
+    assert o.use_frequency and o.use_frequency_in_tournament and o.adaptive_parsimony_scaling == 20.0
+    assert o.migration and o.hof_migration and o.skip_mutation_failures and o.warmup_maxsize_by == 0.0
+    assert E._mutation_weights(o) == E.DEFAULT_MUTATION_WEIGHTS
+
+
+def test_lockstep_equals_serial_default_options():
+    """Islands batched per round give the serial, one-tree-per-call result bit
+    for bit: hall of fame, every population member (tree, loss, score, birth)."""
+    X, y, o = quickstart(npopulations=4, ncycles_per_iteration=12, optimizer_probability=0.3)
+    a, sa, calls_a = _run(o, X, y, lockstep=True)
+    b, sb, calls_b = _run(o, X, y, lockstep=False)
+    assert a == b
+    assert sa["evals"] == sb["evals"]
+    # the batch point: one evaluator call per round instead of one per request
+    assert calls_a * 3 < calls_b
+    assert sa["trees_scored"] == sb["trees_scored"]
+
+
+def test_lockstep_equals_serial_with_batching_and_annealing():
+    X, y, o = quickstart(npopulations=3, ncycles_per_iteration=10, batching=True, batch_size=20, annealing=True,
+                         crossover_probability=0.3, warmup_maxsize_by=0.5)
+    a, sa, _ = _run(o, X, y, lockstep=True, seed=11)
+    b, sb, _ = _run(o, X, y, lockstep=False, seed=11)
+    assert a == b and sa["evals"] == sb["evals"]
+
+
+def test_search_improves_and_hall_of_fame_is_consistent():
+    X, y, o = quickstart(npopulations=4, ncycles_per_iteration=40)
+    ev = OracleSearchEvaluator(o, X, y)
+    hof, stats = srhip.equation_search(X, y, o, niterations=3, seed=1, evaluator=ev)
+    front = hof.pareto()
+    baseline = ev.losses([Node(val=float(np.mean(y)))])[0]
+    assert front and min(m.loss for m in front) < 0.75 * baseline
+    np.testing.assert_array_equal(ev.losses([m.tree for m in front]), [m.loss for m in front])
+    # Pareto: losses strictly decrease with complexity
+    losses = [m.loss for m in front]
+    assert all(a > b for a, b in zip(losses, losses[1:]))
+    assert stats["evals"] > 4 * 3 * 40 * 2 and stats["evals_per_s"] > 0
+    assert srhip.print_hall_of_fame(hof, o)
+
+
+# ----------------------------------------------------------- host routines
+def _o():
+    return srhip.Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"])
+
+
+def test_mutations_leave_the_parent_unchanged():
+    o = _o()
+    rng = np.random.default_rng(0)
+    trees = srhip.random_population(40, o, 5, np.float32, seed=2)
+    T = np.float32
+    for t in trees:
+        before = srhip.string_tree(t, o)
+        n = srhip.count_nodes(t)
+        for f in (lambda c: E.mutate_constant(c, T(1.0), o, T, rng), lambda c: E.mutate_operator(c, o, rng),
+                  lambda c: E.append_random_op(c, o, 5, T, rng), lambda c: E.prepend_random_op(c, o, 5, T, rng),
+                  lambda c: E.insert_random_op(c, o, 5, T, rng), lambda c: E.delete_random_op(c, o, 5, T, rng)):
+            m = f(E.copy_node(t))
+            srhip.flatten([m], o)
+        assert srhip.string_tree(t, o) == before
+        a, b = E.crossover_trees(t, trees[0], rng)
+        assert srhip.count_nodes(a) + srhip.count_nodes(b) == n + srhip.count_nodes(trees[0])
+        assert srhip.string_tree(t, o) == before
+    # insert / prepend add exactly one or two nodes; mutate_operator keeps the size
+    t = trees[5]
+    n = srhip.count_nodes(t)
+    assert srhip.count_nodes(E.mutate_operator(E.copy_node(t), o, rng)) == n
+    assert srhip.count_nodes(E.prepend_random_op(E.copy_node(t), o, 5, T, rng)) in (n + 1, n + 2)
+    assert srhip.count_nodes(E.insert_random_op(E.copy_node(t), o, 5, T, rng)) in (n + 1, n + 2)
+
+
+def test_mutate_constant_negates_as_written():
+    """MutationFunctions.jl:74-76: `rand() > probability_negate_constant` negates."""
+    o = _o()
+    rng = np.random.default_rng(1)
+    flips = 0
+    for _ in range(400):
+        t = E.mutate_constant(Node(val=np.float32(1.0)), np.float32(1.0), o, np.float32, rng)
+        flips += t.val < 0
+        assert 1 / 1.176 - 1e-6 <= abs(t.val) <= 1.176 + 1e-6  # (1 + 0.1 + 0.076·T)^U(0,1)
+    assert flips > 380
+
+
+def test_simplify_and_combine_operators():
+    o = _o()
+    B, U = o.make_binary, o.make_unary
+    T = np.float32
+    x1 = Node("x1")
+    t = B("+", B("*", Node(val=T(2.0)), Node(val=T(3.0))), U("cos", Node(val=T(0.0))))
+    s = E.simplify_tree(t, o, T)
+    assert s.degree == 0 and s.val == T(7.0)
+    # a non-finite fold is kept as a tree (x / 0 with constants)
+    s = E.simplify_tree(B("/", Node(val=T(1.0)), Node(val=T(0.0))), o, T)
+    assert s.degree == 2
+    # ((c + x) + c2) -> (x + (c + c2)): the inner sum is first rewritten (x + c), then combined
+    t = B("+", B("+", Node(val=T(1.5)), x1), Node(val=T(2.0)))
+    c = E.combine_operators(t, o, T)
+    assert srhip.string_tree(c, o) == "(x1 + 3.5)"
+    t = B("*", Node(val=T(2.0)), B("*", x1, Node(val=T(4.0))))
+    assert srhip.string_tree(E.combine_operators(t, o, T), o) == "(x1 * 8.0)"
+    # the four subtraction nestings, checked by value at x1 = 0.7
+    for t in (B("-", Node(val=T(5.0)), B("-", Node(val=T(2.0)), x1)),
+              B("-", Node(val=T(5.0)), B("-", x1, Node(val=T(2.0)))),
+              B("-", B("-", Node(val=T(5.0)), x1), Node(val=T(2.0))),
+              B("-", B("-", x1, Node(val=T(5.0))), Node(val=T(2.0)))):
+        X = np.full((1, 3), 0.7, dtype=T)
+        before = oracle.eval_trees(srhip.flatten([t], o, dtype=T), X, dtype=T)
+        c = E.combine_operators(E.copy_node(t), o, T)
+        assert srhip.count_nodes(c) == 3
+        after = oracle.eval_trees(srhip.flatten([c], o, dtype=T), X, dtype=T)
+        np.testing.assert_allclose(after[0][0], before[0][0], rtol=1e-6)
+
+
+def test_check_constraints_size_test_is_the_references():
+    """CheckConstraints.jl:144 `0 > size > maxsize` never holds: size is not
+    enforced; operator constraints are."""
+    o = srhip.Options(binary_operators=["+", "*"], unary_operators=["cos"], constraints={"cos": 1, "*": (3, -1)})
+    B, U = o.make_binary, o.make_unary
+    big = B("+", B("+", Node("x1"), Node("x2")), B("+", Node("x3"), B("+", Node("x1"), Node("x2"))))
+    assert E.check_constraints(B("+", Node("x1"), Node("x2")), o, 1)  # size 3 > maxsize 1: allowed
+    assert E.check_constraints(U("cos", Node("x1")), o, 20)
+    assert not E.check_constraints(U("cos", B("+", Node("x1"), Node("x2"))), o, 20)
+    assert E.check_constraints(B("*", B("+", Node("x1"), Node("x2")), big), o, 20)
+    assert not E.check_constraints(B("*", B("+", Node("x1"), B("+", Node("x2"), Node("x3"))), Node("x1")), o, 20)
+    n = srhip.Options(binary_operators=["+"], unary_operators=["cos", "exp"], nested_constraints={"cos": {"cos": 0}})
+    U = n.make_unary
+    assert E.check_constraints(U("cos", U("exp", Node("x1"))), n, 20)
+    assert not E.check_constraints(U("cos", U("exp", U("cos", Node("x1")))), n, 20)
+
+
+def test_running_search_statistics_window():
+    o = srhip.Options(maxsize=10)
+    st = E.RunningSearchStatistics(o, window_size=50)
+    assert st.frequencies.size == 12 and np.isclose(st.snapshot().sum(), 1)
+    for s in [3] * 60 + [5] * 20:
+        st.update_frequencies(s)
+    st.update_frequencies(0)
+    st.update_frequencies(13)  # outside 1..maxsize+2: ignored
+    assert st.frequencies.sum() == 12 + 80
+    st.move_window()
+    assert abs(st.frequencies.sum() - 50) < 1e-6 and st.frequencies.min() >= 1 - 1e-12
+    assert st.frequencies[2] == 39 and st.frequencies[4] == 1  # both reduced by 20, then size 3 by 2
+
+
+def test_best_of_sample_tournament():
+    """p = 0.86: the best of the sample wins with probability ~0.86 (ranks by score)."""
+    o = _o()
+    o.use_frequency_in_tournament = False
+    o.tournament_selection_n = 12
+    S = E.Search(o, 5, 100, np.float32, 1.0)
+    isl = E.Island(0, 0)
+    isl.pop = [E.PopMember(Node(val=np.float32(i)), float(i), float(i), i) for i in range(33)]
+    first = 0
+    for k in range(2000):
+        isl.rng = np.random.default_rng(k)
+        idx = np.random.default_rng(k).permutation(33)[:12]  # the sample best_of_sample draws
+        first += E.best_of_sample(isl, S, np.ones(22) / 22).score == min(idx)
+    assert 0.82 < first / 2000 < 0.90
+
+
+def _world_worker(rank, world, port, q):
+    import os
+    import sys
+    from pathlib import Path
+
+    root = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(root / "symbolicregression.jl_amd"), str(root / "oracle"), str(root / "tests")]
+    import torch.distributed as dist
+
+    import srhip as S
+    from test_evolution import OracleSearchEvaluator as OSE, _state as st, quickstart as qs
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    X, y, o = qs(npopulations=4, ncycles_per_iteration=8)
+    hof, stats = S.equation_search(X, y, o, niterations=2, seed=7, rank=rank, world=world,
+                                   evaluator=OSE(o, X, y))
+    q.put((rank, st(hof, stats), stats["evals"]))
+    dist.destroy_process_group()
+
+
+@pytest.mark.timeout(180)
+def test_islands_sharded_over_two_ranks_give_the_single_process_result():
+    """Islands i % world == rank on each rank; every rank runs the head node
+    on all islands' results (all_gather_object): the same search as world 1."""
+    import torch.multiprocessing as mp
+    from test_distributed import free_port
+
+    X, y, o = quickstart(npopulations=4, ncycles_per_iteration=8)
+    ref, sref, _ = _run(o, X, y, lockstep=True, seed=7)
+    world = 2
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = free_port()
+    procs = [ctx.Process(target=_world_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=150) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    for rank, state, evals in res:
+        assert state == ref
+        assert evals == sref["evals"]
+
+
+@pytest.mark.gpu
+def test_default_search_on_engine_quickstart(gpu_ctx):
+    """Config #1 shape on the engine with default Options: the hall of fame's
+    losses are the oracle's for the same trees."""
+    X, y, o = quickstart(npopulations=20, ncycles_per_iteration=60)
+    hof, stats = srhip.equation_search(X, y, o, niterations=3, seed=1)
+    front = hof.pareto()
+    ref = OracleSearchEvaluator(o, X, y).losses([m.tree for m in front])
+    np.testing.assert_allclose([m.loss for m in front], ref, rtol=1e-5)
+    assert min(m.loss for m in front) < 0.75 * float(np.var(y))
+    assert stats["launches"] < 3 * 60 * 3 + 200  # one launch per round, not per tree
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(400)
+def test_config1_full_size_default_options_on_engine(gpu_ctx):
+    """BASELINE config #1 at its stated size: README quickstart data,
+    npopulations = 20, niterations = 40, every other Options field at the
+    reference's default (fast_cycle = false, crossover 0.066, tournament
+    p = 0.86, adaptive parsimony, constant optimisation 0.14). Every hall-of-fame
+    loss is rechecked on the CPU oracle."""
+    X, y, o = quickstart(npopulations=20)
+    assert (o.ncycles_per_iteration, o.npop, o.maxsize) == (550, 33, 20)
+    hof, stats = srhip.equation_search(X, y, o, niterations=40, seed=0)
+    front = hof.pareto()
+    ref = OracleSearchEvaluator(o, X, y).losses([m.tree for m in front])
+    np.testing.assert_allclose([m.loss for m in front], ref, rtol=1e-5)
+    assert stats["iterations"] == 40 and stats["launches"] > 40 * 1500
+    assert min(m.loss for m in front) < 0.05 * float(np.var(y))
+    print({k: v for k, v in stats.items() if k != "result"})

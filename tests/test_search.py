@@ -1,6 +1,7 @@
-"""Lockstep search driver (srhip.equation_search): the callers of the hot path
-batched across islands (RegularizedEvolution.jl
-fast_cycle, SingleIteration.jl, SymbolicRegression.jl migration).
+"""Lockstep search driver, `fast_cycle=true` variant (srhip.search): the
+callers of the hot path batched across islands (SURVEY.md §8(f) rank 1;
+RegularizedEvolution.jl fast_cycle, SingleIteration.jl, SymbolicRegression.jl
+migration). The default path (fast_cycle=false) is tests/test_evolution.py.
 
 CPU tests run the driver over the oracle (scorer / evaluator_factory
 injection); the GPU test runs it on the engine with the README quickstart
@@ -19,7 +20,8 @@ def quickstart(n=100, T=np.float32, seed=0):
     X = rng.standard_normal((5, n)).astype(T)
     y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(T)
     o = srhip.Options(binary_operators=["+", "*", "/", "-"], unary_operators=["cos", "exp"], npopulations=4,
-                      ncycles_per_iteration=40)
+                      ncycles_per_iteration=40, fast_cycle=True, crossover_probability=0.0,
+                      tournament_selection_p=1.0)
     return X, y, o
 
 
@@ -73,8 +75,9 @@ def test_options_search_parameters_and_unknown_keywords():
     with pytest.raises(TypeError):
         srhip.Options(not_an_option=1)  # Options.jl:389: error("Unknown keyword argument")
     with pytest.warns(UserWarning):
-        w = srhip.Options(crossover_probability=0.1)  # control-plane keyword: kept, ignored
-    assert w.ignored == {"crossover_probability": 0.1}
+        w = srhip.Options(output_file="hof.csv")  # control-plane keyword: kept, ignored
+    assert w.ignored == {"output_file": "hof.csv"}
+    assert srhip.Options(crossover_probability=0.1).crossover_probability == 0.1  # a search option now
 
 
 def test_annealing_acceptance_uses_ieee_semantics():
@@ -182,7 +185,7 @@ def test_options_deprecated_aliases_and_optimizer_options():
         o = srhip.Options(batchSize=77, ncyclesperiteration=9, ns=5, hofMigration=False,
                           optimizer_options={"iterations": 3})
     assert (o.batch_size, o.ncycles_per_iteration, o.tournament_selection_n, o.optimizer_iterations) == (77, 9, 5, 3)
-    assert o.ignored == {"hof_migration": False}
+    assert o.ignored == {} and o.hof_migration is False
     assert sum(issubclass(x.category, DeprecationWarning) for x in w) == 4
     with pytest.raises(srhip.Unsupported):
         srhip.Options(optimizer_options={"g_abstol": 1e-3})
