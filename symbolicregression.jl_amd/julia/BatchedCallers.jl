@@ -10,6 +10,11 @@
 #
 #   * `population_batched`      — Population(dataset; npop, nlength, options, nfeatures)
 #   * `finalize_scores_batched` — finalize_scores(dataset, pop, options)
+#   * `reg_evol_cycle_lockstep` — reg_evol_cycle with the reference's DEFAULT
+#     semantics (fast_cycle = false: best_of_sample, next_generation or
+#     crossover_generation, replace-oldest, step by step per island), every
+#     island's candidates of a step — both crossover children included — in
+#     one launch; `s_r_cycle_lockstep` runs a whole s_r_cycle that way.
 #   * `reg_evol_cycle_batched`  — reg_evol_cycle with fast_cycle semantics
 #     (one baby per tournament_selection_n-member subsample, replace-oldest),
 #     for several islands in lockstep: every island's babies in one launch,
@@ -28,9 +33,9 @@
 # mutation needs no score (simplify, optimize, do_nothing, a failed
 # constraint check) is decided in `propose`, as in the reference.
 #
-# UNTESTED AS JULIA (no Julia in the build image). The Python mirror of the
-# same lockstep loop (symbolicregression.jl_amd/srhip/search.py) runs in the
-# test suite; tests/test_julia_binding.py checks this file's references to
+# UNTESTED AS JULIA (no Julia in the build image). The Python mirrors of the
+# same lockstep loops (symbolicregression.jl_amd/srhip/evolution.py for the
+# default path, srhip/search.py for fast_cycle) run in the test suite; tests/test_julia_binding.py checks this file's references to
 # the reference's functions and to SRHip statically.
 module BatchedCallers
 
@@ -40,11 +45,12 @@ import ..ComplexityModule: compute_complexity
 import ..LossFunctionsModule: score_func, score_func_batch, loss_to_score
 import ..CheckConstraintsModule: check_constraints
 import ..AdaptiveParsimonyModule: RunningSearchStatistics
-import ..PopMemberModule: PopMember
-import ..PopulationModule: Population
+import ..PopMemberModule: PopMember, copy_pop_member
+import ..PopulationModule: Population, best_of_sample
+import ..HallOfFameModule: HallOfFame
 import ..MutationFunctionsModule:
     gen_random_tree, gen_random_tree_fixed_size, mutate_constant, mutate_operator, append_random_op,
-    prepend_random_op, insert_random_op, delete_random_op
+    prepend_random_op, insert_random_op, delete_random_op, crossover_trees
 import ..ConstantOptimizationModule: optimize_constants
 import ..UtilsModule: get_birth_order
 import ..PopMemberModule: generate_reference
@@ -355,5 +361,160 @@ function reg_evol_cycle_batched(dataset::Dataset{T}, pops::AbstractVector{<:Popu
 end
 
 shuffle!(v) = (for i in length(v):-1:2; j = rand(1:i); v[i], v[j] = v[j], v[i]; end; v)
+
+# ---- reg_evol_cycle, DEFAULT semantics (fast_cycle = false), islands in lockstep ----------
+
+# One island's step in flight: a mutation (Proposal) or a crossover pair.
+struct Step{T}
+    crossover::Bool
+    prop::Union{Proposal{T},Nothing}        # mutation: next_generation's proposal
+    parents::Tuple{Vararg{PopMember{T}}}     # crossover: (allstar1, allstar2)
+    children::Union{Tuple{Node{T},Node{T}},Nothing}  # crossover children; nothing = failed constraints
+end
+
+"""
+    crossover_children(m1, m2, curmaxsize, options) -> (child1, child2) or nothing
+
+crossover_generation (src/Mutate.jl:285-313) up to its score_func calls:
+crossover_trees until both children pass check_constraints, at most 11 tries.
+"""
+function crossover_children(m1::PopMember{T}, m2::PopMember{T}, curmaxsize::Int, options::Options) where {T}
+    c1, c2 = crossover_trees(m1.tree, m2.tree)
+    num_tries = 1
+    while !(check_constraints(c1, options, curmaxsize) && check_constraints(c2, options, curmaxsize))
+        num_tries > 10 && return nothing
+        c1, c2 = crossover_trees(m1.tree, m2.tree)
+        num_tries += 1
+    end
+    return (c1, c2)
+end
+
+"""
+    reg_evol_cycle_lockstep(dataset, pops, temperature, curmaxsize, stats, options) -> (pops, num_evals)
+
+reg_evol_cycle with the reference's DEFAULT semantics (src/RegularizedEvolution.jl:81-155:
+`fast_cycle = false`, crossover with probability `crossover_probability`,
+`best_of_sample` tournaments with `tournament_selection_p`) for every island
+of `pops` in lockstep. Each of the round(npop / tournament_selection_n) steps
+is taken by every island together: its own `rand() > crossover_probability`
+draw, `best_of_sample` (once, or twice for crossover), the mutation proposal
+or the crossover children; then ALL islands' candidates — every mutated tree
+and both children of every crossover — are scored in ONE launch, and each
+island accepts and replaces its oldest member(s) in the reference's order.
+Within an island the steps stay sequential (step i+1's tournament sees step
+i's replacement), so each island runs the reference's algorithm unchanged;
+`stats[k]` is island k's RunningSearchStatistics (the copy its worker holds).
+The Python mirror (srhip/evolution.py) is tested to give, over the oracle,
+exactly the serial per-island result.
+"""
+function reg_evol_cycle_lockstep(dataset::Dataset{T}, pops::AbstractVector{<:Population}, temperature,
+                                 curmaxsize::Int, stats::AbstractVector{RunningSearchStatistics},
+                                 options::Options) where {T}
+    num_evals = 0.0
+    nsteps = round(Int, pops[1].n / options.tournament_selection_n)
+    for _ in 1:nsteps
+        steps = Vector{Step{T}}(undef, length(pops))
+        for (k, pop) in enumerate(pops)
+            if rand() > options.crossover_probability
+                allstar = best_of_sample(pop, stats[k], options)
+                before = if options.batching  # src/Mutate.jl:41-47
+                    bs, bl = score_func_batch(dataset, allstar.tree, options)
+                    num_evals += options.batch_size / dataset.n
+                    (bs, bl)
+                else
+                    (allstar.score, allstar.loss)
+                end
+                steps[k] = Step{T}(false, propose(dataset, allstar, before, temperature, curmaxsize, options),
+                                   (allstar,), nothing)
+            else
+                a1 = best_of_sample(pop, stats[k], options)
+                a2 = best_of_sample(pop, stats[k], options)
+                steps[k] = Step{T}(true, nothing, (a1, a2), crossover_children(a1, a2, curmaxsize, options))
+            end
+        end
+        # every :optimize proposal of this step, all islands, in one optimiser call
+        to_opt = PopMember{T}[s.prop.member for s in steps if !s.crossover && s.prop.optimize]
+        num_evals += sum(optimize_constants_batched(dataset, to_opt, options); init=0.0)
+        # ONE launch: mutated trees and both crossover children of every island
+        trees = Node{T}[]
+        for s in steps
+            if s.crossover
+                s.children === nothing || append!(trees, s.children)
+            elseif s.prop.member === nothing
+                push!(trees, s.prop.tree)
+            end
+        end
+        scores, losses = options.batching ? score_batch_minibatch(dataset, trees, options) :
+                         score_batch(dataset, trees, options)
+        j = 0
+        for (k, pop) in enumerate(pops)
+            s = steps[k]
+            if !s.crossover
+                p = s.prop
+                num_evals += p.num_evals
+                baby, accepted = if p.member === nothing
+                    j += 1
+                    num_evals += options.batching ? options.batch_size / dataset.n : 1.0
+                    accept(p, scores[j], losses[j], temperature, stats[k], options)
+                else
+                    (p.member, p.accepted)
+                end
+                (!accepted && options.skip_mutation_failures) && continue
+                pop.members[argmin([m.birth for m in pop.members])] = baby
+            else
+                a1, a2 = s.parents
+                if s.children === nothing
+                    options.skip_mutation_failures && continue
+                    b1, b2 = a1, a2  # a failed crossover returns member1, member2 (src/Mutate.jl:309)
+                else
+                    b1 = PopMember(s.children[1], scores[j + 1], losses[j + 1]; parent=a1.ref,
+                                   deterministic=options.deterministic)
+                    b2 = PopMember(s.children[2], scores[j + 2], losses[j + 2]; parent=a2.ref,
+                                   deterministic=options.deterministic)
+                    j += 2
+                    # src/Mutate.jl:314-322: 2·batch_size/n with batching, batch_size/n without
+                    num_evals += options.batching ? 2 * (options.batch_size / dataset.n) :
+                                 options.batch_size / dataset.n
+                end
+                pop.members[argmin([m.birth for m in pop.members])] = b1
+                pop.members[argmin([m.birth for m in pop.members])] = b2
+            end
+        end
+    end
+    return pops, num_evals
+end
+
+"""
+    s_r_cycle_lockstep(dataset, pops, ncycles, curmaxsize, stats, options) -> (pops, best_seen, num_evals)
+
+s_r_cycle (src/SingleIteration.jl:17-61) for every island at once: the
+temperature schedule, reg_evol_cycle_lockstep (or reg_evol_cycle_batched when
+options.fast_cycle), and each island's best-seen hall of fame. The head node
+calls it once per round with every island it would have spawned, instead of
+one @sr_spawner job per island (INTEGRATION.md §4).
+"""
+function s_r_cycle_lockstep(dataset::Dataset{T}, pops::AbstractVector{<:Population}, ncycles::Int,
+                            curmaxsize::Int, stats::AbstractVector{RunningSearchStatistics},
+                            options::Options) where {T}
+    max_temp = T(1.0)
+    min_temp = options.annealing ? T(0.0) : max_temp
+    best_seen = [HallOfFame(options, T) for _ in pops]
+    num_evals = 0.0
+    for temperature in LinRange(max_temp, min_temp, ncycles)
+        _, ev = options.fast_cycle ?
+                reg_evol_cycle_batched(dataset, pops, temperature, curmaxsize, stats, options) :
+                reg_evol_cycle_lockstep(dataset, pops, temperature, curmaxsize, stats, options)
+        num_evals += ev
+        for (k, pop) in enumerate(pops), member in pop.members
+            size = compute_complexity(member.tree, options)
+            if 0 < size <= options.maxsize &&
+               (!best_seen[k].exists[size] || member.score < best_seen[k].members[size].score)
+                best_seen[k].exists[size] = true
+                best_seen[k].members[size] = copy_pop_member(member)
+            end
+        end
+    end
+    return pops, best_seen, num_evals
+end
 
 end # module

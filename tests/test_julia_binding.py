@@ -185,13 +185,15 @@ def test_batched_callers_use_existing_functions():
         imported += [n.strip() for n in m.group(2).split(",")]
     assert {"next_generation"} .isdisjoint(imported)  # it is split, not called
     for need in ("mutate_constant", "mutate_operator", "append_random_op", "prepend_random_op", "insert_random_op",
-                 "delete_random_op", "check_constraints", "score_func", "loss_to_score", "optimize_constants"):
+                 "delete_random_op", "check_constraints", "score_func", "loss_to_score", "optimize_constants",
+                 "best_of_sample", "crossover_trees"):
         assert need in imported, need
     srhip_jl = JL.read_text()
     for call in set(re.findall(r"SRHip\.([\w!]+)", code)):
         c = re.escape(call)
         assert re.search(rf"(function {c}\(|struct {c}\b|^{c}\()", srhip_jl, re.M), f"SRHip.{call} missing"
-    for fn in ("population_batched", "finalize_scores_batched", "reg_evol_cycle_batched", "propose", "accept"):
+    for fn in ("population_batched", "finalize_scores_batched", "reg_evol_cycle_batched", "propose", "accept",
+               "reg_evol_cycle_lockstep", "s_r_cycle_lockstep", "crossover_children"):
         assert re.search(rf"^function {fn}\(", code, re.M), fn
     if REFERENCE_SRC.exists():
         defs = "\n".join(p.read_text() for p in REFERENCE_SRC.glob("*.jl"))
