@@ -35,6 +35,7 @@ the same bounded row sample of the same workload.
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -146,7 +147,7 @@ def main():
         if args.stub:
             tdist.init_process_group("gloo")
         elif SHARED_GPU:
-            # rehearsal of the N > 1 paths on a one-GPU box (tools/gpu_bench_n2.sh):
+            # rehearsal of the N > 1 paths on a one-GPU box (tools/gpu_run.sh n2):
             # every rank on GPU 0, gloo, host-side reductions; not a measurement
             torch.cuda.set_device(0)
             tdist.init_process_group("gloo")
@@ -271,14 +272,25 @@ def main():
     esz = np.dtype(T).itemsize
     alg_bytes = X.shape[1] * (args.nfeat + 1) * esz + prog.ntrees * 17
     roof["hbm_algorithmic_GBs"] = alg_bytes / (k_ms * 1e-3) / 1e9
+    # counter fields from the rocprofv3 --pmc passes of this bench command
+    # (tools/gpu_run.sh profile → profiles/current_pmc_summary.json), attached
+    # only when that summary measured the kernel this run launched, from the
+    # same libsrhip.so (kernel symbol + sha256 of the library)
+    ran = ctx.last_kernel_name()
+    lib_sha = hashlib.sha256(srhip._lib.LIB_PATH.read_bytes()).hexdigest()
+    roof["kernel"] = ran
     prof = ROOT / "profiles" / "current_pmc_summary.json"
     if prof.exists():
         try:
             pm = json.loads(prof.read_text())
-            if pm.get("kernel") and pm.get("workload") == "config#2":
+            same = pm.get("kernel") == ran and pm.get("lib_sha256") == lib_sha and pm.get("workload") == "config#2"
+            if same and args.rows == 1_000_000 and args.ntrees == 4096 and world == 1:
                 roof["traffic"] = pm.get("hbm_bytes_per_launch")
                 roof["valu_busy"] = pm.get("valu_busy")
                 roof["pmc_source"] = "profiles/current_pmc_summary.json (rocprofv3 --pmc passes of this bench)"
+            else:
+                roof["pmc_source"] = (f"none: profiles/current_pmc_summary.json measured {pm.get('kernel')} "
+                                      f"from lib {str(pm.get('lib_sha256'))[:12]}, this run {ran} from {lib_sha[:12]}")
         except Exception:
             pass
 

@@ -163,6 +163,11 @@ int32_t srhip_op_lookup(const char* name, int32_t* out_arity, int32_t* out_id);
 int32_t srhip_op_eval(int32_t dtype, int32_t arity, int32_t id, double a, double b,
                       double* out);
 
+/* The symbol name of the main evaluation kernel the calling thread launched
+ * last ("sr_jit_eval_dlp", "eval_kernel<float>", "sr_jit_grad_dl", ...), as
+ * rocprofv3 reports it: ties a profile to the kernel that ran (bench.py). */
+int32_t srhip_last_kernel_name(char* buf, int32_t len);
+
 /* ---- dataset: Dataset(X, y; weights) src/Dataset.jl:43-64 ----------------
  * Uploads rows [row_begin, row_end) of X / y / w once (the row shard of this
  * device); X is transposed to feature-major on the device. w may be NULL

@@ -30,6 +30,14 @@
 #include "jit.h"
 #include "kernels.h"
 
+namespace srhip {
+namespace {
+thread_local const char* t_last_kernel = "";
+}
+void note_kernel(const char* name) { t_last_kernel = name ? name : ""; }
+const char* last_kernel() { return t_last_kernel; }
+}  // namespace srhip
+
 using namespace srhip;
 
 namespace {
@@ -725,16 +733,32 @@ void ensure_pinned(srhip_ctx* c, size_t nt);
 // Wait for a call's last launch by polling the stream instead of the runtime's
 // blocking wait: hipStreamSynchronize sleeps on a completion interrupt, whose
 // wake-up costs tens of microseconds per call on an idle host (more when the
-// cores sit in deep C-states), on every synchronous eval_loss. SRHIP_SPIN=0:
-// the blocking wait (A/B measurements).
+// cores sit in deep C-states), on every synchronous eval_loss. The spin is
+// bounded (SRHIP_SPIN_US, default 200 µs: a loss call of a search-sized batch
+// ends well within it) and then falls back to the blocking wait, so a long
+// kernel (config #5's 48 ms gradients) does not hold a host core that the
+// caller's other threads need. SRHIP_SPIN=0: the blocking wait (A/B).
 void wait_stream(hipStream_t s) {
   const char* e = std::getenv("SRHIP_SPIN");  // read per call: A/B measurements
   if (e && e[0] == '0') {
     HIP_CHECK(hipStreamSynchronize(s));
     return;
   }
+  static const double budget_us = [] {
+    const char* b = std::getenv("SRHIP_SPIN_US");
+    return b ? std::max(0.0, std::atof(b)) : 200.0;
+  }();
+  const auto t0 = std::chrono::steady_clock::now();
   hipError_t r;
-  while ((r = hipStreamQuery(s)) == hipErrorNotReady) __builtin_ia32_pause();
+  int k = 0;
+  while ((r = hipStreamQuery(s)) == hipErrorNotReady) {
+    __builtin_ia32_pause();
+    if ((++k & 63) == 0 &&
+        std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count() > budget_us) {
+      HIP_CHECK(hipStreamSynchronize(s));
+      return;
+    }
+  }
   HIP_CHECK(r);
 }
 
@@ -816,7 +840,9 @@ void build_program(srhip_program* p) {
     // Float64 tree code (jit64.cpp) for the shallow trees of large batches;
     // SRHIP_JIT64=0: interpreted
     static const bool on64 = [] { const char* e = std::getenv("SRHIP_JIT64"); return !(e && e[0] == '0'); }();
-    if (on64 && p->jit_allowed && jit_wanted((int)a.size()) && jit::available64()) {
+    // Float64 tree code holds its constants as literals: a VARYING_CONSTANTS program (the
+    // optimiser's candidates) would rebuild it interpreted at its first set_constants
+    if (on64 && p->jit_allowed && !p->jit_memc && jit_wanted((int)a.size()) && jit::available64()) {
       std::vector<int32_t> jl, rest;
       p->jit64 = jit::build64(cb, a, jl, rest, &p->jit_stats);
       if (p->jit64) {
@@ -1022,6 +1048,7 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, jit::Module* jm, const E
     c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<T>));
     a.partial = static_cast<Part<T>*>(c->partial.p);
     const int tk = timed_begin(c, s);
+    note_kernel(sizeof(T) == 4 ? "eval_kernel<float>" : "eval_kernel<double>");
     HIP_CHECK(launch_eval<T>(plan, a, MODE_LOSS, s));
     timed_end(c, s, tk);
     HIP_CHECK(launch_finalize<T>(a, c->res_sum, c->res_ok, s));
@@ -1340,6 +1367,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
         HIP_CHECK(jit::launch64(jm64, launches[li].part, plan, a, s));
       }
     } else {
+      note_kernel(sizeof(T) == 4 ? "eval_kernel<float>" : "eval_kernel<double>");
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
     timed_end(c, s, tk);
@@ -1711,6 +1739,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
     a.out_grad = out_grad;
     a.out_stride = out_stride;
     const int tk = timed_begin(c, s);
+    note_kernel(sizeof(T) == 4 ? "grad_kernel<float>" : "grad_kernel<double>");
     HIP_CHECK(launch_grad<T>(plan, a, mode, s));
     timed_end(c, s, tk);
     HIP_CHECK(launch_grad_finalize<T>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p),
@@ -1914,6 +1943,14 @@ int32_t srhip_op_lookup(const char* name, int32_t* out_arity, int32_t* out_id) {
       }
     }
     throw Error(SRHIP_ERR_UNSUPPORTED, std::string("operator not supported by the engine: ") + name);
+  });
+}
+
+int32_t srhip_last_kernel_name(char* buf, int32_t len) {
+  return guarded([&] {
+    if (!buf || len <= 0) throw Error(SRHIP_ERR_INVALID, "null or empty buffer");
+    std::snprintf(buf, (size_t)len, "%s", srhip::last_kernel());
+    return SRHIP_OK;
   });
 }
 

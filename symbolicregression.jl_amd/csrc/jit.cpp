@@ -1544,13 +1544,22 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + (ja.part_lds ? part_bytes : 0) + 16;
   // the hand-written loop keeps its tree counter in the last 16 bytes
   hipFunction_t fn = a.w ? q.fn_w : q.fn;
-  if (q.fn_dl && !m->out && dynloop()) fn = a.w ? q.fn_dlw : q.fn_dl;
+  const char* name = m->out ? (m->memc ? "sr_jit_out_m" : "sr_jit_out")
+                            : m->memc ? (a.w ? "sr_jit_eval_mw" : "sr_jit_eval_m") : (a.w ? "sr_jit_eval_w" : "sr_jit_eval");
+  if (q.fn_dl && !m->out && dynloop()) {
+    fn = a.w ? q.fn_dlw : q.fn_dl;
+    name = m->memc ? (a.w ? "sr_jit_eval_dlmw" : "sr_jit_eval_dlm") : (a.w ? "sr_jit_eval_dlw" : "sr_jit_eval_dl");
+  }
   // literal code: the loop that claims the next tree and loads its flag and
   // code offset before running this one (interleaved A/B, profiles/
   // r04_loop_ab.jsonl: config #2 3.247 → 3.231 ms, a 512-tree shard 0.503 →
   // 0.483); SRHIP_JIT_PREFETCH=0 (read per launch): without
   static const auto prefetch = [] { const char* e = std::getenv("SRHIP_JIT_PREFETCH"); return !(e && e[0] == '0'); };
-  if (q.fn_dlp && !m->out && dynloop() && prefetch()) fn = a.w ? q.fn_dlpw : q.fn_dlp;
+  if (q.fn_dlp && !m->out && dynloop() && prefetch()) {
+    fn = a.w ? q.fn_dlpw : q.fn_dlp;
+    name = a.w ? "sr_jit_eval_dlpw" : "sr_jit_eval_dlp";
+  }
+  note_kernel(name);
   return hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds + pad, stream, nullptr, cfg);
 }
 

@@ -697,7 +697,9 @@ hipError_t launch64(Module64* m, int k, const EvalPlan& plan, const EvalArgs<dou
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)TILE2 * sizeof(double) + 16;
   // the hand-written tree loop (its counter in the last 16 bytes); SRHIP_JIT_DYNLOOP=0: the compiled one
   const char* dl = std::getenv("SRHIP_JIT_DYNLOOP");
-  hipFunction_t fn = (dl && dl[0] == '0') ? (a.w ? q.fn_w : q.fn) : (a.w ? q.fn_dlw : q.fn_dl);
+  const bool st = dl && dl[0] == '0';
+  hipFunction_t fn = st ? (a.w ? q.fn_w : q.fn) : (a.w ? q.fn_dlw : q.fn_dl);
+  note_kernel(st ? (a.w ? "sr_jit64_eval_w" : "sr_jit64_eval") : (a.w ? "sr_jit64_eval_dlw" : "sr_jit64_eval_dl"));
   return hipModuleLaunchKernel(fn, (unsigned)a.nrg * (unsigned)a.ntg, 1, 1, 256, 1, 1, (unsigned)lds, stream, nullptr,
                                cfg);
 }

@@ -1295,7 +1295,9 @@ hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + 16;
   // the hand-written tree loop (its counter in the last 16 bytes); SRHIP_JIT_DYNLOOP=0: the compiled one
   const char* dl = std::getenv("SRHIP_JIT_DYNLOOP");
-  hipFunction_t fn = (dl && dl[0] == '0') ? (a.w ? pt.fn_w : pt.fn) : (a.w ? pt.fn_dlw : pt.fn_dl);
+  const bool st = dl && dl[0] == '0';
+  hipFunction_t fn = st ? (a.w ? pt.fn_w : pt.fn) : (a.w ? pt.fn_dlw : pt.fn_dl);
+  note_kernel(st ? (a.w ? "sr_jit_grad_w" : "sr_jit_grad") : (a.w ? "sr_jit_grad_dlw" : "sr_jit_grad_dl"));
   return hipModuleLaunchKernel(fn, grid, 1, 1, (unsigned)plan.threads, 1, 1, (unsigned)lds,
                                stream, nullptr, cfg);
 }

@@ -134,4 +134,10 @@ constexpr int uop_cost(int op) {
              : (op == SRHIP_UOP_EXP || op == SRHIP_UOP_SQRT || op == SRHIP_UOP_INV) ? 14 : 40;
 }
 
+// The name of the main (evaluation) kernel the calling thread launched last:
+// set at each launch site, read by srhip_last_kernel_name (bench.py ties a
+// rocprofv3 PMC summary to the kernel that ran).
+void note_kernel(const char* name);
+const char* last_kernel();
+
 }  // namespace srhip

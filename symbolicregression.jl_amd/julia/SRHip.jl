@@ -255,19 +255,6 @@ function release_dataset!(dataset::Dataset)
     end
     return nothing
 end
-# the device copy of the Dataset whose X this is, if one is uploaded (an
-# eval_tree_array on a Dataset's own X reuses it instead of uploading X again)
-function uploaded_dataset_of(X::AbstractMatrix, device::Int)
-    lock(CTX_LOCK) do
-        for (ds, copies) in DEVICE_DATASETS
-            ds.X === X || continue
-            d = get(copies, device, nothing)
-            d !== nothing && d.h != C_NULL && return d.h
-        end
-        return nothing
-    end
-end
-
 # ---- eval_loss (src/LossFunctions.jl:34-67), batched ------------------------------
 """
     eval_loss_batch(trees, dataset, options; idx=nothing) -> Vector{T}
@@ -399,16 +386,40 @@ end
 """
     eval_tree_array_batch(trees, X, options) -> (outputs::Matrix (n, ntrees), did_succeed::Vector{Bool})
 
-Per-row outputs of many trees in one launch. When X is the X of a Dataset
-already on the device (device_dataset), that copy is used; otherwise X is
-uploaded for this call.
+Per-row outputs of many trees in one launch; X is uploaded for this call (it
+may have changed since any earlier upload, as the reference re-reads it).
 """
 function eval_tree_array_batch(trees::AbstractVector{Node{T}}, X::AbstractMatrix{T}, options::Options;
                                device::Int=0) where {T}
     n = size(X, 2)
+    ds = upload(X, zeros(T, n), nothing, device)
+    try
+        return eval_tree_array_on(trees, ds, n, options, device)
+    finally
+        destroy_dataset(ds)
+    end
+end
+
+"""
+    eval_tree_array_batch(trees, dataset::Dataset, options) -> (outputs, did_succeed)
+
+The same on a Dataset's X through its device copy (device_dataset, uploaded
+once; a Dataset is not modified after construction). `dataset` and its
+DeviceCopy are rooted across the call, so neither the WeakKeyDict entry nor
+the device memory can be freed while the kernel reads it.
+"""
+function eval_tree_array_batch(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, options::Options;
+                               device::Int=0) where {T}
+    h = device_dataset(dataset, device)
+    dcopy = lock(() -> DEVICE_DATASETS[dataset][device], CTX_LOCK)
+    GC.@preserve dataset dcopy begin
+        return eval_tree_array_on(trees, h, dataset.n, options, device)
+    end
+end
+
+function eval_tree_array_on(trees::AbstractVector{Node{T}}, ds::Ptr{Cvoid}, n::Int, options::Options,
+                            device::Int) where {T}
     nt = length(trees)
-    shared = uploaded_dataset_of(X, device)
-    ds = shared === nothing ? upload(X, zeros(T, n), nothing, device) : shared
     p = Program(trees, options, device)
     out = Matrix{T}(undef, n, nt); ok = Vector{UInt8}(undef, nt)
     try
@@ -416,7 +427,6 @@ function eval_tree_array_batch(trees::AbstractVector{Node{T}}, X::AbstractMatrix
                                         (Ptr{Cvoid}, Ptr{Cvoid}, Ptr{Cvoid}, Ptr{UInt8}), ds, p.h, out, ok))
     finally
         destroy(p)
-        shared === nothing && destroy_dataset(ds)
     end
     return out, ok .== 1
 end

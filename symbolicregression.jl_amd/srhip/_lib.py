@@ -71,6 +71,7 @@ SIGNATURES = {
     "srhip_close": [C.c_void_p],
     "srhip_op_lookup": [C.c_char_p, C.POINTER(C.c_int32), C.POINTER(C.c_int32)],
     "srhip_op_eval": [C.c_int32, C.c_int32, C.c_int32, C.c_double, C.c_double, C.POINTER(C.c_double)],
+    "srhip_last_kernel_name": [C.c_char_p, C.c_int32],
     "srhip_dataset_create": [C.c_void_p, C.c_int32, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                              C.c_int64, C.c_int32, C.c_int64, C.c_int64, C.POINTER(C.c_void_p)],
     "srhip_dataset_destroy": [C.c_void_p],

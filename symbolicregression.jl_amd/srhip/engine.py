@@ -67,6 +67,12 @@ class Context:
         """Trees of the last eval whose tree code handed a tile back."""
         return self.last_jit_events()[0]
 
+    def last_kernel_name(self) -> str:
+        """The main evaluation kernel this thread launched last (srhip_last_kernel_name)."""
+        buf = C.create_string_buffer(128)
+        check(lib().srhip_last_kernel_name(buf, 128))
+        return buf.value.decode()
+
     def last_tree_code(self) -> int:
         """Trees the last eval ran as tree code (srhip_last_tree_code)."""
         n = C.c_int32(0)

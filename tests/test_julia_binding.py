@@ -224,12 +224,18 @@ def test_device_datasets_are_weak_and_freed():
 
 
 def test_eval_tree_array_reuses_an_uploaded_dataset():
-    """eval_tree_array on a Dataset's own X uses that dataset's device copy
-    (no per-call upload of X); other X are uploaded for the call and freed."""
+    """a Dataset's device copy is reused only when the caller
+    passes the Dataset itself, with the Dataset and its DeviceCopy rooted
+    (GC.@preserve) across the ccall; a bare X is uploaded for the call (it may
+    have changed) and freed."""
     src = JL.read_text()
-    body = re.search(r"function eval_tree_array_batch\(.*?\nend", src, re.S).group(0)
-    assert "uploaded_dataset_of(X, device)" in body
-    assert "shared === nothing && destroy_dataset(ds)" in body
+    assert "uploaded_dataset_of" not in src
+    mats = re.findall(r"function eval_tree_array_batch\(.*?\nend", src, re.S)
+    assert len(mats) == 2
+    by_x = next(b for b in mats if "X::AbstractMatrix" in b.split("\n")[0])
+    by_ds = next(b for b in mats if "dataset::Dataset" in b.split("\n")[0])
+    assert "upload(X" in by_x and "destroy_dataset(ds)" in by_x
+    assert "device_dataset(dataset, device)" in by_ds and "GC.@preserve dataset dcopy" in by_ds
     one = re.search(r"function eval_tree_array\(.*?\nend", src, re.S).group(0)
     assert "eval_tree_array_batch(" in one and "upload(" not in one
 

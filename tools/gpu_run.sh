@@ -1,24 +1,30 @@
 #!/bin/bash
-# One runner for the GPU box (gpurun): each step under its own time limit,
-# the first crash / hang / abort ends the script (no retries).
-#   tools/gpu_run.sh suite    GPU test suite            -> gpurun_out/pytest_gpu.log
-#   tools/gpu_run.sh smoke    __graft_entry__.smoke()   -> gpurun_out/smoke.log
-#   tools/gpu_run.sh bench    bench.py (BENCH_ARGS)     -> gpurun_out/bench.json
-#   tools/gpu_run.sh profile  bench under rocprofv3: kernel trace + PMC passes (tools/gpu_bench_profile.sh)
-#   tools/gpu_run.sh configs  tools/bench_configs.py   -> gpurun_out/configs.jsonl
-#   tools/gpu_run.sh final    suite, smoke, bench, profile
-# Several modes may be given: tools/gpu_run.sh suite bench
-# The round-3 measurements in profiles/ came from these tools, each step under
-# its own `timeout -k 10 ...` on the box: ab_env.py (env-knob A/Bs: tail split,
-# tree groups, waves), step_overhead.py, out_copy.py + hostcopy.cpp (per-row
-# outputs), prof_grad.py / pmc_grad.sh / debug_grads.py (gradient tree code),
-# pmc_shard.sh (512 vs 4096 trees), bench_constopt.py / prof_constopt.py,
-# census.py (no GPU: the VALU-issue budget).
+# The one runner for the GPU box (gpurun): each step under its own time limit,
+# the first crash / hang / abort ends the script (no retries). Several modes
+# may be given: tools/gpu_run.sh suite bench
+#   suite     GPU test suite (one process)               -> gpurun_out/pytest_gpu.log
+#   smoke     __graft_entry__.smoke()                    -> gpurun_out/smoke.log
+#   bench     bench.py $BENCH_ARGS                       -> gpurun_out/bench.json
+#   profile   bench.py under rocprofv3: kernel trace + the PMC passes -> gpurun_out/benchprof/summary.json
+#             (copy to profiles/current_pmc_summary.json: bench.py attaches it when kernel + lib hash match)
+#   pmc       PMC passes of any command: PMC_KERNEL=<name substring> PMC_CMD="python3 tools/x.py ..."
+#   configs   tools/bench_configs.py                     -> gpurun_out/configs.jsonl
+#   search    default-Options EquationSearch: the search GPU tests, configs #1 and #4
+#             (tools/run_search.py)                      -> gpurun_out/search_config{1,4}.json
+#   n2        bench.py's N > 1 paths rehearsed with two ranks on GPU 0 over gloo (not a measurement)
+#   variants  the suite under the static tree loops and with every program as tree code
+#   final     suite, smoke, bench, profile
+# Measurement tools run on the box through this script (each under timeout):
+# ab_env.py / loop_ab.py (interleaved A/Bs), step_overhead.py, out_copy.py,
+# prof_grad.py, prof_target.py, shard_probe.py, bench_constopt.py,
+# prof_constopt.py; census.py needs no GPU.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 1
 mkdir -p gpurun_out
+export TMPDIR=/tmp
+PYTEST="python -u -m pytest -v --timeout 300 --timeout-method thread"
+
 run_suite() {
-  timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread \
-    > gpurun_out/pytest_gpu.log 2>&1
+  timeout -k 10 900 $PYTEST tests -m gpu > gpurun_out/pytest_gpu.log 2>&1
   local rc=$?
   echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
   # 1 = test failures (the GPU is fine): go on; anything else (crash, time limit) stops
@@ -36,9 +42,60 @@ run_configs() {
   timeout -k 10 400 python -u tools/bench_configs.py > gpurun_out/configs.jsonl 2> gpurun_out/configs.err || exit $?
   cat gpurun_out/configs.jsonl
 }
+# pmc_passes <outdir> <kernel substring> <command...>: the counter passes of
+# MI355X_MICROARCH.md, each its own run (rocprofv3 does not split passes)
+pmc_passes() {
+  local out=$1 kern=$2; shift 2
+  mkdir -p "$out"
+  local P1="SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_VALU SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_INSTS_LDS SQ_INSTS_BRANCH"
+  local P2="SQ_WAIT_INST_ANY SQ_WAIT_ANY SQ_IFETCH SQ_ACTIVE_INST_ANY SQ_INSTS_SMEM SQ_INST_CYCLES_SALU SQ_THREAD_CYCLES_VALU SQ_BUSY_CU_CYCLES"
+  local P3="SQ_WAIT_INST_LDS SQ_ACTIVE_INST_LDS SQ_ACTIVE_INST_SCA SQ_ACTIVE_INST_MISC SQ_INST_LEVEL_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU_TRANS_F32"
+  local P4="SQC_ICACHE_HITS SQC_ICACHE_MISSES SQC_ICACHE_MISSES_DUPLICATE GRBM_GUI_ACTIVE"
+  local i=0 P
+  for P in "$P1" "$P2" "$P3" "$P4" "FETCH_SIZE" "WRITE_SIZE"; do
+    i=$((i+1))
+    timeout -s KILL 150 rocprofv3 --pmc $P --output-format csv -d "$out/pmc$i" -o pmc$i -- "$@" \
+      > "$out/run_pmc$i.out" 2>> "$out/log.txt" || { echo "pmc pass $i failed"; exit 1; }
+  done
+  KERNEL="$kern" python3 tools/pmc_summary.py "$out" > "$out/summary.json" && cat "$out/summary.json"
+}
 run_profile() {
-  bash tools/gpu_bench_profile.sh > gpurun_out/benchprof.log 2>&1 || exit $?
-  tail -30 gpurun_out/benchprof.log
+  local OUT=gpurun_out/benchprof
+  mkdir -p $OUT
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/kt -o kt -- \
+    python3 bench.py --steps 20 --warmup 10 --no-cpu --no-row-shard > $OUT/bench_kt.json 2> $OUT/log.txt || exit $?
+  pmc_passes $OUT sr_jit_eval python3 bench.py --steps 3 --warmup 1 --no-cpu --no-row-shard
+}
+run_pmc() {
+  [ -n "$PMC_CMD" ] || { echo "PMC_CMD not set"; exit 2; }
+  pmc_passes gpurun_out/pmc "${PMC_KERNEL:-sr_jit}" $PMC_CMD
+}
+run_search() {
+  timeout -k 10 700 $PYTEST tests/test_evolution.py tests/test_search.py tests/test_configs_gpu.py -m gpu -s \
+    -k "search or evolution or config4 or config1" > gpurun_out/pytest_search.log 2>&1
+  local rc=$?; grep -E "PASSED|FAILED|passed|failed" gpurun_out/pytest_search.log | tail -8
+  [ $rc -le 1 ] || exit $rc
+  timeout -k 10 400 python -u tools/run_search.py config1 --iterations 40 --out gpurun_out/search_config1.json \
+    > gpurun_out/search_c1.log 2>&1 || exit $?
+  tail -3 gpurun_out/search_c1.log | cut -c1-400
+  timeout -k 10 600 python -u tools/run_search.py config4 --iterations ${C4_ITERS:-3} --out gpurun_out/search_config4.json \
+    > gpurun_out/search_c4.log 2>&1 || exit $?
+  tail -5 gpurun_out/search_c4.log | cut -c1-600
+}
+run_n2() {
+  SRHIP_BENCH_SHARED_GPU=1 timeout -k 10 300 python3 bench.py --gpus 2 --steps 5 --warmup 2 --rs-steps 2 \
+    > gpurun_out/bench_n2_rows.json 2> gpurun_out/bench_n2_rows.err || { tail -20 gpurun_out/bench_n2_rows.err; exit 1; }
+  SRHIP_BENCH_SHARED_GPU=1 timeout -k 10 300 python3 bench.py --gpus 2 --shard trees --steps 5 --warmup 2 --no-row-shard \
+    > gpurun_out/bench_n2_trees.json 2> gpurun_out/bench_n2_trees.err || { tail -20 gpurun_out/bench_n2_trees.err; exit 1; }
+  tail -c 300 gpurun_out/bench_n2_rows.json gpurun_out/bench_n2_trees.json
+}
+run_variants() {
+  SRHIP_JIT_DYNLOOP=0 SRHIP_INTERP_DYN=0 timeout -k 10 600 $PYTEST tests -m gpu -q > gpurun_out/pytest_static.log 2>&1
+  local rc=$?; echo "static loops rc=$rc"; tail -2 gpurun_out/pytest_static.log
+  [ $rc -le 1 ] || exit $rc
+  SRHIP_JIT=1 timeout -k 10 600 $PYTEST tests -m gpu -q > gpurun_out/pytest_jitall.log 2>&1
+  rc=$?; echo "SRHIP_JIT=1 rc=$rc"; tail -2 gpurun_out/pytest_jitall.log
+  [ $rc -le 1 ] || exit $rc
 }
 for mode in "$@"; do
   case "$mode" in
@@ -46,7 +103,11 @@ for mode in "$@"; do
     smoke) run_smoke ;;
     bench) run_bench ;;
     profile) run_profile ;;
+    pmc) run_pmc ;;
     configs) run_configs ;;
+    search) run_search ;;
+    n2) run_n2 ;;
+    variants) run_variants ;;
     final) run_suite; run_smoke; run_bench; run_profile ;;
     *) echo "unknown mode $mode"; exit 2 ;;
   esac

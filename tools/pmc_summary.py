@@ -26,7 +26,20 @@ if kt:
     for r in csv.DictReader(open(kt[0])):
         if want in r["Name"]:
             dur = float(r["AverageNs"]) / 1e6
-res = {"kernel": want, "avg_ms_kernel_trace": dur, "counters_per_dispatch": avg}
+# the exact kernel symbol the passes measured (the most dispatched match)
+names = defaultdict(int)
+for f in glob.glob(os.path.join(out, "pmc*", "*counter_collection.csv")):
+    for r in csv.DictReader(open(f)):
+        if want in r["Kernel_Name"]:
+            names[r["Kernel_Name"]] += 1
+exact = max(names, key=names.get) if names else want
+res = {"kernel": exact, "avg_ms_kernel_trace": dur, "counters_per_dispatch": avg}
+# the library the passes ran: bench.py attaches this summary to its JSON line
+# only when its own run launched the same kernel from the same libsrhip.so
+import hashlib  # noqa: E402
+_lib = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "symbolicregression.jl_amd", "lib", "libsrhip.so")
+if os.path.exists(_lib):
+    res["lib_sha256"] = hashlib.sha256(open(_lib, "rb").read()).hexdigest()
 # the same average over the bench's timed steps only (the last STEPS dispatches;
 # the first warmup calls run on a cold instruction cache)
 ktr = glob.glob(os.path.join(out, "kt", "*kernel_trace.csv"))
