@@ -1367,7 +1367,9 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
         HIP_CHECK(jit::launch64(jm64, launches[li].part, plan, a, s));
       }
     } else {
-      note_kernel(sizeof(T) == 4 ? "eval_kernel<float>" : "eval_kernel<double>");
+      // the interpreter's pass after a tree-code pass runs the few trees left
+      // over: the call's main kernel stays the tree code
+      if (nj == 0) note_kernel(sizeof(T) == 4 ? "eval_kernel<float>" : "eval_kernel<double>");
       HIP_CHECK(launch_eval<T>(plan, a, mode, s));
     }
     timed_end(c, s, tk);
