@@ -376,8 +376,10 @@ int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int
                                int64_t* inout_noffsets);
 /* Testing hook, same contract: the loss tree code (grad = 0; fast: its
  * guarded FAST path) or the gradient tree code (grad = 1) of Float32 trees
- * for the elementwise loss `loss` (SRHIP_LOSS_*) with its parameter.
- * SRHIP_ERR_UNSUPPORTED when tree code has no routine for that loss. */
+ * for the elementwise loss `loss` (SRHIP_LOSS_*) with its parameter; fast
+ * bit 3: Float64 trees through the Float64 tree compiler with that loss's
+ * routine in the tile tail. SRHIP_ERR_UNSUPPORTED when Float32 tree code has
+ * no routine for that loss (a Float64 tree without one is not compiled). */
 int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t fast, int32_t loss, double loss_param,
                                uint8_t* out_bytes, int64_t* inout_nbytes, char* out_text, int64_t* inout_ntext,
                                int32_t* out_offsets, int64_t* inout_noffsets);

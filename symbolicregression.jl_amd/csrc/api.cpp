@@ -254,6 +254,10 @@ struct srhip_program {
   // built at a loss's first evaluation; null m: that loss runs interpreted
   struct LossJit { int kind; uint64_t bits; jit::Module* m; };
   mutable std::vector<LossJit> jit_loss;
+  // Float64 programs: the same trees' tree code for the other losses and for
+  // per-row outputs (kind -2), built at first use (module64)
+  struct LossJit64 { int kind; uint64_t bits; jit::Module64* m; };
+  mutable std::vector<LossJit64> jit64_loss;
   // the constants the tree code was built with: the trees of a later loss or
   // output build are compiled with them, so that every tree folds and fails
   // statically as in that build (the slot layouts match); memory-constant code
@@ -419,6 +423,8 @@ void upload_gconsts(srhip_program* p) {
 void free_loss_jits(const srhip_program* p) {
   for (auto& l : p->jit_loss) jit::destroy(l.m);
   p->jit_loss.clear();
+  for (auto& l : p->jit64_loss) jit::destroy64(l.m);
+  p->jit64_loss.clear();
 }
 
 void free_program_device(srhip_program* p) {
@@ -848,6 +854,7 @@ void build_program(srhip_program* p) {
       if (p->jit64) {
         p->nlist_j = (int)jl.size();
         p->h_jit_list = jl;
+        p->jit_consts = p->consts;
         a = jl;
         a.insert(a.end(), rest.begin(), rest.end());
       }
@@ -1137,6 +1144,45 @@ jit::Module* loss_module(const srhip_program* p, int loss, double lparam) {
   return m;
 }
 
+// The Float64 tree code of a program for an elementwise loss (L2: the build
+// itself; the others: the same trees with that loss's routine in the tile
+// tail, jit64.cpp emit_tail_loss) or for per-row outputs (kind -2:
+// srhip_eval_tree_array, jit64.cpp emit_store_out), built at its first use
+// and kept with the program; null (SRHIP_JIT64_EXTRA=0, a different slot
+// layout): interpreted. The constants are literals of the code: new constants
+// destroy it with the L2 build (update_constants).
+jit::Module64* module64(const srhip_program* p, int kind, double lparam) {
+  if (!p->jit64 || p->nlist_j == 0) return nullptr;
+  if (kind == SRHIP_LOSS_L2) return p->jit64;
+  static const bool on = [] { const char* e = std::getenv("SRHIP_JIT64_EXTRA"); return !(e && e[0] == '0'); }();
+  if (!on || kind < -2 || kind >= SRHIP_NUM_LOSSES) return nullptr;
+  uint64_t bits = 0;
+  if (kind != -2) std::memcpy(&bits, &lparam, 8);
+  for (const auto& l : p->jit64_loss)
+    if (l.kind == kind && l.bits == bits) return l.m;
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->jit_consts.data();
+  CompiledBatch<double> cb = compile_batch_par<double>(tr);
+  jit::Opts64 o;
+  o.out = kind == -2;
+  o.loss = kind == -2 ? SRHIP_LOSS_L2 : kind;
+  o.lparam = bits;
+  std::vector<int32_t> jl, rest;
+  jit::Stats st;
+  jit::Module64* m = jit::build64(cb, p->h_jit_list, jl, rest, &st, o);
+  if (m && (jl != p->h_jit_list || !rest.empty())) {
+    jit::destroy64(m);  // a different slot layout: interpreted
+    m = nullptr;
+  }
+  p->jit64_loss.push_back({kind, bits, m});
+  return m;
+}
+
 // The per-row output tree code of a Float32 program (srhip_eval_tree_array):
 // the same trees compiled with jit::Options::out, PRECISE routines only, built
 // at the first per-row evaluation and kept with the program (kind -2 in
@@ -1229,10 +1275,10 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   jit::Module* jm = !std::is_same<T, float>::value ? nullptr
                     : mode == MODE_LOSS          ? loss_module(p, loss, lparam)
                                                  : out_module(p);
-  // Float64 programs: their tree code (L2 loss)
+  // Float64 programs: their tree code (this loss, or per-row outputs)
   jit::Module64* jm64 = nullptr;
   if constexpr (std::is_same<T, double>::value)
-    if (mode == MODE_LOSS && loss == SRHIP_LOSS_L2 && p->jit64 && p->nlist_j > 0) jm64 = p->jit64;
+    if (p->jit64 && p->nlist_j > 0) jm64 = module64(p, mode == MODE_LOSS ? loss : -2, lparam);
   const bool use_jit = jm != nullptr || jm64 != nullptr;
   c->last_jit_trees = (use_jit && rows > 0) ? p->nlist_j : 0;
   const int nj = use_jit ? p->nlist_j : 0;
@@ -2396,13 +2442,18 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
     std::memcpy(&lbits, &lparam, 8);
     if (mode == 2 && !jit::has_dloss_routine(loss))
       throw Error(SRHIP_ERR_UNSUPPORTED, "no gradient tree code for this loss");
-    if (mode != 2 && !jit::has_loss_routine(loss)) throw Error(SRHIP_ERR_UNSUPPORTED, "no tree code for this loss");
-    if (mode == 5) {  // Float64 tree code (jit64.cpp)
+    if (mode != 2 && mode != 5 && !jit::has_loss_routine(loss))
+      throw Error(SRHIP_ERR_UNSUPPORTED, "no tree code for this loss");
+    if (mode == 5) {  // Float64 tree code (jit64.cpp): L2, another loss's tail, or per-row outputs
       CompiledBatch<double> cb = compile_batch<double>(*trees);
       std::vector<int32_t> cand;
       for (int t = 0; t < cb.ntrees; ++t)
         if (cb.tree_off[t] >= 0 && cb.need[t] <= kShallowSlots) cand.push_back(t);
-      jit::compile_only64(cb, cand, &bytes, &text, &offs);
+      jit::Opts64 o;
+      o.out = out_mode;
+      o.loss = out_mode ? SRHIP_LOSS_L2 : loss;
+      o.lparam = lbits;
+      jit::compile_only64(cb, cand, &bytes, &text, &offs, o);
     } else if (mode == 2) {  // gradient tree code
       CompiledBatch<float> cb = compile_batch<float>(*trees, /*grad=*/true);
       std::vector<int32_t> cand, coff(trees->const_off, trees->const_off + trees->ntrees + 1);
@@ -2446,8 +2497,9 @@ int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_b
                           int64_t* inout_noffsets) {
   // fast: bit 0 the FAST path, bit 1 memory-constant code (mode 3 / 4 below),
   // bit 2 per-row output code, bit 3 Float64 trees (jit64.cpp; the other bits ignored)
-  if (fast & 8)  // Float64 trees
-    return jit_compile_hook(trees, 5, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets, inout_noffsets);
+  if (fast & 8)  // Float64 trees (bit 2: their per-row output code)
+    return jit_compile_hook(trees, 5, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets, inout_noffsets,
+                            SRHIP_LOSS_L2, 0.0, (fast & 4) != 0);
   return jit_compile_hook(trees, (fast & 2) ? ((fast & 1) ? 4 : 3) : ((fast & 1) ? 1 : 0), out_bytes, inout_nbytes,
                           out_text, inout_ntext, out_offsets, inout_noffsets, SRHIP_LOSS_L2, 0.0, (fast & 4) != 0);
 }
@@ -2461,8 +2513,9 @@ int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int
 int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t fast, int32_t loss, double loss_param,
                                uint8_t* out_bytes, int64_t* inout_nbytes, char* out_text, int64_t* inout_ntext,
                                int32_t* out_offsets, int64_t* inout_noffsets) {
-  return jit_compile_hook(trees, grad ? 2 : (fast ? 1 : 0), out_bytes, inout_nbytes, out_text, inout_ntext,
-                          out_offsets, inout_noffsets, loss, loss_param);
+  // fast bit 3: the Float64 tree compiler (jit64.cpp) with this loss's tail
+  return jit_compile_hook(trees, (fast & 8) ? 5 : grad ? 2 : ((fast & 1) ? 1 : 0), out_bytes, inout_nbytes, out_text,
+                          inout_ntext, out_offsets, inout_noffsets, loss, loss_param);
 }
 
 namespace {

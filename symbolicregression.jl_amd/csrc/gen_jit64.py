@@ -31,6 +31,8 @@ import gen_asm_interp as G  # noqa: E402
 
 UOPS, BOPS = G.UOPS, G.BOPS
 LOSSY_UOPS, LOSSY_LHS, LOSSY_RHS = G.LOSSY_UOPS, G.LOSSY_LHS, G.LOSSY_RHS
+LOSSES = {m.group(1): int(m.group(2)) for m in
+          re.finditer(r"#define SRHIP_LOSS_(\w+)\s+(\d+)", open(G.INCLUDE).read())}
 INLINE_BOPS = {"ADD", "SUB", "MUL"}
 INLINE_UOPS = {"NEG", "ABS", "SQUARE", "CUBE"}
 
@@ -127,6 +129,14 @@ def routine_list():
         rs.append((f"b_{b.lower()}_rc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], imm);")))
         mk = "chk = mark(s.a[r], chk); " if b in LOSSY_RHS else ""
         rs.append((f"b_{b.lower()}_lc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);")))
+    # elementwise losses but L2 (inline): r in A -> ℓ(r) in A, the parameter
+    # (Float64 bits) in s_k : s_kh — device_ops.h elem_loss with ŷ = r, y = 0
+    # (r - 0 = r exactly), the Float64 interpreter's loss code
+    for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
+        if name == "L2":
+            continue
+        rs.append((f"l_{name.lower()}",
+                   imm + rows(f"s.a[r] = dev::elem_loss<double>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0);")))
     return rs
 
 
@@ -213,6 +223,8 @@ def build(hipcc, outdir):
             f.write(f"#define SR_JIT64_BOP_ROUTINE_{suf.upper()} {{" + ", ".join(
                 str(-1 if b[2:].upper() in INLINE_BOPS else rid(f"{b}_{suf}")) for _, b in sorted(bop_rt.items()))
                 + "}\n")
+        f.write("#define SR_JIT64_LOSS_ROUTINE {" + ", ".join(
+            str(-1 if n == "L2" else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write(f"#define SR_JIT64_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT64_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT64_CLOBBERS " + ", ".join([f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s]

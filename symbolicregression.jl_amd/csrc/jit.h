@@ -156,9 +156,17 @@ bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t
 // lane, 128-row tiles. Constants are literals: a program whose constants are
 // set again runs on the interpreter.
 struct Module64;
+// Options of a Float64 build: per-row output code (srhip_eval_tree_array) or
+// the loss of the tile tail (L2 inline, the others by a loss routine, the
+// parameter's Float64 bits as literals)
+struct Opts64 {
+  bool out = false;
+  int loss = SRHIP_LOSS_L2;
+  uint64_t lparam = 0;
+};
 bool available64();
 Module64* build64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list,
-                  std::vector<int32_t>& rest, Stats* st);
+                  std::vector<int32_t>& rest, Stats* st, const Opts64& opt = Opts64());
 void destroy64(Module64* m);
 int nparts64(const Module64* m);
 void part64(const Module64* m, int k, int* slot0, int* nslots);
@@ -166,7 +174,8 @@ int nraw64(const Module64* m);  // feature columns the code reads (staged per ti
 // plan: tile 128 rows, 256 threads; EvalArgs as for the interpreter (list / fail / partial of the part)
 hipError_t launch64(Module64* m, int k, const EvalPlan& plan, const EvalArgs<double>& a, hipStream_t stream);
 bool compile_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes,
-                    std::string* text, std::vector<int32_t>* offsets);
+                    std::string* text, std::vector<int32_t>* offsets,
+                    const Opts64& opt = Opts64());
 
 }  // namespace jit
 }  // namespace srhip

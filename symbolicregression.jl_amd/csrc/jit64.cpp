@@ -67,11 +67,13 @@ const int kBop64[SRHIP_NUM_BOPS] = SR_JIT64_BOP_ROUTINE;
 const int kBop64RC[SRHIP_NUM_BOPS] = SR_JIT64_BOP_ROUTINE_RC;
 const int kBop64LC[SRHIP_NUM_BOPS] = SR_JIT64_BOP_ROUTINE_LC;
 const char* const kName64[kNum64] = SR_JIT64_ROUTINE_NAMES;
+const int kLoss64[SRHIP_NUM_LOSSES] = SR_JIT64_LOSS_ROUTINE;
+constexpr int T_OUT = 92;  // s[92:93]: out mode, the tree's output rows of the current tile
 
 // gfx950 encodings used here and not by jit.cpp (checked against llvm-mc by tests/test_jit.py)
 enum : int {
   VOP3_FMA_F64 = 0x1cc, VOP3_ADD_F64 = 0x280, VOP3_MUL_F64 = 0x281, VOPC_U_F64 = 0x68,
-  VOP1_MOV = 0x01, VOP2_CNDMASK = 0x00, VOP2_AND_B32 = 0x13, VOP2_XOR_B32 = 0x15, VOP2_ADD_U32 = 0x34,
+  VOP1_MOV = 0x01, VOP2_CNDMASK = 0x00, VOP2_LSHLREV_B32 = 0x12, VOP2_AND_B32 = 0x13, VOP2_XOR_B32 = 0x15, VOP2_ADD_U32 = 0x34,
   VOP3P_MOV_B32 = 0x33, VOPC_GT_I32 = 0xc4,
   SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
   SOP2_ADD_U32 = 0x00, SOP2_SUB_I32 = 0x03, SOP2_ADDC_U32 = 0x04,
@@ -229,8 +231,9 @@ struct Gen64 {
   bool has_call = false;
   int L_tile = -1, L_done = -1;
   std::string why;
+  Opts64 opt;  // out mode / loss of this build
 
-  Gen64(Asm& a, const Tmpl64& t, uint64_t va) : as(a), T(t), base_va(va) {}
+  Gen64(Asm& a, const Tmpl64& t, uint64_t va, const Opts64& o) : as(a), T(t), base_va(va), opt(o) {}
   uint64_t cur_va() const { return base_va + as.bytes(); }
   static int blk(int k) { return POOL2 + 4 * k; }
 
@@ -267,6 +270,10 @@ struct Gen64 {
     }
     if (!usef(root, n, true)) return false;
     if (root.k == Q_VAL) last[root.v] = n;
+    if (!opt.out && opt.loss != SRHIP_LOSS_L2) {  // the loss routine of the tile tail
+      if (opt.loss < 0 || opt.loss >= SRHIP_NUM_LOSSES || kLoss64[opt.loss] < 0) { why = "no Float64 loss routine"; return false; }
+      has_call = true;
+    }
     if ((int)feats.size() > NPOOL2) { why = "more features than register blocks"; return false; }
     return true;
   }
@@ -439,6 +446,68 @@ struct Gen64 {
     as.bind(L_nomask);
   }
 
+  // L2: residuals r = ŷ - y, masked, squared (weighted) into the lane's sum
+  void emit_tail_l2(int rreg) {
+    for (int e = 0; e < R2; ++e) vop3d(VOP3_ADD_F64, "v_add_f64", Y2 + 2 * e, V(rreg + 2 * e), V(Y2 + 2 * e), nullptr, 2);
+    emit_mask(Y2);
+    const int L_unw = as.label(), L_sum = as.label();
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(T_WOFF), K(0));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
+    as.vop2(VOP2_ADD_U32, "v_add_u32_e32", GT2, S(T_WOFF), LANE2);
+    as.ds_read_b128(GT2, GT2, 0);
+    as.waitcnt_lgkm(0);
+    for (int e = 0; e < R2; ++e) {  // Σ w·(r·r)
+      const Src r = V(Y2 + 2 * e);
+      vop3d(VOP3_MUL_F64, "v_mul_f64", Y2 + 2 * e, r, r, nullptr, 0);
+      const Src w = V(GT2 + 2 * e), t = V(Y2 + 2 * e), l = V(LSUM2);
+      vop3d(VOP3_FMA_F64, "v_fma_f64", LSUM2, w, t, &l, 0);
+    }
+    as.branch(SOPP_BRANCH, "s_branch", L_sum);
+    as.bind(L_unw);
+    for (int e = 0; e < R2; ++e) {
+      const Src r = V(Y2 + 2 * e), l = V(LSUM2);
+      vop3d(VOP3_FMA_F64, "v_fma_f64", LSUM2, r, r, &l, 0);
+    }
+    as.bind(L_sum);
+  }
+
+  // any other loss: r = ŷ - y into A, ℓ(r) by the loss routine (the Float64
+  // interpreter's elem_loss, its parameter in s_k : s_kh), times w when
+  // weighted, masked past the last row, summed into the lane's sum
+  void emit_tail_loss(int rreg) {
+    for (int e = 0; e < R2; ++e) vop3d(VOP3_ADD_F64, "v_add_f64", A2 + 2 * e, V(rreg + 2 * e), V(Y2 + 2 * e), nullptr, 2);
+    as.sop1(SOP1_MOV, "s_mov_b32", T_K, K((uint32_t)opt.lparam), "s" + std::to_string(T_K));
+    as.sop1(SOP1_MOV, "s_mov_b32", T_KH, K((uint32_t)(opt.lparam >> 32)), "s" + std::to_string(T_KH));
+    routine(kLoss64[opt.loss]);
+    const int L_unw = as.label();
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(T_WOFF), K(0));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
+    as.vop2(VOP2_ADD_U32, "v_add_u32_e32", GT2, S(T_WOFF), LANE2);
+    as.ds_read_b128(GT2, GT2, 0);
+    as.waitcnt_lgkm(0);
+    for (int e = 0; e < R2; ++e) vop3d(VOP3_MUL_F64, "v_mul_f64", A2 + 2 * e, V(GT2 + 2 * e), V(A2 + 2 * e), nullptr, 0);
+    as.bind(L_unw);
+    emit_mask(A2);
+    for (int e = 0; e < R2; ++e) vop3d(VOP3_ADD_F64, "v_add_f64", LSUM2, V(LSUM2), V(A2 + 2 * e), nullptr, 0);
+  }
+
+  // out mode: the tile's root values to the tree's output rows (lane ℓ holds
+  // rows 2ℓ, 2ℓ+1: one coalesced 1 KiB global_store_dwordx4 per wave at
+  // s[92:93] + 16ℓ), then the next tile's rows. Rows past the last are
+  // written too: they lie in the output's padding (stride n_pad).
+  void emit_store_out(int rreg) {
+    const int voff = Y2;  // no y in out mode: 16ℓ = 8 · (2ℓ)
+    as.vop2(VOP2_LSHLREV_B32, "v_lshlrev_b32_e32", voff, K(3), LROW2);
+    as.put(0xdc7c8000u);  // global_store_dwordx4 voff, v[rreg:rreg+3], s[T_OUT:T_OUT+1]
+    as.put((uint32_t)voff | ((uint32_t)rreg << 8) | ((uint32_t)T_OUT << 16));
+    if (as.want_text)
+      as.lines.push_back("global_store_dwordx4 v" + std::to_string(voff) + ", v[" + std::to_string(rreg) + ":" +
+                         std::to_string(rreg + 3) + "], s[" + std::to_string(T_OUT) + ":" + std::to_string(T_OUT + 1) +
+                         "]");
+    as.sop2(SOP2_ADD_U32, "s_add_u32", T_OUT, S(T_OUT), K((uint32_t)(TILE2 * 8)));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", T_OUT + 1, S(T_OUT + 1), K(0));
+  }
+
   bool emit_tree() {
     if (!analyze()) return false;
     L_tile = as.label();
@@ -452,8 +521,10 @@ struct Gen64 {
     for (int k = 0; k < NPOOL2; ++k) owner[k] = -1;
     nloads = 0;
     waited = 0;
-    as.ds_read_b128(Y2, LANE2, 0);
-    ++nloads;
+    if (!opt.out) {  // out mode: no y column
+      as.ds_read_b128(Y2, LANE2, 0);
+      ++nloads;
+    }
     for (size_t j = 0; j < feats.size(); ++j) {
       const int f = feats[j];
       xblk[f] = (int)j;
@@ -479,34 +550,16 @@ struct Gen64 {
       vop3d(VOP3_FMA_F64, "v_fma_f64", CHK2, r, z, &c, 0);
     }
     wait_all();
-    // residuals r = ŷ - y, masked, squared (weighted) into the lane's sum
-    for (int e = 0; e < R2; ++e) vop3d(VOP3_ADD_F64, "v_add_f64", Y2 + 2 * e, V(rreg + 2 * e), V(Y2 + 2 * e), nullptr, 2);
-    emit_mask(Y2);
-    {
-      const int L_unw = as.label(), L_sum = as.label();
-      as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(T_WOFF), K(0));
-      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
-      as.vop2(VOP2_ADD_U32, "v_add_u32_e32", GT2, S(T_WOFF), LANE2);
-      as.ds_read_b128(GT2, GT2, 0);
-      as.waitcnt_lgkm(0);
-      for (int e = 0; e < R2; ++e) {  // Σ w·(r·r)
-        const Src r = V(Y2 + 2 * e);
-        vop3d(VOP3_MUL_F64, "v_mul_f64", Y2 + 2 * e, r, r, nullptr, 0);
-        const Src w = V(GT2 + 2 * e), t = V(Y2 + 2 * e), l = V(LSUM2);
-        vop3d(VOP3_FMA_F64, "v_fma_f64", LSUM2, w, t, &l, 0);
-      }
-      as.branch(SOPP_BRANCH, "s_branch", L_sum);
-      as.bind(L_unw);
-      for (int e = 0; e < R2; ++e) {
-        const Src r = V(Y2 + 2 * e), l = V(LSUM2);
-        vop3d(VOP3_FMA_F64, "v_fma_f64", LSUM2, r, r, &l, 0);
-      }
-      as.bind(L_sum);
+    if (opt.out) {
+      emit_store_out(rreg);
+    } else {
+      if (opt.loss == SRHIP_LOSS_L2) emit_tail_l2(rreg);
+      else emit_tail_loss(rreg);
+      // a failed tile ends the tree (out mode: every tile is evaluated, as MODE_OUT does)
+      as.put(0x7c000000u | ((uint32_t)VOPC_U_F64 << 17) | ((uint32_t)CHK2 << 9) | (uint32_t)(256 + CHK2));
+      if (as.want_text) as.t("v_cmp_u_f64_e32 vcc, " + pr(CHK2) + ", " + pr(CHK2));
+      as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
     }
-    // a failed tile ends the tree
-    as.put(0x7c000000u | ((uint32_t)VOPC_U_F64 << 17) | ((uint32_t)CHK2 << 9) | (uint32_t)(256 + CHK2));
-    if (as.want_text) as.t("v_cmp_u_f64_e32 vcc, " + pr(CHK2) + ", " + pr(CHK2));
-    as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
     // ---- next tile
     as.vop2(VOP2_ADD_U32, "v_add_u32_e32", LANE2, S(T_TILEBYTES), LANE2);
     as.sop2(SOP2_ADD_U32, "s_add_u32", T_TILE, S(T_TILE), K(1));
@@ -519,7 +572,7 @@ struct Gen64 {
   }
 };
 
-bool gen_tree64(const Ins<double>* prog, const Tmpl64& T, bool text, std::vector<uint32_t>& out,
+bool gen_tree64(const Ins<double>* prog, const Tmpl64& T, const Opts64& opt, bool text, std::vector<uint32_t>& out,
                 std::vector<std::string>* lines, int32_t* off, int* max_feat, std::string* why) {
   std::vector<Op64> ir;
   Q root;
@@ -527,7 +580,7 @@ bool gen_tree64(const Ins<double>* prog, const Tmpl64& T, bool text, std::vector
   const size_t start = (out.size() + 15) / 16 * 16;  // 64-byte aligned entries
   Asm as;
   as.want_text = text;
-  Gen64 g(as, T, T.area_va + start * 4);
+  Gen64 g(as, T, T.area_va + start * 4, opt);
   g.ops = ir;
   g.root = root;
   if (!g.emit_tree()) { *why = g.why; return false; }
@@ -548,7 +601,8 @@ bool gen_tree64(const Ins<double>* prog, const Tmpl64& T, bool text, std::vector
 
 // Trees that compile are appended to ok_trees / offs, the others to `rest`; a
 // tree that no longer fits in the area ends the call (returns its position).
-size_t codegen64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, size_t from, bool text,
+size_t codegen64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, size_t from, const Opts64& opt,
+                 bool text,
                  std::vector<uint32_t>& words, std::vector<std::string>* lines, std::vector<int32_t>& offs,
                  std::vector<int32_t>& ok_trees, std::vector<int32_t>& rest, int* max_feat, Stats* st) {
   const Tmpl64& T = tmpl64();
@@ -558,7 +612,7 @@ size_t codegen64(const CompiledBatch<double>& cb, const std::vector<int32_t>& ca
     std::string why;
     const size_t before = words.size(), lbefore = lines ? lines->size() : 0;
     int mf = *max_feat;
-    const bool okc = cb.tree_off[t] >= 0 && gen_tree64(&cb.code[cb.tree_off[t]], T, text, words, lines, &off, &mf, &why);
+    const bool okc = cb.tree_off[t] >= 0 && gen_tree64(&cb.code[cb.tree_off[t]], T, opt, text, words, lines, &off, &mf, &why);
     if (okc && words.size() * 4 > T.area_bytes) {
       words.resize(before);
       if (lines) lines->resize(lbefore);
@@ -593,6 +647,7 @@ struct Part64 {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr;
   hipFunction_t fn_dl = nullptr, fn_dlw = nullptr;  // the hand-written tree loop (sr_jit64_eval_dl)
+  hipFunction_t fn_out = nullptr;                   // per-row output code (sr_jit64_out)
   int32_t* d_off = nullptr;
   int slot0 = 0, nslots = 0;
 };
@@ -600,12 +655,13 @@ struct Module64 {
   std::vector<Part64> parts;
   int nslots = 0;
   int nraw = 0;
+  bool out = false;
 };
 
 bool available64() { return tmpl64().ok; }
 
 Module64* build64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list,
-                  std::vector<int32_t>& rest, Stats* st) {
+                  std::vector<int32_t>& rest, Stats* st, const Opts64& opt) {
   const Tmpl64& T = tmpl64();
   if (!T.ok) { rest = cand; return nullptr; }
   const auto t0 = std::chrono::steady_clock::now();
@@ -616,7 +672,7 @@ Module64* build64(const CompiledBatch<double>& cb, const std::vector<int32_t>& c
   constexpr int kMaxParts64 = 8;
   while (pos < cand.size()) {
     Chunk ch;
-    const size_t next = codegen64(cb, cand, pos, false, ch.words, nullptr, ch.offs, ch.slots, rest, &max_feat, st);
+    const size_t next = codegen64(cb, cand, pos, opt, false, ch.words, nullptr, ch.offs, ch.slots, rest, &max_feat, st);
     if (next == pos) { rest.push_back(cand[pos]); if (st) st->nrejected++; pos = next + 1; continue; }
     if ((int)chunks.size() + 1 == kMaxParts64 && next < cand.size()) {
       for (size_t k = next; k < cand.size(); ++k) rest.push_back(cand[k]);
@@ -633,6 +689,7 @@ Module64* build64(const CompiledBatch<double>& cb, const std::vector<int32_t>& c
   const auto t1 = std::chrono::steady_clock::now();
   Module64* m = new Module64();
   m->nraw = max_feat + 1;
+  m->out = opt.out;
   try {
     for (Chunk& ch : chunks) {
       Part64 pt;
@@ -647,7 +704,8 @@ Module64* build64(const CompiledBatch<double>& cb, const std::vector<int32_t>& c
       HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, "sr_jit64_eval_w"));
       HIP_CHECK(hipModuleGetFunction(&q.fn_dl, q.mod, "sr_jit64_eval_dl"));
       HIP_CHECK(hipModuleGetFunction(&q.fn_dlw, q.mod, "sr_jit64_eval_dlw"));
-      for (hipFunction_t f : {q.fn, q.fn_w, q.fn_dl, q.fn_dlw})
+      HIP_CHECK(hipModuleGetFunction(&q.fn_out, q.mod, "sr_jit64_out"));
+      for (hipFunction_t f : {q.fn, q.fn_w, q.fn_dl, q.fn_dlw, q.fn_out})
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
       HIP_CHECK(hipMalloc((void**)&q.d_off, ch.offs.size() * sizeof(int32_t)));
@@ -687,6 +745,7 @@ int nraw64(const Module64* m) { return m ? m->nraw : 0; }
 hipError_t launch64(Module64* m, int k, const EvalPlan& plan, const EvalArgs<double>& a, hipStream_t stream) {
   const Part64& q = m->parts[k];
   if (a.nlist != q.nslots || m->nraw > a.nfeat || plan.tile != TILE2 || plan.threads != 256) return hipErrorInvalidValue;
+  if (m->out && (a.w != nullptr || a.out == nullptr || a.out_stride < a.n_pad)) return hipErrorInvalidValue;
   Jit64Args ja;
   ja.e = a;
   ja.code_off = q.d_off;
@@ -700,19 +759,23 @@ hipError_t launch64(Module64* m, int k, const EvalPlan& plan, const EvalArgs<dou
   const bool st = dl && dl[0] == '0';
   hipFunction_t fn = st ? (a.w ? q.fn_w : q.fn) : (a.w ? q.fn_dlw : q.fn_dl);
   note_kernel(st ? (a.w ? "sr_jit64_eval_w" : "sr_jit64_eval") : (a.w ? "sr_jit64_eval_dlw" : "sr_jit64_eval_dl"));
+  if (m->out) {  // per-row outputs: the compiled loop, every tree on every tile
+    fn = q.fn_out;
+    note_kernel("sr_jit64_out");
+  }
   return hipModuleLaunchKernel(fn, (unsigned)a.nrg * (unsigned)a.ntg, 1, 1, 256, 1, 1, (unsigned)lds, stream, nullptr,
                                cfg);
 }
 
 bool compile_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes,
-                    std::string* text, std::vector<int32_t>* offsets) {
+                    std::string* text, std::vector<int32_t>* offsets, const Opts64& opt) {
   const Tmpl64& T = tmpl64();
   if (!T.ok) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("Float64 jit template unavailable: ") + T.why);
   std::vector<uint32_t> words;
   std::vector<std::string> lines;
   std::vector<int32_t> offs, okt, rest;
   int mf = -1;
-  codegen64(cb, cand, 0, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, &mf, nullptr);
+  codegen64(cb, cand, 0, opt, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, &mf, nullptr);
   if (bytes) {
     bytes->resize(words.size() * 4);
     std::memcpy(bytes->data(), words.data(), bytes->size());

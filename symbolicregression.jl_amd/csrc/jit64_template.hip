@@ -2,11 +2,12 @@
 //
 // The Float64 counterpart of jit_template.hip: built once (make) into a
 // standalone gfx950 code object, embedded in libsrhip.so, copied and patched
-// per program. Three kernels:
+// per program. Kernels:
 //   sr_jit64_routines  never launched: the Float64 operator routines of
 //                      gen_jit64.py (one region: Float64 has no FAST path);
 //   sr_jit64_area      never launched: s_endpgm, then the code area;
-//   sr_jit64_eval(_w)  the driver: one workgroup = (row group, tree group) as
+//   sr_jit64_eval(_w), sr_jit64_eval_dl(w) (the hand-written tree loop), sr_jit64_out
+//                      (per-row outputs)  the driver: one workgroup = (row group, tree group) as
 //                      in eval_kernel.h, the row group staged tile-major
 //                      ([tile][y, x_0 .. x_{F-1}, w][128 rows of Float64], the
 //                      1 KiB per column of the Float32 tiles), each tree one call
@@ -43,7 +44,11 @@ struct Jit64Args {
   int nraw;                 // feature columns staged (the largest feature the code reads + 1)
 };
 
-template <bool W>
+// OUT: per-row output tree code (srhip_eval_tree_array): no y column is
+// staged, no failure flags are read or set (every tile of every tree is
+// evaluated, as the interpreter's MODE_OUT does), and each tree's code gets
+// its output rows of this row group in s[92:93] (jit64.cpp T_OUT).
+template <bool W, bool OUT = false>
 __device__ __forceinline__ void jit64_eval_body(const Jit64Args& ja) {
   const EvalArgs<double>& a = ja.e;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -63,6 +68,7 @@ __device__ __forceinline__ void jit64_eval_body(const Jit64Args& ja) {
       const int tk = idx / V;
       const int k = tk % narr;
       const int t = tk / narr;
+      if (OUT && k == 0) continue;  // no y
       const double* src = k == 0 ? a.y : (k <= ja.nraw ? a.X + (size_t)(k - 1) * a.n_pad : a.w);
       reinterpret_cast<double2*>(sX + (size_t)tk * TILE64)[v] =
           reinterpret_cast<const double2*>(src + row0 + (int64_t)t * TILE64)[v];
@@ -80,7 +86,9 @@ __device__ __forceinline__ void jit64_eval_body(const Jit64Args& ja) {
   auto code_of = [&](int s) {
     return __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(ja.code_off))[s]);
   };
-  auto ld_flag = [&](int slot) { return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  auto ld_flag = [&](int slot) {
+    return OUT ? 0u : __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
   uint64_t area;
   asm volatile(
       "s_getpc_b64 s[88:89]\n"
@@ -113,17 +121,28 @@ __device__ __forceinline__ void jit64_eval_body(const Jit64Args& ja) {
       const uint64_t target = area + (uint32_t)code_of(s);
       uint32_t la = lds_lane;
       uint32_t tile = 0, status;
-      asm volatile("s_swappc_b64 s[76:77], %[tgt]"
-                   : "+{v[44:45]}"(lsum), "+{v[40:41]}"(chk), "+{v42}"(la), "+{s64}"(tile), "={s69}"(status)
-                   : [tgt] "s"(target), "{v43}"(lane2), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
-                     "{s68}"(woff)
-                   : SR_JIT64_CLOBBERS, "memory");
+      if constexpr (OUT) {  // the tree's output rows of this row group
+        const int t = __builtin_amdgcn_readfirstlane(a.list[s]);
+        uint64_t optr = reinterpret_cast<uint64_t>(a.out + (size_t)t * (size_t)a.out_stride + row0);
+        asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                     : "+{v[44:45]}"(lsum), "+{v[40:41]}"(chk), "+{v42}"(la), "+{s64}"(tile), "={s69}"(status),
+                       "+{s[92:93]}"(optr)
+                     : [tgt] "s"(target), "{v43}"(lane2), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+                       "{s68}"(woff)
+                     : SR_JIT64_CLOBBERS, "memory");
+      } else {
+        asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                     : "+{v[44:45]}"(lsum), "+{v[40:41]}"(chk), "+{v42}"(la), "+{s64}"(tile), "={s69}"(status)
+                     : [tgt] "s"(target), "{v43}"(lane2), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+                       "{s68}"(woff)
+                     : SR_JIT64_CLOBBERS, "memory");
+      }
       (void)status;
     }
     lsum = wave_sum(lsum);
     chk = __builtin_amdgcn_ballot_w64(chk != chk) != 0 ? __builtin_nan("") : 0.0;
     if (lane == 0) dst[i] = Part<double>{lsum, chk};
-    if (!skip && chk != chk && lane == 0)
+    if (!OUT && !skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 }
@@ -297,3 +316,4 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit64_eval_dl(Jit64Args ja
 extern "C" __global__ void __launch_bounds__(1024) sr_jit64_eval_dlw(Jit64Args ja) { jit64_eval_dl_body<true>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit64_eval(Jit64Args ja) { jit64_eval_body<false>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit64_eval_w(Jit64Args ja) { jit64_eval_body<true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit64_out(Jit64Args ja) { jit64_eval_body<false, true>(ja); }

@@ -299,9 +299,12 @@ def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bo
     nb, nt, no = C.c_int64(0), C.c_int64(0), C.c_int64(0)
 
     def call(*bufs):
-        if f64:  # the Float64 tree compiler (jit64.cpp)
-            return lib().srhip_jit_compile(C.byref(tr), 8, bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
-                                           C.byref(no))
+        if f64 and loss is not None:  # the Float64 tree compiler with another loss's tail
+            return lib().srhip_jit_compile_loss(C.byref(tr), 0, 8, int(loss.kind), float(loss.param),
+                                                bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2], C.byref(no))
+        if f64:  # the Float64 tree compiler (jit64.cpp), L2 or per-row outputs
+            return lib().srhip_jit_compile(C.byref(tr), 8 | (4 if out else 0), bufs[0], C.byref(nb), bufs[1],
+                                           C.byref(nt), bufs[2], C.byref(no))
         if loss is not None:
             return lib().srhip_jit_compile_loss(C.byref(tr), int(grad), int(fast), int(loss.kind), float(loss.param),
                                                 bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2], C.byref(no))

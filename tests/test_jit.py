@@ -190,3 +190,26 @@ def test_float64_tree_code_equals_llvm_mc(k):
     assert len(offs) >= 0.6 * len(trees), f"only {len(offs)} of {len(trees)} trees compiled"
     assert "v_add_f64" in text or "v_mul_f64" in text
     assert assemble(text) == code
+
+
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.parametrize("what", ["out", "L1", "HUBER", "LP", "PERIODIC", "LOGITDIST"])
+def test_float64_output_and_loss_tree_code_equals_llvm_mc(what):
+    """The Float64 tree compiler's per-row output code (the root block stored
+    per tile) and its tile tails for the other losses (a loss routine of the
+    Float64 interpreter's elem_loss): same byte check, and every shallow tree
+    of config #3's operator set still compiles."""
+    b_ops, u_ops = F64_OPSETS[0]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    trees = srhip.random_population(200, o, 5, np.float64, seed=71)
+    flat = srhip.flatten(trees, o, dtype=np.float64)
+    _, _, base = jit_compile(flat)
+    if what == "out":
+        code, text, offs = jit_compile(flat, out=True)
+        assert "global_store_dwordx4" in text
+    else:
+        loss = srhip.SupervisedLoss(srhip.constants.LOSS[what], 2.5 if what in ("LP", "PERIODIC") else 0.7)
+        code, text, offs = jit_compile(flat, loss=loss)
+        assert "s_swappc_b64" in text
+    assert set(offs) == set(base)
+    assert assemble(text) == code

@@ -85,3 +85,75 @@ def test_float64_tree_code_new_constants_run_interpreted(gpu_ctx):
     s0, _, ok0 = progs["0"].eval_loss(ds, K.LOSS["L2"])
     assert np.array_equal(ok1, ok0)
     np.testing.assert_array_equal(s1[ok1], s0[ok0])
+
+
+def test_float64_output_tree_code_equals_interpreter(gpu_ctx):
+    """eval_tree_array of a Float64 program (config #3, InterfaceDynamicExpressions.jl:50-52)
+    through its per-row output tree code (jit64.cpp emit_store_out): every
+    tree's outputs identical to the interpreter's MODE_OUT (NaN where NaN),
+    did_succeed = interpreter = oracle."""
+    o = srhip.Options(**CFG3)
+    rng = np.random.default_rng(35)
+    n = 20_001
+    X = rng.uniform(-3, 3, (5, n))
+    y = np.zeros(n)
+    trees = srhip.random_population(1024, o, 5, np.float64, seed=36)
+    flat = srhip.flatten(trees, o, dtype=np.float64)
+    ctx = gpu_ctx
+    ds = srhip.DeviceDataset(ctx, X, y)
+    progs = _progs(ctx, flat)
+    out1, ok1 = progs["1"].eval_tree_array(ds)
+    assert ctx.last_tree_code() > 500 and ctx.last_kernel_name() == "sr_jit64_out"
+    out0, ok0 = progs["0"].eval_tree_array(ds)
+    assert ctx.last_tree_code() == 0
+    assert np.array_equal(ok1, ok0)
+    assert np.array_equal(out1, out0, equal_nan=True)
+    _, _, rok = oracle.eval_loss_batch(flat, X, y, dtype=np.float64, nthreads=16)
+    assert np.array_equal(ok1, rok)
+    # the values of succeeding trees against the oracle's Float64 evaluation
+    # (device vs host libm: ulp-level differences, amplified by cancellations)
+    ref = oracle.eval_trees(flat, X[:, :2000], dtype=np.float64)[0]
+    sel = np.flatnonzero(ok1)[:200]
+    with np.errstate(invalid="ignore", divide="ignore"):
+        rel = np.abs(out1[sel, :2000] - ref[sel]) / np.maximum(np.abs(ref[sel]), 1e-300)
+    assert np.mean(rel <= 1e-9) > 0.999, float(np.mean(rel <= 1e-9))
+
+
+LOSS_CASES = [("L1", 0.0), ("LP", 2.5), ("HUBER", 1.0), ("LOGCOSH", 0.0), ("L1EPSINS", 0.3), ("L2EPSINS", 0.3),
+              ("QUANTILE", 0.3), ("PERIODIC", 2.0), ("LOGITDIST", 0.0)]
+
+
+@pytest.mark.parametrize("loss,param", LOSS_CASES, ids=[c[0] for c in LOSS_CASES])
+def test_float64_loss_tree_code_other_losses(gpu_ctx, loss, param):
+    """Float64 tree code with another elementwise loss in the tile tail
+    (jit64.cpp emit_tail_loss: the Float64 interpreter's elem_loss as a
+    routine), weighted for half of the losses: tree code ran, did_succeed =
+    interpreter = oracle, losses within 1e-11 of the interpreter's (row-sum
+    order) and 1e-9 of the oracle's."""
+    o = srhip.Options(**CFG3)
+    k = [c[0] for c in LOSS_CASES].index(loss)
+    rng = np.random.default_rng(37 + k)
+    n = 10_001
+    X = rng.uniform(-3, 3, (5, n))
+    y = rng.standard_normal(n)
+    w = rng.uniform(0.5, 2.0, n) if k % 2 else None
+    trees = srhip.random_population(600, o, 5, np.float64, seed=38)
+    flat = srhip.flatten(trees, o, dtype=np.float64)
+    ctx = gpu_ctx
+    ds = srhip.DeviceDataset(ctx, X, y, w)
+    progs = _progs(ctx, flat)
+    s1, w1, ok1 = progs["1"].eval_loss(ds, K.LOSS[loss], [param])
+    assert ctx.last_tree_code() > 300
+    s0, w0, ok0 = progs["0"].eval_loss(ds, K.LOSS[loss], [param])
+    assert ctx.last_tree_code() == 0 and w1 == w0
+    assert np.array_equal(ok1, ok0)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        rel = np.abs(s1 - s0) / np.abs(s0)
+    m = ok1 & (s0 != 0) & np.isfinite(s0)
+    assert np.all(rel[m] <= 1e-11), float(np.nanmax(rel[m]))
+    _, rl, rok = oracle.eval_loss_batch(flat, X, y, w, K.LOSS[loss], (param,), dtype=np.float64, nthreads=16)
+    assert np.array_equal(ok1, rok)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        relo = np.abs(s1 / w1 - rl) / np.abs(rl)
+    mo = ok1 & np.isfinite(rl) & (rl != 0)
+    assert np.all(relo[mo] <= 1e-9), float(np.nanmax(relo[mo]))
