@@ -75,6 +75,12 @@ class JitRegs:
         return out
 
 
+# SGPRs held live across a loss routine besides tree-code state: the memory
+# constants (s24..s39), the hand-written loop's state (s40..s63) and the
+# registers above the state, so that its temporaries stay in s0..s23
+LOSS_PINNED_S = list(range(24, 64)) + [88, 89] + list(range(91, 102))
+
+
 def snippet_source(rg, routines):
     R = rg.R
     _, rest = rg.vstate()
@@ -107,10 +113,25 @@ def snippet_source(rg, routines):
         out.append(f'extern "C" __global__ void __launch_bounds__(64) sr_h_{name}() {{')
         out.append("  St s;")
         out += pins("in")
+        if name.startswith(("l_", "d_")):
+            # a loss routine runs inside the hand-written tree loop (its state
+            # in s40..s57) and between the tiles of memory-constant code (its
+            # constants in s24..s39): LOSS_PINNED_S are held live across it, so
+            # the compiler keeps its temporaries in s0..s23
+            zs = LOSS_PINNED_S
+            out.append(f"  unsigned zz[{len(zs)}];")
+            for i in range(0, len(zs), 8):
+                out.append('  asm volatile("; IN" : ' + ", ".join(f'"={{s{zs[j]}}}"(zz[{j}])'
+                                                                for j in range(i, min(i + 8, len(zs)))) + ");")
         out.append("  float& chk = s.chk; (void)chk;")
         out.append(f"  constexpr int R = {R}; (void)R;")
         out.append("  " + body)
         out += pins("out")
+        if name.startswith(("l_", "d_")):
+            zs = LOSS_PINNED_S
+            for i in range(0, len(zs), 8):
+                out.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{s{zs[j]}}}"(zz[{j}])'
+                                                                 for j in range(i, min(i + 8, len(zs)))) + ");")
         out.append("}")
     out.append("}  // namespace")
     return "\n".join(out) + "\n"
@@ -118,6 +139,13 @@ def snippet_source(rg, routines):
 
 def rows(expr):
     return f"_Pragma(\"unroll\") for (int r = 0; r < R; ++r) {{ {expr} }}"
+
+
+def rows_serial(expr):
+    """The R rows one after the other, the scheduler fenced between them: the
+    registers of one row's evaluation at a time (the Float64 pow / cos of the
+    parametric losses do not fit the routine temporaries four rows at once)."""
+    return " ".join("{ constexpr int r = %d; %s } __builtin_amdgcn_sched_barrier(0);" % (r, expr) for r in range(4))
 
 
 # sin / cos routines that hand arguments beyond the fast reduction back to the
@@ -200,7 +228,8 @@ def routine_list():
         imm = ("const double imm = __builtin_bit_cast(double, ((unsigned long long)s.s_kh << 32) | "
                "(unsigned long long)s.s_k); ")
         rs.append((f"l_{name.lower()}",
-                   imm + rows(f"s.a[r] = dev::elem_loss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"), False))
+                   imm + rows_serial(f"s.a[r] = dev::elem_loss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"),
+                   False))
     # dℓ/dr of the same losses (the gradient tree code's seed, jit_grad.cpp)
     for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
         if name == "L2":
@@ -208,7 +237,8 @@ def routine_list():
         imm = ("const double imm = __builtin_bit_cast(double, ((unsigned long long)s.s_kh << 32) | "
                "(unsigned long long)s.s_k); ")
         rs.append((f"d_{name.lower()}",
-                   imm + rows(f"s.a[r] = dev::elem_dloss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"), False))
+                   imm + rows_serial(f"s.a[r] = dev::elem_dloss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"),
+                   False))
     return rs
 
 
@@ -515,12 +545,17 @@ def build(hipcc, outdir, R):
     # reach them (logcosh, logitdist: Float64 constants) is left out, and that
     # loss runs interpreted (SR_JIT_LOSS_ROUTINE -1)
     # (and one whose VGPR temporaries run into the state block: LP's Float64 pow)
+    # A loss routine is compiled with LOSS_PINNED_S held live (snippet_source):
+    # the compiler may still borrow one of them, but saves it to a VGPR lane
+    # first and restores it before the routine ends (v_writelane /
+    # v_readlane), so those are not temporaries of the routine.
+    pinned = set(LOSS_PINNED_S)
     for n in [n for n in names if n.startswith(("l_", "d_"))]:
         used, vused = set(), set()
         for d in (fast, prec):
-            used |= G.regs_used(d[n], G.REG_S) - sstate
+            used |= G.regs_used(d[n], G.REG_S) - sstate - pinned
             vused |= G.regs_used(d[n], G.REG_V) - vstate
-        if any(24 <= r < 64 for r in used) or any(r >= rg.A for r in vused):
+        if any(r >= 24 for r in used) or any(r >= rg.A for r in vused):
             sys.stderr.write(f"gen_jit: loss routine {n} left out (SGPR temps {sorted(r for r in used if r >= 24)}, "
                              f"VGPR temps up to v{max(vused, default=0)})\n")
             names.remove(n)
@@ -528,7 +563,7 @@ def build(hipcc, outdir, R):
     for d in (fast, prec):
         for n in names:
             vtemp |= G.regs_used(d[n], G.REG_V) - vstate
-            stemp |= G.regs_used(d[n], G.REG_S) - sstate
+            stemp |= G.regs_used(d[n], G.REG_S) - sstate - (pinned if n.startswith(("l_", "d_")) else set())
     if vtemp & vstate or stemp & sstate:
         raise SystemExit("gen_jit: temp/state overlap")
     if max(vtemp, default=0) >= rg.A:

@@ -31,7 +31,7 @@ LOSSES = [
     (srhip.L1DistLoss(), True), (srhip.LPDistLoss(1.7), False), (srhip.LPDistLoss(3.0), False),
     (srhip.HuberLoss(0.8), True), (srhip.L1EpsilonInsLoss(0.3), True), (srhip.L2EpsilonInsLoss(0.3), True),
     (srhip.QuantileLoss(0.3), True), (srhip.PeriodicLoss(2.0), False),
-    (srhip.LogCoshLoss(), False), (srhip.LogitDistLoss(), False),
+    (srhip.LogCoshLoss(), True), (srhip.LogitDistLoss(), True),
 ]
 
 
@@ -95,12 +95,16 @@ def _dloss(loss, r):
         return np.where(ar > p, sg, 0.0)
     if kind == K.LOSS["L2EPSINS"]:
         return np.where(ar > p, 2.0 * (ar - p) * sg, 0.0)
+    if kind == K.LOSS["LOGCOSH"]:  # in T, as the loss: tanh(r)
+        return np.tanh(r)
+    if kind == K.LOSS["LOGITDIST"]:  # tanh(r / 2)
+        return np.tanh(0.5 * r)
     assert kind == K.LOSS["QUANTILE"]
     return np.where(r >= 0, p, p - 1.0)
 
 
 GRAD_LOSSES = [srhip.L1DistLoss(), srhip.HuberLoss(0.8), srhip.L1EpsilonInsLoss(0.3), srhip.L2EpsilonInsLoss(0.3),
-               srhip.QuantileLoss(0.3)]
+               srhip.QuantileLoss(0.3), srhip.LogCoshLoss(), srhip.LogitDistLoss()]
 
 
 @pytest.mark.parametrize("loss", GRAD_LOSSES, ids=[f"{l.kind}-{l.params}" for l in GRAD_LOSSES])
