@@ -240,6 +240,41 @@ BAD = ("s_swappc", "s_setpc", "s_getpc", "scratch_", "buffer_", "global_", "flat
        "s_buffer", "s_dcache", "s_endpgm", "s_sendmsg", "ds_", "s_waitcnt")
 
 
+def pins_first(asm_text, name):
+    """False if handler `name` writes a register ahead of the "; IN <regs>"
+    marker that pins it (live from the routine's entry in the tree code): the
+    compiler, which sees the register defined only at the marker, took it for
+    a free temporary there. Markers without a register list are not checked."""
+    m = re.search(rf"^sr_h_{name}:.*?$(.*?)^\.Lfunc_end", asm_text, re.S | re.M)
+    if not m:
+        raise SystemExit(f"gen_asm_interp: handler {name} not found in compiler output")
+    written_s, written_v, in_marker = set(), set(), False
+    for ln in m.group(1).splitlines():
+        s = ln.strip()
+        if s.startswith(";;#ASMSTART"):
+            in_marker = True
+            continue
+        if s.startswith(";;#ASMEND"):
+            in_marker = False
+            continue
+        if in_marker:
+            if s.startswith("; IN "):
+                regs = s[5:].split()
+                if (regs_used(regs, REG_S) & written_s) or (regs_used(regs, REG_V) & written_v):
+                    return False
+            continue
+        s = s.split(";")[0].strip()
+        parts = s.split(None, 1)
+        if not s or s.startswith(".") or len(parts) < 2:
+            continue
+        if parts[0].startswith(("s_cmp", "s_bitcmp", "s_cbranch", "s_branch", "s_nop", "v_cmpx")):
+            continue
+        dst = parts[1].split(",")[0]
+        written_s |= regs_used([dst], REG_S)
+        written_v |= regs_used([dst], REG_V)
+    return True
+
+
 def extract(asm_text, name):
     m = re.search(rf"^sr_h_{name}:.*?$(.*?)^\.Lfunc_end", asm_text, re.S | re.M)
     if not m:

@@ -75,10 +75,14 @@ class JitRegs:
         return out
 
 
-# SGPRs held live across a loss routine besides tree-code state: the memory
-# constants (s24..s39), the hand-written loop's state (s40..s63) and the
-# registers above the state, so that its temporaries stay in s0..s23
-LOSS_PINNED_S = list(range(24, 64)) + [88, 89] + list(range(91, 102))
+# Routine temporaries: s0..s22 and v0..v29. s23 is the prefetching tree
+# loop's next code offset (jit_template.hip SR_JIT_LOOP_PF_TEXT), v30 / v31
+# the loop's LDS tile / counter addresses: all live across every call.
+ROUTINE_S_END, ROUTINE_V_END = 23, 30
+# SGPRs held live across a loss routine besides tree-code state: s23, the
+# memory constants (s24..s39), the hand-written loop's state (s40..s63) and
+# the registers above the state, so that its temporaries stay in s0..s22
+LOSS_PINNED_S = list(range(23, 64)) + [88, 89] + list(range(91, 102))
 
 
 def snippet_source(rg, routines):
@@ -97,14 +101,16 @@ def snippet_source(rg, routines):
         for i in range(0, len(regs), 8):
             ch = regs[i:i + 8]
             if kind == "in":
-                lines.append('  asm volatile("; IN" : ' + ", ".join(f'"={{v{r}}}"(s.{e})' for e, r in ch) + ");")
+                lines.append('  asm volatile("; IN ' + " ".join(f"v{r}" for _, r in ch) + '" : ' +
+                             ", ".join(f'"={{v{r}}}"(s.{e})' for e, r in ch) + ");")
             else:
                 lines.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{v{r}}}"(s.{e})' for e, r in ch) + ");")
         ss = rg.sregs()
         for i in range(0, len(ss), 8):
             ch = ss[i:i + 8]
             if kind == "in":
-                lines.append('  asm volatile("; IN" : ' + ", ".join(f'"={{s{r}}}"(s.s_{n})' for n, r in ch) + ");")
+                lines.append('  asm volatile("; IN ' + " ".join(f"s{r}" for _, r in ch) + '" : ' +
+                             ", ".join(f'"={{s{r}}}"(s.s_{n})' for n, r in ch) + ");")
             else:
                 lines.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{s{r}}}"(s.s_{n})' for n, r in ch) + ");")
         return lines
@@ -117,11 +123,12 @@ def snippet_source(rg, routines):
             # a loss routine runs inside the hand-written tree loop (its state
             # in s40..s57) and between the tiles of memory-constant code (its
             # constants in s24..s39): LOSS_PINNED_S are held live across it, so
-            # the compiler keeps its temporaries in s0..s23
+            # the compiler keeps its temporaries in s0..s22
             zs = LOSS_PINNED_S
             out.append(f"  unsigned zz[{len(zs)}];")
             for i in range(0, len(zs), 8):
-                out.append('  asm volatile("; IN" : ' + ", ".join(f'"={{s{zs[j]}}}"(zz[{j}])'
+                out.append('  asm volatile("; IN ' + " ".join(f"s{zs[j]}" for j in range(i, min(i + 8, len(zs)))) +
+                           '" : ' + ", ".join(f'"={{s{zs[j]}}}"(zz[{j}])'
                                                                 for j in range(i, min(i + 8, len(zs)))) + ");")
         out.append("  float& chk = s.chk; (void)chk;")
         out.append(f"  constexpr int R = {R}; (void)R;")
@@ -495,6 +502,8 @@ def compile_bodies(hipcc, rg, routines, extra):
     bodies = {}
     for n, _, _ in routines:
         try:
+            if not G.pins_first(asm, n):  # a pinned register used as a temporary before its pin
+                raise SystemExit("code placed ahead of the register pins")
             bodies[n] = G.extract(asm, n)
         except SystemExit as e:  # a body the block cannot hold (memory operands, calls): no routine
             sys.stderr.write(f"gen_jit: routine {n} skipped ({e})\n")
@@ -555,8 +564,8 @@ def build(hipcc, outdir, R):
         for d in (fast, prec):
             used |= G.regs_used(d[n], G.REG_S) - sstate - pinned
             vused |= G.regs_used(d[n], G.REG_V) - vstate
-        if any(r >= 24 for r in used) or any(r >= rg.A for r in vused):
-            sys.stderr.write(f"gen_jit: loss routine {n} left out (SGPR temps {sorted(r for r in used if r >= 24)}, "
+        if any(r >= ROUTINE_S_END for r in used) or any(r >= ROUTINE_V_END for r in vused):
+            sys.stderr.write(f"gen_jit: loss routine {n} left out (SGPR temps {sorted(r for r in used if r >= ROUTINE_S_END)}, "
                              f"VGPR temps up to v{max(vused, default=0)})\n")
             names.remove(n)
     vtemp, stemp = set(), set()
@@ -566,10 +575,10 @@ def build(hipcc, outdir, R):
             stemp |= G.regs_used(d[n], G.REG_S) - sstate - (pinned if n.startswith(("l_", "d_")) else set())
     if vtemp & vstate or stemp & sstate:
         raise SystemExit("gen_jit: temp/state overlap")
-    if max(vtemp, default=0) >= rg.A:
-        raise SystemExit(f"gen_jit: routine VGPR temps reach v{max(vtemp)} (state starts at v{rg.A})")
-    if max(stemp, default=0) >= 64:
-        raise SystemExit(f"gen_jit: routine SGPR temps reach s{max(stemp)}")
+    if max(vtemp, default=0) >= ROUTINE_V_END:
+        raise SystemExit(f"gen_jit: routine VGPR temps reach v{max(vtemp)} (v{ROUTINE_V_END}+ held by the tree loop)")
+    if max(stemp, default=0) >= ROUTINE_S_END:
+        raise SystemExit(f"gen_jit: routine SGPR temps reach s{max(stemp)} (s{ROUTINE_S_END}+ held by the tree loop)")
 
     def with_ret(lines, n, t):
         body = list(lines)

@@ -66,6 +66,16 @@ class Regs64:
         return out
 
 
+# Registers of the hand-written Float64 tree loop (jit64_template.hip
+# SR_JIT64_LOOP_TEXT) live across every tree-code call: s46..s57 its state,
+# s60 / s61 the tree and slot, s[88:89] the code area, s[94:95] its return.
+# Held live across each routine (the compiler may borrow one only saved to a
+# VGPR lane and restored), so routine SGPR temporaries stay in s0..s45;
+# VGPR temporaries stay below v88 (the loop's LDS tile / counter addresses).
+LOOP64_PINNED_S = list(range(46, 64)) + [88, 89] + list(range(94, 98))
+ROUTINE64_S_END, ROUTINE64_V_END = 46, 88
+
+
 def snippet_source(rg, routines):
     pins, rest = rg.vpins()
     out = ["#define SRHIP_INLINE_ALL 1", '#include "interp.h"', "using namespace srhip; using namespace srhip::interp;",
@@ -79,14 +89,16 @@ def snippet_source(rg, routines):
         for i in range(0, len(pins), 8):
             ch = pins[i:i + 8]
             if kind == "in":
-                lines.append('  asm volatile("; IN" : ' + ", ".join(f'"={{{r}}}"(s.{e})' for e, r in ch) + ");")
+                lines.append('  asm volatile("; IN ' + " ".join(r for _, r in ch) + '" : ' +
+                             ", ".join(f'"={{{r}}}"(s.{e})' for e, r in ch) + ");")
             else:
                 lines.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{{r}}}"(s.{e})' for e, r in ch) + ");")
         ss = rg.sregs()
         for i in range(0, len(ss), 8):
             ch = ss[i:i + 8]
             if kind == "in":
-                lines.append('  asm volatile("; IN" : ' + ", ".join(f'"={{s{r}}}"(s.s_{n})' for n, r in ch) + ");")
+                lines.append('  asm volatile("; IN ' + " ".join(f"s{r}" for _, r in ch) + '" : ' +
+                             ", ".join(f'"={{s{r}}}"(s.s_{n})' for n, r in ch) + ");")
             else:
                 lines.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{s{r}}}"(s.s_{n})' for n, r in ch) + ");")
         return lines
@@ -95,10 +107,20 @@ def snippet_source(rg, routines):
         out.append(f'extern "C" __global__ void __launch_bounds__(64) sr_h_{name}() {{')
         out.append("  St s;")
         out += pin_lines("in")
+        zs = LOOP64_PINNED_S
+        out.append(f"  unsigned zz[{len(zs)}];")
+        for i in range(0, len(zs), 8):
+            out.append('  asm volatile("; IN ' + " ".join(f"s{zs[j]}" for j in range(i, min(i + 8, len(zs)))) +
+                       '" : ' + ", ".join(f'"={{s{zs[j]}}}"(zz[{j}])'
+                                                            for j in range(i, min(i + 8, len(zs)))) + ");")
+        out.append("  __builtin_amdgcn_sched_barrier(0);")  # the body after every pin
         out.append("  double& chk = s.chk; (void)chk;")
         out.append("  constexpr int R = 2; (void)R;")
         out.append("  " + body)
         out += pin_lines("out")
+        for i in range(0, len(zs), 8):
+            out.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{s{zs[j]}}}"(zz[{j}])'
+                                                             for j in range(i, min(i + 8, len(zs)))) + ");")
         out.append("}")
     out.append("}  // namespace")
     return "\n".join(out) + "\n"
@@ -156,6 +178,8 @@ def compile_bodies(hipcc, rg, routines):
     bodies = {}
     for n, _ in routines:
         try:
+            if not G.pins_first(asm, n):  # a pinned register used as a temporary before its pin
+                raise SystemExit("code placed ahead of the register pins")
             bodies[n] = G.extract(asm, n)
         except SystemExit as e:  # memory operands, calls: no routine (the operator stays interpreted)
             sys.stderr.write(f"gen_jit64: routine {n} left out ({e})\n")
@@ -172,17 +196,19 @@ def build(hipcc, outdir):
     sstate = {r for _, r in rg.sregs()}
     # a routine whose temporaries would live in tree-code state (or reach the
     # SGPRs above the state) is left out too
+    pinned = set(LOOP64_PINNED_S)  # borrowed ones are saved to a VGPR lane and restored
     for n in list(names):
         vt = G.regs_used(bodies[n], G.REG_V) - vstate
-        st = G.regs_used(bodies[n], G.REG_S) - sstate
-        if any(r >= 96 for r in vt) or any(64 <= r for r in st):
+        st = G.regs_used(bodies[n], G.REG_S) - sstate - pinned
+        if any(r >= ROUTINE64_V_END for r in vt) or any(r >= ROUTINE64_S_END for r in st):
             sys.stderr.write(f"gen_jit64: routine {n} left out (VGPRs up to v{max(vt, default=0)}, "
                              f"SGPRs up to s{max(st, default=0)})\n")
             names.remove(n)
     vtemp, stemp = set(), set()
     for n in names:
         vtemp |= G.regs_used(bodies[n], G.REG_V) - vstate
-        stemp |= G.regs_used(bodies[n], G.REG_S) - sstate
+        stemp |= G.regs_used(bodies[n], G.REG_S) - sstate - pinned
+    assert max(stemp, default=0) < ROUTINE64_S_END and max(vtemp, default=0) < ROUTINE64_V_END
     text = ["s_endpgm", ".p2align 8", ".globl sr_rt64", "sr_rt64:"]
     for n in names:
         body = list(bodies[n])

@@ -118,3 +118,54 @@ def test_the_lint_catches_the_round4_bug():
 def test_clobber_macros_declare_scc():
     for name in MACROS:
         assert _macro_has_scc(name), name
+
+
+def test_routine_temporaries_stay_clear_of_the_tree_loop():
+    """The hand-written prefetching tree loop (jit_template.hip
+    SR_JIT_LOOP_PF_TEXT) keeps the next tree's code offset in s23 and its LDS
+    addresses in v30 / v31 across every tree-code call: no routine may use them
+    as temporaries (round 5: a LogCosh routine that did faulted the GPU). A
+    loss routine may borrow s23 only saved to and restored from a VGPR lane."""
+    hdr = (CSRC / "gen" / "jit_layout_r4.h").read_text()
+    m = re.search(r"// routine VGPR temps v0\.\.v(\d+), SGPR temps \[([0-9, ]*)\]", hdr)
+    assert m, "layout header lost its temporaries line"
+    assert int(m.group(1)) < 30
+    assert max(int(s) for s in m.group(2).split(",")) < 23
+    inc = (CSRC / "gen" / "jit_routines_r4.inc").read_text()
+    lines = re.findall(r'^\s*"([^"\n]*)\\n"', inc, re.M)
+    bodies, cur = {}, None
+    for ln in lines:
+        m = re.match(r"(sr_rt_(?:fast|prec)_\w+):$", ln)
+        if m:
+            cur = m.group(1)
+            bodies[cur] = []
+        elif cur and not ln.startswith((".globl", ".L", ".p2align", ".fill")):
+            bodies[cur].append(ln)
+    assert len(bodies) > 50
+    borrowed = 0
+    for name, body in bodies.items():
+        uses = [ln for ln in body if re.search(r"\bs23\b", ln)]
+        if not uses:
+            continue
+        borrowed += 1
+        # saved first, restored last, from the same lane
+        assert re.match(r"v_writelane_b32 (v\d+), s23, (\d+)$", uses[0]), (name, uses[0])
+        v, lane = re.match(r"v_writelane_b32 (v\d+), s23, (\d+)$", uses[0]).groups()
+        assert uses[-1] == f"v_readlane_b32 s23, {v}, {lane}", (name, uses[-1])
+        assert name.startswith(("sr_rt_fast_l_", "sr_rt_prec_l_", "sr_rt_fast_d_", "sr_rt_prec_d_")), name
+    assert borrowed <= 8
+
+
+def test_float64_routine_temporaries_stay_clear_of_the_tree_loop():
+    """The hand-written Float64 tree loop (jit64_template.hip
+    SR_JIT64_LOOP_TEXT) keeps its state in s46..s57, s60/s61, s[88:89],
+    s[94:95] and v88/v89 across every call (round 5: LogCosh / LogitDist
+    routines with temporaries up to s51 sent its tree walk astray)."""
+    hdr = (CSRC / "gen" / "jit64_layout.h").read_text()
+    m = re.search(r"// routine VGPR temps \[([0-9, ]*)\], SGPR temps \[([0-9, ]*)\]", hdr)
+    assert m, "layout header lost its temporaries line"
+    assert max(int(v) for v in m.group(1).split(",")) < 88
+    assert max(int(s) for s in m.group(2).split(",")) < 46
+    clob = re.search(r"#define SR_JIT64_CLOBBERS (.*)", hdr).group(1)
+    for r in list(range(46, 58)) + [60, 61, 88, 89, 94, 95]:
+        assert f'"s{r}"' not in clob, r

@@ -193,7 +193,7 @@ def test_float64_tree_code_equals_llvm_mc(k):
 
 
 @pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
-@pytest.mark.parametrize("what", ["out", "L1", "HUBER", "LP", "PERIODIC", "LOGITDIST"])
+@pytest.mark.parametrize("what", ["out", "L1", "HUBER", "LP", "PERIODIC", "QUANTILE"])
 def test_float64_output_and_loss_tree_code_equals_llvm_mc(what):
     """The Float64 tree compiler's per-row output code (the root block stored
     per tile) and its tile tails for the other losses (a loss routine of the
