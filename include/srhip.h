@@ -326,13 +326,16 @@ int32_t srhip_optimize_constants_cb(const srhip_trees* trees, int32_t dtype, con
                                     uint8_t* out_converged, double* out_num_evals);
 
 /* ---- tree compiler ---------------------------------------------------------
- * Large Float32 programs are compiled to machine code, one block per tree
- * (symbolicregression.jl_amd/csrc/jit.cpp; SRHIP_JIT=0 turns it off, =1 on
- * for every size). Tree code computes exactly what the interpreter computes
- * (eval_loss with the L2 loss; other losses and per-row outputs run
- * interpreted). This reports: trees compiled, of which with a guarded
- * Float32-transcendental path, code bytes, host code generation and
- * code-object load times (ms). All zero for an interpreted program. */
+ * Large programs are compiled to machine code, one block per tree
+ * (symbolicregression.jl_amd/csrc/jit.cpp for Float32, jit64.cpp for
+ * Float64; SRHIP_JIT=0 turns it off, =1 on for every size). Tree code
+ * computes exactly what the interpreter computes: eval_loss with L2 and with
+ * the elementwise losses that have a loss routine (Float32: all but LP and
+ * Periodic; Float64: all but LogCosh and LogitDist — the others run
+ * interpreted), and the per-row outputs of eval_tree_array. This reports:
+ * trees compiled, of which with a guarded Float32-transcendental path, code
+ * bytes, host code generation and code-object load times (ms). All zero for
+ * an interpreted program. */
 int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nfast,
                                int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load);
 /* How srhip_program_set_constants applied new constants so far: in place
@@ -343,7 +346,8 @@ int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, i
  * as memory-constant tree code). */
 int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inplace, int64_t* out_rebuilt);
 /* Gradient tree code of this program (reverse-mode ∂L/∂c for
- * srhip_eval_loss_grad with the L2 loss, built on the first gradient call):
+ * srhip_eval_loss_grad with L2 and the losses with a Float32 dℓ/dr routine —
+ * all but LP and Periodic — built on the first gradient call):
  * trees compiled, trees left to the forward-mode interpreter, code bytes,
  * codegen and load times (ms). All zero before the first gradient call or for
  * Float64 programs. */
