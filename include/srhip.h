@@ -312,6 +312,13 @@ typedef struct srhip_constopt_options {
 int32_t srhip_optimize_constants_batch(srhip_ctx* ctx, srhip_dataset* ds, const srhip_trees* trees,
                                        const srhip_constopt_options* opts, void* out_consts, double* out_loss,
                                        uint8_t* out_converged, double* out_num_evals);
+/* Where the last srhip_optimize_constants_batch call of this thread spent
+ * its time: out[0..8] = total, program builds, set_constants, loss calls,
+ * gradient calls, the kernels inside those calls (HIP events) — seconds —
+ * then the number of builds, loss calls, gradient calls and full program
+ * rebuilds inside set_constants (the first n of these 10 written). The rest
+ * of the total is the host optimiser's own algebra. */
+int32_t srhip_constopt_profile(double* out, int32_t n);
 /* The same optimiser over any evaluator (row-sharded datasets whose partials
  * the caller all-reduces, custom losses on the CPU, tests): fn scores
  * ntasks candidates — tree_idx[k] is the input tree of candidate k, consts

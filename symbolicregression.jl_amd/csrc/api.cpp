@@ -514,7 +514,7 @@ bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::
   sub.arg = s_arg.data();
   sub.const_off = s_coff.data();
   sub.consts = s_c.data();
-  CompiledBatch<T> rb = compile_batch_par<T>(sub, grad);
+  CompiledBatch<T> rb = compile_batch_par<T>(sub, grad, p->jit_memc);
   for (int r = 0; r < nr; ++r) {
     const int t = redo[r];
     if (rb.tree_off[r] >= 0) {
@@ -585,7 +585,7 @@ void build_grad_program(srhip_program* p) {
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
   tr.consts = p->consts.data();
-  CompiledBatch<T> cb = compile_batch_par<T>(tr, /*grad=*/true);
+  CompiledBatch<T> cb = compile_batch_par<T>(tr, /*grad=*/true, p->jit_memc);
   if (p->ntrees >= (1 << 24)) throw Error(SRHIP_ERR_UNSUPPORTED, "too many trees for gradient work items");
   p->g_static_fail = cb.static_fail;
   p->g_opset = OPSET_BASIC;
@@ -790,7 +790,7 @@ void build_program(srhip_program* p) {
   tr.arg = p->arg.data();
   tr.const_off = p->const_off.data();
   tr.consts = p->consts.data();
-  CompiledBatch<T> cb = compile_batch_par<T>(tr);
+  CompiledBatch<T> cb = compile_batch_par<T>(tr, /*grad=*/false, p->jit_memc);
   p->nodes = cb.nodes;
   p->static_fail = cb.static_fail;
   p->fail_if_rows = cb.fail_if_rows;
@@ -938,6 +938,9 @@ void update_constants(srhip_program* p) {
                       &p->fail_if_rows, /*grad=*/false, &vchg)) {
     ++p->n_rebuild;
     build_program<T>(p);
+    if (std::getenv("SRHIP_DEBUG_SETC"))
+      std::fprintf(stderr, "srhip set_constants: full rebuild of %d trees %.1f us\n", p->ntrees,
+                   std::chrono::duration<double, std::micro>(std::chrono::steady_clock::now() - t0).count());
     return;
   }
   if (vchg) p->verdict_stale = true;
@@ -2630,6 +2633,18 @@ void write_result(const copt::Result& r, int dtype, void* out_consts, double* ou
   }
 }
 
+// Where the time of the last srhip_optimize_constants_batch call on this
+// thread went (srhip_constopt_profile): program builds, constant uploads,
+// loss and gradient calls (wall), the kernels inside them (HIP events).
+struct CoptProfile {
+  double total = 0, create = 0, set = 0, loss = 0, grad = 0, kernel_ms = 0;
+  int64_t ncreate = 0, nloss = 0, ngrad = 0, nrebuilt = 0;
+};
+thread_local CoptProfile t_copt;
+double secs_since(std::chrono::steady_clock::time_point t0) {
+  return std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count();
+}
+
 // The candidates of one evaluation set as a program on the engine (memory-
 // constant tree code: constant updates never recompile); loss and ∂L/∂c of
 // every member in one call each, finished as the reference's loss (:12-19).
@@ -2667,15 +2682,21 @@ struct EngineSet : copt::Set {
     tr.arg = arg.data();
     tr.const_off = coff.data();
     tr.consts = cst.data();
+    const auto t0 = std::chrono::steady_clock::now();
     check_rc(srhip_program_create_ex(ctx, dtype, &tr, SRHIP_PROGRAM_VARYING_CONSTANTS, &prog));
+    t_copt.create += secs_since(t0);
+    t_copt.ncreate += 1;
   }
   ~EngineSet() override {
+    int64_t inplace = 0, rebuilt = 0;
+    if (prog && srhip_program_update_stats(prog, &inplace, &rebuilt) == SRHIP_OK) t_copt.nrebuilt += rebuilt;
     if (prog) (void)srhip_program_destroy(prog);
   }
   void eval(const std::vector<double>& X, bool grad, std::vector<double>& f, std::vector<double>& g) override {
     const int n = (int)coff.size() - 1;
     const size_t nc = (size_t)coff.back();
     if (X.size() != nc) throw Error(SRHIP_ERR_INVALID, "constant count mismatch");
+    auto t0 = std::chrono::steady_clock::now();
     if (dtype == SRHIP_F32) {
       std::vector<float> c(nc);
       for (size_t j = 0; j < nc; ++j) c[j] = (float)X[j];
@@ -2683,11 +2704,19 @@ struct EngineSet : copt::Set {
     } else {
       check_rc(srhip_program_set_constants(prog, X.data()));
     }
+    t_copt.set += secs_since(t0);
     std::vector<double> sums(std::max(n, 1)), dl(std::max<size_t>(nc, 1));
     std::vector<uint8_t> ok(std::max(n, 1));
     double wsum = 0.0;
+    t0 = std::chrono::steady_clock::now();
     if (grad) check_rc(srhip_eval_loss_grad(ds, prog, loss, params, sums.data(), dl.data(), &wsum, ok.data()));
     else check_rc(srhip_eval_loss(ds, prog, loss, params, nullptr, 0, sums.data(), &wsum, ok.data()));
+    (grad ? t_copt.grad : t_copt.loss) += secs_since(t0);
+    (grad ? t_copt.ngrad : t_copt.nloss) += 1;
+    {
+      double ms = 0.0;
+      if (srhip_last_kernel_time(ctx, &ms, nullptr) == SRHIP_OK) t_copt.kernel_ms += ms;
+    }
     f.assign(n, 0.0);
     for (int t = 0; t < n; ++t) {
       const double v = sums[t] / wsum;
@@ -2754,6 +2783,8 @@ int32_t srhip_optimize_constants_batch(srhip_ctx* ctx, srhip_dataset* ds, const 
     if (!ds) throw Error(SRHIP_ERR_INVALID, "null dataset");
     if (!opts) throw Error(SRHIP_ERR_INVALID, "null options");
     if (opts->loss_kind < 0 || opts->loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
+    t_copt = CoptProfile();
+    const auto t0 = std::chrono::steady_clock::now();
     copt::Problem pb = make_problem(trees, ds->dtype);
     EngineFactory fac;
     fac.ctx = ctx ? ctx : ds->ctx;
@@ -2764,6 +2795,18 @@ int32_t srhip_optimize_constants_batch(srhip_ctx* ctx, srhip_dataset* ds, const 
     fac.params = opts->loss_params;
     const copt::Result r = copt::optimize(pb, make_copt_options(opts), fac);
     write_result(r, ds->dtype, out_consts, out_loss, out_converged, out_num_evals, true);
+    t_copt.total = secs_since(t0);
+    return SRHIP_OK;
+  });
+}
+
+int32_t srhip_constopt_profile(double* out, int32_t n) {
+  return guarded([&] {
+    if (!out || n < 0) throw Error(SRHIP_ERR_INVALID, "null output");
+    const CoptProfile& q = t_copt;
+    const double v[10] = {q.total, q.create, q.set, q.loss, q.grad, q.kernel_ms * 1e-3,
+                          (double)q.ncreate, (double)q.nloss, (double)q.ngrad, (double)q.nrebuilt};
+    for (int32_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
     return SRHIP_OK;
   });
 }

@@ -216,7 +216,7 @@ struct TreeCompiler {
 }  // namespace
 
 template <typename T>
-CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
+CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad, bool keep_layout) {
   if (trees.ntrees < 0) throw Error(SRHIP_ERR_INVALID, "negative tree count");
   if (trees.ntrees > 0 && (!trees.node_off || !trees.kind || !trees.arg || !trees.const_off))
     throw Error(SRHIP_ERR_INVALID, "null tree arrays");
@@ -296,26 +296,38 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
     if (grad) {
       // gradient programs: no folding; a non-finite constant fails statically
       if (ce - cb0 > 255) throw Error(SRHIP_ERR_UNSUPPORTED, "gradients support at most 255 constants per tree");
-      if (tc.any_const_nonfinite(root)) { cb.static_fail[t] = 1; continue; }
+      if (tc.any_const_nonfinite(root)) {
+        cb.static_fail[t] = 1;
+        if (!keep_layout) continue;
+      }
       cb.need[t] = tc.compute_need(root);
       if (cb.need[t] > kMaxSlots) throw Error(SRHIP_ERR_UNSUPPORTED, "tree needs more than 16 stack slots");
       cb.tree_off[t] = (int32_t)cb.code.size();
       tc.emit(root, 0);
       tc.put(OP_END, 0, 0, T(0));
       cb.len[t] = (int32_t)cb.code.size() - cb.tree_off[t];
-      cb.direct[t] = 1;
+      cb.direct[t] = !cb.static_fail[t];  // a failing tree is recompiled at the next set (its verdict)
       continue;
     }
     const bool root_is_leaf = tc.nd[root].deg == 0;
     tc.fold(root);
-    if (tc.fold_fail) { cb.static_fail[t] = 1; continue; }
-    if (root_is_leaf || tc.nd[root].deg == 0) {
+    // keep_layout (programs whose constants change: set_constants patches
+    // them in place): a tree that fails statically keeps its code too — its
+    // verdict decides its result — so that constants that make it finite
+    // again are patched into that code instead of rebuilding the program
+    if (tc.fold_fail) {
+      cb.static_fail[t] = 1;
+      if (!keep_layout) continue;
+    } else if (root_is_leaf || tc.nd[root].deg == 0) {
       // a leaf (or folded) root: `deg0_eval` fill/copy + the final array check
       const HNode& r = tc.nd[root];
-      if (r.feat < 0 && !std::isfinite(r.val)) { cb.fail_if_rows[t] = 1; continue; }
+      if (r.feat < 0 && !std::isfinite(r.val)) {
+        cb.fail_if_rows[t] = 1;
+        if (!keep_layout) continue;
+      }
     } else if (tc.nonroot_const_nonfinite(root)) {
       cb.static_fail[t] = 1;
-      continue;
+      if (!keep_layout) continue;
     }
     cb.need[t] = tc.compute_need(root);
     if (cb.need[t] > kMaxSlots) throw Error(SRHIP_ERR_UNSUPPORTED, "tree needs more than 16 stack slots");
@@ -323,7 +335,9 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
     tc.emit(root, 0);
     tc.put(OP_END, 0, 0, T(0));
     cb.len[t] = (int32_t)cb.code.size() - cb.tree_off[t];
-    cb.direct[t] = 1;  // folded values are in the map too (folds)
+    // folded values are in the map too (folds); a tree kept by keep_layout
+    // despite its verdict is recompiled at the next set, which decides it anew
+    cb.direct[t] = !(cb.static_fail[t] || cb.fail_if_rows[t]);
   }
   cb.max_feature = tc.max_feat;
   // trailing OP_ENDs: the kernels prefetch one instruction past each END and
@@ -333,11 +347,11 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad) {
 }
 
 template <typename T>
-CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad) {
+CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad, bool keep_layout) {
   const int nt = trees.ntrees;
   const unsigned hw = std::max(1u, std::thread::hardware_concurrency());
   const int nthr = (int)std::min<unsigned>(8u, hw);
-  if (nt < 2048 || nthr < 2) return compile_batch<T>(trees, grad);
+  if (nt < 2048 || nthr < 2) return compile_batch<T>(trees, grad, keep_layout);
   const int nchunk = nthr;
   std::vector<CompiledBatch<T>> part(nchunk);
   std::vector<std::exception_ptr> err(nchunk);
@@ -350,7 +364,7 @@ CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad) {
         v.ntrees = t1 - t0;
         v.node_off = trees.node_off + t0;
         v.const_off = trees.const_off + t0;
-        part[k] = compile_batch<T>(v, grad);
+        part[k] = compile_batch<T>(v, grad, keep_layout);
       } catch (...) {
         err[k] = std::current_exception();
       }
@@ -417,10 +431,10 @@ bool eval_fold(const FoldRec& f, const srhip_trees& trees, T* out) {
   return true;
 }
 
-template CompiledBatch<float> compile_batch<float>(const srhip_trees&, bool);
-template CompiledBatch<double> compile_batch<double>(const srhip_trees&, bool);
-template CompiledBatch<float> compile_batch_par<float>(const srhip_trees&, bool);
-template CompiledBatch<double> compile_batch_par<double>(const srhip_trees&, bool);
+template CompiledBatch<float> compile_batch<float>(const srhip_trees&, bool, bool);
+template CompiledBatch<double> compile_batch<double>(const srhip_trees&, bool, bool);
+template CompiledBatch<float> compile_batch_par<float>(const srhip_trees&, bool, bool);
+template CompiledBatch<double> compile_batch_par<double>(const srhip_trees&, bool, bool);
 template bool eval_fold<float>(const FoldRec&, const srhip_trees&, float*);
 template bool eval_fold<double>(const FoldRec&, const srhip_trees&, double*);
 

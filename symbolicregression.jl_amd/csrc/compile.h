@@ -55,13 +55,16 @@ bool eval_fold(const FoldRec& f, const srhip_trees& trees, T* out);
 // grad = true compiles for the constant-gradient kernels: no constant folding,
 // every constant operand carries its get_constants index in the slot field,
 // and a non-finite constant anywhere fails the tree statically.
+// keep_layout = true (programs whose constants change in place): a tree that
+// fails statically is compiled anyway (static_fail / fail_if_rows still set),
+// so its code keeps its place when later constants make it finite again.
 template <typename T>
-CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad = false);
+CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad = false, bool keep_layout = false);
 
 // compile_batch over contiguous slices of the batch on several host threads
 // (large batches: srhip_program_set_constants recompiles every call); the
 // result is identical to compile_batch's.
 template <typename T>
-CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad = false);
+CompiledBatch<T> compile_batch_par(const srhip_trees& trees, bool grad = false, bool keep_layout = false);
 
 }  // namespace srhip

@@ -262,40 +262,47 @@ void run_gradient(const Problem& pb, const std::vector<int>& sel, const Options&
     std::unique_ptr<Set> sev;
     std::vector<int> sub_ks;
     std::vector<int64_t> sub_pos;
+    // the candidates still searching: a candidate that stops never resumes,
+    // and one that does not shrink only has its trial point reset to x
+    std::vector<int> live;
+    for (int k = 0; k < nc; ++k)
+      if (searching[k]) live.push_back(k);
+    std::vector<uint8_t> shrink(nc, 0);
     for (;;) {
       bool any_shrink = false;
-      std::vector<uint8_t> shrink(nc), halve(nc), step(nc);
-      for (int k = 0; k < nc; ++k) {
+      int nshrink = 0;
+      for (int k : live) {
         const bool fin = std::isfinite(phix1[k]);
-        halve[k] = searching[k] && !fin && finite_left[k] > 0;  // halve until the loss is finite
-        bool s = searching[k] && (fin || halve[k]);
+        const bool halve = searching[k] && !fin && finite_left[k] > 0;  // halve until the loss is finite
+        bool s = searching[k] && (fin || halve);
         const bool armijo = s && fin && (phix1[k] <= f[k] + C1 * a2[k] * dphi0[k]);
         s = s && !armijo;
         const bool failed = s && fin && ls_iter[k] >= LS_ITERATIONS;  // a failed line search stays at x
         s = s && !failed;
         searching[k] = s;
         if (failed) phix1[k] = kInf;
-        step[k] = s && fin;
-        if (halve[k]) finite_left[k] -= 1;
-        if (step[k]) ls_iter[k] += 1;
-        const double at = backtrack(a1[k], a2[k], f[k], dphi0[k], phix0[k], phix1[k], first[k]);
-        shrink[k] = halve[k] || step[k];
-        if (shrink[k]) a1[k] = a2[k];
-        a2[k] = halve[k] ? a2[k] * 0.5 : (step[k] ? at : a2[k]);
-        if (step[k]) first[k] = 0;
+        const bool step = s && fin;
+        if (halve) finite_left[k] -= 1;
+        if (step) ls_iter[k] += 1;
+        shrink[k] = halve || step;
+        if (shrink[k]) {
+          const double at = step ? backtrack(a1[k], a2[k], f[k], dphi0[k], phix0[k], phix1[k], first[k]) : 0.0;
+          a1[k] = a2[k];
+          a2[k] = halve ? a2[k] * 0.5 : at;
+        }
+        if (step) first[k] = 0;
         any_shrink = any_shrink || shrink[k];
+        nshrink += shrink[k];
       }
       if (!any_shrink) break;
-      for (int k = 0; k < nc; ++k)
+      for (int k : live)
         for (int64_t j = c.off[k]; j < c.off[k + 1]; ++j)
           Xt[j] = num.rt(shrink[k] ? Xbase[j] + a2[k] * S[j] : Xbase[j]);
-      int nshrink = 0;
-      for (int k = 0; k < nc; ++k) nshrink += shrink[k];
       if (!sev && fac.has_subset() && (int64_t)nshrink * SUBSET_FRACTION < nc) {
         // the stragglers (a line search that keeps shrinking) continue on their own set
         std::vector<int32_t> mem;
-        for (int k = 0; k < nc; ++k)
-          if (searching[k] || halve[k]) {
+        for (int k : live)
+          if (shrink[k]) {
             sub_ks.push_back(k);
             mem.push_back(c.tree[k]);
             for (int64_t j = c.off[k]; j < c.off[k + 1]; ++j) sub_pos.push_back(j);
@@ -311,13 +318,18 @@ void run_gradient(const Problem& pb, const std::vector<int>& sel, const Options&
       } else {
         ev->eval(Xt, false, trial, fdum);
       }
-      for (int k = 0; k < nc; ++k) {
+      for (int k : live) {
         f_calls[k] += shrink[k];
         if (shrink[k]) {
           phix0[k] = phix1[k];
           phix1[k] = trial[k];
         }
       }
+      // who did not shrink this round has stopped searching
+      size_t w = 0;
+      for (int k : live)
+        if (shrink[k]) live[w++] = k;
+      live.resize(w);
     }
 
     // accept, the new gradient (one evaluation), BFGS update, convergence (Optim.converged)

@@ -109,6 +109,7 @@ SIGNATURES = {
     "srhip_jit_compile_loss": [C.POINTER(Trees), C.c_int32, C.c_int32, C.c_int32, C.c_double, C.c_void_p,
                                C.POINTER(C.c_int64), C.c_char_p, C.POINTER(C.c_int64), C.c_void_p,
                                C.POINTER(C.c_int64)],
+    "srhip_constopt_profile": [C.POINTER(C.c_double), C.c_int32],
     "srhip_optimize_constants_batch": [C.c_void_p, C.c_void_p, C.POINTER(Trees), C.POINTER(ConstOptOptions),
                                        C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
     "srhip_optimize_constants_cb": [C.POINTER(Trees), C.c_int32, C.POINTER(ConstOptOptions), CONSTOPT_EVAL_FN,

@@ -24,6 +24,8 @@ before = srhip.eval_loss_batch(trees, ds, o)
 t0 = time.perf_counter()
 res = srhip.optimize_constants_batch(ds, trees, o, rng=np.random.default_rng(0))
 dt = time.perf_counter() - t0
+from srhip.constant_optimization import last_profile  # noqa: E402
+prof = last_profile()
 m = np.isfinite(before)
 print(json.dumps({
     "tool": "bench_constopt", "ntrees": ntrees, "rows": rows, "nfeat": nfeat, "seconds": dt,
@@ -31,4 +33,5 @@ print(json.dumps({
     "loss_evals_x_rows_per_s": float(res.num_evals.sum()) * rows / dt,
     "converged": int(res.converged.sum()),
     "improved": int((res.losses[m] < before[m]).sum()), "finite_before": int(m.sum()),
+    "profile": prof,
 }))
