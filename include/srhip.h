@@ -400,7 +400,9 @@ int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t f
  * gradient programs, grad = 1) and compares every tree with a fresh compile
  * of the new constants: out_mismatch = trees whose instruction stream or
  * static verdict differs (0 is correct), out_recompiled = trees the update
- * compiled again, out_relayout = 1 when it needed a rebuild instead. */
+ * compiled again, out_relayout = 1 when it needed a rebuild instead.
+ * grad | 2: the images of a program whose constants change (VARYING_CONSTANTS
+ * or after its first set: a tree that fails statically keeps its code). */
 int32_t srhip_debug_constant_map(const srhip_trees* trees, int32_t dtype, int32_t grad, const void* new_consts,
                                  int64_t* out_mismatch, int64_t* out_recompiled, int32_t* out_relayout);
 

@@ -280,6 +280,9 @@ struct srhip_program {
   std::vector<int32_t> h_cmap, h_gcmap;
   std::vector<uint8_t> h_direct, h_gdirect;
   std::vector<FoldRec> h_folds, h_gfolds;
+  // the constants each image was last compiled / patched with: a tree that
+  // is recompiled at every set (a failing one) is skipped while they stand
+  std::vector<unsigned char> h_cprev, h_gcprev;
   int64_t n_inplace = 0, n_rebuild = 0;
   int opset = OPSET_FULL;      // smallest operator set covering the compiled programs
   // gradient programs (compiled on first use)
@@ -462,7 +465,7 @@ template <typename T>
 bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::vector<int32_t>& toff,
                  const std::vector<int32_t>& len, std::vector<int32_t>& cmap, std::vector<uint8_t>& direct,
                  std::vector<FoldRec>& folds, std::vector<uint8_t>& sfail, std::vector<uint8_t>* fir, bool grad,
-                 bool* verdicts_changed, int64_t* n_recompiled = nullptr) {
+                 bool* verdicts_changed, std::vector<unsigned char>& cprev, int64_t* n_recompiled = nullptr) {
   const int nt = p->ntrees;
   if (cmap.size() * sizeof(Ins<T>) != code.size() || (int)direct.size() != nt || (int)toff.size() != nt ||
       (int)len.size() != nt || (int)sfail.size() != nt)
@@ -478,7 +481,10 @@ bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::
   tr.const_off = co;
   tr.consts = c;
   std::vector<int32_t> redo;
+  const T* cp = cprev.size() == p->consts.size() ? reinterpret_cast<const T*>(cprev.data()) : nullptr;
   for (int t = 0; t < nt; ++t) {
+    if (!direct[t] && cp && std::memcmp(cp + co[t], c + co[t], (size_t)(co[t + 1] - co[t]) * sizeof(T)) == 0)
+      continue;  // compiled with these very constants: same code, same verdict
     if (direct[t]) {
       bool finite = true;
       for (int k = co[t]; k < co[t + 1]; ++k) finite &= std::isfinite(c[k]);
@@ -493,7 +499,10 @@ bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::
   }
   if (n_recompiled) *n_recompiled = (int64_t)redo.size();
   if (std::getenv("SRHIP_DEBUG_SETC")) std::fprintf(stderr, "srhip set_constants: %d of %d trees recompiled\n", (int)redo.size(), nt);
-  if (redo.empty()) return true;
+  if (redo.empty()) {
+    cprev = p->consts;
+    return true;
+  }
   const int nr = (int)redo.size();
   std::vector<int32_t> s_noff(1, 0), s_coff(1, 0);
   std::vector<uint8_t> s_kind;
@@ -550,6 +559,7 @@ bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::
     sfail[t] = rb.static_fail[r];
     if (fir) (*fir)[t] = rb.fail_if_rows[r];
   }
+  cprev = p->consts;
   return true;
 }
 
@@ -562,7 +572,7 @@ void patch_grad_constants(srhip_program* p) {
   p->grad_stale = false;
   bool vchg = false;  // the gradient kernels read the verdicts from the programs themselves
   if (patch_image<T>(p, p->h_gcode, p->h_gtoff, p->h_glen, p->h_gcmap, p->h_gdirect, p->h_gfolds, p->g_static_fail,
-                     nullptr, /*grad=*/true, &vchg)) {
+                     nullptr, /*grad=*/true, &vchg, p->h_gcprev)) {
     hipStream_t s = p->ctx->stream;
     HIP_CHECK(hipMemcpyAsync(p->d_gcode, p->h_gcode.data(), p->h_gcode.size(), hipMemcpyHostToDevice, s));
     HIP_CHECK(hipStreamSynchronize(s));
@@ -684,6 +694,7 @@ void build_grad_program(srhip_program* p) {
   p->h_gcmap = cb.cmap;
   p->h_gdirect = cb.direct;
   p->h_gfolds = cb.folds;
+  p->h_gcprev = p->consts;
   p->grad_built = true;
   p->grad_stale = false;
 }
@@ -895,6 +906,7 @@ void build_program(srhip_program* p) {
   p->h_cmap = cb.cmap;
   p->h_direct = cb.direct;
   p->h_folds = cb.folds;
+  p->h_cprev = p->consts;
 }
 
 // srhip_program_set_constants: new immediates written into the host image
@@ -935,7 +947,7 @@ void update_constants(srhip_program* p) {
   bool vchg = false;
   const auto t0 = std::chrono::steady_clock::now();
   if (!patch_image<T>(p, p->h_code, p->h_toff, p->h_len, p->h_cmap, p->h_direct, p->h_folds, p->static_fail,
-                      &p->fail_if_rows, /*grad=*/false, &vchg)) {
+                      &p->fail_if_rows, /*grad=*/false, &vchg, p->h_cprev)) {
     ++p->n_rebuild;
     build_program<T>(p);
     if (std::getenv("SRHIP_DEBUG_SETC"))
@@ -2523,10 +2535,11 @@ int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t f
 
 namespace {
 template <typename T>
-void constant_map_check(const srhip_trees* trees, bool grad, const void* new_consts, int64_t* mismatch,
+void constant_map_check(const srhip_trees* trees, bool grad, bool keep, const void* new_consts, int64_t* mismatch,
                         int64_t* recompiled, int32_t* relayout) {
   srhip_program p;  // host state only: patch_image reads the trees and writes the images
   p.ntrees = trees->ntrees;
+  p.jit_memc = keep;  // patch_image recompiles with keep_layout for such programs
   const int nt = trees->ntrees;
   p.node_off.assign(trees->node_off, trees->node_off + nt + 1);
   p.const_off.assign(trees->const_off, trees->const_off + nt + 1);
@@ -2535,26 +2548,32 @@ void constant_map_check(const srhip_trees* trees, bool grad, const void* new_con
   const size_t cbytes = (size_t)p.const_off[nt] * sizeof(T);
   p.consts.resize(std::max<size_t>(cbytes, 1));
   if (cbytes) std::memcpy(p.consts.data(), trees->consts, cbytes);
-  CompiledBatch<T> cb = compile_batch_par<T>(*trees, grad);
+  CompiledBatch<T> cb = compile_batch_par<T>(*trees, grad, keep);
   std::vector<unsigned char> code(reinterpret_cast<const unsigned char*>(cb.code.data()),
                                   reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   std::vector<uint8_t> sfail = cb.static_fail, fir = cb.fail_if_rows;
+  std::vector<unsigned char> cprev = p.consts;  // the constants the image was compiled with
   if (cbytes) std::memcpy(p.consts.data(), new_consts, cbytes);
   bool vchg = false;
   *relayout = patch_image<T>(&p, code, cb.tree_off, cb.len, cb.cmap, cb.direct, cb.folds, sfail, grad ? nullptr : &fir,
-                             grad, &vchg, recompiled) ? 0 : 1;
+                             grad, &vchg, cprev, recompiled) ? 0 : 1;
   if (*relayout) return;
   srhip_trees fresh_trees = *trees;
   fresh_trees.consts = new_consts;
-  const CompiledBatch<T> fresh = compile_batch_par<T>(fresh_trees, grad);
+  const CompiledBatch<T> fresh = compile_batch_par<T>(fresh_trees, grad, keep);
   const Ins<T>* ins = reinterpret_cast<const Ins<T>*>(code.data());
   *mismatch = 0;
   for (int t = 0; t < nt; ++t) {
     bool bad = sfail[t] != fresh.static_fail[t] || (!grad && fir[t] != fresh.fail_if_rows[t]);
-    if (!bad && fresh.tree_off[t] >= 0) {
+    // a tree that fails statically is never evaluated: its immediates are free
+    if (!bad && fresh.tree_off[t] >= 0 && !fresh.static_fail[t] && !fresh.fail_if_rows[t]) {
       bad = cb.tree_off[t] < 0 || cb.len[t] != fresh.len[t] ||
             std::memcmp(ins + cb.tree_off[t], &fresh.code[fresh.tree_off[t]], sizeof(Ins<T>) * fresh.len[t]) != 0;
     }
+    if (bad && std::getenv("SRHIP_DEBUG_CMAP"))
+      std::fprintf(stderr, "cmap mismatch tree %d: sfail %d/%d fir %d/%d toff %d/%d len %d/%d\n", t, sfail[t],
+                   fresh.static_fail[t], fir[t], fresh.fail_if_rows[t], cb.tree_off[t], fresh.tree_off[t], cb.len[t],
+                   fresh.len[t]);
     *mismatch += bad ? 1 : 0;
   }
 }
@@ -2570,8 +2589,9 @@ int32_t srhip_debug_constant_map(const srhip_trees* trees, int32_t dtype, int32_
     *out_mismatch = 0;
     *out_recompiled = 0;
     *out_relayout = 0;
-    if (dtype == SRHIP_F32) constant_map_check<float>(trees, grad != 0, new_consts, out_mismatch, out_recompiled, out_relayout);
-    else if (dtype == SRHIP_F64) constant_map_check<double>(trees, grad != 0, new_consts, out_mismatch, out_recompiled, out_relayout);
+    const bool g = (grad & 1) != 0, keep = (grad & 2) != 0;
+    if (dtype == SRHIP_F32) constant_map_check<float>(trees, g, keep, new_consts, out_mismatch, out_recompiled, out_relayout);
+    else if (dtype == SRHIP_F64) constant_map_check<double>(trees, g, keep, new_consts, out_mismatch, out_recompiled, out_relayout);
     else throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
     return SRHIP_OK;
   });

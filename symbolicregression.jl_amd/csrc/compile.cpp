@@ -18,6 +18,7 @@
 #include "compile.h"
 
 #include <algorithm>
+#include <limits>
 #include <exception>
 #include <thread>
 
@@ -79,7 +80,10 @@ struct TreeCompiler {
     if (x.deg == 0) return;
     if (!x.has_feature) {
       T v;
-      if (!eval_const(i, &v)) fold_fail = true;
+      if (!eval_const(i, &v)) {
+        fold_fail = true;
+        v = std::numeric_limits<T>::quiet_NaN();  // the tree fails statically; a defined immediate (keep_layout)
+      }
       const int first = i - x.size + 1;
       folds->push_back({nbase + first, nbase + i + 1, cbase + nd[first].cpre});
       x.deg = 0; x.feat = -1; x.val = (double)v; x.l = x.r = -1;

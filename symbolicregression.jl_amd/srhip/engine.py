@@ -326,16 +326,18 @@ def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bo
     return bytes(buf[: nb.value]), txt.value.decode(), {int(t): int(o) for t, o in pairs}
 
 
-def debug_constant_map(flat: FlatTrees, new_consts, dtype, grad: bool = False):
+def debug_constant_map(flat: FlatTrees, new_consts, dtype, grad: bool = False, keep_layout: bool = False):
     """srhip_debug_constant_map (no device): (trees that differ from a fresh
     compile after writing new_consts through the constant map, trees the
-    update recompiled, 1 if it needed a rebuild)."""
+    update recompiled, 1 if it needed a rebuild). keep_layout: the images of
+    a program whose constants change (failing trees keep their code)."""
     dt = np.dtype(dtype)
     consts = np.ascontiguousarray(flat.consts, dtype=dt)
     new = np.ascontiguousarray(new_consts, dtype=dt)
     tr = _trees_struct(flat, consts)
     mm, rc, rl = C.c_int64(), C.c_int64(), C.c_int32()
-    check(lib().srhip_debug_constant_map(C.byref(tr), dtype_code(dt), int(grad), _p(new), C.byref(mm), C.byref(rc),
+    check(lib().srhip_debug_constant_map(C.byref(tr), dtype_code(dt), int(grad) | (2 if keep_layout else 0), _p(new),
+                                         C.byref(mm), C.byref(rc),
                                          C.byref(rl)))
     return mm.value, rc.value, rl.value
 

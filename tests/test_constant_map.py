@@ -22,7 +22,11 @@ def _flat(n, T, seed):
     keep = []
     for t in trees:
         f = srhip.flatten([t], OPS, dtype=T)
-        if debug_constant_map(f, np.asarray(f.consts, dtype=T), T)[1] == 0:  # patched in place: it has code
+        # patched in place with no recompile when its constants move by an ulp:
+        # it has code (a failing tree is recompiled at every change; with the
+        # same constants it is skipped, so the same constants cannot tell)
+        nudged = np.nextafter(np.asarray(f.consts, dtype=T), T(np.inf))
+        if debug_constant_map(f, nudged, T)[1] == 0:
             keep.append(t)
     assert len(keep) > 0.8 * n
     return srhip.flatten(keep, OPS, dtype=T)
@@ -80,3 +84,32 @@ def test_non_finite_constants(T):
     # and back to finite values: the failing trees' kept code is patched again
     mismatch, recompiled, relayout = debug_constant_map(flat, c * T(0.9), T, False)
     assert relayout == 0 and mismatch == 0
+
+
+@pytest.mark.parametrize("T", [np.float32, np.float64])
+@pytest.mark.parametrize("grad", [False, True])
+def test_keep_layout_failing_trees_patch_back(T, grad):
+    """Programs whose constants change (the optimiser's, compile_batch
+    keep_layout): a tree that fails statically for its constants (a folded
+    overflow, a NaN constant) keeps its code, so constants that make it
+    finite again are patched in place — no rebuild — and every tree matches a
+    fresh compile; unchanged failing trees are not recompiled."""
+    trees = srhip.random_population(1500, OPS, 5, T, seed=23)
+    flat = srhip.flatten(trees, OPS, dtype=T)
+    c0 = np.asarray(flat.consts, dtype=T)
+    rng = np.random.default_rng(24)
+    bad = c0.copy()
+    bad[rng.choice(len(c0), len(c0) // 8, replace=False)] = T(1e30)
+    bad[rng.choice(len(c0), len(c0) // 20, replace=False)] = T(np.nan)
+    failing = srhip.node.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off, bad, flat.nodes)
+    # compiled with the failing constants, patched back to finite ones
+    mismatch, recompiled, relayout = debug_constant_map(failing, c0, T, grad, keep_layout=True)
+    assert relayout == 0 and mismatch == 0, (mismatch, relayout)
+    assert recompiled > 0
+    # and the other way
+    mismatch, _, relayout = debug_constant_map(flat, bad, T, grad, keep_layout=True)
+    assert relayout == 0 and mismatch == 0, (mismatch, relayout)
+    # the same failing constants again: nothing to recompile
+    assert debug_constant_map(failing, bad, T, grad, keep_layout=True)[:3] == (0, 0, 0)
+    # without keep_layout the first direction needs a rebuild (the failing trees have no code)
+    assert debug_constant_map(failing, c0, T, grad)[2] == 1
