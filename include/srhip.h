@@ -316,8 +316,9 @@ int32_t srhip_optimize_constants_batch(srhip_ctx* ctx, srhip_dataset* ds, const 
  * its time: out[0..8] = total, program builds, set_constants, loss calls,
  * gradient calls, the kernels inside those calls (HIP events) — seconds —
  * then the number of builds, loss calls, gradient calls and full program
- * rebuilds inside set_constants (the first n of these 10 written). The rest
- * of the total is the host optimiser's own algebra. */
+ * rebuilds inside set_constants, then the builds' tree-code generation and
+ * code-object load times (s) (the first n of these 12 written). The rest of
+ * the total is the host optimiser's own algebra. */
 int32_t srhip_constopt_profile(double* out, int32_t n);
 /* The same optimiser over any evaluator (row-sharded datasets whose partials
  * the caller all-reduces, custom losses on the CPU, tests): fn scores

@@ -9,6 +9,7 @@
 #include <algorithm>
 #include <atomic>
 #include <chrono>
+#include <limits>
 #include <condition_variable>
 #include <functional>
 #include <cstdio>
@@ -481,11 +482,42 @@ bool patch_image(srhip_program* p, std::vector<unsigned char>& code, const std::
   tr.const_off = co;
   tr.consts = c;
   std::vector<int32_t> redo;
+  const bool keep = p->jit_memc;  // compiled with keep_layout: every tree has its code
   const T* cp = cprev.size() == p->consts.size() ? reinterpret_cast<const T*>(cprev.data()) : nullptr;
   for (int t = 0; t < nt; ++t) {
     if (!direct[t] && cp && std::memcmp(cp + co[t], c + co[t], (size_t)(co[t + 1] - co[t]) * sizeof(T)) == 0)
       continue;  // compiled with these very constants: same code, same verdict
-    if (direct[t]) {
+    if (direct[t] && keep) {
+      // keep_layout: the code stays, the verdict follows from the patched
+      // immediates as compile_batch decides it — a folded subtree that is no
+      // longer finite fails the tree statically; else a non-finite constant
+      // operand does (fail_if_rows for a tree that is one constant)
+      bool fold_bad = false, const_bad = false, unsure = false;
+      for (int i = toff[t], e = toff[t] + len[t]; i < e; ++i) {
+        const int32_t m = cmap[i];
+        if (m >= 0) {
+          ins[i].imm = c[m];
+          const_bad |= !std::isfinite(c[m]);
+        } else if (m <= -2) {
+          const FoldRec& f = folds[-2 - m];
+          if (!eval_fold<T>(f, tr, &ins[i].imm)) {
+            ins[i].imm = std::numeric_limits<T>::quiet_NaN();
+            if (f.node_e - f.node_b >= kMaxFoldDepth) unsure = true;  // eval_fold's stack, not the value
+            else fold_bad = true;
+          }
+        }
+      }
+      if (!unsure) {
+        const int nb = p->node_off[t], ne = p->node_off[t + 1];
+        const bool one_const = ne - nb == 1 && p->kind[nb] == SRHIP_NODE_CONST;
+        const uint8_t nsf = (uint8_t)(grad ? const_bad : (fold_bad || (const_bad && !one_const)));
+        const uint8_t nfir = (uint8_t)(!grad && !fold_bad && const_bad && one_const);
+        if (sfail[t] != nsf || (fir && (*fir)[t] != nfir)) *verdicts_changed = true;
+        sfail[t] = nsf;
+        if (fir) (*fir)[t] = nfir;
+        continue;
+      }
+    } else if (direct[t]) {
       bool finite = true;
       for (int k = co[t]; k < co[t + 1]; ++k) finite &= std::isfinite(c[k]);
       for (int i = toff[t], e = toff[t] + len[t]; i < e && finite; ++i) {
@@ -2659,6 +2691,7 @@ void write_result(const copt::Result& r, int dtype, void* out_consts, double* ou
 struct CoptProfile {
   double total = 0, create = 0, set = 0, loss = 0, grad = 0, kernel_ms = 0;
   int64_t ncreate = 0, nloss = 0, ngrad = 0, nrebuilt = 0;
+  double jit_codegen_ms = 0, jit_load_ms = 0;  // of the builds (tree code)
 };
 thread_local CoptProfile t_copt;
 double secs_since(std::chrono::steady_clock::time_point t0) {
@@ -2706,6 +2739,15 @@ struct EngineSet : copt::Set {
     check_rc(srhip_program_create_ex(ctx, dtype, &tr, SRHIP_PROGRAM_VARYING_CONSTANTS, &prog));
     t_copt.create += secs_since(t0);
     t_copt.ncreate += 1;
+    {
+      int32_t nt = 0, nf = 0;
+      int64_t nb = 0;
+      double mc = 0, ml = 0;
+      if (srhip_program_jit_info(prog, &nt, &nf, &nb, &mc, &ml) == SRHIP_OK) {
+        t_copt.jit_codegen_ms += mc;
+        t_copt.jit_load_ms += ml;
+      }
+    }
   }
   ~EngineSet() override {
     int64_t inplace = 0, rebuilt = 0;
@@ -2824,9 +2866,10 @@ int32_t srhip_constopt_profile(double* out, int32_t n) {
   return guarded([&] {
     if (!out || n < 0) throw Error(SRHIP_ERR_INVALID, "null output");
     const CoptProfile& q = t_copt;
-    const double v[10] = {q.total, q.create, q.set, q.loss, q.grad, q.kernel_ms * 1e-3,
-                          (double)q.ncreate, (double)q.nloss, (double)q.ngrad, (double)q.nrebuilt};
-    for (int32_t i = 0; i < n && i < 10; ++i) out[i] = v[i];
+    const double v[12] = {q.total, q.create, q.set, q.loss, q.grad, q.kernel_ms * 1e-3,
+                          (double)q.ncreate, (double)q.nloss, (double)q.ngrad, (double)q.nrebuilt,
+                          q.jit_codegen_ms * 1e-3, q.jit_load_ms * 1e-3};
+    for (int32_t i = 0; i < n && i < 12; ++i) out[i] = v[i];
     return SRHIP_OK;
   });
 }

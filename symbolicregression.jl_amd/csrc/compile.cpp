@@ -30,7 +30,6 @@
 namespace srhip {
 namespace {
 
-constexpr int kMaxFoldDepth = 64;  // operand stack of eval_fold (deeper folds recompile)
 
 struct HNode {
   int deg;       // 0, 1, 2
@@ -310,7 +309,7 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad, bool keep_la
       tc.emit(root, 0);
       tc.put(OP_END, 0, 0, T(0));
       cb.len[t] = (int32_t)cb.code.size() - cb.tree_off[t];
-      cb.direct[t] = !cb.static_fail[t];  // a failing tree is recompiled at the next set (its verdict)
+      cb.direct[t] = 1;
       continue;
     }
     const bool root_is_leaf = tc.nd[root].deg == 0;
@@ -339,9 +338,9 @@ CompiledBatch<T> compile_batch(const srhip_trees& trees, bool grad, bool keep_la
     tc.emit(root, 0);
     tc.put(OP_END, 0, 0, T(0));
     cb.len[t] = (int32_t)cb.code.size() - cb.tree_off[t];
-    // folded values are in the map too (folds); a tree kept by keep_layout
-    // despite its verdict is recompiled at the next set, which decides it anew
-    cb.direct[t] = !(cb.static_fail[t] || cb.fail_if_rows[t]);
+    // folded values are in the map too (folds); set_constants decides the
+    // verdict of a keep_layout tree from its patched immediates
+    cb.direct[t] = 1;
   }
   cb.max_feature = tc.max_feat;
   // trailing OP_ENDs: the kernels prefetch one instruction past each END and

@@ -15,6 +15,9 @@ struct Error : std::runtime_error {
 };
 
 // a folded feature-free subtree (CompiledBatch::folds)
+// operand stack of eval_fold: a deeper fold is recompiled instead
+constexpr int kMaxFoldDepth = 64;
+
 struct FoldRec {
   int32_t node_b, node_e;  // postfix nodes [node_b, node_e) of the batch
   int32_t const_b;         // batch-wide index of its first constant

@@ -173,10 +173,10 @@ def _consts_of(tree: Node):
 def last_profile() -> dict:
     """Where the last optimize_constants_batch call of this thread spent its
     time (srhip_constopt_profile): seconds and call counts."""
-    out = (C.c_double * 10)()
-    check(lib().srhip_constopt_profile(out, 10))
+    out = (C.c_double * 12)()
+    check(lib().srhip_constopt_profile(out, 12))
     keys = ("total_s", "create_s", "set_constants_s", "loss_s", "grad_s", "kernel_s", "n_create", "n_loss", "n_grad",
-            "n_rebuilt")
+            "n_rebuilt", "jit_codegen_s", "jit_load_s")
     d = dict(zip(keys, (float(v) for v in out)))
     d["host_s"] = d["total_s"] - d["create_s"] - d["set_constants_s"] - d["loss_s"] - d["grad_s"]
     return d

@@ -92,8 +92,9 @@ def test_keep_layout_failing_trees_patch_back(T, grad):
     """Programs whose constants change (the optimiser's, compile_batch
     keep_layout): a tree that fails statically for its constants (a folded
     overflow, a NaN constant) keeps its code, so constants that make it
-    finite again are patched in place — no rebuild — and every tree matches a
-    fresh compile; unchanged failing trees are not recompiled."""
+    finite again are patched in place — no rebuild, no recompile: the verdict
+    follows from the patched immediates — and every tree matches a fresh
+    compile (instruction stream and verdict)."""
     trees = srhip.random_population(1500, OPS, 5, T, seed=23)
     flat = srhip.flatten(trees, OPS, dtype=T)
     c0 = np.asarray(flat.consts, dtype=T)
@@ -105,7 +106,7 @@ def test_keep_layout_failing_trees_patch_back(T, grad):
     # compiled with the failing constants, patched back to finite ones
     mismatch, recompiled, relayout = debug_constant_map(failing, c0, T, grad, keep_layout=True)
     assert relayout == 0 and mismatch == 0, (mismatch, relayout)
-    assert recompiled > 0
+    assert recompiled == 0  # verdicts decided from the patched immediates, no compile
     # and the other way
     mismatch, _, relayout = debug_constant_map(flat, bad, T, grad, keep_layout=True)
     assert relayout == 0 and mismatch == 0, (mismatch, relayout)
@@ -113,3 +114,23 @@ def test_keep_layout_failing_trees_patch_back(T, grad):
     assert debug_constant_map(failing, bad, T, grad, keep_layout=True)[:3] == (0, 0, 0)
     # without keep_layout the first direction needs a rebuild (the failing trees have no code)
     assert debug_constant_map(failing, c0, T, grad)[2] == 1
+
+
+@pytest.mark.parametrize("grad", [False, True])
+def test_keep_layout_verdicts_with_nan_absorbing_operators(grad):
+    """max / min fold a NaN operand away (fmax): a NaN constant inside a folded
+    subtree need not fail the tree, one in an operand does — the in-place
+    verdicts match a fresh compile's either way."""
+    ops = srhip.Options(binary_operators=["+", "*", "max", "min"], unary_operators=["exp", "cos"])
+    T = np.float32
+    trees = srhip.random_population(1200, ops, 4, T, seed=25)
+    flat = srhip.flatten(trees, ops, dtype=T)
+    c0 = np.asarray(flat.consts, dtype=T)
+    rng = np.random.default_rng(26)
+    bad = c0.copy()
+    bad[rng.choice(len(c0), len(c0) // 6, replace=False)] = T(np.nan)
+    bad[rng.choice(len(c0), len(c0) // 10, replace=False)] = T(1e30)
+    failing = srhip.node.FlatTrees(flat.node_off, flat.kind, flat.arg, flat.const_off, bad, flat.nodes)
+    for src, new in ((failing, c0), (flat, bad)):
+        mismatch, recompiled, relayout = debug_constant_map(src, new, T, grad, keep_layout=True)
+        assert (mismatch, relayout) == (0, 0)
