@@ -416,11 +416,28 @@ __device__ __forceinline__ T uop(T x) {
 // from Float64 literals), so Julia promotes a Float32 residual to Float64 and
 // evaluates them in Float64: so do these, with the parameter as given (never
 // rounded to T), and the value rounded to T once.
+// |r|^p of LPDistLoss for a Float32 residual (p its Float64 field): exp(p ln|r|)
+// in Float64, relative error within ~2^-44 for |p ln|r|| < 700 — far inside
+// the one rounding of the loss to Float32, which it changes only for values
+// within that distance of a Float32 rounding boundary — with pow's values at
+// |r| = 0 and 1. The Float32 tree code's loss routine fits its registers
+// (gen_jit.py; the general pow does not); Float64 data keep pow.
+__device__ __forceinline__ double lp_pow(double ar, double p) {
+  if (ar == 1.0) return 1.0;
+  if (ar == 0.0) return p > 0.0 ? 0.0 : (p == 0.0 ? 1.0 : __builtin_inf());
+  return m_exp(p * m_log(ar));
+}
+template <typename T>
+__device__ __forceinline__ double lp_pow_t(double ar, double p) {
+  if constexpr (std::is_same<T, float>::value) return lp_pow(ar, p);
+  else return m_pow(ar, p);
+}
+
 template <typename T>
 __device__ __forceinline__ double elem_loss_param(int kind, double p, double r) {
   const double ar = __builtin_fabs(r);
   switch (kind) {
-    case SRHIP_LOSS_LP: return m_pow(ar, p);
+    case SRHIP_LOSS_LP: return lp_pow_t<T>(ar, p);
     case SRHIP_LOSS_HUBER: return ar <= p ? 0.5 * r * r : p * (ar - 0.5 * p);
     case SRHIP_LOSS_L1EPSINS: return ar > p ? ar - p : 0.0;
     case SRHIP_LOSS_L2EPSINS: { double e = ar > p ? ar - p : 0.0; return e * e; }
@@ -520,7 +537,7 @@ __device__ __forceinline__ T elem_dloss(int kind, double p, T yhat, T y) {
   }
   const double rd = (double)r, ar = __builtin_fabs(rd), sd = (double)sg;
   switch (kind) {
-    case SRHIP_LOSS_LP: return (T)(p * m_pow(ar, p - 1.0) * sd);
+    case SRHIP_LOSS_LP: return (T)(p * lp_pow_t<T>(ar, p - 1.0) * sd);
     case SRHIP_LOSS_HUBER: return (T)(ar <= p ? rd : p * sd);
     case SRHIP_LOSS_L1EPSINS: return (T)(ar > p ? sd : 0.0);
     case SRHIP_LOSS_L2EPSINS: return (T)(ar > p ? 2.0 * (ar - p) * sd : 0.0);

@@ -7,10 +7,11 @@ of Float32 tree code, weighted and unweighted.
 The parametric losses hold Float64 fields, so Julia evaluates them in
 Float64 for a Float32 residual (device_ops.h elem_loss, the oracle likewise):
 PeriodicLoss's cos(2πr/c) of a large residual made the Float32 evaluation
-0.6 % off before (round 4). L1, Huber, the epsilon-insensitive losses and
-Quantile run as tree code; LP (Float64 pow), Periodic (Float64 cos), LogCosh
-and LogitDist keep the interpreter (their loss routines' registers exceed
-what tree code leaves them), which this checks too.
+0.6 % off before (round 4). L1, LP (exp(p ln|r|) in Float64, device_ops.h
+lp_pow), Huber, the epsilon-insensitive losses, Quantile, LogCosh and
+LogitDist run as tree code; Periodic (Float64 cos of an unbounded argument)
+keeps the interpreter (its routine's registers exceed what tree code leaves
+it), which this checks too.
 
 Per loss: the tree code ran or not (srhip_last_tree_code), did_succeed equals
 the interpreter's and the oracle's on every tree, and losses agree with the
@@ -28,7 +29,7 @@ from srhip import constants as K
 pytestmark = pytest.mark.gpu
 
 LOSSES = [
-    (srhip.L1DistLoss(), True), (srhip.LPDistLoss(1.7), False), (srhip.LPDistLoss(3.0), False),
+    (srhip.L1DistLoss(), True), (srhip.LPDistLoss(1.7), True), (srhip.LPDistLoss(3.0), True),
     (srhip.HuberLoss(0.8), True), (srhip.L1EpsilonInsLoss(0.3), True), (srhip.L2EpsilonInsLoss(0.3), True),
     (srhip.QuantileLoss(0.3), True), (srhip.PeriodicLoss(2.0), False),
     (srhip.LogCoshLoss(), True), (srhip.LogitDistLoss(), True),
@@ -99,12 +100,16 @@ def _dloss(loss, r):
         return np.tanh(r)
     if kind == K.LOSS["LOGITDIST"]:  # tanh(r / 2)
         return np.tanh(0.5 * r)
+    if kind == K.LOSS["LP"]:  # P |r|^(P-1) sign(r)
+        with np.errstate(all="ignore"):
+            return p * ar ** (p - 1.0) * sg
     assert kind == K.LOSS["QUANTILE"]
     return np.where(r >= 0, p, p - 1.0)
 
 
 GRAD_LOSSES = [srhip.L1DistLoss(), srhip.HuberLoss(0.8), srhip.L1EpsilonInsLoss(0.3), srhip.L2EpsilonInsLoss(0.3),
-               srhip.QuantileLoss(0.3), srhip.LogCoshLoss(), srhip.LogitDistLoss()]
+               srhip.QuantileLoss(0.3), srhip.LogCoshLoss(), srhip.LogitDistLoss(), srhip.LPDistLoss(1.7),
+               srhip.LPDistLoss(3.0)]
 
 
 @pytest.mark.parametrize("loss", GRAD_LOSSES, ids=[f"{l.kind}-{l.params}" for l in GRAD_LOSSES])
