@@ -90,10 +90,15 @@ run_n2() {
   tail -c 300 gpurun_out/bench_n2_rows.json gpurun_out/bench_n2_trees.json
 }
 run_variants() {
-  SRHIP_JIT_DYNLOOP=0 SRHIP_INTERP_DYN=0 timeout -k 10 600 $PYTEST tests -m gpu -q > gpurun_out/pytest_static.log 2>&1
+  [ -n "$JITALL_ONLY" ] && { run_jitall; return; }
+  SRHIP_JIT_DYNLOOP=0 SRHIP_INTERP_DYN=0 timeout -k 10 600 $PYTEST tests -m gpu > gpurun_out/pytest_static.log 2>&1
   local rc=$?; echo "static loops rc=$rc"; tail -2 gpurun_out/pytest_static.log
   [ $rc -le 1 ] || exit $rc
-  SRHIP_JIT=1 timeout -k 10 600 $PYTEST tests -m gpu -q > gpurun_out/pytest_jitall.log 2>&1
+  # (the search tests run thousands of small programs: as tree code each one costs a code-object load)
+  run_jitall
+}
+run_jitall() {
+  SRHIP_JIT=1 timeout -k 10 600 $PYTEST tests -m gpu -k "not evolution and not search" > gpurun_out/pytest_jitall.log 2>&1
   rc=$?; echo "SRHIP_JIT=1 rc=$rc"; tail -2 gpurun_out/pytest_jitall.log
   [ $rc -le 1 ] || exit $rc
 }
