@@ -62,24 +62,26 @@ __device__ __forceinline__ float fast_exp_f32(float x) {
 #define SR_PRECISE_TRANSC 1
 #endif
 // e^x = 2^n e^r, n = rint(x log2 e), r = x - n ln2 (two-part ln2, exact
-// products for |n| <= 151), e^r by its Taylor series to r^11 (|r| <= 0.347:
-// truncation < 2^-47 relative), one v_ldexp_f64, one rounding to Float32.
+// products for |n| <= 151), e^r by a degree-10 minimax polynomial (|r| <=
+// 0.347: relative error 2^-51.6; the Taylor series to r^11 of rounds 1-4 had
+// 2^-47 with one more FMA), one v_ldexp_f64, one rounding to Float32. Every
+// float of [-104, 89] rounds as the oracle's (float)exp((double)x) does
+// (tools/check_precise.c: 0 differ; the Taylor form 2).
 __device__ __forceinline__ float precise_exp_f32(float x) {
   x = __builtin_amdgcn_fmed3f(x, -104.0f, 89.0f);
   const double xd = (double)x;
   const double n = __builtin_rint(xd * 1.4426950408889634);
   double r = __builtin_fma(n, -6.93147180369123816490e-01, xd);
   r = __builtin_fma(n, -1.90821492927058770002e-10, r);
-  double p = 2.50521083854417187751e-08;        // 1/11!
-  p = __builtin_fma(p, r, 2.75573192239858906526e-07);  // 1/10!
-  p = __builtin_fma(p, r, 2.75573192239858906526e-06);  // 1/9!
-  p = __builtin_fma(p, r, 2.48015873015873015873e-05);  // 1/8!
-  p = __builtin_fma(p, r, 1.98412698412698412698e-04);  // 1/7!
-  p = __builtin_fma(p, r, 1.38888888888888888889e-03);  // 1/6!
-  p = __builtin_fma(p, r, 8.33333333333333333333e-03);  // 1/5!
-  p = __builtin_fma(p, r, 4.16666666666666666667e-02);  // 1/4!
-  p = __builtin_fma(p, r, 1.66666666666666666667e-01);  // 1/3!
-  p = __builtin_fma(p, r, 0.5);
+  double p = 2.74715993357489975e-07;
+  p = __builtin_fma(p, r, 2.76351209779822652e-06);
+  p = __builtin_fma(p, r, 2.48019464013407408e-05);
+  p = __builtin_fma(p, r, 1.98411849339436464e-04);
+  p = __builtin_fma(p, r, 1.38888885022706824e-03);
+  p = __builtin_fma(p, r, 8.33333337108620349e-03);
+  p = __builtin_fma(p, r, 4.16666666681865250e-02);
+  p = __builtin_fma(p, r, 1.66666666666110797e-01);
+  p = __builtin_fma(p, r, 4.99999999999982736e-01);
   p = __builtin_fma(p, r, 1.0);
   p = __builtin_fma(p, r, 1.0);
   return (float)__builtin_amdgcn_ldexp(p, (int)n);
@@ -147,22 +149,25 @@ __device__ __forceinline__ float fast_sincos_f32(float x, int want_cos, float& n
 #if SR_PRECISE_TRANSC
   // Same reduction in Float64: r = x - m pi/2 (pi/2 = HI + LO, HI with 33
   // significant bits so m*HI is exact for |m| < 2^20; |r| <= pi/2 + tiny),
-  // sin r by its Taylor series to r^17 (truncation < 2^-44 at pi/2), one
-  // rounding to Float32, then the sign of n's parity.
+  // sin r = r + r^3 P(r^2) with P a 7-term minimax fit (relative error
+  // 2^-50.4 on |r| <= pi/2; the Taylor series to r^17 of rounds 1-4 had one
+  // more FMA and 2^-44), one rounding to Float32, then the sign of n's
+  // parity. Over every float with |x| <= 105615, sin rounds as the oracle's
+  // (float)sin((double)x) on all but 2, cos on all (tools/check_precise.c;
+  // the Taylor form: sin 0, cos 114).
   {
     const double md = (double)m;
     double r = __builtin_fma(md, -1.57079632673412561417e+00, (double)x);
     r = __builtin_fma(md, -6.07710050650619224932e-11, r);
     const double s2 = r * r;
-    double p = -2.81145725434552076320e-15;          // -1/17!
-    p = __builtin_fma(p, s2, 7.64716373181981647590e-13);   // 1/15!
-    p = __builtin_fma(p, s2, -1.60590438368216145994e-10);  // -1/13!
-    p = __builtin_fma(p, s2, 2.50521083854417187751e-08);   // 1/11!
-    p = __builtin_fma(p, s2, -2.75573192239858906526e-06);  // -1/9!
-    p = __builtin_fma(p, s2, 1.98412698412698412698e-04);   // 1/7!
-    p = __builtin_fma(p, s2, -8.33333333333333333333e-03);  // -1/5!
-    p = __builtin_fma(p, s2, 1.66666666666666666667e-01);   // 1/3!: sin r = r - r^3 p
-    const double v = __builtin_fma(-p * s2, r, r);
+    double p = -7.34673622570819757e-13;
+    p = __builtin_fma(p, s2, 1.60458129180763398e-10);
+    p = __builtin_fma(p, s2, -2.50518043886916424e-08);
+    p = __builtin_fma(p, s2, 2.75573153848002669e-06);
+    p = __builtin_fma(p, s2, -1.98412698157051834e-04);
+    p = __builtin_fma(p, s2, 8.33333333325722396e-03);
+    p = __builtin_fma(p, s2, -1.66666666666660662e-01);  // sin r = r + r^3 p
+    const double v = __builtin_fma(p * s2, r, r);
     const float f = (float)(want_cos ? -v : v);
     return __int_as_float(__float_as_int(f) ^ ((int)n << 31));
   }
