@@ -92,11 +92,31 @@ static float exp_new(float x) {
   return (float)ldexp(p, (int)n);
 }
 
+
+static float exp_d9(float x) {
+  x = fminf(fmaxf(x, -104.0f), 89.0f);
+  const double xd = (double)x;
+  const double n = rint(xd * 1.4426950408889634);
+  double r = fma(n, -6.93147180369123816490e-01, xd);
+  r = fma(n, -1.90821492927058770002e-10, r);
+  double p = 2.74930749914601988e-06;
+  p = fma(p, r, 2.48808415869387003e-05);
+  p = fma(p, r, 1.98415392254195396e-04);
+  p = fma(p, r, 1.38888110820991131e-03);
+  p = fma(p, r, 8.33333309485798264e-03);
+  p = fma(p, r, 4.16666669626017602e-02);
+  p = fma(p, r, 1.66666666672660641e-01);
+  p = fma(p, r, 4.99999999996637579e-01);
+  p = fma(p, r, 1.0);
+  p = fma(p, r, 1.0);
+  return (float)ldexp(p, (int)n);
+}
+
 int main(void) {
-  long long bad[6] = {0};
+  long long bad[7] = {0};
   long long total[3] = {0};
   // every float bit pattern; domains filtered
-#pragma omp parallel for reduction(+ : bad[:6], total[:3]) schedule(dynamic, 1 << 16)
+#pragma omp parallel for reduction(+ : bad[:7], total[:3]) schedule(dynamic, 1 << 16)
   for (long long u = 0; u < (1LL << 32); ++u) {
     const float x = as_f((uint32_t)u);
     if (!isfinite(x)) continue;
@@ -114,10 +134,11 @@ int main(void) {
       total[2] += 1;
       bad[4] += as_u(exp_old(x)) != as_u(re);
       bad[5] += as_u(exp_new(x)) != as_u(re);
+      bad[6] += as_u(exp_d9(x)) != as_u(re);
     }
   }
   printf("sin: %lld floats, old %lld differ, new %lld differ\n", total[0], bad[0], bad[1]);
   printf("cos: %lld floats, old %lld differ, new %lld differ\n", total[1], bad[2], bad[3]);
-  printf("exp: %lld floats, old %lld differ, new %lld differ\n", total[2], bad[4], bad[5]);
+  printf("exp: %lld floats, old %lld differ, new %lld differ, degree 9: %lld\n", total[2], bad[4], bad[5], bad[6]);
   return 0;
 }
