@@ -188,6 +188,13 @@ void run_gradient(const Problem& pb, const std::vector<int>& sel, const Options&
   std::vector<uint8_t> searching(nc), first(nc), moved(nc), upd(nc);
   std::vector<int> finite_left(nc), ls_iter(nc);
   std::vector<double> sd, gv, Hdg;
+  // Newton's central differences need ∂L/∂c of the one-constant candidates
+  // only: when they are a minority, a set of just them (built once, at the
+  // first Newton step, with every one-constant candidate) takes those two
+  // gradient calls per iteration instead of the whole set
+  std::unique_ptr<Set> nev;
+  std::vector<int> newton_ks;
+  std::vector<double> nx_p, nx_m, nf, nGp, nGm;
   for (int it = 0; it < opt.iterations; ++it) {
     if (!any(active)) break;
     // search directions
@@ -203,8 +210,37 @@ void run_gradient(const Problem& pb, const std::vector<int>& sel, const Options&
         Xm[c.off[k]] -= step[k];
       }
       for (int64_t j = 0; j < nx; ++j) { Xp[j] = num.rt(Xp[j]); Xm[j] = num.rt(Xm[j]); }
-      ev->eval(Xp, true, fdum, Gp);
-      ev->eval(Xm, true, fdum, Gm);
+      if (!nev && fac.has_subset()) {
+        std::vector<int32_t> mem;
+        for (int k = 0; k < nc; ++k)
+          if (c.size(k) == 1) newton_ks.push_back(k);
+        if ((int64_t)newton_ks.size() * 2 < nc) {
+          for (int k : newton_ks) mem.push_back(c.tree[k]);
+          nev = fac.make(mem);
+        } else {
+          newton_ks.clear();
+        }
+      }
+      if (nev) {
+        const size_t nn = newton_ks.size();
+        nx_p.resize(nn);
+        nx_m.resize(nn);
+        for (size_t q = 0; q < nn; ++q) {
+          nx_p[q] = Xp[c.off[newton_ks[q]]];
+          nx_m[q] = Xm[c.off[newton_ks[q]]];
+        }
+        nev->eval(nx_p, true, nf, nGp);
+        nev->eval(nx_m, true, nf, nGm);
+        Gp.assign(nx, 0.0);
+        Gm.assign(nx, 0.0);
+        for (size_t q = 0; q < nn; ++q) {
+          Gp[c.off[newton_ks[q]]] = nGp[q];
+          Gm[c.off[newton_ks[q]]] = nGm[q];
+        }
+      } else {
+        ev->eval(Xp, true, fdum, Gp);
+        ev->eval(Xm, true, fdum, Gm);
+      }
       for (int k = 0; k < nc; ++k) {
         if (!(c.size(k) == 1 && active[k])) continue;
         const int64_t s0 = c.off[k];
