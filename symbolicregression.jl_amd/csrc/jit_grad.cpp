@@ -81,9 +81,9 @@ struct GOp {
 
 constexpr uint32_t kGradUops = (1u << SRHIP_UOP_NEG) | (1u << SRHIP_UOP_ABS) | (1u << SRHIP_UOP_SQUARE) |
                                (1u << SRHIP_UOP_CUBE) | (1u << SRHIP_UOP_EXP) | (1u << SRHIP_UOP_SIN) |
-                               (1u << SRHIP_UOP_COS);
+                               (1u << SRHIP_UOP_COS) | (1u << SRHIP_UOP_LOG) | (1u << SRHIP_UOP_SQRT);
 constexpr uint32_t kGradBops = (1u << SRHIP_BOP_ADD) | (1u << SRHIP_BOP_SUB) | (1u << SRHIP_BOP_MUL) |
-                               (1u << SRHIP_BOP_DIV);
+                               (1u << SRHIP_BOP_DIV) | (1u << SRHIP_BOP_POW);
 
 bool g_inline(const GOp& o) {
   if (o.kind == K_MAT) return true;
@@ -321,9 +321,13 @@ struct GradGen {
         } else if (o.op == SRHIP_BOP_DIV) {
           use(o.b);
           if (ab) last[i] = std::max(last[i], bstep(i));  // the quotient
+        } else if (o.op == SRHIP_BOP_POW) {  // a, b, and for ∂b the power itself
+          use(o.a);
+          use(o.b);
+          if (ab) last[i] = std::max(last[i], bstep(i));
         }
       } else {
-        if (o.op == SRHIP_UOP_EXP) last[i] = std::max(last[i], bstep(i));
+        if (o.op == SRHIP_UOP_EXP || o.op == SRHIP_UOP_SQRT) last[i] = std::max(last[i], bstep(i));
         else if (o.op != SRHIP_UOP_NEG) use(o.a);
       }
     }
@@ -710,6 +714,51 @@ struct GradGen {
           }
           break;
         }
+        case SRHIP_BOP_POW: {
+          // f = safe_pow(a, b): ∂a = g·b·safe_pow(a, b - 1), ∂b = g·f·log(a)
+          // where a > 0, else 0 (device_ops.h bop_d), pow and log by routine
+          if (aa) {
+            fetch(o.a, XS0);
+            fetch(o.b, XS1);
+            for (int e = 0; e < R; ++e) {
+              as.vop1(VOP1_MOV, "v_mov_b32_e32", VA + e, rsrc(o.a, XS0, e));
+              as.vop1(VOP1_MOV, "v_mov_b32_e32", VB + e, rsrc(o.b, XS1, e));
+              as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VB + e, K(0xbf800000u), VB + e);  // b - 1
+            }
+            routine(kBopRoutine[SRHIP_BOP_POW], false);
+            fetch(o.b, XS1);  // the call reused the scratch registers
+            int blk;
+            const int d = dest(o.a, TP, &blk);
+            if (d < 0) return false;
+            for (int e = 0; e < R; ++e) {
+              vmul(d + e, rsrc(o.b, XS1, e), V(VA + e));
+              as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
+            }
+            give(o.a, d, g.neg, blk);
+          }
+          if (ab) {
+            fetch(o.a, XS0);
+            for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", VA + e, rsrc(o.a, XS0, e));
+            routine(kUopRoutine[SRHIP_UOP_LOG], false);
+            fetch(o.a, XS0);
+            int blk;
+            const int d = dest(o.b, TP, &blk);
+            if (d < 0) return false;
+            const int fr = blk_reg(loc[i]);
+            for (int e = 0; e < R; ++e) {
+              as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, V(fr + e), VA + e);
+              as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
+              // 0 where !(a > 0): v_cmp_lt_f32 vcc = 0 < a (VOPC src1 must be a VGPR)
+              if (o.a.k == G_C) as.vop1(VOP1_MOV, "v_mov_b32_e32", TR + e, rsrc(o.a, XS0, e));
+              const int areg = o.a.k == G_C ? TR + e : rsrc(o.a, XS0, e).enc - 256;
+              as.vopc(VOPC_LT_F32, "v_cmp_lt_f32_e32", K(0), areg);
+              as.sopp(0x00, "s_nop", 1);
+              as.vop2(VOP2_CNDMASK, "v_cndmask_b32_e32", d + e, K(0), d + e, ", vcc");
+            }
+            give(o.b, d, g.neg, blk);
+          }
+          break;
+        }
         default: {  // DIV: q = a / b; ∂a = g / b, ∂b = -(g / b) q
           fetch(o.b, XS1);
           for (int e = 0; e < R; ++e) as.vop1(VOP1_RCP_F32, "v_rcp_f32_e32", TR + e, rsrc(o.b, XS1, e));
@@ -759,6 +808,29 @@ struct GradGen {
               as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, K(0x40400000u), ar + e);  // 3x
               as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, V(d + e), ar + e);        // (3x)x
             }
+            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
+          }
+          give(o.a, d, g.neg, blk);
+          break;
+        }
+        case SRHIP_UOP_LOG: {  // g / a (v_rcp_f32, as DIV's 1/b)
+          const int d = dest(o.a, TP, &blk);
+          if (d < 0) return false;
+          const int ar = blk_reg(loc[o.a.v]);
+          for (int e = 0; e < R; ++e) {
+            as.vop1(VOP1_RCP_F32, "v_rcp_f32_e32", d + e, V(ar + e));
+            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
+          }
+          give(o.a, d, g.neg, blk);
+          break;
+        }
+        case SRHIP_UOP_SQRT: {  // g · 0.5 / sqrt(a), from the forward value
+          const int d = dest(o.a, TP, &blk);
+          if (d < 0) return false;
+          const int fr = blk_reg(loc[i]);
+          for (int e = 0; e < R; ++e) {
+            as.vop1(VOP1_RCP_F32, "v_rcp_f32_e32", d + e, V(fr + e));
+            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, K(0x3f000000u), d + e);
             as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
           }
           give(o.a, d, g.neg, blk);

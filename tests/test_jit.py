@@ -90,6 +90,7 @@ def test_memory_constant_code_loads_every_constant():
 GRAD_OPSETS = [
     (["+", "-", "*", "/"], ["cos", "exp"]),  # config #5
     (["+", "-", "*", "/"], ["sin", "cos", "exp", "neg", "square", "cube", "abs"]),
+    (["+", "-", "*", "/", "^"], ["safe_log", "safe_sqrt", "cos", "exp"]),  # config #3's operators
 ]
 
 

@@ -28,6 +28,9 @@ pytestmark = pytest.mark.gpu
 OPSETS = {
     "cfg5": (["+", "-", "*", "/"], ["cos", "exp"]),
     "wide": (["+", "-", "*", "/"], ["sin", "cos", "exp", "neg", "square", "cube", "abs"]),
+    # config #3's operators (round 5: safe_log, safe_sqrt and ^ in the
+    # gradient tree code), on positive features so that most trees succeed
+    "cfg3": (["+", "-", "*", "/", "^"], ["safe_log", "safe_sqrt", "cos", "exp"]),
 }
 
 
@@ -156,9 +159,11 @@ def test_grad_tree_code_matches_interpreter_and_oracle(gpu_ctx, opset, weighted)
     rng = np.random.default_rng(5 + weighted)
     n = 3001  # a partial last tile
     X = rng.standard_normal((5, n)).astype(np.float32)
+    if opset == "cfg3":
+        X = (np.abs(X) + np.float32(0.1)).astype(np.float32)
     y = (2 * np.cos(X[3]) + X[0] ** 2 - 2).astype(np.float32)
     w = np.abs(rng.standard_normal(n)).astype(np.float32) if weighted else None
-    trees = srhip.random_population(600, o, 5, np.float32, seed=91 + weighted)
+    trees = srhip.random_population(600 if opset != "cfg3" else 1500, o, 5, np.float32, seed=91 + weighted)
     s1, g1, w1, ok1, info, prog = run(trees, o, X, y, w, True)
     s0, g0, w0, ok0, info0, _ = run(trees, o, X, y, w, False)
     assert info["ntrees"] >= 0.95 * len(trees), info
