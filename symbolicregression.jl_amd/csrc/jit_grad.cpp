@@ -817,10 +817,10 @@ struct GradGen {
           const int d = dest(o.a, TP, &blk);
           if (d < 0) return false;
           const int ar = blk_reg(loc[o.a.v]);
-          for (int e = 0; e < R; ++e) {
-            as.vop1(VOP1_RCP_F32, "v_rcp_f32_e32", d + e, V(ar + e));
-            as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
-          }
+          // the four reciprocals first: a VALU read of a transcendental's
+          // result right after it needs a wait state on gfx950 (as DIV)
+          for (int e = 0; e < R; ++e) as.vop1(VOP1_RCP_F32, "v_rcp_f32_e32", d + e, V(ar + e));
+          for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
           give(o.a, d, g.neg, blk);
           break;
         }
@@ -828,8 +828,8 @@ struct GradGen {
           const int d = dest(o.a, TP, &blk);
           if (d < 0) return false;
           const int fr = blk_reg(loc[i]);
+          for (int e = 0; e < R; ++e) as.vop1(VOP1_RCP_F32, "v_rcp_f32_e32", d + e, V(fr + e));  // as LOG
           for (int e = 0; e < R; ++e) {
-            as.vop1(VOP1_RCP_F32, "v_rcp_f32_e32", d + e, V(fr + e));
             as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, K(0x3f000000u), d + e);
             as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), d + e);
           }

@@ -113,6 +113,51 @@ def test_gradient_machine_code_equals_llvm_mc(k):
         raise AssertionError(f"word {i}: jit {a[i]:#010x} vs llvm-mc {r[i]:#010x}")
 
 
+TRANS = ("v_rcp_f32", "v_exp_f32", "v_log_f32", "v_sqrt_f32", "v_rsq_f32", "v_sin_f32", "v_cos_f32")
+
+
+def trans_forwarding_hazards(text: str):
+    """Instructions that read a transcendental's destination VGPR right
+    after it: gfx950 needs one wait state in between (a read without it sees
+    the register's old value; round 5's safe_log / safe_sqrt reverse rules
+    did this and their gradients came out wrong on the GPU only)."""
+    import re
+    ins = [ln.strip() for ln in text.splitlines()
+           if ln.strip() and not ln.strip().startswith(";") and not ln.strip().endswith(":")]
+    bad = []
+    for a, b in zip(ins, ins[1:]):
+        if not a.startswith(TRANS):
+            continue
+        dst = a.split()[1].rstrip(",")
+        srcs = b.split(None, 1)[1].split(",")[1:] if len(b.split(None, 1)) > 1 else []
+        if b.startswith("v_") and any(re.fullmatch(re.escape(dst), s.strip().split()[0]) for s in srcs if s.strip()):
+            bad.append((a, b))
+    return bad
+
+
+@pytest.mark.parametrize("k", range(len(GRAD_OPSETS)))
+def test_gradient_code_has_no_transcendental_forwarding_hazard(k):
+    b_ops, u_ops = GRAD_OPSETS[k]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    flat = srhip.flatten(srhip.random_population(300, o, 7, np.float32, seed=31 + k), o, dtype=np.float32)
+    _, text, offs = jit_compile(flat, grad=True)
+    assert offs
+    assert trans_forwarding_hazards("v_rcp_f32_e32 v1, v2\nv_mul_f32_e32 v3, v4, v1") != []  # the check itself
+    bad = trans_forwarding_hazards(text)
+    assert not bad, bad[:3]
+
+
+@pytest.mark.parametrize("k", range(len(OPSETS)))
+def test_loss_code_has_no_transcendental_forwarding_hazard(k):
+    b_ops, u_ops = OPSETS[k]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    flat = srhip.flatten(srhip.random_population(300, o, 7, np.float32, seed=41 + k), o, dtype=np.float32)
+    for fast, memc in ((True, False), (False, False), (True, True)):
+        _, text, _ = jit_compile(flat, fast=fast, memc=memc)
+        bad = trans_forwarding_hazards(text)
+        assert not bad, bad[:3]
+
+
 def test_gradient_code_covers_config5_trees():
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     trees = srhip.random_population(2000, o, 20, np.float32, seed=5)
