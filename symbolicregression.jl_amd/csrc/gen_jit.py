@@ -85,6 +85,13 @@ ROUTINE_S_END, ROUTINE_V_END = 23, 30
 LOSS_PINNED_S = list(range(23, 64)) + [88, 89] + list(range(91, 102))
 
 
+def sgpr_pinned(name):
+    """Routines compiled with LOSS_PINNED_S held live: the losses, and the
+    Float64 pow and logs of PRECISE Float32 ^ and log10 (SGPR temporaries would otherwise
+    reach s23+)."""
+    return name.startswith(("l_", "d_", "b_pow", "u_log"))
+
+
 def snippet_source(rg, routines):
     R = rg.R
     _, rest = rg.vstate()
@@ -119,7 +126,7 @@ def snippet_source(rg, routines):
         out.append(f'extern "C" __global__ void __launch_bounds__(64) sr_h_{name}() {{')
         out.append("  St s;")
         out += pins("in")
-        if name.startswith(("l_", "d_")):
+        if sgpr_pinned(name):
             # a loss routine runs inside the hand-written tree loop (its state
             # in s40..s57) and between the tiles of memory-constant code (its
             # constants in s24..s39): LOSS_PINNED_S are held live across it, so
@@ -130,11 +137,12 @@ def snippet_source(rg, routines):
                 out.append('  asm volatile("; IN ' + " ".join(f"s{zs[j]}" for j in range(i, min(i + 8, len(zs)))) +
                            '" : ' + ", ".join(f'"={{s{zs[j]}}}"(zz[{j}])'
                                                                 for j in range(i, min(i + 8, len(zs)))) + ");")
+            out.append("  __builtin_amdgcn_sched_barrier(0);")  # nothing scheduled ahead of the pins
         out.append("  float& chk = s.chk; (void)chk;")
         out.append(f"  constexpr int R = {R}; (void)R;")
         out.append("  " + body)
         out += pins("out")
-        if name.startswith(("l_", "d_")):
+        if sgpr_pinned(name):
             zs = LOSS_PINNED_S
             for i in range(0, len(zs), 8):
                 out.append('  asm volatile("; OUT" :: ' + ", ".join(f'"{{s{zs[j]}}}"(zz[{j}])'
@@ -214,7 +222,9 @@ def routine_list():
             continue
         mk = ("chk = mark(s.a[r], chk); " if b in LOSSY_LHS else "") + \
              ("chk = mark(s.b[r], chk); " if b in LOSSY_RHS else "")
-        rs.append((f"b_{b.lower()}", rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], s.b[r]);"), False))
+        # Float64 pow (PRECISE Float32 ^) does not fit the temporaries four rows at once
+        rw = rows_serial if b == "POW" else rows
+        rs.append((f"b_{b.lower()}", rw(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], s.b[r]);"), False))
         if b == "DIV":  # the compiled IEEE division, where manual_div sends rows out of its range
             rs.append(("b_div_full", rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], s.b[r]);"), False))
     # constant-operand variants: the constant in SGPR s_k (no VGPR moves of a
@@ -224,9 +234,10 @@ def routine_list():
             continue
         imm = "const float imm = __int_as_float((int)s.s_k); "
         mk = "chk = mark(s.a[r], chk); " if b in LOSSY_LHS else ""
-        rs.append((f"b_{b.lower()}_rc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], imm);"), False))
+        rw = rows_serial if b == "POW" else rows
+        rs.append((f"b_{b.lower()}_rc", imm + rw(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(s.a[r], imm);"), False))
         mk = "chk = mark(s.a[r], chk); " if b in LOSSY_RHS else ""
-        rs.append((f"b_{b.lower()}_lc", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
+        rs.append((f"b_{b.lower()}_lc", imm + rw(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
         if b == "DIV":
             rs.append(("b_div_lc_full", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
     for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
@@ -572,13 +583,18 @@ def build(hipcc, outdir, R):
     for d in (fast, prec):
         for n in names:
             vtemp |= G.regs_used(d[n], G.REG_V) - vstate
-            stemp |= G.regs_used(d[n], G.REG_S) - sstate - (pinned if n.startswith(("l_", "d_")) else set())
+            stemp |= G.regs_used(d[n], G.REG_S) - sstate - (pinned if sgpr_pinned(n) else set())
     if vtemp & vstate or stemp & sstate:
         raise SystemExit("gen_jit: temp/state overlap")
     if max(vtemp, default=0) >= ROUTINE_V_END:
-        raise SystemExit(f"gen_jit: routine VGPR temps reach v{max(vtemp)} (v{ROUTINE_V_END}+ held by the tree loop)")
+        over = sorted({n for d in (fast, prec) for n in names
+                       if max(G.regs_used(d[n], G.REG_V) - vstate, default=0) >= ROUTINE_V_END})
+        raise SystemExit(f"gen_jit: routine VGPR temps reach v{max(vtemp)} (v{ROUTINE_V_END}+ held by the tree loop): {over}")
     if max(stemp, default=0) >= ROUTINE_S_END:
-        raise SystemExit(f"gen_jit: routine SGPR temps reach s{max(stemp)} (s{ROUTINE_S_END}+ held by the tree loop)")
+        over = sorted({n for d in (fast, prec) for n in names
+                       if max(G.regs_used(d[n], G.REG_S) - sstate - (pinned if sgpr_pinned(n) else set()),
+                              default=0) >= ROUTINE_S_END})
+        raise SystemExit(f"gen_jit: routine SGPR temps reach s{max(stemp)} (s{ROUTINE_S_END}+ held by the tree loop): {over}")
 
     def with_ret(lines, n, t):
         body = list(lines)

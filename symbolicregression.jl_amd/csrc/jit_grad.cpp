@@ -716,7 +716,7 @@ struct GradGen {
         }
         case SRHIP_BOP_POW: {
           // f = safe_pow(a, b): ∂a = g·b·safe_pow(a, b - 1), ∂b = g·f·log(a)
-          // where a > 0, else 0 (device_ops.h bop_d), pow and log by routine
+          // where a > 0, else 0 (device_ops.h bop_d), pow and log by PRECISE routine
           if (aa) {
             fetch(o.a, XS0);
             fetch(o.b, XS1);
@@ -725,7 +725,7 @@ struct GradGen {
               as.vop1(VOP1_MOV, "v_mov_b32_e32", VB + e, rsrc(o.b, XS1, e));
               as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VB + e, K(0xbf800000u), VB + e);  // b - 1
             }
-            routine(kBopRoutine[SRHIP_BOP_POW], false);
+            routine(kBopRoutine[SRHIP_BOP_POW], true);  // PRECISE, as the interpreter's bop_d
             fetch(o.b, XS1);  // the call reused the scratch registers
             int blk;
             const int d = dest(o.a, TP, &blk);
@@ -739,7 +739,7 @@ struct GradGen {
           if (ab) {
             fetch(o.a, XS0);
             for (int e = 0; e < R; ++e) as.vop1(VOP1_MOV, "v_mov_b32_e32", VA + e, rsrc(o.a, XS0, e));
-            routine(kUopRoutine[SRHIP_UOP_LOG], false);
+            routine(kUopRoutine[SRHIP_UOP_LOG], true);
             fetch(o.a, XS0);
             int blk;
             const int d = dest(o.b, TP, &blk);
