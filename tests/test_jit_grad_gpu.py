@@ -134,10 +134,8 @@ def scales32(trees, o, X, y, w):
 S_MAX = 1e20
 
 
-def check_grads(g, ref, S, ok_c, rtol, max_bad_frac, msg, noise=None, cond=None):
+def check_grads(g, ref, S, ok_c, rtol, max_bad_frac, msg, noise=None):
     sel = ok_c & np.isfinite(S) & np.isfinite(ref) & (S < S_MAX)
-    if cond is not None:
-        sel &= cond
     if noise is not None:
         sel &= np.isfinite(noise)
     a, b = g[sel], ref[sel]
@@ -192,18 +190,13 @@ def test_grad_tree_code_matches_interpreter_and_oracle(gpu_ctx, opset, weighted)
     assert n1 > 500
     # directly against the oracle's Float32 gradients, tight: 1e-5 of Σ|terms|
     # plus a 4-ulp move of ŷ (the sums' rounding and the FAST forward), none beyond
-    # config #3's safe_log and ^ may round a Float32 result an ulp away from
-    # the oracle's (float)f((double)x): there the tight check covers the
-    # constants whose oracle spread N is within 1e-2 of S (96-97 % of them);
-    # the ill-conditioned rest (N up to 2x S, e.g. cos(u ^ exp(x5))) differ by
-    # as much in both GPU paths alike and are held to the bound above
-    cond = None
-    if opset == "cfg3":
-        cond = N <= 1e-2 * S
-        assert cond[ok_c & np.isfinite(S)].mean() > 0.9
+    # (config #3's safe_log and ^ included: with OCML's logf / powf, 1-ulp
+    # differences turned into up to 1.4 % of the constants beyond this bound
+    # on ill-conditioned trees; since log and pow of Float32 are evaluated in
+    # Float64 and rounded once, as the oracle does, none is)
     S32, G32, DV = scales32(trees, o, X, y, w)
-    check_grads(g1, G32, S32, ok_c, 1e-5, 0.0, "tree code vs Float32 oracle", noise=DV / 4, cond=cond)
-    check_grads(g0, G32, S32, ok_c, 1e-5, 0.0, "interpreter vs Float32 oracle", noise=DV / 4, cond=cond)
+    check_grads(g1, G32, S32, ok_c, 1e-5, 0.0, "tree code vs Float32 oracle", noise=DV / 4)
+    check_grads(g0, G32, S32, ok_c, 1e-5, 0.0, "interpreter vs Float32 oracle", noise=DV / 4)
 
 
 def test_grad_tree_code_many_constants_fall_back(gpu_ctx):
