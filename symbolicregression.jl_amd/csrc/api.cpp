@@ -314,6 +314,10 @@ struct srhip_program {
   int32_t* d_gjit_cidx = nullptr;   // constants of those trees
   int ngjit_cidx = 0;
   float* d_gconsts = nullptr;       // the constants as Float32 (+16 padding)
+  // Float64 programs: the gradient tree code of jit64.cpp (L2), its constants (+16 padding)
+  jit::GradModule64* gjit64 = nullptr;
+  double* d_gconsts64 = nullptr;
+  size_t gcs64_cap = 0;
   size_t gjl_cap = 0, gjc_cap = 0, gcs_cap = 0;
   // byte capacities of the device buffers above (kept across rebuilds)
   size_t code_cap = 0, toff_cap = 0, list_cap = 0;
@@ -390,6 +394,11 @@ void free_grad_device(srhip_program* p) {
   p->gjit = nullptr;
   for (auto& l : p->gjit_loss) jit::destroy_grad(l.m);
   p->gjit_loss.clear();
+  jit::destroy_grad64(p->gjit64);
+  p->gjit64 = nullptr;
+  if (p->d_gconsts64) (void)hipFree(p->d_gconsts64);
+  p->d_gconsts64 = nullptr;
+  p->gcs64_cap = 0;
   p->grad_built = false;
 }
 
@@ -414,13 +423,21 @@ size_t gjit_tile_budget() {
   return b;
 }
 
-// the Float32 constants the gradient tree code reads (s_load), 16 floats of padding
+// the constants the gradient tree code reads (s_load), 16 of padding: Float32
+// (jit_grad.cpp) or Float64 (jit64.cpp) as the program's
 void upload_gconsts(srhip_program* p) {
   const size_t nconst = p->const_off.back();
-  std::vector<float> h(nconst + 16, 0.0f);
-  if (nconst) std::memcpy(h.data(), p->consts.data(), nconst * sizeof(float));
-  ensure_dev((void**)&p->d_gconsts, &p->gcs_cap, h.size() * sizeof(float));
-  HIP_CHECK(hipMemcpyAsync(p->d_gconsts, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, p->ctx->stream));
+  if (p->dtype == SRHIP_F64) {
+    std::vector<double> h(nconst + 16, 0.0);
+    if (nconst) std::memcpy(h.data(), p->consts.data(), nconst * sizeof(double));
+    ensure_dev((void**)&p->d_gconsts64, &p->gcs64_cap, h.size() * sizeof(double));
+    HIP_CHECK(hipMemcpyAsync(p->d_gconsts64, h.data(), h.size() * sizeof(double), hipMemcpyHostToDevice, p->ctx->stream));
+  } else {
+    std::vector<float> h(nconst + 16, 0.0f);
+    if (nconst) std::memcpy(h.data(), p->consts.data(), nconst * sizeof(float));
+    ensure_dev((void**)&p->d_gconsts, &p->gcs_cap, h.size() * sizeof(float));
+    HIP_CHECK(hipMemcpyAsync(p->d_gconsts, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice, p->ctx->stream));
+  }
   HIP_CHECK(hipStreamSynchronize(p->ctx->stream));
 }
 
@@ -608,7 +625,7 @@ void patch_grad_constants(srhip_program* p) {
     hipStream_t s = p->ctx->stream;
     HIP_CHECK(hipMemcpyAsync(p->d_gcode, p->h_gcode.data(), p->h_gcode.size(), hipMemcpyHostToDevice, s));
     HIP_CHECK(hipStreamSynchronize(s));
-    if (p->gjit) upload_gconsts(p);
+    if (p->gjit || p->gjit64) upload_gconsts(p);
   } else {
     p->grad_built = false;  // rebuilt below
   }
@@ -642,6 +659,8 @@ void build_grad_program(srhip_program* p) {
   p->gjit = nullptr;
   for (auto& l : p->gjit_loss) jit::destroy_grad(l.m);
   p->gjit_loss.clear();
+  jit::destroy_grad64(p->gjit64);
+  p->gjit64 = nullptr;
   p->h_gcand.clear();
   p->h_gjl.clear();
   p->gjit_stats = jit::GradStats();
@@ -669,6 +688,26 @@ void build_grad_program(srhip_program* p) {
         }
       else
         gjl.clear();
+    }
+  } else {  // Float64: the gradient tree code of jit64.cpp (L2)
+    std::vector<int32_t> cand;
+    for (int t = 0; t < p->ntrees; ++t)
+      if (cb.tree_off[t] >= 0) cand.push_back(t);
+    if (gjit_wanted((int)cand.size()) && jit::available64()) {
+      std::stable_sort(cand.begin(), cand.end(), [&](int32_t x, int32_t y) {
+        return cb.cost[x] != cb.cost[y] ? cb.cost[x] > cb.cost[y] : x < y;
+      });
+      std::vector<int32_t> rest;
+      p->gjit64 = jit::build_grad64(cb, p->const_off, cand, gjl, rest, &p->gjit_stats);
+      if (p->gjit64) {
+        p->h_gjl = gjl;
+        for (int32_t t : gjl) {
+          in_jit[t] = 1;
+          for (int k = p->const_off[t]; k < p->const_off[t + 1]; ++k) gcidx.push_back(k);
+        }
+      } else {
+        gjl.clear();
+      }
     }
   }
   // a work item carries the tangents of its group only: groups of 1 and 2
@@ -710,7 +749,7 @@ void build_grad_program(srhip_program* p) {
   HIP_CHECK(hipMemcpyAsync(p->d_const_off, p->const_off.data(), p->const_off.size() * sizeof(int32_t),
                            hipMemcpyHostToDevice, s));
   p->ngjit_cidx = (int)gcidx.size();
-  if (p->gjit) {
+  if (p->gjit || p->gjit64) {
     ensure_dev((void**)&p->d_gjit_list, &p->gjl_cap, gjl.size() * sizeof(int32_t));
     HIP_CHECK(hipMemcpyAsync(p->d_gjit_list, gjl.data(), gjl.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
     ensure_dev((void**)&p->d_gjit_cidx, &p->gjc_cap, std::max<size_t>(gcidx.size(), 1) * sizeof(int32_t));
@@ -718,7 +757,7 @@ void build_grad_program(srhip_program* p) {
       HIP_CHECK(hipMemcpyAsync(p->d_gjit_cidx, gcidx.data(), gcidx.size() * sizeof(int32_t), hipMemcpyHostToDevice, s));
   }
   HIP_CHECK(hipStreamSynchronize(s));
-  if (p->gjit) upload_gconsts(p);
+  if (p->gjit || p->gjit64) upload_gconsts(p);
   p->h_gcode.assign(reinterpret_cast<const unsigned char*>(cb.code.data()),
                     reinterpret_cast<const unsigned char*>(cb.code.data() + cb.code.size()));
   p->h_gtoff = cb.tree_off;
@@ -1791,6 +1830,56 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
                                          p->d_gjit_cidx, p->ngjit_cidx, static_cast<double*>(c->dloss.p), s));
       }
     }
+  } else if (p->gjit64 && mode == GRAD_LOSS && ds->rows > 0 && loss == SRHIP_LOSS_L2) {
+    // Float64 gradient tree code: 128-row tiles of y, the features it reads, w
+    jit::GradModule64* gm = p->gjit64;
+    const int nparts = jit::grad64_nparts(gm);
+    const int narr = 1 + jit::grad64_nraw(gm) + (ds->w ? 1 : 0);
+    if (jit::grad64_nraw(gm) > ds->nfeat) throw Error(SRHIP_ERR_INVALID, "dataset has fewer features than the program reads");
+    std::vector<EvalPlan> plans(nparts);
+    use_gjit = true;
+    for (int k = 0; k < nparts && use_gjit; ++k) {
+      int s0, nsl;
+      jit::grad64_part(gm, k, &s0, &nsl);
+      use_gjit = plan_geometry(8, 2, kShallowSlots, narr, 1, ds->rows, nsl, &plans[k], gjit_tile_budget()) &&
+                 plans[k].nrg == plans[0].nrg;
+      plans[k].threads = 256;
+    }
+    if (use_gjit) {
+      c->fail.ensure((size_t)jit::grad64_nslots(gm) * sizeof(uint32_t));
+      c->fail_clean = false;
+      HIP_CHECK(hipMemsetAsync(c->fail.p, 0, (size_t)jit::grad64_nslots(gm) * sizeof(uint32_t), s));
+      c->gpart.ensure(std::max<size_t>((size_t)plans[0].nrg * nconst, 1) * sizeof(double));
+      for (int k = 0; k < nparts; ++k) {
+        int s0, nsl;
+        jit::grad64_part(gm, k, &s0, &nsl);
+        const EvalPlan& plan = plans[k];
+        EvalArgs<double> a;
+        std::memset(&a, 0, sizeof(a));
+        a.list = p->d_gjit_list + s0;
+        a.fail = static_cast<uint32_t*>(c->fail.p) + s0;
+        a.nlist = nsl;
+        a.X = static_cast<const double*>(ds->X);
+        a.y = static_cast<const double*>(ds->y);
+        a.w = static_cast<const double*>(ds->w);
+        a.n = ds->rows;
+        a.n_pad = ds->n_pad;
+        a.nfeat = ds->nfeat;
+        a.ntiles = plan.ntiles;
+        a.ntg = plan.ntg;
+        a.tpb = plan.tpb;
+        a.nrg = plan.nrg;
+        a.loss = loss;
+        c->partial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<double>));
+        a.partial = static_cast<Part<double>*>(c->partial.p);
+        const int tk = timed_begin(c, s);
+        HIP_CHECK(jit::launch_grad_code64(gm, k, plan, a, p->d_gconsts64, static_cast<double*>(c->gpart.p), nconst, s));
+        timed_end(c, s, tk);
+        HIP_CHECK(launch_finalize<double>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
+      }
+      HIP_CHECK(launch_gconst_finalize(static_cast<const double*>(c->gpart.p), plans[0].nrg, nconst,
+                                       p->d_gjit_cidx, p->ngjit_cidx, static_cast<double*>(c->dloss.p), s));
+    }
   }
   c->last_jit_trees = use_gjit ? (int)p->h_gjl.size() : 0;
   const int* ngi = use_gjit ? p->ngitems_rest : p->ngitems;
@@ -2426,7 +2515,7 @@ int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntre
                                     int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load) {
   return guarded([&] {
     if (!prog) throw Error(SRHIP_ERR_INVALID, "null program");
-    const bool on = prog->gjit != nullptr;
+    const bool on = prog->gjit != nullptr || prog->gjit64 != nullptr;
     if (out_ntrees) *out_ntrees = on ? prog->gjit_stats.ntrees : 0;
     if (out_nrejected) *out_nrejected = on ? prog->gjit_stats.nrejected : 0;
     if (out_code_bytes) *out_code_bytes = on ? (int64_t)prog->gjit_stats.code_bytes : 0;
@@ -2489,9 +2578,16 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
     std::memcpy(&lbits, &lparam, 8);
     if (mode == 2 && !jit::has_dloss_routine(loss))
       throw Error(SRHIP_ERR_UNSUPPORTED, "no gradient tree code for this loss");
-    if (mode != 2 && mode != 5 && !jit::has_loss_routine(loss))
+    if (mode != 2 && mode != 5 && mode != 6 && !jit::has_loss_routine(loss))
       throw Error(SRHIP_ERR_UNSUPPORTED, "no tree code for this loss");
-    if (mode == 5) {  // Float64 tree code (jit64.cpp): L2, another loss's tail, or per-row outputs
+    if (mode == 6) {  // Float64 gradient tree code (jit64.cpp GradGen64): L2
+      if (loss != SRHIP_LOSS_L2) throw Error(SRHIP_ERR_UNSUPPORTED, "Float64 gradient tree code: L2 only");
+      CompiledBatch<double> cb = compile_batch<double>(*trees, /*grad=*/true);
+      std::vector<int32_t> cand, coff(trees->const_off, trees->const_off + trees->ntrees + 1);
+      for (int t = 0; t < cb.ntrees; ++t)
+        if (cb.tree_off[t] >= 0) cand.push_back(t);
+      jit::compile_grad_only64(cb, coff, cand, &bytes, &text, &offs);
+    } else if (mode == 5) {  // Float64 tree code (jit64.cpp): L2, another loss's tail, or per-row outputs
       CompiledBatch<double> cb = compile_batch<double>(*trees);
       std::vector<int32_t> cand;
       for (int t = 0; t < cb.ntrees; ++t)
@@ -2560,8 +2656,8 @@ int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int
 int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t fast, int32_t loss, double loss_param,
                                uint8_t* out_bytes, int64_t* inout_nbytes, char* out_text, int64_t* inout_ntext,
                                int32_t* out_offsets, int64_t* inout_noffsets) {
-  // fast bit 3: the Float64 tree compiler (jit64.cpp) with this loss's tail
-  return jit_compile_hook(trees, (fast & 8) ? 5 : grad ? 2 : ((fast & 1) ? 1 : 0), out_bytes, inout_nbytes, out_text,
+  // fast bit 3: the Float64 tree compiler (jit64.cpp) with this loss's tail, or with grad its gradient code
+  return jit_compile_hook(trees, (fast & 8) ? (grad ? 6 : 5) : grad ? 2 : ((fast & 1) ? 1 : 0), out_bytes, inout_nbytes, out_text,
                           inout_ntext, out_offsets, inout_noffsets, loss, loss_param);
 }
 

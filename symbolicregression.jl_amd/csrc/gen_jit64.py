@@ -255,6 +255,22 @@ def build(hipcc, outdir):
         f.write("#define SR_JIT64_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT64_CLOBBERS " + ", ".join([f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s]
                                                          + ['"vcc"', '"scc"']) + "\n")
+        # Float64 gradient tree code (jit64.cpp GradGen64): the same routines, a
+        # larger value pool, the tree's constants as VGPR pairs (the routines'
+        # SGPR temporaries reach s45), one Float64 accumulator pair per constant;
+        # its inputs: s[78:79] the tree's constants, s[84:85] its ∂L/∂c partials
+        g = dict(POOL0=56, NPOOL=20, C0=136, ACC=168, NACC=16, SCPTR=78, SGPTR=84)
+        assert g["POOL0"] + 4 * g["NPOOL"] == g["C0"] and g["C0"] + 2 * g["NACC"] == g["ACC"]
+        for k, v in g.items():
+            f.write(f"#define SR_JIT64_G_{k} {v}\n")
+        gin_v = {rg.CHK, rg.CHK + 1, rg.LANE, rg.LANE2, rg.LSUM, rg.LSUM + 1}
+        gclob_v = sorted((vtemp | set(range(rg.A, g["ACC"] + 2 * g["NACC"]))) - gin_v)
+        gin_s = {rg.S[k] for k in ("tile", "nt", "partial", "tilebytes", "woff", "status")} | \
+            {g["SCPTR"], g["SCPTR"] + 1, g["SGPTR"], g["SGPTR"] + 1}
+        assert not gin_s & (stemp | {20, 21})
+        gclob_s = sorted((stemp | set(range(20, 22)) | sstate) - gin_s)
+        f.write("#define SR_JIT64_GRAD_CLOBBERS " + ", ".join([f'"v{r}"' for r in gclob_v] + [f'"s{r}"' for r in gclob_s]
+                                                              + ['"vcc"', '"scc"']) + "\n")
         f.write(f"// routine VGPR temps {sorted(vtemp)}, SGPR temps {sorted(stemp)}\n")
 
 

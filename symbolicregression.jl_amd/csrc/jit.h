@@ -177,5 +177,27 @@ bool compile_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>&
                     std::string* text, std::vector<int32_t>* offsets,
                     const Opts64& opt = Opts64());
 
+// ---- Float64 gradient tree code (jit64.cpp GradGen64) --------------------------------
+// Reverse-mode ∂L/∂c (L2 loss) of gradient programs of Float64 trees whose
+// operators are + - * / ^ neg abs square cube exp log sqrt sin cos, with at
+// most SR_JIT64_G_NACC constants, read from a device array at run time; the
+// Float64 interpreter's routines (forward values and did_succeed are its own).
+struct GradModule64;
+GradModule64* build_grad64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
+                           const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list, std::vector<int32_t>& rest,
+                           GradStats* st);
+void destroy_grad64(GradModule64* m);
+int grad64_nslots(const GradModule64* m);
+int grad64_nparts(const GradModule64* m);
+void grad64_part(const GradModule64* m, int k, int* slot0, int* nslots);
+int grad64_nraw(const GradModule64* m);
+// plan: tile 128 rows, 256 threads; consts = the program's constants (+16
+// readable doubles of padding), gpart = [nrg][nconst] per-row-group ∂L/∂c
+hipError_t launch_grad_code64(GradModule64* m, int part, const EvalPlan& plan, const EvalArgs<double>& a,
+                              const double* consts, double* gpart, int nconst, hipStream_t stream);
+bool compile_grad_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
+                         const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
+                         std::vector<int32_t>* offsets);
+
 }  // namespace jit
 }  // namespace srhip

@@ -312,6 +312,111 @@ __device__ __forceinline__ void jit64_eval_dl_body(const Jit64Args& ja) {
       : SR_JIT64_CLOBBERS, "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s94", "s95", "s96", "s97",
         "v40", "v41", "v42", "v44", "v45", "v90", "v91", "v92", "memory");
 }
+// ---- Float64 gradient tree code (jit64.cpp GradGen64) ------------------------------
+// One workgroup = (row group, tree group) as sr_jit64_eval; each tree's code
+// runs the forward and the reverse pass of every tile, leaves Σ w·r² in LSUM
+// and the marker in CHK, and itself stores Σ_rows ∂L/∂c_j of each of its
+// constants (summed over the wave) to this row group's partials (gpart).
+struct Jit64GradArgs {
+  EvalArgs<double> e;
+  const int32_t* code_off;  // [nlist] byte offset of each slot's gradient code
+  const double* consts;     // [total constants + 16] the program's constants
+  const int32_t* cbase;     // [nlist] first constant of the slot's tree
+  double* gpart;            // [nrg][nconst] per-row-group ∂L/∂c
+  int nconst;
+  int nraw;                 // feature columns staged
+};
+
+template <bool W>
+__device__ __forceinline__ void jit64_grad_body(const Jit64GradArgs& ja) {
+  const EvalArgs<double>& a = ja.e;
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  double* sX = reinterpret_cast<double*>(smem);
+  const int narr = 1 + ja.nraw + (W ? 1 : 0);
+  const int rows = a.ntiles * TILE64;
+  const int rg = blockIdx.x / a.ntg;
+  const int g = blockIdx.x - rg * a.ntg;
+  const int64_t row0 = (int64_t)rg * rows;
+  const int nthreads = __builtin_amdgcn_readfirstlane((int)blockDim.x);
+  {
+    constexpr int V = TILE64 / 2;
+    const int total = a.ntiles * narr * V;
+    for (int idx = threadIdx.x; idx < total; idx += nthreads) {
+      const int v = idx % V;
+      const int tk = idx / V;
+      const int k = tk % narr;
+      const int t = tk / narr;
+      const double* src = k == 0 ? a.y : (k <= ja.nraw ? a.X + (size_t)(k - 1) * a.n_pad : a.w);
+      reinterpret_cast<double2*>(sX + (size_t)tk * TILE64)[v] =
+          reinterpret_cast<const double2*>(src + row0 + (int64_t)t * TILE64)[v];
+    }
+  }
+  __syncthreads();
+  const int lane = threadIdx.x & 63;
+  const int64_t rem = a.n - row0;
+  const int nt_valid = (int)min((int64_t)a.ntiles, (rem + TILE64 - 1) / TILE64);
+  const int last_valid = (int)(rem - (int64_t)(nt_valid - 1) * TILE64);
+  const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+  const int nwaves = nthreads >> 6;
+  auto slot_of = [&](int i) { return i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g); };
+  auto sld = [&](const int32_t* p, int s) {
+    return __builtin_amdgcn_readfirstlane(((const __attribute__((address_space(4))) int32_t*)(p))[s]);
+  };
+  auto ld_flag = [&](int slot) { return __hip_atomic_load(a.fail + slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  uint64_t area;
+  asm volatile(
+      "s_getpc_b64 s[88:89]\n"
+      "s_add_u32 s88, s88, sr_jit64_code@rel32@lo+4\n"
+      "s_addc_u32 s89, s89, sr_jit64_code@rel32@hi+12"
+      : "={s[88:89]}"(area)
+      :
+      : "scc");  // s_add / s_addc: a carry chain of the compiler must not span this
+  const uint32_t lds_lane = (uint32_t)reinterpret_cast<uintptr_t>((const __attribute__((address_space(3))) double*)sX) +
+                            (uint32_t)lane * 16u;
+  const uint32_t tilebytes = (uint32_t)(narr * TILE64 * 8);
+  const uint32_t woff = W ? (uint32_t)((1 + ja.nraw) * TILE64 * 8) : 0u;
+  const uint32_t lane2 = (uint32_t)lane * R64;
+  const uint32_t partial = (uint32_t)last_valid;
+  const uint32_t nt_u = (uint32_t)nt_valid;
+  Part<double>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
+  double* gdst = ja.gpart + (size_t)rg * (size_t)ja.nconst;
+
+  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
+  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
+  m = __builtin_amdgcn_readfirstlane(m);
+  uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
+  for (int k = 0; k < m; ++k) {
+    const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
+    const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
+    const bool more = k + 1 < m;
+    const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
+    if (more) fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
+    double lsum = 0.0, chk = skip ? __builtin_nan("") : 0.0;
+    if (!skip) {
+      const int cb = sld(ja.cbase, s);
+      const uint64_t target = area + (uint32_t)sld(ja.code_off, s);
+      const uint64_t cptr = reinterpret_cast<uint64_t>(ja.consts + cb);
+      const uint64_t gptr = reinterpret_cast<uint64_t>(gdst + cb);
+      uint32_t la = lds_lane;
+      uint32_t tile = 0, status;
+      asm volatile("s_swappc_b64 s[76:77], %[tgt]"
+                   : "+{v[44:45]}"(lsum), "+{v[40:41]}"(chk), "+{v42}"(la), "+{s64}"(tile), "={s69}"(status)
+                   : [tgt] "s"(target), "{v43}"(lane2), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
+                     "{s68}"(woff), "{s[78:79]}"(cptr), "{s[84:85]}"(gptr)
+                   : SR_JIT64_GRAD_CLOBBERS, "memory");
+      (void)status;
+    }
+    // a skipped or failed tree's ∂L/∂c partials are not read (finalize marks it failed)
+    lsum = wave_sum(lsum);
+    chk = __builtin_amdgcn_ballot_w64(chk != chk) != 0 ? __builtin_nan("") : 0.0;
+    if (lane == 0) dst[i] = Part<double>{lsum, chk};
+    if (!skip && chk != chk && lane == 0)
+      __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+extern "C" __global__ void __launch_bounds__(256) sr_jit64_grad(Jit64GradArgs ja) { jit64_grad_body<false>(ja); }
+extern "C" __global__ void __launch_bounds__(256) sr_jit64_grad_w(Jit64GradArgs ja) { jit64_grad_body<true>(ja); }
+
 extern "C" __global__ void __launch_bounds__(1024) sr_jit64_eval_dl(Jit64Args ja) { jit64_eval_dl_body<false>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit64_eval_dlw(Jit64Args ja) { jit64_eval_dl_body<true>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit64_eval(Jit64Args ja) { jit64_eval_body<false>(ja); }

@@ -125,6 +125,9 @@ hipError_t launch_pack_partials(const double* sum, const uint8_t* ok, const uint
                                 double wsum, double* out, hipStream_t stream);
 hipError_t launch_gconst_finalize(const float* gpart, int nrg, int nconst, const int32_t* cidx, int ncidx,
                                   double* out, hipStream_t stream);
+// the same over Float64 partials (jit64.cpp's gradient tree code)
+hipError_t launch_gconst_finalize(const double* gpart, int nrg, int nconst, const int32_t* cidx, int ncidx,
+                                  double* out, hipStream_t stream);
 
 template <typename T>
 hipError_t launch_eval(const EvalPlan& plan, const EvalArgs<T>& a, int mode,

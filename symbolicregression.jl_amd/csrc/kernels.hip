@@ -323,7 +323,8 @@ hipError_t launch_zero_words(uint32_t* a, int64_t na, uint32_t* b, int64_t nb, h
 
 namespace {
 // one wave per 64 constants, the four waves of a workgroup split the row groups
-__global__ void __launch_bounds__(256) gconst_finalize_kernel(const float* __restrict__ gpart, int nrg, int nconst,
+template <typename P>
+__global__ void __launch_bounds__(256) gconst_finalize_kernel(const P* __restrict__ gpart, int nrg, int nconst,
                                                               const int32_t* __restrict__ cidx, int ncidx,
                                                               double* __restrict__ out) {
   __shared__ double sh[4][64];
@@ -343,8 +344,15 @@ __global__ void __launch_bounds__(256) gconst_finalize_kernel(const float* __res
 hipError_t launch_gconst_finalize(const float* gpart, int nrg, int nconst, const int32_t* cidx, int ncidx,
                                   double* out, hipStream_t stream) {
   if (ncidx <= 0) return hipSuccess;
-  hipLaunchKernelGGL(gconst_finalize_kernel, dim3((unsigned)((ncidx + 63) / 64)), dim3(256), 0, stream, gpart, nrg,
-                     nconst, cidx, ncidx, out);
+  hipLaunchKernelGGL(gconst_finalize_kernel<float>, dim3((unsigned)((ncidx + 63) / 64)), dim3(256), 0, stream, gpart,
+                     nrg, nconst, cidx, ncidx, out);
+  return hipGetLastError();
+}
+hipError_t launch_gconst_finalize(const double* gpart, int nrg, int nconst, const int32_t* cidx, int ncidx,
+                                  double* out, hipStream_t stream) {
+  if (ncidx <= 0) return hipSuccess;
+  hipLaunchKernelGGL(gconst_finalize_kernel<double>, dim3((unsigned)((ncidx + 63) / 64)), dim3(256), 0, stream, gpart,
+                     nrg, nconst, cidx, ncidx, out);
   return hipGetLastError();
 }
 

@@ -135,6 +135,27 @@ def trans_forwarding_hazards(text: str):
     return bad
 
 
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.parametrize("k", range(len(GRAD_OPSETS)))
+def test_float64_gradient_machine_code_equals_llvm_mc(k):
+    """The Float64 reverse-mode gradient tree code (jit64.cpp GradGen64): same
+    check, and every tree of these operator sets compiles."""
+    b_ops, u_ops = GRAD_OPSETS[k]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    trees = srhip.random_population(300, o, 7, np.float64, seed=51 + k)
+    flat = srhip.flatten(trees, o, dtype=np.float64)
+    code, text, offs = jit_compile(flat, grad=True)
+    assert len(offs) >= 0.95 * len(trees), f"only {len(offs)} of {len(trees)} trees compiled"
+    ref = assemble(text)
+    assert len(ref) == len(code)
+    if ref != code:
+        a = np.frombuffer(code, dtype=np.uint32)
+        r = np.frombuffer(ref, dtype=np.uint32)
+        i = int(np.flatnonzero(a != r)[0])
+        raise AssertionError(f"word {i}: jit {a[i]:#010x} vs llvm-mc {r[i]:#010x}")
+    assert not trans_forwarding_hazards(text)
+
+
 @pytest.mark.parametrize("k", range(len(GRAD_OPSETS)))
 def test_gradient_code_has_no_transcendental_forwarding_hazard(k):
     b_ops, u_ops = GRAD_OPSETS[k]
