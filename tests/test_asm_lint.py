@@ -22,7 +22,8 @@ SCC_WRITERS = re.compile(
 
 # clobber macros and the generator that defines each (must emit "scc")
 MACROS = {"SR_JIT_CLOBBERS": "gen_jit.py", "SR_JIT_CLOBBERS_MEMC": "gen_jit.py", "SR_JIT_GRAD_CLOBBERS": "gen_jit.py",
-          "SR_JIT64_CLOBBERS": "gen_jit64.py", "SR_TI_CLOBBERS": "gen_asm_interp.py"}
+          "SR_JIT64_CLOBBERS": "gen_jit64.py", "SR_JIT64_GRAD_CLOBBERS": "gen_jit64.py",
+          "SR_TI_CLOBBERS": "gen_asm_interp.py"}
 
 
 def _statements(text, holders=False):
