@@ -338,7 +338,7 @@ int32_t srhip_optimize_constants_cb(const srhip_trees* trees, int32_t dtype, con
  * (symbolicregression.jl_amd/csrc/jit.cpp for Float32, jit64.cpp for
  * Float64; SRHIP_JIT=0 turns it off, =1 on for every size). Tree code
  * computes exactly what the interpreter computes: eval_loss with L2 and with
- * the elementwise losses that have a loss routine (Float32: all but LP and
+ * the elementwise losses that have a loss routine (Float32: all but
  * Periodic; Float64: all but LogCosh and LogitDist — the others run
  * interpreted), and the per-row outputs of eval_tree_array. This reports:
  * trees compiled, of which with a guarded Float32-transcendental path, code
@@ -354,11 +354,10 @@ int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, i
  * as memory-constant tree code). */
 int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inplace, int64_t* out_rebuilt);
 /* Gradient tree code of this program (reverse-mode ∂L/∂c for
- * srhip_eval_loss_grad with L2 and the losses with a Float32 dℓ/dr routine —
- * all but LP and Periodic — built on the first gradient call):
+ * srhip_eval_loss_grad, built on the first gradient call; Float32: L2 and the
+ * losses with a dℓ/dr routine — all but Periodic; Float64: L2, jit64.cpp):
  * trees compiled, trees left to the forward-mode interpreter, code bytes,
- * codegen and load times (ms). All zero before the first gradient call or for
- * Float64 programs. */
+ * codegen and load times (ms). All zero before the first gradient call. */
 int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nrejected,
                                     int64_t* out_code_bytes, double* out_ms_codegen, double* out_ms_load);
 /* Trees of the last eval on this context whose tree code handed a tile back
@@ -367,9 +366,8 @@ int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntre
  * guard fired or the tile failed; out_redone may be NULL). */
 int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* out_redone);
 /* Trees the last eval or gradient on this context ran as tree code (0: all
- * interpreted; Float32 loss evaluations and srhip_eval_loss_grad: L2 and,
- * compiled at their first use, L1 / Huber / the epsilon-insensitive losses /
- * Quantile). */
+ * interpreted; srhip_eval_loss_grad: Float32 with L2 and, compiled at their
+ * first use, the other losses with a dℓ/dr routine; Float64 with L2). */
 int32_t srhip_last_tree_code(const srhip_ctx* ctx, int32_t* out_ntrees);
 /* Testing hook (no device needed): compile Float32 trees with the tree
  * compiler (fast: bit 0 the guarded FAST path, bit 1 memory-constant code,
@@ -390,8 +388,9 @@ int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int
  * guarded FAST path) or the gradient tree code (grad = 1) of Float32 trees
  * for the elementwise loss `loss` (SRHIP_LOSS_*) with its parameter; fast
  * bit 3: Float64 trees through the Float64 tree compiler with that loss's
- * routine in the tile tail. SRHIP_ERR_UNSUPPORTED when Float32 tree code has
- * no routine for that loss (a Float64 tree without one is not compiled). */
+ * routine in the tile tail, or with grad = 1 (L2 only) their gradient tree
+ * code. SRHIP_ERR_UNSUPPORTED when Float32 tree code has no routine for that
+ * loss (a Float64 tree without one is not compiled). */
 int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t fast, int32_t loss, double loss_param,
                                uint8_t* out_bytes, int64_t* inout_nbytes, char* out_text, int64_t* inout_ntext,
                                int32_t* out_offsets, int64_t* inout_noffsets);

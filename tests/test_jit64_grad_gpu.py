@@ -11,9 +11,9 @@ bop_d / uop_d's with the quotients by the Float64 division routine (g/b where
 the interpreter multiplies by 1/b), so each row's term moves by a few ulp and
 a constant's sum by a few ulp of S_j = Σ_rows |w·2r·∂ŷ/∂c_j|: tolerance
 1e-10·S_j against the interpreter. Against the oracle (host libm, one ulp away
-from OCML's pow / log / exp on some rows) the tolerance is 1e-8·S_j plus what
-a 1e-15 relative perturbation of X and the constants moves the oracle's own
-gradient by, times 4 (ill-conditioned trees)."""
+from OCML's pow / log / exp on some rows) the tolerance is 1e-8·S_j plus 4x
+the largest move of the oracle's own gradient under three 1e-15 relative
+perturbations of X and the constants (ill-conditioned trees)."""
 import os
 
 import numpy as np
@@ -90,17 +90,20 @@ def test_float64_grad_tree_code_matches_interpreter_and_oracle(gpu_ctx, opset, w
     assert w1 == w0
     with np.errstate(invalid="ignore", divide="ignore"):
         rel = np.abs(s1 - s0) / np.abs(s0)
-    m = ok1 & (s0 != 0)
+    m = ok1 & np.isfinite(s0) & (s0 != 0)
     assert np.all(rel[m] <= 1e-12), float(np.nanmax(rel[m]))
+    assert np.array_equal(s1[ok1 & ~np.isfinite(s0)], s0[ok1 & ~np.isfinite(s0)])  # overflowing sums: inf in both
     ok_c = np.repeat(ok1, np.diff(prog.flat.const_off))
     assert np.all(np.isnan(g1[~ok_c])) and np.all(np.isnan(g0[~ok_c]))
     S, G = oracle_terms(trees, o, X, y, w)
-    _, Gp = oracle_terms(trees, o, X, y, w, eps=1e-15, seed=5)
-    sel = ok_c & np.isfinite(S) & np.isfinite(G) & np.isfinite(Gp) & (S < 1e100)
+    spread = np.zeros_like(G)  # the oracle's own move under three 1e-15 perturbations
+    for seed in range(3):
+        spread = np.maximum(spread, np.abs(oracle_terms(trees, o, X, y, w, eps=1e-15, seed=5 + seed)[1] - G))
+    sel = ok_c & np.isfinite(S) & np.isfinite(G) & np.isfinite(spread) & (S < 1e100)
     assert sel.sum() > 300
     err_i = np.abs(g1[sel] - g0[sel])
     assert np.all(err_i <= 1e-10 * S[sel] + 1e-300), float(np.max(err_i / S[sel]))
-    bound = 1e-8 * S[sel] + 4 * np.abs(Gp[sel] - G[sel]) + 1e-300
+    bound = 1e-8 * S[sel] + 4 * spread[sel] + 1e-300
     for g, name in ((g1, "tree code"), (g0, "interpreter")):
         err = np.abs(g[sel] - G[sel])
         assert np.all(err <= bound), (name, int((err > bound).sum()), float(np.max(err / bound)))
