@@ -3,7 +3,8 @@
 
   #1  README quickstart shape: X 5x100 F32, ops [+,*,/,-]/[cos,exp]: call latency
   #3  NaN-heavy F64: [+,-,*,/,^]/[safe_log,safe_sqrt,cos,exp], X ~ U(-3,3),
-      4096 trees x 100k rows: eval_loss and eval_tree_array, did_succeed rate
+      4096 trees x 100k rows: eval_loss, eval_loss_grad and eval_tree_array,
+      did_succeed rate
   #5  20 features x 10M rows F32, 16k trees: eval_loss over all rows, over the
       1.25M-row shard one of 8 GPUs holds, and the fused constant gradients
       (eval_loss_grad) over the shard
@@ -79,6 +80,10 @@ def main():
              node_rows_per_s=nodes3 * n3 / k, call_node_rows_per_s=nodes3 * n3 / w, kernel_ms=k * 1e3,
              did_succeed_rate=float(np.mean(ok)), tree_code_trees=p3.jit_info()["ntrees"],
              ok_sum=int(np.sum(ok)))
+        w, k = timed(ctx, lambda: p3.eval_loss_grad(ds3, K.LOSS["L2"]))
+        emit(config="#3 NaN-heavy F64", what="eval_loss_grad (dL/dc of every constant) 4096 trees x 100k rows",
+             dtype="f64", node_rows_per_s=nodes3 * n3 / k, kernel_ms=k * 1e3, call_ms=w * 1e3,
+             grad_tree_code_trees=p3.grad_jit_info()["ntrees"], constants=int(p3.flat.const_off[-1]))
         p3o = srhip.Program(ctx, srhip.flatten(t3[:1024], o3, np.float64), np.float64)
         _, nodes3o, _ = p3o.info()
         w, k = timed(ctx, lambda: p3o.eval_tree_array(ds3))
