@@ -316,6 +316,8 @@ struct srhip_program {
   float* d_gconsts = nullptr;       // the constants as Float32 (+16 padding)
   // Float64 programs: the gradient tree code of jit64.cpp (L2), its constants (+16 padding)
   jit::GradModule64* gjit64 = nullptr;
+  struct GradLossJit64 { int kind; uint64_t bits; jit::GradModule64* m; };
+  std::vector<GradLossJit64> gjit64_loss;  // other losses' Float64 gradient tree code (same slots)
   double* d_gconsts64 = nullptr;
   size_t gcs64_cap = 0;
   size_t gjl_cap = 0, gjc_cap = 0, gcs_cap = 0;
@@ -396,6 +398,8 @@ void free_grad_device(srhip_program* p) {
   p->gjit_loss.clear();
   jit::destroy_grad64(p->gjit64);
   p->gjit64 = nullptr;
+  for (auto& l : p->gjit64_loss) jit::destroy_grad64(l.m);
+  p->gjit64_loss.clear();
   if (p->d_gconsts64) (void)hipFree(p->d_gconsts64);
   p->d_gconsts64 = nullptr;
   p->gcs64_cap = 0;
@@ -661,6 +665,8 @@ void build_grad_program(srhip_program* p) {
   p->gjit_loss.clear();
   jit::destroy_grad64(p->gjit64);
   p->gjit64 = nullptr;
+  for (auto& l : p->gjit64_loss) jit::destroy_grad64(l.m);
+  p->gjit64_loss.clear();
   p->h_gcand.clear();
   p->h_gjl.clear();
   p->gjit_stats = jit::GradStats();
@@ -700,7 +706,9 @@ void build_grad_program(srhip_program* p) {
       std::vector<int32_t> rest;
       p->gjit64 = jit::build_grad64(cb, p->const_off, cand, gjl, rest, &p->gjit_stats);
       if (p->gjit64) {
+        p->h_gcand = cand;
         p->h_gjl = gjl;
+        p->gjit_consts = p->consts;
         for (int32_t t : gjl) {
           in_jit[t] = 1;
           for (int k = p->const_off[t]; k < p->const_off[t + 1]; ++k) gcidx.push_back(k);
@@ -1335,6 +1343,36 @@ jit::GradModule* grad_module(srhip_program* p, int loss, double lparam) {
   return m;
 }
 
+// The same for a Float64 program (jit64.cpp GradGen64): the L2 build, or the
+// same candidates compiled with that loss's seed; null: interpreted.
+jit::GradModule64* grad_module64(srhip_program* p, int loss, double lparam) {
+  if (!p->gjit64) return nullptr;
+  if (loss == SRHIP_LOSS_L2) return p->gjit64;
+  static const bool on = [] { const char* e = std::getenv("SRHIP_JIT_LOSSES"); return !(e && e[0] == '0'); }();
+  if (!on || loss < 0 || loss >= SRHIP_NUM_LOSSES || !jit::has_dloss_routine64(loss)) return nullptr;
+  uint64_t bits;
+  std::memcpy(&bits, &lparam, 8);
+  for (const auto& l : p->gjit64_loss)
+    if (l.kind == loss && l.bits == bits) return l.m;
+  srhip_trees tr;
+  tr.ntrees = p->ntrees;
+  tr.node_off = p->node_off.data();
+  tr.kind = p->kind.data();
+  tr.arg = p->arg.data();
+  tr.const_off = p->const_off.data();
+  tr.consts = p->gjit_consts.data();
+  CompiledBatch<double> cb = compile_batch_par<double>(tr, /*grad=*/true);
+  std::vector<int32_t> gjl, rest;
+  jit::GradStats st;
+  jit::GradModule64* m = jit::build_grad64(cb, p->const_off, p->h_gcand, gjl, rest, &st, loss, bits);
+  if (m && gjl != p->h_gjl) {
+    jit::destroy_grad64(m);
+    m = nullptr;
+  }
+  p->gjit64_loss.push_back({loss, bits, m});
+  return m;
+}
+
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
 // n_pad) may be the dataset itself or a gathered row subset.
 template <typename T>
@@ -1830,9 +1868,9 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
                                          p->d_gjit_cidx, p->ngjit_cidx, static_cast<double*>(c->dloss.p), s));
       }
     }
-  } else if (p->gjit64 && mode == GRAD_LOSS && ds->rows > 0 && loss == SRHIP_LOSS_L2) {
+  } else if (jit::GradModule64* gm = (p->gjit64 && mode == GRAD_LOSS && ds->rows > 0) ? grad_module64(p, loss, lparam)
+                                                                                      : nullptr) {
     // Float64 gradient tree code: 128-row tiles of y, the features it reads, w
-    jit::GradModule64* gm = p->gjit64;
     const int nparts = jit::grad64_nparts(gm);
     const int narr = 1 + jit::grad64_nraw(gm) + (ds->w ? 1 : 0);
     if (jit::grad64_nraw(gm) > ds->nfeat) throw Error(SRHIP_ERR_INVALID, "dataset has fewer features than the program reads");
@@ -2580,13 +2618,13 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
       throw Error(SRHIP_ERR_UNSUPPORTED, "no gradient tree code for this loss");
     if (mode != 2 && mode != 5 && mode != 6 && !jit::has_loss_routine(loss))
       throw Error(SRHIP_ERR_UNSUPPORTED, "no tree code for this loss");
-    if (mode == 6) {  // Float64 gradient tree code (jit64.cpp GradGen64): L2
-      if (loss != SRHIP_LOSS_L2) throw Error(SRHIP_ERR_UNSUPPORTED, "Float64 gradient tree code: L2 only");
+    if (mode == 6) {  // Float64 gradient tree code (jit64.cpp GradGen64)
+      if (!jit::has_dloss_routine64(loss)) throw Error(SRHIP_ERR_UNSUPPORTED, "no Float64 gradient tree code for this loss");
       CompiledBatch<double> cb = compile_batch<double>(*trees, /*grad=*/true);
       std::vector<int32_t> cand, coff(trees->const_off, trees->const_off + trees->ntrees + 1);
       for (int t = 0; t < cb.ntrees; ++t)
         if (cb.tree_off[t] >= 0) cand.push_back(t);
-      jit::compile_grad_only64(cb, coff, cand, &bytes, &text, &offs);
+      jit::compile_grad_only64(cb, coff, cand, &bytes, &text, &offs, loss, lbits);
     } else if (mode == 5) {  // Float64 tree code (jit64.cpp): L2, another loss's tail, or per-row outputs
       CompiledBatch<double> cb = compile_batch<double>(*trees);
       std::vector<int32_t> cand;

@@ -159,6 +159,12 @@ def routine_list():
             continue
         rs.append((f"l_{name.lower()}",
                    imm + rows(f"s.a[r] = dev::elem_loss<double>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0);")))
+    # dℓ/dr of the same losses (the Float64 gradient tree code's seed, jit64.cpp GradGen64)
+    for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
+        if name == "L2":
+            continue
+        rs.append((f"d_{name.lower()}",
+                   imm + rows(f"s.a[r] = dev::elem_dloss<double>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0);")))
     return rs
 
 
@@ -251,6 +257,8 @@ def build(hipcc, outdir):
                 + "}\n")
         f.write("#define SR_JIT64_LOSS_ROUTINE {" + ", ".join(
             str(-1 if n == "L2" else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
+        f.write("#define SR_JIT64_DLOSS_ROUTINE {" + ", ".join(
+            str(-1 if n == "L2" else rid(f"d_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write(f"#define SR_JIT64_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT64_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT64_CLOBBERS " + ", ".join([f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s]

@@ -178,14 +178,16 @@ bool compile_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>&
                     const Opts64& opt = Opts64());
 
 // ---- Float64 gradient tree code (jit64.cpp GradGen64) --------------------------------
-// Reverse-mode ∂L/∂c (L2 loss) of gradient programs of Float64 trees whose
+// Reverse-mode ∂L/∂c (L2, or any loss has_dloss_routine64 accepts) of gradient programs of Float64 trees whose
 // operators are + - * / ^ neg abs square cube exp log sqrt sin cos, with at
 // most SR_JIT64_G_NACC constants, read from a device array at run time; the
 // Float64 interpreter's routines (forward values and did_succeed are its own).
 struct GradModule64;
 GradModule64* build_grad64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
                            const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list, std::vector<int32_t>& rest,
-                           GradStats* st);
+                           GradStats* st, int loss = SRHIP_LOSS_L2, uint64_t lparam = 0);
+// the Float64 gradient tree code can seed its reverse pass with this loss
+bool has_dloss_routine64(int loss);
 void destroy_grad64(GradModule64* m);
 int grad64_nslots(const GradModule64* m);
 int grad64_nparts(const GradModule64* m);
@@ -197,7 +199,7 @@ hipError_t launch_grad_code64(GradModule64* m, int part, const EvalPlan& plan, c
                               const double* consts, double* gpart, int nconst, hipStream_t stream);
 bool compile_grad_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
                          const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
-                         std::vector<int32_t>* offsets);
+                         std::vector<int32_t>* offsets, int loss = SRHIP_LOSS_L2, uint64_t lparam = 0);
 
 }  // namespace jit
 }  // namespace srhip

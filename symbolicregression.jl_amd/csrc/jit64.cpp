@@ -68,6 +68,7 @@ const int kBop64RC[SRHIP_NUM_BOPS] = SR_JIT64_BOP_ROUTINE_RC;
 const int kBop64LC[SRHIP_NUM_BOPS] = SR_JIT64_BOP_ROUTINE_LC;
 const char* const kName64[kNum64] = SR_JIT64_ROUTINE_NAMES;
 const int kLoss64[SRHIP_NUM_LOSSES] = SR_JIT64_LOSS_ROUTINE;
+const int kDLoss64[SRHIP_NUM_LOSSES] = SR_JIT64_DLOSS_ROUTINE;
 constexpr int T_OUT = 92;  // s[92:93]: out mode, the tree's output rows of the current tile
 
 // gfx950 encodings used here and not by jit.cpp (checked against llvm-mc by tests/test_jit.py)
@@ -759,6 +760,8 @@ struct GradGen64 {
   std::vector<HOp> ops;
   HOpnd root;
   int nc = 0;
+  int loss = SRHIP_LOSS_L2;
+  uint64_t lparam = 0;  // bits of the loss's Float64 parameter
   std::string why;
   int n = 0;
   std::vector<uint8_t> hasc;  // the value's subtree holds a constant: it needs an adjoint
@@ -846,6 +849,13 @@ struct GradGen64 {
     if (!usef(root, n, true)) return false;
     if (root.k == H_VAL) last[root.v] = std::max(last[root.v], n);
     if ((int)feats.size() > GNP) { why = "more features than register blocks"; return false; }
+    if (loss != SRHIP_LOSS_L2) {  // the seed by the loss's ℓ and dℓ/dr routines
+      if (loss < 0 || loss >= SRHIP_NUM_LOSSES || kLoss64[loss] < 0 || kDLoss64[loss] < 0) {
+        why = "no Float64 loss / dℓ/dr routine";
+        return false;
+      }
+      has_call = true;
+    }
     return true;
   }
 
@@ -1285,6 +1295,41 @@ struct GradGen64 {
     as.bind(L_nomask);
   }
 
+  // any other elementwise loss: Σ w·ℓ(r) into LSUM and the seed w·ℓ'(r) into
+  // Y (r in Y, 0 past the last row), ℓ and ℓ' by the Float64 loss routines
+  // (device_ops.h elem_loss / elem_dloss, the parameter in s_k : s_kh), both
+  // masked after the call (ℓ'(0) need not be 0: Quantile's is τ); LSUM in the
+  // Float64 loss tree code's order (Gen64::emit_tail_loss)
+  bool emit_loss_seed() {
+    const int k = free_block();
+    if (k < 0) { why = "register pool exhausted (loss)"; return false; }
+    const int rb = blk(k);
+    mov_block(rb, Y2);
+    mov_block(A2, Y2);
+    as.sop1(SOP1_MOV, "s_mov_b32", T_K, K((uint32_t)lparam), "s" + std::to_string(T_K));
+    as.sop1(SOP1_MOV, "s_mov_b32", T_KH, K((uint32_t)(lparam >> 32)), "s" + std::to_string(T_KH));
+    routine(kLoss64[loss]);
+    mov_block(Y2, A2);
+    mov_block(A2, rb);
+    routine(kDLoss64[loss]);
+    const int L_unw = as.label();
+    as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(T_WOFF), K(0));
+    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
+    as.vop2(VOP2_ADD_U32, "v_add_u32_e32", GT2, S(T_WOFF), LANE2);
+    as.ds_read_b128(GT2, GT2, 0);
+    as.waitcnt_lgkm(0);
+    for (int e = 0; e < R2; ++e) {
+      mul(Y2 + 2 * e, V(GT2 + 2 * e), V(Y2 + 2 * e));
+      mul(A2 + 2 * e, V(GT2 + 2 * e), V(A2 + 2 * e));
+    }
+    as.bind(L_unw);
+    emit_mask(Y2);
+    emit_mask(A2);
+    for (int e = 0; e < R2; ++e) vop3d(VOP3_ADD_F64, "v_add_f64", LSUM2, V(LSUM2), V(Y2 + 2 * e), nullptr, 0);
+    mov_block(Y2, A2);
+    return true;
+  }
+
   void dpp_mov(int vdst, int vsrc, uint32_t ctrl, uint32_t row, const char* txt) {
     as.put(0x7e000000u | ((uint32_t)vdst << 17) | ((uint32_t)VOP1_MOV << 9) | 0xfau);
     as.put((uint32_t)vsrc | (ctrl << 8) | (0xfu << 24) | (row << 28));
@@ -1357,7 +1402,9 @@ struct GradGen64 {
     free_values_at(n);
     free_feats_at(n);
     emit_mask(Y2);
-    {
+    if (loss != SRHIP_LOSS_L2) {
+      if (!emit_loss_seed()) return false;
+    } else {
       const int L_unw = as.label(), L_seed = as.label();
       as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(T_WOFF), K(0));
       as.branch(SOPP_SCC1, "s_cbranch_scc1", L_unw);
@@ -1444,7 +1491,8 @@ struct GradGen64 {
 };
 
 bool gen_grad_tree64(const Ins<double>* prog, int nc, const Tmpl64& T, bool text, std::vector<uint32_t>& out,
-                     std::vector<std::string>* lines, int32_t* off, int* max_feat, std::string* why) {
+                     std::vector<std::string>* lines, int32_t* off, int* max_feat, std::string* why, int loss,
+                     uint64_t lparam) {
   if (nc > GNACC) { *why = "more constants than accumulators"; return false; }
   std::vector<HOp> ir;
   HOpnd root;
@@ -1456,6 +1504,8 @@ bool gen_grad_tree64(const Ins<double>* prog, int nc, const Tmpl64& T, bool text
   g.ops = ir;
   g.root = root;
   g.nc = nc;
+  g.loss = loss;
+  g.lparam = lparam;
   if (!g.emit_tree()) { *why = g.why; return false; }
   as.finish();
   while (out.size() < start) {
@@ -1475,7 +1525,7 @@ bool gen_grad_tree64(const Ins<double>* prog, int nc, const Tmpl64& T, bool text
 size_t grad_codegen64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
                       const std::vector<int32_t>& cand, size_t from, bool text, std::vector<uint32_t>& words,
                       std::vector<std::string>* lines, std::vector<int32_t>& offs, std::vector<int32_t>& ok_trees,
-                      std::vector<int32_t>& rest, int* max_feat, GradStats* st) {
+                      std::vector<int32_t>& rest, int* max_feat, GradStats* st, int loss, uint64_t lparam) {
   const Tmpl64& T = tmpl64();
   for (size_t k = from; k < cand.size(); ++k) {
     const int32_t t = cand[k];
@@ -1485,7 +1535,7 @@ size_t grad_codegen64(const CompiledBatch<double>& cb, const std::vector<int32_t
     int mf = *max_feat;
     const int nc = const_off[t + 1] - const_off[t];
     const bool okc = cb.tree_off[t] >= 0 &&
-                     gen_grad_tree64(&cb.code[cb.tree_off[t]], nc, T, text, words, lines, &off, &mf, &why);
+                     gen_grad_tree64(&cb.code[cb.tree_off[t]], nc, T, text, words, lines, &off, &mf, &why, loss, lparam);
     if (okc && words.size() * 4 > T.area_bytes) {
       words.resize(before);
       if (lines) lines->resize(lbefore);
@@ -1535,7 +1585,7 @@ struct GradModule64 {
 
 GradModule64* build_grad64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
                            const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list, std::vector<int32_t>& rest,
-                           GradStats* st) {
+                           GradStats* st, int loss, uint64_t lparam) {
   const Tmpl64& T = tmpl64();
   if (!T.ok) { rest = cand; return nullptr; }
   const auto t0 = std::chrono::steady_clock::now();
@@ -1547,7 +1597,7 @@ GradModule64* build_grad64(const CompiledBatch<double>& cb, const std::vector<in
   while (pos < cand.size()) {
     Chunk ch;
     const size_t next = grad_codegen64(cb, const_off, cand, pos, false, ch.words, nullptr, ch.offs, ch.slots, rest,
-                                       &max_feat, st);
+                                       &max_feat, st, loss, lparam);
     if (next == pos) { rest.push_back(cand[pos]); if (st) st->nrejected++; pos = next + 1; continue; }
     if ((int)chunks.size() + 1 == kMaxParts && next < cand.size()) {
       for (size_t k = next; k < cand.size(); ++k) rest.push_back(cand[k]);
@@ -1618,6 +1668,10 @@ void grad64_part(const GradModule64* m, int k, int* slot0, int* nslots) {
   *nslots = m->parts[k].nslots;
 }
 int grad64_nraw(const GradModule64* m) { return m ? m->nraw : 0; }
+bool has_dloss_routine64(int loss) {
+  return loss == SRHIP_LOSS_L2 ||
+         (loss >= 0 && loss < SRHIP_NUM_LOSSES && kLoss64[loss] >= 0 && kDLoss64[loss] >= 0);
+}
 
 hipError_t launch_grad_code64(GradModule64* m, int part, const EvalPlan& plan, const EvalArgs<double>& a,
                               const double* consts, double* gpart, int nconst, hipStream_t stream) {
@@ -1642,14 +1696,15 @@ hipError_t launch_grad_code64(GradModule64* m, int part, const EvalPlan& plan, c
 
 bool compile_grad_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
                          const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
-                         std::vector<int32_t>* offsets) {
+                         std::vector<int32_t>* offsets, int loss, uint64_t lparam) {
   const Tmpl64& T = tmpl64();
   if (!T.ok) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("Float64 jit template unavailable: ") + T.why);
   std::vector<uint32_t> words;
   std::vector<std::string> lines;
   std::vector<int32_t> offs, okt, rest;
   int mf = -1;
-  grad_codegen64(cb, const_off, cand, 0, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, &mf, nullptr);
+  grad_codegen64(cb, const_off, cand, 0, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, &mf, nullptr,
+                 loss, lparam);
   if (bytes) {
     bytes->resize(words.size() * 4);
     std::memcpy(bytes->data(), words.data(), bytes->size());

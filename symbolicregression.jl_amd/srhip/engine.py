@@ -299,9 +299,10 @@ def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bo
     nb, nt, no = C.c_int64(0), C.c_int64(0), C.c_int64(0)
 
     def call(*bufs):
-        if f64 and grad:  # the Float64 gradient tree code (jit64.cpp GradGen64), L2
-            return lib().srhip_jit_compile_loss(C.byref(tr), 1, 8, 0, 0.0, bufs[0], C.byref(nb), bufs[1], C.byref(nt),
-                                                bufs[2], C.byref(no))
+        if f64 and grad:  # the Float64 gradient tree code (jit64.cpp GradGen64)
+            kind, param = (0, 0.0) if loss is None else (int(loss.kind), float(loss.param))
+            return lib().srhip_jit_compile_loss(C.byref(tr), 1, 8, kind, param, bufs[0], C.byref(nb), bufs[1],
+                                                C.byref(nt), bufs[2], C.byref(no))
         if f64 and loss is not None:  # the Float64 tree compiler with another loss's tail
             return lib().srhip_jit_compile_loss(C.byref(tr), 0, 8, int(loss.kind), float(loss.param),
                                                 bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2], C.byref(no))
