@@ -193,6 +193,18 @@ LOSS_CASES = [srhip.L1DistLoss(), srhip.HuberLoss(0.7), srhip.L1EpsilonInsLoss(0
 
 
 @pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+@pytest.mark.parametrize("loss", LOSS_CASES + [srhip.PeriodicLoss(2.0)], ids=lambda l: f"kind{l.kind}")
+def test_float64_gradient_loss_seeds_equal_llvm_mc(loss):
+    """The Float64 gradient tree code seeded by another loss's ℓ and dℓ/dr
+    routines (jit64.cpp GradGen64::emit_loss_seed): machine code = llvm-mc's."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/", "^"], unary_operators=["safe_log", "cos", "exp"])
+    flat = srhip.flatten(srhip.random_population(100, o, 5, np.float64, seed=61), o, dtype=np.float64)
+    code, text, offs = jit_compile(flat, grad=True, loss=loss)
+    assert len(offs) >= 95
+    assert assemble(text) == code
+
+
 @pytest.mark.parametrize("loss", LOSS_CASES, ids=lambda l: f"kind{l.kind}")
 def test_loss_tails_equal_llvm_mc(loss):
     """Tree code of the non-L2 elementwise losses: the loss tree code's tile

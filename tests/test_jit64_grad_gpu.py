@@ -140,3 +140,75 @@ def test_float64_grad_tree_code_new_constants(gpu_ctx):
     np.testing.assert_array_equal(s1[ok1], s2[ok2])
     ok_c = np.repeat(ok1, np.diff(flat.const_off))
     np.testing.assert_array_equal(g1[ok_c], g2[ok_c])
+
+
+def dloss_np(kind, p, r):
+    """ℓ'(r) of device_ops.h elem_dloss in Float64."""
+    sg = np.sign(r)
+    ar = np.abs(r)
+    if kind == 1:
+        return sg
+    if kind == 3:
+        return np.where(ar <= p, r, p * sg)
+    if kind == 5:
+        return np.where(ar > p, sg, 0.0)
+    if kind == 6:
+        return np.where(ar > p, 2.0 * (ar - p) * sg, 0.0)
+    if kind == 7:
+        return np.where(r >= 0, p, p - 1.0)
+    if kind == 8:
+        k = 2 * np.pi / p
+        return k * np.sin(k * r)
+    raise ValueError(kind)
+
+
+LOSSES64 = [srhip.L1DistLoss(), srhip.HuberLoss(0.7), srhip.L1EpsilonInsLoss(0.3), srhip.L2EpsilonInsLoss(0.25),
+            srhip.QuantileLoss(0.8), srhip.PeriodicLoss(2.0)]
+
+
+@pytest.mark.parametrize("loss", LOSSES64, ids=lambda l: f"kind{l.kind}")
+def test_float64_grad_tree_code_other_losses(gpu_ctx, loss):
+    """The Float64 gradient tree code seeded by the loss's ℓ / dℓ/dr routines
+    ran (srhip_last_tree_code), did_succeed and losses as the interpreter's,
+    each constant within 1e-10 of Σ_rows |w·ℓ'(r)·∂ŷ/∂c_j| (the oracle's
+    Float64 terms) of the interpreter's gradient."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/", "^"], unary_operators=["safe_log", "cos", "exp"])
+    rng = np.random.default_rng(81)
+    n = 2001
+    X = np.abs(rng.uniform(-3, 3, (5, n))) + 0.1
+    y = 2 * np.cos(X[3]) + X[0] ** 2 - 2
+    w = rng.uniform(0.5, 2.0, n)
+    trees = srhip.random_population(400, o, 5, np.float64, seed=82)
+
+    def go(gjit):
+        os.environ["SRHIP_GJIT"] = "1" if gjit else "0"
+        try:
+            ds = srhip.DeviceDataset(gpu_ctx, X, y, w)
+            prog = srhip.Program(gpu_ctx, srhip.flatten(trees, o, dtype=np.float64), np.float64)
+            s, g, _, ok = prog.eval_loss_grad(ds, loss.kind, [loss.param])
+            return s.copy(), g.copy(), ok.copy(), gpu_ctx.last_tree_code(), prog
+        finally:
+            del os.environ["SRHIP_GJIT"]
+
+    s1, g1, ok1, ntc, prog = go(True)
+    s0, g0, ok0, ntc0, _ = go(False)
+    assert ntc >= 380 and ntc0 == 0
+    assert np.array_equal(ok1, ok0)
+    m = ok1 & np.isfinite(s0) & (s0 != 0)
+    assert np.all(np.abs(s1[m] - s0[m]) <= 1e-12 * np.abs(s0[m]))
+    flat = srhip.flatten(trees, o, dtype=np.float64)
+    S = []
+    for t in range(len(trees)):
+        k, a, c = flat.tree(t)
+        if len(c) == 0:
+            continue
+        with np.errstate(all="ignore"):
+            out, g, okt = oracle.eval_grad_consts(k, a, np.asarray(c, dtype=np.float64), X, len(c))
+            S.append(np.abs(w * dloss_np(loss.kind, loss.param, out - y) * g).sum(axis=1) if okt
+                     else np.full(len(c), np.nan))
+    S = np.concatenate(S)
+    ok_c = np.repeat(ok1, np.diff(prog.flat.const_off))
+    sel = ok_c & np.isfinite(S) & (S < 1e100)
+    assert sel.sum() > 200
+    err = np.abs(g1[sel] - g0[sel])
+    assert np.all(err <= 1e-10 * S[sel] + 1e-300), float(np.max(err / (S[sel] + 1e-300)))
