@@ -355,7 +355,8 @@ int32_t srhip_program_jit_info(const srhip_program* prog, int32_t* out_ntrees, i
 int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inplace, int64_t* out_rebuilt);
 /* Gradient tree code of this program (reverse-mode ∂L/∂c for
  * srhip_eval_loss_grad, built on the first gradient call; Float32: L2 and the
- * losses with a dℓ/dr routine — all but Periodic; Float64: L2, jit64.cpp):
+ * losses with a dℓ/dr routine — all but Periodic; Float64 (jit64.cpp): all
+ * but LP, LogCosh and LogitDist):
  * trees compiled, trees left to the forward-mode interpreter, code bytes,
  * codegen and load times (ms). All zero before the first gradient call. */
 int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nrejected,
@@ -366,8 +367,8 @@ int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntre
  * guard fired or the tile failed; out_redone may be NULL). */
 int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* out_redone);
 /* Trees the last eval or gradient on this context ran as tree code (0: all
- * interpreted; srhip_eval_loss_grad: Float32 with L2 and, compiled at their
- * first use, the other losses with a dℓ/dr routine; Float64 with L2). */
+ * interpreted; srhip_eval_loss_grad: L2 and, compiled at their first use,
+ * the other losses with a dℓ/dr routine, Float32 and Float64). */
 int32_t srhip_last_tree_code(const srhip_ctx* ctx, int32_t* out_ntrees);
 /* Testing hook (no device needed): compile Float32 trees with the tree
  * compiler (fast: bit 0 the guarded FAST path, bit 1 memory-constant code,
@@ -388,8 +389,7 @@ int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int
  * guarded FAST path) or the gradient tree code (grad = 1) of Float32 trees
  * for the elementwise loss `loss` (SRHIP_LOSS_*) with its parameter; fast
  * bit 3: Float64 trees through the Float64 tree compiler with that loss's
- * routine in the tile tail, or with grad = 1 (L2 only) their gradient tree
- * code. SRHIP_ERR_UNSUPPORTED when Float32 tree code has no routine for that
+ * routine in the tile tail, or with grad = 1 their gradient tree code. SRHIP_ERR_UNSUPPORTED when Float32 tree code has no routine for that
  * loss (a Float64 tree without one is not compiled). */
 int32_t srhip_jit_compile_loss(const srhip_trees* trees, int32_t grad, int32_t fast, int32_t loss, double loss_param,
                                uint8_t* out_bytes, int64_t* inout_nbytes, char* out_text, int64_t* inout_ntext,
