@@ -68,11 +68,16 @@ class Regs64:
 
 # Registers of the hand-written Float64 tree loop (jit64_template.hip
 # SR_JIT64_LOOP_TEXT) live across every tree-code call: s46..s57 its state,
-# s60 / s61 the tree and slot, s[88:89] the code area, s[94:95] its return.
-# Held live across each routine (the compiler may borrow one only saved to a
-# VGPR lane and restored), so routine SGPR temporaries stay in s0..s45;
-# VGPR temporaries stay below v88 (the loop's LDS tile / counter addresses).
-LOOP64_PINNED_S = list(range(46, 64)) + [88, 89] + list(range(94, 98))
+# s60 / s61 the tree and slot, s[88:89] the code area, s[94:95] its return;
+# and every SGPR above the routine temporaries that no state names (the
+# gradient tree code's constant / partial pointers s[78:79], s[84:85]
+# among them). Held live across each routine (the compiler may borrow one
+# only saved to a VGPR lane and restored), so routine SGPR temporaries stay
+# in s0..s45 — which lets the LogCosh / LogitDist / erfc routines in (round 5;
+# with fewer pins their exp / log1p constants went to s70..s85); VGPR
+# temporaries stay below v88 (the loop's LDS tile / counter addresses).
+LOOP64_PINNED_S = (list(range(46, 64)) + [70, 71, 78, 79, 80, 83, 84, 85, 88, 89] + list(range(91, 94)) +
+                   list(range(94, 102)))
 ROUTINE64_S_END, ROUTINE64_V_END = 46, 88
 
 

@@ -143,13 +143,9 @@ def test_float64_loss_tree_code_other_losses(gpu_ctx, loss, param):
     ds = srhip.DeviceDataset(ctx, X, y, w)
     progs = _progs(ctx, flat)
     s1, w1, ok1 = progs["1"].eval_loss(ds, K.LOSS[loss], [param])
-    if loss in ("LOGCOSH", "LOGITDIST"):
-        # no Float64 routine for these two: with the tree loop's registers
-        # held live their exp / log1p constants need SGPRs above the routine
-        # temporaries (gen_jit64.py leaves them out), so they run interpreted
-        assert ctx.last_tree_code() == 0
-    else:
-        assert ctx.last_tree_code() > 300
+    # every loss has a Float64 routine (LogCosh / LogitDist since round 5: the
+    # SGPRs above the routine temporaries are held live, gen_jit64.py)
+    assert ctx.last_tree_code() > 300
     s0, w0, ok0 = progs["0"].eval_loss(ds, K.LOSS[loss], [param])
     assert ctx.last_tree_code() == 0 and w1 == w0
     assert np.array_equal(ok1, ok0)

@@ -159,11 +159,15 @@ def dloss_np(kind, p, r):
     if kind == 8:
         k = 2 * np.pi / p
         return k * np.sin(k * r)
+    if kind == 4:
+        return np.tanh(r)
+    if kind == 9:
+        return np.tanh(0.5 * r)
     raise ValueError(kind)
 
 
 LOSSES64 = [srhip.L1DistLoss(), srhip.HuberLoss(0.7), srhip.L1EpsilonInsLoss(0.3), srhip.L2EpsilonInsLoss(0.25),
-            srhip.QuantileLoss(0.8), srhip.PeriodicLoss(2.0)]
+            srhip.QuantileLoss(0.8), srhip.PeriodicLoss(2.0), srhip.LogCoshLoss(), srhip.LogitDistLoss()]
 
 
 @pytest.mark.parametrize("loss", LOSSES64, ids=lambda l: f"kind{l.kind}")
