@@ -339,7 +339,7 @@ int32_t srhip_optimize_constants_cb(const srhip_trees* trees, int32_t dtype, con
  * Float64; SRHIP_JIT=0 turns it off, =1 on for every size). Tree code
  * computes exactly what the interpreter computes: eval_loss with L2 and with
  * the elementwise losses that have a loss routine (Float32: all but
- * Periodic; Float64: all but LogCosh and LogitDist — the others run
+ * Periodic; Float64: every loss — the others run
  * interpreted), and the per-row outputs of eval_tree_array. This reports:
  * trees compiled, of which with a guarded Float32-transcendental path, code
  * bytes, host code generation and code-object load times (ms). All zero for
@@ -356,7 +356,7 @@ int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inpla
 /* Gradient tree code of this program (reverse-mode ∂L/∂c for
  * srhip_eval_loss_grad, built on the first gradient call; Float32: L2 and the
  * losses with a dℓ/dr routine — all but Periodic; Float64 (jit64.cpp): all
- * but LP, LogCosh and LogitDist):
+ * but LP):
  * trees compiled, trees left to the forward-mode interpreter, code bytes,
  * codegen and load times (ms). All zero before the first gradient call. */
 int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nrejected,
