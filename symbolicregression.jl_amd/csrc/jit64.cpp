@@ -1573,6 +1573,7 @@ struct Jit64GradArgs {
 struct GradPart64 {
   hipModule_t mod = nullptr;
   hipFunction_t fn = nullptr, fn_w = nullptr;
+  hipFunction_t fn_dl = nullptr, fn_dlw = nullptr;  // the hand-written tree loop (sr_jit64_grad_dl)
   int32_t* d_off = nullptr;    // [nslots] code offsets
   int32_t* d_cbase = nullptr;  // [nslots] first constant of the slot's tree
   int slot0 = 0, nslots = 0;
@@ -1626,7 +1627,9 @@ GradModule64* build_grad64(const CompiledBatch<double>& cb, const std::vector<in
       HIP_CHECK(hipModuleLoadData(&q.mod, img.data()));
       HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, "sr_jit64_grad"));
       HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, "sr_jit64_grad_w"));
-      for (hipFunction_t f : {q.fn, q.fn_w})
+      HIP_CHECK(hipModuleGetFunction(&q.fn_dl, q.mod, "sr_jit64_grad_dl"));
+      HIP_CHECK(hipModuleGetFunction(&q.fn_dlw, q.mod, "sr_jit64_grad_dlw"));
+      for (hipFunction_t f : {q.fn, q.fn_w, q.fn_dl, q.fn_dlw})
         HIP_CHECK(hipFuncSetAttribute(reinterpret_cast<const void*>(f), hipFuncAttributeMaxDynamicSharedMemorySize,
                                       160 * 1024));
       std::vector<int32_t> cbase(ch.slots.size());
@@ -1688,10 +1691,14 @@ hipError_t launch_grad_code64(GradModule64* m, int part, const EvalPlan& plan, c
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const size_t narr = 1 + (size_t)m->nraw + (a.w ? 1 : 0);
-  const size_t lds = narr * (size_t)plan.ntiles * (size_t)TILE2 * sizeof(double);
-  note_kernel(a.w ? "sr_jit64_grad_w" : "sr_jit64_grad");
-  return hipModuleLaunchKernel(a.w ? q.fn_w : q.fn, (unsigned)a.nrg * (unsigned)a.ntg, 1, 1, 256, 1, 1, (unsigned)lds,
-                               stream, nullptr, cfg);
+  const size_t lds = narr * (size_t)plan.ntiles * (size_t)TILE2 * sizeof(double) + 16;
+  // the hand-written tree loop (its counter in the last 16 bytes); SRHIP_JIT_DYNLOOP=0: the compiled one
+  const char* dl = std::getenv("SRHIP_JIT_DYNLOOP");
+  const bool stl = dl && dl[0] == '0';
+  hipFunction_t fn = stl ? (a.w ? q.fn_w : q.fn) : (a.w ? q.fn_dlw : q.fn_dl);
+  note_kernel(stl ? (a.w ? "sr_jit64_grad_w" : "sr_jit64_grad") : (a.w ? "sr_jit64_grad_dlw" : "sr_jit64_grad_dl"));
+  return hipModuleLaunchKernel(fn, (unsigned)a.nrg * (unsigned)a.ntg, 1, 1, 256, 1, 1, (unsigned)lds, stream, nullptr,
+                               cfg);
 }
 
 bool compile_grad_only64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
