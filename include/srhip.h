@@ -373,7 +373,9 @@ int32_t srhip_last_tree_code(const srhip_ctx* ctx, int32_t* out_ntrees);
 /* Testing hook (no device needed): compile Float32 trees with the tree
  * compiler (fast: bit 0 the guarded FAST path, bit 1 memory-constant code,
  * bit 2 the per-row output code of srhip_eval_tree_array; bit 3: the trees
- * are Float64 (consts double) and go through the Float64 tree compiler).
+ * are Float64 (consts double) and go through the Float64 tree compiler; bit
+ * 4: no assembly text — the multi-threaded code generation of the product
+ * path, whose bytes must equal the text path's).
  * Returns the code bytes, their assembly text ('\n'-separated lines)
  * and, per compiled tree, (tree id, byte offset). Each inout_n* holds the
  * capacity on entry and the size on return; SRHIP_ERR_INVALID if too small. */

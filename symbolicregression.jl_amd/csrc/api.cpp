@@ -2604,7 +2604,7 @@ int32_t srhip_last_bailed(const srhip_ctx* ctx, int32_t* out_ntrees, int64_t* ou
 namespace {
 int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes, int64_t* inout_nbytes,
                          char* out_text, int64_t* inout_ntext, int32_t* out_offsets, int64_t* inout_noffsets,
-                         int loss = SRHIP_LOSS_L2, double lparam = 0.0, bool out_mode = false) {
+                         int loss = SRHIP_LOSS_L2, double lparam = 0.0, bool out_mode = false, bool notext = false) {
   return guarded([&] {
     if (!trees || !inout_nbytes || !inout_ntext || !inout_noffsets) throw Error(SRHIP_ERR_INVALID, "null argument");
     if (!jit::available()) throw Error(SRHIP_ERR_UNSUPPORTED, std::string("tree compiler: ") + jit::unavailable_reason());
@@ -2649,7 +2649,7 @@ int32_t jit_compile_hook(const srhip_trees* trees, int mode, uint8_t* out_bytes,
       jit::Options jo;
       jo.fast = mode == 1 || mode == 4;
       jo.memc = mode == 3 || mode == 4;
-      jo.text = true;
+      jo.text = !notext;  // no text: the parallel code generation of build()
       jo.loss = loss;
       jo.lparam = lbits;
       jo.out = out_mode;
@@ -2682,7 +2682,8 @@ int32_t srhip_jit_compile(const srhip_trees* trees, int32_t fast, uint8_t* out_b
     return jit_compile_hook(trees, 5, out_bytes, inout_nbytes, out_text, inout_ntext, out_offsets, inout_noffsets,
                             SRHIP_LOSS_L2, 0.0, (fast & 4) != 0);
   return jit_compile_hook(trees, (fast & 2) ? ((fast & 1) ? 4 : 3) : ((fast & 1) ? 1 : 0), out_bytes, inout_nbytes,
-                          out_text, inout_ntext, out_offsets, inout_noffsets, SRHIP_LOSS_L2, 0.0, (fast & 4) != 0);
+                          out_text, inout_ntext, out_offsets, inout_noffsets, SRHIP_LOSS_L2, 0.0, (fast & 4) != 0,
+                          (fast & 16) != 0);
 }
 
 int32_t srhip_jit_compile_grad(const srhip_trees* trees, uint8_t* out_bytes, int64_t* inout_nbytes,

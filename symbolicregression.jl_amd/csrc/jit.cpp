@@ -36,7 +36,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <atomic>
 #include <mutex>
+#include <thread>
 
 #include "jit_asm.h"
 
@@ -1163,6 +1165,97 @@ bool can_bail() {
 }
 const char* unavailable_reason() { return templates().why.c_str(); }
 
+// Host threads for code generation (SRHIP_JIT_THREADS, default min(16,
+// hardware threads); 1: serial).
+static int codegen_threads() {
+  static const int n = [] {
+    const char* e = std::getenv("SRHIP_JIT_THREADS");
+    const int hw = (int)std::max(1u, std::thread::hardware_concurrency());
+    return e ? std::max(1, std::atoi(e)) : std::min(16, hw);
+  }();
+  return n;
+}
+template <typename F>
+static void parallel_for(size_t n, F&& body) {
+  const int nth = (int)std::min<size_t>((size_t)codegen_threads(), (n + 63) / 64);
+  std::atomic<size_t> next{0};
+  auto work = [&] {
+    for (;;) {
+      const size_t b = next.fetch_add(64);
+      if (b >= n) return;
+      for (size_t k = b; k < std::min(n, b + 64); ++k) body(k);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int i = 1; i < nth; ++i) th.emplace_back(work);
+  work();
+  for (auto& t : th) t.join();
+}
+
+// codegen on several host threads: every tree at a provisional address (its
+// size does not depend on the address: the routine-base offsets are literals
+// either way), the layout in order, then every placed tree again at its final
+// address; the result is the serial codegen's word for word (false: a size
+// changed, the caller runs the serial one).
+static bool codegen_par(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, size_t from,
+                        const Options& opt, std::vector<uint32_t>& words, std::vector<int32_t>& offs,
+                        std::vector<int32_t>& ok_trees, std::vector<int32_t>& rest, Stats* st, const Tmpl& T,
+                        const Columns& cols, size_t* stop) {
+  DerivedMap dm;
+  dm.cols = &cols;
+  const size_t n = cand.size() - from;
+  struct R { std::vector<uint32_t> w; bool ok = false, fast = false; std::string why; size_t start = 0; };
+  std::vector<R> res(n);
+  parallel_for(n, [&](size_t k) {
+    const int32_t t = cand[from + k];
+    R& r = res[k];
+    int32_t off;
+    r.ok = cb.tree_off[t] >= 0 && gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, false, r.w, nullptr, T.area_va, &off,
+                                           &r.fast, &r.why, dm, opt.memc, opt.loss, opt.lparam, opt.out);
+  });
+  size_t pos = words.size(), end = n;
+  for (size_t k = 0; k < n; ++k) {
+    if (!res[k].ok) continue;
+    const size_t start = (pos + 15) / 16 * 16;
+    if ((start + res[k].w.size()) * 4 > T.area_bytes) { end = k; break; }
+    res[k].start = start;
+    pos = start + res[k].w.size();
+  }
+  bool same = true;
+  parallel_for(end, [&](size_t k) {
+    R& r = res[k];
+    if (!r.ok) return;
+    const size_t sz = r.w.size();
+    r.w.clear();
+    int32_t off;
+    bool f;
+    std::string why;
+    const int32_t t = cand[from + k];
+    if (!gen_tree(&cb.code[cb.tree_off[t]], T, opt.fast, false, r.w, nullptr, T.area_va + r.start * 4, &off, &f, &why,
+                  dm, opt.memc, opt.loss, opt.lparam, opt.out) ||
+        r.w.size() != sz)
+      same = false;
+  });
+  if (!same) return false;
+  static const bool dbg = std::getenv("SRHIP_JIT_DEBUG") != nullptr;
+  for (size_t k = 0; k < end; ++k) {
+    const R& r = res[k];
+    if (!r.ok) {
+      rest.push_back(cand[from + k]);
+      if (st) st->nrejected++;
+      if (dbg) std::fprintf(stderr, "jit: tree %d not compiled: %s\n", cand[from + k], r.why.c_str());
+      continue;
+    }
+    words.resize(r.start, 0xbf800000u);  // s_nop padding to the 64-byte entry
+    words.insert(words.end(), r.w.begin(), r.w.end());
+    ok_trees.push_back(cand[from + k]);
+    offs.push_back((int32_t)(r.start * 4));
+    if (st) { st->ntrees++; st->nfast += r.fast ? 1 : 0; }
+  }
+  *stop = end == n ? cand.size() : from + end;
+  return true;
+}
+
 // Trees that compile are appended to ok_trees / offs, the others to `rest`; a
 // tree that no longer fits in the area ends the call (returns its position in
 // cand; cand.size() when all were done).
@@ -1170,6 +1263,17 @@ static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>
                       const Options& opt, std::vector<uint32_t>& words, std::vector<std::string>* lines,
                       std::vector<int32_t>& offs, std::vector<int32_t>& ok_trees, std::vector<int32_t>& rest,
                       Stats* st, const Tmpl& T, const Columns& cols) {
+  if (!lines && cand.size() - from >= 512 && codegen_threads() > 1) {
+    const size_t w0 = words.size(), o0 = offs.size(), k0 = ok_trees.size(), r0 = rest.size();
+    const Stats s0 = st ? *st : Stats();
+    size_t stop = 0;
+    if (codegen_par(cb, cand, from, opt, words, offs, ok_trees, rest, st, T, cols, &stop)) return stop;
+    words.resize(w0);  // a size changed with the address: the serial layout below
+    offs.resize(o0);
+    ok_trees.resize(k0);
+    rest.resize(r0);
+    if (st) *st = s0;
+  }
   DerivedMap dm;
   dm.cols = &cols;
   for (size_t k = from; k < cand.size(); ++k) {

@@ -286,7 +286,7 @@ def _trees_struct(flat: FlatTrees, consts: np.ndarray) -> Trees:
 
 
 def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bool = False, loss=None,
-                out: bool = False):
+                out: bool = False, text: bool = True):
     """Tree compiler without a device (srhip_jit_compile, or with grad=True
     srhip_jit_compile_grad: the reverse-mode gradient tree code; memc: the
     memory-constant loss tree code; loss: a Loss other than L2, through
@@ -315,7 +315,8 @@ def jit_compile(flat: FlatTrees, fast: bool = True, grad: bool = False, memc: bo
         if grad:
             return lib().srhip_jit_compile_grad(C.byref(tr), bufs[0], C.byref(nb), bufs[1], C.byref(nt), bufs[2],
                                                 C.byref(no))
-        return lib().srhip_jit_compile(C.byref(tr), int(fast) | (2 if memc else 0) | (4 if out else 0), bufs[0],
+        return lib().srhip_jit_compile(C.byref(tr), int(fast) | (2 if memc else 0) | (4 if out else 0) |
+                                       (0 if text else 16), bufs[0],
                                        C.byref(nb), bufs[1],
                                        C.byref(nt), bufs[2], C.byref(no))
 

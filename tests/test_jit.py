@@ -55,6 +55,21 @@ def test_machine_code_equals_llvm_mc(k):
             raise AssertionError(f"word {i}: jit {a[i]:#010x} vs llvm-mc {r[i]:#010x} near '{lines[:]}'"[:400])
 
 
+@pytest.mark.parametrize("k", range(len(OPSETS)))
+def test_threaded_code_generation_equals_serial(k):
+    """build()'s code generation on several host threads (every tree at a
+    provisional address, the layout, every tree again at its final address)
+    gives the serial generator's bytes and offsets exactly."""
+    b_ops, u_ops = OPSETS[k]
+    o = srhip.Options(binary_operators=b_ops, unary_operators=u_ops)
+    flat = srhip.flatten(srhip.random_population(1500, o, 7, np.float32, seed=71 + k), o, dtype=np.float32)
+    for fast, memc in ((True, False), (False, False), (True, True)):
+        code_t, _, offs_t = jit_compile(flat, fast=fast, memc=memc)
+        code_p, text_p, offs_p = jit_compile(flat, fast=fast, memc=memc, text=False)
+        assert text_p == ""
+        assert offs_p == offs_t and code_p == code_t
+
+
 def test_every_tree_of_config2_compiles():
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     trees = srhip.random_population(1000, o, 5, np.float32, seed=0)
