@@ -21,6 +21,7 @@ import pytest
 
 import oracle
 import srhip
+from srhip import Node
 from srhip import constants as K
 
 pytestmark = pytest.mark.gpu
@@ -216,3 +217,26 @@ def test_float64_grad_tree_code_other_losses(gpu_ctx, loss):
     assert sel.sum() > 200
     err = np.abs(g1[sel] - g0[sel])
     assert np.all(err <= 1e-10 * S[sel] + 1e-300), float(np.max(err / (S[sel] + 1e-300)))
+
+
+def test_float64_grad_tree_code_many_constants_fall_back(gpu_ctx):
+    """A Float64 tree with more constants than accumulators runs on the
+    interpreter, the others as tree code, in the same call."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(3)
+    X = rng.standard_normal((3, 1000))
+    y = X[0] * 2 - 1
+    big = Node(val=0.5)
+    for k in range(20):  # 21 constants
+        big = o.make_binary("+", o.make_binary("*", big, Node(val=1.0 + 0.01 * k)), Node("x1"))
+    trees = srhip.random_population(300, o, 3, np.float64, seed=4) + [big]
+    s1, g1, _, ok1, info, ntc, prog = run(gpu_ctx, trees, o, X, y, None, True)
+    s0, g0, _, ok0, _, _, _ = run(gpu_ctx, trees, o, X, y, None, False)
+    assert info["nrejected"] >= 1 and info["ntrees"] >= 280
+    assert np.array_equal(ok1, ok0)
+    co = prog.flat.const_off
+    np.testing.assert_array_equal(g1[co[-2]:co[-1]], g0[co[-2]:co[-1]])  # the big tree: same kernel
+    ok_c = np.repeat(ok1, np.diff(co))
+    S, _ = oracle_terms(trees, o, X, y, None)
+    sel = ok_c & np.isfinite(S)
+    assert np.all(np.abs(g1[sel] - g0[sel]) <= 1e-10 * S[sel] + 1e-300)
