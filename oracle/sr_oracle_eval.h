@@ -353,7 +353,7 @@ static inline double CAT(elem_loss_d, SFX)(int loss, const double* p, double r) 
     case SRHIP_LOSS_L1EPSINS: return ar > p[0] ? ar - p[0] : 0.0;
     case SRHIP_LOSS_L2EPSINS: { double e = ar > p[0] ? ar - p[0] : 0.0; return e * e; }
     case SRHIP_LOSS_QUANTILE: return r >= 0 ? p[0] * r : (p[0] - 1.0) * r;
-    case SRHIP_LOSS_PERIODIC: return 1.0 - cos(2.0 * 3.14159265358979323846 * r / p[0]);
+    case SRHIP_LOSS_PERIODIC: return 1.0 - cos(r * (2.0 * 3.14159265358979323846 / p[0])); /* k = 2π/c stored, 1 - cos(r·k) */
     case SRHIP_LOSS_LOGITDIST: return ar + 2.0 * log1p(exp(-ar)) - 1.38629436111989061883;
   }
   return NAN;

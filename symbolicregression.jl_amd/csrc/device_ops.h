@@ -470,7 +470,8 @@ __device__ __forceinline__ double elem_loss_param(int kind, double p, double r) 
     case SRHIP_LOSS_L1EPSINS: return ar > p ? ar - p : 0.0;
     case SRHIP_LOSS_L2EPSINS: { double e = ar > p ? ar - p : 0.0; return e * e; }
     case SRHIP_LOSS_QUANTILE: return r >= 0.0 ? p * r : (p - 1.0) * r;
-    case SRHIP_LOSS_PERIODIC: return 1.0 - m_cos(6.28318530717958647692 * r / p);
+    // LossFunctions' PeriodicLoss stores k = 2π/c and evaluates 1 - cos(r·k)
+    case SRHIP_LOSS_PERIODIC: return 1.0 - m_cos(r * (6.28318530717958647692 / p));
   }
   return qnan<double>();
 }
