@@ -1097,7 +1097,7 @@ void rerun_bailed(srhip_ctx* c, const srhip_program* p, jit::Module* jm, const E
   if constexpr (std::is_same<T, float>::value) {
     hipStream_t s = c->stream;
     const int nj = p->nlist_j;
-    if (!jit::can_bail()) return;  // no routine hands a tile back: the finalize copied the counters
+    if (!jit::module_bails(jm)) return;  // no routine hands a tile back: the finalize copied the counters
     std::vector<uint32_t> flags((size_t)nj + 2);
     HIP_CHECK(hipMemcpyAsync(flags.data(), jit::bail_flags(jm), flags.size() * sizeof(uint32_t),
                              hipMemcpyDeviceToHost, s));
@@ -1410,7 +1410,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   // the previous call left them clean; one clearing launch only after a new
   // buffer, an interrupted call or a path that leaves them set (gradients,
   // tree code that can hand tiles back)
-  const bool jit_bail = jm != nullptr && jit::can_bail();
+  const bool jit_bail = jm != nullptr && jit::module_bails(jm);
   if (mode == MODE_LOSS) {
     const size_t need = std::max<size_t>(nslots, 1) * sizeof(uint32_t);
     if (c->fail.bytes < need) {

@@ -461,6 +461,56 @@ __device__ __forceinline__ double lp_pow_t(double ar, double p) {
   else return m_pow(ar, p);
 }
 
+// cos(x) in Float64 for |x| <= kCwCosMax: x - n·π/2 by Cody-Waite in three
+// parts (33 + 33 + 53 bits of π/2, exact products for |n| < 2^20), then the
+// quadrant's cos / sin polynomial (Taylor to r^18 / r^19 on |r| <= π/4,
+// truncation below 2^-56). A few ulp of a double, so one rounding to Float32
+// matches the correctly rounded value but within ~2^-28 of a boundary. No
+// large-argument reduction: `big` reports |x| > kCwCosMax (the value is then
+// unspecified) — the Float32 Periodic loss routine of the tree code hands
+// such a tile back to the interpreter, which takes OCML's cos there.
+constexpr double kCwCosMax = 1.6e6;  // < 2^20 · π/2
+__device__ __forceinline__ double cw_cos(double x, bool& big) {
+  big = !(__builtin_fabs(x) <= kCwCosMax);
+  const double n = __builtin_rint(x * 6.36619772367581382433e-01);  // 2/π
+  double r = __builtin_fma(-n, 1.57079632673412561417e+00, x);
+  r = __builtin_fma(-n, 6.07710050630396597660e-11, r);
+  r = __builtin_fma(-n, 2.02226624879595063154e-21, r);
+  const double z = r * r;
+  double c = 1.5619206968586225e-16;  // 1/18!
+  c = __builtin_fma(c, z, -4.7794773323873853e-14);
+  c = __builtin_fma(c, z, 1.1470745597729725e-11);
+  c = __builtin_fma(c, z, -2.0876756987868099e-09);
+  c = __builtin_fma(c, z, 2.7557319223985891e-07);
+  c = __builtin_fma(c, z, -2.4801587301587302e-05);
+  c = __builtin_fma(c, z, 1.3888888888888889e-03);
+  c = __builtin_fma(c, z, -4.1666666666666664e-02);
+  c = __builtin_fma(c, z, 0.5);
+  c = __builtin_fma(-c, z, 1.0);
+  double sn = 8.2206352466243295e-18;  // 1/19!
+  sn = __builtin_fma(sn, z, -2.8114572543455206e-15);
+  sn = __builtin_fma(sn, z, 7.6471637318198164e-13);
+  sn = __builtin_fma(sn, z, -1.6059043836821613e-10);
+  sn = __builtin_fma(sn, z, 2.5052108385441720e-08);
+  sn = __builtin_fma(sn, z, -2.7557319223985893e-06);
+  sn = __builtin_fma(sn, z, 1.9841269841269841e-04);
+  sn = __builtin_fma(sn, z, -8.3333333333333332e-03);
+  sn = __builtin_fma(sn, z, 1.6666666666666666e-01);
+  sn = __builtin_fma(-sn * z, r, r);
+  const int q = (int)((long long)n & 3);
+  const double v = (q & 1) ? sn : c;
+  return (q == 1 || q == 2) ? -v : v;
+}
+// Float32 data's PeriodicLoss value, 1 - cos(r·k), k = 2π/c (LossFunctions'
+// PeriodicLoss stores k); the interpreter's and, but for a tile with some
+// |r·k| > kCwCosMax (handed back), the tree code's
+__device__ __forceinline__ double periodic_f32(double r, double p) {
+  const double x = r * (6.28318530717958647692 / p);
+  bool big;
+  const double c = cw_cos(x, big);
+  return 1.0 - (big ? m_cos(x) : c);
+}
+
 template <typename T>
 __device__ __forceinline__ double elem_loss_param(int kind, double p, double r) {
   const double ar = __builtin_fabs(r);
@@ -471,7 +521,9 @@ __device__ __forceinline__ double elem_loss_param(int kind, double p, double r) 
     case SRHIP_LOSS_L2EPSINS: { double e = ar > p ? ar - p : 0.0; return e * e; }
     case SRHIP_LOSS_QUANTILE: return r >= 0.0 ? p * r : (p - 1.0) * r;
     // LossFunctions' PeriodicLoss stores k = 2π/c and evaluates 1 - cos(r·k)
-    case SRHIP_LOSS_PERIODIC: return 1.0 - m_cos(r * (6.28318530717958647692 / p));
+    case SRHIP_LOSS_PERIODIC:
+      if constexpr (std::is_same<T, float>::value) return periodic_f32(r, p);
+      else return 1.0 - m_cos(r * (6.28318530717958647692 / p));
   }
   return qnan<double>();
 }

@@ -245,6 +245,14 @@ def routine_list():
             continue
         imm = ("const double imm = __builtin_bit_cast(double, ((unsigned long long)s.s_kh << 32) | "
                "(unsigned long long)s.s_k); ")
+        if name == "PERIODIC":  # Cody-Waite cos; a row beyond it hands the tile back (the bail flag)
+            body = (imm + "bool big = false; " +
+                    rows_serial("bool b; const double x = (double)s.a[r] * (6.28318530717958647692 / imm); "
+                                "const double c = dev::cw_cos(x, b); big = big || b; s.a[r] = (float)(1.0 - c);") +
+                    " const unsigned long long fl = __builtin_amdgcn_ballot_w64(big);"
+                    " s.s_flag = (unsigned)fl; s.s_flag_hi = (unsigned)(fl >> 32);")
+            rs.append((f"l_{name.lower()}", body, True))
+            continue
         rs.append((f"l_{name.lower()}",
                    imm + rows_serial(f"s.a[r] = dev::elem_loss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"),
                    False))

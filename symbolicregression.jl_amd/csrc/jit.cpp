@@ -94,6 +94,12 @@ uint32_t fbits(float f) {
 
 // Derived columns of a build (jit.h Columns): the column of u(x_f), -1 when
 // u(x_f) is not derived
+// the loss routine of the tile tail can hand a tile back (the Float32
+// Periodic routine's Cody-Waite range, gen_jit.py)
+bool loss_bails(int loss) {
+  return loss > SRHIP_LOSS_L2 && loss < SRHIP_NUM_LOSSES && kLossRoutine[loss] >= 0 && kRoutineTrig[kLossRoutine[loss]];
+}
+
 struct DerivedMap {
   const Columns* cols = nullptr;
   int col(int op, int f) const {
@@ -341,6 +347,8 @@ struct Gen {
         if (q.k == O_VAL) { ops[q.v].consumer = i; ops[q.v].cpos = s; }
       }
     }
+    // a loss routine that hands a tile back (Float32 Periodic beyond its Cody-Waite range)
+    if (!out && loss_bails(loss)) has_trig = true;
     if (memc) {
       cpcs.clear();
       for (const IrOp& o : ops) {
@@ -984,6 +992,11 @@ struct Gen {
     as.sop1(SOP1_MOV, "s_mov_b32", S_K, K((uint32_t)lparam), "s" + std::to_string(S_K));
     as.sop1(SOP1_MOV, "s_mov_b32", S_KH, K((uint32_t)(lparam >> 32)), "s" + std::to_string(S_KH));
     call_precise(kLossRoutine[loss]);
+    if (loss_bails(loss)) {  // a row beyond the routine's range: the tree goes back to the interpreter
+      as.sopc(SOPC_LG_U64, "s_cmp_lg_u64", S(S_FLAG), K(0),
+              "s[" + std::to_string(S_FLAG) + ":" + std::to_string(S_FLAG + 1) + "]");
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_bail);
+    }
     mov_block_reg(VY, VA);
     const int L_unw = as.label(), L_sum = as.label();
     as.sopc(SOPC_EQ_U32, "s_cmp_eq_u32", S(S_WOFF), K(0));
@@ -1151,6 +1164,7 @@ struct ModulePart {
 struct Module {
   Columns cols;
   bool memc = false;
+  bool bails = false;  // its tree code can hand a tree back (rerun_bailed reads the flags)
   bool out = false;  // per-row output code: fn runs sr_jit_out(_m)
   std::vector<ModulePart> parts;
   uint32_t* d_bail = nullptr;  // [nslots + 2]: bail flags of all slots, bail count, PRECISE redo count
@@ -1158,11 +1172,16 @@ struct Module {
 };
 
 bool available() { return templates().ok; }
+// an operator routine that hands tiles back (gen_jit.py TRIG_BAIL): every module's
 bool can_bail() {
-  for (int k = 0; k < kNumRoutines; ++k)
-    if (kRoutineTrig[k]) return true;
+  for (int k = 0; k < kNumRoutines; ++k) {
+    bool is_loss = false;
+    for (int l = 0; l < SRHIP_NUM_LOSSES; ++l) is_loss = is_loss || kLossRoutine[l] == k;
+    if (kRoutineTrig[k] && !is_loss) return true;
+  }
   return false;
 }
+bool module_bails(const Module* m) { return m && m->bails; }
 const char* unavailable_reason() { return templates().why.c_str(); }
 
 // Host threads for code generation (SRHIP_JIT_THREADS, default min(16,
@@ -1472,6 +1491,7 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
   Module* m = new Module();
   m->cols = cols;
   m->memc = opt.memc;
+  m->bails = can_bail() || (!opt.out && loss_bails(opt.loss));
   m->out = opt.out;
   try {
     for (Chunk& ch : chunks) {

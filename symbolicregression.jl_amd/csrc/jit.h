@@ -83,6 +83,9 @@ bool available();
 // some routine can hand a tile back to the interpreter (sin/cos built with
 // TRIG_BAIL in gen_jit.py); false: the bail flags never need reading
 bool can_bail();
+// this module's tree code can hand a tree back: can_bail(), or its loss
+// routine can (Float32 Periodic beyond the routine's Cody-Waite range)
+bool module_bails(const Module* m);
 const char* unavailable_reason();
 
 // Compile the trees `cand` (tree ids, in list order) of `cb`. Trees that

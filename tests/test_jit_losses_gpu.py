@@ -7,11 +7,11 @@ of Float32 tree code, weighted and unweighted.
 The parametric losses hold Float64 fields, so Julia evaluates them in
 Float64 for a Float32 residual (device_ops.h elem_loss, the oracle likewise):
 PeriodicLoss's cos(2πr/c) of a large residual made the Float32 evaluation
-0.6 % off before (round 4). L1, LP (exp(p ln|r|) in Float64, device_ops.h
-lp_pow), Huber, the epsilon-insensitive losses, Quantile, LogCosh and
-LogitDist run as tree code; Periodic (Float64 cos of an unbounded argument)
-keeps the interpreter (its routine's registers exceed what tree code leaves
-it), which this checks too.
+0.6 % off before (round 4). Every loss runs as tree code: L1, LP (exp(p
+ln|r|) in Float64, device_ops.h lp_pow), Huber, the epsilon-insensitive
+losses, Quantile, LogCosh, LogitDist and, since round 5, Periodic (a
+Cody-Waite Float64 cos, device_ops.h cw_cos; a tile with some |r·k| beyond
+its range hands the tree back to the interpreter, which this checks too).
 
 Per loss: the tree code ran or not (srhip_last_tree_code), did_succeed equals
 the interpreter's and the oracle's on every tree, and losses agree with the
@@ -31,7 +31,7 @@ pytestmark = pytest.mark.gpu
 LOSSES = [
     (srhip.L1DistLoss(), True), (srhip.LPDistLoss(1.7), True), (srhip.LPDistLoss(3.0), True),
     (srhip.HuberLoss(0.8), True), (srhip.L1EpsilonInsLoss(0.3), True), (srhip.L2EpsilonInsLoss(0.3), True),
-    (srhip.QuantileLoss(0.3), True), (srhip.PeriodicLoss(2.0), False),
+    (srhip.QuantileLoss(0.3), True), (srhip.PeriodicLoss(2.0), True),
     (srhip.LogCoshLoss(), True), (srhip.LogitDistLoss(), True),
 ]
 
@@ -81,6 +81,38 @@ def test_tree_code_losses_match_oracle(gpu_ctx, loss, jit):
         bad = np.flatnonzero(m & ~(rel <= 1e-5))
         assert bad.size == 0, (name, bad[:10], float(np.nanmax(rel[m])))
         assert m.sum() > 300
+
+
+def test_periodic_tree_code_hands_large_residuals_back(gpu_ctx):
+    """Float32 Periodic: trees whose residuals leave the routine's Cody-Waite
+    range on some rows (x1·1e7) hand their tree back — counted, then rerun by
+    the interpreter, so their losses are the interpreter's bit for bit — the
+    others stay tree code; all within 1e-5 of the oracle."""
+    o, X, y, w, trees = _problem()
+    big = [o.make_binary("*", srhip.Node("x1"), srhip.Node(val=np.float32(v))) for v in (1e7, -3e6, 2.5e6)]
+    trees = trees[:300] + big
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    loss = srhip.PeriodicLoss(2.0)
+    progs = {}
+    for mode in ("1", "0"):
+        os.environ["SRHIP_JIT"] = mode
+        try:
+            progs[mode] = srhip.Program(gpu_ctx, flat, np.float32)
+        finally:
+            del os.environ["SRHIP_JIT"]
+    ds = srhip.DeviceDataset(gpu_ctx, X, y)
+    s, wsum, ok = progs["1"].eval_loss(ds, loss.kind, loss.params)
+    assert gpu_ctx.last_tree_code() > 250
+    assert gpu_ctx.last_bailed() >= 3
+    si, _, oki = progs["0"].eval_loss(ds, loss.kind, loss.params)
+    assert np.array_equal(ok, oki)
+    np.testing.assert_array_equal(s[-3:], si[-3:])  # rerun by the interpreter
+    _, rl, rok = oracle.eval_loss_batch(flat, X, y, None, loss.kind, loss.params, dtype=np.float32, nthreads=16)
+    assert np.array_equal(ok, rok)
+    m = ok & np.isfinite(rl)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        rel = np.abs(s / wsum - rl) / np.abs(rl)
+    assert np.all(rel[m] <= 1e-5), float(np.nanmax(rel[m]))
 
 
 def _dloss(loss, r):
