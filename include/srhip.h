@@ -338,9 +338,9 @@ int32_t srhip_optimize_constants_cb(const srhip_trees* trees, int32_t dtype, con
  * (symbolicregression.jl_amd/csrc/jit.cpp for Float32, jit64.cpp for
  * Float64; SRHIP_JIT=0 turns it off, =1 on for every size). Tree code
  * computes exactly what the interpreter computes: eval_loss with L2 and with
- * the elementwise losses that have a loss routine (Float32: all but
- * Periodic; Float64: every loss — the others run
- * interpreted), and the per-row outputs of eval_tree_array. This reports:
+ * every elementwise loss (Float32 Periodic: a tile whose |r·2π/c| leaves
+ * its routine's Cody-Waite range hands the tree back to the interpreter),
+ * and the per-row outputs of eval_tree_array. This reports:
  * trees compiled, of which with a guarded Float32-transcendental path, code
  * bytes, host code generation and code-object load times (ms). All zero for
  * an interpreted program. */
