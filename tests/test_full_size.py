@@ -109,3 +109,54 @@ def test_config3_full_nan_heavy_f64(gpu_ctx):
     _check_losses(trees, o, X, y, np.float64, losses, ok, ref_l, ref_ok, 1e-5, name="config3_1e-5", strict=True)
     n, _ = _check_losses(trees, o, X, y, np.float64, losses, ok, ref_l, ref_ok, 1e-10, name="config3")
     assert 0.05 < ok.mean() < 0.95 and n > 200
+
+
+def test_config3_full_f64_gradients(gpu_ctx):
+    """Config #3 at full size through the Float64 gradient tree code (round 5):
+    ∂L/∂c of every constant of the 4096 trees × 100k rows against the
+    forward-mode interpreter — did_succeed and the NaN pattern identical on
+    every constant, losses within 1e-12, and on every 8th tree each constant
+    within 1e-10 of Σ_rows |2r·∂ŷ/∂c| (the Float64 oracle's terms)."""
+    import os
+
+    from srhip import constants as K
+    o = srhip.Options(binary_operators=["+", "-", "*", "/", "^"],
+                      unary_operators=["safe_log", "safe_sqrt", "cos", "exp"])
+    trees = srhip.random_population(4096, o, 5, np.float64, seed=3)
+    rng = np.random.default_rng(4)
+    X = rng.uniform(-3, 3, (5, 100_000))
+    y = rng.standard_normal(100_000)
+    flat = srhip.flatten(trees, o, dtype=np.float64)
+    res = {}
+    for mode in ("1", "0"):
+        os.environ["SRHIP_GJIT"] = mode
+        try:
+            ds = srhip.DeviceDataset(gpu_ctx, X, y)
+            prog = srhip.Program(gpu_ctx, flat, np.float64)
+            s, g, _, ok = prog.eval_loss_grad(ds, K.LOSS["L2"])
+            res[mode] = (s.copy(), g.copy(), ok.copy(), gpu_ctx.last_tree_code())
+        finally:
+            del os.environ["SRHIP_GJIT"]
+    (s1, g1, ok1, n1), (s0, g0, ok0, n0) = res["1"], res["0"]
+    assert n1 > 4000 and n0 == 0
+    assert np.array_equal(ok1, ok0)
+    assert np.array_equal(np.isnan(g1), np.isnan(g0))
+    m = ok1 & np.isfinite(s0) & (s0 != 0)
+    assert np.all(np.abs(s1[m] - s0[m]) <= 1e-12 * np.abs(s0[m]))
+    co = flat.const_off
+    checked = 0
+    for t in range(0, len(trees), 8):
+        nc = co[t + 1] - co[t]
+        if nc == 0 or not ok1[t]:
+            continue
+        k, a, c = flat.tree(t)
+        with np.errstate(all="ignore"):
+            out, gr, okt = oracle.eval_grad_consts(k, a, np.asarray(c, dtype=np.float64), X, nc)
+            if not okt:
+                continue
+            S = np.abs(2.0 * (out - y) * gr).sum(axis=1)
+        sl = slice(co[t], co[t + 1])
+        fin = np.isfinite(S) & (S < 1e100)
+        assert np.all(np.abs(g1[sl][fin] - g0[sl][fin]) <= 1e-10 * S[fin] + 1e-300), t
+        checked += int(fin.sum())
+    assert checked > 100
