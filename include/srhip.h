@@ -124,7 +124,13 @@ extern "C" {
 #define SRHIP_LOSS_QUANTILE 7  /* r>=0 ? tau*r : (tau-1)*r,  params[0] = tau */
 #define SRHIP_LOSS_PERIODIC 8  /* 1 - cos(2πr/c), params[0] = c             */
 #define SRHIP_LOSS_LOGITDIST 9 /* -log(4 e^r / (1+e^r)^2)                   */
-#define SRHIP_NUM_LOSSES 10
+/* LPDistLoss{n} with an INTEGER n (LPDistLoss(3), not LPDistLoss(3.0)):
+ * |r|^n by Julia's T^Integer — Float32 stays Float32 (|r|*|r|*|r| for n = 3,
+ * else Float64 power by squaring rounded once), Float64 by compensated power
+ * by squaring; params[0] = n, integral with |n| < 2^31 (else INVALID).
+ * Interpreted only (no tree code). */
+#define SRHIP_LOSS_LPINT 10
+#define SRHIP_NUM_LOSSES 11
 
 typedef struct srhip_ctx srhip_ctx;
 typedef struct srhip_dataset srhip_dataset;

@@ -46,6 +46,8 @@ def load(variant: str = "simd"):
         g.restype = None
     L.oracle_elem_loss_f64.argtypes = [C.c_int, vp, C.c_double, C.c_double]
     L.oracle_elem_loss_f64.restype = C.c_double
+    L.oracle_elem_loss_f32.argtypes = [C.c_int, vp, C.c_float, C.c_float]
+    L.oracle_elem_loss_f32.restype = C.c_float
     for sfx in ("f32", "f64"):
         f = getattr(L, f"oracle_eval_grad_consts_{sfx}")
         f.argtypes = [vp, vp, vp, i32, vp, i64, i32, vp, vp]
@@ -73,6 +75,14 @@ def binop(op: int, x, y, dtype=np.float32):
 def unop(op: int, x, dtype=np.float32):
     L = load()
     return (L.oracle_unop_f32 if _sfx(dtype) == "f32" else L.oracle_unop_f64)(op, x)
+
+
+def elem_loss(loss: int, params, yhat, y, dtype=np.float32):
+    """One elementwise loss value in T (sr_oracle_eval.h elem_loss)."""
+    L = load()
+    p = np.asarray(list(params) if params is not None else [0.0], dtype=np.float64)
+    f = L.oracle_elem_loss_f32 if _sfx(dtype) == "f32" else L.oracle_elem_loss_f64
+    return f(loss, _p(p), yhat, y)
 
 
 def julia_X(X: np.ndarray, dtype) -> np.ndarray:

@@ -54,6 +54,65 @@ static inline double oracle_noise_f64(double v) {
   return v * (1.0 + g_noise_eps * u);
 }
 
+/* |r|^n of LPDistLoss{n} with an integer n (SRHIP_LOSS_LPINT): Julia's
+ * ^(::Float32, ::Integer) and ^(::Float64, ::Integer), Base math.jl (Julia
+ * 1.9+: Float32 keeps literal_pow's x*x*x for n = 3 and (1/x)^2 for n = -2,
+ * else Base.power_by_squaring in Float64 rounded once; Float64 by pow_body,
+ * power by squaring with each product's error carried by fma). Not in
+ * /root/reference (Julia's Base); restated from its published source, parity
+ * unpinned. */
+static double oracle_pbs(double x, long long p) {
+  if (p == 0) return 1.0;
+  if (p == 1) return x;
+  if (p == 2) return x * x;
+  int t = __builtin_ctzll((unsigned long long)p) + 1;
+  p >>= t;
+  while ((t -= 1) > 0) x = x * x;
+  double y = x;
+  while (p > 0) {
+    t = __builtin_ctzll((unsigned long long)p) + 1;
+    p >>= t;
+    while ((t -= 1) >= 0) x = x * x;
+    y = y * x;
+  }
+  return y;
+}
+static float ipow_f32(float x, long long n) {
+  if (n == -2) { float i = 1.0f / x; return i * i; }
+  if (n == 3) return x * x * x;
+  if (n < 0) return (float)oracle_pbs(1.0 / (double)x, -n);
+  return (float)oracle_pbs((double)x, n);
+}
+static double ipow_f64(double x, long long n) {
+  double y = 1.0, xnlo = 0.0, ynlo = 0.0;
+  if (n == 0) return 1.0;
+  if (n == 3) return x * x * x;
+  if (n < 0) {
+    double rx = 1.0 / x;
+    if (n == -2) return rx * rx;
+    if (isfinite(x)) xnlo = -fma(x, rx, -1.0) * rx;
+    x = rx;
+    n = -n;
+  }
+  while (n > 1) {
+    if (n & 1) {
+      double err = fma(y, xnlo, x * ynlo);
+      double xy = x * y;
+      ynlo = fma(x, y, -xy);
+      y = xy;
+      ynlo += err;
+    }
+    double err = x * 2 * xnlo;
+    double xx = x * x;
+    xnlo = fma(x, x, -xx);
+    x = xx;
+    xnlo += err;
+    n >>= 1;
+  }
+  double err = fma(y, xnlo, x * ynlo);
+  return (isfinite(x) && isfinite(err)) ? fma(x, y, err) : x * y;
+}
+
 /* ---------------- T = float ---------------- */
 #define T float
 #define TNOISE(v) (v)

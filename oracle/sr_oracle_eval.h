@@ -365,6 +365,7 @@ static inline T CAT(elem_loss, SFX)(int loss, const double* p, T yhat, T y) {
   T r = yhat - y;
   if (loss == SRHIP_LOSS_L2) return r * r;
   if (loss == SRHIP_LOSS_L1) return FABS(r);
+  if (loss == SRHIP_LOSS_LPINT) return CAT(ipow, SFX)(FABS(r), (long long)p[0]); /* T^Integer in T */
   return (T)CAT(elem_loss_d, SFX)(loss, p, (double)r);
 }
 

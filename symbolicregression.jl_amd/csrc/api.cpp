@@ -1249,7 +1249,7 @@ jit::Module64* module64(const srhip_program* p, int kind, double lparam) {
   if (!p->jit64 || p->nlist_j == 0) return nullptr;
   if (kind == SRHIP_LOSS_L2) return p->jit64;
   static const bool on = [] { const char* e = std::getenv("SRHIP_JIT64_EXTRA"); return !(e && e[0] == '0'); }();
-  if (!on || kind < -2 || kind >= SRHIP_NUM_LOSSES) return nullptr;
+  if (!on || kind < -2 || kind >= SRHIP_NUM_LOSSES || (kind >= 0 && !jit::has_loss_routine64(kind))) return nullptr;
   uint64_t bits = 0;
   if (kind != -2) std::memcpy(&bits, &lparam, 8);
   for (const auto& l : p->jit64_loss)
@@ -2409,16 +2409,24 @@ int32_t srhip_program_set_constants(srhip_program* prog, const void* consts) {
   });
 }
 
+// A SRHIP_LOSS_* kind and its parameter: UNSUPPORTED beyond the table,
+// INVALID without a needed parameter or for LPDistLoss{n} with n not an integer
+// of magnitude below 2^31
+static void check_loss(int32_t kind, const double* params) {
+  if (kind < 0 || kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
+  const bool needs = kind != SRHIP_LOSS_L2 && kind != SRHIP_LOSS_L1 && kind != SRHIP_LOSS_LOGCOSH &&
+                     kind != SRHIP_LOSS_LOGITDIST;
+  if (needs && !params) throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
+  if (kind == SRHIP_LOSS_LPINT && !(params[0] == std::trunc(params[0]) && std::fabs(params[0]) < 2147483648.0))
+    throw Error(SRHIP_ERR_INVALID, "LPDistLoss{n} (SRHIP_LOSS_LPINT) needs an integer n");
+}
+
 int32_t srhip_eval_loss(srhip_dataset* ds, const srhip_program* prog, int32_t loss_kind,
                         const double* loss_params, const int64_t* row_idx, int64_t nidx,
                         double* out_loss_sum, double* out_weight_sum, uint8_t* out_ok) {
   return guarded([&] {
     check_program_vs_dataset(ds, prog);
-    if (loss_kind < 0 || loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
-    const bool needs_param = loss_kind == SRHIP_LOSS_LP || loss_kind == SRHIP_LOSS_HUBER ||
-                             loss_kind == SRHIP_LOSS_L1EPSINS || loss_kind == SRHIP_LOSS_L2EPSINS ||
-                             loss_kind == SRHIP_LOSS_QUANTILE || loss_kind == SRHIP_LOSS_PERIODIC;
-    if (needs_param && !loss_params) throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
+    check_loss(loss_kind, loss_params);
     std::lock_guard<std::mutex> lk(prog->ctx->mu);
     HIP_CHECK(hipSetDevice(prog->ctx->device));
     if (ds->dtype == SRHIP_F32)
@@ -2432,11 +2440,7 @@ int32_t srhip_eval_loss_packed(srhip_dataset* ds, srhip_program* prog, int32_t l
   return guarded([&] {
     check_program_vs_dataset(ds, prog);
     if (!d_out) throw Error(SRHIP_ERR_INVALID, "null output");
-    if (loss_kind < 0 || loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
-    const bool needs_param = loss_kind == SRHIP_LOSS_LP || loss_kind == SRHIP_LOSS_HUBER ||
-                             loss_kind == SRHIP_LOSS_L1EPSINS || loss_kind == SRHIP_LOSS_L2EPSINS ||
-                             loss_kind == SRHIP_LOSS_QUANTILE || loss_kind == SRHIP_LOSS_PERIODIC;
-    if (needs_param && !loss_params) throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
+    check_loss(loss_kind, loss_params);
     hipPointerAttribute_t at;
     if (hipPointerGetAttributes(&at, d_out) != hipSuccess || at.type != hipMemoryTypeDevice)
       throw Error(SRHIP_ERR_INVALID, "d_out is not device memory");
@@ -2488,10 +2492,7 @@ int32_t srhip_eval_loss_grad(srhip_dataset* ds, const srhip_program* prog, int32
                              double* out_weight_sum, uint8_t* out_ok) {
   return guarded([&] {
     check_program_vs_dataset(ds, prog);
-    if (loss_kind < 0 || loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
-    if (loss_kind != SRHIP_LOSS_L2 && loss_kind != SRHIP_LOSS_L1 && loss_kind != SRHIP_LOSS_LOGCOSH &&
-        loss_kind != SRHIP_LOSS_LOGITDIST && !loss_params)
-      throw Error(SRHIP_ERR_INVALID, "loss needs a parameter");
+    check_loss(loss_kind, loss_params);
     std::lock_guard<std::mutex> lk(prog->ctx->mu);
     HIP_CHECK(hipSetDevice(prog->ctx->device));
     auto* p = const_cast<srhip_program*>(prog);  // gradient programs are built lazily
@@ -2979,7 +2980,7 @@ int32_t srhip_optimize_constants_batch(srhip_ctx* ctx, srhip_dataset* ds, const 
   return guarded([&] {
     if (!ds) throw Error(SRHIP_ERR_INVALID, "null dataset");
     if (!opts) throw Error(SRHIP_ERR_INVALID, "null options");
-    if (opts->loss_kind < 0 || opts->loss_kind >= SRHIP_NUM_LOSSES) throw Error(SRHIP_ERR_UNSUPPORTED, "unsupported loss");
+    check_loss(opts->loss_kind, opts->loss_params);
     t_copt = CoptProfile();
     const auto t0 = std::chrono::steady_clock::now();
     copt::Problem pb = make_problem(trees, ds->dtype);

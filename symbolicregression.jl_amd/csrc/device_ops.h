@@ -511,6 +511,63 @@ __device__ __forceinline__ double periodic_f32(double r, double p) {
   return 1.0 - (big ? m_cos(x) : c);
 }
 
+// |r|^n of LPDistLoss{n} for an INTEGER n (SRHIP_LOSS_LPINT). Julia's
+// ^(::Float32, ::Integer) and ^(::Float64, ::Integer) (Base math.jl, Julia
+// 1.9+; earlier Julias differ, so parity is unpinned): Float32 stays in
+// Float32 — 1/x squared for n = -2, x*x*x for n = 3 (literal_pow's), otherwise
+// Base.power_by_squaring in Float64 (of 1/x for n < 0) rounded once; Float64
+// by pow_body: power by squaring carrying each product's error (two_mul by
+// fma), x*x*x for n = 3, (1/x)^2 for n = -2.
+__device__ __forceinline__ double pow_by_squaring(double x, long long p) {  // p >= 0
+  if (p == 0) return 1.0;
+  if (p == 1) return x;
+  if (p == 2) return x * x;
+  int t = __builtin_ctzll((unsigned long long)p) + 1;
+  p >>= t;
+  while (--t > 0) x = x * x;
+  double y = x;
+  while (p > 0) {
+    t = __builtin_ctzll((unsigned long long)p) + 1;
+    p >>= t;
+    while (--t >= 0) x = x * x;
+    y = y * x;
+  }
+  return y;
+}
+__device__ __forceinline__ float ipow(float x, long long n) {
+  if (n == -2) { const float i = 1.0f / x; return i * i; }
+  if (n == 3) return x * x * x;
+  if (n < 0) return (float)pow_by_squaring(1.0 / (double)x, -n);
+  return (float)pow_by_squaring((double)x, n);
+}
+__device__ __forceinline__ double ipow(double x, long long n) {
+  if (n == 0) return 1.0;
+  if (n == 3) return x * x * x;
+  double xlo = 0.0, y = 1.0, ylo = 0.0;
+  if (n < 0) {
+    const double rx = 1.0 / x;
+    if (n == -2) return rx * rx;
+    if (__builtin_isfinite(x)) xlo = -__builtin_fma(x, rx, -1.0) * rx;
+    x = rx;
+    n = -n;
+  }
+  while (n > 1) {
+    if (n & 1) {
+      const double err = __builtin_fma(y, xlo, x * ylo);
+      const double h = x * y;
+      ylo = __builtin_fma(x, y, -h) + err;
+      y = h;
+    }
+    const double err = x * 2.0 * xlo;
+    const double h = x * x;
+    xlo = __builtin_fma(x, x, -h) + err;
+    x = h;
+    n >>= 1;
+  }
+  const double err = __builtin_fma(y, xlo, x * ylo);
+  return (__builtin_isfinite(x) && __builtin_isfinite(err)) ? __builtin_fma(x, y, err) : x * y;
+}
+
 template <typename T>
 __device__ __forceinline__ double elem_loss_param(int kind, double p, double r) {
   const double ar = __builtin_fabs(r);
@@ -536,6 +593,7 @@ __device__ __forceinline__ T elem_loss(int kind, double p, T yhat, T y) {
     case SRHIP_LOSS_L1: return ar;
     case SRHIP_LOSS_LOGCOSH: return ar + m_log1p(m_exp(T(-2) * ar)) - T(0.69314718055994530942);
     case SRHIP_LOSS_LOGITDIST: return ar + T(2) * m_log1p(m_exp(-ar)) - T(1.38629436111989061883);
+    case SRHIP_LOSS_LPINT: return ipow(ar, (long long)p);  // T^Integer stays in T
   }
   return (T)elem_loss_param<T>(kind, p, (double)r);
 }
@@ -615,6 +673,10 @@ __device__ __forceinline__ T elem_dloss(int kind, double p, T yhat, T y) {
     case SRHIP_LOSS_L1: return sg;
     case SRHIP_LOSS_LOGCOSH: return m_tanh(r);
     case SRHIP_LOSS_LOGITDIST: return m_tanh(T(0.5) * r);
+    case SRHIP_LOSS_LPINT: {  // LossFunctions' deriv: P * abs(r)^(P-1) * sign(r), in T
+      const long long n = (long long)p;
+      return T(n) * ipow(m_fabs(r), n - 1) * sg;
+    }
   }
   const double rd = (double)r, ar = __builtin_fabs(rd), sd = (double)sg;
   switch (kind) {

@@ -111,6 +111,7 @@ __device__ __forceinline__ T tile_loss_any(int lk, const T (&acc)[R], const T (&
     case SRHIP_LOSS_L2EPSINS: return tile_loss<SRHIP_LOSS_L2EPSINS, W, MASK>(acc, yv, wv, lp, lane, valid);
     case SRHIP_LOSS_QUANTILE: return tile_loss<SRHIP_LOSS_QUANTILE, W, MASK>(acc, yv, wv, lp, lane, valid);
     case SRHIP_LOSS_PERIODIC: return tile_loss<SRHIP_LOSS_PERIODIC, W, MASK>(acc, yv, wv, lp, lane, valid);
+    case SRHIP_LOSS_LPINT: return tile_loss<SRHIP_LOSS_LPINT, W, MASK>(acc, yv, wv, lp, lane, valid);
     default: return tile_loss<SRHIP_LOSS_LOGITDIST, W, MASK>(acc, yv, wv, lp, lane, valid);
   }
 }

@@ -180,6 +180,9 @@ def losses():
 
 
 LOSSES = losses()
+# no loss routine: L2 is inline, LPDistLoss{n} with an integer n (LPINT) runs
+# interpreted (its power-by-squaring loop is not a routine)
+NO_LOSS_ROUTINE = {"L2", "LPINT"}
 
 
 def routine_list():
@@ -241,7 +244,7 @@ def routine_list():
         if b == "DIV":
             rs.append(("b_div_lc_full", imm + rows(f"{mk}s.a[r] = dev::bop<SRHIP_BOP_{b}>(imm, s.a[r]);"), False))
     for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
-        if name == "L2":
+        if name in NO_LOSS_ROUTINE:
             continue
         imm = ("const double imm = __builtin_bit_cast(double, ((unsigned long long)s.s_kh << 32) | "
                "(unsigned long long)s.s_k); ")
@@ -258,7 +261,7 @@ def routine_list():
                    False))
     # dℓ/dr of the same losses (the gradient tree code's seed, jit_grad.cpp)
     for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
-        if name == "L2":
+        if name in NO_LOSS_ROUTINE:
             continue
         imm = ("const double imm = __builtin_bit_cast(double, ((unsigned long long)s.s_kh << 32) | "
                "(unsigned long long)s.s_k); ")
@@ -680,10 +683,10 @@ def build(hipcc, outdir, R):
                 for _, b_name in sorted(bop_rt.items())) + "}\n")
         f.write("// routine of each elementwise loss, by SRHIP_LOSS_* (-1: L2, inline)\n")
         f.write("#define SR_JIT_LOSS_ROUTINE {" + ", ".join(
-            str(-1 if n == "L2" else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
+            str(-1 if n in NO_LOSS_ROUTINE else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write("// dℓ/dr routine of each elementwise loss (-1: L2, inline, or left out)\n")
         f.write("#define SR_JIT_DLOSS_ROUTINE {" + ", ".join(
-            str(-1 if n == "L2" else rid(f"d_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
+            str(-1 if n in NO_LOSS_ROUTINE else rid(f"d_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write(f"#define SR_JIT_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT_ROUTINE_TRIG {" + ", ".join("1" if n in trig else "0" for n in names) + "}\n")

@@ -33,6 +33,7 @@ UOPS, BOPS = G.UOPS, G.BOPS
 LOSSY_UOPS, LOSSY_LHS, LOSSY_RHS = G.LOSSY_UOPS, G.LOSSY_LHS, G.LOSSY_RHS
 LOSSES = {m.group(1): int(m.group(2)) for m in
           re.finditer(r"#define SRHIP_LOSS_(\w+)\s+(\d+)", open(G.INCLUDE).read())}
+NO_LOSS_ROUTINE = {"L2", "LPINT"}  # L2 inline; integer LPDistLoss interpreted (gen_jit.py)
 INLINE_BOPS = {"ADD", "SUB", "MUL"}
 INLINE_UOPS = {"NEG", "ABS", "SQUARE", "CUBE"}
 
@@ -160,13 +161,13 @@ def routine_list():
     # (Float64 bits) in s_k : s_kh — device_ops.h elem_loss with ŷ = r, y = 0
     # (r - 0 = r exactly), the Float64 interpreter's loss code
     for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
-        if name == "L2":
+        if name in NO_LOSS_ROUTINE:
             continue
         rs.append((f"l_{name.lower()}",
                    imm + rows(f"s.a[r] = dev::elem_loss<double>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0);")))
     # dℓ/dr of the same losses (the Float64 gradient tree code's seed, jit64.cpp GradGen64)
     for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
-        if name == "L2":
+        if name in NO_LOSS_ROUTINE:
             continue
         rs.append((f"d_{name.lower()}",
                    imm + rows(f"s.a[r] = dev::elem_dloss<double>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0);")))
@@ -261,9 +262,9 @@ def build(hipcc, outdir):
                 str(-1 if b[2:].upper() in INLINE_BOPS else rid(f"{b}_{suf}")) for _, b in sorted(bop_rt.items()))
                 + "}\n")
         f.write("#define SR_JIT64_LOSS_ROUTINE {" + ", ".join(
-            str(-1 if n == "L2" else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
+            str(-1 if n in NO_LOSS_ROUTINE else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write("#define SR_JIT64_DLOSS_ROUTINE {" + ", ".join(
-            str(-1 if n == "L2" else rid(f"d_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
+            str(-1 if n in NO_LOSS_ROUTINE else rid(f"d_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write(f"#define SR_JIT64_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT64_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT64_CLOBBERS " + ", ".join([f'"v{r}"' for r in clob_v] + [f'"s{r}"' for r in clob_s]

@@ -189,6 +189,8 @@ struct GradModule64;
 GradModule64* build_grad64(const CompiledBatch<double>& cb, const std::vector<int32_t>& const_off,
                            const std::vector<int32_t>& cand, std::vector<int32_t>& jit_list, std::vector<int32_t>& rest,
                            GradStats* st, int loss = SRHIP_LOSS_L2, uint64_t lparam = 0);
+// the Float64 loss tree code has this loss's routine
+bool has_loss_routine64(int loss);
 // the Float64 gradient tree code can seed its reverse pass with this loss
 bool has_dloss_routine64(int loss);
 void destroy_grad64(GradModule64* m);

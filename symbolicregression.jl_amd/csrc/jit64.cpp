@@ -1671,6 +1671,9 @@ void grad64_part(const GradModule64* m, int k, int* slot0, int* nslots) {
   *nslots = m->parts[k].nslots;
 }
 int grad64_nraw(const GradModule64* m) { return m ? m->nraw : 0; }
+bool has_loss_routine64(int loss) {
+  return loss == SRHIP_LOSS_L2 || (loss >= 0 && loss < SRHIP_NUM_LOSSES && kLoss64[loss] >= 0);
+}
 bool has_dloss_routine64(int loss) {
   return loss == SRHIP_LOSS_L2 ||
          (loss >= 0 && loss < SRHIP_NUM_LOSSES && kLoss64[loss] >= 0 && kDLoss64[loss] >= 0);

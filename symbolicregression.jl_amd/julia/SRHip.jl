@@ -23,8 +23,8 @@ const SRHIP_ERR_UNSUPPORTED = Int32(-2)
 const NODE_CONST, NODE_FEATURE, NODE_UNARY, NODE_BINARY = UInt8(0), UInt8(1), UInt8(2), UInt8(3)
 const X_JULIA = Int32(0)
 const LOSS_L2, LOSS_L1, LOSS_LP, LOSS_HUBER, LOSS_LOGCOSH = Int32(0), Int32(1), Int32(2), Int32(3), Int32(4)
-const LOSS_L1EPSINS, LOSS_L2EPSINS, LOSS_QUANTILE, LOSS_PERIODIC, LOSS_LOGITDIST =
-    Int32(5), Int32(6), Int32(7), Int32(8), Int32(9)
+const LOSS_L1EPSINS, LOSS_L2EPSINS, LOSS_QUANTILE, LOSS_PERIODIC, LOSS_LOGITDIST, LOSS_LPINT =
+    Int32(5), Int32(6), Int32(7), Int32(8), Int32(9), Int32(10)
 
 struct SrhipTrees              # include/srhip.h: srhip_trees
     ntrees::Int32
@@ -59,7 +59,8 @@ dtype_code(::Type) = throw(Unsupported("only Float32/Float64 run on the GPU"))
 # src/Options.jl:429-431 default L2DistLoss; docs/src/losses.md) ----------------
 loss_code(::L2DistLoss) = (LOSS_L2, 0.0)
 loss_code(::L1DistLoss) = (LOSS_L1, 0.0)
-loss_code(::LPDistLoss{P}) where {P} = (LOSS_LP, Float64(P))
+# LPDistLoss{P} with an Int P keeps Julia's T^Integer rules (srhip.h SRHIP_LOSS_LPINT)
+loss_code(::LPDistLoss{P}) where {P} = (P isa Integer ? LOSS_LPINT : LOSS_LP, Float64(P))
 loss_code(l::HuberLoss) = (LOSS_HUBER, Float64(l.d))
 loss_code(::LogCoshLoss) = (LOSS_LOGCOSH, 0.0)
 loss_code(l::L1EpsilonInsLoss) = (LOSS_L1EPSINS, Float64(l.ε))

@@ -14,7 +14,7 @@ BOP = {n: i for i, n in enumerate(BOPS)}
 UOP = {n: i for i, n in enumerate(UOPS)}
 
 LOSSES = ["L2", "L1", "LP", "HUBER", "LOGCOSH", "L1EPSINS", "L2EPSINS", "QUANTILE", "PERIODIC",
-          "LOGITDIST"]
+          "LOGITDIST", "LPINT"]
 LOSS = {n: i for i, n in enumerate(LOSSES)}
 
 # Julia operator names → (arity, id), applying binopmap / unaopmap

@@ -5,6 +5,7 @@ batch_size, turbo — with the reference's defaults and operator mapping.
 """
 from __future__ import annotations
 
+import numbers
 import warnings
 from dataclasses import dataclass
 from typing import Callable, Optional, Sequence, Tuple
@@ -32,7 +33,12 @@ def L1DistLoss():
     return SupervisedLoss(K.LOSS["L1"])
 
 
-def LPDistLoss(p: float):
+def LPDistLoss(p):
+    """LPDistLoss{p}: an integer p (LPDistLoss(3)) keeps Julia's T^Integer
+    rules (SRHIP_LOSS_LPINT, srhip.h), a float p (LPDistLoss(3.0)) is |r|^p in
+    Float64."""
+    if isinstance(p, numbers.Integral) and not isinstance(p, bool):
+        return SupervisedLoss(K.LOSS["LPINT"], int(p))
     return SupervisedLoss(K.LOSS["LP"], p)
 
 

@@ -142,6 +142,8 @@ def test_constants_and_loss_table_match_the_header():
     assert losses == hdr_losses
     # every loss code has a loss_code method
     mapped = set(re.findall(r"loss_code\([^)]*\)(?: where \{P\})? = \((LOSS_\w+),", src))
+    for a, b in re.findall(r"loss_code\([^)]*\)(?: where \{P\})? = \(P isa Integer \? (LOSS_\w+) : (LOSS_\w+),", src):
+        mapped |= {a, b}  # LPDistLoss{P}: Int P → LPINT, else LP
     assert mapped == set(hdr_losses), set(hdr_losses) ^ mapped
     # node kinds and the X layout
     kinds = re.search(r"const NODE_CONST, NODE_FEATURE, NODE_UNARY, NODE_BINARY = (.*)", src).group(1)
