@@ -176,6 +176,11 @@ def test_gpu_integer_lp_sums_match_oracle(gpu_ctx, dtype):
             m = ok & np.isfinite(rl) & (rl != 0)
             with np.errstate(invalid="ignore", divide="ignore"):
                 rel = np.abs(s / wsum - rl) / np.abs(rl)
-            assert m.sum() > 100 and np.all(rel[m] <= 1e-5), float(np.nanmax(rel[m]))
+            assert m.sum() > 100
+            if dtype == np.float32:
+                assert np.all(rel[m] <= 1e-5), float(np.nanmax(rel[m]))
+            else:  # as test_jit64_gpu's losses: a few trees take cos of huge arguments, where
+                # 1-ulp device / host exp or pow differences move the value anywhere
+                assert np.mean(rel[m] <= 1e-9) >= 0.98 and np.median(rel[m]) <= 1e-13, np.sort(rel[m])[-5:]
     with pytest.raises(Exception, match="integer n"):  # srhip.h: INVALID for a non-integral n
         prog.eval_loss(ds, K.LOSS["LPINT"], [2.5])
