@@ -60,7 +60,9 @@ head stream, so a sharded search gives exactly the single-process result.
 """
 from __future__ import annotations
 
+import bisect
 import ctypes as C
+import itertools
 import math
 import time
 from dataclasses import dataclass, field
@@ -666,6 +668,11 @@ class Search:
         self.weights = list(_mutation_weights(options))
         p, n = options.tournament_selection_p, options.tournament_selection_n
         self.tournament_weights = [p * (1 - p) ** k for k in range(n)]  # sample_tournament (:122-132)
+        # the same draw as _sample_weighted(tournament_weights): u < c over the running sums
+        self.tournament_wsum = sum(self.tournament_weights)
+        self.tournament_cum = list(itertools.accumulate(self.tournament_weights))
+        self.tournament_last = max(i for i, w in enumerate(self.tournament_weights) if w > 0) if n else 0
+        self.freq_scale = float(T(options.adaptive_parsimony_scaling))
 
     def batch_score_of(self, loss_ok, size: int):
         """score_func_batch's (score, loss): (0, Inf) when the evaluation
@@ -715,18 +722,31 @@ def best_of_sample(isl: Island, S: Search, freqs: np.ndarray) -> PopMember:
     n_t = o.tournament_selection_n
     pop = isl.pop
     sample = [pop[i] for i in rng.permutation(len(pop))[:n_t].tolist()]  # sample_pop, replace=false
-    T = S.T
     if o.use_frequency_in_tournament:
-        scale = float(T(o.adaptive_parsimony_scaling))
+        scale = S.freq_scale
         maxsize = o.maxsize
+        fr = freqs.tolist()
+        exp = math.exp
+        f32 = S.T is np.float32
         scores = []
         for m in sample:
             size = (m.info or minfo(m, o))[0]
-            freq = freqs[size - 1] if 0 < size <= maxsize else 0.0
-            scores.append(float(T(m.score * math.exp(scale * freq))))
+            v = m.score * exp(scale * (fr[size - 1] if 0 < size <= maxsize else 0.0))
+            scores.append(float(np.float32(v)) if f32 else v)  # T(...): Float64 values are already T
     else:
         scores = [m.score for m in sample]
-    k = 0 if o.tournament_selection_p == 1.0 else _sample_weighted(S.tournament_weights, rng)
+    if o.tournament_selection_p == 1.0:
+        k = 0
+    else:  # StatsBase.sample(1:n, Weights(w)) by the cumulative weights (_sample_weighted)
+        k = bisect.bisect_right(S.tournament_cum, rng.random() * S.tournament_wsum)
+        if k >= n_t:
+            k = S.tournament_last
+    if k == 0:  # partialsortperm(scores, 1): the first smallest, NaN last (isless)
+        best, bv = 0, math.nan
+        for i, v in enumerate(scores):
+            if v < bv or (bv != bv and v == v):
+                best, bv = i, v
+        return sample[best]
     # partialsortperm(scores, k+1): NaN sorts last (isless)
     order = sorted(range(n_t), key=lambda i: (math.isnan(scores[i]), scores[i]))
     return sample[order[k]]
