@@ -179,8 +179,20 @@ def test_gpu_integer_lp_sums_match_oracle(gpu_ctx, dtype):
             assert m.sum() > 100
             if dtype == np.float32:
                 assert np.all(rel[m] <= 1e-5), float(np.nanmax(rel[m]))
-            else:  # as test_jit64_gpu's losses: a few trees take cos of huge arguments, where
-                # 1-ulp device / host exp or pow differences move the value anywhere
-                assert np.mean(rel[m] <= 1e-9) >= 0.98 and np.median(rel[m]) <= 1e-13, np.sort(rel[m])[-5:]
+            else:
+                # a few trees of this population take cos / exp of huge or cancelling
+                # arguments, where 1-ulp device / host differences move the value
+                # anywhere (as in test_jit64_gpu's losses): 95 % within 1e-9 of the
+                # oracle, and every tree's integer-n sum within 1e-12 of the same
+                # engine's LPDistLoss(float(n)) sum, whose element values differ by
+                # the few ulp of x*x*x / pow_body vs pow (the conditioning of the
+                # tree is then the same on both sides)
+                assert np.mean(rel[m] <= 1e-9) >= 0.95 and np.median(rel[m]) <= 1e-13, np.sort(rel[m])[-5:]
+                sf, wf, okf = prog.eval_loss(ds, K.LOSS["LP"], [float(p)])
+                assert np.array_equal(ok, okf) and wf == wsum
+                mf = ok & np.isfinite(sf) & (sf != 0)
+                with np.errstate(invalid="ignore", divide="ignore"):
+                    relf = np.abs(s - sf) / np.abs(sf)
+                assert np.all(relf[mf] <= 1e-12), float(np.nanmax(relf[mf]))
     with pytest.raises(Exception, match="integer n"):  # srhip.h: INVALID for a non-integral n
         prog.eval_loss(ds, K.LOSS["LPINT"], [2.5])
