@@ -85,9 +85,21 @@ _new_node = Node.__new__
 def copy_node(t: Node) -> Node:
     """DynamicExpressions.copy_node (deep copy)."""
     n = _new_node(Node)
-    n.degree, n.constant, n.val, n.feature, n.op = t.degree, t.constant, t.val, t.feature, t.op
-    n.l = copy_node(t.l) if t.degree >= 1 else None
-    n.r = copy_node(t.r) if t.degree == 2 else None
+    d = t.degree
+    n.degree = d
+    n.constant = t.constant
+    n.val = t.val
+    n.feature = t.feature
+    n.op = t.op
+    if d == 0:
+        n.l = None
+        n.r = None
+    elif d == 1:
+        n.l = copy_node(t.l)
+        n.r = None
+    else:
+        n.l = copy_node(t.l)
+        n.r = copy_node(t.r)
     return n
 
 
@@ -139,27 +151,23 @@ def count_constants(t: Node) -> int:
     return sum(1 for n in nodes_preorder(t) if n.degree == 0 and n.constant)
 
 
+def _info(t: Node):
+    """(node count, depth, constant count) of t."""
+    d = t.degree
+    if d == 0:
+        return 1, 1, 1 if t.constant else 0
+    n, h, k = _info(t.l)
+    if d == 1:
+        return n + 1, h + 1, k
+    n2, h2, k2 = _info(t.r)
+    return n + n2 + 1, (h if h > h2 else h2) + 1, k + k2
+
+
 def tree_info(t: Node, options):
     """(compute_complexity, count_depth, count_constants) in one traversal."""
     if options.complexity_use:
         return compute_complexity(t, options), count_depth(t), count_constants(t)
-    n = k = 0
-    depth = 0
-    stack = [(t, 1)]
-    while stack:
-        x, d = stack.pop()
-        n += 1
-        if d > depth:
-            depth = d
-        deg = x.degree
-        if deg == 0:
-            if x.constant:
-                k += 1
-        else:
-            stack.append((x.l, d + 1))
-            if deg == 2:
-                stack.append((x.r, d + 1))
-    return n, depth, k
+    return _info(t)
 
 
 def compute_complexity(t: Node, options) -> int:
