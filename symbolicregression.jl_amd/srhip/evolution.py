@@ -739,8 +739,9 @@ def best_of_sample(isl: Island, S: Search, freqs: np.ndarray) -> PopMember:
         scores = []
         for m in sample:
             size = (m.info or minfo(m, o))[0]
-            v = m.score * exp(scale * (fr[size - 1] if 0 < size <= maxsize else 0.0))
-            scores.append(float(np.float32(v)) if f32 else v)  # T(...): Float64 values are already T
+            scores.append(m.score * exp(scale * (fr[size - 1] if 0 < size <= maxsize else 0.0)))
+        if f32:  # T(...), all at once (Float64 values are already T)
+            scores = np.array(scores).astype(np.float32).tolist()
     else:
         scores = [m.score for m in sample]
     if o.tournament_selection_p == 1.0:
