@@ -127,8 +127,7 @@ extern "C" {
 /* LPDistLoss{n} with an INTEGER n (LPDistLoss(3), not LPDistLoss(3.0)):
  * |r|^n by Julia's T^Integer — Float32 stays Float32 (|r|*|r|*|r| for n = 3,
  * else Float64 power by squaring rounded once), Float64 by compensated power
- * by squaring; params[0] = n, integral with |n| < 2^31 (else INVALID).
- * Interpreted only (no tree code). */
+ * by squaring; params[0] = n, integral with |n| < 2^31 (else INVALID). */
 #define SRHIP_LOSS_LPINT 10
 #define SRHIP_NUM_LOSSES 11
 

@@ -180,9 +180,9 @@ def losses():
 
 
 LOSSES = losses()
-# no loss routine: L2 is inline, LPDistLoss{n} with an integer n (LPINT) runs
-# interpreted (its power-by-squaring loop is not a routine)
-NO_LOSS_ROUTINE = {"L2", "LPINT"}
+# no loss routine: L2 is inline (LPDistLoss{n} with an integer n has one: its
+# power-by-squaring loop runs over the wave-uniform n in SGPRs)
+NO_LOSS_ROUTINE = {"L2"}
 
 
 def routine_list():

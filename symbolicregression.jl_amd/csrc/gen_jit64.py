@@ -33,7 +33,7 @@ UOPS, BOPS = G.UOPS, G.BOPS
 LOSSY_UOPS, LOSSY_LHS, LOSSY_RHS = G.LOSSY_UOPS, G.LOSSY_LHS, G.LOSSY_RHS
 LOSSES = {m.group(1): int(m.group(2)) for m in
           re.finditer(r"#define SRHIP_LOSS_(\w+)\s+(\d+)", open(G.INCLUDE).read())}
-NO_LOSS_ROUTINE = {"L2", "LPINT"}  # L2 inline; integer LPDistLoss interpreted (gen_jit.py)
+NO_LOSS_ROUTINE = {"L2"}  # L2 inline
 INLINE_BOPS = {"ADD", "SUB", "MUL"}
 INLINE_UOPS = {"NEG", "ABS", "SQUARE", "CUBE"}
 

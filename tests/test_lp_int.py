@@ -11,9 +11,12 @@ LossFunctions' deriv is P * abs(r)^(P-1) * sign(r) in T. Julia's Base is not in
 published source: parity unpinned beyond that restatement. The CPU tests pin
 the oracle against an independent Python restatement (and the Float64 values
 within an ulp of the exact rational power); the GPU tests check the
-interpreter's element values bit for bit against the oracle through
-one-row datasets (ŷ = c, y = 0), its sums at size, and its gradients.
+element values of the tree code's integer-n loss routine (gen_jit.py /
+gen_jit64.py l_lpint, d_lpint: the interpreter's device_ops.h code) bit for
+bit against the oracle through one-row datasets (ŷ = x1·c = c, y = 0), their
+gradients, and the sums at size against the interpreter and the oracle.
 """
+import os
 from fractions import Fraction
 
 import numpy as np
@@ -120,8 +123,9 @@ def test_oracle_float64_integer_power_within_an_ulp(n):
 # ---- GPU: the interpreter -------------------------------------------------------
 
 def _const_trees(cs, dtype):
+    """x1 * c per constant: with x1 = 1 the prediction is c exactly."""
     o = srhip.Options(binary_operators=["+", "*"], unary_operators=[])
-    trees = [srhip.Node(val=dtype(c)) for c in cs]
+    trees = [o.make_binary("*", srhip.Node("x1"), srhip.Node(val=dtype(c))) for c in cs]
     return o, srhip.flatten(trees, o, dtype=dtype)
 
 
@@ -132,7 +136,7 @@ def test_gpu_integer_lp_values_bit_exact(gpu_ctx, dtype, n):
     rng = np.random.default_rng(300 + n)
     cs = np.concatenate([rng.standard_normal(700) * 2, rng.uniform(0.9, 1.1, 300)]).astype(dtype)
     o, flat = _const_trees(cs, dtype)
-    X = np.zeros((1, 1), dtype=dtype)
+    X = np.ones((1, 1), dtype=dtype)
     y = np.zeros(1, dtype=dtype)
     ds = srhip.DeviceDataset(gpu_ctx, X, y)
     prog = srhip.Program(gpu_ctx, flat, dtype)
@@ -141,7 +145,8 @@ def test_gpu_integer_lp_values_bit_exact(gpu_ctx, dtype, n):
     assert wsum == 1.0 and ok.all()
     want = np.array([oracle.elem_loss(loss.kind, loss.params, dtype(c), dtype(0), dtype=dtype) for c in cs])
     np.testing.assert_array_equal(s.astype(dtype), want.astype(dtype))
-    # gradient: dℓ/dc = n |c|^(n-1) sign(c) in T
+    assert gpu_ctx.last_tree_code() > 900  # constant trees: tree code with the integer-n loss routine
+    # gradient: dℓ/dc = n |c|^(n-1) sign(c) in T (gradient tree code seeded by the dℓ/dr routine)
     s2, g, w2, ok2 = prog.eval_loss_grad(ds, loss.kind, loss.params)
     assert ok2.all()
     with np.errstate(all="ignore"):
@@ -164,13 +169,26 @@ def test_gpu_integer_lp_sums_match_oracle(gpu_ctx, dtype):
     w = np.abs(rng.standard_normal(n)).astype(dtype)
     trees = srhip.random_population(512, o, 5, dtype, seed=78)
     flat = srhip.flatten(trees, o, dtype=dtype)
-    prog = srhip.Program(gpu_ctx, flat, dtype)
+    progs = {}
+    for mode in ("1", "0"):
+        os.environ["SRHIP_JIT"] = mode
+        try:
+            progs[mode] = srhip.Program(gpu_ctx, flat, dtype)
+        finally:
+            del os.environ["SRHIP_JIT"]
+    prog = progs["1"]
     for p in (3, 4):
         loss = srhip.LPDistLoss(p)
         for weights in (None, w):
             ds = srhip.DeviceDataset(gpu_ctx, X, y, weights)
             s, wsum, ok = prog.eval_loss(ds, loss.kind, loss.params)
-            assert gpu_ctx.last_tree_code() == 0  # interpreted (no LPINT routine)
+            assert gpu_ctx.last_tree_code() > 300  # the integer-n loss routine in the tile tail
+            si, wi, oki = progs["0"].eval_loss(ds, loss.kind, loss.params)
+            assert gpu_ctx.last_tree_code() == 0 and wi == wsum and np.array_equal(ok, oki)
+            mi = ok & np.isfinite(si) & (si != 0)
+            with np.errstate(invalid="ignore", divide="ignore"):
+                reli = np.abs(s - si) / np.abs(si)
+            assert np.all(reli[mi] <= (1e-5 if dtype == np.float32 else 1e-11)), float(np.nanmax(reli[mi]))
             _, rl, rok = oracle.eval_loss_batch(flat, X, y, weights, loss.kind, loss.params, dtype=dtype, nthreads=16)
             assert np.array_equal(ok, rok)
             m = ok & np.isfinite(rl) & (rl != 0)
