@@ -361,7 +361,7 @@ int32_t srhip_program_update_stats(const srhip_program* prog, int64_t* out_inpla
 /* Gradient tree code of this program (reverse-mode ∂L/∂c for
  * srhip_eval_loss_grad, built on the first gradient call; Float32: L2 and the
  * losses with a dℓ/dr routine — all but Periodic; Float64 (jit64.cpp): all
- * but LP):
+ * but LP, the non-integer LPDistLoss; LPINT has its routines in both):
  * trees compiled, trees left to the forward-mode interpreter, code bytes,
  * codegen and load times (ms). All zero before the first gradient call. */
 int32_t srhip_program_grad_jit_info(const srhip_program* prog, int32_t* out_ntrees, int32_t* out_nrejected,
