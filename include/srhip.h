@@ -200,6 +200,10 @@ int32_t srhip_program_create(srhip_ctx* ctx, int32_t dtype,
  * code is built reading its constants from memory from the start, so no
  * constant set ever recompiles it (without the flag the first set does). */
 #define SRHIP_PROGRAM_VARYING_CONSTANTS 1u
+/* SRHIP_PROGRAM_INTERPRETED: build no loss / output tree code (the program is
+ * scored only on per-tree row sets, srhip_eval_loss_rowsets, which run in the
+ * interpreter: a large batch then skips the code generation and load). */
+#define SRHIP_PROGRAM_INTERPRETED 2u
 int32_t srhip_program_create_ex(srhip_ctx* ctx, int32_t dtype, const srhip_trees* trees, uint32_t flags,
                                 srhip_program** out_prog);
 int32_t srhip_program_destroy(srhip_program* prog);
@@ -256,6 +260,32 @@ int32_t srhip_eval_loss_batch_ctx(srhip_ctx* ctx, srhip_dataset* ds, const srhip
                                   const int64_t* row_idx, int64_t nidx,
                                   double* out_loss_sum, double* out_weight_sum,
                                   uint8_t* out_ok);
+
+/* ---- per-tree minibatches: score_func_batch src/LossFunctions.jl:95-115 ----
+ * The reference draws a fresh sample of batch_size rows (with replacement,
+ * :98) for EVERY call, i.e. for every candidate it scores (src/Mutate.jl:41-47
+ * parents, :199-205 babies). This scores every tree of the program on its own
+ * sample in ONE launch: row_idx is [ntrees][batch_size] (0-based within the
+ * shard, repetition allowed), tree t evaluated on rows row_idx[t][0..bs).
+ *   out_loss_sum[t]   = Σ_k w_{idx[t][k]} · ℓ(ŷ_t, y) over tree t's sample
+ *   out_weight_sum[t] = Σ_k w_{idx[t][k]} (batch_size when unweighted)
+ *   out_ok[t]         = did_succeed on that sample
+ * The loss is out_loss_sum[t] / out_weight_sum[t] in T (Inf if !ok), as
+ * srhip_eval_loss. Runs in the interpreter (one tree per workgroup over its
+ * gathered sample). */
+int32_t srhip_eval_loss_rowsets(srhip_dataset* ds, const srhip_program* prog,
+                                int32_t loss_kind, const double* loss_params,
+                                const int64_t* row_idx, int64_t batch_size,
+                                double* out_loss_sum, double* out_weight_sum,
+                                uint8_t* out_ok);
+/* Convenience: program (SRHIP_PROGRAM_INTERPRETED) in ctx (NULL = the
+ * dataset's context) + srhip_eval_loss_rowsets + destroy — Julia's batched
+ * score_func_batch over a vector of candidates. */
+int32_t srhip_eval_loss_batch_rowsets_ctx(srhip_ctx* ctx, srhip_dataset* ds, const srhip_trees* trees,
+                                          int32_t loss_kind, const double* loss_params,
+                                          const int64_t* row_idx, int64_t batch_size,
+                                          double* out_loss_sum, double* out_weight_sum,
+                                          uint8_t* out_ok);
 
 /* ---- per-row outputs: eval_tree_array src/InterfaceDynamicExpressions.jl:50-52
  * out is [ntrees][rows] of the dataset dtype (row-major per tree); rows of a

@@ -1378,7 +1378,7 @@ jit::GradModule64* grad_module64(srhip_program* p, int loss, double lparam) {
 template <typename T>
 void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const T* y,
               const T* w, int64_t rows, int64_t n_pad, int nfeat, int loss, double lparam,
-              T* out, int64_t out_stride) {
+              T* out, int64_t out_stride, int64_t seg = 0) {
   hipStream_t s = c->stream;
   timing_reset(c);
   c->sums.ensure(std::max<size_t>(p->ntrees, 1) * sizeof(double));
@@ -1396,13 +1396,14 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
   }
   const size_t nslots = (size_t)p->nlist_a + p->nlist_b;
   // slot ranges: [0, nj) tree code, [nj, nlist_a) shallow interpreter, then deep
-  jit::Module* jm = !std::is_same<T, float>::value ? nullptr
-                    : mode == MODE_LOSS          ? loss_module(p, loss, lparam)
-                                                 : out_module(p);
+  // (per-tree row sets, seg > 0: the interpreter, one tree per workgroup)
+  jit::Module* jm = (!std::is_same<T, float>::value || seg > 0) ? nullptr
+                    : mode == MODE_LOSS                          ? loss_module(p, loss, lparam)
+                                                                 : out_module(p);
   // Float64 programs: their tree code (this loss, or per-row outputs)
   jit::Module64* jm64 = nullptr;
   if constexpr (std::is_same<T, double>::value)
-    if (p->jit64 && p->nlist_j > 0) jm64 = module64(p, mode == MODE_LOSS ? loss : -2, lparam);
+    if (p->jit64 && p->nlist_j > 0 && seg == 0) jm64 = module64(p, mode == MODE_LOSS ? loss : -2, lparam);
   const bool use_jit = jm != nullptr || jm64 != nullptr;
   c->last_jit_trees = (use_jit && rows > 0) ? p->nlist_j : 0;
   const int nj = use_jit ? p->nlist_j : 0;
@@ -1485,6 +1486,14 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     } else if (!plan_eval(p->dtype, pass == 1, p->opset, mode, w != nullptr, nfeat, rows, nlist, &plan)) {
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
     }
+    if (seg > 0) {
+      // per-tree row sets: one tree per workgroup of one wave, staging its
+      // own segment (eval_kernel.h seg0); the segment holds the row groups
+      plan.tpb = 1;
+      plan.ntg = nlist;
+      plan.threads = 64;
+      if ((int64_t)plan.nrg * plan.rows_wg > seg) throw Error(SRHIP_ERR_INVALID, "row set segment too short");
+    }
     EvalArgs<T> a;
     a.prog = static_cast<const Ins<T>*>(p->d_code);
     a.tree_off = p->d_tree_off;
@@ -1520,6 +1529,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     a.partial = static_cast<Part<T>*>(c->partial.p);
     a.out = out;
     a.out_stride = out_stride;
+    a.seg = seg;
     const int tk = timed_begin(c, s);
     if (pass == -1) {
       if constexpr (std::is_same<T, float>::value) {
@@ -1636,7 +1646,7 @@ int eval_loss_impl(srhip_dataset* ds, const srhip_program* p, int loss, const do
     if (nidx > 0) {
       HIP_CHECK(hipMemcpyAsync(c->scratch_idx.p, row_idx, nidx * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
       HIP_CHECK(launch_gather_rows<T>(X, y, w, ds->nfeat, ds->n_pad,
-                                      static_cast<const int64_t*>(c->scratch_idx.p), nidx, gp, Xg,
+                                      static_cast<const int64_t*>(c->scratch_idx.p), nidx, 0, gp, Xg,
                                       yg, w ? wg : nullptr, c->stream));
     }
     if (w) {  // Σ w over the (repeated) sample
@@ -1654,6 +1664,57 @@ int eval_loss_impl(srhip_dataset* ds, const srhip_program* p, int loss, const do
   run_eval<T>(c, p, MODE_LOSS, X, y, w, rows, n_pad, ds->nfeat, loss, params ? params[0] : 0.0, nullptr, 0);
   collect_results(c, p, rows, out_sum, out_ok);
   if (out_wsum) *out_wsum = wsum;
+  return SRHIP_OK;
+}
+
+// score_func_batch for every tree of the program on its OWN row sample
+// (src/LossFunctions.jl:95-115 draws `batch_size` rows with replacement per
+// call): the samples are gathered into one segment per tree — seg rows,
+// row set t in [t·seg, t·seg + bs), padded with its last row — and the
+// interpreter runs one tree per workgroup over its segment (run_eval seg).
+// One gather, one evaluation launch and one finalize for all trees.
+template <typename T>
+int eval_loss_rowsets_impl(srhip_dataset* ds, const srhip_program* p, int loss, const double* params,
+                           const int64_t* row_idx, int64_t bs, double* out_sum, double* out_wsum,
+                           uint8_t* out_ok) {
+  srhip_ctx* c = p->ctx;
+  const int nt = p->ntrees;
+  if (bs < 0) throw Error(SRHIP_ERR_INVALID, "negative batch size");
+  if (bs > 0 && nt > 0 && !row_idx) throw Error(SRHIP_ERR_INVALID, "row_idx is NULL");
+  const int64_t nidx = (int64_t)nt * bs;
+  for (int64_t k = 0; k < nidx; ++k)
+    if (row_idx[k] < 0 || row_idx[k] >= ds->rows) throw Error(SRHIP_ERR_INVALID, "row index out of range");
+  // segment: a power of two >= the row group of any interpreter variant
+  // (rows_wg = tiles · 64R is a power of two < 2·bs, or one 512-row tile)
+  int64_t seg = 512;
+  while (seg < bs && seg < kRowPad) seg *= 2;
+  if (seg < bs) seg = pad_rows(bs);
+  const T* w = static_cast<const T*>(ds->w);
+  const int64_t gp = seg * std::max(nt, 1);
+  const size_t es = sizeof(T);
+  c->scratch_idx.ensure((size_t)std::max<int64_t>(nidx, 1) * sizeof(int64_t));
+  c->gather.ensure((size_t)gp * (ds->nfeat + 2) * es);
+  T* Xg = static_cast<T*>(c->gather.p);
+  T* yg = Xg + (size_t)gp * ds->nfeat;
+  T* wg = yg + gp;
+  if (nidx > 0) {
+    HIP_CHECK(hipMemcpyAsync(c->scratch_idx.p, row_idx, nidx * sizeof(int64_t), hipMemcpyHostToDevice, c->stream));
+    HIP_CHECK(launch_gather_rows<T>(static_cast<const T*>(ds->X), static_cast<const T*>(ds->y), w, ds->nfeat,
+                                    ds->n_pad, static_cast<const int64_t*>(c->scratch_idx.p), bs, seg, gp, Xg, yg,
+                                    w ? wg : nullptr, c->stream));
+  }
+  run_eval<T>(c, p, MODE_LOSS, Xg, yg, w ? wg : nullptr, bs, gp, ds->nfeat, loss, params ? params[0] : 0.0, nullptr,
+              0, seg);
+  collect_results(c, p, bs, out_sum, out_ok);  // (the copy of row_idx is ordered before these waits)
+  if (out_wsum)
+    for (int t = 0; t < nt; ++t) {  // Σ w over tree t's (repeated) sample
+      double s = 0.0;
+      if (w)
+        for (int64_t k = 0; k < bs; ++k) s += ds->h_w[row_idx[(size_t)t * bs + k]];
+      else
+        s = (double)bs;
+      out_wsum[t] = s;
+    }
   return SRHIP_OK;
 }
 
@@ -2327,13 +2388,15 @@ int32_t srhip_program_create_ex(srhip_ctx* ctx, int32_t dtype, const srhip_trees
     *out_prog = nullptr;
     if (dtype != SRHIP_F32 && dtype != SRHIP_F64) throw Error(SRHIP_ERR_UNSUPPORTED, "dtype must be F32 or F64");
     if (trees->ntrees < 0) throw Error(SRHIP_ERR_INVALID, "negative tree count");
-    if (flags & ~SRHIP_PROGRAM_VARYING_CONSTANTS) throw Error(SRHIP_ERR_INVALID, "unknown program flags");
+    if (flags & ~(SRHIP_PROGRAM_VARYING_CONSTANTS | SRHIP_PROGRAM_INTERPRETED))
+      throw Error(SRHIP_ERR_INVALID, "unknown program flags");
     const int nt = trees->ntrees;
     auto* p = new srhip_program();
     p->ctx = ctx;
     p->dtype = dtype;
     p->ntrees = nt;
     p->jit_memc = (flags & SRHIP_PROGRAM_VARYING_CONSTANTS) != 0;
+    if (flags & SRHIP_PROGRAM_INTERPRETED) p->jit_allowed = false;
     try {
       if (nt > 0) {
         if (!trees->node_off || !trees->const_off) throw Error(SRHIP_ERR_INVALID, "null offsets");
@@ -2471,6 +2534,40 @@ int32_t srhip_eval_loss_batch_ctx(srhip_ctx* ctx, srhip_dataset* ds, const srhip
   int32_t rc = srhip_program_create(ctx, ds->dtype, trees, &p);
   if (rc != SRHIP_OK) return rc;
   rc = srhip_eval_loss(ds, p, loss_kind, loss_params, row_idx, nidx, out_loss_sum, out_weight_sum, out_ok);
+  std::string err = g_last_error;
+  srhip_program_destroy(p);
+  g_last_error = err;
+  return rc;
+}
+
+int32_t srhip_eval_loss_rowsets(srhip_dataset* ds, const srhip_program* prog, int32_t loss_kind,
+                                const double* loss_params, const int64_t* row_idx, int64_t batch_size,
+                                double* out_loss_sum, double* out_weight_sum, uint8_t* out_ok) {
+  return guarded([&] {
+    check_program_vs_dataset(ds, prog);
+    check_loss(loss_kind, loss_params);
+    std::lock_guard<std::mutex> lk(prog->ctx->mu);
+    HIP_CHECK(hipSetDevice(prog->ctx->device));
+    if (ds->dtype == SRHIP_F32)
+      return eval_loss_rowsets_impl<float>(ds, prog, loss_kind, loss_params, row_idx, batch_size, out_loss_sum,
+                                           out_weight_sum, out_ok);
+    return eval_loss_rowsets_impl<double>(ds, prog, loss_kind, loss_params, row_idx, batch_size, out_loss_sum,
+                                          out_weight_sum, out_ok);
+  });
+}
+
+int32_t srhip_eval_loss_batch_rowsets_ctx(srhip_ctx* ctx, srhip_dataset* ds, const srhip_trees* trees,
+                                          int32_t loss_kind, const double* loss_params, const int64_t* row_idx,
+                                          int64_t batch_size, double* out_loss_sum, double* out_weight_sum,
+                                          uint8_t* out_ok) {
+  if (!ds) return set_error(SRHIP_ERR_INVALID, "null dataset");
+  if (!ctx) ctx = ds->ctx;
+  srhip_program* p = nullptr;
+  // row sets run in the interpreter: no tree code to build
+  int32_t rc = srhip_program_create_ex(ctx, ds->dtype, trees, SRHIP_PROGRAM_INTERPRETED, &p);
+  if (rc != SRHIP_OK) return rc;
+  rc = srhip_eval_loss_rowsets(ds, p, loss_kind, loss_params, row_idx, batch_size, out_loss_sum, out_weight_sum,
+                               out_ok);
   std::string err = g_last_error;
   srhip_program_destroy(p);
   g_last_error = err;

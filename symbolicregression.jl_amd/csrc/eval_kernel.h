@@ -199,6 +199,8 @@ eval_kernel(EvalArgs<T> a) {
   const int rg = blockIdx.x / a.ntg;
   const int g = blockIdx.x - rg * a.ntg;
   const int64_t row0 = (int64_t)rg * rows;
+  // per-tree row sets: the group's one tree (slot g) reads its own segment
+  const int64_t seg0 = a.seg ? a.seg * (int64_t)a.list[g < a.nlist ? g : 0] : 0;
 
   // 1. stage the row group in LDS
   {
@@ -208,7 +210,7 @@ eval_kernel(EvalArgs<T> a) {
       const int arr = idx / vper;
       const int v = idx - arr * vper;
       const T* src = arr < a.nfeat ? a.X + (size_t)arr * a.n_pad : (arr == a.nfeat ? a.y : a.w);
-      reinterpret_cast<V*>(sX + (size_t)arr * rows)[v] = reinterpret_cast<const V*>(src + row0)[v];
+      reinterpret_cast<V*>(sX + (size_t)arr * rows)[v] = reinterpret_cast<const V*>(src + seg0 + row0)[v];
     }
     for (int i = threadIdx.x; i < a.tpb; i += blockDim.x) sPart[i] = Part<T>{T(0), T(0)};
     if (threadIdx.x == 0) *reinterpret_cast<uint32_t*>(sPart + a.tpb) = 0u;  // tree counter (a.rotate & 4)

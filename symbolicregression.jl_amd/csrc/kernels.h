@@ -45,6 +45,9 @@ struct EvalArgs {
   Part<T>* partial;        // [nrg][ntg*tpb]
   T* out;                  // MODE_OUT: [ntrees][out_stride]
   int64_t out_stride;
+  // per-tree row sets (srhip_eval_loss_rowsets; interpreter, one tree per
+  // group): tree t reads rows [t·seg, t·seg + n) of X / y / w; 0 = shared rows
+  int64_t seg = 0;
 };
 
 // Geometry of one evaluation launch, chosen by plan_eval().
@@ -152,10 +155,12 @@ hipError_t launch_pack_x(const T* src, int layout, int64_t src_stride,
 template <typename T>
 hipError_t launch_pack_vec(const T* src, int64_t rows, int64_t n_pad, T* dst,
                            hipStream_t stream);
-// Row gather for score_func_batch: dst[f][k] = src[f][idx[k]] (+ y, w).
+// Row gather for score_func_batch: dst[f][k] = src[f][idx[k]] (+ y, w);
+// seg > 0: one sample of nidx rows per segment of seg rows (per-tree samples,
+// srhip_eval_loss_rowsets), idx = [dst_pad / seg][nidx].
 template <typename T>
 hipError_t launch_gather_rows(const T* X, const T* y, const T* w, int nfeat,
-                              int64_t src_pad, const int64_t* idx, int64_t nidx,
+                              int64_t src_pad, const int64_t* idx, int64_t nidx, int64_t seg,
                               int64_t dst_pad, T* Xd, T* yd, T* wd,
                               hipStream_t stream);
 

@@ -119,15 +119,19 @@ __global__ void pack_vec_kernel(const T* __restrict__ src, int64_t rows, int64_t
 template <typename T>
 __global__ void gather_rows_kernel(const T* __restrict__ X, const T* __restrict__ y,
                                    const T* __restrict__ w, int nfeat, int64_t src_pad,
-                                   const int64_t* __restrict__ idx, int64_t nidx,
+                                   const int64_t* __restrict__ idx, int64_t nidx, int64_t seg,
                                    int64_t dst_pad, T* __restrict__ Xd, T* __restrict__ yd,
                                    T* __restrict__ wd) {
+  // seg > 0: dst_pad / seg samples back to back, sample t = idx[t·nidx ..
+  // t·nidx + nidx) in rows [t·seg, t·seg + nidx), padded with its last row
   const int64_t total = dst_pad * (nfeat + 2);
   for (int64_t k = blockIdx.x * (int64_t)blockDim.x + threadIdx.x; k < total;
        k += (int64_t)gridDim.x * blockDim.x) {
     const int64_t f = k / dst_pad;
     const int64_t j = k - f * dst_pad;
-    const int64_t r = idx[j < nidx ? j : nidx - 1];
+    const int64_t t = seg ? j / seg : 0;
+    const int64_t jj = j - t * seg;
+    const int64_t r = idx[t * nidx + (jj < nidx ? jj : nidx - 1)];
     if (f < nfeat) Xd[f * dst_pad + j] = X[f * src_pad + r];
     else if (f == nfeat) yd[j] = y[r];
     else if (w) wd[j] = w[r];
@@ -377,13 +381,13 @@ hipError_t launch_pack_vec(const T* src, int64_t rows, int64_t n_pad, T* dst, hi
 
 template <typename T>
 hipError_t launch_gather_rows(const T* X, const T* y, const T* w, int nfeat, int64_t src_pad,
-                              const int64_t* idx, int64_t nidx, int64_t dst_pad, T* Xd, T* yd,
-                              T* wd, hipStream_t stream) {
+                              const int64_t* idx, int64_t nidx, int64_t seg, int64_t dst_pad, T* Xd,
+                              T* yd, T* wd, hipStream_t stream) {
   const int64_t total = dst_pad * (nfeat + 2);
   unsigned grid = (unsigned)std::min<int64_t>((total + 255) / 256, 4096);
   if (grid == 0) grid = 1;
   hipLaunchKernelGGL((gather_rows_kernel<T>), dim3(grid), dim3(256), 0, stream, X, y, w, nfeat,
-                     src_pad, idx, nidx, dst_pad, Xd, yd, wd);
+                     src_pad, idx, nidx, seg, dst_pad, Xd, yd, wd);
   return hipGetLastError();
 }
 
@@ -393,8 +397,8 @@ hipError_t launch_gather_rows(const T* X, const T* y, const T* w, int nfeat, int
                                        int*, hipStream_t);                                    \
   template hipError_t launch_pack_vec<T>(const T*, int64_t, int64_t, T*, hipStream_t);         \
   template hipError_t launch_gather_rows<T>(const T*, const T*, const T*, int, int64_t,        \
-                                            const int64_t*, int64_t, int64_t, T*, T*, T*,      \
-                                            hipStream_t);
+                                            const int64_t*, int64_t, int64_t, int64_t, T*, T*, \
+                                            T*, hipStream_t);
 SR_INST(float)
 SR_INST(double)
 

@@ -55,6 +55,7 @@ import ..ConstantOptimizationModule: optimize_constants
 import ..UtilsModule: get_birth_order
 import ..PopMemberModule: generate_reference
 import ..RecorderModule: @recorder
+import ..SingleIterationModule: s_r_cycle
 import DynamicExpressions: string_tree
 import ..SRHip
 
@@ -81,15 +82,17 @@ end
 """
     score_batch_minibatch(dataset, trees, options) -> (scores, losses)
 
-score_func_batch (src/LossFunctions.jl:95-115) for every tree: one row sample
-of batch_size rows (with replacement) shared by the launch; a failed
-evaluation scores (0, Inf) as in the reference.
+score_func_batch (src/LossFunctions.jl:95-115) for every tree: each tree on
+its OWN sample of batch_size rows drawn with replacement, as the reference
+draws one per call (:98), all trees in one launch
+(SRHip.eval_loss_batch_rowsets); a failed evaluation scores (0, Inf) as in
+the reference.
 """
 function score_batch_minibatch(dataset::Dataset{T}, trees::AbstractVector{Node{T}}, options::Options) where {T}
     if !isempty(trees) && SRHip.enabled(options)
         try
-            idx = rand(1:(dataset.n), options.batch_size)
-            losses = SRHip.eval_loss_batch(trees, dataset, options; idx=idx)
+            idx = rand(1:(dataset.n), options.batch_size, length(trees))  # column t: tree t's sample
+            losses = SRHip.eval_loss_batch_rowsets(trees, dataset, options, idx)
             scores = [isfinite(l) ? loss_to_score(l, dataset.baseline_loss, t, options) : zero(T)
                       for (l, t) in zip(losses, trees)]
             return scores, losses
@@ -414,23 +417,32 @@ function reg_evol_cycle_lockstep(dataset::Dataset{T}, pops::AbstractVector{<:Pop
     nsteps = round(Int, pops[1].n / options.tournament_selection_n)
     for _ in 1:nsteps
         steps = Vector{Step{T}}(undef, length(pops))
+        # tournaments first: each island's crossover draw and best_of_sample
+        allstars = Vector{Union{PopMember{T},Nothing}}(nothing, length(pops))
         for (k, pop) in enumerate(pops)
             if rand() > options.crossover_probability
-                allstar = best_of_sample(pop, stats[k], options)
-                before = if options.batching  # src/Mutate.jl:41-47
-                    bs, bl = score_func_batch(dataset, allstar.tree, options)
-                    num_evals += options.batch_size / dataset.n
-                    (bs, bl)
-                else
-                    (allstar.score, allstar.loss)
-                end
-                steps[k] = Step{T}(false, propose(dataset, allstar, before, temperature, curmaxsize, options),
-                                   (allstar,), nothing)
+                allstars[k] = best_of_sample(pop, stats[k], options)
             else
                 a1 = best_of_sample(pop, stats[k], options)
                 a2 = best_of_sample(pop, stats[k], options)
                 steps[k] = Step{T}(true, nothing, (a1, a2), crossover_children(a1, a2, curmaxsize, options))
             end
+        end
+        # with options.batching every next_generation re-scores its parent on a
+        # fresh minibatch (src/Mutate.jl:41-47): all islands' parents in ONE launch,
+        # each on its own sample
+        mut = findall(a -> a !== nothing, allstars)
+        before = if options.batching && !isempty(mut)
+            ps, pl = score_batch_minibatch(dataset, Node{T}[allstars[k].tree for k in mut], options)
+            num_evals += length(mut) * (options.batch_size / dataset.n)
+            Dict(k => (ps[i], pl[i]) for (i, k) in enumerate(mut))
+        else
+            Dict(k => (allstars[k].score, allstars[k].loss) for k in mut)
+        end
+        for k in mut
+            allstar = allstars[k]
+            steps[k] = Step{T}(false, propose(dataset, allstar, before[k], temperature, curmaxsize, options),
+                               (allstar,), nothing)
         end
         # every :optimize proposal of this step, all islands, in one optimiser call
         to_opt = PopMember{T}[s.prop.member for s in steps if !s.crossover && s.prop.optimize]
@@ -492,10 +504,25 @@ temperature schedule, reg_evol_cycle_lockstep (or reg_evol_cycle_batched when
 options.fast_cycle), and each island's best-seen hall of fame. The head node
 calls it once per round with every island it would have spawned, instead of
 one @sr_spawner job per island (INTEGRATION.md §4).
+
+With options.recorder the lockstep loops would write no genealogy (the
+mutation / death events of src/RegularizedEvolution.jl:103-132), so every
+island runs the reference's own s_r_cycle instead, recording into records[k].
 """
 function s_r_cycle_lockstep(dataset::Dataset{T}, pops::AbstractVector{<:Population}, ncycles::Int,
                             curmaxsize::Int, stats::AbstractVector{RunningSearchStatistics},
-                            options::Options) where {T}
+                            options::Options; records=nothing) where {T}
+    if options.recorder
+        best_seen = Vector{HallOfFame{T}}(undef, length(pops))
+        num_evals = 0.0
+        for k in eachindex(pops)
+            rec = records === nothing ? RecordType() : records[k]
+            pops[k], best_seen[k], ev = s_r_cycle(dataset, pops[k], ncycles, curmaxsize, stats[k];
+                                                  options=options, record=rec)
+            num_evals += ev
+        end
+        return pops, best_seen, num_evals
+    end
     max_temp = T(1.0)
     min_temp = options.annealing ? T(0.0) : max_temp
     best_seen = [HallOfFame(options, T) for _ in pops]

@@ -125,6 +125,9 @@ ENV["SRHIP_DISABLE"] = "1" to force the reference path.
 """
 function enabled(options::Options)
     get(ENV, "SRHIP_DISABLE", "0") == "1" && return false
+    # the recorder's genealogy (src/Recorder.jl, Options.jl:597-599) is written by
+    # the reference's per-candidate loops: with it on, the search stays there
+    options.recorder && return false
     options.loss_function === nothing || return false
     device_available() || return false
     try
@@ -283,6 +286,36 @@ function eval_loss_batch(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, op
                     idx === nothing ? Ptr{Int64}(C_NULL) : pointer(rows), length(rows), sums, wsum, ok))
     end
     return [ok[i] == 1 ? T(sums[i] / wsum[]) : T(Inf) for i in 1:nt]
+end
+
+"""
+    eval_loss_batch_rowsets(trees, dataset, options, idx::Matrix{Int}) -> Vector{T}
+
+score_func_batch's loss (src/LossFunctions.jl:95-115) for every tree on its OWN
+row sample: idx is (batch_size, ntrees), column t the 1-based rows (with
+repetition) of trees[t] — one `StatsBase.sample(1:n, batch_size;
+replace=true)` per candidate, as the reference draws per call (:98). One
+launch (srhip_eval_loss_batch_rowsets_ctx); T(Inf) where evaluation fails.
+"""
+function eval_loss_batch_rowsets(trees::AbstractVector{Node{T}}, dataset::Dataset{T}, options::Options,
+                                 idx::AbstractMatrix{<:Integer}; device::Int=0) where {T}
+    nt = length(trees)
+    size(idx, 2) == nt || throw(ArgumentError("one row sample (column of idx) per tree"))
+    node_off, kind, arg, const_off, consts = flatten(trees, options)
+    sums = Vector{Float64}(undef, nt); ok = Vector{UInt8}(undef, nt); wsum = Vector{Float64}(undef, nt)
+    kindcode, param = loss_code(options.elementwise_loss)
+    params = Float64[param]
+    rows = Matrix{Int64}(idx .- 1)  # column-major: tree t's sample is contiguous ([ntrees][bs] in C)
+    GC.@preserve node_off kind arg const_off consts sums ok wsum params rows begin
+        tr = Ref(SrhipTrees(Int32(nt), pointer(node_off), pointer(kind), pointer(arg), pointer(const_off),
+                            Ptr{Cvoid}(pointer(consts))))
+        check(ccall((:srhip_eval_loss_batch_rowsets_ctx, libsrhip), Int32,
+                    (Ptr{Cvoid}, Ptr{Cvoid}, Ref{SrhipTrees}, Int32, Ptr{Float64}, Ptr{Int64}, Int64, Ptr{Float64},
+                     Ptr{Float64}, Ptr{UInt8}),
+                    context(device), device_dataset(dataset, device), tr, kindcode, params, rows,
+                    size(rows, 1), sums, wsum, ok))
+    end
+    return [ok[i] == 1 ? T(sums[i] / wsum[i]) : T(Inf) for i in 1:nt]
 end
 
 """

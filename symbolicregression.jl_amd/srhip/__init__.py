@@ -11,7 +11,7 @@ from .constant_optimization import ConstOptResult, optimize_constants_batch
 from .dataset import Dataset
 from .engine import Context, DeviceDataset, Program, device_count, get_context
 from .interface import (compile_trees, compute_complexity, eval_diff_tree_array, eval_grad_tree_array, eval_loss, eval_loss_batch,
-                        eval_loss_batch_ok, eval_loss_grad_batch,
+                        eval_loss_batch_ok, eval_loss_batch_rowsets, eval_loss_grad_batch,
                         eval_tree_array, loss_to_score, score_func, score_func_batch, score_func_batched,
                         update_baseline_loss_)
 from .node import (FlatTrees, Node, count_nodes, flatten, get_constants, has_constants, set_constants,

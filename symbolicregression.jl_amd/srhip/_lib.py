@@ -89,6 +89,10 @@ SIGNATURES = {
                               C.c_int64, C.c_void_p, C.POINTER(C.c_double), C.c_void_p],
     "srhip_eval_loss_batch_ctx": [C.c_void_p, C.c_void_p, C.POINTER(Trees), C.c_int32, C.c_void_p, C.c_void_p,
                                   C.c_int64, C.c_void_p, C.POINTER(C.c_double), C.c_void_p],
+    "srhip_eval_loss_rowsets": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_int64,
+                                C.c_void_p, C.c_void_p, C.c_void_p],
+    "srhip_eval_loss_batch_rowsets_ctx": [C.c_void_p, C.c_void_p, C.POINTER(Trees), C.c_int32, C.c_void_p,
+                                          C.c_void_p, C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p],
     "srhip_eval_tree_array": [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p],
     "srhip_eval_loss_grad": [C.c_void_p, C.c_void_p, C.c_int32, C.c_void_p, C.c_void_p, C.c_void_p,
                              C.POINTER(C.c_double), C.c_void_p],

@@ -3,6 +3,7 @@ tests/test_abi.py)."""
 
 F32, F64 = 0, 1
 PROGRAM_VARYING_CONSTANTS = 1  # srhip_program_create_ex flag (include/srhip.h)
+PROGRAM_INTERPRETED = 2  # srhip_program_create_ex flag: no loss / output tree code (include/srhip.h)
 X_JULIA, X_FEATURE_MAJOR = 0, 1
 NODE_CONST, NODE_FEATURE, NODE_UNARY, NODE_BINARY = 0, 1, 2, 3
 

@@ -157,7 +157,8 @@ class Program:
     varying_constants (SRHIP_PROGRAM_VARYING_CONSTANTS): the caller will set
     new constants, so Float32 tree code reads them from memory from the start."""
 
-    def __init__(self, ctx: Context, flat: FlatTrees, dtype, varying_constants: bool = False):
+    def __init__(self, ctx: Context, flat: FlatTrees, dtype, varying_constants: bool = False,
+                 interpreted: bool = False):
         self.ctx = ctx
         self.dtype = np.dtype(dtype)
         self.flat = flat
@@ -173,7 +174,8 @@ class Program:
         )
         h = C.c_void_p()
         check(lib().srhip_program_create_ex(ctx.handle, dtype_code(self.dtype), C.byref(tr),
-                                            K.PROGRAM_VARYING_CONSTANTS if varying_constants else 0, C.byref(h)))
+                                            (K.PROGRAM_VARYING_CONSTANTS if varying_constants else 0)
+                                            | (K.PROGRAM_INTERPRETED if interpreted else 0), C.byref(h)))
         self.handle = h
         self.ntrees = flat.ntrees
 
@@ -226,6 +228,21 @@ class Program:
         check(lib().srhip_eval_loss(ds.handle, self.handle, int(loss_kind), _p(par), _p(idx), nidx, _p(sums),
                                     C.byref(wsum), _p(ok)))
         return sums[:nt], wsum.value, ok[:nt].view(bool)  # 0/1 bytes: a view, no copy
+
+    def eval_loss_rowsets(self, ds: DeviceDataset, loss_kind: int, row_idx, params=None):
+        """srhip_eval_loss_rowsets: tree t on its own rows row_idx[t] (an
+        (ntrees, batch_size) integer array): (Σ w·ℓ per tree, Σ w per tree, ok)."""
+        nt = self.ntrees
+        idx = np.ascontiguousarray(row_idx, dtype=np.int64)
+        if idx.ndim != 2 or idx.shape[0] != nt:
+            raise ValueError("row_idx must be (ntrees, batch_size)")
+        sums = np.empty(max(nt, 1), dtype=np.float64)
+        wsum = np.empty(max(nt, 1), dtype=np.float64)
+        ok = np.empty(max(nt, 1), dtype=np.uint8)
+        par = None if params is None else np.asarray(params, dtype=np.float64)
+        check(lib().srhip_eval_loss_rowsets(ds.handle, self.handle, int(loss_kind), _p(par), _p(idx), idx.shape[1],
+                                            _p(sums), _p(wsum), _p(ok)))
+        return sums[:nt], wsum[:nt], ok[:nt].view(bool)
 
     def eval_loss_packed(self, ds: DeviceDataset, loss_kind: int, d_out: int, params=None):
         """srhip_eval_loss_packed: [Σw·ℓ, failed] per tree + Σw written to the

@@ -214,18 +214,35 @@ def eval_loss_batch_rowsets(trees: Sequence[Node], dataset: Dataset, options: Op
                             rows: Sequence[np.ndarray], device: Optional[int] = None
                             ) -> Tuple[np.ndarray, np.ndarray]:
     """score_func_batch's evaluation for many trees, tree t on its OWN row
-    sample rows[t] (with replacement, LossFunctions.jl:95-115): (losses in T,
-    did_succeed). Trees that share a sample share a launch."""
+    sample rows[t] (with replacement, LossFunctions.jl:95-115; the reference
+    draws one sample per call, :98): (losses in T, did_succeed). One engine
+    launch for all trees (srhip_eval_loss_rowsets) when the samples have one
+    length (the reference's batch_size); one per distinct length otherwise.
+    score_func_batch uses options.elementwise_loss even when loss_function is
+    set (:101-111), and so does this."""
     T = dataset.T
-    losses = np.zeros(len(trees), dtype=T)
-    ok = np.zeros(len(trees), dtype=bool)
-    groups = {}
+    n = len(trees)
+    losses = np.zeros(n, dtype=T)
+    ok = np.zeros(n, dtype=bool)
+    if n == 0:
+        return losses, ok
+    rows = [np.asarray(r, dtype=np.int64) for r in rows]
+    if len(rows) != n:
+        raise ValueError("one row sample per tree")
+    dev = dataset.device(device)
+    loss = options.elementwise_loss
+    by_len = {}
     for t, r in enumerate(rows):
-        groups.setdefault(np.asarray(r, dtype=np.int64).tobytes(), []).append(t)
-    for key, idx in groups.items():
-        r = np.frombuffer(key, dtype=np.int64)
-        l, k = eval_loss_batch_ok([trees[t] for t in idx], dataset, options, row_idx=r, device=device)
-        losses[idx] = l
+        by_len.setdefault(len(r), []).append(t)
+    for bs, idx in by_len.items():
+        sub = [trees[t] for t in idx]
+        prog = Program(dev.ctx, flatten(sub, options, dtype=T), T, interpreted=True)
+        R = np.stack([rows[t] for t in idx]) if bs else np.zeros((len(idx), 0), dtype=np.int64)
+        sums, wsum, k = prog.eval_loss_rowsets(dev, loss.kind, R, loss.params)
+        with np.errstate(invalid="ignore", divide="ignore"):
+            lv = (sums / wsum).astype(T)
+        lv[~k] = T(np.inf)
+        losses[idx] = lv
         ok[idx] = k
     return losses, ok
 
