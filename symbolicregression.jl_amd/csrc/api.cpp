@@ -201,6 +201,7 @@ struct srhip_ctx {
   int last_jit_trees = 0;  // trees the last evaluation ran as tree code
   int64_t last_redone = 0;  // tiles tree code redid with the PRECISE routines
   DevBuf partial, sums, oks, dloss, scratch_idx, gather, derived;
+  DevBuf gderived;  // [ngcol][n_pad] shared-subtree columns of the tree code (jit.h Columns)
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
   bool fail_clean = false;  // all of `fail` is zero: the finalize kernels clear the flags they read
   DevBuf ti_rec;  // threaded-interpreter records of the shallow f32 list
@@ -1542,7 +1543,16 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
           if (launches[li].part == 0) HIP_CHECK(jit::launch_derive(jm, X, n_pad, static_cast<float*>(c->derived.p), s));
           dcols = static_cast<const float*>(c->derived.p);
         }
-        HIP_CHECK(jit::launch(jm, launches[li].part, plan, a, jit_fast_enabled(), dcols, s));
+        // the shared subtrees of this call, once per row, before the first part
+        // (inside the timed region: their cost is the call's)
+        const float* gcols = nullptr;
+        if (jc.ngcol > 0) {
+          c->gderived.ensure((size_t)jc.ngcol * (size_t)n_pad * sizeof(float));
+          if (launches[li].part == 0)
+            HIP_CHECK(jit::launch_gderive(jm, X, n_pad, static_cast<float*>(c->gderived.p), s));
+          gcols = static_cast<const float*>(c->gderived.p);
+        }
+        HIP_CHECK(jit::launch(jm, launches[li].part, plan, a, jit_fast_enabled(), dcols, s, gcols));
       } else {
         HIP_CHECK(jit::launch64(jm64, launches[li].part, plan, a, s));
       }
@@ -2209,6 +2219,7 @@ int32_t srhip_close(srhip_ctx* ctx) {
       if (h) (void)hipHostFree(h);
     ctx->gpart.release();
     ctx->derived.release();
+    ctx->gderived.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return SRHIP_OK;

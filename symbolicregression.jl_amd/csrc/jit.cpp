@@ -37,8 +37,10 @@
 #include <cstdlib>
 #include <cstring>
 #include <atomic>
+#include <functional>
 #include <mutex>
 #include <thread>
+#include <unordered_map>
 
 #include "jit_asm.h"
 
@@ -102,6 +104,15 @@ bool loss_bails(int loss) {
 
 struct DerivedMap {
   const Columns* cols = nullptr;
+  // shared-subtree columns (Columns::gkey): key -> g, column gbase + g of the
+  // tree code; empty: none (memory-constant or per-row output code)
+  std::unordered_map<std::string, int> gidx;
+  int gbase = 1 << 30;
+  void set_shared(const Columns& c) {
+    gidx.clear();
+    for (int g = 0; g < c.ngcol; ++g) gidx.emplace(c.gkey[g], g);
+    gbase = c.gbase();
+  }
   int col(int op, int f) const {
     if (!cols) return -1;
     const uint32_t key = ((uint32_t)op << 16) | (uint32_t)f;
@@ -174,6 +185,136 @@ bool build_ir(const Ins<float>* p, std::vector<IrOp>& ops, Opnd& root, const Der
   }
 }
 
+// ---- shared subtrees (jit.h Columns::gkey) -----------------------------------------
+// The canonical text of an IR value's subtree in raw features, e.g.
+// "b3(u11(x3),x0)" for cos(x4) / x1 (an LDS-derived column spelled as its
+// u(x_f)), or "" when the subtree reads a constant: constants differ from
+// tree to tree, so only constant-free subtrees are shared.
+static std::string leaf_key(const Opnd& q, const Columns* cols) {
+  if (q.k != O_X) return "";
+  if (!q.der) return "x" + std::to_string(q.v);
+  if (cols && q.v >= cols->nraw && q.v < cols->nraw + cols->nder) {
+    const uint32_t d = cols->der[q.v - cols->nraw];
+    return "u" + std::to_string(d >> 16) + "(x" + std::to_string(d & 0xffffu) + ")";
+  }
+  return "";  // a shared-subtree column (keys are taken before the substitution)
+}
+// Per value: its key, and the SIMD cycles per 256-row tile that its subtree's
+// operators cost as FAST tree code and as PRECISE code (tools/census.py's
+// prices: a routine ~120 FAST, ~260 PRECISE; + - * neg abs square cube ~8),
+// its postfix stack depth and whether it holds a routine.
+struct SubtreeInfo {
+  std::vector<std::string> key;
+  std::vector<int> fast, precise, depth;
+  std::vector<char> routine;
+};
+static void subtree_keys(const std::vector<IrOp>& ops, const Columns* cols, SubtreeInfo& si) {
+  const size_t n = ops.size();
+  si.key.assign(n, std::string());
+  si.fast.assign(n, 0);
+  si.precise.assign(n, 0);
+  si.depth.assign(n, 1);
+  si.routine.assign(n, 0);
+  for (size_t i = 0; i < n; ++i) {
+    const IrOp& o = ops[i];
+    const bool inl = is_inline(o);
+    int f = inl ? 8 : 120, p = inl ? 8 : 260;
+    bool r = !inl;
+    auto part = [&](const Opnd& q, int* d) {
+      *d = 1;
+      if (q.k != O_VAL) {
+        if (q.k == O_X && q.der) *d = 2;  // u(x_f): feature then operator
+        return leaf_key(q, cols);
+      }
+      f += si.fast[q.v];
+      p += si.precise[q.v];
+      r = r || si.routine[q.v];
+      *d = si.depth[q.v];
+      return si.key[q.v];
+    };
+    int da = 1, db = 0;
+    const std::string ka = part(o.a, &da);
+    if (ka.empty()) continue;
+    if (o.un) {
+      si.key[i] = "u" + std::to_string(o.op) + "(" + ka + ")";
+    } else {
+      const std::string kb = part(o.b, &db);
+      if (kb.empty()) continue;
+      si.key[i] = "b" + std::to_string(o.op) + "(" + ka + "," + kb + ")";
+    }
+    si.fast[i] = f;
+    si.precise[i] = p;
+    si.routine[i] = r;
+    si.depth[i] = o.un ? da : std::max(da, db + 1);
+  }
+}
+// The postfix node stream (srhip_trees kinds / args, raw features) of a value.
+static void subtree_postfix(const std::vector<IrOp>& ops, const Opnd& q, const Columns* cols,
+                            std::vector<uint8_t>& kind, std::vector<uint16_t>& arg) {
+  if (q.k == O_X) {
+    if (!q.der) {
+      kind.push_back(SRHIP_NODE_FEATURE);
+      arg.push_back((uint16_t)q.v);
+    } else {
+      const uint32_t d = cols->der[q.v - cols->nraw];
+      kind.push_back(SRHIP_NODE_FEATURE);
+      arg.push_back((uint16_t)(d & 0xffffu));
+      kind.push_back(SRHIP_NODE_UNARY);
+      arg.push_back((uint16_t)(d >> 16));
+    }
+    return;
+  }
+  const IrOp& o = ops[q.v];
+  subtree_postfix(ops, o.a, cols, kind, arg);
+  if (!o.un) subtree_postfix(ops, o.b, cols, kind, arg);
+  kind.push_back(o.un ? SRHIP_NODE_UNARY : SRHIP_NODE_BINARY);
+  arg.push_back((uint16_t)o.op);
+}
+// Every maximal shared subtree of the IR becomes a read of its column (O_X,
+// der, column gbase + g); the operations that only it used are dropped.
+// Returns false (IR unchanged) when the tree holds none.
+static bool substitute_shared(std::vector<IrOp>& ops, Opnd& root, const DerivedMap& dm) {
+  if (dm.gidx.empty()) return false;
+  SubtreeInfo si;
+  subtree_keys(ops, dm.cols, si);
+  bool any = false;
+  std::vector<char> live(ops.size(), 0);
+  std::function<void(Opnd&)> rw = [&](Opnd& q) {
+    if (q.k != O_VAL) return;
+    if (!si.key[q.v].empty()) {
+      auto it = dm.gidx.find(si.key[q.v]);
+      if (it != dm.gidx.end()) {
+        Opnd x;
+        x.k = O_X;
+        x.v = dm.gbase + it->second;
+        x.der = true;
+        q = x;
+        any = true;
+        return;
+      }
+    }
+    live[q.v] = 1;
+    IrOp& o = ops[q.v];
+    rw(o.a);
+    if (!o.un) rw(o.b);
+  };
+  rw(root);
+  if (!any) return false;
+  std::vector<int> nid(ops.size(), -1);
+  std::vector<IrOp> out;
+  for (size_t i = 0; i < ops.size(); ++i) {
+    if (!live[i]) continue;
+    IrOp o = ops[i];
+    if (o.a.k == O_VAL) o.a.v = nid[o.a.v];
+    if (!o.un && o.b.k == O_VAL) o.b.v = nid[o.b.v];
+    nid[i] = (int)out.size();
+    out.push_back(o);
+  }
+  if (root.k == O_VAL) root.v = nid[root.v];
+  ops.swap(out);
+  return true;
+}
+
 // ---- code generation of one tree --------------------------------------------------
 struct Gen {
   Asm& as;
@@ -201,6 +342,14 @@ struct Gen {
   std::string why;
   bool out = false;              // per-row output code (Options::out)
   int out_rreg = -1;             // the root block of the tile (out mode)
+  // shared-subtree columns (jit.h Columns): O_X columns from gbase on are read
+  // from device memory — s[36:37] = column 0 at this row group's first row,
+  // s38 = the column stride in bytes (the driver's, jit_template.hip) — with
+  // one global load each at the tile start; gwaited: their vmcnt wait is done
+  int gbase = 1 << 30;
+  bool gwaited = true;
+  static constexpr int S_GCOL = 36, S_GSTRIDE = 38;
+  bool is_g(int v) const { return v >= gbase; }
 
   // SRHIP_JIT_TRIG_FULL=1 (tests): sin / cos through the complete compiled
   // routines instead of the hand-scheduled FAST bodies
@@ -423,6 +572,8 @@ struct Gen {
     }
     if (!usef(root, n)) return false;
     if (root.k == O_X) xinl[root.v] = true;
+    for (int f : feats)
+      if (is_g(f)) xinl[f] = true;  // a shared-subtree column is loaded once, at the tile start
     {
       std::vector<int> pre;
       for (int f : feats)
@@ -431,7 +582,7 @@ struct Gen {
     }
     if ((int)feats.size() > NPOOL) { why = "more features than register blocks"; return false; }
     for (int f : feats)
-      if ((1 + f) * TILE * 4 + 3 * 4 * 64 > 65535) { why = "feature offset beyond the DS immediate"; return false; }
+      if (!is_g(f) && (1 + f) * TILE * 4 + 3 * 4 * 64 > 65535) { why = "feature offset beyond the DS immediate"; return false; }
     next_call.assign(n + 1, n);
     for (int i = n - 1; i >= 0; --i) next_call[i] = ops[i].rid >= 0 ? i : next_call[i + 1];
     loc.assign(n, L_NONE);
@@ -448,6 +599,10 @@ struct Gen {
 
   void wait_for(const Opnd& q) {
     if (q.k != O_X) return;
+    if (is_g(q.v)) {
+      if (!gwaited) { as.waitcnt_vm(0); gwaited = true; }
+      return;
+    }
     const int li = load_idx[q.v];
     if (li >= waited) {
       as.waitcnt_lgkm(nloads - 1 - li);
@@ -459,6 +614,7 @@ struct Gen {
       as.waitcnt_lgkm(0);
       waited = nloads;
     }
+    if (!gwaited) { as.waitcnt_vm(0); gwaited = true; }
   }
   int free_block() const {
     for (int k = 0; k < NPOOL; ++k)
@@ -502,7 +658,7 @@ struct Gen {
   }
   // a call operand into block `dst` (A or B): features not preloaded (or all
   // of them with xdirect) are read from the LDS tile, other operands moved
-  bool load_x_direct(const Opnd& q) const { return q.k == O_X && (xdirect || xblk[q.v] < 0); }
+  bool load_x_direct(const Opnd& q) const { return q.k == O_X && !is_g(q.v) && (xdirect || xblk[q.v] < 0); }
   void operand_to(int dst, const Opnd& q, bool* issued) {
     if (load_x_direct(q)) {
       as.ds_read_b128(dst, VLANE, (1 + q.v) * TILE * 4);
@@ -868,12 +1024,38 @@ struct Gen {
       as.ds_read_b128(VY, VLANE, 0);
       ++nloads;
     }
+    bool gany = false;
     for (size_t j = 0; j < feats.size(); ++j) {
       const int f = feats[j];
       xblk[f] = (int)j;
       pool_owner[j] = 1000 + f;
+      if (is_g(f)) { gany = true; continue; }
       load_idx[f] = nloads++;
       as.ds_read_b128(VPOOL0 + R * (int)j, VLANE, (1 + f) * TILE * 4);
+    }
+    // shared-subtree columns: this tile's rows of column g at s[36:37] +
+    // tile·1024 + g·stride + lane·16, one 1 KiB global load per wave each
+    // (s0..s3 are routine temporaries, free until the first call)
+    gwaited = !gany;
+    if (gany) {
+      as.vop2(VOP2_LSHLREV_B32, "v_lshlrev_b32_e32", VGT, K(2), VLANE4);
+      as.sop2(SOP2_LSHL_B32, "s_lshl_b32", 0, S(S_TILE), K(10));
+      as.sop2(SOP2_ADD_U32, "s_add_u32", 0, S(S_GCOL), S(0));
+      as.sop2(SOP2_ADDC_U32, "s_addc_u32", 1, S(S_GCOL + 1), K(0));
+      for (size_t j = 0; j < feats.size(); ++j) {
+        const int f = feats[j];
+        if (!is_g(f)) continue;
+        const uint32_t g = (uint32_t)(f - gbase);
+        int sb = 0;
+        if (g > 0) {
+          as.sop2(SOP2_MUL_I32, "s_mul_i32", 2, S(S_GSTRIDE), K(g));
+          as.sop2(SOP2_MUL_HI_U32, "s_mul_hi_u32", 3, S(S_GSTRIDE), K(g));
+          as.sop2(SOP2_ADD_U32, "s_add_u32", 2, S(0), S(2));
+          as.sop2(SOP2_ADDC_U32, "s_addc_u32", 3, S(1), S(3));
+          sb = 2;
+        }
+        as.global_load_dwordx4(VPOOL0 + R * (int)j, VGT, sb, 0);
+      }
     }
     std::fill(loc.begin(), loc.end(), (int)L_NONE);
     for (int i = 0; i < (int)ops.size(); ++i) {
@@ -1127,15 +1309,36 @@ static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool 
   Opnd root;
   if (!build_ir(prog, ir, root, &dm)) { *why = "program not translatable"; return false; }
   const size_t start = (out.size() + 15) / 16 * 16;  // 64-byte aligned entries
+  // shared subtrees read from their columns; a tree whose code then does not
+  // fit (its columns and features exceed the register blocks) computes them
+  std::vector<IrOp> ir0;
+  Opnd root0 = root;
+  const bool shared = !memc && !out_mode && !dm.gidx.empty();
+  if (shared) ir0 = ir;
+  const bool subst = shared && substitute_shared(ir, root, dm);
   Asm as;
-  as.want_text = text;
-  Gen g(as, T, area_va + start * 4, fast_opt && loss != SRHIP_LOSS_PERIODIC && !out_mode);
-  g.out = out_mode;
-  g.memc = memc;
-  g.loss = loss;
-  g.lparam = lparam;
-  if (!g.emit_tree(ir, root)) { *why = g.why; return false; }
-  g.emit_tail();
+  for (int attempt = 0;; ++attempt) {
+    as = Asm();
+    as.want_text = text;
+    Gen g(as, T, area_va + start * 4, fast_opt && loss != SRHIP_LOSS_PERIODIC && !out_mode);
+    g.out = out_mode;
+    g.memc = memc;
+    g.loss = loss;
+    g.lparam = lparam;
+    if (subst && attempt == 0) g.gbase = dm.gbase;
+    if (!g.emit_tree(ir, root)) {
+      if (subst && attempt == 0) {
+        ir = ir0;
+        root = root0;
+        continue;
+      }
+      *why = g.why;
+      return false;
+    }
+    g.emit_tail();
+    *is_fast = g.fast;
+    break;
+  }
   as.finish();
   while (out.size() < start) {  // s_nop padding
     out.push_back(0xbf800000u);
@@ -1147,7 +1350,6 @@ static bool gen_tree(const Ins<float>* prog, const Tmpl& T, bool fast_opt, bool 
     lines->insert(lines->end(), as.lines.begin(), as.lines.end());
   }
   *off = (int32_t)(start * 4);
-  *is_fast = g.fast;
   return true;
 }
 
@@ -1169,6 +1371,10 @@ struct Module {
   std::vector<ModulePart> parts;
   uint32_t* d_bail = nullptr;  // [nslots + 2]: bail flags of all slots, bail count, PRECISE redo count
   int nslots = 0;
+  // the shared subtrees' postfix streams in device memory (launch_gderive)
+  uint8_t* d_gkind = nullptr;
+  uint16_t* d_garg = nullptr;
+  int32_t* d_goff = nullptr;
 };
 
 bool available() { return templates().ok; }
@@ -1222,6 +1428,7 @@ static bool codegen_par(const CompiledBatch<float>& cb, const std::vector<int32_
                         const Columns& cols, size_t* stop) {
   DerivedMap dm;
   dm.cols = &cols;
+  dm.set_shared(cols);
   const size_t n = cand.size() - from;
   struct R { std::vector<uint32_t> w; bool ok = false, fast = false; std::string why; size_t start = 0; };
   std::vector<R> res(n);
@@ -1295,6 +1502,7 @@ static size_t codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>
   }
   DerivedMap dm;
   dm.cols = &cols;
+  dm.set_shared(cols);
   for (size_t k = from; k < cand.size(); ++k) {
     const int32_t t = cand[k];
     int32_t off = -1;
@@ -1351,6 +1559,89 @@ int choose_waves(int nraw) {
 size_t lds_per_workgroup(int waves) {
   const int per_cu = std::max(1, 20 / std::max(1, waves));
   return (size_t)160 * 1024 / (size_t)per_cu;
+}
+
+// The shared-subtree columns of a batch (jit.h Columns::gkey): the
+// constant-free subtrees holding a routine, counted per occurrence in the
+// trees' IR (after the LDS columns). Largest first, a subtree is kept when
+// its occurrences save more FAST tree-code cycles than twice what the derive
+// pass spends on it PRECISE (count·(fast − 16) > 2·precise: a read costs a
+// load and a block); a kept subtree's occurrences are taken off the subtrees
+// inside it. At most SRHIP_JIT_GCOLS (default 64; 0: none) columns, the most
+// profitable ones; none for per-row output or memory-constant code (their
+// constants change; their drivers pass no column base).
+static void plan_shared(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt, bool on,
+                        Columns& c) {
+  const char* ge = std::getenv("SRHIP_JIT_GCOLS");  // read per build: A/B tests
+  const int gmax = ge ? std::max(0, std::min(kMaxGlobalCols, std::atoi(ge))) : 64;
+  const int room = std::min(gmax, 255 - c.gbase());
+  if (!on || opt.out || opt.memc || room <= 0) return;
+  struct Info {
+    int count = 0, fast = 0, precise = 0, size = 0;
+    std::vector<std::string> kids;
+    std::vector<uint8_t> kind;
+    std::vector<uint16_t> arg;
+  };
+  std::unordered_map<std::string, Info> info;
+  DerivedMap dm;
+  dm.cols = &c;
+  std::vector<IrOp> ir;
+  Opnd root;
+  SubtreeInfo si;
+  for (int32_t t : cand) {
+    if (cb.tree_off[t] < 0 || !build_ir(&cb.code[cb.tree_off[t]], ir, root, &dm)) continue;
+    subtree_keys(ir, &c, si);
+    for (size_t i = 0; i < ir.size(); ++i) {
+      if (si.key[i].empty() || !si.routine[i] || si.depth[i] > 8) continue;
+      Info& I = info[si.key[i]];
+      if (I.count++ == 0) {
+        I.fast = si.fast[i];
+        I.precise = si.precise[i];
+        I.size = (int)si.key[i].size();
+        for (const Opnd* q : {&ir[i].a, &ir[i].b}) {
+          if (q == &ir[i].b && ir[i].un) break;
+          if (q->k == O_VAL && !si.key[q->v].empty()) I.kids.push_back(si.key[q->v]);
+        }
+        Opnd v;
+        v.k = O_VAL;
+        v.v = (int)i;
+        subtree_postfix(ir, v, &c, I.kind, I.arg);
+      }
+    }
+  }
+  std::vector<std::pair<const std::string*, Info*>> order;
+  for (auto& kv : info) order.push_back({&kv.first, &kv.second});
+  std::sort(order.begin(), order.end(), [](const auto& a, const auto& b) {
+    return a.second->size != b.second->size ? a.second->size > b.second->size : *a.first < *b.first;
+  });
+  std::function<void(const std::string&, int)> absorb = [&](const std::string& k, int n) {
+    auto it = info.find(k);
+    if (it == info.end()) return;
+    it->second.count -= n;
+    for (const std::string& kid : it->second.kids) absorb(kid, n);
+  };
+  std::vector<std::pair<int64_t, const std::string*>> kept;
+  for (auto& e : order) {
+    const Info& I = *e.second;
+    const int64_t gain = (int64_t)I.count * (I.fast - 16) - 2 * (int64_t)I.precise;
+    if (I.count < 2 || gain <= 0) continue;
+    kept.push_back({gain, e.first});
+    for (const std::string& kid : I.kids) absorb(kid, I.count);
+  }
+  std::stable_sort(kept.begin(), kept.end(), [](const auto& a, const auto& b) { return a.first > b.first; });
+  if ((int)kept.size() > room) kept.resize(room);
+  c.goff.assign(1, 0);
+  for (auto& kv : kept) {
+    const Info& I = info[*kv.second];
+    c.gkey.push_back(*kv.second);
+    c.gkind.insert(c.gkind.end(), I.kind.begin(), I.kind.end());
+    c.garg.insert(c.garg.end(), I.arg.begin(), I.arg.end());
+    c.goff.push_back((int32_t)c.gkind.size());
+  }
+  c.ngcol = (int)kept.size();
+  if (std::getenv("SRHIP_JIT_DEBUG"))
+    for (size_t g = 0; g < kept.size(); ++g)
+      std::fprintf(stderr, "jit: shared column %zu: %s gain %lld\n", g, kept[g].second->c_str(), (long long)kept[g].first);
 }
 
 // The derived columns of a batch: every u(x_f) (u a routine operator) used by
@@ -1417,6 +1708,7 @@ static Columns plan_columns(const CompiledBatch<float>& cb, const std::vector<in
   }
   c.nder = (int)chosen.size();
   for (int k = 0; k < c.nder; ++k) c.der[k] = chosen[k];
+  plan_shared(cb, cand, opt, on, c);
   return c;
 }
 
@@ -1526,6 +1818,14 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       m->nslots += pt.nslots;
       jit_list.insert(jit_list.end(), ch.slots.begin(), ch.slots.end());
     }
+    if (cols.ngcol > 0) {
+      HIP_CHECK(hipMalloc((void**)&m->d_gkind, cols.gkind.size()));
+      HIP_CHECK(hipMalloc((void**)&m->d_garg, cols.garg.size() * sizeof(uint16_t)));
+      HIP_CHECK(hipMalloc((void**)&m->d_goff, cols.goff.size() * sizeof(int32_t)));
+      HIP_CHECK(hipMemcpy(m->d_gkind, cols.gkind.data(), cols.gkind.size(), hipMemcpyHostToDevice));
+      HIP_CHECK(hipMemcpy(m->d_garg, cols.garg.data(), cols.garg.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
+      HIP_CHECK(hipMemcpy(m->d_goff, cols.goff.data(), cols.goff.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
     HIP_CHECK(hipMalloc((void**)&m->d_bail, (size_t)(m->nslots + 2) * sizeof(uint32_t)));
     // clean from the start: each call's finalize leaves the counters clean again
     HIP_CHECK(hipMemset(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t)));
@@ -1550,6 +1850,9 @@ void destroy(Module* m) {
     if (q.mod) (void)hipModuleUnload(q.mod);
   }
   if (m->d_bail) (void)hipFree(m->d_bail);
+  if (m->d_gkind) (void)hipFree(m->d_gkind);
+  if (m->d_garg) (void)hipFree(m->d_garg);
+  if (m->d_goff) (void)hipFree(m->d_goff);
   delete m;
 }
 
@@ -1575,6 +1878,7 @@ struct JitArgs {
   const float* dcols;
   int nbig, ts;
   int dyn;
+  const float* gcols;  // [ngcol][n_pad] shared-subtree columns of this call, or null
 };
 struct DeriveArgs {
   const float* X;
@@ -1597,6 +1901,11 @@ hipError_t launch_derive(Module* m, const float* X, int64_t n_pad, float* out, h
   const unsigned gx = (unsigned)std::min<int64_t>(1024, (n_pad / 4 + 255) / 256);
   return hipModuleLaunchKernel(m->parts[0].fn_derive, std::max(gx, 1u), (unsigned)m->cols.nder, 1, 256, 1, 1, 0,
                                stream, nullptr, cfg);
+}
+
+hipError_t launch_gderive(Module* m, const float* X, int64_t n_pad, float* out, hipStream_t stream) {
+  if (m->cols.ngcol == 0) return hipSuccess;
+  return launch_derive_columns(m->d_gkind, m->d_garg, m->d_goff, m->cols.ngcol, X, n_pad, out, stream);
 }
 
 int64_t flag_words(Module* m) { return (int64_t)m->nslots + 2; }
@@ -1622,7 +1931,7 @@ static bool dynloop() {
 }
 
 hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, const float* dcols,
-                  hipStream_t stream) {
+                  hipStream_t stream, const float* gcols) {
   const ModulePart& q = m->parts[k];
   if (a.nlist != q.nslots) return hipErrorInvalidValue;
   if (m->out && (a.w != nullptr || a.out == nullptr || a.out_stride < a.n_pad)) return hipErrorInvalidValue;
@@ -1636,6 +1945,10 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   ja.nder = m->cols.nder;
   std::memcpy(ja.der, m->cols.der, sizeof(ja.der));
   ja.dcols = dcols;
+  // shared-subtree columns: tree code reads them (jit_template.hip passes
+  // s[36:37] = gcols + row0, s38 = n_pad·4)
+  if (m->cols.ngcol > 0 && (!gcols || (uint64_t)a.n_pad * 4u > 0xffffffffu)) return hipErrorInvalidValue;
+  ja.gcols = m->cols.ngcol > 0 ? gcols : nullptr;
   ja.nbig = plan.nbig >= 0 ? plan.nbig : a.nrg;
   ja.ts = plan.nbig >= 0 ? plan.ts : plan.ntiles;
   // Sticky PRECISE per tree across row groups (prefetching hand-written loop):

@@ -343,6 +343,15 @@ struct Asm {
     if (want_text) t("ds_read_b128 v[" + std::to_string(vdst) + ":" + std::to_string(vdst + 3) + "], v" + std::to_string(vaddr) +
       (offset ? " offset:" + std::to_string(offset) : ""));
   }
+  // global_load_dwordx4 v[vdst:vdst+3], v[vaddr], s[saddr:saddr+1] offset:off (13-bit signed)
+  void global_load_dwordx4(int vdst, int vaddr, int saddr, int off) {
+    put(0xdc5c8000u | ((uint32_t)off & 0x1fffu));
+    put((uint32_t)vaddr | ((uint32_t)saddr << 16) | ((uint32_t)vdst << 24));
+    if (want_text)
+      t("global_load_dwordx4 v[" + std::to_string(vdst) + ":" + std::to_string(vdst + 3) + "], v" + std::to_string(vaddr) +
+        ", s[" + std::to_string(saddr) + ":" + std::to_string(saddr + 1) + "]" + (off ? " offset:" + std::to_string(off) : ""));
+  }
+  void waitcnt_vm(int n) { sopp(0x0c, "s_waitcnt", 0x0f70 | (n & 15), false); if (want_text) lines.back() = "s_waitcnt vmcnt(" + std::to_string(n) + ")"; }
   void waitcnt_lgkm(int n) { sopp(0x0c, "s_waitcnt", 0xc07f | (n << 8), false); if (want_text) lines.back() = "s_waitcnt lgkmcnt(" + std::to_string(n) + ")"; }
 
   void finish() {
@@ -373,7 +382,7 @@ enum : int {
   VOPC_NGE_F32 = 0x49, VOPC_NGT_F32 = 0x4b, VOPC_NLE_F32 = 0x4c,
   SOP1_MOV = 0x00, SOP1_GETPC = 0x1c, SOP1_SETPC = 0x1d, SOP1_SWAPPC = 0x1e,
   SOP2_ADD_U32 = 0x00, SOP2_SUB_U32 = 0x01, SOP2_SUB_I32 = 0x03, SOP2_SUBB_U32 = 0x05, SOP2_ADDC_U32 = 0x04, SOP2_CSELECT = 0x0a,
-  SOP2_AND_B32 = 0x0c,
+  SOP2_AND_B32 = 0x0c, SOP2_LSHL_B32 = 0x1c, SOP2_MUL_I32 = 0x24, SOP2_MUL_HI_U32 = 0x2c,
   SOPC_EQ_U32 = 0x06, SOPC_LG_U32 = 0x07, SOPC_GE_U32 = 0x09, SOPC_LT_U32 = 0x0a, SOPC_LG_U64 = 0x13,
   SOPP_BRANCH = 0x02, SOPP_SCC0 = 0x04, SOPP_SCC1 = 0x05, SOPP_VCCNZ = 0x07,
 };

@@ -85,6 +85,8 @@ struct JitArgs {
   int nbig;                 // row groups [0, nbig) hold e.ntiles tiles; the tail row groups after them
   int ts;                   // hold ts tiles each (the last round of workgroups in smaller pieces)
   int dyn;                  // hand-written prefetching loop: a tree redone PRECISE in one row group runs PRECISE in the later ones
+  const float* gcols;       // [ngcol][n_pad] shared-subtree columns (jit.h Columns), or null: tree code
+                            // reads column g of this row group at s[36:37] + g·s38 (literal code only)
 };
 
 // A derived column's value: the PRECISE routine of the operator (the same
@@ -104,6 +106,12 @@ __device__ __forceinline__ float derive_uop(int op, float x) {
 #undef SR_DERIVE_CASE
     default: return __builtin_nanf("");  // not derivable: jit.cpp never asks
   }
+}
+
+// a wave-uniform 64-bit value in an SGPR pair (inline-asm operands pinned to SGPRs)
+__device__ __forceinline__ uint64_t sgpr64(uint64_t v) {
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)v) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(v >> 32)) << 32);
 }
 
 // OUT: per-row output tree code (srhip_eval_tree_array): no y column is
@@ -200,6 +208,9 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const uint32_t partial = (uint32_t)last_valid;
   const uint32_t nt_u = (uint32_t)nt_valid;
   const uint32_t fastok = (uint32_t)ja.fast;
+  // shared-subtree columns: column 0 at this row group's first row, column stride in bytes
+  const uint64_t gcb = sgpr64(ja.gcols ? reinterpret_cast<uint64_t>(ja.gcols + row0) : 0ull);
+  const uint32_t gstride = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a.n_pad * 4));
 
   int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
   while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
@@ -255,7 +266,7 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
                      : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status),
                        "+{s84}"(redos)
                      : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial),
-                       "{s67}"(tilebytes), "{s68}"(woff), "{s79}"(fastok)
+                       "{s67}"(tilebytes), "{s68}"(woff), "{s79}"(fastok), "{s[36:37]}"(gcb), "{s38}"(gstride)
                      : SR_JIT_CLOBBERS, "memory");
       }
       if (__builtin_amdgcn_readfirstlane((int)status) != 0) {
@@ -703,6 +714,8 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
   const uint64_t failp = reinterpret_cast<uint64_t>(a.fail), codep = reinterpret_cast<uint64_t>(ja.code_off);
   const uint64_t dstp = reinterpret_cast<uint64_t>(gdst), bailp = reinterpret_cast<uint64_t>(ja.bail);
   const uint64_t cntp = reinterpret_cast<uint64_t>(ja.counters);
+  const uint64_t gcb = sgpr64(ja.gcols ? reinterpret_cast<uint64_t>(ja.gcols + row0) : 0ull);
+  const uint32_t gstride = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a.n_pad * 4));
   uint32_t redos = 0;
   if constexpr (MEMC) {
     const uint64_t progp = reinterpret_cast<uint64_t>(a.prog), lop = reinterpret_cast<uint64_t>(a.list_off);
@@ -729,7 +742,7 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
         : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
           "{s68}"(woff), "{s45}"(fastflags), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
           "{s[46:47]}"(failp), "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s52}"(plds), "{s53}"(spart),
-          "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area)
+          "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area), "{s[36:37]}"(gcb), "{s38}"(gstride)
         : SR_JIT_CLOBBERS, "s23", "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s79", "s91", "s94", "s95",
           "s96", "s97", "v40", "v41", "v42", "v89", "v90", "v91", "v92", "memory");
   } else {
@@ -742,7 +755,7 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
         : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
           "{s68}"(woff), "{s79}"(fastok), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist),
           "{s[46:47]}"(failp), "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s52}"(plds), "{s53}"(spart),
-          "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area)
+          "{s[54:55]}"(bailp), "{s[92:93]}"(cntp), "{s[88:89]}"(area), "{s[36:37]}"(gcb), "{s38}"(gstride)
         : SR_JIT_CLOBBERS, "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s91", "s94", "s95", "s96", "s97",
           "v40", "v41", "v42", "v89", "v90", "v91", "memory");
   }

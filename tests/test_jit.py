@@ -80,6 +80,21 @@ def test_every_tree_of_config2_compiles():
     print(f"{len(offs)} trees, {len(code) / len(offs):.0f} bytes per tree")
 
 
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+def test_shared_subtree_columns_equal_llvm_mc():
+    """Config #2's shared subtrees (cos(x_f), exp(cos(x_f)), x_i / x_j, ...) are
+    read from their columns with global loads (jit.h Columns::gkey): the code
+    holds them, its bytes are llvm-mc's, and memory-constant code (whose
+    driver passes no column base) holds none."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    flat = srhip.flatten(srhip.random_population(1500, o, 5, np.float32, seed=1000), o, dtype=np.float32)
+    code, text, offs = jit_compile(flat)
+    assert text.count("global_load_dwordx4") > 500 and "s_waitcnt vmcnt(0)" in text
+    assert assemble(text) == code
+    _, text_m, _ = jit_compile(flat, memc=True)
+    assert "global_load_dwordx4" not in text_m
+
+
 def test_memory_constant_code_loads_every_constant():
     """Memory-constant tree code (set_constants without new code): no
     literal of the tree's constants remains in its code, and every constant
