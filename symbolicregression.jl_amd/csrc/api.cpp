@@ -202,6 +202,7 @@ struct srhip_ctx {
   int64_t last_redone = 0;  // tiles tree code redid with the PRECISE routines
   DevBuf partial, sums, oks, dloss, scratch_idx, gather, derived;
   DevBuf gderived;  // [ngcol][n_pad] shared-subtree columns of the tree code (jit.h Columns)
+  DevBuf gpartial, gsum, gok, gti;  // their derive pass's partials, per-column results, threaded records
   DevBuf fail;  // [list slots] early-exit flags of the eval kernel (MODE_LOSS)
   bool fail_clean = false;  // all of `fail` is zero: the finalize kernels clear the flags they read
   DevBuf ti_rec;  // threaded-interpreter records of the shallow f32 list
@@ -325,6 +326,11 @@ struct srhip_program {
   // byte capacities of the device buffers above (kept across rebuilds)
   size_t code_cap = 0, toff_cap = 0, list_cap = 0;
   size_t gcode_cap = 0, gtoff_cap = 0, gitems_cap = 0, gconst_cap = 0;
+  // the shared subtrees of the tree code (jit.h Columns) as a program of their
+  // own, run by the interpreter's per-row output mode once per call
+  // (derive_shared); built at the first call that needs it
+  mutable srhip_program* shared = nullptr;
+  mutable std::vector<std::string> shared_keys;
 };
 
 namespace {
@@ -454,6 +460,12 @@ void free_loss_jits(const srhip_program* p) {
 }
 
 void free_program_device(srhip_program* p) {
+  if (p->shared) {
+    free_program_device(p->shared);
+    delete p->shared;
+    p->shared = nullptr;
+    p->shared_keys.clear();
+  }
   jit::destroy(p->jit);
   p->jit = nullptr;
   jit::destroy64(p->jit64);
@@ -989,6 +1001,8 @@ void build_program(srhip_program* p) {
   p->h_cprev = p->consts;
 }
 
+void build_program_f32(srhip_program* p) { build_program<float>(p); }
+
 // srhip_program_set_constants: new immediates written into the host image
 // through its constant map (patch_image) and the device programs overwritten
 // in place (no reallocation, no list rebuild; the gradient programs are
@@ -1374,6 +1388,96 @@ jit::GradModule64* grad_module64(srhip_program* p, int loss, double lparam) {
   return m;
 }
 
+// The shared subtrees of a tree-code module (jit.h Columns), once per row of
+// the call, into c->gderived ([ngcol][n_pad]): the subtrees are a program of
+// their own (p->shared, interpreted, no tree code) run in the interpreter's
+// per-row output mode — the interpreter's values, which the tree code's
+// PRECISE routines equal bit for bit — and its finalize gives each subtree's
+// did_succeed over the call's rows; a subtree that failed (some node
+// non-finite on some row) has its whole column set to NaN, so every tree
+// that reads it fails, as DynamicExpressions fails a tree with a non-finite
+// node on any row (src/InterfaceDynamicExpressions.jl:17-48).
+void derive_shared(srhip_ctx* c, const srhip_program* p, const jit::Columns& jc, const float* X, int64_t rows,
+                   int64_t n_pad, int nfeat) {
+  hipStream_t s = c->stream;
+  if (!p->shared || p->shared_keys != jc.gkey) {
+    if (p->shared) {
+      free_program_device(p->shared);
+      delete p->shared;
+      p->shared = nullptr;
+    }
+    auto* q = new srhip_program();
+    q->ctx = c;
+    q->dtype = SRHIP_F32;
+    q->ntrees = jc.ngcol;
+    q->jit_allowed = false;
+    q->node_off.assign(jc.goff.begin(), jc.goff.end());
+    q->const_off.assign((size_t)jc.ngcol + 1, 0);
+    q->kind = jc.gkind;
+    q->arg = jc.garg;
+    q->consts.resize(1);
+    try {
+      build_program_f32(q);
+    } catch (...) {
+      free_program_device(q);
+      delete q;
+      throw;
+    }
+    p->shared = q;
+    p->shared_keys = jc.gkey;
+  }
+  const srhip_program* q = p->shared;
+  const int ng = jc.ngcol;
+  c->gderived.ensure((size_t)ng * (size_t)n_pad * sizeof(float));
+  c->gsum.ensure((size_t)ng * sizeof(double));
+  c->gok.ensure((size_t)ng);
+  float* out = static_cast<float*>(c->gderived.p);
+  if (q->nlist_a + q->nlist_b != ng) throw Error(SRHIP_ERR_INVALID, "shared subtree failed statically");
+  const int lists[2][2] = {{0, q->nlist_a}, {q->nlist_a, q->nlist_b}};
+  for (int pass = 0; pass < 2; ++pass) {
+    const int s0 = lists[pass][0], nlist = lists[pass][1];
+    if (nlist == 0) continue;
+    EvalPlan plan;
+    if (!plan_eval(SRHIP_F32, pass == 1, q->opset, MODE_OUT, false, nfeat, rows, nlist, &plan))
+      throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
+    EvalArgs<float> a;
+    a.prog = static_cast<const Ins<float>*>(q->d_code);
+    a.tree_off = q->d_tree_off;
+    a.list = q->d_list + s0;
+    a.list_off = q->d_list + (q->nlist_a + q->nlist_b) + s0;
+    a.fail = nullptr;
+    a.ti_rec = nullptr;
+    if (ti_enabled() && pass == 0) {
+      c->gti.ensure((size_t)nlist * 64 * sizeof(uint4));
+      HIP_CHECK(launch_ti_records(a.prog, a.list_off, nlist, (uint32_t)(plan.ntiles * plan.tile * sizeof(float)),
+                                  static_cast<uint4*>(c->gti.p), s));
+      a.ti_rec = static_cast<const uint4*>(c->gti.p);
+    }
+    a.nlist = nlist;
+    a.X = X;
+    a.y = nullptr;
+    a.w = nullptr;
+    a.n = rows;
+    a.n_pad = n_pad;
+    a.nfeat = nfeat;
+    a.ntiles = plan.ntiles;
+    a.ntg = plan.ntg;
+    a.tpb = plan.tpb;
+    a.nrg = plan.nrg;
+    a.loss = SRHIP_LOSS_L2;
+    a.rotate = interp_dyn() ? 4 : 0;
+    a.contig = 0;
+    a.lparam = 0.0;
+    c->gpartial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<float>));
+    a.partial = static_cast<Part<float>*>(c->gpartial.p);
+    a.out = out;
+    a.out_stride = n_pad;
+    HIP_CHECK(launch_eval<float>(plan, a, MODE_OUT, s));
+    HIP_CHECK(launch_finalize<float>(a, static_cast<double*>(c->gsum.p), static_cast<uint8_t*>(c->gok.p), s));
+  }
+  HIP_CHECK(launch_poison_columns(static_cast<const uint8_t*>(c->gok.p), ng, out, n_pad, s));
+}
+
 // Run the evaluation kernels for both tree lists. The view (X, y, w, rows,
 // n_pad) may be the dataset itself or a gathered row subset.
 template <typename T>
@@ -1547,9 +1651,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
         // (inside the timed region: their cost is the call's)
         const float* gcols = nullptr;
         if (jc.ngcol > 0) {
-          c->gderived.ensure((size_t)jc.ngcol * (size_t)n_pad * sizeof(float));
-          if (launches[li].part == 0)
-            HIP_CHECK(jit::launch_gderive(jm, X, n_pad, static_cast<float*>(c->gderived.p), s));
+          if (launches[li].part == 0) derive_shared(c, p, jc, X, rows, n_pad, nfeat);
           gcols = static_cast<const float*>(c->gderived.p);
         }
         HIP_CHECK(jit::launch(jm, launches[li].part, plan, a, jit_fast_enabled(), dcols, s, gcols));
@@ -2220,6 +2322,10 @@ int32_t srhip_close(srhip_ctx* ctx) {
     ctx->gpart.release();
     ctx->derived.release();
     ctx->gderived.release();
+    ctx->gpartial.release();
+    ctx->gsum.release();
+    ctx->gok.release();
+    ctx->gti.release();
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
     return SRHIP_OK;

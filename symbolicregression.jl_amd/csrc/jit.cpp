@@ -240,7 +240,9 @@ static void subtree_keys(const std::vector<IrOp>& ops, const Columns* cols, Subt
     } else {
       const std::string kb = part(o.b, &db);
       if (kb.empty()) continue;
-      si.key[i] = "b" + std::to_string(o.op) + "(" + ka + "," + kb + ")";
+      // + and * commute exactly in IEEE arithmetic: one key for both orders
+      const bool comm = o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_MUL;
+      si.key[i] = "b" + std::to_string(o.op) + "(" + (comm && kb < ka ? kb + "," + ka : ka + "," + kb) + ")";
     }
     si.fast[i] = f;
     si.precise[i] = p;
@@ -348,6 +350,41 @@ struct Gen {
   // one global load each at the tile start; gwaited: their vmcnt wait is done
   int gbase = 1 << 30;
   bool gwaited = true;
+  // the global loads of the tile in issue order: column f is load gidx[f] of
+  // gnum; loads return in issue order (gfx9 vmcnt), so its wait is
+  // vmcnt(gnum - 1 - gidx[f]) and later columns may still be in flight
+  int gidx[256];
+  int gnum = 0, gdone = 0;
+  bool gany = false;   // the tree reads shared-subtree columns
+  // SRHIP_JIT_GPREFETCH=1 (read per build): the next tile's column loads
+  // issued at the end of the current one instead of at its start; measured
+  // no faster (config #2 2.589 vs 2.563 ms, interleaved, profiles/r06_ab_build1.jsonl)
+  bool gprefetch = [] { const char* e = std::getenv("SRHIP_JIT_GPREFETCH"); return e && e[0] == '1'; }();
+  int L_reload = -1;   // issue this tile's column loads, then the tile (a FAST redo)
+  // The column loads of tile S_TILE into their pool blocks (xblk): issued
+  // before the tile runs — for the first tile in the prologue, for the next
+  // one at the end of the current tile (their latency under its tail and the
+  // next tile's LDS reads) — and again before a redone tile.
+  void emit_gloads() {
+    as.vop2(VOP2_LSHLREV_B32, "v_lshlrev_b32_e32", VGT, K(2), VLANE4);  // lane·16
+    as.sop2(SOP2_LSHL_B32, "s_lshl_b32", 0, S(S_TILE), K(10));         // tile·1024
+    as.sop2(SOP2_ADD_U32, "s_add_u32", 0, S(S_GCOL), S(0));
+    as.sop2(SOP2_ADDC_U32, "s_addc_u32", 1, S(S_GCOL + 1), K(0));
+    for (size_t j = 0; j < feats.size(); ++j) {
+      const int f = feats[j];
+      if (!is_g(f)) continue;
+      const uint32_t g = (uint32_t)(f - gbase);
+      int sb = 0;
+      if (g > 0) {
+        as.sop2(SOP2_MUL_I32, "s_mul_i32", 2, S(S_GSTRIDE), K(g));
+        as.sop2(SOP2_MUL_HI_U32, "s_mul_hi_u32", 3, S(S_GSTRIDE), K(g));
+        as.sop2(SOP2_ADD_U32, "s_add_u32", 2, S(0), S(2));
+        as.sop2(SOP2_ADDC_U32, "s_addc_u32", 3, S(1), S(3));
+        sb = 2;
+      }
+      as.global_load_dwordx4(VPOOL0 + R * (int)j, VGT, sb, 0);
+    }
+  }
   static constexpr int S_GCOL = 36, S_GSTRIDE = 38;
   bool is_g(int v) const { return v >= gbase; }
 
@@ -600,7 +637,12 @@ struct Gen {
   void wait_for(const Opnd& q) {
     if (q.k != O_X) return;
     if (is_g(q.v)) {
-      if (!gwaited) { as.waitcnt_vm(0); gwaited = true; }
+      const int k = gidx[q.v];
+      if (k >= gdone) {
+        as.waitcnt_vm(gnum - 1 - k);
+        gdone = k + 1;
+        gwaited = gdone == gnum;
+      }
       return;
     }
     const int li = load_idx[q.v];
@@ -614,7 +656,7 @@ struct Gen {
       as.waitcnt_lgkm(0);
       waited = nloads;
     }
-    if (!gwaited) { as.waitcnt_vm(0); gwaited = true; }
+    if (!gwaited) { as.waitcnt_vm(0); gwaited = true; gdone = gnum; }
   }
   int free_block() const {
     for (int k = 0; k < NPOOL; ++k)
@@ -1009,8 +1051,22 @@ struct Gen {
     }
     as.sopc(SOPC_GE_U32, "s_cmp_ge_u32", S(S_TILE), S(S_NT));
     as.branch(SOPP_SCC1, "s_cbranch_scc1", L_done);
+    // the pool blocks of the preloaded features and columns (first-use order),
+    // the columns' load order
+    gany = false;
+    gnum = 0;
+    for (size_t j = 0; j < feats.size(); ++j) {
+      xblk[feats[j]] = (int)j;
+      if (is_g(feats[j])) { gany = true; gidx[feats[j]] = gnum++; }
+    }
+    if (gany && gprefetch) {
+      L_reload = as.label();
+      as.bind(L_reload);
+      emit_gloads();
+    }
     // ---- tile
     as.bind(L_tile);
+    if (gany && !gprefetch) emit_gloads();  // each tile issues its own column loads
     if (fast || has_trig) as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHKSAVE, V(VCHK));  // for a redo / bail
     if (g_can) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGCAN, K(0xbf800000u));   // -1
     if (g_min) as.vop1(VOP1_MOV, "v_mov_b32_e32", VGMIN, K(0x3f800000u));   // 1
@@ -1024,39 +1080,15 @@ struct Gen {
       as.ds_read_b128(VY, VLANE, 0);
       ++nloads;
     }
-    bool gany = false;
     for (size_t j = 0; j < feats.size(); ++j) {
       const int f = feats[j];
-      xblk[f] = (int)j;
       pool_owner[j] = 1000 + f;
-      if (is_g(f)) { gany = true; continue; }
+      if (is_g(f)) continue;  // in flight since the tile's column loads (emit_gloads)
       load_idx[f] = nloads++;
       as.ds_read_b128(VPOOL0 + R * (int)j, VLANE, (1 + f) * TILE * 4);
     }
-    // shared-subtree columns: this tile's rows of column g at s[36:37] +
-    // tile·1024 + g·stride + lane·16, one 1 KiB global load per wave each
-    // (s0..s3 are routine temporaries, free until the first call)
     gwaited = !gany;
-    if (gany) {
-      as.vop2(VOP2_LSHLREV_B32, "v_lshlrev_b32_e32", VGT, K(2), VLANE4);
-      as.sop2(SOP2_LSHL_B32, "s_lshl_b32", 0, S(S_TILE), K(10));
-      as.sop2(SOP2_ADD_U32, "s_add_u32", 0, S(S_GCOL), S(0));
-      as.sop2(SOP2_ADDC_U32, "s_addc_u32", 1, S(S_GCOL + 1), K(0));
-      for (size_t j = 0; j < feats.size(); ++j) {
-        const int f = feats[j];
-        if (!is_g(f)) continue;
-        const uint32_t g = (uint32_t)(f - gbase);
-        int sb = 0;
-        if (g > 0) {
-          as.sop2(SOP2_MUL_I32, "s_mul_i32", 2, S(S_GSTRIDE), K(g));
-          as.sop2(SOP2_MUL_HI_U32, "s_mul_hi_u32", 3, S(S_GSTRIDE), K(g));
-          as.sop2(SOP2_ADD_U32, "s_add_u32", 2, S(0), S(2));
-          as.sop2(SOP2_ADDC_U32, "s_addc_u32", 3, S(1), S(3));
-          sb = 2;
-        }
-        as.global_load_dwordx4(VPOOL0 + R * (int)j, VGT, sb, 0);
-      }
-    }
+    gdone = 0;
     std::fill(loc.begin(), loc.end(), (int)L_NONE);
     for (int i = 0; i < (int)ops.size(); ++i) {
       if (ops[i].rid >= 0) { if (!emit_call(i)) return false; }
@@ -1275,7 +1307,13 @@ struct Gen {
     as.vop2(VOP2_ADD_U32, "v_add_u32_e32", VLANE, S(S_TILEBYTES), VLANE);
     as.sop2(SOP2_ADD_U32, "s_add_u32", S_TILE, S(S_TILE), K(1));
     as.sopc(SOPC_LT_U32, "s_cmp_lt_u32", S(S_TILE), S(S_NT));
-    as.branch(SOPP_SCC1, "s_cbranch_scc1", L_tile);
+    if (gany && gprefetch) {  // the next tile's column loads before it starts
+      as.branch(SOPP_SCC0, "s_cbranch_scc0", L_done);
+      emit_gloads();
+      as.branch(SOPP_BRANCH, "s_branch", L_tile);
+    } else {
+      as.branch(SOPP_SCC1, "s_cbranch_scc1", L_tile);
+    }
     as.bind(L_done);
     as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(S_RT), "");
     if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(S_RT) + ":" + std::to_string(S_RT + 1) + "]";
@@ -1285,11 +1323,12 @@ struct Gen {
       as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHK, V(VCHKSAVE));
       as.sop1(SOP1_MOV, "s_mov_b32", S_MODE, K(1), "s" + std::to_string(S_MODE));
       shift_base(true);
-      as.branch(SOPP_BRANCH, "s_branch", L_tile);
+      as.branch(SOPP_BRANCH, "s_branch", (gany && gprefetch) ? L_reload : L_tile);  // the columns' blocks were reused
     }
     if (has_trig) {
       as.bind(L_bail);
       as.waitcnt_lgkm(0);
+      if (gany) as.waitcnt_vm(0);  // no column load may land after the tree has returned
       as.vop1(VOP1_MOV, "v_mov_b32_e32", VCHK, V(VCHKSAVE));
       as.sop1(SOP1_MOV, "s_mov_b32", S_STATUS, K(1), "s" + std::to_string(S_STATUS));
       as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(S_RT), "");
@@ -1371,10 +1410,6 @@ struct Module {
   std::vector<ModulePart> parts;
   uint32_t* d_bail = nullptr;  // [nslots + 2]: bail flags of all slots, bail count, PRECISE redo count
   int nslots = 0;
-  // the shared subtrees' postfix streams in device memory (launch_gderive)
-  uint8_t* d_gkind = nullptr;
-  uint16_t* d_garg = nullptr;
-  int32_t* d_goff = nullptr;
 };
 
 bool available() { return templates().ok; }
@@ -1567,13 +1602,13 @@ size_t lds_per_workgroup(int waves) {
 // its occurrences save more FAST tree-code cycles than twice what the derive
 // pass spends on it PRECISE (count·(fast − 16) > 2·precise: a read costs a
 // load and a block); a kept subtree's occurrences are taken off the subtrees
-// inside it. At most SRHIP_JIT_GCOLS (default 64; 0: none) columns, the most
-// profitable ones; none for per-row output or memory-constant code (their
+// inside it. At most SRHIP_JIT_GCOLS (default 32; 0: none) columns, the most
+// profitable ones (32: config #2 2.66 ms against 2.68 at 16 and 3.00 at 64 with the derive pass, profiles/r06_gcols_ab.txt); none for per-row output or memory-constant code (their
 // constants change; their drivers pass no column base).
 static void plan_shared(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt, bool on,
                         Columns& c) {
   const char* ge = std::getenv("SRHIP_JIT_GCOLS");  // read per build: A/B tests
-  const int gmax = ge ? std::max(0, std::min(kMaxGlobalCols, std::atoi(ge))) : 64;
+  const int gmax = ge ? std::max(0, std::min(kMaxGlobalCols, std::atoi(ge))) : 32;
   const int room = std::min(gmax, 255 - c.gbase());
   if (!on || opt.out || opt.memc || room <= 0) return;
   struct Info {
@@ -1818,14 +1853,6 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       m->nslots += pt.nslots;
       jit_list.insert(jit_list.end(), ch.slots.begin(), ch.slots.end());
     }
-    if (cols.ngcol > 0) {
-      HIP_CHECK(hipMalloc((void**)&m->d_gkind, cols.gkind.size()));
-      HIP_CHECK(hipMalloc((void**)&m->d_garg, cols.garg.size() * sizeof(uint16_t)));
-      HIP_CHECK(hipMalloc((void**)&m->d_goff, cols.goff.size() * sizeof(int32_t)));
-      HIP_CHECK(hipMemcpy(m->d_gkind, cols.gkind.data(), cols.gkind.size(), hipMemcpyHostToDevice));
-      HIP_CHECK(hipMemcpy(m->d_garg, cols.garg.data(), cols.garg.size() * sizeof(uint16_t), hipMemcpyHostToDevice));
-      HIP_CHECK(hipMemcpy(m->d_goff, cols.goff.data(), cols.goff.size() * sizeof(int32_t), hipMemcpyHostToDevice));
-    }
     HIP_CHECK(hipMalloc((void**)&m->d_bail, (size_t)(m->nslots + 2) * sizeof(uint32_t)));
     // clean from the start: each call's finalize leaves the counters clean again
     HIP_CHECK(hipMemset(m->d_bail, 0, (size_t)(m->nslots + 2) * sizeof(uint32_t)));
@@ -1850,9 +1877,6 @@ void destroy(Module* m) {
     if (q.mod) (void)hipModuleUnload(q.mod);
   }
   if (m->d_bail) (void)hipFree(m->d_bail);
-  if (m->d_gkind) (void)hipFree(m->d_gkind);
-  if (m->d_garg) (void)hipFree(m->d_garg);
-  if (m->d_goff) (void)hipFree(m->d_goff);
   delete m;
 }
 
@@ -1901,11 +1925,6 @@ hipError_t launch_derive(Module* m, const float* X, int64_t n_pad, float* out, h
   const unsigned gx = (unsigned)std::min<int64_t>(1024, (n_pad / 4 + 255) / 256);
   return hipModuleLaunchKernel(m->parts[0].fn_derive, std::max(gx, 1u), (unsigned)m->cols.nder, 1, 256, 1, 1, 0,
                                stream, nullptr, cfg);
-}
-
-hipError_t launch_gderive(Module* m, const float* X, int64_t n_pad, float* out, hipStream_t stream) {
-  if (m->cols.ngcol == 0) return hipSuccess;
-  return launch_derive_columns(m->d_gkind, m->d_garg, m->d_goff, m->cols.ngcol, X, n_pad, out, stream);
 }
 
 int64_t flag_words(Module* m) { return (int64_t)m->nslots + 2; }

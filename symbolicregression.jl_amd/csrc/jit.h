@@ -42,12 +42,13 @@ struct Options {
 // features 0 .. nraw-1, the derived columns, w.
 constexpr int kMaxDerived = 48;
 // Shared subtrees (round 6): a constant-free subtree that several trees of the
-// batch contain (cos(x4), exp(x1), cos(exp(x2)), x1 / cos(x3), ...) is
-// evaluated once per row per call by the derive pass (kernels.hip
-// derive_columns_kernel: the interpreter's operators, NaN on every row where
-// some node of the subtree is non-finite) into a column of device memory,
-// [ngcol][n_pad], and the tree code reads it with a global load at the tile
-// start instead of computing it (tree code column gbase() + g).
+// batch contain (cos(x4), exp(x1), cos(exp(x2)), x1 / x3, ...) is evaluated
+// once per row per call by the derive pass (api.cpp derive_shared: the
+// interpreter's per-row outputs of the subtrees as a program of their own; a
+// subtree non-finite at some node on some row has its whole column set to
+// NaN) into a column of device memory, [ngcol][n_pad], and the tree code reads
+// it with a global load at the tile start instead of computing it (tree code
+// column gbase() + g).
 constexpr int kMaxGlobalCols = 128;
 struct Columns {
   int nraw = 0;                  // raw feature columns staged (max feature used + 1)
@@ -125,14 +126,12 @@ int64_t flag_words(Module* m);
 // list_off / fail / partial of the part's slots).
 // dcols: the derived columns of this call ([nder][n_pad], launch_derive), or
 // null: the driver computes the staged ones itself
-// gcols: the shared-subtree columns of this call ([ngcol][n_pad], launch_gderive), or
+// gcols: the shared-subtree columns of this call ([ngcol][n_pad], api.cpp derive_shared), or
 // null when the module has none
 hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, const float* dcols,
                   hipStream_t stream, const float* gcols = nullptr);
 // out[k][r] = u_k(x_{f_k}[r]) for the module's derived columns (nothing to do when there are none)
 hipError_t launch_derive(Module* m, const float* X, int64_t n_pad, float* out, hipStream_t stream);
-// out[g][r] = the module's shared subtree g at row r (NaN where it fails), r < n_pad
-hipError_t launch_gderive(Module* m, const float* X, int64_t n_pad, float* out, hipStream_t stream);
 
 // Test hook: compile without loading; returns bytes and (opt.text) the
 // assembly text of the whole area image.

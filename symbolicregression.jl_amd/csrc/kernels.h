@@ -155,11 +155,9 @@ hipError_t launch_pack_x(const T* src, int layout, int64_t src_stride,
 template <typename T>
 hipError_t launch_pack_vec(const T* src, int64_t rows, int64_t n_pad, T* dst,
                            hipStream_t stream);
-// Shared-subtree columns (jit.h Columns): out[g][r] = subtree g at row r of X
-// ([nfeat][n_pad]), NaN where a node of it is non-finite; kind / arg / off
-// (device memory) are the subtrees' postfix node streams, at most 8 values deep.
-hipError_t launch_derive_columns(const uint8_t* kind, const uint16_t* arg, const int32_t* off, int ncol,
-                                 const float* X, int64_t n_pad, float* out, hipStream_t stream);
+// Shared-subtree columns (jit.h Columns): every row of column g of cols
+// ([ncol][n_pad]) set to NaN when ok[g] == 0 (device memory).
+hipError_t launch_poison_columns(const uint8_t* ok, int ncol, float* cols, int64_t n_pad, hipStream_t stream);
 // Row gather for score_func_batch: dst[f][k] = src[f][idx[k]] (+ y, w);
 // seg > 0: one sample of nidx rows per segment of seg rows (per-tree samples,
 // srhip_eval_loss_rowsets), idx = [dst_pad / seg][nidx].

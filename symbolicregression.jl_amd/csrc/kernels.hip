@@ -6,7 +6,6 @@
 
 #include <cstdlib>
 
-#include "device_ops.h"
 #include "kernels.h"
 
 #include <algorithm>
@@ -139,83 +138,25 @@ __global__ void gather_rows_kernel(const T* __restrict__ X, const T* __restrict_
   }
 }
 
-// ---- shared-subtree columns (jit.h Columns, round 6) ---------------------------
-// One value of a shared subtree with the interpreter's operators (interp.h
-// un_apply / bin_apply call the same dev::uop / dev::bop); a node whose value
-// is not finite makes the row's value NaN, which is what the tree reading the
-// column then carries: DynamicExpressions fails a tree when any node's value
-// is non-finite on any row, and NaN reaches the tree code's root check or a
-// lossy operator's input mark like any other non-finite value.
-__device__ __forceinline__ float dc_uop(int op, float x) {
-  switch (op) {
-#define SR_DC_U(U) case U: return dev::uop<U>(x);
-    SR_DC_U(SRHIP_UOP_NEG) SR_DC_U(SRHIP_UOP_SQUARE) SR_DC_U(SRHIP_UOP_CUBE) SR_DC_U(SRHIP_UOP_EXP)
-    SR_DC_U(SRHIP_UOP_ABS) SR_DC_U(SRHIP_UOP_LOG) SR_DC_U(SRHIP_UOP_LOG2) SR_DC_U(SRHIP_UOP_LOG10)
-    SR_DC_U(SRHIP_UOP_LOG1P) SR_DC_U(SRHIP_UOP_SQRT) SR_DC_U(SRHIP_UOP_SIN) SR_DC_U(SRHIP_UOP_COS)
-    SR_DC_U(SRHIP_UOP_TAN) SR_DC_U(SRHIP_UOP_SINH) SR_DC_U(SRHIP_UOP_COSH) SR_DC_U(SRHIP_UOP_TANH)
-    SR_DC_U(SRHIP_UOP_ATAN) SR_DC_U(SRHIP_UOP_ASINH) SR_DC_U(SRHIP_UOP_ACOSH) SR_DC_U(SRHIP_UOP_ATANH_CLIP)
-    SR_DC_U(SRHIP_UOP_ERF) SR_DC_U(SRHIP_UOP_ERFC) SR_DC_U(SRHIP_UOP_GAMMA) SR_DC_U(SRHIP_UOP_RELU)
-    SR_DC_U(SRHIP_UOP_ROUND) SR_DC_U(SRHIP_UOP_FLOOR) SR_DC_U(SRHIP_UOP_CEIL) SR_DC_U(SRHIP_UOP_SIGN)
-    SR_DC_U(SRHIP_UOP_INV)
-#undef SR_DC_U
-    default: return __builtin_nanf("");
-  }
-}
-__device__ __forceinline__ float dc_bop(int op, float x, float y) {
-  switch (op) {
-#define SR_DC_B(B) case B: return dev::bop<B>(x, y);
-    SR_DC_B(SRHIP_BOP_ADD) SR_DC_B(SRHIP_BOP_SUB) SR_DC_B(SRHIP_BOP_MUL) SR_DC_B(SRHIP_BOP_DIV)
-    SR_DC_B(SRHIP_BOP_POW) SR_DC_B(SRHIP_BOP_GREATER) SR_DC_B(SRHIP_BOP_LOGICAL_OR)
-    SR_DC_B(SRHIP_BOP_LOGICAL_AND) SR_DC_B(SRHIP_BOP_MOD) SR_DC_B(SRHIP_BOP_MAX) SR_DC_B(SRHIP_BOP_MIN)
-#undef SR_DC_B
-    default: return __builtin_nanf("");
-  }
-}
-
-// out[g][r] for column g = blockIdx.y, rows r < n_pad (padding rows repeat the
-// last row, as X does): a postfix program of at most kDeriveStack live values,
-// wave-uniform (every lane runs the same node sequence), one row per lane.
-constexpr int kDeriveStack = 8;
-__global__ void __launch_bounds__(256) derive_columns_kernel(const uint8_t* __restrict__ kind,
-                                                             const uint16_t* __restrict__ arg,
-                                                             const int32_t* __restrict__ off, const float* __restrict__ X,
-                                                             int64_t n_pad, float* __restrict__ out) {
+// Columns of shared subtrees (jit.h Columns) whose subtree failed somewhere
+// (ok[g] == 0: a node non-finite on some row) become NaN on every row, so
+// every tree reading the column fails, as DynamicExpressions fails a tree
+// whose node is non-finite on any row.
+__global__ void __launch_bounds__(256) poison_columns_kernel(const uint8_t* __restrict__ ok, float* __restrict__ cols,
+                                                            int64_t n_pad) {
   const int g = blockIdx.y;
-  const auto* ko = (const __attribute__((address_space(4))) uint8_t*)kind;
-  const auto* ao = (const __attribute__((address_space(4))) uint16_t*)arg;
-  const auto* oo = (const __attribute__((address_space(4))) int32_t*)off;
-  const int n0 = oo[g], n1 = oo[g + 1];
-  float* o = out + (size_t)g * n_pad;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x) {
-    float st[kDeriveStack];
-    int sp = 0;
-    bool bad = false;
-    for (int k = n0; k < n1; ++k) {
-      const int kd = ko[k], a = ao[k];
-      float v;
-      if (kd == SRHIP_NODE_FEATURE) {
-        v = X[(size_t)a * n_pad + i];
-      } else if (kd == SRHIP_NODE_UNARY) {
-        v = dc_uop(a, st[--sp]);
-      } else {
-        const float y = st[--sp];
-        v = dc_bop(a, st[--sp], y);
-      }
-      bad = bad || !__builtin_isfinite(v);
-      st[sp++] = v;
-    }
-    o[i] = bad ? __builtin_nanf("") : st[0];
-  }
+  if (ok[g]) return;
+  float* o = cols + (size_t)g * n_pad;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n_pad; i += (int64_t)gridDim.x * blockDim.x)
+    o[i] = __builtin_nanf("");
 }
 
 }  // namespace
 
-hipError_t launch_derive_columns(const uint8_t* kind, const uint16_t* arg, const int32_t* off, int ncol,
-                                 const float* X, int64_t n_pad, float* out, hipStream_t stream) {
+hipError_t launch_poison_columns(const uint8_t* ok, int ncol, float* cols, int64_t n_pad, hipStream_t stream) {
   if (ncol <= 0 || n_pad <= 0) return hipSuccess;
-  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_pad + 255) / 256, 2048));
-  hipLaunchKernelGGL(derive_columns_kernel, dim3(gx, (unsigned)ncol), dim3(256), 0, stream, kind, arg, off, X,
-                     n_pad, out);
+  const unsigned gx = (unsigned)std::max<int64_t>(1, std::min<int64_t>((n_pad + 255) / 256, 512));
+  hipLaunchKernelGGL(poison_columns_kernel, dim3(gx, (unsigned)ncol), dim3(256), 0, stream, ok, cols, n_pad);
   return hipGetLastError();
 }
 
