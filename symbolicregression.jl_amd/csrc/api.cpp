@@ -331,6 +331,9 @@ struct srhip_program {
   // (derive_shared); built at the first call that needs it
   mutable srhip_program* shared = nullptr;
   mutable std::vector<std::string> shared_keys;
+  // the same for the gradient tree code's columns (jit::grad_columns)
+  mutable srhip_program* gshared = nullptr;
+  mutable std::vector<std::string> gshared_keys;
 };
 
 namespace {
@@ -460,12 +463,14 @@ void free_loss_jits(const srhip_program* p) {
 }
 
 void free_program_device(srhip_program* p) {
-  if (p->shared) {
-    free_program_device(p->shared);
-    delete p->shared;
-    p->shared = nullptr;
-    p->shared_keys.clear();
-  }
+  for (srhip_program** q : {&p->shared, &p->gshared})
+    if (*q) {
+      free_program_device(*q);
+      delete *q;
+      *q = nullptr;
+    }
+  p->shared_keys.clear();
+  p->gshared_keys.clear();
   jit::destroy(p->jit);
   p->jit = nullptr;
   jit::destroy64(p->jit64);
@@ -1397,14 +1402,16 @@ jit::GradModule64* grad_module64(srhip_program* p, int loss, double lparam) {
 // non-finite on some row) has its whole column set to NaN, so every tree
 // that reads it fails, as DynamicExpressions fails a tree with a non-finite
 // node on any row (src/InterfaceDynamicExpressions.jl:17-48).
-void derive_shared(srhip_ctx* c, const srhip_program* p, const jit::Columns& jc, const float* X, int64_t rows,
-                   int64_t n_pad, int nfeat) {
+// slot / keys: the program's cache of the subtree program (p->shared for the
+// loss tree code, p->gshared for the gradient tree code).
+void derive_shared(srhip_ctx* c, srhip_program*& slot, std::vector<std::string>& keys, const jit::Columns& jc,
+                   const float* X, int64_t rows, int64_t n_pad, int nfeat) {
   hipStream_t s = c->stream;
-  if (!p->shared || p->shared_keys != jc.gkey) {
-    if (p->shared) {
-      free_program_device(p->shared);
-      delete p->shared;
-      p->shared = nullptr;
+  if (!slot || keys != jc.gkey) {
+    if (slot) {
+      free_program_device(slot);
+      delete slot;
+      slot = nullptr;
     }
     auto* q = new srhip_program();
     q->ctx = c;
@@ -1423,10 +1430,10 @@ void derive_shared(srhip_ctx* c, const srhip_program* p, const jit::Columns& jc,
       delete q;
       throw;
     }
-    p->shared = q;
-    p->shared_keys = jc.gkey;
+    slot = q;
+    keys = jc.gkey;
   }
-  const srhip_program* q = p->shared;
+  const srhip_program* q = slot;
   const int ng = jc.ngcol;
   c->gderived.ensure((size_t)ng * (size_t)n_pad * sizeof(float));
   c->gsum.ensure((size_t)ng * sizeof(double));
@@ -1440,6 +1447,8 @@ void derive_shared(srhip_ctx* c, const srhip_program* p, const jit::Columns& jc,
     EvalPlan plan;
     if (!plan_eval(SRHIP_F32, pass == 1, q->opset, MODE_OUT, false, nfeat, rows, nlist, &plan))
       throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
+    if (plan.tile % 256 != 0)  // the tree code reads whole 256-row tiles of the columns
+      throw Error(SRHIP_ERR_INVALID, "shared-subtree derive pass: tile of " + std::to_string(plan.tile) + " rows");
     EvalArgs<float> a;
     a.prog = static_cast<const Ins<float>*>(q->d_code);
     a.tree_off = q->d_tree_off;
@@ -1651,7 +1660,7 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
         // (inside the timed region: their cost is the call's)
         const float* gcols = nullptr;
         if (jc.ngcol > 0) {
-          if (launches[li].part == 0) derive_shared(c, p, jc, X, rows, n_pad, nfeat);
+          if (launches[li].part == 0) derive_shared(c, p->shared, p->shared_keys, jc, X, rows, n_pad, nfeat);
           gcols = static_cast<const float*>(c->gderived.p);
         }
         HIP_CHECK(jit::launch(jm, launches[li].part, plan, a, jit_fast_enabled(), dcols, s, gcols));
@@ -1999,6 +2008,16 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
         c->fail_clean = false;  // the gradient kernels leave their flags set
         HIP_CHECK(hipMemsetAsync(c->fail.p, 0, (size_t)nsl_all * sizeof(uint32_t), s));
         c->gpart.ensure(std::max<size_t>((size_t)plans[0].nrg * nconst, 1) * sizeof(float));
+        // the shared subtrees' columns of this call (jit::grad_columns), timed with the call
+        const jit::Columns& gcj = jit::grad_columns(gm);
+        const float* gcols = nullptr;
+        if (gcj.ngcol > 0) {
+          const int tk = timed_begin(c, s);
+          derive_shared(c, p->gshared, p->gshared_keys, gcj, static_cast<const float*>(ds->X), ds->rows, ds->n_pad,
+                        ds->nfeat);
+          timed_end(c, s, tk);
+          gcols = static_cast<const float*>(c->gderived.p);
+        }
         for (int k = 0; k < nparts; ++k) {
           int s0, nsl;
           jit::grad_part(gm, k, &s0, &nsl);
@@ -2025,7 +2044,7 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
           a.partial = static_cast<Part<float>*>(c->partial.p);
           const int tk = timed_begin(c, s);
           HIP_CHECK(jit::launch_grad_code(gm, k, plan, a, p->d_gconsts, static_cast<float*>(c->gpart.p), nconst,
-                                          s));
+                                          s, gcols));
           timed_end(c, s, tk);
           HIP_CHECK(launch_finalize<float>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
           static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;

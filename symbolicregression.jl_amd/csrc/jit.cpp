@@ -1605,12 +1605,14 @@ size_t lds_per_workgroup(int waves) {
 // inside it. At most SRHIP_JIT_GCOLS (default 32; 0: none) columns, the most
 // profitable ones (32: config #2 2.66 ms against 2.68 at 16 and 3.00 at 64 with the derive pass, profiles/r06_gcols_ab.txt); none for per-row output or memory-constant code (their
 // constants change; their drivers pass no column base).
-static void plan_shared(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, const Options& opt, bool on,
-                        Columns& c) {
-  const char* ge = std::getenv("SRHIP_JIT_GCOLS");  // read per build: A/B tests
-  const int gmax = ge ? std::max(0, std::min(kMaxGlobalCols, std::atoi(ge))) : 32;
+// precise: the tree code runs its routines PRECISE (the gradient code's
+// forward), so an occurrence saves the PRECISE price; env: the cap's variable.
+static void plan_shared(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, bool on, Columns& c,
+                        bool precise = false, const char* env = "SRHIP_JIT_GCOLS", int dflt = 32) {
+  const char* ge = std::getenv(env);  // read per build: A/B tests
+  const int gmax = ge ? std::max(0, std::min(kMaxGlobalCols, std::atoi(ge))) : dflt;
   const int room = std::min(gmax, 255 - c.gbase());
-  if (!on || opt.out || opt.memc || room <= 0) return;
+  if (!on || room <= 0) return;
   struct Info {
     int count = 0, fast = 0, precise = 0, size = 0;
     std::vector<std::string> kids;
@@ -1630,7 +1632,7 @@ static void plan_shared(const CompiledBatch<float>& cb, const std::vector<int32_
       if (si.key[i].empty() || !si.routine[i] || si.depth[i] > 8) continue;
       Info& I = info[si.key[i]];
       if (I.count++ == 0) {
-        I.fast = si.fast[i];
+        I.fast = precise ? si.precise[i] : si.fast[i];
         I.precise = si.precise[i];
         I.size = (int)si.key[i].size();
         for (const Opnd* q : {&ir[i].a, &ir[i].b}) {
@@ -1743,7 +1745,17 @@ static Columns plan_columns(const CompiledBatch<float>& cb, const std::vector<in
   }
   c.nder = (int)chosen.size();
   for (int k = 0; k < c.nder; ++k) c.der[k] = chosen[k];
-  plan_shared(cb, cand, opt, on, c);
+  plan_shared(cb, cand, on && !opt.out && !opt.memc, c);
+  return c;
+}
+
+Columns plan_grad_columns(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand) {
+  Columns c;
+  c.nraw = kGradGbase;  // raw features stay below (the gradient code's DS immediates end at feature 62)
+  static const bool env_on = [] { const char* e = std::getenv("SRHIP_JIT_DERIVE"); return !(e && e[0] == '0'); }();
+  // 64: config #5's shard gradient 42.2 ms against 42.8 at 32 and 45.9 without (interleaved,
+  // tools/ab_build.py --grad, profiles/r06_grad_gcols_ab.txt)
+  plan_shared(cb, cand, env_on, c, /*precise=*/true, "SRHIP_GJIT_GCOLS", 64);
   return c;
 }
 

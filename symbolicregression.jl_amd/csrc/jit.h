@@ -145,6 +145,14 @@ bool compile_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& ca
 // operators are + - * / neg abs square cube exp sin cos and that have at
 // most SR_JIT_G_NGACC constants. Constants are read from a device array at
 // run time: new constant sets need no new code.
+// Shared subtrees (Columns::gkey) in the gradient code: a constant-free
+// subtree needs no adjoint, so the derive pass's column (api.cpp
+// derive_shared) stands in for its forward value; the column stays in its
+// register block from the tile start to its last forward or reverse use.
+// Columns from kGradGbase on (raw features stay below); SRHIP_GJIT_GCOLS caps
+// them (default 64, 0: none).
+constexpr int kGradGbase = 64;
+Columns plan_grad_columns(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand);
 struct GradModule;
 struct GradStats {
   int ntrees = 0;
@@ -164,8 +172,12 @@ void grad_part(const GradModule* m, int k, int* slot0, int* nslots);
 // Launch part `part` over its slots (EvalArgs as for launch(): list / fail /
 // partial of the slots); consts = the program's constants (+16 readable
 // floats of padding), gpart = [nrg][nconst] per-row-group ∂L/∂c partials.
+// gcols: the module's shared-subtree columns of this call ([ngcol][n_pad],
+// api.cpp derive_shared), or null when grad_columns(m).ngcol == 0
 hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const EvalArgs<float>& a,
-                            const float* consts, float* gpart, int nconst, hipStream_t stream);
+                            const float* consts, float* gpart, int nconst, hipStream_t stream,
+                            const float* gcols = nullptr);
+const Columns& grad_columns(const GradModule* m);
 bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
                        const std::vector<int32_t>& cand, std::vector<uint8_t>* bytes, std::string* text,
                        std::vector<int32_t>* offsets, GradStats* st, int loss = SRHIP_LOSS_L2, uint64_t lparam = 0);

@@ -35,6 +35,8 @@
 #include <chrono>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
+#include <unordered_map>
 
 #include "jit.h"
 #include "jit_asm.h"
@@ -155,6 +157,75 @@ bool build_gir(const Ins<float>* p, std::vector<GOp>& ops, GOpnd& root, std::str
   }
 }
 
+// ---- shared subtrees (jit.h kGradGbase, Columns::gkey) -----------------------------
+// The canonical text of each value's subtree in the spelling of jit.cpp
+// subtree_keys ("x3", "u11(x3)", "b2(x0,x1)", + and * operands ordered), ""
+// when the subtree reads a constant.
+void gir_keys(const std::vector<GOp>& ops, std::vector<std::string>& key) {
+  key.assign(ops.size(), std::string());
+  for (size_t i = 0; i < ops.size(); ++i) {
+    const GOp& o = ops[i];
+    if (o.kind == K_MAT) continue;
+    auto part = [&](const GOpnd& q) -> std::string {
+      if (q.k == G_X) return "x" + std::to_string(q.v);
+      return q.k == G_VAL ? key[q.v] : std::string();
+    };
+    const std::string ka = part(o.a);
+    if (ka.empty()) continue;
+    if (o.kind == K_UN) {
+      key[i] = "u" + std::to_string(o.op) + "(" + ka + ")";
+      continue;
+    }
+    const std::string kb = part(o.b);
+    if (kb.empty()) continue;
+    const bool comm = o.op == SRHIP_BOP_ADD || o.op == SRHIP_BOP_MUL;
+    key[i] = "b" + std::to_string(o.op) + "(" + (comm && kb < ka ? kb + "," + ka : ka + "," + kb) + ")";
+  }
+}
+// Every maximal shared subtree becomes a read of its column (G_X, feature
+// kGradGbase + g); the operations only it used are dropped. False (IR
+// unchanged): the tree holds none.
+bool gir_substitute(std::vector<GOp>& ops, GOpnd& root, const std::unordered_map<std::string, int>& gidx) {
+  if (gidx.empty()) return false;
+  std::vector<std::string> key;
+  gir_keys(ops, key);
+  bool any = false;
+  std::vector<char> live(ops.size(), 0);
+  std::function<void(GOpnd&)> rw = [&](GOpnd& q) {
+    if (q.k != G_VAL) return;
+    if (!key[q.v].empty()) {
+      auto it = gidx.find(key[q.v]);
+      if (it != gidx.end()) {
+        GOpnd x;
+        x.k = G_X;
+        x.v = kGradGbase + it->second;
+        q = x;
+        any = true;
+        return;
+      }
+    }
+    live[q.v] = 1;
+    GOp& o = ops[q.v];
+    rw(o.a);
+    if (o.kind == K_BIN) rw(o.b);
+  };
+  rw(root);
+  if (!any) return false;
+  std::vector<int> nid(ops.size(), -1);
+  std::vector<GOp> out;
+  for (size_t i = 0; i < ops.size(); ++i) {
+    if (!live[i]) continue;
+    GOp o = ops[i];
+    if (o.a.k == G_VAL) o.a.v = nid[o.a.v];
+    if (o.kind == K_BIN && o.b.k == G_VAL) o.b.v = nid[o.b.v];
+    nid[i] = (int)out.size();
+    out.push_back(o);
+  }
+  if (root.k == G_VAL) root.v = nid[root.v];
+  ops.swap(out);
+  return true;
+}
+
 // ---- code generation of one tree ---------------------------------------------------
 struct GradGen {
   Asm& as;
@@ -181,6 +252,17 @@ struct GradGen {
   int nloads = 0, waited = 0;
   bool has_call = false;
   int L_tile = -1, L_done = -1, L_redo = -1;
+  // shared-subtree columns: G_X features from gbase on are read from device
+  // memory — s[98:99] = column 0 at this row group's first row, s100 = the
+  // column stride in bytes (jit_template.hip's gradient drivers) — one global
+  // load each at the tile start into the block that holds the column until
+  // its last forward or reverse use; loads return in issue order, so column
+  // f's wait is vmcnt(gnum - 1 - gidx[f])
+  static constexpr int S_GCOL = 98, S_GSTRIDE = 100;
+  int gbase = 1 << 30;
+  int gidx[256];
+  int gnum = 0, gdone = 0;
+  bool is_g(int f) const { return f >= gbase; }
   // guarded FAST forward (as the loss tree code, jit.cpp): exp / sin / cos by
   // their FAST routines; a tile whose guards fire (or that fails) runs its
   // forward again with the PRECISE routines before the loss and the reverse
@@ -307,11 +389,14 @@ struct GradGen {
       }
     }
     // reverse-pass reads of saved values (operands and own results)
+    int xg_rev[256];
+    for (int f = 0; f < 256; ++f) xg_rev[f] = -1;
     for (int i = 0; i < n; ++i) {
       const GOp& o = ops[i];
       if (!hasc[i] || o.kind == K_MAT) continue;
       auto use = [&](const GOpnd& q) {
         if (q.k == G_VAL) last[q.v] = std::max(last[q.v], bstep(i));
+        if (q.k == G_X && q.v >= 0 && q.v < 256 && is_g(q.v)) xg_rev[q.v] = std::max(xg_rev[q.v], bstep(i));
       };
       if (o.kind == K_BIN) {
         const bool aa = needs_adj(o.a), ab = needs_adj(o.b);
@@ -337,7 +422,7 @@ struct GradGen {
     auto usef = [&](const GOpnd& q, int i, bool inl) {
       if (q.k != G_X) return true;
       if (q.v < 0 || q.v > 255) return false;
-      if (inl) {
+      if (inl || is_g(q.v)) {  // a column is always preloaded
         if (!xinl[q.v]) feats.push_back(q.v);
         xinl[q.v] = true;
         xlast[q.v] = std::max(xlast[q.v], i);
@@ -350,8 +435,13 @@ struct GradGen {
       if (ops[i].kind == K_BIN && !usef(ops[i].b, i, inl)) { why = "feature index"; return false; }
     }
     if (!usef(root, n, true)) { why = "feature index"; return false; }
-    for (int f = 0; f < 256; ++f)
+    for (int f = 0; f < 256; ++f) {
+      if (is_g(f)) {
+        xlast[f] = std::max(xlast[f], xg_rev[f]);
+        continue;
+      }
       if (xlast[f] >= 0 && (1 + f) * TILE * 4 + 3 * 4 * 64 > 65535) { why = "feature offset beyond the DS immediate"; return false; }
+    }
     if ((int)feats.size() > GNPOOL) { why = "more features than register blocks"; return false; }
     return true;
   }
@@ -390,6 +480,13 @@ struct GradGen {
 
   // ---- emission helpers
   void wait_for_feat(int f) {
+    if (is_g(f)) {
+      if (gidx[f] >= gdone) {
+        as.waitcnt_vm(gnum - 1 - gidx[f]);
+        gdone = gidx[f] + 1;
+      }
+      return;
+    }
     const int li = load_idx[f];
     if (li >= waited) {
       as.waitcnt_lgkm(nloads - 1 - li);
@@ -398,6 +495,34 @@ struct GradGen {
   }
   void wait_all() {
     if (waited < nloads) { as.waitcnt_lgkm(0); waited = nloads; }
+    if (gdone < gnum) { as.waitcnt_vm(0); gdone = gnum; }  // no load may land after the tile
+  }
+  void emit_gloads() {  // this tile's column loads (emit_tree's tile prologue)
+    gnum = 0;
+    gdone = 0;
+    bool first = true;
+    for (size_t j = 0; j < feats.size(); ++j) {
+      const int f = feats[j];
+      if (!is_g(f)) continue;
+      if (first) {
+        as.vop2(VOP2_LSHLREV_B32, "v_lshlrev_b32_e32", VGT, K(2), VLANE4);  // lane·16
+        as.sop2(SOP2_LSHL_B32, "s_lshl_b32", 0, S(S_TILE), K(10));         // tile·1024
+        as.sop2(SOP2_ADD_U32, "s_add_u32", 0, S(S_GCOL), S(0));
+        as.sop2(SOP2_ADDC_U32, "s_addc_u32", 1, S(S_GCOL + 1), K(0));
+        first = false;
+      }
+      const uint32_t g = (uint32_t)(f - gbase);
+      int sb = 0;
+      if (g > 0) {
+        as.sop2(SOP2_MUL_I32, "s_mul_i32", 2, S(S_GSTRIDE), K(g));
+        as.sop2(SOP2_MUL_HI_U32, "s_mul_hi_u32", 3, S(S_GSTRIDE), K(g));
+        as.sop2(SOP2_ADD_U32, "s_add_u32", 2, S(0), S(2));
+        as.sop2(SOP2_ADDC_U32, "s_addc_u32", 3, S(1), S(3));
+        sb = 2;
+      }
+      as.global_load_dwordx4(blk_reg((int)j), VGT, sb, 0);
+      gidx[f] = gnum++;
+    }
   }
   Src fsrc(const GOpnd& q, int e) const {  // forward operand source
     if (q.k == G_C) return S(SC0 + q.ci);
@@ -572,6 +697,11 @@ struct GradGen {
     return true;
   }
   void operand_to(int dst, const GOpnd& q) {
+    if (q.k == G_X && is_g(q.v)) {
+      wait_for_feat(q.v);
+      mov4(dst, blk_reg(xblk[q.v]));
+      return;
+    }
     if (q.k == G_X) { read_feat(dst, q.v); return; }
     if (vreg(q.v) == dst) return;  // already there (a result kept in VA)
     mov4(dst, vreg(q.v));
@@ -650,11 +780,12 @@ struct GradGen {
     // value of an operand in the reverse pass (features re-read from LDS)
     auto rsrc = [&](const GOpnd& q, int scratch, int e) {
       if (q.k == G_C) return S(SC0 + q.ci);
+      if (q.k == G_X && is_g(q.v)) return V(blk_reg(xblk[q.v]) + e);  // a column: in its block
       if (q.k == G_X) return V(scratch + e);
       return V(blk_reg(loc[q.v]) + e);
     };
     auto fetch = [&](const GOpnd& q, int scratch) {
-      if (q.k == G_X) read_feat(scratch, q.v);
+      if (q.k == G_X && !is_g(q.v)) read_feat(scratch, q.v);
     };
     // adjoint of operand q = (products already in block `reg`) with sign `neg`
     auto give = [&](const GOpnd& q, int reg, bool neg, int blk) {
@@ -925,12 +1056,16 @@ struct GradGen {
     }
     nloads = 0;
     waited = 0;
+    for (size_t j = 0; j < feats.size(); ++j) {
+      xblk[feats[j]] = (int)j;
+      owner[j] = 1000 + feats[j];
+    }
+    emit_gloads();  // the columns first: their latency is the longer one
     as.ds_read_b128(VY, VLANE, 0);
     ++nloads;
     for (size_t j = 0; j < feats.size(); ++j) {
       const int f = feats[j];
-      xblk[f] = (int)j;
-      owner[j] = 1000 + f;
+      if (is_g(f)) continue;
       load_idx[f] = nloads++;
       as.ds_read_b128(blk_reg((int)j), VLANE, (1 + f) * TILE * 4);
     }
@@ -1031,6 +1166,7 @@ struct GradGen {
     for (int i = n - 1; i >= 0; --i) {
       if (hasc[i] && !emit_reverse(i)) return false;
       free_values_at(bstep(i));
+      free_feats_at(bstep(i));
     }
     for (int k = 0; k < GNPOOL; ++k)
       if (owner[k] != -1) { why = "internal: block live after the reverse pass"; return false; }
@@ -1132,23 +1268,38 @@ struct GradGen {
   }
 };
 
+using ColIndex = std::unordered_map<std::string, int>;
+
+// gidx: the module's shared-subtree columns (key -> g), or null. A tree whose
+// code with its columns does not fit (register pool) is compiled without them.
 bool gen_grad_tree(const Ins<float>* prog, int nc, const Tmpl& T, bool text, std::vector<uint32_t>& out,
-                   std::vector<std::string>* lines, int32_t* off, std::string* why, int loss, uint64_t lparam) {
+                   std::vector<std::string>* lines, int32_t* off, std::string* why, int loss, uint64_t lparam,
+                   const ColIndex* gidx) {
   if (nc > NGACC) { *why = "more constants than accumulators"; return false; }
   if (!has_dloss_routine(loss)) { *why = "loss without gradient routines"; return false; }
   std::vector<GOp> ir;
   GOpnd root;
   if (!build_gir(prog, ir, root, why)) return false;
+  std::vector<GOp> irs = ir;
+  GOpnd roots = root;
+  const bool subst = gidx && gir_substitute(irs, roots, *gidx);
   const size_t start = (out.size() + 15) / 16 * 16;
   Asm as;
-  as.want_text = text;
-  GradGen g(as, T, T.area_va + start * 4);
-  g.ops = ir;
-  g.root = root;
-  g.nc = nc;
-  g.loss = loss;
-  g.lparam = lparam;
-  if (!g.emit_tree()) { *why = g.why; return false; }
+  bool ok = false;
+  for (int attempt = subst ? 0 : 1; attempt < 2 && !ok; ++attempt) {
+    as = Asm();
+    as.want_text = text;
+    GradGen g(as, T, T.area_va + start * 4);
+    g.ops = attempt == 0 ? irs : ir;
+    g.root = attempt == 0 ? roots : root;
+    if (attempt == 0) g.gbase = kGradGbase;
+    g.nc = nc;
+    g.loss = loss;
+    g.lparam = lparam;
+    ok = g.emit_tree();
+    if (!ok) *why = g.why;
+  }
+  if (!ok) return false;
   as.finish();
   while (out.size() < start) {
     out.push_back(0xbf800000u);
@@ -1169,7 +1320,8 @@ bool gen_grad_tree(const Ins<float>* prog, int nc, const Tmpl& T, bool text, std
 size_t grad_codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& const_off,
                     const std::vector<int32_t>& cand, size_t from, bool text, std::vector<uint32_t>& words,
                     std::vector<std::string>* lines, std::vector<int32_t>& offs, std::vector<int32_t>& ok_trees,
-                    std::vector<int32_t>& rest, GradStats* st, const Tmpl& T, int loss, uint64_t lparam) {
+                    std::vector<int32_t>& rest, GradStats* st, const Tmpl& T, int loss, uint64_t lparam,
+                    const ColIndex* gidx) {
   for (size_t k = from; k < cand.size(); ++k) {
     const int32_t t = cand[k];
     int32_t off = -1;
@@ -1178,7 +1330,7 @@ size_t grad_codegen(const CompiledBatch<float>& cb, const std::vector<int32_t>& 
     const size_t lbefore = lines ? lines->size() : 0;
     const int nc = const_off[t + 1] - const_off[t];
     const bool okc = cb.tree_off[t] >= 0 && gen_grad_tree(&cb.code[cb.tree_off[t]], nc, T, text, words, lines, &off, &why,
-                                                                  loss, lparam);
+                                                                  loss, lparam, gidx);
     if (okc && words.size() * 4 > T.area_bytes) {  // area full: the next part takes it
       words.resize(before);
       if (lines) lines->resize(lbefore);
@@ -1216,6 +1368,7 @@ struct GradPart {
 struct GradModule {
   std::vector<GradPart> parts;
   int nslots = 0;
+  Columns cols;  // shared-subtree columns (ngcol 0: none)
 };
 
 namespace {
@@ -1253,6 +1406,10 @@ GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t
   const Templates& TT = templates();
   if (!TT.ok) { rest = cand; return nullptr; }
   auto t0 = std::chrono::steady_clock::now();
+  Columns cols = plan_grad_columns(cb, cand);
+  ColIndex gidx;
+  for (int g = 0; g < cols.ngcol; ++g) gidx.emplace(cols.gkey[g], g);
+  const ColIndex* gi = gidx.empty() ? nullptr : &gidx;
   struct Chunk { std::vector<uint32_t> words; std::vector<int32_t> offs, slots; const Tmpl* T; };
   std::vector<Chunk> chunks;
   size_t pos = 0;
@@ -1261,7 +1418,7 @@ GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t
     Chunk ch;
     ch.T = &TT.large;
     const size_t next = grad_codegen(cb, const_off, cand, pos, false, ch.words, nullptr, ch.offs, ch.slots, rest, st,
-                                     TT.large, loss, lparam);
+                                     TT.large, loss, lparam, gi);
     if (next == pos) { rest.push_back(cand[pos]); if (st) st->nrejected++; pos = next + 1; continue; }  // one tree > area
     if ((int)chunks.size() + 1 == kMaxGradParts && next < cand.size()) {  // the rest stays interpreted
       for (size_t k = next; k < cand.size(); ++k) rest.push_back(cand[k]);
@@ -1276,7 +1433,7 @@ GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t
       sm.T = &TT.small;
       std::vector<int32_t> rs;
       grad_codegen(cb, const_off, ch.slots, 0, false, sm.words, nullptr, sm.offs, sm.slots, rs, nullptr, TT.small, loss,
-                   lparam);
+                   lparam, gi);
       if (sm.slots != ch.slots) throw Error(SRHIP_ERR_INVALID, "jit-grad: small-template relayout differs");
       ch = std::move(sm);
     }
@@ -1286,6 +1443,7 @@ GradModule* build_grad(const CompiledBatch<float>& cb, const std::vector<int32_t
   if (chunks.empty()) return nullptr;
   auto t1 = std::chrono::steady_clock::now();
   GradModule* m = new GradModule();
+  m->cols = std::move(cols);
   try {
     for (Chunk& ch : chunks) {
       GradPart pt;
@@ -1326,6 +1484,7 @@ bool has_dloss_routine(int loss) {
 }
 
 int grad_nslots(const GradModule* m) { return m ? m->nslots : 0; }
+const Columns& grad_columns(const GradModule* m) { return m->cols; }
 int grad_nparts(const GradModule* m) { return m ? (int)m->parts.size() : 0; }
 void grad_part(const GradModule* m, int k, int* slot0, int* nslots) {
   *slot0 = m->parts[k].slot0;
@@ -1342,11 +1501,17 @@ struct JitGradArgs {
   float* gpart;
   int nconst;
   int dyn;
+  const float* gcols;
 };
 
 hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const EvalArgs<float>& a,
-                            const float* consts, float* gpart, int nconst, hipStream_t stream) {
+                            const float* consts, float* gpart, int nconst, hipStream_t stream, const float* gcols) {
   if (plan.threads != 256) return hipErrorInvalidValue;  // the scratch holds 4 waves
+  // the columns' byte offsets (s_mul_i32 / s_mul_hi_u32 of the stride, 32-bit lane offsets) and rows
+  if (m->cols.ngcol > 0 && (!gcols || (uint64_t)a.n_pad * 4u * (uint64_t)m->cols.ngcol >= (1ull << 40) ||
+                            (uint64_t)a.n_pad * 4u >= (1ull << 32) ||
+                            (int64_t)a.nrg * a.ntiles * TILE > a.n_pad))
+    return hipErrorInvalidValue;
   const GradPart& pt = m->parts[part];
   if (a.nlist != pt.nslots) return hipErrorInvalidValue;
   JitGradArgs ja;
@@ -1358,6 +1523,7 @@ hipError_t launch_grad_code(GradModule* m, int part, const EvalPlan& plan, const
   ja.gpart = gpart;
   ja.nconst = nconst;
   ja.dyn = dynamic_trees() ? 1 : 0;
+  ja.gcols = m->cols.ngcol > 0 ? gcols : nullptr;
   size_t sz = sizeof(ja);
   void* cfg[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &ja, HIP_LAUNCH_PARAM_BUFFER_SIZE, &sz, HIP_LAUNCH_PARAM_END};
   const unsigned grid = a.rotate >= 2 ? (unsigned)((a.nrg + 7) / 8 * 8) * (unsigned)a.ntg
@@ -1382,8 +1548,11 @@ bool compile_grad_only(const CompiledBatch<float>& cb, const std::vector<int32_t
   std::vector<uint32_t> words;
   std::vector<std::string> lines;
   std::vector<int32_t> offs, okt, rest;
+  const Columns cols = plan_grad_columns(cb, cand);
+  ColIndex gidx;
+  for (int g = 0; g < cols.ngcol; ++g) gidx.emplace(cols.gkey[g], g);
   grad_codegen(cb, const_off, cand, 0, text != nullptr, words, text ? &lines : nullptr, offs, okt, rest, st, TT.large, loss,
-               lparam);
+               lparam, gidx.empty() ? nullptr : &gidx);
   if (bytes) {
     bytes->resize(words.size() * 4);
     std::memcpy(bytes->data(), words.data(), bytes->size());

@@ -789,6 +789,7 @@ struct JitGradArgs {
   float* gpart;             // [nrg][nconst] per-row-group Σ w·ℓ'·∂ŷ/∂c
   int nconst;
   int dyn;                  // (reserved, as JitArgs::dyn)
+  const float* gcols;       // [ngcol][n_pad] shared-subtree columns (jit_grad.cpp GradGen::S_GCOL), or null
 };
 
 template <bool W>
@@ -849,6 +850,8 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
   uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
   float* gdst = ja.gpart + (size_t)rg * (size_t)ja.nconst;
   Part<float>* dst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
+  const uint64_t gcb = sgpr64(ja.gcols ? reinterpret_cast<uint64_t>(ja.gcols + row0) : 0ull);
+  const uint32_t gstride = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a.n_pad * 4));
   for (int k = 0; k < m; ++k) {
     const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
     const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
@@ -866,7 +869,7 @@ __device__ __forceinline__ void jit_grad_body(const JitGradArgs& ja) {
       asm volatile("s_swappc_b64 s[76:77], %[tgt]"
                    : "+{v42}"(lsum), "+{v40}"(chk), "+{v41}"(la), "+{s64}"(tile), "={s69}"(status)
                    : [tgt] "s"(target), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
-                     "{s68}"(woff), "{s[78:79]}"(cptr), "{s[84:85]}"(gptr)
+                     "{s68}"(woff), "{s[78:79]}"(cptr), "{s[84:85]}"(gptr), "{s[98:99]}"(gcb), "{s100}"(gstride)
                    : SR_JIT_GRAD_CLOBBERS, "memory");
       (void)status;
     }
@@ -1035,6 +1038,8 @@ __device__ __forceinline__ void jit_grad_dl_body(const JitGradArgs& ja) {
   const uint64_t dstp = reinterpret_cast<uint64_t>(a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb);
   const uint64_t cbp = reinterpret_cast<uint64_t>(ja.cbase), constp = reinterpret_cast<uint64_t>(ja.consts);
   const uint64_t gdstp = reinterpret_cast<uint64_t>(ja.gpart + (size_t)rg * (size_t)ja.nconst);
+  const uint64_t gcb = sgpr64(ja.gcols ? reinterpret_cast<uint64_t>(ja.gcols + row0) : 0ull);
+  const uint32_t gstride = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a.n_pad * 4));
   asm volatile(
       "s_getpc_b64 s[96:97]\n"
       "s_add_u32 s96, s96, sr_jit_gloop@rel32@lo+4\n"
@@ -1044,7 +1049,7 @@ __device__ __forceinline__ void jit_grad_dl_body(const JitGradArgs& ja) {
       : "{v30}"(lds_lane), "{v31}"(cnt_addr), "{v43}"(lane4), "{s65}"(nt_u), "{s66}"(partial), "{s67}"(tilebytes),
         "{s68}"(woff), "{s40}"(tpb), "{s41}"(ntg), "{s42}"(gg), "{s43}"(g1), "{s44}"(nlist), "{s[46:47]}"(failp),
         "{s[48:49]}"(codep), "{s[50:51]}"(dstp), "{s[52:53]}"(cbp), "{s[54:55]}"(constp), "{s[56:57]}"(gdstp),
-        "{s[88:89]}"(area)
+        "{s[88:89]}"(area), "{s[98:99]}"(gcb), "{s100}"(gstride)
       : SR_JIT_GRAD_CLOBBERS, "s58", "s59", "s60", "s61", "s62", "s63", "s64", "s69", "s78", "s79", "s84", "s85",
         "s91", "s94", "s95", "s96", "s97", "v40", "v41", "v42", "v153", "v154", "v155", "memory");
 }

@@ -744,8 +744,14 @@ def best_of_sample(isl: Island, S: Search, freqs: np.ndarray) -> PopMember:
             scores = np.array(scores).astype(np.float32).tolist()
     else:
         scores = [m.score for m in sample]
-    if o.tournament_selection_p == 1.0:
-        k = 0
+    if o.tournament_selection_p == 1.0:  # argmin(scores) (Population.jl:109-110): the first NaN, else the first minimum
+        best, bv = 0, math.inf
+        for i, v in enumerate(scores):
+            if v != v:
+                return sample[i]
+            if v < bv:
+                best, bv = i, v
+        return sample[best]
     else:  # StatsBase.sample(1:n, Weights(w)) by the cumulative weights (_sample_weighted)
         k = bisect.bisect_right(S.tournament_cum, rng.random() * S.tournament_wsum)
         if k >= n_t:

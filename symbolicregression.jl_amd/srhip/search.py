@@ -182,8 +182,10 @@ class _CallbackEvaluator:
         return np.asarray(self.scorer(trees), dtype=np.float64)
 
     def losses_rows(self, trees, rows):
+        # a NaN loss is a failed evaluation (score 0, loss Inf: batch_score_of);
+        # a completed Inf loss keeps its Inf score, as score_func_batch's
         out = np.asarray([self.batch_scorer([t], r)[0] for t, r in zip(trees, rows)], dtype=np.float64)
-        return out, np.isfinite(out)
+        return out, ~np.isnan(out)
 
     def optimize(self, trees, noise):
         return optimize_constants_batch(self.dataset, trees, self.options, noise=noise,

@@ -10,6 +10,8 @@ every island's pending requests) reproduces the serial per-island schedule
 `score_func` call) EXACTLY, over the CPU oracle, with default Options
 (crossover, adaptive parsimony, tournament p = 0.86, constant optimisation),
 with batching, and sharded over two gloo ranks."""
+import math
+
 import numpy as np
 import pytest
 
@@ -233,6 +235,30 @@ def test_best_of_sample_tournament():
         idx = np.random.default_rng(k).permutation(33)[:12]  # the sample best_of_sample draws
         first += E.best_of_sample(isl, S, np.ones(22) / 22).score == min(idx)
     assert 0.82 < first / 2000 < 0.90
+
+
+def test_best_of_sample_p1_argmin_nan_first():
+    """p = 1: argmin(scores) (Population.jl:109-110) — Julia's findmin takes
+    the first NaN as the minimum; without NaN the first smallest wins."""
+    o = _o()
+    o.use_frequency_in_tournament = False
+    o.tournament_selection_n = 12
+    o.tournament_selection_p = 1.0
+    S = E.Search(o, 5, 100, np.float32, 1.0)
+    isl = E.Island(0, 0)
+    for nan_at in (None, 7, 20):
+        scores = [float(i % 9) for i in range(33)]
+        if nan_at is not None:
+            scores[nan_at] = math.nan
+        isl.pop = [E.PopMember(Node(val=np.float32(i)), scores[i], scores[i], i) for i in range(33)]
+        for k in range(50):
+            isl.rng = np.random.default_rng(k)
+            idx = np.random.default_rng(k).permutation(33)[:12].tolist()
+            s = [scores[i] for i in idx]
+            nans = [j for j, v in enumerate(s) if v != v]
+            want = idx[nans[0]] if nans else idx[int(np.argmin(s))]
+            got = E.best_of_sample(isl, S, np.ones(22) / 22)
+            assert got is isl.pop[want]
 
 
 def _world_worker(rank, world, port, q):

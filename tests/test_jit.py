@@ -209,6 +209,32 @@ def test_loss_code_has_no_transcendental_forwarding_hazard(k):
         assert not bad, bad[:3]
 
 
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+def test_gradient_shared_subtree_columns_equal_llvm_mc():
+    """Config #5-like gradient programs read their shared constant-free
+    subtrees (cos(x_f), exp(x_f), ...) from columns (jit.h kGradGbase): the
+    code holds the global loads, its bytes are llvm-mc's, and as many trees
+    compile as without columns (a tree whose columns exhaust the register
+    pool falls back to its own code)."""
+    import os
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    trees = srhip.random_population(1000, o, 20, np.float32, seed=5)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    code, text, offs = jit_compile(flat, grad=True)
+    assert text.count("global_load_dwordx4") > 300 and "s_waitcnt vmcnt(0)" in text
+    assert assemble(text) == code
+    os.environ["SRHIP_GJIT_GCOLS"] = "0"
+    try:
+        code0, text0, offs0 = jit_compile(flat, grad=True)
+    finally:
+        del os.environ["SRHIP_GJIT_GCOLS"]
+    assert "global_load_dwordx4" not in text0
+    assert len(offs) == len(offs0)
+    calls, calls0 = text.count("s_swappc_b64"), text0.count("s_swappc_b64")
+    print(f"routine calls {calls} with columns, {calls0} without")
+    assert calls < 0.9 * calls0
+
+
 def test_gradient_code_covers_config5_trees():
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     trees = srhip.random_population(2000, o, 20, np.float32, seed=5)

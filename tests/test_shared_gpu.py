@@ -95,3 +95,68 @@ def test_shared_columns_that_fail(gpu_ctx):
     y = (2 * np.cos(X[3]) + X[0] * X[0] - 2).astype(np.float32)
     ok = check_batch(trees, o, X, y)
     assert not ok[:len(special)].any(), "every tree with a failing shared subtree fails"
+
+
+def grad_eval(dev, trees, o, gcols=None):
+    """A program's first eval_loss_grad (its gradient tree code is built
+    there, reading SRHIP_GJIT_GCOLS) and the code's size."""
+    from srhip import constants as K
+    old = os.environ.get("SRHIP_GJIT_GCOLS")
+    try:
+        if gcols is not None:
+            os.environ["SRHIP_GJIT_GCOLS"] = str(gcols)
+        p = srhip.engine.Program(dev.ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32)
+        return p, p.eval_loss_grad(dev, K.LOSS["L2"])
+    finally:
+        if gcols is not None:
+            if old is None:
+                del os.environ["SRHIP_GJIT_GCOLS"]
+            else:
+                os.environ["SRHIP_GJIT_GCOLS"] = old
+
+
+@pytest.mark.parametrize("weighted", [False, True])
+def test_gradient_shared_columns_bit_identical(gpu_ctx, weighted):
+    """The gradient tree code reading shared constant-free subtrees from
+    columns (jit.h kGradGbase) gives the losses, ∂L/∂c and did_succeed of the
+    same program built without them (SRHIP_GJIT_GCOLS=0) bit for bit: the
+    columns hold the interpreter's values, which the gradient code's PRECISE
+    forward equals; failing shared subtrees (exp(exp(x)) overflow, x / x at
+    a zero) fail exactly the oracle's trees."""
+    from srhip import constants as K
+    o = srhip.Options(binary_operators=F32_OPS[0], unary_operators=F32_OPS[1])
+    x1 = Node(feature=1)
+    special = []
+    for k in range(12):
+        ee = o.make_unary("exp", o.make_unary("exp", x1.copy()))
+        special.append(o.make_binary("*", ee, Node(val=0.5 + k)))
+        dd = o.make_binary("/", Node(feature=2), Node(feature=2))
+        special.append(o.make_binary("-", o.make_binary("*", dd, Node(val=1.0 + k)), Node(val=0.25)))
+    trees = special + srhip.random_population(1500, o, 20, np.float32, seed=17, maxsize=30)
+    rng = np.random.default_rng(3 + weighted)
+    n = 20_001
+    X = rng.standard_normal((20, n)).astype(np.float32)
+    X[0, 777] = 5.0   # exp(exp(5)) overflows
+    X[1, 999] = 0.0   # x2 / x2 = NaN there
+    y = (2 * np.cos(X[3]) + X[0] * X[0] - 2).astype(np.float32)
+    w = np.abs(rng.standard_normal(n)).astype(np.float32) if weighted else None
+    ds = srhip.Dataset(X, y, weights=w)
+    dev = ds.device()
+    p_on, (s1, g1, w1, k1) = grad_eval(dev, trees, o)
+    p_off, (s0, g0, w0, k0) = grad_eval(dev, trees, o, gcols=0)
+    info_on, info_off = p_on.grad_jit_info(), p_off.grad_jit_info()
+    assert info_on["ntrees"] >= 0.95 * len(trees) and info_on["ntrees"] == info_off["ntrees"]
+    assert info_on["code_bytes"] != info_off["code_bytes"], "no shared columns in use"
+    s2, g2, _, k2 = p_on.eval_loss_grad(dev, K.LOSS["L2"])  # again: the cached subtree program
+    assert np.array_equal(k2, k1)
+    np.testing.assert_array_equal(g2, g1)
+    assert np.array_equal(k1, k0)
+    assert not k1[:len(special)].any(), "every tree with a failing shared subtree fails"
+    assert w1 == w0
+    np.testing.assert_array_equal(s1[k1], s0[k0])
+    ok_c = np.repeat(k1, np.diff(p_on.flat.const_off))
+    np.testing.assert_array_equal(g1[ok_c], g0[ok_c])
+    assert np.all(np.isnan(g1[~ok_c]))
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    _, _, rok = oracle.eval_loss_batch(flat, X, y, w, dtype=np.float32)
+    assert np.array_equal(k1, rok)

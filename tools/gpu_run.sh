@@ -14,6 +14,8 @@
 #   n2        bench.py's N > 1 paths rehearsed with two ranks on GPU 0 over gloo (not a measurement)
 #   variants  the suite under the static tree loops and with every program as tree code
 #   final     suite, smoke, bench, profile
+#   tests     some GPU tests: TESTS="tests/test_a.py tests/test_b.py -k x"   -> gpurun_out/pytest_some.log
+#   tool      one measurement tool: TOOL="tools/ab_build.py --grad A B"       -> gpurun_out/tool.log
 # Measurement tools run on the box through this script (each under timeout):
 # ab_env.py / loop_ab.py (interleaved A/Bs), step_overhead.py, out_copy.py,
 # prof_grad.py, prof_target.py, shard_probe.py, bench_constopt.py,
@@ -97,6 +99,16 @@ run_variants() {
   # (the search tests run thousands of small programs: as tree code each one costs a code-object load)
   run_jitall
 }
+run_tests() {
+  timeout -k 10 600 $PYTEST $TESTS -m gpu > gpurun_out/pytest_some.log 2>&1
+  local rc=$?; echo "pytest rc=$rc"; grep -E "FAILED|Error|passed|failed" gpurun_out/pytest_some.log | tail -12
+  [ $rc -le 1 ] || exit $rc
+}
+run_tool() {
+  [ -n "$TOOL" ] || { echo "TOOL not set"; exit 2; }
+  timeout -k 10 ${TOOL_TIMEOUT:-600} python -u $TOOL > gpurun_out/tool.log 2> gpurun_out/tool.err || { tail -20 gpurun_out/tool.err; exit 1; }
+  cat gpurun_out/tool.log | cut -c1-700
+}
 run_jitall() {
   SRHIP_JIT=1 timeout -k 10 600 $PYTEST tests -m gpu -k "not evolution and not search" > gpurun_out/pytest_jitall.log 2>&1
   rc=$?; echo "SRHIP_JIT=1 rc=$rc"; tail -2 gpurun_out/pytest_jitall.log
@@ -114,6 +126,8 @@ for mode in "$@"; do
     n2) run_n2 ;;
     variants) run_variants ;;
     final) run_suite; run_smoke; run_bench; run_profile ;;
+    tests) run_tests ;;
+    tool) run_tool ;;
     *) echo "unknown mode $mode"; exit 2 ;;
   esac
 done
