@@ -2107,6 +2107,10 @@ void run_grad(srhip_ctx* c, srhip_program* p, int mode, const srhip_dataset* ds,
         timed_end(c, s, tk);
         HIP_CHECK(launch_finalize<double>(a, static_cast<double*>(c->sums.p), static_cast<uint8_t*>(c->oks.p), s));
       }
+      // gpart is not cleared: a failed tree's row groups stop writing their partials, so its constants'
+      // sums here may hold an earlier call's values; collect_grad_results (the only reader of c->dloss)
+      // reports NaN for every constant of a failed tree (test_jit64_grad_gpu.py
+      // test_failed_trees_gradients_are_nan_not_stale)
       HIP_CHECK(launch_gconst_finalize(static_cast<const double*>(c->gpart.p), plans[0].nrg, nconst,
                                        p->d_gjit_cidx, p->ngjit_cidx, static_cast<double*>(c->dloss.p), s));
     }

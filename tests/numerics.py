@@ -112,3 +112,46 @@ def assert_close_conditioned(actual, desired, spread, rtol, atol=0.0, factor=4.0
         raise AssertionError(f"{msg}: {bad.sum()} of {bad.size} beyond the conditioned bound; "
                              f"actual={actual.ravel()[i]} desired={desired.ravel()[i]} "
                              f"spread={np.asarray(spread).ravel()[i]}")
+
+
+def record_tail(name, rec):
+    """Append one tail record (worst error / spread ratios of a parity test) to
+    gpurun_out/parity_tails.jsonl (copied to profiles/ after a GPU run)."""
+    import json
+    from pathlib import Path
+
+    out = Path(__file__).resolve().parent.parent / "gpurun_out"
+    out.mkdir(exist_ok=True)
+    with open(out / "parity_tails.jsonl", "a") as f:
+        f.write(json.dumps(dict(test=name, **rec)) + "\n")
+
+
+def assert_loss_tail(name, actual, desired, mask, flat, X, y, w, T, kind, params, rtol, bar=1e-5):
+    """Every tree of `mask` within `rtol` of the oracle's mean loss, or — for the
+    ill-conditioned tail — within 4x the oracle's own perturbation spread
+    (loss_spread_flat: ulp-scale moves of X and the constants plus
+    per-operator rounding noise), no fraction of trees left unchecked.
+    Records the tail (count outside rtol, outside `bar` = north_star's 1e-5,
+    worst error / spread) under gpurun_out/parity_tails.jsonl."""
+    actual = np.asarray(actual, dtype=np.float64)
+    desired = np.asarray(desired, dtype=np.float64)
+    with np.errstate(invalid="ignore", divide="ignore"):
+        rel = np.abs(actual - desired) / np.abs(desired)
+    out = np.flatnonzero(mask & ~(rel <= rtol))
+    rec = dict(checked=int(mask.sum()), rtol=rtol, outside_rtol=int(out.size),
+               outside_bar=int(np.sum(mask & ~(rel <= bar))), bar=bar,
+               max_rel=float(np.max(rel[mask])) if mask.any() else 0.0, max_err_over_spread=0.0)
+    if out.size:
+        from types import SimpleNamespace
+
+        wsum = float(len(y)) if w is None else float(np.sum(w, dtype=np.float64))
+        sp = loss_spread_flat(flat.take(out), X, y, w, T, SimpleNamespace(kind=kind, params=tuple(params)),
+                              nperturb=3) / wsum
+        err = np.abs(actual[out] - desired[out]) - rtol * np.abs(desired[out])
+        with np.errstate(invalid="ignore", divide="ignore"):
+            rec["max_err_over_spread"] = float(np.nanmax(err / sp))
+        record_tail(name, rec)
+        assert_close_conditioned(actual[out], desired[out], sp, rtol=rtol, factor=4.0, msg=f"{name} tail")
+    else:
+        record_tail(name, rec)
+    return rec

@@ -14,6 +14,7 @@ import pytest
 
 import oracle
 import srhip
+from numerics import assert_close_conditioned, assert_loss_tail, output_spread_flat, record_tail
 from srhip import constants as K
 
 pytestmark = pytest.mark.gpu
@@ -116,7 +117,20 @@ def test_float64_output_tree_code_equals_interpreter(gpu_ctx):
     sel = np.flatnonzero(ok1)[:200]
     with np.errstate(invalid="ignore", divide="ignore"):
         rel = np.abs(out1[sel, :2000] - ref[sel]) / np.maximum(np.abs(ref[sel]), 1e-300)
-    assert np.mean(rel <= 1e-9) > 0.999, float(np.mean(rel <= 1e-9))
+    # every row within 1e-9, or (the ill-conditioned rows) within 4x the
+    # oracle's own spread under ulp-scale perturbations: no row unchecked
+    bad = ~(rel <= 1e-9) & ~(np.isnan(out1[sel, :2000]) & np.isnan(ref[sel]))
+    rows = np.flatnonzero(bad.any(axis=0))
+    tr = np.flatnonzero(bad.any(axis=1))
+    rec = dict(checked=int(rel.size), rtol=1e-9, outside_rtol=int(bad.sum()), max_err_over_spread=0.0)
+    if tr.size:
+        sp = output_spread_flat(flat.take(sel[tr]), X[:, rows], np.float64)
+        a, d = out1[sel[tr]][:, rows], ref[sel[tr]][:, rows]
+        with np.errstate(invalid="ignore", divide="ignore"):
+            rec["max_err_over_spread"] = float(np.nanmax(np.where(bad[np.ix_(tr, rows)],
+                                                                  (np.abs(a - d) - 1e-9 * np.abs(d)) / sp, 0)))
+        assert_close_conditioned(a, d, sp, rtol=1e-9, factor=4.0, msg="Float64 per-row outputs")
+    record_tail("float64_output_tree_code_rows", rec)
 
 
 LOSS_CASES = [("L1", 0.0), ("LP", 2.5), ("HUBER", 1.0), ("LOGCOSH", 0.0), ("L1EPSINS", 0.3), ("L2EPSINS", 0.3),
@@ -161,14 +175,10 @@ def test_float64_loss_tree_code_other_losses(gpu_ctx, loss, param):
     # one tree of this population, cos(exp(cos(c)^x5)·(c - x2)), takes cos of
     # arguments up to 1e20: a 1-ulp difference of device and host pow / exp
     # moves that cos anywhere (1e-4 .. 1e-3 here, interpreter and tree code
-    # alike), so the oracle bound holds for all but 2% of the trees
-    tol = np.full(len(rl), 1e-9)
-    if loss == "PERIODIC":
-        # 1 - cos(2πr/c) moves by up to (2π/c)·|Δr|, and |Δr| is ulps of |ŷ|,
-        # which reach 1e10 and more here: that bound per tree, relative
-        ref = oracle.eval_trees(flat, X, dtype=np.float64)[0]
-        ww = np.ones(n) if w is None else w
-        with np.errstate(all="ignore"):
-            tol += (2 * np.pi / param) * (np.abs(ref) * ww).sum(axis=1) * 1e-13 / np.abs(rl * ww.sum())
-    assert np.mean(relo[mo] <= tol[mo]) >= 0.98, np.sort(relo[mo] / tol[mo])[-5:]
+    # alike): such trees are held to the oracle's perturbation spread below
+    # every tree within 1e-9 of the oracle, or within 4x the oracle's own
+    # perturbation spread (Periodic: 1 - cos(2πr/c) of |ŷ| up to 1e10 moves by
+    # (2π/c)·|Δr|, which the perturbed oracle runs show), no tree unchecked
+    assert_loss_tail(f"float64_loss_tree_code_{loss}", s1 / w1, rl, mo, flat, X, y, w, np.float64,
+                     K.LOSS[loss], (param,), rtol=1e-9)
     assert np.median(relo[mo]) <= 1e-13

@@ -240,3 +240,37 @@ def test_float64_grad_tree_code_many_constants_fall_back(gpu_ctx):
     S, _ = oracle_terms(trees, o, X, y, None)
     sel = ok_c & np.isfinite(S)
     assert np.all(np.abs(g1[sel] - g0[sel]) <= 1e-10 * S[sel] + 1e-300)
+
+
+def test_failed_trees_gradients_are_nan_not_stale(gpu_ctx):
+    """the gradient tree code's per-row-group partials are not
+    cleared between calls, and a failing tree's row groups stop writing them.
+    The C ABI (api.cpp collect_grad_results) reports NaN for every constant of
+    a failed tree, so a stale partial from an earlier call never reaches a
+    caller: call 1 on finite data, call 2 on data where some trees fail
+    (safe_log of a negative feature -> NaN), call 3 on the first data again
+    (= call 1 bit for bit)."""
+    o = srhip.Options(binary_operators=OPSETS["cfg3"][0], unary_operators=OPSETS["cfg3"][1])
+    rng = np.random.default_rng(91)
+    n = 4001
+    Xa = rng.uniform(0.5, 3.0, (5, n))
+    Xb = Xa.copy()
+    Xb[:, 1000] = -2.0  # every tree reading any feature through a log / sqrt / ^ now fails
+    y = rng.standard_normal(n)
+    trees = srhip.random_population(600, o, 5, np.float64, seed=92)
+    flat = srhip.flatten(trees, o, dtype=np.float64)
+    prog = srhip.Program(gpu_ctx, flat, np.float64)
+    dsa = srhip.DeviceDataset(gpu_ctx, Xa, y)
+    dsb = srhip.DeviceDataset(gpu_ctx, Xb, y)
+    s1, g1, _, ok1 = [np.array(v, copy=True) for v in prog.eval_loss_grad(dsa, K.LOSS["L2"])]
+    assert gpu_ctx.last_tree_code() > 0
+    s2, g2, _, ok2 = [np.array(v, copy=True) for v in prog.eval_loss_grad(dsb, K.LOSS["L2"])]
+    failed = np.flatnonzero(ok1.astype(bool) & ~ok2.astype(bool))
+    assert failed.size > 10, failed.size
+    co = flat.const_off
+    for t in failed:
+        assert np.all(np.isnan(g2[co[t]:co[t + 1]])) and np.isnan(s2[t])
+    s3, g3, _, ok3 = prog.eval_loss_grad(dsa, K.LOSS["L2"])
+    assert np.array_equal(ok1, ok3)
+    np.testing.assert_array_equal(s3, s1)
+    np.testing.assert_array_equal(g3, g1)

@@ -1,5 +1,5 @@
 """Recorded default-Options searches on the engine (tools/run_search.py,
-profiles/r05_search_config*.json): every hall-of-fame loss the GPU run stored
+profiles/r0*_search_config*.json): every hall-of-fame loss the GPU run stored
 is rechecked here on the CPU oracle, for the same trees and the same data
 (BASELINE configs #1 and #4)."""
 import json
@@ -12,7 +12,8 @@ import oracle
 import srhip
 
 ROOT = Path(__file__).resolve().parent.parent
-RECORDS = sorted((ROOT / "profiles").glob("r05_search_config*.json"))
+# every recorded search (r05_search_*, r05_final_search_*, r06_* ...): whatever DESIGN.md cites is rechecked
+RECORDS = sorted((ROOT / "profiles").glob("r0*search_config*.json"))
 
 
 def _data(cfg):
