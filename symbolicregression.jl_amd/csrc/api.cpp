@@ -1676,7 +1676,9 @@ void run_eval(srhip_ctx* c, const srhip_program* p, int mode, const T* X, const 
     timed_end(c, s, tk);
     // the last tree-code part's finalize hands over and clears the tree code's counters
     uint32_t* cnt = (last_jit && jm && !jit_bail) ? jit::bail_flags(jm) + nj : nullptr;
-    HIP_CHECK(launch_finalize<T>(a, c->res_sum, c->res_ok, s, cnt, cnt ? c->pin_cnt : nullptr));
+    EvalArgs<T> af = a;  // the hand-written tree loops write 4-byte partials
+    if constexpr (std::is_same<T, float>::value) af.part4 = (pass == -1 && jit::partials4(jm, launches[li].part)) ? 1 : 0;
+    HIP_CHECK(launch_finalize<T>(af, c->res_sum, c->res_ok, s, cnt, cnt ? c->pin_cnt : nullptr));
     if (cnt) c->cnt_pending = true;
     static const bool dbg = std::getenv("SRHIP_DEBUG_PASSES") != nullptr;
     if (dbg) {  // debugging only: wait for the launch to report its time

@@ -332,6 +332,49 @@ __device__ __forceinline__ float d_sincos_f32(float x, int want_cos) {
   }
   return v;
 }
+// sin / cos for the gradient tree code's forward pass together with the
+// value its reverse pass needs (jit_grad.cpp: the routine u_sin_pd / u_cos_pd
+// leaves it in B and the tree keeps it instead of x): d = cos x for sin,
+// sin x for cos. The returned value is fast_sincos_f32's, bit for bit. With
+// the same reduction r = x - m pi/2 both are (-1)^n cos r, evaluated as
+// sin(pi/2 - |r|) from the Float64 r (relative accuracy at d's own zeros)
+// with the FAST odd polynomial: <= 2 ulp as d_sincos_f32. nabs as
+// fast_sincos_f32 (the caller's large-argument test).
+__device__ __forceinline__ float sincos_pd_f32(float x, int want_cos, float& d, float& nabs) {
+#if SR_PRECISE_TRANSC
+  const float n = want_cos ? __builtin_rintf(__builtin_fmaf(x, 0.318309873f, -0.5f))
+                           : __builtin_rintf(x * 0.318309873f);
+  nabs = __builtin_fabsf(n);
+  const float m = want_cos ? __builtin_fmaf(n, 2.0f, 1.0f) : n + n;
+  const double md = (double)m;
+  double r = __builtin_fma(md, -1.57079632673412561417e+00, (double)x);
+  r = __builtin_fma(md, -6.07710050650619224932e-11, r);
+  const double s2 = r * r;
+  double p = -7.34673622570819757e-13;
+  p = __builtin_fma(p, s2, 1.60458129180763398e-10);
+  p = __builtin_fma(p, s2, -2.50518043886916424e-08);
+  p = __builtin_fma(p, s2, 2.75573153848002669e-06);
+  p = __builtin_fma(p, s2, -1.98412698157051834e-04);
+  p = __builtin_fma(p, s2, 8.33333333325722396e-03);
+  p = __builtin_fma(p, s2, -1.66666666666660662e-01);
+  const double v = __builtin_fma(p * s2, r, r);
+  const float f = (float)(want_cos ? -v : v);
+  const int sg = (int)n << 31;
+  // sin x of a cos node near x = 0 directly (pi/2 - |r| would cancel: x is not bounded away
+  // from that zero of sin as floats are from the others, k pi, k != 0)
+  const bool small = want_cos && __builtin_fabsf(x) < 0.785398163f;
+  const float t = small ? x : (float)(1.5707963267948966 - __builtin_fabs(r));
+  const float s = t * t;
+  float q = __builtin_fmaf(__builtin_fmaf(__builtin_fmaf(2.606342605e-06f, s, -1.980987436e-04f), s,
+                                          8.333070204e-03f), s, -1.666665971e-01f);
+  q = q * s;
+  d = __int_as_float(__float_as_int(__builtin_fmaf(q, t, t)) ^ (small ? 0 : sg));
+  return __int_as_float(__float_as_int(f) ^ sg);
+#else
+  d = d_sincos_f32(x, !want_cos);
+  return fast_sincos_f32(x, want_cos, nabs);
+#endif
+}
 __device__ __forceinline__ double m_sin(double x) { return m_sin_ocml(x); }
 __device__ __forceinline__ double m_cos(double x) { return m_cos_ocml(x); }
 

@@ -89,7 +89,7 @@ def sgpr_pinned(name):
     """Routines compiled with LOSS_PINNED_S held live: the losses, and the
     Float64 pow and logs of PRECISE Float32 ^ and log10 (SGPR temporaries would otherwise
     reach s23+)."""
-    return name.startswith(("l_", "d_", "b_pow", "u_log"))
+    return name.startswith(("l_", "d_", "b_pow", "u_log", "u_sin_pd", "u_cos_pd"))
 
 
 def snippet_source(rg, routines):
@@ -220,6 +220,23 @@ def routine_list():
             rs.append((f"u_{u.lower()}", rows(f"{mk}s.a[r] = dev::uop<SRHIP_UOP_{u}>(s.a[r]);"), False))
             if u == "EXP":  # the compiled body beside the hand-scheduled one (tests: SRHIP_JIT_MANUAL=0)
                 rs.append(("u_exp_full", rows(f"{mk}s.a[r] = dev::uop<SRHIP_UOP_{u}>(s.a[r]);"), False))
+    # the gradient tree code's forward sin / cos (jit_grad.cpp): the value in A
+    # (u_sin / u_cos's, bit for bit) and the reverse pass's factor in B — cos x
+    # for sin, sin x for cos (device_ops.h sincos_pd_f32) — so that the
+    # reverse pass multiplies instead of calling the other routine
+    if not TRIG_BAIL:
+        for u in ("SIN", "COS"):
+            wc = 1 if u == "COS" else 0
+            body = (f"float v[R]; float dv[R]; float qmax = 0.0f; "
+                    f"for (int r = 0; r < R; ++r) {{ float qa; v[r] = dev::sincos_pd_f32(s.a[r], {wc}, dv[r], qa); "
+                    f"qmax = __builtin_fmaxf(qmax, qa); }} "
+                    f"if (__builtin_amdgcn_ballot_w64(!(qmax <= dev::kTrigQMax)) != 0) {{ "
+                    f"for (int r = 0; r < R; ++r) if (__builtin_amdgcn_ballot_w64(dev::trig_big(s.a[r])) != 0) {{ "
+                    f"const bool bg = dev::trig_big(s.a[r]); const float o = dev::big_sincos_f32(s.a[r], {wc}); "
+                    f"v[r] = bg ? o : v[r]; const float od = dev::big_sincos_f32(s.a[r], {1 - wc}); "
+                    f"dv[r] = bg ? od : dv[r]; }} }} "
+                    f"for (int r = 0; r < R; ++r) {{ s.a[r] = v[r]; s.b[r] = dv[r]; }}")
+            rs.append((f"u_{u.lower()}_pd", body, False))
     for b in sorted(BOPS, key=lambda k: BOPS[k]):
         if b in INLINE_BOPS:
             continue
@@ -687,6 +704,8 @@ def build(hipcc, outdir, R):
         f.write("// dℓ/dr routine of each elementwise loss (-1: L2, inline, or left out)\n")
         f.write("#define SR_JIT_DLOSS_ROUTINE {" + ", ".join(
             str(-1 if n in NO_LOSS_ROUTINE else rid(f"d_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
+        f.write("// the gradient forward's sin / cos with the reverse factor in B (-1: not built)\n")
+        f.write(f"#define SR_JIT_SINCOS_PD_ROUTINE {{{rid('u_sin_pd')}, {rid('u_cos_pd')}}}\n")
         f.write(f"#define SR_JIT_NUM_ROUTINES {len(names)}\n")
         f.write("#define SR_JIT_ROUTINE_NAMES {" + ", ".join(f'"{n}"' for n in names) + "}\n")
         f.write("#define SR_JIT_ROUTINE_TRIG {" + ", ".join("1" if n in trig else "0" for n in names) + "}\n")

@@ -1961,6 +1961,11 @@ static bool dynloop() {
   return !(e && e[0] == '0');
 }
 
+bool partials4(Module* m, int k) {
+  const ModulePart& q = m->parts[k];
+  return q.fn_dl && !m->out && dynloop();
+}
+
 hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, const float* dcols,
                   hipStream_t stream, const float* gcols) {
   const ModulePart& q = m->parts[k];

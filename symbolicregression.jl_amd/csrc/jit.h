@@ -128,6 +128,9 @@ int64_t flag_words(Module* m);
 // null: the driver computes the staged ones itself
 // gcols: the shared-subtree columns of this call ([ngcol][n_pad], api.cpp derive_shared), or
 // null when the module has none
+// whether launch() of part k runs a hand-written loop, which writes 4-byte
+// partials (EvalArgs::part4 for the finalize)
+bool partials4(Module* m, int k);
 hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>& a, bool fast, const float* dcols,
                   hipStream_t stream, const float* gcols = nullptr);
 // out[k][r] = u_k(x_{f_k}[r]) for the module's derived columns (nothing to do when there are none)

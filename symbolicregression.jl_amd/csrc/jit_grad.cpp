@@ -64,6 +64,8 @@ constexpr int TP = 12, TR = 16, TQ = 20;  // product / reciprocal / quotient-adj
 // guard of sin / cos arguments (FAST forward), above the accumulators
 constexpr int VGTRIG_G = GACC + NGACC;
 enum : int { VOP1_RCP_F32 = 0x22, VOPC_NEQ_F32 = 0x4d, VOP3_MUL_F32 = 0x105 };
+// forward sin / cos with the reverse factor in VB (gen_jit.py u_sin_pd / u_cos_pd)
+const int kSinCosPd[2] = SR_JIT_SINCOS_PD_ROUTINE;
 
 // ---- IR: the accumulator machine of a gradient program, renamed ----------------
 enum { G_VAL = 0, G_X = 1, G_C = 2 };
@@ -241,6 +243,16 @@ struct GradGen {
   std::vector<uint8_t> hasc;      // value's subtree holds a constant: it needs an adjoint
   std::vector<int> last;          // last step (forward i, loss n, reverse 2n-i) that reads the value
   std::vector<int> loc;           // pool block of each value, -1 none, LOC_VA: in the routine registers VA
+  // sin / cos whose operand needs an adjoint: the forward call (u_sin_pd / u_cos_pd) also leaves
+  // cos a / sin a in VB, kept in block dloc[i] (owner 3000 + i) for the reverse pass, which then
+  // multiplies instead of calling the FAST cos / sin routine on a saved operand (fuse_trig)
+  bool fuse_trig = false;
+  std::vector<int> dloc;
+  bool fused(int i) const {
+    const GOp& o = ops[i];
+    return fuse_trig && o.kind == K_UN && (o.op == SRHIP_UOP_SIN || o.op == SRHIP_UOP_COS) && needs_adj(o.a) &&
+           kSinCosPd[o.op == SRHIP_UOP_COS ? 1 : 0] >= 0;
+  }
   static constexpr int LOC_VA = -7, LOC_VB = -8;
   int owner[GNPOOL];              // pool block: -1 free, value id, 1000 + feature (forward), 2000 + k adjoint
   int refs[GNPOOL];               // adjoint references of a block
@@ -321,6 +333,7 @@ struct GradGen {
     hasc.assign(n, 0);
     last.assign(n, -1);
     loc.assign(n, -1);
+    dloc.assign(n, -1);
     adj.assign(n, Adj());
     for (int i = 0; i < n; ++i) {
       GOp& o = ops[i];
@@ -413,7 +426,7 @@ struct GradGen {
         }
       } else {
         if (o.op == SRHIP_UOP_EXP || o.op == SRHIP_UOP_SQRT) last[i] = std::max(last[i], bstep(i));
-        else if (o.op != SRHIP_UOP_NEG) use(o.a);
+        else if (o.op != SRHIP_UOP_NEG && !fused(i)) use(o.a);  // fused sin / cos: the factor in dloc[i]
       }
     }
     if (root.k == G_VAL) last[root.v] = std::max(last[root.v], n);  // read by the loss step
@@ -744,7 +757,14 @@ struct GradGen {
       if (fast && g_trig && trig_tainted(o)) guard_max(VGTRIG_G, VA);
       const bool tsmall = fast && trig_small(o);
       if (tsmall) mov4(VGT, VA);
-      routine(o.rid, prec);
+      routine(fused(i) ? kSinCosPd[o.op == SRHIP_UOP_COS ? 1 : 0] : o.rid, prec);
+      if (fused(i)) {  // the reverse factor out of VB before anything reuses it
+        const int kd = free_block();
+        if (kd < 0) { why = "register pool exhausted (sin / cos factor)"; return false; }
+        mov4(blk_reg(kd), VB);
+        owner[kd] = 3000 + i;
+        dloc[i] = kd;
+      }
       if (tsmall) {  // fires when 2^-k·|u| - |sin/cos u| >= 0 (or NaN): max into GCAN
         for (int e = 0; e < R; ++e) {
           const Src u = V(VGT + e), eps = S(S_EPS), r = V(VA + e);
@@ -983,6 +1003,16 @@ struct GradGen {
         }
         default: {  // SIN: g cos(a); COS: -g sin(a) — the FAST routines, <= 2 ulp
           const bool is_sin = o.op == SRHIP_UOP_SIN;
+          if (dloc[i] >= 0) {  // the factor the forward call left (sincos_pd_f32, <= 2 ulp)
+            const int d = dest(o.a, TP, &blk);
+            if (d < 0) return false;
+            const int fr = blk_reg(dloc[i]);
+            for (int e = 0; e < R; ++e) as.vop2(VOP2_MUL_F32, "v_mul_f32_e32", d + e, gv(e), fr + e);
+            owner[dloc[i]] = -1;
+            dloc[i] = -1;
+            give(o.a, d, g.neg != !is_sin, blk);
+            break;
+          }
           mov4(VA, blk_reg(loc[o.a.v]));
           routine(kUopRoutine[is_sin ? SRHIP_UOP_COS : SRHIP_UOP_SIN], false);
           const int d = dest(o.a, TP, &blk);
@@ -1201,10 +1231,11 @@ struct GradGen {
       }
       as.sopp(0x00, "s_nop", 1);
     }
-    for (int j = 0; j < nc; ++j) {
+    const char* st1e = std::getenv("SRHIP_GJIT_STORE1");  // read per build (tools/ab_build.py)
+    const bool store1 = !(st1e && st1e[0] == '0');
+    for (int j = 0; j < nc && !store1; ++j) {  // SRHIP_GJIT_STORE1=0: one store per constant (round 5)
       const int a = GACC + j;
-      // lane 63 holds the sum: v_readlane_b32 s20, v_a, 63 (s20: a routine temporary, free here)
-      as.put(0xd2890000u | 20u);
+      as.put(0xd2890000u | 20u);  // v_readlane_b32 s20, v_a, 63
       as.put((uint32_t)(256 + a) | (191u << 9));
       if (as.want_text) as.lines.push_back("v_readlane_b32 s20, v" + std::to_string(a) + ", 63");
       as.sopp(0x00, "s_nop", 4);
@@ -1216,6 +1247,42 @@ struct GradGen {
         as.lines.push_back("global_store_dword v" + std::to_string(TS + 1) + ", v" + std::to_string(TS) + ", s[" +
                            std::to_string(SGPTR) + ":" + std::to_string(SGPTR + 1) + "]" +
                            (j ? " offset:" + std::to_string(4 * j) : ""));
+    }
+    if (nc > 0 && store1) {
+      // lane 63 of each accumulator holds its sum: v_readlane_b32 s_j, v_acc_j, 63 (s0..s15: routine
+      // temporaries, free here), then lane j of TS takes constant j's sum and ONE store of lanes
+      // 0..nc-1 writes the tree's nc contiguous partials (one write request per tree and row group,
+      // where a store per constant cost a request each: the round-5 PMC summary's 0.49 GB per dispatch)
+      for (int j = 0; j < nc; ++j) {
+        as.put(0xd2890000u | (uint32_t)j);
+        as.put((uint32_t)(256 + GACC + j) | (191u << 9));
+        if (as.want_text) as.lines.push_back("v_readlane_b32 s" + std::to_string(j) + ", v" + std::to_string(GACC + j) + ", 63");
+      }
+      as.sopp(0x00, "s_nop", 4);
+      for (int j = 0; j < nc; ++j) {  // v_writelane_b32 v[TS], s_j, j
+        as.put(0xd28a0000u | (uint32_t)TS);
+        as.put((uint32_t)j | ((128u + (uint32_t)j) << 9));
+        if (as.want_text)
+          as.lines.push_back("v_writelane_b32 v" + std::to_string(TS) + ", s" + std::to_string(j) + ", " + std::to_string(j));
+      }
+      as.put(0xbe80017eu | (16u << 16));  // s_mov_b64 s[16:17], exec
+      if (as.want_text) as.lines.push_back("s_mov_b64 s[16:17], exec");
+      const uint32_t mask = (uint32_t)((1ull << nc) - 1);  // s_mov_b64 exec, mask (inline constant up to 64)
+      if (mask <= 64) {
+        as.put(0xbefe0100u | (128u + mask));
+      } else {
+        as.put(0xbefe01ffu);
+        as.put(mask);
+      }
+      if (as.want_text) as.lines.push_back("s_mov_b64 exec, " + std::to_string(mask));
+      // global_store_dword v[VLANE4] (= 4·lane), v[TS], s[SGPTR:SGPTR+1]
+      as.put(0xdc708000u);
+      as.put((uint32_t)VLANE4 | ((uint32_t)TS << 8) | ((uint32_t)SGPTR << 16));
+      if (as.want_text)
+        as.lines.push_back("global_store_dword v" + std::to_string(VLANE4) + ", v" + std::to_string(TS) + ", s[" +
+                           std::to_string(SGPTR) + ":" + std::to_string(SGPTR + 1) + "]");
+      as.put(0xbefe0110u);  // s_mov_b64 exec, s[16:17]
+      if (as.want_text) as.lines.push_back("s_mov_b64 exec, s[16:17]");
     }
     as.sop1(SOP1_SETPC, "s_setpc_b64", 0, S(S_RT), "");
     if (as.want_text) as.lines.back() = "s_setpc_b64 s[" + std::to_string(S_RT) + ":" + std::to_string(S_RT + 1) + "]";
@@ -1286,13 +1353,20 @@ bool gen_grad_tree(const Ins<float>* prog, int nc, const Tmpl& T, bool text, std
   const size_t start = (out.size() + 15) / 16 * 16;
   Asm as;
   bool ok = false;
-  for (int attempt = subst ? 0 : 1; attempt < 2 && !ok; ++attempt) {
+  // SRHIP_GJIT_SINCOS=0: sin / cos derivatives by the FAST routines in the reverse pass (round 5);
+  // a tree whose fused factors exhaust the register pool is compiled without them
+  const char* sce = std::getenv("SRHIP_GJIT_SINCOS");
+  const bool fuse = !(sce && sce[0] == '0');
+  for (int attempt = subst ? 0 : 2; attempt < 4 && !ok; ++attempt) {
+    if ((attempt & 1) == 0 && !fuse) continue;
     as = Asm();
     as.want_text = text;
     GradGen g(as, T, T.area_va + start * 4);
-    g.ops = attempt == 0 ? irs : ir;
-    g.root = attempt == 0 ? roots : root;
-    if (attempt == 0) g.gbase = kGradGbase;
+    const bool sub = attempt < 2;
+    g.ops = sub ? irs : ir;
+    g.root = sub ? roots : root;
+    g.fuse_trig = (attempt & 1) == 0;
+    if (sub) g.gbase = kGradGbase;
     g.nc = nc;
     g.loss = loss;
     g.lparam = lparam;

@@ -418,17 +418,16 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_mov_b64 s[58:59], exec\n"                                                        \
   "s_mov_b64 exec, 1\n"                                                               \
   "v_mov_b32_e32 v0, s62\n"                                                           \
-  "v_mov_b32_e32 v1, s63\n"                                                           \
-  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "s_lshl_b32 s62, s60, 2\n"                                                          \
   "s_cmp_eq_u32 s52, 0\n"                                                             \
   "s_cbranch_scc1 .L" #NAME "_g1\n"                                                         \
   "v_mov_b32_e32 v2, s53\n"                                                           \
   "v_add_u32_e32 v2, s62, v2\n"                                                       \
-  "ds_write_b64 v2, v[0:1]\n"                                                         \
+  "ds_write_b32 v2, v0\n"                                                         \
   "s_branch .L" #NAME "_st1\n"                                                              \
   ".L" #NAME "_g1:\n"                                                                       \
   "v_mov_b32_e32 v2, s62\n"                                                           \
-  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  "global_store_dword v2, v0, s[50:51]\n"                                       \
   ".L" #NAME "_st1:\n"                                                                      \
   "s_cmp_eq_u32 s63, 0\n"                                                             \
   "s_cbranch_scc1 .L" #NAME "_nf\n"                                                         \
@@ -442,17 +441,16 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_mov_b64 s[58:59], exec\n"                                                        \
   "s_mov_b64 exec, 1\n"                                                               \
   "v_mov_b32_e32 v0, 0\n"                                                             \
-  "v_mov_b32_e32 v1, 0x7fc00000\n"                                                    \
-  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "s_lshl_b32 s62, s60, 2\n"                                                          \
   "s_cmp_eq_u32 s52, 0\n"                                                             \
   "s_cbranch_scc1 .L" #NAME "_g2\n"                                                         \
   "v_mov_b32_e32 v2, s53\n"                                                           \
   "v_add_u32_e32 v2, s62, v2\n"                                                       \
-  "ds_write_b64 v2, v[0:1]\n"                                                         \
+  "ds_write_b32 v2, v0\n"                                                         \
   "s_branch .L" #NAME "_st2\n"                                                              \
   ".L" #NAME "_g2:\n"                                                                       \
   "v_mov_b32_e32 v2, s62\n"                                                           \
-  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  "global_store_dword v2, v0, s[50:51]\n"                                       \
   ".L" #NAME "_st2:\n"                                                                      \
   "s_mov_b64 exec, s[58:59]\n"                                                        \
   "s_branch .L" #NAME "_next\n"                                                             \
@@ -580,17 +578,16 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_mov_b64 s[96:97], exec\n"                                                        \
   "s_mov_b64 exec, 1\n"                                                               \
   "v_mov_b32_e32 v0, s62\n"                                                           \
-  "v_mov_b32_e32 v1, s63\n"                                                           \
-  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "s_lshl_b32 s62, s60, 2\n"                                                          \
   "s_cmp_eq_u32 s52, 0\n"                                                             \
   "s_cbranch_scc1 .L" #NAME "_g1\n"                                                         \
   "v_mov_b32_e32 v2, s53\n"                                                           \
   "v_add_u32_e32 v2, s62, v2\n"                                                       \
-  "ds_write_b64 v2, v[0:1]\n"                                                         \
+  "ds_write_b32 v2, v0\n"                                                         \
   "s_branch .L" #NAME "_st1\n"                                                              \
   ".L" #NAME "_g1:\n"                                                                       \
   "v_mov_b32_e32 v2, s62\n"                                                           \
-  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  "global_store_dword v2, v0, s[50:51]\n"                                       \
   ".L" #NAME "_st1:\n"                                                                      \
   "s_cmp_eq_u32 s63, 0\n"                                                             \
   "s_cbranch_scc1 .L" #NAME "_nf\n"                                                         \
@@ -604,17 +601,16 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { ji
   "s_mov_b64 s[96:97], exec\n"                                                        \
   "s_mov_b64 exec, 1\n"                                                               \
   "v_mov_b32_e32 v0, 0\n"                                                             \
-  "v_mov_b32_e32 v1, 0x7fc00000\n"                                                    \
-  "s_lshl_b32 s62, s60, 3\n"                                                          \
+  "s_lshl_b32 s62, s60, 2\n"                                                          \
   "s_cmp_eq_u32 s52, 0\n"                                                             \
   "s_cbranch_scc1 .L" #NAME "_g2\n"                                                         \
   "v_mov_b32_e32 v2, s53\n"                                                           \
   "v_add_u32_e32 v2, s62, v2\n"                                                       \
-  "ds_write_b64 v2, v[0:1]\n"                                                         \
+  "ds_write_b32 v2, v0\n"                                                         \
   "s_branch .L" #NAME "_st2\n"                                                              \
   ".L" #NAME "_g2:\n"                                                                       \
   "v_mov_b32_e32 v2, s62\n"                                                           \
-  "global_store_dwordx2 v2, v[0:1], s[50:51]\n"                                       \
+  "global_store_dword v2, v0, s[50:51]\n"                                       \
   ".L" #NAME "_st2:\n"                                                                      \
   "s_mov_b64 exec, s[96:97]\n"                                                        \
   "s_branch .L" #NAME "_next\n"                                                             \
@@ -651,7 +647,9 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
   const int ntl = tail ? ja.ts : a.ntiles;
   const int64_t row0 = tail ? (int64_t)ja.nbig * rows + (int64_t)(rg - ja.nbig) * ja.ts * TILE : (int64_t)rg * rows;
   const int nthreads = __builtin_amdgcn_readfirstlane((int)blockDim.x);
-  Part<float>* gdst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
+  // 4-byte partials (Σ only): a failed tree is known from its slot's failure
+  // flag, which every loop sets when a row fails (finalize_kernel part4)
+  float* gdst = reinterpret_cast<float*>(a.partial) + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
   Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
   // the tree counter after the tiles (and the partials): launch() adds 16 bytes
   uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(sPart) +
@@ -764,7 +762,8 @@ __device__ __forceinline__ void jit_eval_dl_body(const JitArgs& ja) {
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (ja.part_lds) {  // slots no wave ran keep whatever: finalize ignores them
     __syncthreads();
-    for (int i = threadIdx.x; i < a.tpb; i += nthreads) gdst[i] = sPart[i];
+    const float* sPart4 = reinterpret_cast<const float*>(sPart);
+    for (int i = threadIdx.x; i < a.tpb; i += nthreads) gdst[i] = sPart4[i];
   }
 }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_dl(JitArgs ja) { jit_eval_dl_body<false, false>(ja); }

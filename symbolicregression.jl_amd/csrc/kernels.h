@@ -48,6 +48,9 @@ struct EvalArgs {
   // per-tree row sets (srhip_eval_loss_rowsets; interpreter, one tree per
   // group): tree t reads rows [t·seg, t·seg + n) of X / y / w; 0 = shared rows
   int64_t seg = 0;
+  // finalize only: the launch wrote 4-byte partials (Σ; float at partial + rg·npos + pos) and a
+  // failed tree is the one whose slot failure flag is set (the hand-written loss tree loops)
+  int part4 = 0;
 };
 
 // Geometry of one evaluation launch, chosen by plan_eval().

@@ -45,11 +45,17 @@ __global__ void __launch_bounds__(64 * kFinWaves) finalize_kernel(EvalArgs<T> a,
   const int pos = blockIdx.x * kFinPos + p;
   double s = 0.0, c = 0.0;
   if (pos < npos) {
+    if (a.part4) {  // Σ only (float: the Float32 tree code's loops)
+      const float* p4 = reinterpret_cast<const float*>(a.partial);
 #pragma unroll 4
-    for (int rg = w * kFinSub + r; rg < a.nrg; rg += kFinStride) {
-      const Part<T> q = a.partial[(size_t)rg * npos + pos];
-      s += (double)q.sum;
-      c += (double)q.chk;
+      for (int rg = w * kFinSub + r; rg < a.nrg; rg += kFinStride) s += (double)p4[(size_t)rg * npos + pos];
+    } else {
+#pragma unroll 4
+      for (int rg = w * kFinSub + r; rg < a.nrg; rg += kFinStride) {
+        const Part<T> q = a.partial[(size_t)rg * npos + pos];
+        s += (double)q.sum;
+        c += (double)q.chk;
+      }
     }
   }
   const int row = w * kFinSub + r;  // = threadIdx.x / kFinPos
@@ -71,7 +77,7 @@ __global__ void __launch_bounds__(64 * kFinWaves) finalize_kernel(EvalArgs<T> a,
     const int sidx = a.contig ? g * a.tpb + i : i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
     if (sidx < a.nlist) {
       const int t = a.list[sidx];
-      const bool ok = !__builtin_isnan(c);
+      const bool ok = a.part4 ? a.fail[sidx] == 0u : !__builtin_isnan(c);
       out_sum[t] = ok ? s : __builtin_nan("");
       out_ok[t] = ok ? 1 : 0;
       if (a.fail) a.fail[sidx] = 0u;

@@ -45,7 +45,7 @@ from .dataset import Dataset
 from .interface import compute_complexity, eval_loss_batch, loss_to_score, update_baseline_loss_
 from .node import Node, _postorder, string_tree
 from .options import Options
-from .trees import _set_node, append_random_op, gen_random_tree, gen_random_tree_fixed_size, make_random_leaf
+from .trees import gen_random_tree
 
 MUTATION_WEIGHTS = dict(mutate_constant=0.048, mutate_operator=0.47, add_node=0.79, insert_node=5.1,
                         delete_node=1.7, simplify=0.0020, randomize=0.00023, do_nothing=0.21, optimize=0.0)
@@ -108,67 +108,29 @@ def _depth(t: Node) -> int:
     return 1 + max(_depth(t.l), _depth(t.r) if t.degree == 2 else 0)
 
 
-def _nodes_and_parents(tree: Node):
-    out, stack = [], [(tree, None, None)]
-    while stack:
-        t, p, side = stack.pop()
-        out.append((t, p, side))
-        if t.degree >= 1:
-            stack.append((t.l, t, "l"))
-        if t.degree == 2:
-            stack.append((t.r, t, "r"))
-    return out
-
-
 def mutate(tree: Node, choice: str, options: Options, nfeat: int, T, temperature: float, curmaxsize: int,
            rng: np.random.Generator) -> Node:
-    """One mutation of a copy of `tree` (MutationFunctions.jl)."""
-    t = tree.copy()
-    nodes = _nodes_and_parents(t)
+    """One mutation of a copy of `tree` (MutationFunctions.jl), by the same
+    functions as the default path (srhip.evolution; one implementation of the
+    mutation rules for both search variants)."""
+    from . import evolution as E
+
+    t = E.copy_node(tree)
     if choice == "mutate_constant":
-        consts = [n for n, _, _ in nodes if n.degree == 0 and n.constant]
-        if consts:
-            n = consts[rng.integers(len(consts))]
-            max_change = _opt(options, "perturbation_factor") * temperature + 1.1
-            factor = max_change ** rng.random()
-            n.val = T(n.val * factor) if rng.random() > 0.5 else T(n.val / factor)
-            # as written in MutationFunctions.jl:74-76: negates unless rand() <= p
-            if rng.random() > _opt(options, "probability_negate_constant"):
-                n.val = T(-n.val)
-        return t
+        return E.mutate_constant(t, temperature, options, T, rng)
     if choice == "mutate_operator":
-        ops = [n for n, _, _ in nodes if n.degree > 0]
-        if ops:
-            n = ops[rng.integers(len(ops))]
-            n.op = int(rng.integers(1, (options.nuna if n.degree == 1 else options.nbin) + 1))
-        return t
-    if choice == "add_node":
+        return E.mutate_operator(t, options, rng)
+    if choice == "add_node":  # Mutate.jl: append or prepend with equal probability
         if rng.random() < 0.5:
-            return append_random_op(t, options, nfeat, T, rng)
-        return _new_op(t, options, nfeat, T, rng)  # prepend
+            return E.append_random_op(t, options, nfeat, T, rng)
+        return E.prepend_random_op(t, options, nfeat, T, rng)
     if choice == "insert_node":
-        n = nodes[rng.integers(len(nodes))][0]
-        _set_node(n, _new_op(n.copy(), options, nfeat, T, rng))
-        return t
+        return E.insert_random_op(t, options, nfeat, T, rng)
     if choice == "delete_node":
-        n, parent, side = nodes[rng.integers(len(nodes))]
-        if n.degree == 0:
-            _set_node(n, make_random_leaf(nfeat, T, rng))
-            return t
-        keep = n.l if (n.degree == 1 or rng.random() < 0.5) else n.r
-        if parent is None:
-            return keep
-        setattr(parent, side, keep)
-        return t
+        return E.delete_random_op(t, options, nfeat, T, rng)
     if choice == "randomize":
-        return gen_random_tree_fixed_size(int(rng.integers(1, curmaxsize + 1)), options, nfeat, T, rng)
+        return E.gen_random_tree_fixed_size(int(rng.integers(1, curmaxsize + 1)), options, nfeat, T, rng)
     return t  # do_nothing / simplify
-
-
-def _new_op(left: Node, options: Options, nfeat: int, T, rng) -> Node:
-    if rng.random() < options.nbin / (options.nuna + options.nbin):
-        return Node(int(rng.integers(1, options.nbin + 1)), left, make_random_leaf(nfeat, T, rng))
-    return Node(int(rng.integers(1, options.nuna + 1)), left)
 
 
 class _CallbackEvaluator:

@@ -55,7 +55,7 @@ def main():
     flat = srhip.flatten(trees, o, dtype=np.float32)
     progs = []
     for v in args.variants:
-        env = dict(kv.split("=", 1) for kv in v.split())
+        env = dict(kv.split("=", 1) for kv in v.replace(",", " ").split())  # "A=1,B=0": two knobs
         old = {k: os.environ.get(k) for k in env}
         os.environ.update(env)
         try:
@@ -69,7 +69,7 @@ def main():
                 else:
                     os.environ[k] = x
     call = (lambda p: p.eval_loss_grad(ds, K.LOSS["L2"])) if args.grad else (lambda p: p.eval_loss(ds, 0))
-    res = [call(p) for p in progs]
+    res = [tuple(np.array(x, copy=True) if hasattr(x, "shape") else x for x in call(p)) for p in progs]
     for p in progs:  # warm-up
         for _ in range(3):
             call(p)
@@ -86,6 +86,10 @@ def main():
                               "did_succeed_equal": bool(np.array_equal(k, k0)),
                               "loss_equal": bool(np.array_equal(s[k & k0], s0[k & k0])),
                               "grad_equal": bool(np.array_equal(g[okc], g0[okc], equal_nan=True)),
+                              # a variant that evaluates a derivative differently (SRHIP_GJIT_SINCOS):
+                              # constants off the first variant's by > 1e-4 relative, and the largest
+                              "grad_rel_gt_1e-4": int(np.sum(~(np.abs(g[okc] - g0[okc]) <= 1e-4 * np.abs(g0[okc])))),
+                              "grad_max_rel": float(np.nanmax(np.abs(g[okc] - g0[okc]) / np.maximum(np.abs(g0[okc]), 1e-30))),
                               "grad_jit": p.grad_jit_info(),
                               "ntrees": len(trees)}))
             sys.stdout.flush()

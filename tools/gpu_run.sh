@@ -59,7 +59,7 @@ pmc_passes() {
     timeout -s KILL 150 rocprofv3 --pmc $P --output-format csv -d "$out/pmc$i" -o pmc$i -- "$@" \
       > "$out/run_pmc$i.out" 2>> "$out/log.txt" || { echo "pmc pass $i failed"; exit 1; }
   done
-  KERNEL="$kern" python3 tools/pmc_summary.py "$out" > "$out/summary.json" && cat "$out/summary.json"
+  KERNEL="$kern" WORKLOAD="${WORKLOAD:-config#2}" python3 tools/pmc_summary.py "$out" > "$out/summary.json" && cat "$out/summary.json"
 }
 run_profile() {
   local OUT=gpurun_out/benchprof
@@ -70,7 +70,11 @@ run_profile() {
 }
 run_pmc() {
   [ -n "$PMC_CMD" ] || { echo "PMC_CMD not set"; exit 2; }
-  pmc_passes gpurun_out/pmc "${PMC_KERNEL:-sr_jit}" $PMC_CMD
+  mkdir -p gpurun_out/pmc
+  # the same command under the kernel trace first: the summary's avg_ms_kernel_trace
+  timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/pmc/kt -o kt -- $PMC_CMD \
+    > gpurun_out/pmc/kt.out 2>> gpurun_out/pmc/log.txt || { echo "kernel trace failed"; exit 1; }
+  WORKLOAD="${PMC_WORKLOAD:-unlabelled}" pmc_passes gpurun_out/pmc "${PMC_KERNEL:-sr_jit}" $PMC_CMD
 }
 run_search() {
   timeout -k 10 700 $PYTEST tests/test_evolution.py tests/test_search.py tests/test_configs_gpu.py -m gpu -s \
