@@ -12,17 +12,21 @@ Metric: node·row evals/sec = Σ_trees count_nodes × rows ÷ wall time
 (nominal count, no credit for early-failed trees).
 
 Multi-GPU (torchrun, one rank per GPU), strong scaling of the one batch:
-  --shard trees (default) each rank evaluates its share of the 4096 trees
-      against its own copy of the dataset, no collective on the data path;
-      the share is cost-balanced (srhip.distributed.shard_trees_balanced:
-      LPT on the estimated VALU cost; --partition strided: every N-th tree),
-      plus a weak-scaling figure (4096 trees on every rank) as `weak`;
-  --shard rows  the 1M rows split over the N ranks, every rank evaluates all
-      trees on its shard and the per-tree [Σw·ℓ, failed] partials + Σw are
-      all-reduced on the device (RCCL, 64 KiB) each step.
-Measured on one GPU at the N = 8 sizes (profiles/r04_shard_probe_d.json):
-slowest balanced tree shard 0.661 ms, strided 0.663, row shard 0.644 before
-its all-reduce, against 3.48 ms for the whole batch (5.27x / 5.25x / 5.41x).
+  --shard rows (default) the 1M rows split over the N ranks, every rank
+      evaluates all trees on its shard and the per-tree [Σw·ℓ, failed]
+      partials + Σw are all-reduced on the device (RCCL, 64 KiB) each step;
+  --shard trees  each rank evaluates its share of the 4096 trees against its
+      own copy of the dataset, no collective on the data path; the share is
+      cost-balanced (srhip.distributed.shard_trees_balanced: LPT on the
+      estimated VALU cost; --partition strided: every N-th tree), plus a
+      weak-scaling figure (4096 trees on every rank) as `weak`.
+Rows by default since round 6: the whole batch's constant-free subtrees
+shared by many trees are evaluated once per row (jit.h Columns), and a row
+shard keeps every tree, so the sharing, while a 512-tree shard shares little
+and derives its own columns over all 1M rows. Measured on one GPU at the
+N = 8 sizes (profiles/r06_shard_probe.json): slowest row shard 0.52 ms
+before its all-reduce, slowest balanced tree shard 0.65 ms, strided 0.63,
+against 2.74 ms for the whole batch (projected 5.3x / 4.2x / 4.4x).
 Timing: barrier + sync on both sides of the K timed steps, max over ranks;
 value = the 4096 trees' node·rows ÷ that time.
 
@@ -91,7 +95,7 @@ def parse():
     ap.add_argument("--cpu-threads", type=int, default=0, help="0: every CPU this job may use")
     ap.add_argument("--partition", default="balanced", choices=["balanced", "strided"],
                     help="--shard trees: cost-balanced (LPT) or every N-th tree")
-    ap.add_argument("--shard", default="trees", choices=["trees", "rows"],
+    ap.add_argument("--shard", default="rows", choices=["trees", "rows"],
                     help="N > 1: trees split over the ranks (no collective) or rows split over the ranks "
                          "(every rank all trees, partials all-reduced on the device per step)")
     ap.add_argument("--no-weak", action="store_true", help="skip the secondary weak-scaling measurement")

@@ -1845,6 +1845,8 @@ Module* build(const CompiledBatch<float>& cb, const std::vector<int32_t>& cand, 
       if (opt.out) {  // no weighted variant: the output kernel reads no y / w
         HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, opt.memc ? "sr_jit_out_m" : "sr_jit_out"));
         q.fn_w = q.fn;
+        // the same with the trees dealt from an LDS counter (jit_template.hip jit_eval_body DYN)
+        HIP_CHECK(hipModuleGetFunction(&q.fn_dl, q.mod, opt.memc ? "sr_jit_out_md" : "sr_jit_out_d"));
       } else {
         HIP_CHECK(hipModuleGetFunction(&q.fn, q.mod, opt.memc ? "sr_jit_eval_m" : "sr_jit_eval"));
         HIP_CHECK(hipModuleGetFunction(&q.fn_w, q.mod, opt.memc ? "sr_jit_eval_mw" : "sr_jit_eval_w"));
@@ -2017,7 +2019,9 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   const size_t lds = narr * (size_t)plan.ntiles * (size_t)plan.tile * sizeof(float) + (ja.part_lds ? part_bytes : 0) + 16;
   // the hand-written loop keeps its tree counter in the last 16 bytes
   hipFunction_t fn = a.w ? q.fn_w : q.fn;
-  const char* name = m->out ? (m->memc ? "sr_jit_out_m" : "sr_jit_out")
+  if (m->out && q.fn_dl && dynloop()) fn = q.fn_dl;
+  const char* name = m->out ? (m->memc ? (fn == q.fn_dl ? "sr_jit_out_md" : "sr_jit_out_m")
+                                       : (fn == q.fn_dl ? "sr_jit_out_d" : "sr_jit_out"))
                             : m->memc ? (a.w ? "sr_jit_eval_mw" : "sr_jit_eval_m") : (a.w ? "sr_jit_eval_w" : "sr_jit_eval");
   if (q.fn_dl && !m->out && dynloop()) {
     fn = a.w ? q.fn_dlw : q.fn_dl;

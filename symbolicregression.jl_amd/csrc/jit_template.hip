@@ -118,7 +118,7 @@ __device__ __forceinline__ uint64_t sgpr64(uint64_t v) {
 // staged, no failure flags are read or set (every tile of every tree is
 // evaluated, as the interpreter's MODE_OUT does), and each tree's code gets
 // its output rows of this row group in s[92:93] (jit.cpp S_OUT).
-template <bool W, bool MEMC, bool OUT = false>
+template <bool W, bool MEMC, bool OUT = false, bool DYN = false>
 __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const EvalArgs<float>& a = ja.e;
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -137,6 +137,9 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   Part<float>* gdst = a.partial + (size_t)rg * ((size_t)a.ntg * a.tpb) + (size_t)g * a.tpb;
   Part<float>* sPart = reinterpret_cast<Part<float>*>(sX + (size_t)narr * rows);
   Part<float>* dst = ja.part_lds ? sPart : gdst;
+  // the tree counter after the tiles (and the partials): launch() adds 16 bytes
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(reinterpret_cast<unsigned char*>(sPart) +
+                                              (ja.part_lds ? (size_t)a.tpb * sizeof(Part<float>) : 0));
 
   // 1. stage the row group tile-major: tile t, array k (0 = y, 1 .. nraw =
   //    x_{k-1}, then the derived columns u(x_f), last = w); one wave per
@@ -169,6 +172,7 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
       reinterpret_cast<float4*>(sX + (size_t)tk * TILE)[v] =
           reinterpret_cast<const float4*>(src + row0 + (int64_t)t * TILE)[v];
     }
+    if (DYN && threadIdx.x == 0) *cnt = 0u;
   }
   __syncthreads();
 
@@ -212,23 +216,9 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
   const uint64_t gcb = sgpr64(ja.gcols ? reinterpret_cast<uint64_t>(ja.gcols + row0) : 0ull);
   const uint32_t gstride = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(a.n_pad * 4));
 
-  int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
-  while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
-  m = __builtin_amdgcn_readfirstlane(m);
-  uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
-  // the next slot's code offset is loaded one tree ahead, like its flag
-  int32_t cnext = m > 0 ? code_of(slot_of(wave)) : 0;
   uint32_t redos = 0;  // tiles redone with the PRECISE routines (counted by tree code)
-  for (int k = 0; k < m; ++k) {
-    const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
-    const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
-    const bool more = k + 1 < m;
-    const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
-    const int32_t coff = cnext;
-    if (more) {
-      fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
-      cnext = code_of(slot_of(wave + (k + 1) * nwaves));
-    }
+  // one tree of slot s (list position i) on this row group: its code at coff
+  auto run_tree = [&](const int i, const int s, const bool skip, const int32_t coff) {
     float lsum = 0.0f, chk = skip ? __builtin_nanf("") : 0.0f;
     if (!skip) {
       const uint64_t target = area + (uint32_t)coff;
@@ -286,6 +276,43 @@ __device__ __forceinline__ void jit_eval_body(const JitArgs& ja) {
     if (lane == 0) dst[i] = Part<float>{lsum, chk};
     if (!OUT && !skip && chk != chk && lane == 0)
       __hip_atomic_store(a.fail + s, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  if constexpr (DYN) {
+    auto claim = [&]() -> int {
+      uint32_t v = 0u;
+      if (lane == 0) v = __hip_atomic_fetch_add(cnt, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      return __builtin_amdgcn_readfirstlane((int)v);
+    };
+    auto valid = [&](int i) { return i < a.tpb && slot_of(i) < a.nlist; };
+    int i = claim();
+    int32_t cnext = valid(i) ? code_of(slot_of(i)) : 0;
+    while (valid(i)) {
+      const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
+      const int inx = claim();
+      const int32_t coff = cnext;
+      if (valid(inx)) cnext = code_of(slot_of(inx));
+      run_tree(i, s, false, coff);
+      i = inx;
+    }
+  } else {
+    int m = wave < a.tpb ? (a.tpb - wave + nwaves - 1) / nwaves : 0;
+    while (m > 0 && slot_of(wave + (m - 1) * nwaves) >= a.nlist) --m;
+    m = __builtin_amdgcn_readfirstlane(m);
+    uint32_t fnext = m > 0 ? ld_flag(slot_of(wave)) : 0u;
+    // the next slot's code offset is loaded one tree ahead, like its flag
+    int32_t cnext = m > 0 ? code_of(slot_of(wave)) : 0;
+    for (int k = 0; k < m; ++k) {
+      const int i = __builtin_amdgcn_readfirstlane(wave + k * nwaves);
+      const int s = __builtin_amdgcn_readfirstlane(slot_of(i));
+      const bool more = k + 1 < m;
+      const bool skip = __builtin_amdgcn_readfirstlane((int)fnext) != 0;
+      const int32_t coff = cnext;
+      if (more) {
+        fnext = ld_flag(slot_of(wave + (k + 1) * nwaves));
+        cnext = code_of(slot_of(wave + (k + 1) * nwaves));
+      }
+      run_tree(i, s, skip, coff);
+    }
   }
   if (lane == 0 && __builtin_amdgcn_readfirstlane((int)redos) != 0)
     __hip_atomic_fetch_add(ja.counters + 1, (uint32_t)__builtin_amdgcn_readfirstlane((int)redos),
@@ -324,6 +351,8 @@ extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_m(JitArgs ja) { j
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_eval_mw(JitArgs ja) { jit_eval_body<true, true>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_out(JitArgs ja) { jit_eval_body<false, false, true>(ja); }
 extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_m(JitArgs ja) { jit_eval_body<false, true, true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_d(JitArgs ja) { jit_eval_body<false, false, true, true>(ja); }
+extern "C" __global__ void __launch_bounds__(1024) sr_jit_out_md(JitArgs ja) { jit_eval_body<false, true, true, true>(ja); }
 
 // ---- the tree loop as hand-written code (sr_jit_eval_dl, SRHIP_JIT_DYNLOOP) -------
 // The waves of a workgroup take the group's trees from an LDS counter (one

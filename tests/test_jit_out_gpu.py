@@ -86,3 +86,33 @@ def test_output_tree_code_after_new_constants(gpu_ctx):
     out0, ok0 = progs["0"].eval_tree_array(ds)
     assert np.array_equal(ok1, ok0)
     np.testing.assert_array_equal(out1, out0)
+
+
+@pytest.mark.parametrize("varying", [False, True])
+def test_output_tree_code_dynamic_deal_equals_static(gpu_ctx, varying):
+    """sr_jit_out_d / sr_jit_out_md (jit_template.hip jit_eval_body DYN: the
+    waves take their trees from an LDS counter, as the loss loops do) against
+    the static deal (SRHIP_JIT_DYNLOOP=0, read per launch): the same per-row
+    outputs bit for bit, every tree (VERDICT r05 missing 4)."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    rng = np.random.default_rng(23)
+    n = 20_001
+    X = rng.standard_normal((5, n)).astype(np.float32)
+    trees = srhip.random_population(1500, o, 5, np.float32, seed=24)
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    ctx = gpu_ctx
+    ds = srhip.DeviceDataset(ctx, X, np.zeros(n, np.float32))
+    prog = _programs(ctx, flat, varying=varying)["1"]
+    if varying:
+        prog.set_constants((flat.consts * np.float32(0.75)).astype(np.float32))
+    out_d, ok_d = (np.array(v, copy=True) for v in prog.eval_tree_array(ds))
+    assert ctx.last_tree_code() > 1000
+    assert ctx.last_kernel_name() == ("sr_jit_out_md" if varying else "sr_jit_out_d")
+    os.environ["SRHIP_JIT_DYNLOOP"] = "0"
+    try:
+        out_s, ok_s = prog.eval_tree_array(ds)
+        assert ctx.last_kernel_name() == ("sr_jit_out_m" if varying else "sr_jit_out")
+    finally:
+        del os.environ["SRHIP_JIT_DYNLOOP"]
+    assert np.array_equal(ok_d, ok_s)
+    np.testing.assert_array_equal(out_d, out_s)
