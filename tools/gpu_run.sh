@@ -84,6 +84,9 @@ run_search() {
   timeout -k 10 400 python -u tools/run_search.py config1 --iterations 40 --out gpurun_out/search_config1.json \
     > gpurun_out/search_c1.log 2>&1 || exit $?
   tail -3 gpurun_out/search_c1.log | cut -c1-400
+  timeout -k 10 400 python -u tools/run_search.py config1 --iterations 40 --batching --out gpurun_out/search_config1_batching.json \
+    > gpurun_out/search_c1b.log 2>&1 || exit $?
+  tail -3 gpurun_out/search_c1b.log | cut -c1-400
   timeout -k 10 600 python -u tools/run_search.py config4 --iterations ${C4_ITERS:-3} --out gpurun_out/search_config4.json \
     > gpurun_out/search_c4.log 2>&1 || exit $?
   tail -5 gpurun_out/search_c4.log | cut -c1-600

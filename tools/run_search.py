@@ -40,20 +40,50 @@ def data(cfg):
 
 
 class TimedEngine(E.EngineEvaluator):
-    """The engine evaluator, printing a progress line every ~20 s."""
+    """The engine evaluator, printing a progress line every ~20 s, and timing
+    each request kind: calls, trees, host seconds inside the call (flatten,
+    program build, launch, wait) and the device time of its kernels (HIP
+    events of the context, srhip Context.last_kernel_time)."""
 
     def __init__(self, *a):
         super().__init__(*a)
         self.t_last = time.perf_counter()
         self.calls = 0
+        self.kinds = {k: {"calls": 0, "trees": 0, "host_s": 0.0, "kernel_ms": 0.0}
+                      for k in ("losses", "losses_rows", "optimize")}
 
-    def losses(self, trees):
+    def _timed(self, kind, n, fn):
         self.calls += 1
         now = time.perf_counter()
         if now - self.t_last > 20:
             print(json.dumps({"progress_calls": self.calls}), flush=True)
             self.t_last = now
-        return super().losses(trees)
+        out = fn()
+        k = self.kinds[kind]
+        k["host_s"] += time.perf_counter() - now
+        k["calls"] += 1
+        k["trees"] += n
+        if kind != "optimize":
+            k["kernel_ms"] += float(srhip.get_context(0).last_kernel_time()[0])
+        return out
+
+    def losses(self, trees):
+        return self._timed("losses", len(trees), lambda: super(TimedEngine, self).losses(trees))
+
+    def losses_rows(self, trees, rows):
+        return self._timed("losses_rows", len(trees), lambda: super(TimedEngine, self).losses_rows(trees, rows))
+
+    def optimize(self, trees, noise):
+        return self._timed("optimize", len(trees), lambda: super(TimedEngine, self).optimize(trees, noise))
+
+    def report(self):
+        out = {}
+        for kind, k in self.kinds.items():
+            if k["calls"]:
+                out[kind] = dict(k, host_ms_per_call=1e3 * k["host_s"] / k["calls"],
+                                 kernel_ms_per_call=k["kernel_ms"] / k["calls"] if kind != "optimize" else None,
+                                 trees_per_call=k["trees"] / k["calls"])
+        return out
 
 
 def main():
@@ -62,8 +92,13 @@ def main():
     ap.add_argument("--iterations", type=int, default=None)
     ap.add_argument("--seed", type=int, default=0)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--batching", action="store_true",
+                    help="Options(batching=true, batch_size=50): score_func_batch's per-candidate row samples, "
+                         "all candidates of a round in one launch (srhip_eval_loss_rowsets)")
     a = ap.parse_args()
     X, y, o = data(a.config)
+    if a.batching:
+        o.batching = True
     nit = a.iterations or (40 if a.config == "config1" else 2)
     ds = srhip.Dataset(X, y)
     ev = TimedEngine(ds, o)
@@ -75,7 +110,8 @@ def main():
     rec = {"tool": "run_search", "config": a.config, "npopulations": o.npopulations, "niterations": nit,
            "rows": int(X.shape[1]), "nfeat": int(X.shape[0]), "options": "defaults (fast_cycle=false, "
            "crossover_probability=0.066, tournament_selection_p=0.86, use_frequency, optimizer_probability=0.14)",
-           "wall_s": wall, **{k: v for k, v in st.items() if k != "result"},
+           "batching": bool(o.batching), "wall_s": wall, **{k: v for k, v in st.items() if k != "result"},
+           "engine_by_kind": ev.report(),
            "hall_of_fame": [{"complexity": srhip.compute_complexity(m.tree, o), "loss": m.loss, "score": m.score,
                              "equation": srhip.string_tree(m.tree, o)} for m in front],
            "flat": {"node_off": flat.node_off.tolist(), "kind": flat.kind.tolist(), "arg": flat.arg.tolist(),
