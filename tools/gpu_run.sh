@@ -16,6 +16,9 @@
 #   final     suite, smoke, bench, profile
 #   tests     some GPU tests: TESTS="tests/test_a.py tests/test_b.py -k x"   -> gpurun_out/pytest_some.log
 #   tool      one measurement tool: TOOL="tools/ab_build.py --grad A B"       -> gpurun_out/tool.log
+#   envab     bench kernel time under environment settings, interleaved over ROUNDS (default 2):
+#             ENV_VARIANTS="default SRHIP_TREE_NT=6 SRHIP_JIT_GCOLS=16,SRHIP_JIT_STICKY_TREE=1 SRHIP_LIB=ab/x.so"
+#             (replaces the single-use *_probe.sh / *_ab.sh scripts of rounds 3-6)
 # Measurement tools run on the box through this script (each under timeout):
 # ab_env.py / loop_ab.py (interleaved A/Bs), step_overhead.py, out_copy.py,
 # prof_grad.py, prof_target.py, shard_probe.py, bench_constopt.py,
@@ -116,6 +119,19 @@ run_tool() {
   timeout -k 10 ${TOOL_TIMEOUT:-600} python -u $TOOL > gpurun_out/tool.log 2> gpurun_out/tool.err || { tail -20 gpurun_out/tool.err; exit 1; }
   cat gpurun_out/tool.log | cut -c1-700
 }
+run_envab() {
+  mkdir -p gpurun_out/envab
+  local r v E tag
+  for r in $(seq ${ROUNDS:-2}); do
+    for v in ${ENV_VARIANTS:-default}; do
+      E=$(echo "$v" | tr ',' ' '); [ "$v" = default ] && E=""
+      tag=$(echo "$v" | tr -c 'A-Za-z0-9_=\n' '_')
+      env $E timeout -k 10 200 python3 bench.py --steps 20 --warmup 5 --no-cpu --no-row-shard \
+        > gpurun_out/envab/${tag}_$r.json 2>> gpurun_out/envab/err.log || { echo "$v failed"; exit 1; }
+      python3 -c "import json; d=json.loads(open('gpurun_out/envab/${tag}_$r.json').read().strip().splitlines()[-1]); print('$v', round(d['value']/1e12, 3), round(d['roofline']['kernel_ms'], 4))"
+    done
+  done
+}
 run_jitall() {
   SRHIP_JIT=1 timeout -k 10 600 $PYTEST tests -m gpu -k "not evolution and not search" > gpurun_out/pytest_jitall.log 2>&1
   rc=$?; echo "SRHIP_JIT=1 rc=$rc"; tail -2 gpurun_out/pytest_jitall.log
@@ -135,6 +151,7 @@ for mode in "$@"; do
     final) run_suite; run_smoke; run_bench; run_profile ;;
     tests) run_tests ;;
     tool) run_tool ;;
+    envab) run_envab ;;
     *) echo "unknown mode $mode"; exit 2 ;;
   esac
 done
