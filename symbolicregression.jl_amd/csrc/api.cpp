@@ -270,6 +270,10 @@ struct srhip_program {
   // tree code is compiled for one constant set: a program whose constants are
   // set again (srhip_program_set_constants) runs on the interpreter
   bool jit_allowed = true;
+  // tree code whatever the tree count (the shared-subtree derive program: a few dozen subtrees
+  // over every row of the call; jit_wanted's 256-tree bar is for the cost of loading a code object
+  // per program, which this program pays once and keeps)
+  bool jit_forced = false;
   // tree code reads its constants from the device programs (jit::Options::memc):
   // built at the first new constant set, after which set_constants only
   // updates the programs in place
@@ -935,7 +939,7 @@ void build_program(srhip_program* p) {
   p->nlist_j = 0;
   p->jit_stats = jit::Stats();
   if constexpr (std::is_same<T, float>::value) {
-    if (p->jit_allowed && jit_wanted((int)a.size())) {
+    if (p->jit_allowed && (jit_wanted((int)a.size()) || (p->jit_forced && jit::available() && !a.empty()))) {
       std::vector<int32_t> jl, rest;
       jit::Options jo;
       jo.fast = jit_fast_enabled();
@@ -1404,6 +1408,10 @@ jit::GradModule64* grad_module64(srhip_program* p, int loss, double lparam) {
 // node on any row (src/InterfaceDynamicExpressions.jl:17-48).
 // slot / keys: the program's cache of the subtree program (p->shared for the
 // loss tree code, p->gshared for the gradient tree code).
+bool derive_jit_enabled() {
+  static const bool on = [] { const char* e = std::getenv("SRHIP_DERIVE_JIT"); return !(e && e[0] == '0'); }();
+  return on;
+}
 void derive_shared(srhip_ctx* c, srhip_program*& slot, std::vector<std::string>& keys, const jit::Columns& jc,
                    const float* X, int64_t rows, int64_t n_pad, int nfeat) {
   hipStream_t s = c->stream;
@@ -1417,7 +1425,9 @@ void derive_shared(srhip_ctx* c, srhip_program*& slot, std::vector<std::string>&
     q->ctx = c;
     q->dtype = SRHIP_F32;
     q->ntrees = jc.ngcol;
-    q->jit_allowed = false;
+    // per-row output tree code for the subtrees (SRHIP_DERIVE_JIT=0: the interpreter's MODE_OUT)
+    q->jit_allowed = derive_jit_enabled();
+    q->jit_forced = true;
     q->node_off.assign(jc.goff.begin(), jc.goff.end());
     q->const_off.assign((size_t)jc.ngcol + 1, 0);
     q->kind = jc.gkind;
@@ -1440,6 +1450,59 @@ void derive_shared(srhip_ctx* c, srhip_program*& slot, std::vector<std::string>&
   c->gok.ensure((size_t)ng);
   float* out = static_cast<float*>(c->gderived.p);
   if (q->nlist_a + q->nlist_b != ng) throw Error(SRHIP_ERR_INVALID, "shared subtree failed statically");
+  // every subtree as per-row output tree code (jit_template.hip sr_jit_out_d, PRECISE routines:
+  // the interpreter's values bit for bit, test_jit_out_gpu.py): one launch per code object part
+  jit::Module* om = (q->jit && q->nlist_j == ng && rows > 0) ? out_module(q) : nullptr;
+  if (om && !jit::module_bails(om)) {
+    const jit::Columns& jc2 = jit::columns(om);
+    if (jc2.nraw > nfeat) throw Error(SRHIP_ERR_INVALID, "dataset has fewer features than the subtrees read");
+    const int narr = 1 + jc2.nraw + jc2.nder;
+    const int jw = jc2.waves;
+    const size_t lds_wg = jit::lds_per_workgroup(jw);
+    const size_t budget = std::max(jit_tile_budget() * jw / 4,
+                                   lds_wg - (jit::part_global() ? 0 : std::min<size_t>(lds_wg / 4, 8192)));
+    for (int k = 0; k < jit::nparts(om); ++k) {
+      int s0, nsl;
+      jit::part(om, k, &s0, &nsl);
+      if (nsl == 0) continue;
+      EvalPlan plan;
+      if (!plan_geometry(4, 4, kShallowSlots, narr, 1, rows, nsl, &plan, budget, 52 * 1024 * jw / 4,
+                         16384 * 4 / jw, 64 * jw / 4))
+        throw Error(SRHIP_ERR_UNSUPPORTED, "row tile of " + std::to_string(nfeat) + " features does not fit in LDS");
+      plan.threads = 64 * jw;
+      tail_split(c, &plan, rows, jw);
+      EvalArgs<float> a;
+      a.prog = static_cast<const Ins<float>*>(q->d_code);
+      a.tree_off = q->d_tree_off;
+      a.list = q->d_list + s0;
+      a.list_off = q->d_list + (q->nlist_a + q->nlist_b) + s0;
+      a.fail = nullptr;
+      a.ti_rec = nullptr;
+      a.nlist = nsl;
+      a.X = X;
+      a.y = nullptr;
+      a.w = nullptr;
+      a.n = rows;
+      a.n_pad = n_pad;
+      a.nfeat = nfeat;
+      a.ntiles = plan.ntiles;
+      a.ntg = plan.ntg;
+      a.tpb = plan.tpb;
+      a.nrg = plan.nrg;
+      a.loss = SRHIP_LOSS_L2;
+      a.rotate = rg_xcd() ? rotate_mode() : (rotate_enabled() ? 1 : 0);
+      a.contig = 0;
+      a.lparam = 0.0;
+      c->gpartial.ensure((size_t)plan.nrg * plan.ntg * plan.tpb * sizeof(Part<float>));
+      a.partial = static_cast<Part<float>*>(c->gpartial.p);
+      a.out = out;
+      a.out_stride = n_pad;
+      HIP_CHECK(jit::launch(om, k, plan, a, false, nullptr, s, nullptr));
+      HIP_CHECK(launch_finalize<float>(a, static_cast<double*>(c->gsum.p), static_cast<uint8_t*>(c->gok.p), s));
+    }
+    HIP_CHECK(launch_poison_columns(static_cast<const uint8_t*>(c->gok.p), ng, out, n_pad, s));
+    return;
+  }
   const int lists[2][2] = {{0, q->nlist_a}, {q->nlist_a, q->nlist_b}};
   for (int pass = 0; pass < 2; ++pass) {
     const int s0 = lists[pass][0], nlist = lists[pass][1];

@@ -5,6 +5,7 @@ strided shard, over 1M / 500k / 250k / 125k rows, each timed
   ok_only   the trees that succeed on the 1M rows only (the failing trees'
             work until their row groups skip them is per launch, not per row)
   precise   every tile PRECISE (SRHIP_JIT_FAST=0: no redone tiles)
+  gcols0    no shared-subtree columns (SRHIP_JIT_GCOLS=0: no derive pass)
 Kernel time = median HIP-event time of K calls. One JSON line per case plus
 the least-squares fit kernel_ms = a + b·rows per (set, variant)."""
 import json
@@ -31,7 +32,7 @@ def main():
     trees = srhip.random_population(4096, o, 5, np.float32, seed=1000, maxsize=30)
     ctx = srhip.get_context(0)
     dss = {n: srhip.DeviceDataset(ctx, np.ascontiguousarray(X[:, :n]), y[:n]) for n in
-           (1_000_000, 500_000, 250_000, 125_000)}
+           (1_000_000, 500_000, 250_000, 125_000, 62_500)}
 
     def timed(sub, ds):
         prog = srhip.Program(ctx, srhip.flatten(sub, o, dtype=np.float32), np.float32)
@@ -47,11 +48,16 @@ def main():
     shard = [trees[i] for i in shard_trees(len(trees), 0, 8)]
     sets = {"4096": trees, "4096_ok": [t for t, k in zip(trees, ok_full) if k],
             "512": shard, "512_ok": [trees[i] for i in shard_trees(len(trees), 0, 8) if ok_full[i]]}
+    only = os.environ.get("FIXED_SETS")  # e.g. "4096,4096_ok"
+    if only:
+        sets = {k: v for k, v in sets.items() if k in only.split(",")}
     fits = {}
     for name, sub in sets.items():
-        for variant in ("default", "precise"):
+        for variant in ("default", "precise", "gcols0"):
             if variant == "precise":
                 os.environ["SRHIP_JIT_FAST"] = "0"
+            if variant == "gcols0":  # no shared-subtree columns (read per build)
+                os.environ["SRHIP_JIT_GCOLS"] = "0"
             pts = []
             try:
                 for n, ds in dss.items():
@@ -64,6 +70,7 @@ def main():
                     pts.append((n, ms))
             finally:
                 os.environ.pop("SRHIP_JIT_FAST", None)
+                os.environ.pop("SRHIP_JIT_GCOLS", None)
             r = np.asarray([p[0] for p in pts], dtype=float)
             t = np.asarray([p[1] for p in pts])
             b, a = np.polyfit(r, t, 1)
