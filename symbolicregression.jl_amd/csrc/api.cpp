@@ -274,6 +274,8 @@ struct srhip_program {
   // over every row of the call; jit_wanted's 256-tree bar is for the cost of loading a code object
   // per program, which this program pays once and keeps)
   bool jit_forced = false;
+  // gradient tree code allowed (the rerun of Periodic's handed-back trees: none)
+  bool gjit_allowed = true;
   // tree code reads its constants from the device programs (jit::Options::memc):
   // built at the first new constant set, after which set_constants only
   // updates the programs in place
@@ -698,7 +700,7 @@ void build_grad_program(srhip_program* p) {
     std::vector<int32_t> cand;
     for (int t = 0; t < p->ntrees; ++t)
       if (cb.tree_off[t] >= 0) cand.push_back(t);
-    if (gjit_wanted((int)cand.size())) {
+    if (p->gjit_allowed && gjit_wanted((int)cand.size())) {
       std::stable_sort(cand.begin(), cand.end(), [&](int32_t x, int32_t y) {
         return cb.cost[x] != cb.cost[y] ? cb.cost[x] > cb.cost[y] : x < y;
       });
@@ -721,7 +723,7 @@ void build_grad_program(srhip_program* p) {
     std::vector<int32_t> cand;
     for (int t = 0; t < p->ntrees; ++t)
       if (cb.tree_off[t] >= 0) cand.push_back(t);
-    if (gjit_wanted((int)cand.size()) && jit::available64()) {
+    if (p->gjit_allowed && gjit_wanted((int)cand.size()) && jit::available64()) {
       std::stable_sort(cand.begin(), cand.end(), [&](int32_t x, int32_t y) {
         return cb.cost[x] != cb.cost[y] ? cb.cost[x] > cb.cost[y] : x < y;
       });
@@ -2266,9 +2268,83 @@ void collect_grad_results(srhip_ctx* c, const srhip_program* p, int64_t rows, do
 template <typename T>
 int eval_loss_grad_impl(srhip_dataset* ds, srhip_program* p, int loss, const double* params,
                         double* out_sum, double* out_dloss, double* out_wsum, uint8_t* out_ok) {
-  run_grad<T>(p->ctx, p, GRAD_LOSS, ds, loss, params ? params[0] : 0.0, nullptr, nullptr, 0);
-  collect_grad_results(p->ctx, p, ds->rows, out_sum, out_dloss, out_ok);
+  srhip_ctx* c = p->ctx;
+  run_grad<T>(c, p, GRAD_LOSS, ds, loss, params ? params[0] : 0.0, nullptr, nullptr, 0);
   if (out_wsum) *out_wsum = ds->w ? ds->sum_w : (double)ds->rows;
+  const bool periodic = std::is_same<T, float>::value && loss == SRHIP_LOSS_PERIODIC && c->last_jit_trees > 0;
+  if (!periodic) {
+    collect_grad_results(c, p, ds->rows, out_sum, out_dloss, out_ok);
+    return SRHIP_OK;
+  }
+  // Float32 Periodic as gradient tree code: a row beyond the Cody-Waite range made its tree fail
+  // there (device_ops.h periodic_g_f32); every failed tree of the call is evaluated again in the
+  // forward-mode interpreter (a program of those trees, no tree code), whose results replace the
+  // tree code's — failing trees fail there too, the others get OCML's full-range sin / cos
+  const int nt = p->ntrees, nconst = p->const_off.back();
+  std::vector<double> sum(nt), dl(std::max(nconst, 1));
+  std::vector<uint8_t> ok(nt);
+  collect_grad_results(c, p, ds->rows, sum.data(), dl.data(), ok.data());
+  std::vector<int32_t> redo;
+  for (int t = 0; t < nt; ++t)
+    if (!ok[t] && !p->g_static_fail[t]) redo.push_back(t);
+  if (!redo.empty()) {
+    const double ms = c->last_ms;
+    const int nl = c->last_launches;
+    const int ljt = c->last_jit_trees;  // the call's tree code (the rerun below reports none)
+    const char* lkn = t_last_kernel;  // string literals only
+    std::vector<int32_t> noff{0}, coff{0};
+    std::vector<uint8_t> kind;
+    std::vector<uint16_t> arg;
+    std::vector<T> cs;
+    const T* pc = reinterpret_cast<const T*>(p->consts.data());
+    for (int32_t t : redo) {
+      kind.insert(kind.end(), p->kind.begin() + p->node_off[t], p->kind.begin() + p->node_off[t + 1]);
+      arg.insert(arg.end(), p->arg.begin() + p->node_off[t], p->arg.begin() + p->node_off[t + 1]);
+      noff.push_back((int32_t)kind.size());
+      cs.insert(cs.end(), pc + p->const_off[t], pc + p->const_off[t + 1]);
+      coff.push_back((int32_t)cs.size());
+    }
+    // the program of those trees, built here (the caller holds the context's lock)
+    auto* q = new srhip_program();
+    q->ctx = c;
+    q->dtype = p->dtype;
+    q->ntrees = (int)redo.size();
+    q->jit_allowed = false;
+    q->gjit_allowed = false;
+    q->node_off = noff;
+    q->const_off = coff;
+    q->kind = kind;
+    q->arg = arg;
+    q->consts.resize(std::max<size_t>(cs.size() * sizeof(T), 1));
+    if (!cs.empty()) std::memcpy(q->consts.data(), cs.data(), cs.size() * sizeof(T));
+    std::vector<double> s2(redo.size()), d2(std::max<size_t>(cs.size(), 1));
+    std::vector<uint8_t> ok2(redo.size());
+    try {
+      build_program<T>(q);
+      eval_loss_grad_impl<T>(ds, q, loss, params, s2.data(), d2.data(), nullptr, ok2.data());
+    } catch (...) {
+      (void)hipStreamSynchronize(c->stream);
+      free_program_device(q);
+      delete q;
+      throw;
+    }
+    HIP_CHECK(hipStreamSynchronize(c->stream));
+    free_program_device(q);
+    delete q;
+    for (size_t i = 0; i < redo.size(); ++i) {
+      const int32_t t = redo[i];
+      sum[t] = s2[i];
+      ok[t] = ok2[i];
+      for (int32_t k = p->const_off[t]; k < p->const_off[t + 1]; ++k) dl[k] = d2[coff[i] + (k - p->const_off[t])];
+    }
+    c->last_ms += ms;  // the call's kernel time: both runs
+    c->last_launches += nl;
+    c->last_jit_trees = ljt;
+    t_last_kernel = lkn;
+  }
+  if (out_sum) std::copy(sum.begin(), sum.end(), out_sum);
+  if (out_dloss && nconst > 0) std::copy(dl.begin(), dl.begin() + nconst, out_dloss);
+  if (out_ok) std::copy(ok.begin(), ok.end(), out_ok);
   return SRHIP_OK;
 }
 

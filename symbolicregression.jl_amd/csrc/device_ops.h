@@ -513,7 +513,8 @@ __device__ __forceinline__ double lp_pow_t(double ar, double p) {
 // unspecified) — the Float32 Periodic loss routine of the tree code hands
 // such a tile back to the interpreter, which takes OCML's cos there.
 constexpr double kCwCosMax = 1.6e6;  // < 2^20 · π/2
-__device__ __forceinline__ double cw_cos(double x, bool& big) {
+// qshift 0: cos x; 3: sin x = cos(x - π/2), the quadrant index one lower
+__device__ __forceinline__ double cw_trig(double x, bool& big, int qshift) {
   big = !(__builtin_fabs(x) <= kCwCosMax);
   const double n = __builtin_rint(x * 6.36619772367581382433e-01);  // 2/π
   double r = __builtin_fma(-n, 1.57079632673412561417e+00, x);
@@ -540,10 +541,11 @@ __device__ __forceinline__ double cw_cos(double x, bool& big) {
   sn = __builtin_fma(sn, z, -8.3333333333333332e-03);
   sn = __builtin_fma(sn, z, 1.6666666666666666e-01);
   sn = __builtin_fma(-sn * z, r, r);
-  const int q = (int)((long long)n & 3);
+  const int q = (int)(((long long)n + qshift) & 3);
   const double v = (q & 1) ? sn : c;
   return (q == 1 || q == 2) ? -v : v;
 }
+__device__ __forceinline__ double cw_cos(double x, bool& big) { return cw_trig(x, big, 0); }
 // Float32 data's PeriodicLoss value, 1 - cos(r·k), k = 2π/c (LossFunctions'
 // PeriodicLoss stores k); the interpreter's and, but for a tile with some
 // |r·k| > kCwCosMax (handed back), the tree code's
@@ -552,6 +554,22 @@ __device__ __forceinline__ double periodic_f32(double r, double p) {
   bool big;
   const double c = cw_cos(x, big);
   return 1.0 - (big ? m_cos(x) : c);
+}
+
+// Float32 data's PeriodicLoss for the gradient tree code (jit_grad.cpp, routines
+// g_periodic / d_periodic of gen_jit.py): ℓ = 1 - cos(r·k) or ℓ' = k·sin(r·k),
+// k = 2π/c, by the Cody-Waite routine (the interpreter's values but within
+// ~2^-28 of a Float32 rounding boundary). A row beyond its range (|r·k| >
+// kCwCosMax) gives NaN: the tree "fails" in the tree code and the host reruns
+// every failed tree of the call in the forward-mode interpreter (api.cpp
+// eval_loss_grad_impl), whose OCML sin / cos reduce fl(r·k) exactly — the
+// gradient code's form of the loss tree code's hand-back.
+__device__ __forceinline__ double periodic_g_f32(double r, double p, bool deriv) {
+  const double k = 6.28318530717958647692 / p;
+  bool big;
+  const double v = cw_trig(r * k, big, deriv ? 3 : 0);
+  if (big) return __builtin_nan("");
+  return deriv ? k * v : 1.0 - v;
 }
 
 // |r|^n of LPDistLoss{n} for an INTEGER n (SRHIP_LOSS_LPINT). Julia's

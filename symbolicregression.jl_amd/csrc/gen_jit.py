@@ -89,7 +89,7 @@ def sgpr_pinned(name):
     """Routines compiled with LOSS_PINNED_S held live: the losses, and the
     Float64 pow and logs of PRECISE Float32 ^ and log10 (SGPR temporaries would otherwise
     reach s23+)."""
-    return name.startswith(("l_", "d_", "b_pow", "u_log", "u_sin_pd", "u_cos_pd"))
+    return name.startswith(("l_", "d_", "g_", "b_pow", "u_log", "u_sin_pd", "u_cos_pd"))
 
 
 def snippet_source(rg, routines):
@@ -282,6 +282,13 @@ def routine_list():
             continue
         imm = ("const double imm = __builtin_bit_cast(double, ((unsigned long long)s.s_kh << 32) | "
                "(unsigned long long)s.s_k); ")
+        if name == "PERIODIC":  # no OCML sin (its registers): device_ops.h periodic_g_f32
+            rs.append(("d_periodic", imm + rows_serial(
+                "s.a[r] = (float)dev::periodic_g_f32((double)s.a[r], imm, true);"), False))
+            # and the gradient code's ℓ without the loss code's hand-back
+            rs.append(("g_periodic", imm + rows_serial(
+                "s.a[r] = (float)dev::periodic_g_f32((double)s.a[r], imm, false);"), False))
+            continue
         rs.append((f"d_{name.lower()}",
                    imm + rows_serial(f"s.a[r] = dev::elem_dloss<float>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0f);"),
                    False))
@@ -598,7 +605,7 @@ def build(hipcc, outdir, R):
     # first and restores it before the routine ends (v_writelane /
     # v_readlane), so those are not temporaries of the routine.
     pinned = set(LOSS_PINNED_S)
-    for n in [n for n in names if n.startswith(("l_", "d_"))]:
+    for n in [n for n in names if n.startswith(("l_", "d_", "g_"))]:
         used, vused = set(), set()
         for d in (fast, prec):
             used |= G.regs_used(d[n], G.REG_S) - sstate - pinned
@@ -701,6 +708,11 @@ def build(hipcc, outdir, R):
         f.write("// routine of each elementwise loss, by SRHIP_LOSS_* (-1: L2, inline)\n")
         f.write("#define SR_JIT_LOSS_ROUTINE {" + ", ".join(
             str(-1 if n in NO_LOSS_ROUTINE else rid(f"l_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
+        f.write("// ℓ routine of each elementwise loss in the gradient tree code (the loss routine, but\n"
+                "// Periodic's without the hand-back)\n")
+        f.write("#define SR_JIT_GRAD_LOSS_ROUTINE {" + ", ".join(
+            str(-1 if n in NO_LOSS_ROUTINE else rid("g_periodic" if n == "PERIODIC" else f"l_{n.lower()}"))
+            for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")
         f.write("// dℓ/dr routine of each elementwise loss (-1: L2, inline, or left out)\n")
         f.write("#define SR_JIT_DLOSS_ROUTINE {" + ", ".join(
             str(-1 if n in NO_LOSS_ROUTINE else rid(f"d_{n.lower()}")) for n in sorted(LOSSES, key=lambda k: LOSSES[k])) + "}\n")

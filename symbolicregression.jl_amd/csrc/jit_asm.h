@@ -54,6 +54,7 @@ const int kBopRoutineRC[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE_RC;  // rhs constan
 const int kBopRoutineLC[SRHIP_NUM_BOPS] = SR_JIT_BOP_ROUTINE_LC;  // lhs constant in s_k
 const int kLossRoutine[SRHIP_NUM_LOSSES] = SR_JIT_LOSS_ROUTINE;     // -1: L2 (inline)
 const int kDLossRoutine[SRHIP_NUM_LOSSES] = SR_JIT_DLOSS_ROUTINE;   // dℓ/dr; -1: L2 (inline)
+const int kGradLossRoutine[SRHIP_NUM_LOSSES] = SR_JIT_GRAD_LOSS_ROUTINE;  // ℓ in the gradient code
 const char* const kRoutineName[kNumRoutines] = SR_JIT_ROUTINE_NAMES;
 const int kRoutineTrig[kNumRoutines] = SR_JIT_ROUTINE_TRIG;
 const int kRoutineInline[kNumRoutines] = SR_JIT_ROUTINE_INLINE;        // same FAST / PRECISE code, small

@@ -1307,7 +1307,7 @@ struct GradGen {
     mov4(VA, VY);
     as.sop1(SOP1_MOV, "s_mov_b32", S_K, K((uint32_t)lparam), "s" + std::to_string(S_K));
     as.sop1(SOP1_MOV, "s_mov_b32", S_KH, K((uint32_t)(lparam >> 32)), "s" + std::to_string(S_KH));
-    routine(kLossRoutine[loss], true);
+    routine(kGradLossRoutine[loss], true);  // Periodic: g_periodic (no hand-back)
     mov4(VY, VA);
     mov4(VA, rb);
     routine(kDLossRoutine[loss], true);
@@ -1322,6 +1322,15 @@ struct GradGen {
     as.bind(L_unw);
     emit_mask(VY);
     emit_mask(VA);
+    if (loss == SRHIP_LOSS_PERIODIC) {  // NaN ℓ' = a row beyond the Cody-Waite range (periodic_g_f32):
+      // marked as a failure, the tree ends, and the host reruns it in the interpreter
+      for (int e = 0; e < R; ++e) {
+        const Src d = V(VA + e), z = K(0), c = V(VCHK);
+        as.vop3(VOP3_FMA_F32, "v_fma_f32", VCHK, d, z, &c, 0, 0);
+      }
+      as.vopc(VOPC_U_F32, "v_cmp_u_f32_e32", V(VCHK), VCHK);
+      as.branch(SOPP_VCCNZ, "s_cbranch_vccnz", L_done);
+    }
     as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 2);
     as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY + 1, V(VY + 1), VY + 3);
     as.vop2(VOP2_ADD_F32, "v_add_f32_e32", VY, V(VY), VY + 1);
@@ -1554,7 +1563,7 @@ void destroy_grad(GradModule* m) {
 
 bool has_dloss_routine(int loss) {
   return loss == SRHIP_LOSS_L2 ||
-         (loss >= 0 && loss < SRHIP_NUM_LOSSES && kLossRoutine[loss] >= 0 && kDLossRoutine[loss] >= 0);
+         (loss >= 0 && loss < SRHIP_NUM_LOSSES && kGradLossRoutine[loss] >= 0 && kDLossRoutine[loss] >= 0);
 }
 
 int grad_nslots(const GradModule* m) { return m ? m->nslots : 0; }

@@ -157,7 +157,7 @@ def test_routine_temporaries_stay_clear_of_the_tree_loop():
         # two large-argument reductions inline), compiled with LOSS_PINNED_S held live
         assert name.startswith(("sr_rt_fast_l_", "sr_rt_prec_l_", "sr_rt_fast_d_", "sr_rt_prec_d_",
                                 "sr_rt_fast_u_sin_pd", "sr_rt_prec_u_sin_pd", "sr_rt_fast_u_cos_pd",
-                                "sr_rt_prec_u_cos_pd")), name
+                                "sr_rt_prec_u_cos_pd", "sr_rt_fast_g_", "sr_rt_prec_g_")), name
     assert borrowed <= 12
 
 

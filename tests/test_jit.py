@@ -282,11 +282,25 @@ def test_loss_tails_equal_llvm_mc(loss):
 
 
 def test_losses_without_routines_are_unsupported():
+    """Float64 LPDistLoss has no dℓ/dr routine (its Float64 pow exceeds the
+    routine registers): its gradients run interpreted. Every Float32 loss has
+    gradient routines (Periodic since round 6: g_periodic / d_periodic)."""
     o = srhip.Options(binary_operators=["+", "*"], unary_operators=["cos"])
-    flat = srhip.flatten(srhip.random_population(4, o, 3, np.float32, seed=1), o, dtype=np.float32)
-    for loss in (srhip.PeriodicLoss(2.0),):  # LPDist has routines since round 5
-        with pytest.raises(srhip.Unsupported):
-            jit_compile(flat, grad=True, loss=loss)
+    flat64 = srhip.flatten(srhip.random_population(4, o, 3, np.float64, seed=1), o, dtype=np.float64)
+    with pytest.raises(srhip.Unsupported):
+        jit_compile(flat64, grad=True, loss=srhip.LPDistLoss(2.5))
+
+
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+def test_float32_periodic_gradient_code_equals_llvm_mc():
+    """Float32 PeriodicLoss gradient tree code (round 6): the seed calls
+    g_periodic (ℓ without the loss code's hand-back) and d_periodic (ℓ' =
+    k·sin(r·k), device_ops.h periodic_g_f32); machine code = llvm-mc's."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
+    flat = srhip.flatten(srhip.random_population(120, o, 5, np.float32, seed=33), o, dtype=np.float32)
+    code, text, offs = jit_compile(flat, grad=True, loss=srhip.PeriodicLoss(2.0))
+    assert len(offs) >= 0.9 * 120
+    assert assemble(text) == code
 
 
 @pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")

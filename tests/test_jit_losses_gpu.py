@@ -135,13 +135,16 @@ def _dloss(loss, r):
     if kind == K.LOSS["LP"]:  # P |r|^(P-1) sign(r)
         with np.errstate(all="ignore"):
             return p * ar ** (p - 1.0) * sg
+    if kind == K.LOSS["PERIODIC"]:  # k sin(k r), k = 2π/c, in Float64
+        k = 2 * np.pi / p
+        return k * np.sin(k * r)
     assert kind == K.LOSS["QUANTILE"]
     return np.where(r >= 0, p, p - 1.0)
 
 
 GRAD_LOSSES = [srhip.L1DistLoss(), srhip.HuberLoss(0.8), srhip.L1EpsilonInsLoss(0.3), srhip.L2EpsilonInsLoss(0.3),
                srhip.QuantileLoss(0.3), srhip.LogCoshLoss(), srhip.LogitDistLoss(), srhip.LPDistLoss(1.7),
-               srhip.LPDistLoss(3.0)]
+               srhip.LPDistLoss(3.0), srhip.PeriodicLoss(2.0)]  # Periodic: round 6 (periodic_g_f32)
 
 
 @pytest.mark.parametrize("loss", GRAD_LOSSES, ids=[f"{l.kind}-{l.params}" for l in GRAD_LOSSES])
@@ -205,3 +208,40 @@ def test_gradient_tree_code_losses_match_oracle(gpu_ctx, loss):
                 assert np.all(err[sel] <= bound[sel]), (name, loss.kind, t, err[sel].tolist(), bound[sel].tolist())
             checked += int(sel.sum())
         assert checked > 300
+
+
+def test_periodic_gradient_tree_code_large_residuals(gpu_ctx):
+    """Float32 Periodic gradients as tree code (round 6, device_ops.h
+    periodic_g_f32): a row beyond the Cody-Waite range makes the tree fail in
+    the tree code, and the host reruns every failed tree of the call in the
+    forward-mode interpreter (api.cpp eval_loss_grad_impl) — so trees whose
+    residuals reach |r·k| ≈ 1e8 (x1·3e7, ...) get the interpreter's OCML
+    values bit for bit, the others stay tree code (within 1e-5 of the
+    interpreter's losses; their ∂L/∂c are checked against the oracle in
+    test_gradient_tree_code_losses_match_oracle)."""
+    o, X, y, w, trees = _problem()
+    big = [o.make_binary("*", o.make_binary("+", srhip.Node("x1"), srhip.Node(val=np.float32(0.25))),
+                         srhip.Node(val=np.float32(v))) for v in (3e7, -3e6, 2.5e6)]
+    trees = trees[:300] + big
+    flat = srhip.flatten(trees, o, dtype=np.float32)
+    loss = srhip.PeriodicLoss(2.0)
+    ds = srhip.DeviceDataset(gpu_ctx, X, y)
+    res = {}
+    for mode in ("1", "0"):
+        os.environ["SRHIP_GJIT"] = mode
+        try:
+            prog = srhip.Program(gpu_ctx, flat, np.float32)
+            res[mode] = [np.array(v, copy=True) for v in prog.eval_loss_grad(ds, loss.kind, loss.params)]
+            res[mode + "ran"] = gpu_ctx.last_tree_code()
+        finally:
+            del os.environ["SRHIP_GJIT"]
+    assert res["1ran"] >= 290 and res["0ran"] == 0
+    s1, g1, _, ok1 = res["1"]
+    s0, g0, _, ok0 = res["0"]
+    assert np.array_equal(ok1, ok0)
+    m = ok1.astype(bool) & np.isfinite(s0) & (s0 != 0)
+    assert np.all(np.abs(s1[m] - s0[m]) <= 1e-5 * np.abs(s0[m]))
+    co = flat.const_off
+    for t in range(len(trees) - 3, len(trees)):  # the large-residual trees: the interpreter's, bit for bit
+        assert ok1[t] and s1[t] == s0[t], (t, s1[t], s0[t])
+        np.testing.assert_array_equal(g1[co[t]:co[t + 1]], g0[co[t]:co[t + 1]])

@@ -94,6 +94,8 @@ def test_output_tree_code_dynamic_deal_equals_static(gpu_ctx, varying):
     waves take their trees from an LDS counter, as the loss loops do) against
     the static deal (SRHIP_JIT_DYNLOOP=0, read per launch): the same per-row
     outputs bit for bit, every tree (VERDICT r05 missing 4)."""
+    if os.environ.get("SRHIP_JIT_DYNLOOP") == "0":
+        pytest.skip("the static tree loops are forced for the whole run (tools/gpu_run.sh variants)")
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     rng = np.random.default_rng(23)
     n = 20_001
