@@ -556,6 +556,21 @@ __device__ __forceinline__ double periodic_f32(double r, double p) {
   return 1.0 - (big ? m_cos(x) : c);
 }
 
+// LPDistLoss's dℓ/dr of Float64 data for the Float64 gradient tree code
+// (gen_jit64.py d_lp): elem_dloss's p·|r|^(p-1)·sign(r) bit for bit, written so
+// that only the pow's own temporaries are live (r is the routine's operand
+// register, p an SGPR pair): ×sign(r) is copysign for r ≠ 0, and ×0 at r = 0
+// (NaN when |r|^(p-1) is Inf, as Julia's P * abs(r)^(P-1) * sign(r))
+__device__ __forceinline__ double lp_dloss_f64(double a, double p) {
+  // p - 1 made wave-uniform (readfirstlane of both halves), so that the pow's exponent stays in SGPRs
+  const unsigned long long b = __builtin_bit_cast(unsigned long long, p - 1.0);
+  const double pm1 = __builtin_bit_cast(
+      double, ((unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)(b >> 32)) << 32) |
+                  (unsigned long long)(unsigned)__builtin_amdgcn_readfirstlane((int)(unsigned)b));
+  const double v = p * m_pow(__builtin_fabs(a), pm1);
+  return a == 0.0 ? v * 0.0 : __builtin_copysign(v, a);
+}
+
 // Float32 data's PeriodicLoss for the gradient tree code (jit_grad.cpp, routines
 // g_periodic / d_periodic of gen_jit.py): ℓ = 1 - cos(r·k) or ℓ' = k·sin(r·k),
 // k = 2π/c, by the Cody-Waite routine (the interpreter's values but within

@@ -165,12 +165,19 @@ def routine_list():
             continue
         rs.append((f"l_{name.lower()}",
                    imm + rows(f"s.a[r] = dev::elem_loss<double>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0);")))
-    # dℓ/dr of the same losses (the Float64 gradient tree code's seed, jit64.cpp GradGen64)
+    # dℓ/dr of the same losses (the Float64 gradient tree code's seed, jit64.cpp GradGen64);
+    # LP's Float64 pow runs its two rows one after the other (scheduler fenced between them:
+    # both at once exceed the routine registers)
     for name in sorted(LOSSES, key=lambda k: LOSSES[k]):
         if name in NO_LOSS_ROUTINE:
             continue
-        rs.append((f"d_{name.lower()}",
-                   imm + rows(f"s.a[r] = dev::elem_dloss<double>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0);")))
+        body = f"s.a[r] = dev::elem_dloss<double>(SRHIP_LOSS_{name}, imm, s.a[r], 0.0);"
+        if name == "LP":  # elem_dloss's value with only pow's temporaries live, one row at a time
+            rs.append(("d_lp", imm + "const double pm1 = imm - 1.0; " + rows(
+                "{ const double a = s.a[r]; const double v = imm * dev::elem_loss<double>(SRHIP_LOSS_LP, pm1, a, 0.0); "
+                "s.a[r] = a == 0.0 ? v * 0.0 : __builtin_copysign(v, a); }")))
+            continue
+        rs.append((f"d_{name.lower()}", imm + rows(body)))
     return rs
 
 

@@ -281,14 +281,17 @@ def test_loss_tails_equal_llvm_mc(loss):
             assert text.count("s_swappc_b64") == l2text.count("s_swappc_b64") + 2 * len(offs)
 
 
-def test_losses_without_routines_are_unsupported():
-    """Float64 LPDistLoss has no dℓ/dr routine (its Float64 pow exceeds the
-    routine registers): its gradients run interpreted. Every Float32 loss has
-    gradient routines (Periodic since round 6: g_periodic / d_periodic)."""
-    o = srhip.Options(binary_operators=["+", "*"], unary_operators=["cos"])
-    flat64 = srhip.flatten(srhip.random_population(4, o, 3, np.float64, seed=1), o, dtype=np.float64)
-    with pytest.raises(srhip.Unsupported):
-        jit_compile(flat64, grad=True, loss=srhip.LPDistLoss(2.5))
+@pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")
+def test_every_loss_has_gradient_tree_code():
+    """Since round 6 every elementwise loss has gradient routines in both
+    dtypes (Float32 Periodic: g_periodic / d_periodic; Float64 LP: d_lp with
+    only the pow's temporaries live): the Float64 LP gradient code compiles
+    and equals llvm-mc's bytes."""
+    o = srhip.Options(binary_operators=["+", "-", "*", "/", "^"], unary_operators=["safe_log", "cos", "exp"])
+    flat64 = srhip.flatten(srhip.random_population(100, o, 5, np.float64, seed=61), o, dtype=np.float64)
+    code, text, offs = jit_compile(flat64, grad=True, loss=srhip.LPDistLoss(2.5))
+    assert len(offs) >= 95
+    assert assemble(text) == code
 
 
 @pytest.mark.skipif(not (LLVM / "llvm-mc").exists(), reason="llvm-mc not installed")

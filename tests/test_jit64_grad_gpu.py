@@ -164,11 +164,15 @@ def dloss_np(kind, p, r):
         return np.tanh(r)
     if kind == 9:
         return np.tanh(0.5 * r)
+    if kind == 2:  # LP: P |r|^(P-1) sign(r)
+        with np.errstate(all="ignore"):
+            return p * ar ** (p - 1.0) * sg
     raise ValueError(kind)
 
 
 LOSSES64 = [srhip.L1DistLoss(), srhip.HuberLoss(0.7), srhip.L1EpsilonInsLoss(0.3), srhip.L2EpsilonInsLoss(0.25),
-            srhip.QuantileLoss(0.8), srhip.PeriodicLoss(2.0), srhip.LogCoshLoss(), srhip.LogitDistLoss()]
+            srhip.QuantileLoss(0.8), srhip.PeriodicLoss(2.0), srhip.LogCoshLoss(), srhip.LogitDistLoss(),
+            srhip.LPDistLoss(2.5), srhip.LPDistLoss(0.7)]  # LP: round 6 (gen_jit64.py d_lp)
 
 
 @pytest.mark.parametrize("loss", LOSSES64, ids=lambda l: f"kind{l.kind}")
