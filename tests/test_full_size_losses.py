@@ -16,11 +16,12 @@ import srhip
 
 pytestmark = pytest.mark.gpu
 
-LOSSES = [srhip.L1DistLoss(), srhip.HuberLoss(1.0), srhip.LogCoshLoss()]
+LOSSES = [srhip.L1DistLoss(), srhip.HuberLoss(1.0), srhip.LogCoshLoss(), srhip.L2DistLoss()]
 
 
 @pytest.mark.parametrize("loss", LOSSES, ids=lambda l: f"kind{l.kind}")
 def test_config2_full_size_other_losses(gpu_ctx, loss):
+    """(L2 here with row weights: the weighted loops, sr_jit_eval_dlpw)"""
     o = srhip.Options(binary_operators=["+", "-", "*", "/"], unary_operators=["cos", "exp"])
     trees = srhip.random_population(4096, o, 5, np.float32, seed=0)
     rng = np.random.default_rng(1)
@@ -28,11 +29,14 @@ def test_config2_full_size_other_losses(gpu_ctx, loss):
     y = (np.float32(2) * np.cos(X[3]) + X[0] * X[0] - np.float32(2)).astype(np.float32)
     flat = srhip.flatten(trees, o, dtype=np.float32)
     prog = srhip.Program(gpu_ctx, flat, np.float32)
-    ds = srhip.DeviceDataset(gpu_ctx, X, y)
+    w = None
+    if loss.kind == 0:  # L2: the weighted tree loops
+        w = np.abs(rng.standard_normal(1_000_000)).astype(np.float32) + np.float32(0.1)
+    ds = srhip.DeviceDataset(gpu_ctx, X, y, w)
     s, wsum, ok = prog.eval_loss(ds, loss.kind, loss.params)
     assert gpu_ctx.last_tree_code() > 4000
     ok = np.asarray(ok, dtype=bool)
-    _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, None, loss.kind, loss.params, dtype=np.float32,
+    _, ref_l, ref_ok = oracle.eval_loss_batch(flat, X, y, w, loss.kind, loss.params, dtype=np.float32,
                                               nthreads=16)
     bad = np.flatnonzero(ok != ref_ok.astype(bool))
     assert bad.size == 0, f"did_succeed differs on {bad[:20]}"
@@ -40,7 +44,7 @@ def test_config2_full_size_other_losses(gpu_ctx, loss):
     with np.errstate(invalid="ignore", divide="ignore"):
         rel = np.abs(np.asarray(s, dtype=np.float64) / wsum - ref_l) / np.abs(ref_l)
     out = np.flatnonzero(m & ~(rel <= 1e-5))
-    rec = {"test": f"config2_full_loss_kind{loss.kind}", "succeeding": int(m.sum()), "outside_1e-5": int(out.size),
+    rec = {"test": f"config2_full_loss_kind{loss.kind}" + ("_weighted" if w is not None else ""), "succeeding": int(m.sum()), "outside_1e-5": int(out.size),
            "max_rel": float(np.max(rel[m])), "median_rel": float(np.median(rel[m]))}
     d = Path(__file__).resolve().parent.parent / "gpurun_out"
     d.mkdir(exist_ok=True)
