@@ -1995,12 +1995,15 @@ hipError_t launch(Module* m, int k, const EvalPlan& plan, const EvalArgs<float>&
   // PRECISE where FAST would have held): 4096 config #2 trees, interleaved
   // A/B (profiles/r04_sticky_tree_sizes.jsonl, r04_sticky_tree_ab.jsonl):
   // 30k rows 0.248 → 0.190 ms, 100k 0.449 → 0.449, 250k 0.956 → 0.951, 500k
-  // 1.734 → 1.762, 1M 3.28 → 3.39. A default of "on for at most 128 row
-  // groups" is the next step once it has run through the GPU suite; until then
-  // SRHIP_JIT_STICKY_TREE=1 (read per launch) turns it on.
+  // 1.734 → 1.762, 1M 3.28 → 3.39. Round 6 (shared subtrees; profiles/
+  // r06_sticky_tree.txt): 4096 trees on 10k rows 0.120 → 0.105 ms, 30k 0.217
+  // → 0.191, 62.5k even, 125k +1 %, 250k +3 %; 512 trees even. So it is on
+  // for at most 48 row groups (≈ 48k rows); SRHIP_JIT_STICKY_TREE=1 / 0 (read
+  // per launch) forces it on / off. The mark is bit 1 of the tree's flag word
+  // (bit 0: failed), which the finalize ignores.
   {
     const char* e = std::getenv("SRHIP_JIT_STICKY_TREE");
-    ja.dyn = (e && e[0] == '1') ? 1 : 0;
+    ja.dyn = (e && e[0] == '1') ? 1 : (e && e[0] == '0') ? 0 : (a.nrg <= 48 ? 1 : 0);
   }
   if (ja.nraw > a.nfeat) return hipErrorInvalidValue;
   if (ja.nbig > a.nrg || ja.ts < 1 || ja.ts > plan.ntiles) return hipErrorInvalidValue;

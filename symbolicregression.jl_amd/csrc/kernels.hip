@@ -77,7 +77,8 @@ __global__ void __launch_bounds__(64 * kFinWaves) finalize_kernel(EvalArgs<T> a,
     const int sidx = a.contig ? g * a.tpb + i : i * a.ntg + ((i & 1) ? (a.ntg - 1 - g) : g);
     if (sidx < a.nlist) {
       const int t = a.list[sidx];
-      const bool ok = a.part4 ? a.fail[sidx] == 0u : !__builtin_isnan(c);
+      // part4: failed = bit 0 of the flag word (bit 1 marks a tree sticky PRECISE, JitArgs::dyn)
+      const bool ok = a.part4 ? (a.fail[sidx] & 1u) == 0u : !__builtin_isnan(c);
       out_sum[t] = ok ? s : __builtin_nan("");
       out_ok[t] = ok ? 1 : 0;
       if (a.fail) a.fail[sidx] = 0u;

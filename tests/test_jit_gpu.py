@@ -31,7 +31,11 @@ class env:
 
     def __enter__(self):
         self.old = {k: os.environ.get(k) for k in self.kv}
-        os.environ.update({k: str(v) for k, v in self.kv.items()})
+        for k, v in self.kv.items():  # None: unset (the library's default)
+            if v is None:
+                os.environ.pop(k, None)
+            else:
+                os.environ[k] = str(v)
 
     def __exit__(self, *a):
         for k, v in self.old.items():
@@ -348,3 +352,32 @@ def test_hand_written_tree_loop_equals_compiled(gpu_ctx, weighted):
     np.testing.assert_array_equal(s0[ok0], s1[ok1])
     for a, b in zip(g0, g1):
         assert np.array_equal(np.asarray(a), np.asarray(b), equal_nan=True)
+
+
+def test_sticky_precise_tree_keeps_did_succeed(gpu_ctx):
+    """Sticky PRECISE per tree across row groups (JitArgs::dyn, on by default
+    for at most 48 row groups): a tree redone PRECISE in one row group runs
+    PRECISE in the later ones, marked by bit 1 of its flag word. The finalize
+    reads failure from bit 0 only, so did_succeed is the same with the mark on,
+    off and by default (round 6: a flag word of 2 read as a failure), the
+    losses the same within the 1e-5 bar, and fewer tiles are redone (which
+    row group marks a tree first depends on the schedule, so neither the
+    count nor the FAST / PRECISE choice per tile is fixed)."""
+    o = srhip.Options(**CFG2)
+    trees = srhip.random_population(1024, o, 5, np.float32, seed=77)
+    X, y, _ = data(5, 30_000, 78)
+    ctx = gpu_ctx
+    ds = srhip.DeviceDataset(ctx, X, y)
+    prog = srhip.Program(ctx, srhip.flatten(trees, o, dtype=np.float32), np.float32)
+    res = {}
+    for mode in ("0", "1", None):
+        with env(SRHIP_JIT_STICKY_TREE=mode):
+            res[mode] = (prog.eval_loss(ds, K.LOSS["L2"]), ctx.last_jit_events()[1])
+    (s0, _, ok0), red0 = res["0"]
+    (s1, _, ok1), red1 = res["1"]
+    (sd, _, okd), redd = res[None]
+    assert ok0.sum() > 700
+    assert np.array_equal(ok0, ok1) and np.array_equal(ok0, okd)
+    np.testing.assert_allclose(s1[ok1], s0[ok0], rtol=1e-5)
+    np.testing.assert_allclose(sd[okd], s0[ok0], rtol=1e-5)
+    assert red1 < red0 and redd < red0, (red0, red1, redd)
